@@ -1,0 +1,126 @@
+"""Loader for libvst_hip.so (the C ABI declared in include/vst_hip.h).
+
+The product path has no fallback: if the shared library is missing or fails to load, importing the
+ops raises.  The library is built in-tree (``_build/libvst_hip.so``) by :func:`build` with hipcc for
+gfx950; it is loaded AFTER torch so that it binds to the HIP runtime torch already loaded
+(both export soname libamdhip64.so.7), which keeps torch's streams valid inside the library.
+"""
+import ctypes
+import glob
+import os
+import subprocess
+
+import torch  # noqa: F401  (must be loaded first: see module docstring)
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(PKG)
+BUILD = os.path.join(PKG, "_build")
+LIB_PATH = os.path.join(BUILD, "libvst_hip.so")
+CSRC = os.path.join(PKG, "csrc")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+
+_lib = None
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+L = ctypes.c_long
+F = ctypes.c_float
+D = ctypes.c_double
+SZ = ctypes.c_size_t
+
+# name -> (restype, argtypes); mirrors include/vst_hip.h
+SIGNATURES = {
+    "vst_last_error": (ctypes.c_char_p, []),
+    "vst_version": (I, []),
+    "vst_nchw_to_nhwc": (I, [P, P, I, I, I, I, I, P]),
+    "vst_nhwc_to_nchw": (I, [P, P, I, I, I, I, I, P]),
+    "vst_weight_pack": (I, [P, P, I, I, I, I, I, I, I, P]),
+    "vst_conv2d_fwd": (I, [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, P]),
+    "vst_conv2d_tfwd": (I, [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, F, P]),
+    "vst_conv2d_wgrad_ws_bytes": (SZ, [I, I, I, I, I, I, I, I, I]),
+    "vst_conv2d_wgrad": (I, [P, P, P, P, P, SZ, I, I, I, I, I, I, I, I, I, I, I, I, I, I, L, L, I, P]),
+    "vst_reflect_fold": (I, [P, P, P, I, I, I, I, I, P]),
+    "vst_channel_sum_ws_bytes": (SZ, [L, I]),
+    "vst_channel_sum": (I, [P, P, P, L, I, I, I, P]),
+    "vst_instnorm_ws_bytes": (SZ, [I, I, I]),
+    "vst_instnorm_stats": (I, [P, P, P, I, I, I, F, P]),
+    "vst_instnorm_act_fwd": (I, [P, P, P, P, I, I, I, I, F, P]),
+    "vst_instnorm_act_bwd": (I, [P, P, P, P, P, I, I, I, I, F, P]),
+    "vst_act_bwd": (I, [P, P, P, L, I, F, P]),
+    "vst_warp_fwd": (I, [P, P, P, I, I, I, I, I, P]),
+    "vst_warp_bwd_input": (I, [P, P, P, I, I, I, I, I, P]),
+    "vst_fbcheck": (I, [P, P, P, I, I, I, P]),
+    "vst_loss_part_floats": (I, [L]),
+    "vst_loss_temporal": (I, [P, P, P, P, P, P, I, I, I, I, I, F, P]),
+    "vst_loss_temporal_bwd": (I, [P, P, P, P, P, P, P, I, I, I, I, I, F, P]),
+    "vst_loss_l1": (I, [P, P, P, P, L, I, I, F, P]),
+    "vst_loss_l1_bwd": (I, [P, P, P, P, L, I, I, F, P]),
+    "vst_loss_mse_const": (I, [P, F, P, P, L, I, I, F, P]),
+    "vst_loss_mse_const_bwd": (I, [P, F, P, P, L, I, I, F, P]),
+    "vst_finish_sum": (I, [P, I, P, D, P]),
+    "vst_adam_step": (I, [P, P, P, P, L, F, F, F, F, I, P]),
+    "vst_axpby": (I, [P, P, L, F, F, P]),
+}
+
+
+def sources():
+    return sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+
+
+def build(force=False, verbose=False):
+    """Compile every HIP source into _build/libvst_hip.so for gfx950 (cross-compiles without a GPU)."""
+    os.makedirs(BUILD, exist_ok=True)
+    srcs = sources()
+    deps = srcs + glob.glob(os.path.join(CSRC, "*.h")) + [os.path.join(REPO, "include", "vst_hip.h")]
+    if not force and os.path.exists(LIB_PATH):
+        if os.path.getmtime(LIB_PATH) >= max(os.path.getmtime(d) for d in deps):
+            return LIB_PATH
+    objs = []
+    procs = []
+    for s in srcs:
+        o = os.path.join(BUILD, os.path.basename(s) + ".o")
+        objs.append(o)
+        cmd = [HIPCC, "-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-munsafe-fp-atomics",
+               "-Wall", "-Wno-unused-function", "-c", s, "-o", o]
+        procs.append((cmd, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
+    for cmd, p in procs:
+        out, _ = p.communicate()
+        if p.returncode != 0:
+            raise RuntimeError("hipcc failed: %s\n%s" % (" ".join(cmd), out.decode(errors="replace")))
+        if verbose and out:
+            print(out.decode(errors="replace"))
+    tmp = LIB_PATH + ".tmp"
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+    if r.returncode != 0:
+        raise RuntimeError("link failed: %s\n%s" % (" ".join(cmd), r.stdout.decode(errors="replace")))
+    os.replace(tmp, LIB_PATH)
+    return LIB_PATH
+
+
+def load():
+    """Return the loaded ctypes library; raises if it is missing (no CPU fallback exists)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"libvst_hip.so not found at {LIB_PATH}; run __graft_entry__.build() (hipcc, gfx950)")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def exported_symbols():
+    return list(SIGNATURES)
+
+
+def check(rc, what=""):
+    if rc != 0:
+        msg = _lib.vst_last_error().decode(errors="replace") if _lib is not None else ""
+        raise RuntimeError(f"libvst_hip {what} failed (status {rc}): {msg}")

@@ -1,0 +1,69 @@
+// Shared helpers for the gfx950 kernels of libvst_hip.so (see include/vst_hip.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "../../include/vst_hip.h"
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+
+namespace vst {
+
+// per-thread last error message (host side)
+void set_error(const char* fmt, ...);
+
+inline int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error("%s: %s", what, hipGetErrorString(e));
+    return VST_EHIP;
+  }
+  return VST_OK;
+}
+
+#define VST_REQUIRE(cond, ...)            \
+  do {                                    \
+    if (!(cond)) {                        \
+      ::vst::set_error(__VA_ARGS__);      \
+      return VST_EINVAL;                  \
+    }                                     \
+  } while (0)
+
+__device__ __forceinline__ int reflect_idx(int i, int n) {
+  // ReflectionPad2d index map: mirror without repeating the edge.
+  i = i < 0 ? -i : i;
+  return i >= n ? 2 * n - 2 - i : i;
+}
+
+__device__ __forceinline__ float apply_act(float v, int act, float slope) {
+  if (act == VST_ACT_RELU) return v > 0.f ? v : 0.f;
+  if (act == VST_ACT_LRELU) return v > 0.f ? v : v * slope;
+  if (act == VST_ACT_TANH) return tanhf(v);
+  return v;
+}
+
+// derivative of the activation expressed through its OUTPUT y (valid for relu/lrelu/tanh)
+__device__ __forceinline__ float act_grad_from_out(float y, int act, float slope) {
+  if (act == VST_ACT_RELU) return y > 0.f ? 1.f : 0.f;
+  if (act == VST_ACT_LRELU) return y > 0.f ? 1.f : slope;
+  if (act == VST_ACT_TANH) return 1.f - y * y;
+  return 1.f;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
+
+}  // namespace vst

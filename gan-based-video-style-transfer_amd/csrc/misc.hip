@@ -1,0 +1,133 @@
+// Layout conversion, weight packing, fused Adam and small helpers; error reporting for the C ABI.
+#include <stdarg.h>
+
+#include "common.h"
+
+namespace vst {
+
+static thread_local char g_err[512] = "";
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+__global__ void nchw_to_nhwc_k(const float* __restrict__ x, float* __restrict__ y, int C, int HW,
+                               int Cs, long total) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int c = i % Cs;
+  const long pix = i / Cs;
+  const long n = pix / HW, p = pix - n * HW;
+  y[i] = c < C ? x[(n * C + c) * HW + p] : 0.f;
+}
+
+__global__ void nhwc_to_nchw_k(const float* __restrict__ x, float* __restrict__ y, int C, int HW,
+                               int Cs, long total) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const long p = i % HW;
+  const long nc = i / HW;
+  const int c = nc % C;
+  const long n = nc / C;
+  y[i] = x[(n * HW + p) * Cs + c];
+}
+
+// w[O][I][R][S] -> KC: out[r][s][i][o] (Ip x Op per tap) or CK: out[r][s][o][i] (Op x Ip per tap)
+__global__ void weight_pack_k(const float* __restrict__ w, float* __restrict__ out, int O, int I,
+                              int R, int S, int Op, int Ip, int mode, long total) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= total) return;
+  const int RS = R * S;
+  int o, i, rs;
+  if (mode == VST_PACK_KC) {  // idx = (rs*Ip + i)*Op + o
+    o = idx % Op;
+    const long q = idx / Op;
+    i = q % Ip;
+    rs = q / Ip;
+  } else {  // idx = (rs*Op + o)*Ip + i
+    i = idx % Ip;
+    const long q = idx / Ip;
+    o = q % Op;
+    rs = q / Op;
+  }
+  out[idx] = (o < O && i < I) ? w[((long)o * I + i) * RS + rs] : 0.f;
+}
+
+__global__ void adam_k(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                       float* __restrict__ v, long n, float lr, float b1, float b2, float eps,
+                       float bc1, float bc2_sqrt) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float gi = g[i];
+  // exp_avg.lerp_(grad, 1 - beta1) with ATen's two-sided lerp formula
+  const float w = 1.f - b1, m0 = m[i];
+  const float mi = w < 0.5f ? m0 + w * (gi - m0) : gi - (gi - m0) * (1.f - w);
+  // exp_avg_sq.mul_(beta2).addcmul_(grad, grad, value=1 - beta2)
+  const float vi = v[i] * b2 + (1.f - b2) * (gi * gi);
+  m[i] = mi;
+  v[i] = vi;
+  // torch.optim.Adam (single-tensor, capturable=False):
+  //   denom = sqrt(v) / sqrt(1 - b2^t) + eps ; p -= (lr / (1 - b1^t)) * m / denom
+  const float denom = sqrtf(vi) / bc2_sqrt + eps;
+  p[i] -= (lr / bc1) * (mi / denom);
+}
+
+__global__ void axpby_k(const float* __restrict__ x, float* __restrict__ y, long n, float a,
+                        float b) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) y[i] = a * x[i] + b * y[i];
+}
+
+}  // namespace vst
+
+using namespace vst;
+
+extern "C" const char* vst_last_error(void) { return g_err; }
+extern "C" int vst_version(void) { return 1; }
+
+extern "C" int vst_nchw_to_nhwc(const float* x, float* y, int N, int C, int H, int W, int Cs,
+                                void* stream) {
+  VST_REQUIRE(x && y && C <= Cs, "nchw_to_nhwc: bad args");
+  const long total = (long)N * H * W * Cs;
+  hipLaunchKernelGGL(nchw_to_nhwc_k, dim3(ceil_div(total, 256)), dim3(256), 0, (hipStream_t)stream, x,
+                     y, C, H * W, Cs, total);
+  return check_launch("nchw_to_nhwc");
+}
+
+extern "C" int vst_nhwc_to_nchw(const float* x, float* y, int N, int C, int H, int W, int Cs,
+                                void* stream) {
+  VST_REQUIRE(x && y && C <= Cs, "nhwc_to_nchw: bad args");
+  const long total = (long)N * C * H * W;
+  hipLaunchKernelGGL(nhwc_to_nchw_k, dim3(ceil_div(total, 256)), dim3(256), 0, (hipStream_t)stream, x,
+                     y, C, H * W, Cs, total);
+  return check_launch("nhwc_to_nchw");
+}
+
+extern "C" int vst_weight_pack(const float* w, float* out, int O, int I, int R, int S, int Op,
+                               int Ip, int mode, void* stream) {
+  VST_REQUIRE(w && out && O <= Op && I <= Ip && (mode == VST_PACK_KC || mode == VST_PACK_CK),
+              "weight_pack: bad args");
+  const long total = (long)R * S * Op * Ip;
+  hipLaunchKernelGGL(weight_pack_k, dim3(ceil_div(total, 256)), dim3(256), 0, (hipStream_t)stream, w,
+                     out, O, I, R, S, Op, Ip, mode, total);
+  return check_launch("weight_pack");
+}
+
+extern "C" int vst_adam_step(float* p, const float* g, float* m, float* v, long n, float lr,
+                             float beta1, float beta2, float eps, int step, void* stream) {
+  VST_REQUIRE(p && g && m && v && step >= 1, "adam_step: bad args");
+  const double bc1 = 1.0 - pow((double)beta1, step);
+  const double bc2 = 1.0 - pow((double)beta2, step);
+  hipLaunchKernelGGL(adam_k, dim3(ceil_div(n, 256)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n,
+                     lr, beta1, beta2, eps, (float)bc1, (float)sqrt(bc2));
+  return check_launch("adam_step");
+}
+
+extern "C" int vst_axpby(const float* x, float* y, long n, float a, float b, void* stream) {
+  VST_REQUIRE(x && y, "axpby: bad args");
+  hipLaunchKernelGGL(axpby_k, dim3(ceil_div(n, 256)), dim3(256), 0, (hipStream_t)stream, x, y, n, a, b);
+  return check_launch("axpby");
+}

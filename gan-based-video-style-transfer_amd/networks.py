@@ -1,0 +1,640 @@
+"""Network factory — drop-in for methods/GAN-based/CycleGAN/models/networks.py, HIP-backed.
+
+Public API mirrors the reference (same names, argument meaning and errors):
+  get_norm_layer (18-35), get_scheduler (38-64), init_weights (67-98), init_net (101-116),
+  define_G (119-159), define_D (162-203), GANLoss (209-275), ResnetGenerator (315-373),
+  ResnetBlock (376-433), NLayerDiscriminator (538-583).
+
+MI355X design (not a translation):
+  * Each network keeps the reference's nn.Sequential index structure so ``state_dict()`` keys and
+    shapes are identical (``model.10.conv_block.1.weight`` …) and reference checkpoints load
+    unmodified; the parameters themselves are views into ONE flat fp32 buffer per network (and the
+    grads into one flat grad buffer) so the optimizer and the DP all-reduce are single fused calls.
+  * ``forward`` runs the WHOLE network as one autograd node whose forward/backward are sequences
+    of libvst_hip kernels: NHWC implicit-GEMM convs on fp32 MFMA with reflect padding / stride /
+    transposition folded into address generation, fp64-reduced InstanceNorm fused with the
+    activation and the residual add, deterministic split-K weight gradients written straight into
+    the flat grad buffer (accumulating across the several passes of one train step).
+  * Activations are NHWC with channel stride a multiple of 4; images are NHWC4.  ``forward`` takes
+    and returns NCHW like the reference; ``forward_nhwc`` is the internal zero-copy entry.
+"""
+import functools
+
+import torch
+import torch.nn as nn
+from torch.nn import init
+from torch.optim import lr_scheduler
+
+from . import ops
+from .ops import cpad
+
+
+###############################################################################
+# Helper Functions (reference networks.py:13-116)
+###############################################################################
+class Identity(nn.Module):
+    def forward(self, x):
+        return x
+
+
+def get_norm_layer(norm_type='instance'):
+    """networks.py:18-35.  Only 'instance' is on the HIP hot path (reference defaults)."""
+    if norm_type == 'batch':
+        return functools.partial(nn.BatchNorm2d, affine=True, track_running_stats=True)
+    elif norm_type == 'instance':
+        return functools.partial(nn.InstanceNorm2d, affine=False, track_running_stats=False)
+    elif norm_type == 'none':
+        def norm_layer(x):
+            return Identity()
+        return norm_layer
+    raise NotImplementedError('normalization layer [%s] is not found' % norm_type)
+
+
+def get_scheduler(optimizer, opt):
+    """networks.py:38-64 (linear | step | plateau | cosine)."""
+    if opt.lr_policy == 'linear':
+        def lambda_rule(epoch):
+            return 1.0 - max(0, epoch + opt.epoch_count - opt.n_epochs) / float(opt.n_epochs_decay + 1)
+        return lr_scheduler.LambdaLR(optimizer, lr_lambda=lambda_rule)
+    elif opt.lr_policy == 'step':
+        return lr_scheduler.StepLR(optimizer, step_size=opt.lr_decay_iters, gamma=0.1)
+    elif opt.lr_policy == 'plateau':
+        return lr_scheduler.ReduceLROnPlateau(optimizer, mode='min', factor=0.2, threshold=0.01, patience=5)
+    elif opt.lr_policy == 'cosine':
+        return lr_scheduler.CosineAnnealingLR(optimizer, T_max=opt.n_epochs, eta_min=0)
+    return NotImplementedError('learning rate policy [%s] is not implemented', opt.lr_policy)
+
+
+def init_weights(net, init_type='normal', init_gain=0.02):
+    """networks.py:67-98: conv weights ~ init, conv biases = 0."""
+    def init_func(m):
+        classname = m.__class__.__name__
+        if hasattr(m, 'weight') and m.weight is not None and (classname.find('Conv') != -1):
+            with torch.no_grad():
+                if init_type == 'normal':
+                    init.normal_(m.weight.data, 0.0, init_gain)
+                elif init_type == 'xavier':
+                    init.xavier_normal_(m.weight.data, gain=init_gain)
+                elif init_type == 'kaiming':
+                    init.kaiming_normal_(m.weight.data, a=0, mode='fan_in')
+                elif init_type == 'orthogonal':
+                    init.orthogonal_(m.weight.data, gain=init_gain)
+                else:
+                    raise NotImplementedError('initialization method [%s] is not implemented' % init_type)
+                if getattr(m, 'bias', None) is not None:
+                    init.constant_(m.bias.data, 0.0)
+    print('initialize network with %s' % init_type)
+    net.apply(init_func)
+    if isinstance(net, FlatNet):
+        net.bump_version()
+
+
+def _device_for(gpu_ids):
+    if len(gpu_ids) > 0:
+        assert torch.cuda.is_available()
+        return torch.device('cuda:%d' % gpu_ids[0])
+    if torch.cuda.is_available():
+        return torch.device('cuda:%d' % torch.cuda.current_device())
+    return torch.device('cpu')
+
+
+def init_net(net, init_type='normal', init_gain=0.02, gpu_ids=[]):
+    """networks.py:101-116.  Instead of nn.DataParallel (single-process multi-GPU), multi-GPU runs
+    one process per GPU with torch.distributed (see dp.py); the net is placed on gpu_ids[0]."""
+    net.to(_device_for(gpu_ids))
+    init_weights(net, init_type, init_gain=init_gain)
+    return net
+
+
+###############################################################################
+# Parameter holders: keep the reference module tree / state_dict keys
+###############################################################################
+class Conv2d(nn.Module):
+    """Parameter holder with nn.Conv2d's state (weight [Co,Ci,k,k], bias [Co])."""
+
+    def __init__(self, cin, cout, k, stride=1, padding=0, bias=True):
+        super().__init__()
+        self.in_channels, self.out_channels, self.kernel_size = cin, cout, k
+        self.stride, self.padding = stride, padding
+        self.weight = nn.Parameter(torch.empty(cout, cin, k, k))
+        self.bias = nn.Parameter(torch.zeros(cout)) if bias else None
+
+    def extra_repr(self):
+        return f"{self.in_channels}, {self.out_channels}, kernel_size={self.kernel_size}, stride={self.stride}, padding={self.padding}"
+
+
+class ConvTranspose2d(nn.Module):
+    """Parameter holder with nn.ConvTranspose2d's state (weight [Ci,Co,k,k], bias [Co])."""
+
+    def __init__(self, cin, cout, k, stride=1, padding=0, output_padding=0, bias=True):
+        super().__init__()
+        self.in_channels, self.out_channels, self.kernel_size = cin, cout, k
+        self.stride, self.padding, self.output_padding = stride, padding, output_padding
+        self.weight = nn.Parameter(torch.empty(cin, cout, k, k))
+        self.bias = nn.Parameter(torch.zeros(cout)) if bias else None
+
+    def extra_repr(self):
+        return f"{self.in_channels}, {self.out_channels}, kernel_size={self.kernel_size}, stride={self.stride}"
+
+
+class _Marker(nn.Module):
+    """Stateless placeholder for a fused layer (pad / norm / activation) — keeps indices & repr."""
+
+    def __init__(self, what):
+        super().__init__()
+        self.what = what
+
+    def extra_repr(self):
+        return self.what
+
+
+###############################################################################
+# Flat parameter / gradient storage
+###############################################################################
+class FlatNet(nn.Module):
+    """Base for HIP-backed networks: every parameter is a view into self.flat_param and its .grad a
+    view into self.flat_grad.  Moving the module re-flattens on the new device."""
+
+    def _flatten(self):
+        params = list(self.parameters())
+        dev = params[0].device
+        n = sum(p.numel() for p in params)
+        flat = torch.zeros(n, device=dev, dtype=torch.float32)
+        gflat = torch.zeros(n, device=dev, dtype=torch.float32)
+        off = 0
+        for p in params:
+            k = p.numel()
+            flat[off:off + k].copy_(p.data.reshape(-1))
+            p.data = flat[off:off + k].view_as(p)
+            p.grad = gflat[off:off + k].view_as(p)
+            off += k
+        self.flat_param, self.flat_grad = flat, gflat
+        self._wversion = getattr(self, "_wversion", 0) + 1
+        self._packs = None
+
+    def _apply(self, fn, *args, **kwargs):
+        super()._apply(fn, *args, **kwargs)
+        self._flatten()
+        return self
+
+    def bump_version(self):
+        self._wversion += 1
+
+    def _version_key(self):
+        return (self._wversion, sum(p._version for p in self.parameters()))
+
+    def zero_grad(self, set_to_none=False):
+        self.flat_grad.zero_()
+
+    def weights_trainable(self):
+        return any(p.requires_grad for p in self.parameters())
+
+    def packs(self):
+        key = self._version_key()
+        if self._packs is None or self._packs[0] != key:
+            self._packs = (key, self._make_packs())
+        return self._packs[1]
+
+    def _anchor(self):
+        a = getattr(self, "_anchor_t", None)
+        if a is None or a.device != self.flat_param.device:
+            a = torch.zeros((), device=self.flat_param.device, requires_grad=True)
+            self._anchor_t = a
+        return a if self.weights_trainable() and torch.is_grad_enabled() else a.detach()
+
+    def forward(self, x):
+        """Reference-compatible NCHW entry: [N, C, H, W] -> [N, C', H', W']."""
+        cin = self.input_nc
+        y = self.forward_nhwc(_ToNHWC.apply(x, cpad(cin)))
+        return _ToNCHW.apply(y, self.output_nc)
+
+
+class _ToNHWC(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, cs):
+        ctx.c = x.shape[1]
+        return ops.nchw_to_nhwc(x.contiguous(), cs)
+
+    @staticmethod
+    def backward(ctx, g):
+        return ops.nhwc_to_nchw(g.contiguous(), ctx.c), None
+
+
+class _ToNCHW(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, c):
+        ctx.cs = x.shape[-1]
+        return ops.nhwc_to_nchw(x, c)
+
+    @staticmethod
+    def backward(ctx, g):
+        return ops.nchw_to_nhwc(g.contiguous(), ctx.cs), None
+
+
+def _pack_conv(m):
+    return (ops.weight_pack(m.weight, ops.PACK_KC), ops.weight_pack(m.weight, ops.PACK_CK),
+            _padded_bias(m))
+
+
+def _padded_bias(m):
+    if m.bias is None:
+        return None
+    cp = cpad(m.bias.numel())
+    if cp == m.bias.numel():
+        return m.bias.detach()
+    b = torch.zeros(cp, device=m.bias.device)
+    b[:m.bias.numel()] = m.bias.detach()
+    return b
+
+
+###############################################################################
+# ResnetGenerator (networks.py:315-433)
+###############################################################################
+class ResnetBlock(nn.Module):
+    """networks.py:376-433 (reflect padding, instance norm): x + [pad,conv,IN,ReLU,pad,conv,IN](x)."""
+
+    def __init__(self, dim, padding_type, norm_layer, use_dropout, use_bias):
+        super().__init__()
+        if padding_type != 'reflect':
+            raise NotImplementedError('padding [%s] is not on the HIP path' % padding_type)
+        if use_dropout:
+            raise NotImplementedError('dropout is not on the HIP path (CycleGAN default no_dropout)')
+        self.conv_block = nn.Sequential(
+            _Marker('ReflectionPad2d(1)'), Conv2d(dim, dim, 3, bias=use_bias), _Marker('InstanceNorm2d'),
+            _Marker('ReLU'), _Marker('ReflectionPad2d(1)'), Conv2d(dim, dim, 3, bias=use_bias),
+            _Marker('InstanceNorm2d'))
+
+
+class ResnetGenerator(FlatNet):
+    """networks.py:315-373: c7s1-ngf, d(2ngf), d(4ngf), n_blocks x R(4ngf), u(2ngf), u(ngf), c7s1-out, tanh."""
+
+    def __init__(self, input_nc, output_nc, ngf=64, norm_layer=nn.BatchNorm2d, use_dropout=False,
+                 n_blocks=6, padding_type='reflect'):
+        assert n_blocks >= 0
+        super().__init__()
+        if not (isinstance(norm_layer, functools.partial) and norm_layer.func == nn.InstanceNorm2d):
+            raise NotImplementedError('only norm=instance is implemented on the HIP path')
+        use_bias = True
+        self.input_nc, self.output_nc, self.ngf, self.n_blocks = input_nc, output_nc, ngf, n_blocks
+        L = [_Marker('ReflectionPad2d(3)'), Conv2d(input_nc, ngf, 7, bias=use_bias),
+             _Marker('InstanceNorm2d'), _Marker('ReLU')]
+        for i in range(2):
+            m = 2 ** i
+            L += [Conv2d(ngf * m, ngf * m * 2, 3, stride=2, padding=1, bias=use_bias),
+                  _Marker('InstanceNorm2d'), _Marker('ReLU')]
+        for _ in range(n_blocks):
+            L += [ResnetBlock(ngf * 4, padding_type, norm_layer, use_dropout, use_bias)]
+        for i in range(2):
+            m = 2 ** (2 - i)
+            L += [ConvTranspose2d(ngf * m, ngf * m // 2, 3, stride=2, padding=1, output_padding=1,
+                                  bias=use_bias),
+                  _Marker('InstanceNorm2d'), _Marker('ReLU')]
+        L += [_Marker('ReflectionPad2d(3)'), Conv2d(ngf, output_nc, 7, bias=True), _Marker('Tanh')]
+        self.model = nn.Sequential(*L)
+        self._flatten()
+
+    # layer handles in execution order
+    def _layers(self):
+        mdl = self.model
+        c0 = mdl[1]
+        d = [mdl[4], mdl[7]]
+        blocks = [mdl[10 + i] for i in range(self.n_blocks)]
+        u = [mdl[10 + self.n_blocks], mdl[13 + self.n_blocks]]
+        f = mdl[17 + self.n_blocks]
+        return c0, d, blocks, u, f
+
+    def _make_packs(self):
+        c0, d, blocks, u, f = self._layers()
+        P = {"c0": _pack_conv(c0), "d0": _pack_conv(d[0]), "d1": _pack_conv(d[1]), "f": _pack_conv(f)}
+        for i, b in enumerate(blocks):
+            P[f"b{i}a"] = _pack_conv(b.conv_block[1])
+            P[f"b{i}b"] = _pack_conv(b.conv_block[5])
+        for i, m in enumerate(u):
+            # ConvTranspose2d fwd = transposed kernel with rows (r,s,ci) -> CK pack of Wt[Ci][Co];
+            # its dgrad = forward conv with KC pack of Wt seen as [O=Ci][I=Co] -> rows (r,s,co), cols ci
+            P[f"u{i}"] = (ops.weight_pack(m.weight, ops.PACK_KC), ops.weight_pack(m.weight, ops.PACK_CK),
+                          _padded_bias(m))
+        return P
+
+    def forward_nhwc(self, x):
+        return _GeneratorFn.apply(x, self._anchor(), self)
+
+
+class _GeneratorFn(torch.autograd.Function):
+    """Whole-generator forward/backward on libvst_hip kernels."""
+
+    @staticmethod
+    def forward(ctx, x, anchor, net):
+        P = net.packs()
+        c0, d, blocks, u, f = net._layers()
+        ngf = net.ngf
+        sv = {"x": x}
+        N, H, W, _ = x.shape
+
+        def conv_in_relu(inp, key, cout, R, st, pad, mode):
+            kc, _, b = P[key]
+            y = ops.conv2d_fwd(inp, kc, b, cpad(cout), R, R, st, pad, mode)
+            s = ops.instnorm_stats(y)
+            return y, s, ops.instnorm_act_fwd(y, s, "relu")
+
+        y, s, a = conv_in_relu(x, "c0", ngf, 7, 1, 3, "reflect")
+        sv["c0"] = (y, s, a)
+        y, s, a = conv_in_relu(a, "d0", 2 * ngf, 3, 2, 1, "zero")
+        sv["d0"] = (y, s, a)
+        y, s, a = conv_in_relu(a, "d1", 4 * ngf, 3, 2, 1, "zero")
+        sv["d1"] = (y, s, a)
+        h = a
+        for i in range(len(blocks)):
+            t, s1, uu = conv_in_relu(h, f"b{i}a", 4 * ngf, 3, 1, 1, "reflect")
+            kc, _, b = P[f"b{i}b"]
+            v = ops.conv2d_fwd(uu, kc, b, 4 * ngf, 3, 3, 1, 1, "reflect")
+            s2 = ops.instnorm_stats(v)
+            hn = ops.instnorm_act_fwd(v, s2, "none", residual=h)
+            sv[f"b{i}"] = (h, t, s1, uu, v, s2)
+            h = hn
+        a = h
+        for i in range(2):
+            cout = ngf * 2 ** (1 - i)
+            _, ck, b = P[f"u{i}"]
+            Hi, Wi = a.shape[1], a.shape[2]
+            y = ops.conv2d_tfwd(a, ck, b, 2 * Hi, 2 * Wi, cpad(cout), 3, 3, 2, 1)
+            s = ops.instnorm_stats(y)
+            an = ops.instnorm_act_fwd(y, s, "relu")
+            sv[f"u{i}"] = (a, y, s, an)
+            a = an
+        kc, _, b = P["f"]
+        out = ops.conv2d_fwd(a, kc, b, cpad(net.output_nc), 7, 7, 1, 3, "reflect", act="tanh")
+        sv["f"] = (a, out)
+        ctx.sv, ctx.net, ctx.P = sv, net, P
+        ctx.train_w = anchor.requires_grad
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        sv, net, P = ctx.sv, ctx.net, ctx.P
+        c0, d, blocks, u, f = net._layers()
+        ngf = net.ngf
+        train_w = ctx.train_w
+        gout = gout.contiguous()
+
+        def wgrad(mod, inp, dy, R, st, pad, mode, db=True):
+            if not train_w:
+                return
+            w = mod.weight
+            co, ci = w.shape[0], w.shape[1]
+            ops.conv2d_wgrad(inp, dy, w.grad, mod.bias.grad if (db and mod.bias is not None) else None,
+                             R, R, st, pad, mode, co, ci, ci * R * R, R * R, accumulate=True)
+
+        def dgrad_reflect(dy, key, cin_p, R, p, H, W, addend=None):
+            _, ck, _ = P[key]
+            dxp = ops.conv2d_tfwd(dy, ck, None, H + 2 * p, W + 2 * p, cin_p, R, R, 1, 0)
+            return ops.reflect_fold(dxp, p, addend)
+
+        def dgrad_s2(dy, key, cin_p, H, W):
+            _, ck, _ = P[key]
+            return ops.conv2d_tfwd(dy, ck, None, H, W, cin_p, 3, 3, 2, 1)
+
+        # final conv + tanh
+        a, out = sv["f"]
+        g = ops.act_bwd(gout, out, "tanh")
+        wgrad(f, a, g, 7, 1, 3, "reflect")
+        ga = dgrad_reflect(g, "f", a.shape[-1], 7, 3, a.shape[1], a.shape[2])
+        # up-sampling convT layers
+        for i in (1, 0):
+            a_in, y, s, an = sv[f"u{i}"]
+            dy = ops.instnorm_act_bwd(ga, y, s, "relu")
+            m = u[i]
+            if train_w:
+                # Wt[ci][co] grad = wgrad of the equivalent conv x_T = conv(dy_T, .) (see header)
+                ci_t, co_t = m.weight.shape[0], m.weight.shape[1]
+                ops.conv2d_wgrad(dy, a_in, m.weight.grad, None, 3, 3, 2, 1, "zero", ci_t, co_t,
+                                 co_t * 9, 9, accumulate=True)
+                ops.channel_sum(dy, m.bias.grad, co_t)
+            kc, _, _ = P[f"u{i}"]
+            ga = ops.conv2d_fwd(dy, kc, None, a_in.shape[-1], 3, 3, 2, 1, "zero")
+        # residual blocks
+        gh = ga
+        for i in reversed(range(len(blocks))):
+            h, t, s1, uu, v, s2 = sv[f"b{i}"]
+            blk = blocks[i].conv_block
+            dv = ops.instnorm_act_bwd(gh, v, s2, "none")
+            wgrad(blk[5], uu, dv, 3, 1, 1, "reflect")
+            du = dgrad_reflect(dv, f"b{i}b", uu.shape[-1], 3, 1, uu.shape[1], uu.shape[2])
+            dt = ops.instnorm_act_bwd(du, t, s1, "relu")
+            wgrad(blk[1], h, dt, 3, 1, 1, "reflect")
+            gh = dgrad_reflect(dt, f"b{i}a", h.shape[-1], 3, 1, h.shape[1], h.shape[2], addend=gh)
+        ga = gh
+        # down-sampling convs
+        for key, mod, prev in (("d1", d[1], "d0"), ("d0", d[0], "c0")):
+            y, s, _ = sv[key]
+            a_in = sv[prev][2]
+            dy = ops.instnorm_act_bwd(ga, y, s, "relu")
+            wgrad(mod, a_in, dy, 3, 2, 1, "zero")
+            ga = dgrad_s2(dy, key, a_in.shape[-1], a_in.shape[1], a_in.shape[2])
+        # first conv
+        x = sv["x"]
+        y, s, _ = sv["c0"]
+        dy = ops.instnorm_act_bwd(ga, y, s, "relu")
+        wgrad(c0, x, dy, 7, 1, 3, "reflect")
+        gx = None
+        if ctx.needs_input_grad[0]:
+            gx = dgrad_reflect(dy, "c0", x.shape[-1], 7, 3, x.shape[1], x.shape[2])
+        ctx.sv = None
+        return gx, None, None
+
+
+###############################################################################
+# NLayerDiscriminator (networks.py:538-583)
+###############################################################################
+class NLayerDiscriminator(FlatNet):
+    """PatchGAN: C64(s2)+LReLU, [C(s2)+IN+LReLU] x (n-1), C(s1)+IN+LReLU, C1(s1)."""
+
+    def __init__(self, input_nc, ndf=64, n_layers=3, norm_layer=nn.BatchNorm2d):
+        super().__init__()
+        if not (isinstance(norm_layer, functools.partial) and norm_layer.func == nn.InstanceNorm2d):
+            raise NotImplementedError('only norm=instance is implemented on the HIP path')
+        self.input_nc, self.output_nc = input_nc, 1
+        kw, padw = 4, 1
+        seq = [Conv2d(input_nc, ndf, kw, stride=2, padding=padw), _Marker('LeakyReLU(0.2)')]
+        self.spec = [(ndf, 2, False)]  # (cout, stride, has_in)
+        nf_mult = 1
+        for n in range(1, n_layers):
+            prev, nf_mult = nf_mult, min(2 ** n, 8)
+            seq += [Conv2d(ndf * prev, ndf * nf_mult, kw, stride=2, padding=padw, bias=True),
+                    _Marker('InstanceNorm2d'), _Marker('LeakyReLU(0.2)')]
+            self.spec.append((ndf * nf_mult, 2, True))
+        prev, nf_mult = nf_mult, min(2 ** n_layers, 8)
+        seq += [Conv2d(ndf * prev, ndf * nf_mult, kw, stride=1, padding=padw, bias=True),
+                _Marker('InstanceNorm2d'), _Marker('LeakyReLU(0.2)')]
+        self.spec.append((ndf * nf_mult, 1, True))
+        seq += [Conv2d(ndf * nf_mult, 1, kw, stride=1, padding=padw)]
+        self.spec.append((1, 1, False))
+        self.model = nn.Sequential(*seq)
+        self._flatten()
+
+    def _convs(self):
+        return [m for m in self.model if isinstance(m, Conv2d)]
+
+    def _make_packs(self):
+        return [_pack_conv(m) for m in self._convs()]
+
+    def forward_nhwc(self, x):
+        return _DiscriminatorFn.apply(x, self._anchor(), self)
+
+
+SLOPE = 0.2
+
+
+class _DiscriminatorFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, anchor, net):
+        P = net.packs()
+        convs = net._convs()
+        saved = []
+        a = x
+        L = len(convs)
+        for i, (m, (cout, st, has_in)) in enumerate(zip(convs, net.spec)):
+            kc, _, b = P[i]
+            last = i == L - 1
+            if has_in:
+                y = ops.conv2d_fwd(a, kc, b, cpad(cout), 4, 4, st, 1, "zero")
+                s = ops.instnorm_stats(y)
+                an = ops.instnorm_act_fwd(y, s, "lrelu", SLOPE)
+                saved.append((a, y, s, an))
+            else:
+                act = "none" if last else "lrelu"
+                an = ops.conv2d_fwd(a, kc, b, cpad(cout), 4, 4, st, 1, "zero", act=act, slope=SLOPE)
+                saved.append((a, None, None, an))
+            a = an
+        ctx.saved, ctx.net, ctx.P = saved, net, P
+        ctx.train_w = anchor.requires_grad
+        return a
+
+    @staticmethod
+    def backward(ctx, gout):
+        saved, net, P = ctx.saved, ctx.net, ctx.P
+        convs = net._convs()
+        L = len(convs)
+        g = gout.contiguous()
+        gx = None
+        for i in reversed(range(L)):
+            a_in, y, s, an = saved[i]
+            m = convs[i]
+            cout, st, has_in = net.spec[i]
+            if has_in:
+                dy = ops.instnorm_act_bwd(g, y, s, "lrelu", SLOPE)
+            elif i != L - 1:
+                dy = ops.act_bwd(g, an, "lrelu", SLOPE)
+            else:
+                dy = g
+            if ctx.train_w:
+                co, ci = m.weight.shape[0], m.weight.shape[1]
+                ops.conv2d_wgrad(a_in, dy, m.weight.grad, m.bias.grad if m.bias is not None else None,
+                                 4, 4, st, 1, "zero", co, ci, ci * 16, 16, accumulate=True)
+            if i > 0 or ctx.needs_input_grad[0]:
+                _, ck, _ = P[i]
+                g = ops.conv2d_tfwd(dy, ck, None, a_in.shape[1], a_in.shape[2], a_in.shape[-1], 4, 4, st, 1)
+                if i == 0:
+                    gx = g
+        ctx.saved = None
+        return gx, None, None
+
+
+###############################################################################
+# define_G / define_D (networks.py:119-203)
+###############################################################################
+def define_G(input_nc, output_nc, ngf, netG, norm='batch', use_dropout=False, init_type='normal',
+             init_gain=0.02, gpu_ids=[]):
+    norm_layer = get_norm_layer(norm_type=norm)
+    if netG == 'resnet_9blocks':
+        net = ResnetGenerator(input_nc, output_nc, ngf, norm_layer=norm_layer, use_dropout=use_dropout, n_blocks=9)
+    elif netG == 'resnet_6blocks':
+        net = ResnetGenerator(input_nc, output_nc, ngf, norm_layer=norm_layer, use_dropout=use_dropout, n_blocks=6)
+    elif netG in ('unet_128', 'unet_256'):
+        raise NotImplementedError('Generator [%s] is outside the HIP hot path (SURVEY §2)' % netG)
+    else:
+        raise NotImplementedError('Generator model name [%s] is not recognized' % netG)
+    return init_net(net, init_type, init_gain, gpu_ids)
+
+
+def define_D(input_nc, ndf, netD, n_layers_D=3, norm='batch', init_type='normal', init_gain=0.02,
+             gpu_ids=[]):
+    norm_layer = get_norm_layer(norm_type=norm)
+    if netD == 'basic':
+        net = NLayerDiscriminator(input_nc, ndf, n_layers=3, norm_layer=norm_layer)
+    elif netD == 'n_layers':
+        net = NLayerDiscriminator(input_nc, ndf, n_layers_D, norm_layer=norm_layer)
+    elif netD == 'pixel':
+        raise NotImplementedError('Discriminator [pixel] is outside the HIP hot path (SURVEY §2)')
+    else:
+        raise NotImplementedError('Discriminator model name [%s] is not recognized' % netD)
+    return init_net(net, init_type, init_gain, gpu_ids)
+
+
+###############################################################################
+# Losses (networks.py:209-275) on NHWC tensors, HIP-backed
+###############################################################################
+class _MSEConstFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, pred, target, cl):
+        ctx.save_for_backward(pred)
+        ctx.target, ctx.cl = target, cl
+        return ops.loss_mse_const(pred, target, 1.0, cl)
+
+    @staticmethod
+    def backward(ctx, g):
+        (pred,) = ctx.saved_tensors
+        return ops.loss_mse_const_bwd(pred, ctx.target, g.contiguous(), 1.0, ctx.cl), None, None
+
+
+class _L1Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a, b, scale, cl):
+        ctx.save_for_backward(a, b)
+        ctx.scale, ctx.cl = scale, cl
+        return ops.loss_l1(a, b, scale, cl)
+
+    @staticmethod
+    def backward(ctx, g):
+        a, b = ctx.saved_tensors
+        g = g.contiguous()
+        ga = ops.loss_l1_bwd(a, b, g, ctx.scale, ctx.cl) if ctx.needs_input_grad[0] else None
+        gb = ops.loss_l1_bwd(b, a, g, ctx.scale, ctx.cl) if ctx.needs_input_grad[1] else None
+        return ga, gb, None, None
+
+
+def l1_loss(a, b, scale=1.0, cl=3):
+    """scale * nn.L1Loss()(a, b) over the Cl logical channels of NHWC tensors."""
+    return _L1Fn.apply(a, b, float(scale), cl)
+
+
+class GANLoss(nn.Module):
+    """networks.py:209-275.  'lsgan' runs on the HIP loss kernels for NHWC predictions
+    (``nhwc=True``, the path the HIP models use); other modes and NCHW inputs use the reference
+    formula on torch ops (outside the hot path)."""
+
+    def __init__(self, gan_mode, target_real_label=1.0, target_fake_label=0.0):
+        super().__init__()
+        self.register_buffer('real_label', torch.tensor(target_real_label))
+        self.register_buffer('fake_label', torch.tensor(target_fake_label))
+        self.gan_mode = gan_mode
+        self._real, self._fake = float(target_real_label), float(target_fake_label)
+        if gan_mode == 'lsgan':
+            self.loss = nn.MSELoss()
+        elif gan_mode == 'vanilla':
+            self.loss = nn.BCEWithLogitsLoss()
+        elif gan_mode in ['wgangp']:
+            self.loss = None
+        else:
+            raise NotImplementedError('gan mode %s not implemented' % gan_mode)
+
+    def get_target_tensor(self, prediction, target_is_real):
+        t = self.real_label if target_is_real else self.fake_label
+        return t.expand_as(prediction)
+
+    def __call__(self, prediction, target_is_real, nhwc=False):
+        if nhwc and self.gan_mode == 'lsgan':
+            return _MSEConstFn.apply(prediction, self._real if target_is_real else self._fake, 1)
+        if self.gan_mode in ['lsgan', 'vanilla']:
+            return self.loss(prediction, self.get_target_tensor(prediction, target_is_real))
+        return -prediction.mean() if target_is_real else prediction.mean()

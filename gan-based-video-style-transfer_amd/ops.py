@@ -1,0 +1,258 @@
+"""Tensor-level wrappers over the C ABI (include/vst_hip.h).
+
+Every function launches on torch's current HIP stream, takes/returns torch tensors that live on the
+GPU, and raises on a non-zero status.  Activations are NHWC fp32 with a channel stride that is a
+multiple of 4 (``cpad``); images are NHWC4.  There is no CPU fallback: a CPU tensor is an error.
+"""
+import torch
+
+from . import _lib
+
+ACT = {"none": 0, "relu": 1, "lrelu": 2, "tanh": 3}
+PAD = {"zero": 0, "reflect": 1}
+PACK_KC, PACK_CK = 0, 1
+IN_EPS = 1e-5
+
+
+def cpad(c):
+    return (c + 3) // 4 * 4
+
+
+def lib():
+    return _lib.load()
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _p(t):
+    return None if t is None else t.data_ptr()
+
+
+def _dev_check(*ts):
+    for t in ts:
+        if t is not None:
+            if not t.is_cuda:
+                raise RuntimeError("vst ops require GPU tensors (no CPU fallback)")
+            if t.dtype != torch.float32 or not t.is_contiguous():
+                raise RuntimeError("vst ops require contiguous float32 tensors")
+
+
+def _call(name, *args):
+    rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        _lib.check(rc, name)
+
+
+# ------------------------------------------------------------------------------------ layout
+def nchw_to_nhwc(x, cs=None):
+    _dev_check(x)
+    N, C, H, W = x.shape
+    cs = cs or cpad(C)
+    y = torch.empty((N, H, W, cs), device=x.device, dtype=torch.float32)
+    _call("vst_nchw_to_nhwc", _p(x), _p(y), N, C, H, W, cs, _stream())
+    return y
+
+
+def nhwc_to_nchw(x, c):
+    _dev_check(x)
+    N, H, W, cs = x.shape
+    y = torch.empty((N, c, H, W), device=x.device, dtype=torch.float32)
+    _call("vst_nhwc_to_nchw", _p(x), _p(y), N, c, H, W, cs, _stream())
+    return y
+
+
+def weight_pack(w, mode, transposed=False):
+    """Pack a PyTorch conv weight for the GEMM kernels (see vst_weight_pack).  For a
+    ConvTranspose2d weight [Ci][Co][R][S] pass transposed=True: dims are then (O=Ci, I=Co)."""
+    _dev_check(w)
+    O, I_, R, S = w.shape
+    Op, Ip = cpad(O), cpad(I_)
+    shape = (R, S, Ip, Op) if mode == PACK_KC else (R, S, Op, Ip)
+    out = torch.empty(shape, device=w.device, dtype=torch.float32)
+    _call("vst_weight_pack", _p(w), _p(out), O, I_, R, S, Op, Ip, mode, _stream())
+    return out
+
+
+# --------------------------------------------------------------------------------------- conv
+def conv2d_fwd(x, wp, bias, cop, R, S, stride, pad, pad_mode="zero", act="none", slope=0.0,
+               out=None):
+    _dev_check(x, wp, bias)
+    N, H, W, Cx = x.shape
+    Ho = (H + 2 * pad - R) // stride + 1
+    Wo = (W + 2 * pad - S) // stride + 1
+    y = out if out is not None else torch.empty((N, Ho, Wo, cop), device=x.device)
+    _call("vst_conv2d_fwd", _p(x), _p(wp), _p(bias), _p(y), N, H, W, Cx, cop, R, S, stride, pad,
+          PAD[pad_mode], ACT[act], float(slope), _stream())
+    return y
+
+
+def conv2d_tfwd(x, wp, bias, Ho, Wo, cx, R, S, stride, pad, act="none", slope=0.0):
+    _dev_check(x, wp, bias)
+    N, Hi, Wi, Cy = x.shape
+    y = torch.empty((N, Ho, Wo, cx), device=x.device)
+    _call("vst_conv2d_tfwd", _p(x), _p(wp), _p(bias), _p(y), N, Hi, Wi, Cy, Ho, Wo, cx, R, S,
+          stride, pad, ACT[act], float(slope), _stream())
+    return y
+
+
+def conv2d_wgrad(x, dy, dw, db, R, S, stride, pad, pad_mode, co, ci, so, si, accumulate=True):
+    """dw (+)= weight gradient written with strides (so, si) — see vst_conv2d_wgrad."""
+    _dev_check(x, dy)
+    N, H, W, Cx = x.shape
+    _, Ho, Wo, Cyp = dy.shape
+    nbytes = lib().vst_conv2d_wgrad_ws_bytes(N, H, W, Cx, Ho, Wo, Cyp, R, S)
+    ws = torch.empty((nbytes + 3) // 4, device=x.device)
+    _call("vst_conv2d_wgrad", _p(x), _p(dy), _p(dw), _p(db), _p(ws), nbytes, N, H, W, Cx, Ho, Wo,
+          Cyp, R, S, stride, pad, PAD[pad_mode], co, ci, so, si, 1 if accumulate else 0, _stream())
+
+
+def channel_sum(x, db, cl, accumulate=True):
+    """db[c] (+)= sum over pixels of x[..., c] (bias gradient)."""
+    _dev_check(x)
+    cs = x.shape[-1]
+    nhw = x.numel() // cs
+    nbytes = lib().vst_channel_sum_ws_bytes(nhw, cl)
+    ws = torch.empty((nbytes + 3) // 4, device=x.device)
+    _call("vst_channel_sum", _p(x), _p(db), _p(ws), nhw, cs, cl, 1 if accumulate else 0, _stream())
+
+
+def reflect_fold(dxp, p, addend=None):
+    _dev_check(dxp, addend)
+    N, Hp, Wp, C = dxp.shape
+    H, W = Hp - 2 * p, Wp - 2 * p
+    dx = torch.empty((N, H, W, C), device=dxp.device)
+    _call("vst_reflect_fold", _p(dxp), _p(addend), _p(dx), N, H, W, C, p, _stream())
+    return dx
+
+
+# --------------------------------------------------------------------------------- instnorm
+def _in_ws(N, HW, C, device):
+    nbytes = lib().vst_instnorm_ws_bytes(N, HW, C)
+    return torch.empty((nbytes + 7) // 8, dtype=torch.float64, device=device)
+
+
+def instnorm_stats(y):
+    _dev_check(y)
+    N, H, W, C = y.shape
+    stats = torch.empty((N, C, 2), device=y.device)
+    ws = _in_ws(N, H * W, C, y.device)
+    _call("vst_instnorm_stats", _p(y), _p(stats), _p(ws), N, H * W, C, IN_EPS, _stream())
+    return stats
+
+
+def instnorm_act_fwd(y, stats, act="relu", slope=0.0, residual=None):
+    _dev_check(y, stats, residual)
+    N, H, W, C = y.shape
+    a = torch.empty_like(y)
+    _call("vst_instnorm_act_fwd", _p(y), _p(stats), _p(residual), _p(a), N, H * W, C, ACT[act],
+          float(slope), _stream())
+    return a
+
+
+def instnorm_act_bwd(ga, y, stats, act="relu", slope=0.0):
+    _dev_check(ga, y, stats)
+    N, H, W, C = y.shape
+    dy = torch.empty_like(y)
+    ws = _in_ws(N, H * W, C, y.device)
+    _call("vst_instnorm_act_bwd", _p(ga), _p(y), _p(stats), _p(dy), _p(ws), N, H * W, C, ACT[act],
+          float(slope), _stream())
+    return dy
+
+
+def act_bwd(gy, y, act, slope=0.0):
+    _dev_check(gy, y)
+    dx = torch.empty_like(y)
+    _call("vst_act_bwd", _p(gy), _p(y), _p(dx), y.numel(), ACT[act], float(slope), _stream())
+    return dx
+
+
+# ------------------------------------------------------------------------------------- flow
+def warp_nhwc(x, flow, align_corners=False):
+    _dev_check(x, flow)
+    N, H, W, C = x.shape
+    out = torch.empty_like(x)
+    _call("vst_warp_fwd", _p(x), _p(flow), _p(out), N, H, W, C, int(align_corners), _stream())
+    return out
+
+
+def warp_bwd_nhwc(gout, flow, align_corners=False):
+    _dev_check(gout, flow)
+    N, H, W, C = gout.shape
+    gx = torch.zeros_like(gout)
+    _call("vst_warp_bwd_input", _p(gout), _p(flow), _p(gx), N, H, W, C, int(align_corners), _stream())
+    return gx
+
+
+def fbcheck(ff, bf):
+    _dev_check(ff, bf)
+    N, _, H, W = bf.shape
+    mask = torch.empty((N, 1, H, W), device=bf.device)
+    _call("vst_fbcheck", _p(ff), _p(bf), _p(mask), N, H, W, _stream())
+    return mask
+
+
+# ----------------------------------------------------------------------------------- losses
+def _part(npix, device):
+    return torch.empty(lib().vst_loss_part_floats(npix), device=device)
+
+
+def loss_temporal(a, b, flow, mask, lam, cl=3):
+    _dev_check(a, b, flow, mask)
+    N, H, W, Cs = a.shape
+    loss = torch.empty((), device=a.device)
+    _call("vst_loss_temporal", _p(a), _p(b), _p(flow), _p(mask), _p(loss), _p(_part(N * H * W, a.device)),
+          N, H, W, Cs, cl, float(lam), _stream())
+    return loss
+
+
+def loss_temporal_bwd(a, b, flow, mask, gout, ga, gb, lam, cl=3):
+    N, H, W, Cs = a.shape
+    _call("vst_loss_temporal_bwd", _p(a), _p(b), _p(flow), _p(mask), _p(gout), _p(ga), _p(gb), N, H, W,
+          Cs, cl, float(lam), _stream())
+
+
+def loss_l1(a, b, scale, cl=3):
+    _dev_check(a, b)
+    npix = a.numel() // a.shape[-1]
+    loss = torch.empty((), device=a.device)
+    _call("vst_loss_l1", _p(a), _p(b), _p(loss), _p(_part(npix, a.device)), npix, a.shape[-1], cl,
+          float(scale), _stream())
+    return loss
+
+
+def loss_l1_bwd(a, b, gout, scale, cl=3):
+    npix = a.numel() // a.shape[-1]
+    g = torch.empty_like(a)
+    _call("vst_loss_l1_bwd", _p(a), _p(b), _p(gout), _p(g), npix, a.shape[-1], cl, float(scale), _stream())
+    return g
+
+
+def loss_mse_const(a, target, scale=1.0, cl=1):
+    _dev_check(a)
+    npix = a.numel() // a.shape[-1]
+    loss = torch.empty((), device=a.device)
+    _call("vst_loss_mse_const", _p(a), float(target), _p(loss), _p(_part(npix, a.device)), npix,
+          a.shape[-1], cl, float(scale), _stream())
+    return loss
+
+
+def loss_mse_const_bwd(a, target, gout, scale=1.0, cl=1):
+    npix = a.numel() // a.shape[-1]
+    g = torch.empty_like(a)
+    _call("vst_loss_mse_const_bwd", _p(a), float(target), _p(gout), _p(g), npix, a.shape[-1], cl,
+          float(scale), _stream())
+    return g
+
+
+# -------------------------------------------------------------------------------- optimizer
+def adam_step(p, g, m, v, lr, beta1, beta2, eps, step):
+    _dev_check(p, g, m, v)
+    _call("vst_adam_step", _p(p), _p(g), _p(m), _p(v), p.numel(), float(lr), float(beta1),
+          float(beta2), float(eps), int(step), _stream())
+
+
+def axpby(x, y, a, b):
+    _dev_check(x, y)
+    _call("vst_axpby", _p(x), _p(y), x.numel(), float(a), float(b), _stream())

@@ -1,0 +1,166 @@
+/*
+ * vst_hip.h — C ABI of libvst_hip.so, the MI355X (gfx950) HIP implementation of the
+ * GAN-based video style transfer hot path (CycleGAN video train step + generator inference).
+ *
+ * Every entry point takes DEVICE pointers owned by the caller, plain int shapes, and a
+ * hipStream_t passed as void* (0 = null stream).  Nothing here allocates device memory, frees
+ * caller memory or synchronises the host; every call is stream-ordered and graph-capturable.
+ * Returns VST_OK (0) or an error code; vst_last_error() returns a message for the calling thread.
+ *
+ * Tensor conventions
+ *   activations   NHWC fp32, channel stride C a multiple of 4 (padding channels are zero);
+ *                 image tensors are NHWC4 (3 logical channels + a zero channel).
+ *   conv weights  as PyTorch stores them: Conv2d [Co][Ci][R][S], ConvTranspose2d [Ci][Co][R][S];
+ *                 the kernels read a packed copy made by vst_weight_pack (cached by the caller).
+ *
+ * Reference interfaces replaced (paths relative to the reference root):
+ *   vst_conv2d_fwd / vst_conv2d_tfwd / vst_conv2d_wgrad / vst_reflect_fold
+ *       nn.Conv2d, nn.ConvTranspose2d, nn.ReflectionPad2d forward+autograd as used by
+ *       methods/GAN-based/CycleGAN/models/networks.py:340-367 (ResnetGenerator), 404-426
+ *       (ResnetBlock), 556-578 (NLayerDiscriminator)
+ *   vst_instnorm_stats / vst_instnorm_act_fwd / vst_instnorm_act_bwd(_reduce)
+ *       nn.InstanceNorm2d(affine=False) + nn.ReLU / nn.LeakyReLU(0.2), networks.py:30, 343-372, 564-576
+ *   vst_warp_fwd / vst_warp_bwd_input
+ *       utils/flowtools.py:18-32 warp (F.grid_sample, bilinear, zeros, align_corners=False)
+ *       and methods/GAN-based/CycleGANCon/models/cycle_gan_model.py:191-203
+ *   vst_fbcheck                 utils/flowtools.py:34-58 fbcCheckTorch (+ gradient 12-16)
+ *   vst_loss_*                  networks.py:209-275 GANLoss('lsgan'), torch.nn.L1Loss
+ *                               (cycle_gan_model.py:94-95), temporal loss cycle_gan_model.py:204
+ *   vst_adam_step               torch.optim.Adam as constructed at cycle_gan_model.py:97-98
+ */
+#ifndef VST_HIP_H
+#define VST_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { VST_OK = 0, VST_EINVAL = 1, VST_EUNSUPPORTED = 2, VST_EHIP = 3 };
+enum { VST_PAD_ZERO = 0, VST_PAD_REFLECT = 1 };
+enum { VST_ACT_NONE = 0, VST_ACT_RELU = 1, VST_ACT_LRELU = 2, VST_ACT_TANH = 3 };
+enum { VST_PACK_KC = 0,   /* [R][S][Ci][Co]  fprop B operand  (rows k=(r,s,ci), cols co) */
+       VST_PACK_CK = 1 }; /* [R][S][Co][Ci]  dgrad B operand  (rows k=(r,s,co), cols ci) */
+
+const char* vst_last_error(void);
+int vst_version(void);
+
+/* ---- layout ------------------------------------------------------------------------------ */
+/* NCHW (C logical channels) <-> NHWC with channel stride Cs >= C (pad channels written 0). */
+int vst_nchw_to_nhwc(const float* x, float* y, int N, int C, int H, int W, int Cs, void* stream);
+int vst_nhwc_to_nchw(const float* x, float* y, int N, int C, int H, int W, int Cs, void* stream);
+/* Pack a PyTorch conv weight w[O][I][R][S] (ConvTranspose: pass Ci as O) for the GEMM kernels.
+ * mode VST_PACK_KC -> out[R][S][Ip][Op]; VST_PACK_CK -> out[R][S][Op][Ip]; Ip/Op are the padded
+ * channel strides (multiples of 4, zero filled). */
+int vst_weight_pack(const float* w, float* out, int O, int I, int R, int S, int Op, int Ip,
+                    int mode, void* stream);
+
+/* ---- convolution (implicit GEMM on fp32 MFMA) -------------------------------------------- */
+/* y[N][Ho][Wo][Cop] = act(conv(x[N][H][W][Cx], w) + bias).  wp = VST_PACK_KC pack
+ * ([R][S][Cx][Cop]); bias has Cop entries or is NULL.  pad_mode VST_PAD_ZERO / VST_PAD_REFLECT.
+ * Ho = (H + 2*pad - R)/stride + 1. */
+int vst_conv2d_fwd(const float* x, const float* wp, const float* bias, float* y,
+                   int N, int H, int W, int Cx, int Cop, int R, int S, int stride, int pad,
+                   int pad_mode, int act, float slope, void* stream);
+/* Transposed convolution / conv data-gradient (gather form, split by output parity class):
+ *   out[n][h][w][cx] = sum_{r,s,cy : h = ho*stride - pad + r, w = wo*stride - pad + s}
+ *                        in[n][ho][wo][cy] * wp[r][s][cy][cx]        (+ bias[cx], act)
+ * in is [N][Hi][Wi][Cy]; out is [N][Ho][Wo][Cx] (Ho/Wo given: (Hi-1)*stride - 2*pad + R + output_padding).
+ * For ConvTranspose2d forward pass wp = VST_PACK_CK pack of Wt seen as [Ci][Co] (i.e. O=Ci, I=Co)
+ * -> rows (r,s,ci) cols co; for the dgrad of a Conv2d pass its VST_PACK_CK pack. */
+int vst_conv2d_tfwd(const float* in, const float* wp, const float* bias, float* out,
+                    int N, int Hi, int Wi, int Cy, int Ho, int Wo, int Cx, int R, int S,
+                    int stride, int pad, int act, float slope, void* stream);
+/* Weight (and bias) gradient of y = conv(x, w):  dw[co][ci][r][s] (+)= sum_pix x_gather * dy,
+ * db[co] (+)= sum_pix dy (db may be NULL).  x: [N][H][W][Cx], dy: [N][Ho][Wo][Cyp].  dw is written
+ * with strides (so, si) for (co, ci) and r*S+s contiguous, for co < Co, ci < Ci (logical); pass
+ * so = Ci*R*S, si = R*S for a Conv2d weight.  A ConvTranspose2d weight Wt[Ci][Co][R][S] is the
+ * weight gradient of the equivalent conv x_T = conv(dy_T, .): call with x := grad of the convT
+ * output, dy := convT input, (Co, Ci) := (Ci_T, Co_T), db := NULL (use vst_channel_sum).  accumulate != 0 adds into dw/db.  Split-K partial slabs go to
+ * ws (vst_conv2d_wgrad_ws_bytes bytes) and are reduced in a fixed order (deterministic). */
+size_t vst_conv2d_wgrad_ws_bytes(int N, int H, int W, int Cx, int Ho, int Wo, int Cyp, int R, int S);
+int vst_conv2d_wgrad(const float* x, const float* dy, float* dw, float* db, float* ws,
+                     size_t ws_bytes, int N, int H, int W, int Cx, int Ho, int Wo, int Cyp, int R,
+                     int S, int stride, int pad, int pad_mode, int Co, int Ci, long so, long si,
+                     int accumulate, void* stream);
+/* db[c] (+)= sum over NHW pixels of x[p][c] for c < Cl (channel stride Cs); bias gradient of a layer
+ * whose output gradient is x.  ws: vst_channel_sum_ws_bytes bytes; fixed-order (deterministic). */
+size_t vst_channel_sum_ws_bytes(long NHW, int Cl);
+int vst_channel_sum(const float* x, float* db, float* ws, long NHW, int Cs, int Cl, int accumulate,
+                    void* stream);
+/* Fold the gradient of a ReflectionPad2d(p): dx[n][h][w][c] = sum of dxp over padded positions
+ * mapping to (h,w) (+ addend if non-NULL).  dxp: [N][H+2p][W+2p][C], dx/addend: [N][H][W][C]. */
+int vst_reflect_fold(const float* dxp, const float* addend, float* dx, int N, int H, int W, int C,
+                     int p, void* stream);
+
+/* ---- instance norm + activation ---------------------------------------------------------- */
+/* stats[n*C + c] = {mean, rstd} (2 floats interleaved: mean at 2*(n*C+c), rstd at +1), biased
+ * variance, eps.  ws: vst_instnorm_ws_bytes(N, HW, C) bytes. */
+size_t vst_instnorm_ws_bytes(int N, int HW, int C);
+int vst_instnorm_stats(const float* x, float* stats, float* ws, int N, int HW, int C, float eps,
+                       void* stream);
+/* y = act((x - mean) * rstd) (+ residual).  residual may be NULL. */
+int vst_instnorm_act_fwd(const float* x, const float* stats, const float* residual, float* y,
+                         int N, int HW, int C, int act, float slope, void* stream);
+/* Backward of y = act(IN(x)):  dx = rstd * (g - mean(g) - xhat * mean(g*xhat)),
+ * g = gy * act'(xhat).  ws: vst_instnorm_ws_bytes bytes. */
+int vst_instnorm_act_bwd(const float* gy, const float* x, const float* stats, float* dx, float* ws,
+                         int N, int HW, int C, int act, float slope, void* stream);
+/* Elementwise activation backward in place-safe form: dx = gy * act'(y) given the OUTPUT y. */
+int vst_act_bwd(const float* gy, const float* y, float* dx, long n, int act, float slope, void* stream);
+
+/* ---- flow warp, consistency mask, losses --------------------------------------------------- */
+/* out[n][h][w][c] = bilinear sample of x at (w + flow_x, h + flow_y) with the reference's
+ * normalisation (grid/max(W-1,1)) and align_corners flag; zeros padding.  x, out: NHWC (C stride Cs);
+ * flow: [N][2][H][W] (NCHW, as the reference stores it). */
+int vst_warp_fwd(const float* x, const float* flow, float* out, int N, int H, int W, int Cs,
+                 int align_corners, void* stream);
+/* gx[...] += bilinear-transpose scatter of gout (gx must be zero-initialised by the caller). */
+int vst_warp_bwd_input(const float* gout, const float* flow, float* gx, int N, int H, int W, int Cs,
+                       int align_corners, void* stream);
+/* mask[n][0][h][w] in {0,1} from forward/backward flows ff, bf ([N][2][H][W]). */
+int vst_fbcheck(const float* ff, const float* bf, float* mask, int N, int H, int W, void* stream);
+
+/* Losses.  Forward writes the scalar loss to loss[0] (device) using a per-block partial buffer
+ * `part` of vst_loss_part_floats(npix) floats and a fixed-order final sum (deterministic).
+ * Backward reads the upstream scalar gradient from device memory gout[0] (no host sync) and
+ * WRITES the full gradient tensor (padding channels zero), except where noted.
+ * Means run over npix * Cl elements (Cl logical channels of a channel stride Cs). */
+int vst_loss_part_floats(long npix);
+/* temporal (CycleGANCon cycle_gan_model.py:191-204):
+ *   loss = lambda * mean((mask * (b - warp(a, flow)))^2),  a, b: NHWC, flow [N][2][H][W], mask [N][H][W].
+ * bwd: gb written; ga ACCUMULATED (scatter through the warp) — either may be NULL. */
+int vst_loss_temporal(const float* a, const float* b, const float* flow, const float* mask,
+                      float* loss, float* part, int N, int H, int W, int Cs, int Cl, float lambda,
+                      void* stream);
+int vst_loss_temporal_bwd(const float* a, const float* b, const float* flow, const float* mask,
+                          const float* gout, float* ga, float* gb, int N, int H, int W, int Cs,
+                          int Cl, float lambda, void* stream);
+/* L1: loss = scale * mean|a - b|; grad = gout*scale*sign(a-b)/count (sign(0)=0, as torch). */
+int vst_loss_l1(const float* a, const float* b, float* loss, float* part, long npix, int Cs, int Cl,
+                float scale, void* stream);
+int vst_loss_l1_bwd(const float* a, const float* b, const float* gout, float* grad, long npix,
+                    int Cs, int Cl, float scale, void* stream);
+/* LSGAN: loss = scale * mean((a - target)^2); grad = gout*scale*2*(a-target)/count. */
+int vst_loss_mse_const(const float* a, float target, float* loss, float* part, long npix, int Cs,
+                       int Cl, float scale, void* stream);
+int vst_loss_mse_const_bwd(const float* a, float target, const float* gout, float* grad, long npix,
+                           int Cs, int Cl, float scale, void* stream);
+/* out[0] = scale * sum(part[0..n)) in a fixed order. */
+int vst_finish_sum(const float* part, int n, float* out, double scale, void* stream);
+
+/* ---- optimizer ------------------------------------------------------------------------------ */
+/* torch.optim.Adam (no weight decay, no amsgrad) over a flat parameter buffer:
+ *   m = b1 m + (1-b1) g; v = b2 v + (1-b2) g^2;
+ *   p -= lr/(1-b1^t) * m / (sqrt(v)/sqrt(1-b2^t) + eps)                                    */
+int vst_adam_step(float* p, const float* g, float* m, float* v, long n, float lr, float beta1,
+                  float beta2, float eps, int step, void* stream);
+/* y = a*x + b*y over n floats (gradient scaling / DP averaging helper). */
+int vst_axpby(const float* x, float* y, long n, float a, float b, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VST_HIP_H */

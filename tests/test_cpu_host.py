@@ -1,0 +1,82 @@
+"""CPU-only checks: the C-ABI library exports every symbol include/vst_hip.h declares, the host
+logic (state_dict compatibility with the reference, options, plugin discovery) matches the
+reference, and the product path refuses CPU tensors (no silent fallback)."""
+import ctypes
+import os
+import re
+
+import pytest
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _header_symbols():
+    txt = open(os.path.join(REPO, "include", "vst_hip.h")).read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\*?\s+\**(vst_\w+)\(", txt, re.M)))
+
+
+def test_library_exports_every_header_symbol():
+    import gbvst
+    path = gbvst._lib.build()
+    lib = ctypes.CDLL(path)
+    syms = _header_symbols()
+    assert len(syms) >= 25
+    for s in syms:
+        assert hasattr(lib, s), s
+    assert set(syms) == set(gbvst._lib.SIGNATURES), set(syms) ^ set(gbvst._lib.SIGNATURES)
+
+
+def test_state_dict_matches_reference_layout():
+    from gbvst import networks
+    from oracle import cpu_ref
+    for ngf, nb in ((64, 9), (8, 6)):
+        G = networks.define_G(3, 3, ngf, "resnet_%dblocks" % nb, "instance", False, "normal", 0.02, [])
+        R = cpu_ref.RefResnetGenerator(3, 3, ngf, nb)
+        assert cpu_ref.state_shapes(G) == cpu_ref.state_shapes(R)
+    D = networks.define_D(3, 64, "basic", 3, "instance", "normal", 0.02, [])
+    assert cpu_ref.state_shapes(D) == cpu_ref.state_shapes(cpu_ref.RefNLayerDiscriminator(3, 64))
+    assert sum(p.numel() for p in G.parameters()) > 0
+
+
+def test_flat_buffers_are_views():
+    from gbvst import networks
+    G = networks.define_G(3, 3, 8, "resnet_9blocks", "instance", False, "normal", 0.02, [])
+    n = sum(p.numel() for p in G.parameters())
+    assert G.flat_param.numel() == n
+    with torch.no_grad():
+        G.flat_param.fill_(0.5)
+    assert all(float(p.detach().mean()) == 0.5 for p in G.parameters())
+    sd = {k: torch.full_like(v, 0.25) for k, v in G.state_dict().items()}
+    G.load_state_dict(sd)
+    assert float(G.flat_param.mean()) == 0.25
+
+
+def test_unsupported_configs_raise():
+    from gbvst import networks
+    with pytest.raises(NotImplementedError):
+        networks.define_G(3, 3, 64, "unet_256", "instance")
+    with pytest.raises(NotImplementedError):
+        networks.define_G(3, 3, 64, "nope", "instance")
+    with pytest.raises(NotImplementedError):
+        networks.get_norm_layer("group")
+
+
+def test_options_and_plugin_discovery():
+    from gbvst import models, options
+    opt = options.default_opt(True)
+    for k, v in dict(ngf=64, ndf=64, netG="resnet_9blocks", netD="basic", norm="instance",
+                     init_gain=0.02, lr=2e-4, beta1=0.5, gan_mode="lsgan", pool_size=50,
+                     lr_policy="linear", n_epochs=100, n_epochs_decay=100, lambda_A=10.0,
+                     lambda_B=10.0, lambda_T=10.0, lambda_identity=0.5).items():
+        assert getattr(opt, k) == v, k
+    assert opt.gpu_ids == [0]
+    assert models.find_model_using_name("cycle_gan").__name__ == "CycleGANModel"
+    with pytest.raises(NotImplementedError):
+        models.find_model_using_name("pix2pix")
+
+
+def test_ops_refuse_cpu_tensors():
+    from gbvst import ops
+    with pytest.raises(RuntimeError):
+        ops.nchw_to_nhwc(torch.zeros(1, 3, 4, 4))

@@ -1,0 +1,214 @@
+"""GPU parity of every libvst_hip kernel family against the fp32 CPU reference (stock torch ops on
+the same inputs) and against the reference-generated golden fixtures.  Tolerances are written per
+test: convs compare with |err| <= 2e-5 * max|ref| + 1e-6 (fp32 MFMA is an exact fp32 fma chain;
+only the summation order differs from the CPU), elementwise/flow ops 1e-5 absolute."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module")
+def ops():
+    import gbvst
+    from gbvst import ops as o
+    gbvst._lib.load()
+    return o
+
+
+def _g(seed, shape, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(*shape, generator=g) * scale
+
+
+def _close(got, ref, tol=2e-5, what=""):
+    got = got.detach().float().cpu()
+    ref = ref.detach().float().cpu()
+    assert got.shape == ref.shape, (what, got.shape, ref.shape)
+    scale = ref.abs().max().item() + 1e-12
+    err = (got - ref).abs().max().item()
+    assert err <= tol * scale + 1e-6, f"{what}: max|err|={err:.3e} scale={scale:.3e}"
+
+
+def _nhwc(x, ops):
+    return ops.nchw_to_nhwc(x.to(DEV).contiguous())
+
+
+def _nchw(y, c, ops):
+    return ops.nhwc_to_nchw(y.contiguous(), c).cpu()
+
+
+CONV_CASES = [
+    # name, N, Ci, H, W, Co, k, stride, pad, mode
+    ("c7s1_reflect_img", 2, 3, 20, 18, 16, 7, 1, 3, "reflect"),
+    ("d_3x3_s2", 2, 16, 16, 20, 32, 3, 2, 1, "zero"),
+    ("res_3x3_reflect", 2, 32, 12, 10, 32, 3, 1, 1, "reflect"),
+    ("res_wide", 1, 256, 16, 16, 256, 3, 1, 1, "reflect"),
+    ("out_c7s1_3", 2, 16, 14, 14, 3, 7, 1, 3, "reflect"),
+    ("D_4x4_s2_img", 2, 3, 32, 32, 16, 4, 2, 1, "zero"),
+    ("D_4x4_s1", 2, 32, 9, 11, 64, 4, 1, 1, "zero"),
+    ("D_head_1", 2, 64, 7, 7, 1, 4, 1, 1, "zero"),
+    ("odd_big_M", 3, 8, 37, 29, 72, 3, 1, 1, "zero"),
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES, ids=[c[0] for c in CONV_CASES])
+def test_conv_fwd_dgrad_wgrad(ops, case):
+    name, N, Ci, H, W, Co, k, st, pad, mode = case
+    x = _g(1, (N, Ci, H, W))
+    w = _g(2, (Co, Ci, k, k), 0.1)
+    b = _g(3, (Co,), 0.1)
+    xr = x.clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    br = b.clone().requires_grad_(True)
+    xp = F.pad(xr, (pad,) * 4, mode="reflect") if mode == "reflect" else xr
+    yr = F.conv2d(xp, wr, br, stride=st, padding=0 if mode == "reflect" else pad)
+    gy = _g(4, tuple(yr.shape))
+    yr.backward(gy)
+    wd = w.to(DEV)
+    kc = ops.weight_pack(wd, ops.PACK_KC)
+    ck = ops.weight_pack(wd, ops.PACK_CK)
+    bp = torch.zeros(ops.cpad(Co), device=DEV)
+    bp[:Co] = b.to(DEV)
+    xn = _nhwc(x, ops)
+    y = ops.conv2d_fwd(xn, kc, bp, ops.cpad(Co), k, k, st, pad, mode)
+    _close(_nchw(y, Co, ops), yr, what=name + " fwd")
+    # dgrad
+    gyn = _nhwc(gy, ops)
+    if mode == "reflect":
+        dxp = ops.conv2d_tfwd(gyn, ck, None, H + 2 * pad, W + 2 * pad, xn.shape[-1], k, k, 1, 0)
+        dx = ops.reflect_fold(dxp, pad)
+    else:
+        dx = ops.conv2d_tfwd(gyn, ck, None, H, W, xn.shape[-1], k, k, st, pad)
+    _close(_nchw(dx, Ci, ops), xr.grad, what=name + " dgrad")
+    # wgrad + bias grad (accumulate into a pre-filled buffer to test accumulation)
+    dw = torch.full((Co, Ci, k, k), 0.5, device=DEV)
+    db = torch.full((Co,), 0.25, device=DEV)
+    ops.conv2d_wgrad(xn, gyn, dw, db, k, k, st, pad, mode, Co, Ci, Ci * k * k, k * k, accumulate=True)
+    _close(dw.cpu() - 0.5, wr.grad, what=name + " wgrad")
+    _close(db.cpu() - 0.25, br.grad, what=name + " bgrad")
+
+
+@pytest.mark.parametrize("cfg", [(2, 16, 8, 8, 8), (1, 256, 64, 16, 16), (2, 32, 3, 6, 5)])
+def test_conv_transpose(ops, cfg):
+    """ConvTranspose2d(k3, s2, p1, op1) fwd, dgrad (= strided conv) and weight grad."""
+    N, Ci, Co, H, W = cfg
+    x = _g(5, (N, Ci, H, W))
+    w = _g(6, (Ci, Co, 3, 3), 0.1)
+    b = _g(7, (Co,), 0.1)
+    xr, wr, br = (t.clone().requires_grad_(True) for t in (x, w, b))
+    yr = F.conv_transpose2d(xr, wr, br, stride=2, padding=1, output_padding=1)
+    gy = _g(8, tuple(yr.shape))
+    yr.backward(gy)
+    wd = w.to(DEV)
+    kc = ops.weight_pack(wd, ops.PACK_KC)
+    ck = ops.weight_pack(wd, ops.PACK_CK)
+    bp = torch.zeros(ops.cpad(Co), device=DEV)
+    bp[:Co] = b.to(DEV)
+    xn = _nhwc(x, ops)
+    y = ops.conv2d_tfwd(xn, ck, bp, 2 * H, 2 * W, ops.cpad(Co), 3, 3, 2, 1)
+    _close(_nchw(y, Co, ops), yr, what="convT fwd")
+    gyn = _nhwc(gy, ops)
+    dx = ops.conv2d_fwd(gyn, kc, None, xn.shape[-1], 3, 3, 2, 1, "zero")
+    _close(_nchw(dx, Ci, ops), xr.grad, what="convT dgrad")
+    dw = torch.zeros((Ci, Co, 3, 3), device=DEV)
+    ops.conv2d_wgrad(gyn, xn, dw, None, 3, 3, 2, 1, "zero", Ci, Co, Co * 9, 9)
+    _close(dw.cpu(), wr.grad, what="convT wgrad")
+    db = torch.zeros(Co, device=DEV)
+    ops.channel_sum(gyn, db, Co)
+    _close(db.cpu(), br.grad, what="convT bgrad")
+
+
+@pytest.mark.parametrize("act", ["relu", "lrelu", "none"])
+def test_instnorm_act(ops, act):
+    N, C, H, W = 2, 64, 24, 20
+    x = _g(9, (N, C, H, W), 2.0) + 0.5
+    res = _g(10, (N, C, H, W))
+    xr = x.clone().requires_grad_(True)
+    yr = F.instance_norm(xr, eps=1e-5)
+    if act == "relu":
+        yr = F.relu(yr)
+    elif act == "lrelu":
+        yr = F.leaky_relu(yr, 0.2)
+    outr = yr + res if act == "none" else yr
+    gy = _g(11, (N, C, H, W))
+    outr.backward(gy)
+    xn = _nhwc(x, ops)
+    s = ops.instnorm_stats(xn)
+    y = ops.instnorm_act_fwd(xn, s, act, 0.2, residual=_nhwc(res, ops) if act == "none" else None)
+    _close(_nchw(y, C, ops), outr, tol=1e-5, what="IN fwd")
+    dx = ops.instnorm_act_bwd(_nhwc(gy, ops), xn, s, act, 0.2)
+    _close(_nchw(dx, C, ops), xr.grad, tol=1e-5, what="IN bwd")
+
+
+def test_warp_golden(ops, golden):
+    g = golden("warp")
+    for case in ("zero", "int", "frac", "oob", "h1", "w1"):
+        x = torch.from_numpy(g[f"{case}_x"])
+        flow = torch.from_numpy(g[f"{case}_flow"]).to(DEV)
+        C = x.shape[1]
+        y = ops.warp_nhwc(_nhwc(x, ops), flow)
+        np.testing.assert_allclose(_nchw(y, C, ops).numpy(), g[f"{case}_y"], atol=2e-6, err_msg=case)
+        gx = ops.warp_bwd_nhwc(_nhwc(torch.from_numpy(g[f"{case}_gout"]), ops), flow)
+        np.testing.assert_allclose(_nchw(gx, C, ops).numpy(), g[f"{case}_dx"], atol=1e-5, err_msg=case)
+
+
+def test_fbcheck_golden(ops, golden):
+    g = golden("fbc")
+    for case in ("cons", "incons"):
+        m = ops.fbcheck(torch.from_numpy(g[f"{case}_ff"]).to(DEV), torch.from_numpy(g[f"{case}_bf"]).to(DEV))
+        got = m.cpu().numpy()
+        # bit-exact {0,1} mask; a threshold tie may flip a pixel only on fp32 rounding
+        assert (got != g[f"{case}_mask"]).mean() <= 1e-3, case
+
+
+def test_losses(ops):
+    from oracle import cpu_ref
+    N, H, W = 2, 16, 24
+    a = _g(12, (N, 3, H, W))
+    b = _g(13, (N, 3, H, W))
+    flow = _g(14, (N, 2, H, W), 3.0)
+    mask = (torch.rand(N, 1, H, W, generator=torch.Generator().manual_seed(15)) < 0.8).float()
+    ar, br = a.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    lt = cpu_ref.temporal_loss(ar, br, flow, mask, 10.0)
+    lt.backward()
+    an, bn = _nhwc(a, ops), _nhwc(b, ops)
+    fl, mk = flow.to(DEV), mask.to(DEV)
+    l = ops.loss_temporal(an, bn, fl, mk, 10.0)
+    assert abs(l.item() - lt.item()) <= 1e-5 * abs(lt.item())
+    one = torch.ones((), device=DEV)
+    ga, gb = torch.zeros_like(an), torch.empty_like(bn)
+    ops.loss_temporal_bwd(an, bn, fl, mk, one, ga, gb, 10.0)
+    _close(_nchw(ga, 3, ops), ar.grad, 1e-5, "temporal d/da")
+    _close(_nchw(gb, 3, ops), br.grad, 1e-5, "temporal d/db")
+    ar.grad = None
+    l1r = (ar - b).abs().mean() * 5.0
+    l1r.backward()
+    l1 = ops.loss_l1(an, bn, 5.0)
+    assert abs(l1.item() - l1r.item()) <= 1e-5 * l1r.item()
+    _close(_nchw(ops.loss_l1_bwd(an, bn, one, 5.0), 3, ops), ar.grad, 1e-6, "l1 grad")
+    p = _g(16, (N, 1, 7, 7))
+    pr = p.clone().requires_grad_(True)
+    mr = ((pr - 1.0) ** 2).mean()
+    mr.backward()
+    pn = _nhwc(p, ops)
+    assert abs(ops.loss_mse_const(pn, 1.0).item() - mr.item()) <= 1e-5 * mr.item()
+    _close(_nchw(ops.loss_mse_const_bwd(pn, 1.0, one), 1, ops), pr.grad, 1e-6, "mse grad")
+
+
+def test_adam_matches_torch(ops):
+    n = 1000
+    p0 = _g(17, (n,))
+    grads = [_g(18 + i, (n,)) * 10 ** (-i) for i in range(4)]
+    pr = p0.clone().requires_grad_(True)
+    opt = torch.optim.Adam([pr], lr=2e-4, betas=(0.5, 0.999))
+    p, m, v = p0.to(DEV), torch.zeros(n, device=DEV), torch.zeros(n, device=DEV)
+    for i, gr in enumerate(grads):
+        pr.grad = gr.clone()
+        opt.step()
+        ops.adam_step(p, gr.to(DEV), m, v, 2e-4, 0.5, 0.999, 1e-8, i + 1)
+    np.testing.assert_allclose(p.cpu().numpy(), pr.detach().numpy(), rtol=0, atol=1e-7)

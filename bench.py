@@ -1,0 +1,219 @@
+#!/usr/bin/env python3
+"""Benchmark: CycleGAN video train step (G + D + flow-warp temporal loss), 256x256, B=4 per GPU.
+
+BASELINE.json metric "frames/sec: CycleGAN train step (G+D+flow-warp loss) 256x256 at 1/2/4/8 GPUs".
+One step = CycleGANModel.optimize_parameters() (CycleGANCon semantics: 7 generator passes, 6
+discriminator passes, temporal warp loss, two Adam updates) over one synthetic batch already
+resident in HBM.  Weak scaling: every rank processes B_local=4 frame pairs; value = all frames
+processed by all ranks / max-over-ranks wall time of exactly K steps (barrier + device sync on both
+sides).  Multi-GPU: one process per GPU (torchrun), gradients exchanged with RCCL all_reduce.
+
+Also reported (same JSON line):
+  roofline      the dominant kernel (ResnetBlock 3x3 conv fprop, 16384x256x2304 implicit GEMM at
+                B=4) timed with HIP events on its launch stream: algorithmic FLOPs / avg duration
+                vs the fp32 MFMA peak; traffic from profiles/*_pmc.json when present.
+  cpu_baseline  rank 0 only, N=1: the CPU oracle (stock PyTorch, NCHW fp32) on the host cores,
+                one B=4 step after a B=1 warm-up (oracle is imported only for this leg).
+  inference     generator-only inference fps at 256x256, B=16 (north_star's secondary number).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+FP32_MFMA_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 (spec; 155 measured)
+TRAIN_TFLOP_PER_FRAME = 2.1753     # SURVEY §8d / BASELINE.md: CycleGANCon step conv FLOPs @256^2
+G_GFLOP_PER_FRAME = 99.10          # ResnetGenerator fwd @256^2
+
+
+def synthetic_batch(B, H, W, seed, device):
+    """SURVEY §8d synthetic C2 inputs: (u8/255-0.5)/0.5 images, smooth flow (bicubic upsample of an
+    N(0,4^2) 9x9 grid), Bernoulli(0.8) mask on a 32x32 grid — generated on the device."""
+    import torch.nn.functional as F
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    imgs = [((torch.randint(0, 256, (B, 3, H, W), generator=g).float() / 255.0) - 0.5) / 0.5 for _ in range(3)]
+    coarse = torch.randn(B, 2, 9, 9, generator=g) * 4.0
+    flow = F.interpolate(coarse, size=(H, W), mode="bicubic", align_corners=True)
+    mcoarse = (torch.rand(B, 1, 32, 32, generator=g) < 0.8).float()
+    mask = F.interpolate(mcoarse, size=(H, W), mode="nearest")
+    return [t.to(device).contiguous() for t in imgs + [mask, flow]]
+
+
+def dominant_kernel_roofline(device, B, reps=20):
+    """Time the ResnetBlock conv (3x3, reflect 1, 256->256 @64x64, B frames) on its own stream."""
+    from gbvst import ops
+    x = torch.randn(B, 64, 64, 256, device=device)
+    w = torch.randn(256, 256, 3, 3, device=device) * 0.02
+    kc = ops.weight_pack(w, ops.PACK_KC)
+    bias = torch.zeros(256, device=device)
+    y = torch.empty(B, 64, 64, 256, device=device)
+    s = torch.cuda.Stream(device=device)
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            ops.conv2d_fwd(x, kc, bias, 256, 3, 3, 1, 1, "reflect", out=y)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(reps):
+            ops.conv2d_fwd(x, kc, bias, 256, 3, 3, 1, 1, "reflect", out=y)
+        e1.record(s)
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    flop = 2.0 * (B * 64 * 64) * 256 * (256 * 9)
+    achieved = flop / (ms * 1e-3) / 1e12
+    traffic = None
+    pmc = os.path.join(HERE, "profiles", "r01_conv_fprop_pmc.json")
+    if os.path.exists(pmc):
+        try:
+            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    return {"kernel": "conv_fprop_k<128,128,64,64> (ResnetBlock 3x3 256->256 @64x64, B=%d)" % B,
+            "bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
+            "traffic": traffic, "avg_launch_ms": round(ms, 4), "flop_per_launch": flop}
+
+
+def inference_fps(device, B=16, reps=10):
+    from gbvst import networks
+    G = networks.define_G(3, 3, 64, "resnet_9blocks", "instance", False, "normal", 0.02,
+                          [device.index or 0])
+    x = torch.randn(B, 3, 256, 256, device=device)
+    with torch.no_grad():
+        for _ in range(2):
+            G(x)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            G(x)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / reps
+    fps = B / dt
+    return {"metric": "generator-only inference fps 256x256", "batch": B, "value": round(fps, 2),
+            "unit": "frames/s", "tflops": round(fps * G_GFLOP_PER_FRAME / 1e3, 2)}
+
+
+def cpu_baseline(B=4, H=256, W=256):
+    """Oracle (stock PyTorch CPU, NCHW fp32) train step on the host cores: 1 B=1 warm-up step, then
+    one timed B=4 step (a bounded ~10-60 s sample of the same workload)."""
+    from oracle import cpu_ref
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    m = cpu_ref.RefCycleGANCon(device="cpu")
+    a, a2, b, mask, flow = cpu_ref.synthetic_batch(1, H, W, seed=99)
+    m.set_input_fc2(a, a2, b, mask, flow)
+    m.optimize_parameters()
+    a, a2, b, mask, flow = cpu_ref.synthetic_batch(B, H, W, seed=100)
+    m.set_input_fc2(a, a2, b, mask, flow)
+    t0 = time.perf_counter()
+    m.optimize_parameters()
+    dt = time.perf_counter() - t0
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": round(B / dt, 4), "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/cpu_ref.RefCycleGANCon: 1 train step B={B} {H}x{W} fp32 after a B=1 warm-up "
+                      f"({dt:.1f} s; torch CPU threads={threads}; {model})"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=4, help="frame pairs per GPU (C2: 4)")
+    ap.add_argument("--size", type=int, default=256)
+    ap.add_argument("--pool", type=int, default=50)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+
+    import gbvst
+    gbvst._lib.load()
+    from gbvst import dp
+    from gbvst.cycle_gan_model import CycleGANModel
+    from gbvst.options import default_opt
+
+    torch.manual_seed(0)
+    opt = default_opt(True, gpu_ids=[local], pool_size=args.pool)
+    model = CycleGANModel(opt)
+    hookG = hookD = None
+    if world > 1:
+        nets = [model.netG_A, model.netG_B, model.netD_A, model.netD_B]
+        dp.broadcast_params(nets)
+        ex = dp.GradExchange(world)
+        hookG = hookD = ex
+    B, S = args.batch, args.size
+    a, a2, b, mask, flow = synthetic_batch(B, S, S, seed=1234 + rank, device=device)
+    from gbvst import ops
+    model.set_input_nhwc(ops.nchw_to_nhwc(a), ops.nchw_to_nhwc(a2), ops.nchw_to_nhwc(b), mask, flow)
+
+    for _ in range(args.warmup):
+        model.optimize_parameters(hookG, hookD)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        model.optimize_parameters(hookG, hookD)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    losses = model.get_current_losses()
+
+    frames = B * world * args.steps
+    value = frames / elapsed
+    out = {
+        "metric": "frames/sec: CycleGAN train step (G+D+flow-warp loss) 256x256",
+        "value": round(value, 3), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+        "data": "synthetic (SURVEY §8d generator; random-init weights, init_type=normal 0.02)",
+        "config": {"workload": "C2: CycleGANCon optimize_parameters, resnet_9blocks G + basic PatchGAN D, "
+                               "ngf=ndf=64, %dx%d, B_local=%d, pool_size=%d, flow-warp temporal loss" % (S, S, B, args.pool),
+                   "global_batch": B * world, "height": S, "width": S, "parallelism": "dp%d" % world},
+        "algorithmic_tflops": round(value * TRAIN_TFLOP_PER_FRAME, 2),
+        "step_frac_of_fp32_mfma_peak": round(value * TRAIN_TFLOP_PER_FRAME / (FP32_MFMA_PEAK_TFLOPS * world), 4),
+        "final_losses": {k: round(v, 5) for k, v in losses.items()},
+    }
+    if rank == 0 and not args.no_extras:
+        out["roofline"] = dominant_kernel_roofline(device, B)
+        out["inference"] = inference_fps(device)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -37,16 +37,17 @@ SIGNATURES = {
     "vst_nhwc_to_nchw": (I, [P, P, I, I, I, I, I, P]),
     "vst_weight_pack": (I, [P, P, I, I, I, I, I, I, I, P]),
     "vst_conv2d_fwd": (I, [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, P]),
-    "vst_conv2d_tfwd": (I, [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, F, P]),
+    "vst_conv2d_tfwd": (I, [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, F, P]),
     "vst_conv2d_wgrad_ws_bytes": (SZ, [I, I, I, I, I, I, I, I, I]),
-    "vst_conv2d_wgrad": (I, [P, P, P, P, P, SZ, I, I, I, I, I, I, I, I, I, I, I, I, I, I, L, L, I, P]),
+    "vst_conv2d_wgrad": (I, [P, P, P, P, SZ, I, I, I, I, I, I, I, I, I, I, I, I, I, I, L, L, I, P]),
+    "vst_debug_set_tiles": (None, [I, I, I]),
     "vst_reflect_fold": (I, [P, P, P, I, I, I, I, I, P]),
     "vst_channel_sum_ws_bytes": (SZ, [L, I]),
     "vst_channel_sum": (I, [P, P, P, L, I, I, I, P]),
     "vst_instnorm_ws_bytes": (SZ, [I, I, I]),
     "vst_instnorm_stats": (I, [P, P, P, I, I, I, F, P]),
     "vst_instnorm_act_fwd": (I, [P, P, P, P, I, I, I, I, F, P]),
-    "vst_instnorm_act_bwd": (I, [P, P, P, P, P, I, I, I, I, F, P]),
+    "vst_instnorm_act_bwd": (I, [P, P, P, P, P, P, I, I, I, I, F, I, P]),
     "vst_act_bwd": (I, [P, P, P, L, I, F, P]),
     "vst_warp_fwd": (I, [P, P, P, I, I, I, I, I, P]),
     "vst_warp_bwd_input": (I, [P, P, P, I, I, I, I, I, P]),

@@ -64,6 +64,19 @@ __device__ __forceinline__ double wave_sum_d(double v) {
   return v;
 }
 
+__device__ __forceinline__ void add_f4(float4& a, const float4& b) {
+  a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+}
+
 inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
+
+// VALU kernels for convolutions with <= 4 output channels (skinny.hip)
+int skinny_out_launch(int mode, const float* in, const float* wp, const float* bias,
+                      const float* addend, float* out, int N, int Hi, int Wi, int Cin, int Ho,
+                      int Wo, int R, int S, int st, int pad, int reflect, int act, float slope,
+                      hipStream_t s);
+int skinny_wgrad_launch(const float* x, const float* dy, float* slab, int H, int W, int Cx, int Ho,
+                        int Wo, int S, int st, int pad, int reflect, int Mw, int P, int chunk,
+                        int nsplit, hipStream_t s);
 
 }  // namespace vst

@@ -4,32 +4,39 @@
 // nn.ReflectionPad2d dispatch in the reference ResnetGenerator / NLayerDiscriminator
 // (methods/GAN-based/CycleGAN/models/networks.py:340-367, 404-426, 556-578).
 //
-// All three kernels compute a tile C[BM x BN] = sum_k A[m][k] * B[k][n] with
-//   * 256 threads = 4 waves, each wave owning a WM x WN sub-tile of 32x32 MFMA blocks,
-//   * BK = 32 deep K-steps double-buffered in LDS (one barrier per K-step); both LDS operand
-//     images are k-major ([k][row], row contiguous, +4 float pad) so every MFMA operand fetch is
-//     a conflict-free ds_read_b32 over 32 consecutive rows,
-//   * the next K-step's global loads issued into registers before the MFMAs of the current one
-//     (register-staged pipeline), written to the other LDS buffer after them.
-// Operand gathers fold the padding (zero or reflect) and the stride into address generation, so
-// no im2col / padded copy is ever materialised.  fp32 MFMA is exact fp32 fma arithmetic, which is
-// what keeps the path within the reference's fp32 tolerance.
+// Every kernel computes C[BM x BN] = sum_k A[m][k] * B[k][n] per workgroup with
+//   * NW = 4 or 8 waves (256/512 threads), each owning a WM x WN sub-tile of 32x32 MFMA blocks;
+//     a 128x128 tile with 8 waves gives two waves per SIMD inside one workgroup, which is what the
+//     CycleGAN shapes need (B=4: a 16384x256 output is exactly one 128x128 tile per CU);
+//   * BK = 32 deep K-steps double-buffered in LDS, one barrier per K-step.  Both LDS operand images
+//     are k-major ([k][row], +4 float pad) so every MFMA operand fetch is a conflict-free ds_read
+//     over 32 consecutive rows; fragments of step kk+2 are fetched while step kk's MFMAs issue;
+//   * the global loads of the NEXT K-step are interleaved into the MFMA sequence of the current
+//     one (2 per MFMA group, so their address arithmetic runs in the shadow of the 64-cycle fp32
+//     MFMAs) and written to the other LDS buffer after the last MFMA group;
+// Operand gathers fold padding (zero or reflect), stride and transposition into address
+// generation: no im2col, no padded copies, no zero-insertion.  fp32 MFMA is an exact fp32 fma
+// chain, so results differ from the CPU reference only by summation order.
 //
-//   conv_fprop_k  : y = conv(x, w)         m = output pixel, n = out channel, k = (r, s, ci)
-//   conv_tconv_k  : transposed conv / dgrad, gathered per output-parity class (blockIdx.z), so a
-//                   stride-2 layer only walks the taps that hit each class (no zero-insertion)
-//   conv_wgrad_k  : dw = x_gather^T * dy    m = (r, s, ci) [+ one all-ones row -> bias grad],
-//                   n = out channel, k = pixel; split-K over blockIdx.z into an fp32 slab,
-//                   reduced deterministically by wgrad_reduce_k.
+//   conv_fprop_k : y = conv(x, w)            m = output pixel, n = out channel, k = (r, s, ci)
+//   conv_tconv_k : transposed conv / dgrad    gathered per output-parity class (blockIdx.z) so a
+//                  stride-2 layer walks only the taps that hit each class; for stride 1 with
+//                  reflect padding the gather adds the mirrored contributions of ReflectionPad2d's
+//                  backward directly (no padded gradient buffer, no fold pass); optional residual
+//                  addend fused in the epilogue
+//   conv_wgrad_k : dw = x_gather^T * dy       m = (r, s, ci), n = out channel, k = pixel;
+//                  split-K over blockIdx.z into an fp32 slab, summed in a fixed split order
+//                  (deterministic) by wgrad_sum_k and written to [Co][Ci][R][S] by wgrad_store_k.
 #include "common.h"
 
 namespace vst {
 
-constexpr int NT = 256;
 constexpr int BK = 32;
 
 template <int BM, int BN, int WM, int WN>
 struct Tile {
+  static constexpr int NW = (BM / WM) * (BN / WN);
+  static constexpr int NT = 64 * NW;
   static constexpr int LDA = BM + 4;
   static constexpr int LDB = BN + 4;
   static constexpr int WAVES_N = BN / WN;
@@ -37,29 +44,93 @@ struct Tile {
   static constexpr int NI = WN / 32;
   static constexpr int A_ELEMS = BK * LDA;
   static constexpr int B_ELEMS = BK * LDB;
-  static_assert((BM / WM) * (BN / WN) == 4, "4 waves per block");
+  static constexpr int STAGE = A_ELEMS + B_ELEMS;
+  static_assert(NW == 4 || NW == 8, "4 or 8 waves per block");
   static_assert(WM % 32 == 0 && WN % 32 == 0, "32x32 MFMA blocks");
 };
 
-// MFMA over one BK-deep LDS stage.
-template <int BM, int BN, int WM, int WN>
+// MFMA over one BK-deep LDS stage (8 groups of 2 k-pairs).  hook(g) runs at the start of group g
+// (global loads of the next stage); fragments for the next group are fetched during this one.
+template <int BM, int BN, int WM, int WN, class Hook>
 __device__ __forceinline__ void mma_stage(const float* __restrict__ As, const float* __restrict__ Bs,
-                                          f32x16 (&acc)[WM / 32][WN / 32], int wm0, int wn0, int lane) {
+                                          f32x16 (&acc)[WM / 32][WN / 32], int wm0, int wn0, int lane,
+                                          Hook hook) {
   using T = Tile<BM, BN, WM, WN>;
   const int kh = lane >> 5, li = lane & 31;
+  const float* pa = As + kh * T::LDA + wm0 + li;
+  const float* pb = Bs + kh * T::LDB + wn0 + li;
+  float a0[T::MI], b0[T::NI], a1[T::MI], b1[T::NI];
 #pragma unroll
-  for (int kk = 0; kk < BK / 2; ++kk) {
-    const int krow = 2 * kk + kh;
-    float a[T::MI], b[T::NI];
+  for (int i = 0; i < T::MI; ++i) a0[i] = pa[32 * i];
 #pragma unroll
-    for (int i = 0; i < T::MI; ++i) a[i] = As[krow * T::LDA + wm0 + 32 * i + li];
+  for (int j = 0; j < T::NI; ++j) b0[j] = pb[32 * j];
 #pragma unroll
-    for (int j = 0; j < T::NI; ++j) b[j] = Bs[krow * T::LDB + wn0 + 32 * j + li];
+  for (int g = 0; g < BK / 4; ++g) {
+    const int kk = 2 * g;
+    hook(g);
+#pragma unroll
+    for (int i = 0; i < T::MI; ++i) a1[i] = pa[(2 * kk + 2) * T::LDA + 32 * i];
+#pragma unroll
+    for (int j = 0; j < T::NI; ++j) b1[j] = pb[(2 * kk + 2) * T::LDB + 32 * j];
 #pragma unroll
     for (int i = 0; i < T::MI; ++i)
 #pragma unroll
       for (int j = 0; j < T::NI; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[i], b0[j], acc[i][j], 0, 0, 0);
+    if (g + 1 < BK / 4) {
+#pragma unroll
+      for (int i = 0; i < T::MI; ++i) a0[i] = pa[(2 * kk + 4) * T::LDA + 32 * i];
+#pragma unroll
+      for (int j = 0; j < T::NI; ++j) b0[j] = pb[(2 * kk + 4) * T::LDB + 32 * j];
+    }
+#pragma unroll
+    for (int i = 0; i < T::MI; ++i)
+#pragma unroll
+      for (int j = 0; j < T::NI; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[i], b1[j], acc[i][j], 0, 0, 0);
+  }
+}
+
+template <int MI, int NI>
+__device__ __forceinline__ void zero_acc(f32x16 (&acc)[MI][NI]) {
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+}
+
+// Double-buffered K loop shared by all kernels.  load_one(i, k0) issues global load number i
+// (0 <= i < NLOAD, compile-time after unrolling) of the stage starting at k0 into registers;
+// adv() steps the incremental index state by BK; store(buf) writes the staged registers to LDS.
+template <int BM, int BN, int WM, int WN, int NLOAD, class LoadOne, class Adv, class Store>
+__device__ __forceinline__ void main_loop(float* smem, int nk, int kbase,
+                                          f32x16 (&acc)[WM / 32][WN / 32], LoadOne load_one, Adv adv,
+                                          Store store) {
+  using T = Tile<BM, BN, WM, WN>;
+  static_assert(NLOAD <= 2 * (BK / 4), "at most two loads per MFMA group");
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wm0 = (wave / T::WAVES_N) * WM, wn0 = (wave % T::WAVES_N) * WN;
+  if (nk > 0) {
+#pragma unroll
+    for (int i = 0; i < NLOAD; ++i) load_one(i, kbase);
+    store(smem);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    float* cur = smem + (kt & 1) * T::STAGE;
+    const bool next = kt + 1 < nk;
+    if (next) adv();
+    const int k0n = kbase + (kt + 1) * BK;
+    mma_stage<BM, BN, WM, WN>(cur, cur + T::A_ELEMS, acc, wm0, wn0, lane, [&](int g) {
+      if (next) {
+        if (2 * g < NLOAD) load_one(2 * g, k0n);
+        if (2 * g + 1 < NLOAD) load_one(2 * g + 1, k0n);
+      }
+    });
+    if (next) store(smem + ((kt + 1) & 1) * T::STAGE);
+    __syncthreads();
   }
 }
 
@@ -70,37 +141,50 @@ __device__ __forceinline__ int remap_mtile(int bx, int nx) {
   return (bx & 7) * (nx >> 3) + (bx >> 3);
 }
 
+// transposing store of a thread's float4 A chunk (4 consecutive k of one row m) into [k][m]
+template <int LDA>
+__device__ __forceinline__ void store_a_t(float* As, int kr, int ml, const float4& v) {
+  As[(kr + 0) * LDA + ml] = v.x;
+  As[(kr + 1) * LDA + ml] = v.y;
+  As[(kr + 2) * LDA + ml] = v.z;
+  As[(kr + 3) * LDA + ml] = v.w;
+}
+
+__device__ __forceinline__ void add4(float4& a, const float4& b) {
+  a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+}
+
 // ------------------------------------------------------------------------------------------ fprop
 template <int BM, int BN, int WM, int WN>
-__global__ __launch_bounds__(NT, 2) void conv_fprop_k(
+__global__ __launch_bounds__((Tile<BM, BN, WM, WN>::NT), 2) void conv_fprop_k(
     const float* __restrict__ x, const float* __restrict__ wp, const float* __restrict__ bias,
     float* __restrict__ y, int H, int W, int C, int Ho, int Wo, int Cop, int S, int st, int pad,
     int reflect, int act, float slope, int M, int Ktot) {
   using T = Tile<BM, BN, WM, WN>;
-  constexpr int KSTEP4 = NT / BM;             // k4 stride between a thread's A loads
-  constexpr int A_LD = BK / 4 / KSTEP4;       // float4 A loads per thread per stage
+  constexpr int NT = T::NT;
+  constexpr int KSTEP4 = NT / BM;         // k4 stride between a thread's A loads
+  constexpr int A_LD = BK / 4 / KSTEP4;   // float4 A loads per thread per stage
   constexpr int BN4 = BN / 4;
   constexpr int KRSTEP = NT / BN4;
   constexpr int B_LD = BK / KRSTEP;
   static_assert(NT % BM == 0 && A_LD >= 1 && B_LD >= 1, "tile shape");
-  __shared__ __attribute__((aligned(16))) float smem[2 * (T::A_ELEMS + T::B_ELEMS)];
+  __shared__ __attribute__((aligned(16))) float smem[2 * T::STAGE];
 
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int mt = remap_mtile(blockIdx.x, gridDim.x);
   const int m0 = mt * BM, n0 = blockIdx.y * BN;
 
-  // ---- A gather state: one output pixel per thread, A_LD k-offsets
   const int ml = t % BM, k4b = t / BM;
   const int m = m0 + ml;
   const bool mval = m < M;
   int hb = 0, wb = 0;
-  long ibase = 0;
+  const float* xb = x;
   if (mval) {
     const int hw = Ho * Wo;
-    const int n = m / hw, rem = m - n * hw, ho = rem / Wo, wo = rem - (rem / Wo) * Wo;
+    const int n = m / hw, rem = m - n * hw, ho = rem / Wo, wo = rem - ho * Wo;
     hb = ho * st - pad;
     wb = wo * st - pad;
-    ibase = (long)n * H * W * C;
+    xb = x + (long)n * H * W * C;
   }
   int ac[A_LD], as_[A_LD], ar[A_LD];
 #pragma unroll
@@ -111,15 +195,14 @@ __global__ __launch_bounds__(NT, 2) void conv_fprop_k(
     ar[j] = rs / S;
     as_[j] = rs - ar[j] * S;
   }
-  // ---- B state
   const int bn4 = t % BN4, bkr = t / BN4;
   const int bcol = n0 + 4 * bn4;
   const bool bcval = bcol < Cop;
 
   float4 ra[A_LD], rb[B_LD];
-  auto load_a = [&](int k0) {
-#pragma unroll
-    for (int j = 0; j < A_LD; ++j) {
+  auto load_one = [&](int i, int k0) {
+    if (i < A_LD) {
+      const int j = i;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       const int kk = k0 + 4 * (k4b + KSTEP4 * j);
       if (mval && kk < Ktot) {
@@ -131,12 +214,18 @@ __global__ __launch_bounds__(NT, 2) void conv_fprop_k(
         } else {
           ok = (unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W;
         }
-        if (ok) v = *reinterpret_cast<const float4*>(x + ibase + ((long)hi * W + wi) * C + ac[j]);
+        if (ok) v = *reinterpret_cast<const float4*>(xb + ((long)hi * W + wi) * C + ac[j]);
       }
       ra[j] = v;
+    } else {
+      const int j = i - A_LD;
+      const int kr = k0 + bkr + KRSTEP * j;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (bcval && kr < Ktot) v = *reinterpret_cast<const float4*>(wp + (long)kr * Cop + bcol);
+      rb[j] = v;
     }
   };
-  auto adv_a = [&]() {
+  auto adv = [&]() {
 #pragma unroll
     for (int j = 0; j < A_LD; ++j) {
       ac[j] += BK;
@@ -146,58 +235,20 @@ __global__ __launch_bounds__(NT, 2) void conv_fprop_k(
       }
     }
   };
-  auto load_b = [&](int k0) {
-#pragma unroll
-    for (int j = 0; j < B_LD; ++j) {
-      const int kr = k0 + bkr + KRSTEP * j;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (bcval && kr < Ktot) v = *reinterpret_cast<const float4*>(wp + (long)kr * Cop + bcol);
-      rb[j] = v;
-    }
-  };
-  auto store = [&](int buf) {
-    float* As = smem + buf * (T::A_ELEMS + T::B_ELEMS);
+  auto store = [&](float* As) {
     float* Bs = As + T::A_ELEMS;
 #pragma unroll
-    for (int j = 0; j < A_LD; ++j) {
-      const int kr = 4 * (k4b + KSTEP4 * j);
-      As[(kr + 0) * T::LDA + ml] = ra[j].x;
-      As[(kr + 1) * T::LDA + ml] = ra[j].y;
-      As[(kr + 2) * T::LDA + ml] = ra[j].z;
-      As[(kr + 3) * T::LDA + ml] = ra[j].w;
-    }
+    for (int j = 0; j < A_LD; ++j) store_a_t<T::LDA>(As, 4 * (k4b + KSTEP4 * j), ml, ra[j]);
 #pragma unroll
     for (int j = 0; j < B_LD; ++j)
       *reinterpret_cast<float4*>(Bs + (bkr + KRSTEP * j) * T::LDB + 4 * bn4) = rb[j];
   };
 
   f32x16 acc[T::MI][T::NI];
-#pragma unroll
-  for (int i = 0; i < T::MI; ++i)
-#pragma unroll
-    for (int j = 0; j < T::NI; ++j)
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  zero_acc(acc);
+  main_loop<BM, BN, WM, WN, A_LD + B_LD>(smem, (Ktot + BK - 1) / BK, 0, acc, load_one, adv, store);
 
   const int wm0 = (wave / T::WAVES_N) * WM, wn0 = (wave % T::WAVES_N) * WN;
-  const int nk = (Ktot + BK - 1) / BK;
-  load_a(0);
-  load_b(0);
-  store(0);
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) {
-      adv_a();
-      load_a((kt + 1) * BK);
-      load_b((kt + 1) * BK);
-    }
-    const float* As = smem + cur * (T::A_ELEMS + T::B_ELEMS);
-    mma_stage<BM, BN, WM, WN>(As, As + T::A_ELEMS, acc, wm0, wn0, lane);
-    if (kt + 1 < nk) store(cur ^ 1);
-    __syncthreads();
-  }
-
-  // ---- epilogue: bias + activation, NHWC store (32 consecutive channels per half-wave)
 #pragma unroll
   for (int i = 0; i < T::MI; ++i)
 #pragma unroll
@@ -214,21 +265,26 @@ __global__ __launch_bounds__(NT, 2) void conv_fprop_k(
 }
 
 // ------------------------------------------------------------------- transposed conv / dgrad
-// out[n][h][w][cx] = sum in[n][ho][wo][cy] * wp[r][s][cy][cx] over h = ho*st - pad + r.
-// blockIdx.z = parity class (a, b): h = a + st*hh, w = b + st*ww; only taps r = r0 + st*i with
+// out[n][h][w][cx] = sum in[n][ho][wo][cy] * wp[r][s][cy][cx] over h = ho*st - pad + r (zero pad)
+// or, with reflect (st == 1), over reflect(ho + r - pad) == h.
+// blockIdx.z = parity class (a, b): h = a + st*hh; only taps r = r0 + st*i with
 // r0 = (a + pad) mod st contribute, at ho = (h + pad - r) / st (exact).
-template <int BM, int BN, int WM, int WN>
-__global__ __launch_bounds__(NT, 2) void conv_tconv_k(
+constexpr int NOPOS = -(1 << 20);
+
+template <int BM, int BN, int WM, int WN, int ST>
+__global__ __launch_bounds__((Tile<BM, BN, WM, WN>::NT), 2) void conv_tconv_k(
     const float* __restrict__ in, const float* __restrict__ wp, const float* __restrict__ bias,
-    float* __restrict__ out, int Hi, int Wi, int Cy, int Ho, int Wo, int Cx, int R, int S, int st,
-    int pad, int act, float slope, int Nimg) {
+    const float* __restrict__ addend, float* __restrict__ out, int Hi, int Wi, int Cy, int Ho,
+    int Wo, int Cx, int R, int S, int st_rt, int pad, int reflect, int act, float slope, int Nimg) {
   using T = Tile<BM, BN, WM, WN>;
+  const int st = ST > 0 ? ST : st_rt;  // compile-time stride for the CycleGAN layers (1, 2)
+  constexpr int NT = T::NT;
   constexpr int KSTEP4 = NT / BM;
   constexpr int A_LD = BK / 4 / KSTEP4;
   constexpr int BN4 = BN / 4;
   constexpr int KRSTEP = NT / BN4;
   constexpr int B_LD = BK / KRSTEP;
-  __shared__ __attribute__((aligned(16))) float smem[2 * (T::A_ELEMS + T::B_ELEMS)];
+  __shared__ __attribute__((aligned(16))) float smem[2 * T::STAGE];
 
   const int ca = blockIdx.z / st, cb = blockIdx.z % st;
   const int Hc = Ho > ca ? (Ho - ca + st - 1) / st : 0;
@@ -246,44 +302,81 @@ __global__ __launch_bounds__(NT, 2) void conv_tconv_k(
   const int ml = t % BM, k4b = t / BM;
   const int m = m0 + ml;
   const bool mval = m < M;
-  int hp = 0, wq = 0;
-  long ibase = 0;
+  // (h + pad) for the direct term and, for reflect, the one mirrored image row/column
+  int hp = 0, wq = 0, hm = NOPOS, wmr = NOPOS;
+  const float* ib = in;
   if (mval) {
     const int hw = Hc * Wc;
     const int n = m / hw, rem = m - n * hw, hh = rem / Wc, ww = rem - hh * Wc;
-    hp = ca + st * hh + pad;
-    wq = cb + st * ww + pad;
-    ibase = (long)n * Hi * Wi * Cy;
+    const int h = ca + st * hh, w = cb + st * ww;
+    hp = h + pad;
+    wq = w + pad;
+    if (reflect) {
+      if (h >= 1 && h <= pad) hm = pad - h;
+      else if (h >= Ho - 1 - pad && h <= Ho - 2) hm = 2 * Ho - 2 - h + pad;
+      if (w >= 1 && w <= pad) wmr = pad - w;
+      else if (w >= Wo - 1 - pad && w <= Wo - 2) wmr = 2 * Wo - 2 - w + pad;
+    }
+    ib = in + (long)n * Hi * Wi * Cy;
   }
   int ac[A_LD], ais[A_LD], air[A_LD];
 #pragma unroll
   for (int j = 0; j < A_LD; ++j) {
     const int k = 4 * (k4b + KSTEP4 * j);
-    ac[j] = Cy > 0 ? k % Cy : 0;
-    const int tp = Cy > 0 ? k / Cy : 0;
+    ac[j] = k % Cy;
+    const int tp = k / Cy;
     air[j] = ns > 0 ? tp / ns : 0;
     ais[j] = tp - air[j] * ns;
   }
   const int bn4 = t % BN4, bkr = t / BN4;
   const int bcol = n0 + 4 * bn4;
   const bool bcval = bcol < Cx;
+  int bc[B_LD], bis[B_LD], bir[B_LD];
+#pragma unroll
+  for (int j = 0; j < B_LD; ++j) {
+    const int k = bkr + KRSTEP * j;
+    bc[j] = k % Cy;
+    const int tp = k / Cy;
+    bir[j] = ns > 0 ? tp / ns : 0;
+    bis[j] = tp - bir[j] * ns;
+  }
 
   float4 ra[A_LD], rb[B_LD];
-  auto load_a = [&](int k0) {
-#pragma unroll
-    for (int j = 0; j < A_LD; ++j) {
+  auto gather1 = [&](int hpos, int wpos, int r, int s, int c, float4& v) {
+    const int dh = hpos - r, dw = wpos - s;
+    if (dh >= 0 && dw >= 0) {
+      const int ho = dh / st, wo = dw / st;
+      if (ho < Hi && wo < Wi)
+        add4(v, *reinterpret_cast<const float4*>(ib + ((long)ho * Wi + wo) * Cy + c));
+    }
+  };
+  auto load_one = [&](int i, int k0) {
+    if (i < A_LD) {
+      const int j = i;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       const int kk = k0 + 4 * (k4b + KSTEP4 * j);
       if (mval && kk < Ktot) {
         const int r = r0 + st * air[j], s = s0 + st * ais[j];
-        const int ho = (hp - r) / st, wo = (wq - s) / st;
-        if (hp - r >= 0 && wq - s >= 0 && ho < Hi && wo < Wi)
-          v = *reinterpret_cast<const float4*>(in + ibase + ((long)ho * Wi + wo) * Cy + ac[j]);
+        gather1(hp, wq, r, s, ac[j], v);
+        if (hm != NOPOS) gather1(hm, wq, r, s, ac[j], v);
+        if (wmr != NOPOS) {
+          gather1(hp, wmr, r, s, ac[j], v);
+          if (hm != NOPOS) gather1(hm, wmr, r, s, ac[j], v);
+        }
       }
       ra[j] = v;
+    } else {
+      const int j = i - A_LD;
+      const int kk = k0 + bkr + KRSTEP * j;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (bcval && kk < Ktot) {
+        const int row = ((r0 + st * bir[j]) * S + (s0 + st * bis[j])) * Cy + bc[j];
+        v = *reinterpret_cast<const float4*>(wp + (long)row * Cx + bcol);
+      }
+      rb[j] = v;
     }
   };
-  auto adv_a = [&]() {
+  auto adv = [&]() {
 #pragma unroll
     for (int j = 0; j < A_LD; ++j) {
       ac[j] += BK;
@@ -292,66 +385,29 @@ __global__ __launch_bounds__(NT, 2) void conv_tconv_k(
         if (++ais[j] == ns) { ais[j] = 0; ++air[j]; }
       }
     }
-  };
-  // B rows follow the same k decomposition (tap, cy) but index the full [R][S][Cy] row space.
-  auto load_b = [&](int k0) {
 #pragma unroll
     for (int j = 0; j < B_LD; ++j) {
-      const int kk = k0 + bkr + KRSTEP * j;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (bcval && kk < Ktot) {
-        const int cy = kk % Cy, tp = kk / Cy;
-        const int ir = tp / ns, is = tp - ir * ns;
-        const int row = ((r0 + st * ir) * S + (s0 + st * is)) * Cy + cy;
-        v = *reinterpret_cast<const float4*>(wp + (long)row * Cx + bcol);
+      bc[j] += BK;
+      while (bc[j] >= Cy) {
+        bc[j] -= Cy;
+        if (++bis[j] == ns) { bis[j] = 0; ++bir[j]; }
       }
-      rb[j] = v;
     }
   };
-  auto store = [&](int buf) {
-    float* As = smem + buf * (T::A_ELEMS + T::B_ELEMS);
+  auto store = [&](float* As) {
     float* Bs = As + T::A_ELEMS;
 #pragma unroll
-    for (int j = 0; j < A_LD; ++j) {
-      const int kr = 4 * (k4b + KSTEP4 * j);
-      As[(kr + 0) * T::LDA + ml] = ra[j].x;
-      As[(kr + 1) * T::LDA + ml] = ra[j].y;
-      As[(kr + 2) * T::LDA + ml] = ra[j].z;
-      As[(kr + 3) * T::LDA + ml] = ra[j].w;
-    }
+    for (int j = 0; j < A_LD; ++j) store_a_t<T::LDA>(As, 4 * (k4b + KSTEP4 * j), ml, ra[j]);
 #pragma unroll
     for (int j = 0; j < B_LD; ++j)
       *reinterpret_cast<float4*>(Bs + (bkr + KRSTEP * j) * T::LDB + 4 * bn4) = rb[j];
   };
 
   f32x16 acc[T::MI][T::NI];
-#pragma unroll
-  for (int i = 0; i < T::MI; ++i)
-#pragma unroll
-    for (int j = 0; j < T::NI; ++j)
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  zero_acc(acc);
+  main_loop<BM, BN, WM, WN, A_LD + B_LD>(smem, (Ktot + BK - 1) / BK, 0, acc, load_one, adv, store);
 
   const int wm0 = (wave / T::WAVES_N) * WM, wn0 = (wave % T::WAVES_N) * WN;
-  const int nk = (Ktot + BK - 1) / BK;
-  if (nk > 0) {
-    load_a(0);
-    load_b(0);
-    store(0);
-  }
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) {
-      adv_a();
-      load_a((kt + 1) * BK);
-      load_b((kt + 1) * BK);
-    }
-    const float* As = smem + cur * (T::A_ELEMS + T::B_ELEMS);
-    mma_stage<BM, BN, WM, WN>(As, As + T::A_ELEMS, acc, wm0, wn0, lane);
-    if (kt + 1 < nk) store(cur ^ 1);
-    __syncthreads();
-  }
-
   const int hw = Hc * Wc;
 #pragma unroll
   for (int i = 0; i < T::MI; ++i)
@@ -366,20 +422,22 @@ __global__ __launch_bounds__(NT, 2) void conv_tconv_k(
         if (mm >= M) continue;
         const int nimg = mm / hw, rem = mm - nimg * hw, hh = rem / Wc, ww = rem - hh * Wc;
         const long o = (((long)nimg * Ho + (ca + st * hh)) * Wo + (cb + st * ww)) * Cx + n;
-        out[o] = apply_act(acc[i][j][r] + bv, act, slope);
+        float v = apply_act(acc[i][j][r] + bv, act, slope);
+        if (addend) v += addend[o];
+        out[o] = v;
       }
     }
 }
 
 // ------------------------------------------------------------------------------------------ wgrad
-// slab[z][m][n] = sum_{pixels p in split z} A[p][m] * dy[p][n],  A[p][m=(r,s,ci)] = x gathered;
-// row m == Mw (if with_bias) is the all-ones row, giving the bias gradient sum_p dy[p][n].
+// slab[z][m][n] = sum_{pixels p in split z} A[p][m] * dy[p][n],  A[p][m=(r,s,ci)] = x gathered.
 template <int BM, int BN, int WM, int WN>
-__global__ __launch_bounds__(NT, 2) void conv_wgrad_k(
+__global__ __launch_bounds__((Tile<BM, BN, WM, WN>::NT), 2) void conv_wgrad_k(
     const float* __restrict__ x, const float* __restrict__ dy, float* __restrict__ slab, int H,
-    int W, int Cx, int Ho, int Wo, int Cyp, int S, int st, int pad, int reflect, int Mw, int Mtot,
-    int P, int chunk) {
+    int W, int Cx, int Ho, int Wo, int Cyp, int S, int st, int pad, int reflect, int Mw, int P,
+    int chunk) {
   using T = Tile<BM, BN, WM, WN>;
+  constexpr int NT = T::NT;
   constexpr int BM4 = BM / 4;
   constexpr int AKSTEP = NT / BM4;
   constexpr int A_LD = BK / AKSTEP;
@@ -387,25 +445,23 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_k(
   constexpr int KRSTEP = NT / BN4;
   constexpr int B_LD = BK / KRSTEP;
   static_assert(A_LD >= 1 && B_LD >= 1, "tile shape");
-  __shared__ __attribute__((aligned(16))) float smem[2 * (T::A_ELEMS + T::B_ELEMS)];
+  __shared__ __attribute__((aligned(16))) float smem[2 * T::STAGE];
 
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
   const int pbeg = blockIdx.z * chunk;
   const int pend = min(P, pbeg + chunk);
 
-  // A: this thread's 4 consecutive m (fixed tap), AKSTEP-strided pixel rows
   const int am4 = t % BM4, akb = t / BM4;
   const int am = m0 + 4 * am4;
-  const int amode = am < Mw ? 0 : (am == Mw ? 1 : 2);  // 0 gather, 1 ones row, 2 zero
+  const bool amval = am < Mw;
   int ar = 0, as_ = 0, aci = 0;
-  if (amode == 0) {
+  if (amval) {
     aci = am % Cx;
     const int rs = am / Cx;
     ar = rs / S;
     as_ = rs - ar * S;
   }
-  // pixel decomposition for each of this thread's A rows (incremented by BK per stage)
   int pn[A_LD], pho[A_LD], pwo[A_LD];
 #pragma unroll
   for (int j = 0; j < A_LD; ++j) {
@@ -421,31 +477,32 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_k(
   const bool bcval = bcol < Cyp;
 
   float4 ra[A_LD], rb[B_LD];
-  auto load_a = [&](int p0) {
-#pragma unroll
-    for (int j = 0; j < A_LD; ++j) {
+  auto load_one = [&](int i, int p0) {
+    if (i < A_LD) {
+      const int j = i;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       const int p = p0 + akb + AKSTEP * j;
-      if (p < pend) {
-        if (amode == 0) {
-          int hi = pho[j] * st - pad + ar, wi = pwo[j] * st - pad + as_;
-          bool ok = true;
-          if (reflect) {
-            hi = reflect_idx(hi, H);
-            wi = reflect_idx(wi, W);
-          } else {
-            ok = (unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W;
-          }
-          if (ok)
-            v = *reinterpret_cast<const float4*>(x + (((long)pn[j] * H + hi) * W + wi) * Cx + aci);
-        } else if (amode == 1) {
-          v.x = 1.f;
+      if (amval && p < pend) {
+        int hi = pho[j] * st - pad + ar, wi = pwo[j] * st - pad + as_;
+        bool ok = true;
+        if (reflect) {
+          hi = reflect_idx(hi, H);
+          wi = reflect_idx(wi, W);
+        } else {
+          ok = (unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W;
         }
+        if (ok) v = *reinterpret_cast<const float4*>(x + (((long)pn[j] * H + hi) * W + wi) * Cx + aci);
       }
       ra[j] = v;
+    } else {
+      const int j = i - A_LD;
+      const int p = p0 + bkr + KRSTEP * j;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (bcval && p < pend) v = *reinterpret_cast<const float4*>(dy + (long)p * Cyp + bcol);
+      rb[j] = v;
     }
   };
-  auto adv_a = [&]() {
+  auto adv = [&]() {
 #pragma unroll
     for (int j = 0; j < A_LD; ++j) {
       pwo[j] += BK;
@@ -455,17 +512,7 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_k(
       }
     }
   };
-  auto load_b = [&](int p0) {
-#pragma unroll
-    for (int j = 0; j < B_LD; ++j) {
-      const int p = p0 + bkr + KRSTEP * j;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (bcval && p < pend) v = *reinterpret_cast<const float4*>(dy + (long)p * Cyp + bcol);
-      rb[j] = v;
-    }
-  };
-  auto store = [&](int buf) {
-    float* As = smem + buf * (T::A_ELEMS + T::B_ELEMS);
+  auto store = [&](float* As) {
     float* Bs = As + T::A_ELEMS;
 #pragma unroll
     for (int j = 0; j < A_LD; ++j)
@@ -476,34 +523,12 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_k(
   };
 
   f32x16 acc[T::MI][T::NI];
-#pragma unroll
-  for (int i = 0; i < T::MI; ++i)
-#pragma unroll
-    for (int j = 0; j < T::NI; ++j)
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  zero_acc(acc);
+  const int nk = pend > pbeg ? (pend - pbeg + BK - 1) / BK : 0;
+  main_loop<BM, BN, WM, WN, A_LD + B_LD>(smem, nk, pbeg, acc, load_one, adv, store);
 
   const int wm0 = (wave / T::WAVES_N) * WM, wn0 = (wave % T::WAVES_N) * WN;
-  const int nk = pend > pbeg ? (pend - pbeg + BK - 1) / BK : 0;
-  if (nk > 0) {
-    load_a(pbeg);
-    load_b(pbeg);
-    store(0);
-  }
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) {
-      adv_a();
-      load_a(pbeg + (kt + 1) * BK);
-      load_b(pbeg + (kt + 1) * BK);
-    }
-    const float* As = smem + cur * (T::A_ELEMS + T::B_ELEMS);
-    mma_stage<BM, BN, WM, WN>(As, As + T::A_ELEMS, acc, wm0, wn0, lane);
-    if (kt + 1 < nk) store(cur ^ 1);
-    __syncthreads();
-  }
-
-  float* sl = slab + (long)blockIdx.z * Mtot * Cyp;
+  float* sl = slab + (long)blockIdx.z * Mw * Cyp;
 #pragma unroll
   for (int i = 0; i < T::MI; ++i)
 #pragma unroll
@@ -513,33 +538,41 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_k(
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int mm = m0 + wm0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        if (mm < Mtot) sl[(long)mm * Cyp + n] = acc[i][j][r];
+        if (mm < Mw) sl[(long)mm * Cyp + n] = acc[i][j][r];
       }
     }
 }
 
-// dw[co*so + ci*si + rs] (+)= sum_z slab[z][rs*Cx + ci][co];  db[co] (+)= sum_z slab[z][Mw][co].
-__global__ void wgrad_reduce_k(const float* __restrict__ slab, float* __restrict__ dw,
-                               float* __restrict__ db, int nsplit, int Mtot, int Mw, int Cx, int Cyp,
-                               int RS, int Co, int Ci, long so, long si, int accumulate) {
-  const long total = (long)Co * Ci * RS;
-  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx < total) {
-    // idx enumerates (co, ci, rs) with rs fastest -> contiguous dw writes for so/si of PyTorch layout
-    const int rs = idx % RS;
-    const long q = idx / RS;
-    const int ci = q % Ci;
-    const int co = q / Ci;
-    const long row = (long)rs * Cx + ci;
-    float s = 0.f;
-    for (int z = 0; z < nsplit; ++z) s += slab[((long)z * Mtot + row) * Cyp + co];
-    float* d = dw + co * so + ci * si + rs;
-    *d = accumulate ? *d + s : s;
+// slab[0][m][n] = sum_z slab[z][m][n] (fixed order), float4 over n: coalesced and fully parallel.
+__global__ void wgrad_sum_k(float* __restrict__ slab, long n4, int nsplit) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n4) return;
+  float4* s = reinterpret_cast<float4*>(slab);
+  float4 a = s[i];
+  for (int z = 1; z < nsplit; ++z) add4(a, s[i + (long)z * n4]);
+  s[i] = a;
+}
+
+// dw[co*so + ci*si + rs] (+)= S[rs*Cx + ci][co] via a 64x64 LDS transpose tile (reads coalesced
+// along co, writes along m = (rs, ci)).
+__global__ void wgrad_store_k(const float* __restrict__ Ssum, float* __restrict__ dw, int Mw, int Cx,
+                              int Cyp, int RS, int Co, int Ci, long so, long si, int accumulate) {
+  __shared__ float tile[64][65];
+  const int m0 = blockIdx.x * 64, c0 = blockIdx.y * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int r = ty; r < 64; r += 4) {
+    const int m = m0 + r, c = c0 + tx;
+    tile[r][tx] = (m < Mw && c < Cyp) ? Ssum[(long)m * Cyp + c] : 0.f;
   }
-  if (db && idx < Co) {
-    float s = 0.f;
-    for (int z = 0; z < nsplit; ++z) s += slab[((long)z * Mtot + Mw) * Cyp + idx];
-    db[idx] = accumulate ? db[idx] + s : s;
+  __syncthreads();
+  for (int r = ty; r < 64; r += 4) {
+    const int c = c0 + r, m = m0 + tx;
+    if (c >= Co || m >= Mw) continue;
+    const int ci = m % Cx, rs = m / Cx;
+    if (ci >= Ci) continue;
+    float* d = dw + c * so + ci * si + rs;
+    const float v = tile[tx][r];
+    *d = accumulate ? *d + v : v;
   }
 }
 
@@ -566,62 +599,70 @@ __global__ void reflect_fold_k(const float* __restrict__ dxp, const float* __res
   const float4* src = reinterpret_cast<const float4*>(dxp);
   float4 acc = addend ? reinterpret_cast<const float4*>(addend)[idx] : make_float4(0.f, 0.f, 0.f, 0.f);
   for (int a = 0; a < nh; ++a)
-    for (int b = 0; b < nw; ++b) {
-      const float4 v = src[(((long)n * Hp + hs[a]) * Wp + ws[b]) * C4 + c4];
-      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
-    }
+    for (int b = 0; b < nw; ++b) add4(acc, src[(((long)n * Hp + hs[a]) * Wp + ws[b]) * C4 + c4]);
   reinterpret_cast<float4*>(dx)[idx] = acc;
 }
 
 // ---------------------------------------------------------------------------------- dispatch
-template <int BM, int BN, int WM, int WN>
-static int launch_fprop(const float* x, const float* wp, const float* bias, float* y, int N, int H,
-                        int W, int C, int Ho, int Wo, int Cop, int R, int S, int st, int pad,
-                        int reflect, int act, float slope, hipStream_t s) {
-  const int M = N * Ho * Wo, K = R * S * C;
-  dim3 grid(ceil_div(M, BM), ceil_div(Cop, BN));
-  hipLaunchKernelGGL((conv_fprop_k<BM, BN, WM, WN>), grid, dim3(NT), 0, s, x, wp, bias, y, H, W, C,
-                     Ho, Wo, Cop, S, st, pad, reflect, act, slope, M, K);
-  return check_launch("conv2d_fwd");
+// Tile kinds: 0 = 128x128 (8 waves, 64x32 each), 1 = 64x128 (4 waves), 2 = 128x64 (4 waves),
+// 3 = 64x64 (4 waves), 4 = 256x32 (skinny N), 5 = 128x128 (4 waves, 64x64 each).
+enum TileKind { T128x128w8 = 0, T64x128 = 1, T128x64 = 2, T64x64 = 3, T256x32 = 4, T128x128w4 = 5, TAUTO = -1 };
+static int g_tile_override[3] = {TAUTO, TAUTO, TAUTO};
+
+static int tile_bm(TileKind k) { return k == T64x128 || k == T64x64 ? 64 : (k == T256x32 ? 256 : 128); }
+static int tile_bn(TileKind k) {
+  return k == T128x64 || k == T64x64 ? 64 : (k == T256x32 ? 32 : 128);
 }
 
-template <int BM, int BN, int WM, int WN>
-static int launch_tconv(const float* in, const float* wp, const float* bias, float* out, int N,
-                        int Hi, int Wi, int Cy, int Ho, int Wo, int Cx, int R, int S, int st,
-                        int pad, int act, float slope, hipStream_t s) {
-  const int Hc = (Ho + st - 1) / st, Wc = (Wo + st - 1) / st;
-  const int Mmax = N * Hc * Wc;
-  dim3 grid(ceil_div(Mmax, BM), ceil_div(Cx, BN), st * st);
-  hipLaunchKernelGGL((conv_tconv_k<BM, BN, WM, WN>), grid, dim3(NT), 0, s, in, wp, bias, out, Hi,
-                     Wi, Cy, Ho, Wo, Cx, R, S, st, pad, act, slope, N);
-  return check_launch("conv2d_tfwd");
-}
-
-// Tile choice: 128x128 when the channel dim allows and the grid has >= ~2 blocks/CU worth of
-// work, otherwise narrower N tiles (skinny output channels: 3 or 1 logical, 4 padded).
-enum TileKind { T128x128, T128x64, T256x32, T64x64 };
-
-static TileKind pick_tile(long M, int Nc) {
+static TileKind pick_tile(long M, int Nc, int which) {
+  if (g_tile_override[which] != TAUTO) return (TileKind)g_tile_override[which];
   if (Nc <= 32) return T256x32;
-  if (Nc <= 64) return M >= 128L * 256 ? T128x64 : T64x64;
-  if (M / 128 * ((Nc + 127) / 128) >= 256) return T128x128;
+  if (Nc <= 64) return M / 128 >= 256 ? T128x64 : T64x64;
+  const long n128 = (Nc + 127) / 128;
+  if ((M / 128) * n128 >= 200) return T128x128w8;
+  if ((M / 64) * n128 >= 200) return T64x128;
   return T64x64;
 }
 
+#define VST_DISPATCH_TILE(kind, LAUNCH)                       \
+  switch (kind) {                                              \
+    case T128x128w8: LAUNCH(128, 128, 64, 32); break;          \
+    case T64x128: LAUNCH(64, 128, 32, 64); break;              \
+    case T128x64: LAUNCH(128, 64, 64, 32); break;              \
+    case T256x32: LAUNCH(256, 32, 64, 32); break;              \
+    case T128x128w4: LAUNCH(128, 128, 64, 64); break;          \
+    default: LAUNCH(64, 64, 32, 32); break;                    \
+  }
+
 struct WgradPlan {
-  int Mw, Mtot, nsplit, chunk, gx, gy;
+  int Mw, nsplit, chunk;
+  TileKind tile;
 };
 
 static WgradPlan plan_wgrad(int N, int Ho, int Wo, int Cx, int Cyp, int R, int S) {
   WgradPlan p;
   p.Mw = R * S * Cx;
-  p.Mtot = p.Mw + 4;  // + ones row group for the bias gradient
   const int P = N * Ho * Wo;
-  p.gx = ceil_div(p.Mtot, 128);
-  p.gy = ceil_div(Cyp, Cyp <= 32 ? 32 : 64);
-  const int tiles = p.gx * p.gy;
-  int ns = ceil_div(1024, tiles);                     // aim for ~4 blocks per CU
-  const int max_ns = ceil_div(P, 4 * BK);             // at least 4 K-steps per split
+  if (Cyp == 4) {  // VALU skinny path: one thread per (tap, 4 input channels) per split
+    p.tile = T256x32;
+    int ns = ceil_div(65536, p.Mw / 4);
+    if (ns > 64) ns = 64;
+    const int max_ns = ceil_div(P, 64);
+    if (ns > max_ns) ns = max_ns;
+    if (ns < 1) ns = 1;
+    p.chunk = ceil_div(P, ns);
+    p.nsplit = ceil_div(P, p.chunk);
+    return p;
+  }
+  if (Cyp <= 32) p.tile = T256x32;
+  else if (Cyp <= 64) p.tile = p.Mw >= 1024 ? T128x64 : T64x64;
+  else p.tile = p.Mw >= 1024 ? T128x128w8 : T64x128;
+  if (g_tile_override[2] != TAUTO) p.tile = (TileKind)g_tile_override[2];
+  const int tiles = ceil_div(p.Mw, tile_bm(p.tile)) * ceil_div(Cyp, tile_bn(p.tile));
+  const int target = p.tile == T128x128w8 ? 256 : 512;  // ~one 8-wave / two 4-wave blocks per CU
+  int ns = ceil_div(target, tiles);
+  if (ns > 64) ns = 64;
+  const int max_ns = ceil_div(P, 8 * BK);  // at least 8 K-steps per split
   if (ns > max_ns) ns = max_ns;
   if (ns < 1) ns = 1;
   p.chunk = ceil_div(ceil_div(P, ns), BK) * BK;
@@ -632,6 +673,12 @@ static WgradPlan plan_wgrad(int N, int Ho, int Wo, int Cx, int Cyp, int R, int S
 }  // namespace vst
 
 using namespace vst;
+
+extern "C" void vst_debug_set_tiles(int fprop, int tconv, int wgrad) {
+  g_tile_override[0] = fprop;
+  g_tile_override[1] = tconv;
+  g_tile_override[2] = wgrad;
+}
 
 extern "C" int vst_conv2d_fwd(const float* x, const float* wp, const float* bias, float* y, int N,
                               int H, int W, int Cx, int Cop, int R, int S, int stride, int pad,
@@ -645,37 +692,49 @@ extern "C" int vst_conv2d_fwd(const float* x, const float* wp, const float* bias
   VST_REQUIRE(Ho > 0 && Wo > 0, "conv2d_fwd: empty output");
   const int refl = pad_mode == VST_PAD_REFLECT;
   hipStream_t s = (hipStream_t)stream;
-  switch (pick_tile((long)N * Ho * Wo, Cop)) {
-    case T128x128:
-      return launch_fprop<128, 128, 64, 64>(x, wp, bias, y, N, H, W, Cx, Ho, Wo, Cop, R, S, stride, pad, refl, act, slope, s);
-    case T128x64:
-      return launch_fprop<128, 64, 64, 32>(x, wp, bias, y, N, H, W, Cx, Ho, Wo, Cop, R, S, stride, pad, refl, act, slope, s);
-    case T256x32:
-      return launch_fprop<256, 32, 64, 32>(x, wp, bias, y, N, H, W, Cx, Ho, Wo, Cop, R, S, stride, pad, refl, act, slope, s);
-    default:
-      return launch_fprop<64, 64, 32, 32>(x, wp, bias, y, N, H, W, Cx, Ho, Wo, Cop, R, S, stride, pad, refl, act, slope, s);
-  }
+  const int M = N * Ho * Wo, K = R * S * Cx;
+  if (Cop == 4)  // image-channel outputs / PatchGAN head: VALU path (skinny.hip)
+    return skinny_out_launch(0, x, wp, bias, nullptr, y, N, H, W, Cx, Ho, Wo, R, S, stride, pad, refl,
+                             act, slope, s);
+#define VST_FPROP(BM_, BN_, WM_, WN_)                                                           \
+  hipLaunchKernelGGL((conv_fprop_k<BM_, BN_, WM_, WN_>), dim3(ceil_div(M, BM_), ceil_div(Cop, BN_)),  \
+                     dim3(Tile<BM_, BN_, WM_, WN_>::NT), 0, s, x, wp, bias, y, H, W, Cx, Ho, Wo, Cop, S, \
+                     stride, pad, refl, act, slope, M, K)
+  VST_DISPATCH_TILE(pick_tile(M, Cop, 0), VST_FPROP)
+#undef VST_FPROP
+  return check_launch("conv2d_fwd");
 }
 
-extern "C" int vst_conv2d_tfwd(const float* in, const float* wp, const float* bias, float* out,
-                               int N, int Hi, int Wi, int Cy, int Ho, int Wo, int Cx, int R, int S,
-                               int stride, int pad, int act, float slope, void* stream) {
+extern "C" int vst_conv2d_tfwd(const float* in, const float* wp, const float* bias,
+                               const float* addend, float* out, int N, int Hi, int Wi, int Cy,
+                               int Ho, int Wo, int Cx, int R, int S, int stride, int pad,
+                               int pad_mode, int act, float slope, void* stream) {
   VST_REQUIRE(in && wp && out, "conv2d_tfwd: null pointer");
   VST_REQUIRE(N > 0 && Hi > 0 && Wi > 0 && Ho > 0 && Wo > 0 && R > 0 && S > 0 && stride > 0 && pad >= 0,
               "conv2d_tfwd: bad shape");
   VST_REQUIRE(Cy % 4 == 0 && Cx % 4 == 0, "conv2d_tfwd: channel strides must be multiples of 4");
+  const int refl = pad_mode == VST_PAD_REFLECT;
+  VST_REQUIRE(!refl || (stride == 1 && Ho > 2 * pad + 1 && Wo > 2 * pad + 1),
+              "conv2d_tfwd: reflect needs stride 1 and H, W > 2*pad+1");
   hipStream_t s = (hipStream_t)stream;
-  const long Mc = (long)N * ((Ho + stride - 1) / stride) * ((Wo + stride - 1) / stride);
-  switch (pick_tile(Mc * stride * stride, Cx)) {
-    case T128x128:
-      return launch_tconv<128, 128, 64, 64>(in, wp, bias, out, N, Hi, Wi, Cy, Ho, Wo, Cx, R, S, stride, pad, act, slope, s);
-    case T128x64:
-      return launch_tconv<128, 64, 64, 32>(in, wp, bias, out, N, Hi, Wi, Cy, Ho, Wo, Cx, R, S, stride, pad, act, slope, s);
-    case T256x32:
-      return launch_tconv<256, 32, 64, 32>(in, wp, bias, out, N, Hi, Wi, Cy, Ho, Wo, Cx, R, S, stride, pad, act, slope, s);
-    default:
-      return launch_tconv<64, 64, 32, 32>(in, wp, bias, out, N, Hi, Wi, Cy, Ho, Wo, Cx, R, S, stride, pad, act, slope, s);
-  }
+  const int Hc = (Ho + stride - 1) / stride, Wc = (Wo + stride - 1) / stride;
+  const int Mmax = N * Hc * Wc;
+  if (Cx == 4)  // image-channel data gradients: VALU path (skinny.hip)
+    return skinny_out_launch(1, in, wp, bias, addend, out, N, Hi, Wi, Cy, Ho, Wo, R, S, stride, pad,
+                             refl, act, slope, s);
+#define VST_TCONV_ST(BM_, BN_, WM_, WN_, ST_)                                                      \
+  hipLaunchKernelGGL((conv_tconv_k<BM_, BN_, WM_, WN_, ST_>),                                       \
+                     dim3(ceil_div(Mmax, BM_), ceil_div(Cx, BN_), stride * stride),                  \
+                     dim3(Tile<BM_, BN_, WM_, WN_>::NT), 0, s, in, wp, bias, addend, out, Hi, Wi, Cy, \
+                     Ho, Wo, Cx, R, S, stride, pad, refl, act, slope, N)
+#define VST_TCONV(BM_, BN_, WM_, WN_)                     \
+  if (stride == 1) VST_TCONV_ST(BM_, BN_, WM_, WN_, 1);     \
+  else if (stride == 2) VST_TCONV_ST(BM_, BN_, WM_, WN_, 2); \
+  else VST_TCONV_ST(BM_, BN_, WM_, WN_, 0);
+  VST_DISPATCH_TILE(pick_tile((long)Mmax * stride * stride, Cx, 1), VST_TCONV)
+#undef VST_TCONV
+#undef VST_TCONV_ST
+  return check_launch("conv2d_tfwd");
 }
 
 extern "C" size_t vst_conv2d_wgrad_ws_bytes(int N, int H, int W, int Cx, int Ho, int Wo, int Cyp,
@@ -683,10 +742,10 @@ extern "C" size_t vst_conv2d_wgrad_ws_bytes(int N, int H, int W, int Cx, int Ho,
   (void)H;
   (void)W;
   const WgradPlan p = plan_wgrad(N, Ho, Wo, Cx, Cyp, R, S);
-  return (size_t)p.nsplit * p.Mtot * Cyp * sizeof(float);
+  return (size_t)p.nsplit * p.Mw * Cyp * sizeof(float);
 }
 
-extern "C" int vst_conv2d_wgrad(const float* x, const float* dy, float* dw, float* db, float* ws,
+extern "C" int vst_conv2d_wgrad(const float* x, const float* dy, float* dw, float* ws,
                                 size_t ws_bytes, int N, int H, int W, int Cx, int Ho, int Wo,
                                 int Cyp, int R, int S, int stride, int pad, int pad_mode, int Co,
                                 int Ci, long so, long si, int accumulate, void* stream) {
@@ -695,26 +754,32 @@ extern "C" int vst_conv2d_wgrad(const float* x, const float* dy, float* dw, floa
   VST_REQUIRE(Co <= Cyp && Ci <= Cx, "conv2d_wgrad: logical channels exceed strides");
   VST_REQUIRE(pad_mode == VST_PAD_ZERO || (pad < H && pad < W), "conv2d_wgrad: reflect pad >= size");
   const WgradPlan p = plan_wgrad(N, Ho, Wo, Cx, Cyp, R, S);
-  VST_REQUIRE(ws_bytes >= (size_t)p.nsplit * p.Mtot * Cyp * sizeof(float),
+  VST_REQUIRE(ws_bytes >= (size_t)p.nsplit * p.Mw * Cyp * sizeof(float),
               "conv2d_wgrad: workspace too small (%zu bytes)", ws_bytes);
   hipStream_t s = (hipStream_t)stream;
   const int P = N * Ho * Wo;
   const int refl = pad_mode == VST_PAD_REFLECT;
-  if (Cyp <= 32) {
-    dim3 grid(ceil_div(p.Mtot, 128), ceil_div(Cyp, 32), p.nsplit);
-    hipLaunchKernelGGL((conv_wgrad_k<128, 32, 32, 32>), grid, dim3(NT), 0, s, x, dy, ws, H, W, Cx,
-                       Ho, Wo, Cyp, S, stride, pad, refl, p.Mw, p.Mtot, P, p.chunk);
+#define VST_WG(BM_, BN_, WM_, WN_)                                                                 \
+  hipLaunchKernelGGL((conv_wgrad_k<BM_, BN_, WM_, WN_>),                                            \
+                     dim3(ceil_div(p.Mw, BM_), ceil_div(Cyp, BN_), p.nsplit),                        \
+                     dim3(Tile<BM_, BN_, WM_, WN_>::NT), 0, s, x, dy, ws, H, W, Cx, Ho, Wo, Cyp, S,  \
+                     stride, pad, refl, p.Mw, P, p.chunk)
+  if (Cyp == 4) {
+    int rc0 = skinny_wgrad_launch(x, dy, ws, H, W, Cx, Ho, Wo, S, stride, pad, refl, p.Mw, P, p.chunk,
+                                  p.nsplit, s);
+    if (rc0) return rc0;
   } else {
-    dim3 grid(ceil_div(p.Mtot, 128), ceil_div(Cyp, 64), p.nsplit);
-    hipLaunchKernelGGL((conv_wgrad_k<128, 64, 64, 32>), grid, dim3(NT), 0, s, x, dy, ws, H, W, Cx,
-                       Ho, Wo, Cyp, S, stride, pad, refl, p.Mw, p.Mtot, P, p.chunk);
+    VST_DISPATCH_TILE(p.tile, VST_WG)
   }
+#undef VST_WG
   int rc = check_launch("conv2d_wgrad");
   if (rc) return rc;
-  const long total = (long)Co * Ci * R * S;
-  const long threads = total > Co ? total : Co;
-  hipLaunchKernelGGL(wgrad_reduce_k, dim3(ceil_div(threads, 256)), dim3(256), 0, s, ws, dw, db,
-                     p.nsplit, p.Mtot, p.Mw, Cx, Cyp, R * S, Co, Ci, so, si, accumulate);
+  if (p.nsplit > 1) {
+    const long n4 = (long)p.Mw * Cyp / 4;
+    hipLaunchKernelGGL(wgrad_sum_k, dim3(ceil_div(n4, 256)), dim3(256), 0, s, ws, n4, p.nsplit);
+  }
+  hipLaunchKernelGGL(wgrad_store_k, dim3(ceil_div(p.Mw, 64), ceil_div(Cyp, 64)), dim3(256), 0, s, ws,
+                     dw, p.Mw, Cx, Cyp, R * S, Co, Ci, so, si, accumulate);
   return check_launch("conv2d_wgrad_reduce");
 }
 

@@ -2,63 +2,151 @@
 // Replaces nn.InstanceNorm2d (reference networks.py:30, affine=False, track_running_stats=False,
 // eps=1e-5, biased variance) followed by nn.ReLU(True) (G) / nn.LeakyReLU(0.2, True) (D).
 //
-// Statistics are reduced per (n, c) over H*W in fp64 (sum, sum of squares) so the result does not
-// depend on the fp32 summation order: each block owns 64 channels of one image and a slice of the
-// pixels (split over blockIdx.z for parallelism), writes its partials to the workspace, and a
-// finalize kernel folds the slices in a fixed order (deterministic).
+// Reductions are per (n, c) over H*W.  A block owns a slice of one image's pixels and ALL its
+// channels: lanes run along the channel axis 4 at a time (float4, coalesced rows of the NHWC
+// tensor), pixel groups stride the slice, partial sums are kept in fp64 (so the result does not
+// depend on the fp32 summation order), folded through LDS, and written per slice; a finalize
+// kernel folds the slices in a fixed order (deterministic).  The slice size adapts so every layer
+// launches ~512 blocks (64x64x256 res tensors and 256x256x64 outer tensors alike).
 #include "common.h"
 
 namespace vst {
 
-constexpr int IN_SPLIT_PIX = 512;  // pixels per block slice
+constexpr int NRED = 256;
 
-static inline int in_splits(int HW) { return ceil_div(HW, IN_SPLIT_PIX); }
+struct RedGeom {
+  int LP, PG, SP, nsplit;  // lanes per pixel (C/4), pixel groups, pixels per slice, slices
+};
 
-// partial[(n*nsplit + z)*C + c] = {sum, sumsq}  (as double2)
-__global__ void in_partial_k(const float* __restrict__ x, double2* __restrict__ part, int HW, int C,
-                             int nsplit) {
-  __shared__ double2 red[4][64];
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int w = threadIdx.x >> 6;
-  const int n = blockIdx.y, z = blockIdx.z;
-  const int p0 = z * IN_SPLIT_PIX, p1 = min(HW, p0 + IN_SPLIT_PIX);
-  double s = 0.0, q = 0.0;
-  if (c < C) {
-    const float* base = x + (long)n * HW * C + c;
-    for (int p = p0 + w; p < p1; p += 4) {
-      const double v = base[(long)p * C];
-      s += v;
-      q += v * v;
+static bool red_geom(int N, int HW, int C, RedGeom& g) {
+  if (C % 4) return false;
+  g.LP = C / 4;
+  if (g.LP > NRED || NRED % g.LP) return false;
+  g.PG = NRED / g.LP;
+  long sp = ((long)N * HW + 511) / 512;
+  if (sp < 2L * g.PG) sp = 2L * g.PG;
+  sp = (sp + g.PG - 1) / g.PG * g.PG;
+  if (sp > HW) sp = HW;
+  g.SP = (int)sp;
+  g.nsplit = ceil_div(HW, g.SP);
+  return true;
+}
+
+// MODE 0: stats partials {sum x, sum x^2}; MODE 1: backward partials {sum g, sum g*xhat, sum xhat}
+template <int MODE>
+__global__ __launch_bounds__(NRED) void in_partial_k(const float* __restrict__ x,
+                                                     const float* __restrict__ gy,
+                                                     const float* __restrict__ stats,
+                                                     double* __restrict__ part, int HW, int C,
+                                                     int LP, int PG, int SP, int nsplit, int act,
+                                                     float slope) {
+  constexpr int NV = MODE == 0 ? 2 : 3;
+  __shared__ double red[NV * 4][NRED];
+  const int t = threadIdx.x, c4 = t % LP, pg = t / LP;
+  const int n = blockIdx.y, z = blockIdx.x;
+  const int p0 = z * SP, p1 = min(HW, p0 + SP);
+  double acc[NV][4];
+#pragma unroll
+  for (int v = 0; v < NV; ++v)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[v][j] = 0.0;
+  float mean[4] = {0, 0, 0, 0}, rstd[4] = {0, 0, 0, 0};
+  if (MODE == 1) {
+    const float4 s0 = reinterpret_cast<const float4*>(stats)[((long)n * C + 4 * c4) / 2];
+    const float4 s1 = reinterpret_cast<const float4*>(stats)[((long)n * C + 4 * c4) / 2 + 1];
+    mean[0] = s0.x; rstd[0] = s0.y; mean[1] = s0.z; rstd[1] = s0.w;
+    mean[2] = s1.x; rstd[2] = s1.y; mean[3] = s1.z; rstd[3] = s1.w;
+  }
+  const float4* xb = reinterpret_cast<const float4*>(x) + (long)n * HW * LP + c4;
+  const float4* gb = reinterpret_cast<const float4*>(gy) + (long)n * HW * LP + c4;
+  for (int p = p0 + pg; p < p1; p += PG) {
+    const float4 v = xb[(long)p * LP];
+    const float xv[4] = {v.x, v.y, v.z, v.w};
+    if (MODE == 0) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc[0][j] += xv[j];
+        acc[1][j] += (double)xv[j] * xv[j];
+      }
+    } else {
+      const float4 gv = gb[(long)p * LP];
+      const float gg[4] = {gv.x, gv.y, gv.z, gv.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float xh = (xv[j] - mean[j]) * rstd[j];
+        float d = 1.f;
+        if (act == VST_ACT_RELU) d = xh > 0.f ? 1.f : 0.f;
+        else if (act == VST_ACT_LRELU) d = xh > 0.f ? 1.f : slope;
+        const float g = gg[j] * d;
+        acc[0][j] += g;
+        acc[1][j] += (double)g * xh;
+        acc[2][j] += xh;
+      }
     }
   }
-  red[w][threadIdx.x & 63] = make_double2(s, q);
+#pragma unroll
+  for (int v = 0; v < NV; ++v)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) red[v * 4 + j][t] = acc[v][j];
   __syncthreads();
-  if (w == 0 && c < C) {
-    double2 a = red[0][threadIdx.x];
-    for (int i = 1; i < 4; ++i) {
-      a.x += red[i][threadIdx.x].x;
-      a.y += red[i][threadIdx.x].y;
-    }
-    part[((long)n * nsplit + z) * C + c] = a;
+  if (pg == 0) {
+    double out[NV][4];
+#pragma unroll
+    for (int v = 0; v < NV; ++v)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        double s = 0.0;
+        for (int q = 0; q < PG; ++q) s += red[v * 4 + j][q * LP + c4];
+        out[v][j] = s;
+      }
+    double* dst = part + (((long)n * nsplit + z) * C + 4 * c4) * NV;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int v = 0; v < NV; ++v) dst[j * NV + v] = out[v][j];
   }
 }
 
-__global__ void in_finalize_k(const double2* __restrict__ part, float* __restrict__ stats, int N,
+__global__ void in_finalize_k(const double* __restrict__ part, float* __restrict__ stats, int N,
                               int HW, int C, int nsplit, float eps) {
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= N * C) return;
   const int n = idx / C, c = idx - n * C;
   double s = 0.0, q = 0.0;
   for (int z = 0; z < nsplit; ++z) {
-    const double2 a = part[((long)n * nsplit + z) * C + c];
-    s += a.x;
-    q += a.y;
+    const double* a = part + (((long)n * nsplit + z) * C + c) * 2;
+    s += a[0];
+    q += a[1];
   }
   const double mean = s / HW;
   double var = q / HW - mean * mean;
   if (var < 0) var = 0;
   stats[2 * idx] = (float)mean;
   stats[2 * idx + 1] = (float)(1.0 / sqrt(var + (double)eps));
+}
+
+// coef[(n*C+c)] = {mean(g), mean(g*xhat)}; db[c] (+)= sum_n sum_p dx = sum_n rstd*(-mean(g xhat)*sum xhat)
+// (the exact per-channel sum of the IN input gradient: the conv-bias gradient of the layer).
+__global__ void in_bwd_finalize_k(const double* __restrict__ part, const float* __restrict__ stats,
+                                  float2* __restrict__ coef, float* __restrict__ db, int N, int HW,
+                                  int C, int nsplit, int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double dbs = 0.0;
+  for (int n = 0; n < N; ++n) {
+    double sg = 0.0, sgx = 0.0, sx = 0.0;
+    for (int z = 0; z < nsplit; ++z) {
+      const double* a = part + (((long)n * nsplit + z) * C + c) * 3;
+      sg += a[0];
+      sgx += a[1];
+      sx += a[2];
+    }
+    const double mg = sg / HW, mgx = sgx / HW;
+    coef[n * C + c] = make_float2((float)mg, (float)mgx);
+    const double rstd = stats[2 * (n * C + c) + 1];
+    dbs += rstd * ((sg - HW * mg) - mgx * sx);
+  }
+  if (db) db[c] = accumulate ? db[c] + (float)dbs : (float)dbs;
 }
 
 __global__ void in_apply_k(const float4* __restrict__ x, const float* __restrict__ stats,
@@ -76,80 +164,39 @@ __global__ void in_apply_k(const float4* __restrict__ x, const float* __restrict
   v.y = apply_act((v.y - s0.z) * s0.w, act, slope);
   v.z = apply_act((v.z - s1.x) * s1.y, act, slope);
   v.w = apply_act((v.w - s1.z) * s1.w, act, slope);
-  if (res) {
-    const float4 r = res[i];
-    v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w;
-  }
+  if (res) add_f4(v, res[i]);
   y[i] = v;
 }
 
-__device__ __forceinline__ float act_grad_pre(float xh, int act, float slope) {
-  if (act == VST_ACT_RELU) return xh > 0.f ? 1.f : 0.f;
-  if (act == VST_ACT_LRELU) return xh > 0.f ? 1.f : slope;
-  return 1.f;
+__device__ __forceinline__ float in_bwd1(float gy, float x, float mean, float rstd, float2 k, int act,
+                                         float slope) {
+  const float xh = (x - mean) * rstd;
+  float d = 1.f;
+  if (act == VST_ACT_RELU) d = xh > 0.f ? 1.f : 0.f;
+  else if (act == VST_ACT_LRELU) d = xh > 0.f ? 1.f : slope;
+  return rstd * (gy * d - k.x - xh * k.y);
 }
 
-// partials of sum(g) and sum(g * xhat), g = gy * act'(xhat)
-__global__ void in_bwd_partial_k(const float* __restrict__ gy, const float* __restrict__ x,
-                                 const float* __restrict__ stats, double2* __restrict__ part,
-                                 int HW, int C, int nsplit, int act, float slope) {
-  __shared__ double2 red[4][64];
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int w = threadIdx.x >> 6;
-  const int n = blockIdx.y, z = blockIdx.z;
-  const int p0 = z * IN_SPLIT_PIX, p1 = min(HW, p0 + IN_SPLIT_PIX);
-  double s = 0.0, q = 0.0;
-  if (c < C) {
-    const float mean = stats[2 * (n * C + c)], rstd = stats[2 * (n * C + c) + 1];
-    const long off = (long)n * HW * C + c;
-    for (int p = p0 + w; p < p1; p += 4) {
-      const float xh = (x[off + (long)p * C] - mean) * rstd;
-      const float g = gy[off + (long)p * C] * act_grad_pre(xh, act, slope);
-      s += g;
-      q += (double)g * xh;
-    }
-  }
-  red[w][threadIdx.x & 63] = make_double2(s, q);
-  __syncthreads();
-  if (w == 0 && c < C) {
-    double2 a = red[0][threadIdx.x];
-    for (int i = 1; i < 4; ++i) {
-      a.x += red[i][threadIdx.x].x;
-      a.y += red[i][threadIdx.x].y;
-    }
-    part[((long)n * nsplit + z) * C + c] = a;
-  }
-}
-
-// coef[(n*C+c)] = {mean(g), mean(g*xhat)} folded into the partial buffer slot 0 (as float2)
-__global__ void in_bwd_finalize_k(const double2* __restrict__ part, float2* __restrict__ coef,
-                                  int N, int HW, int C, int nsplit) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= N * C) return;
-  const int n = idx / C, c = idx - n * C;
-  double s = 0.0, q = 0.0;
-  for (int z = 0; z < nsplit; ++z) {
-    const double2 a = part[((long)n * nsplit + z) * C + c];
-    s += a.x;
-    q += a.y;
-  }
-  coef[idx] = make_float2((float)(s / HW), (float)(q / HW));
-}
-
-__global__ void in_bwd_apply_k(const float* __restrict__ gy, const float* __restrict__ x,
+__global__ void in_bwd_apply_k(const float4* __restrict__ gy, const float4* __restrict__ x,
                                const float* __restrict__ stats, const float2* __restrict__ coef,
-                               float* __restrict__ dx, long total, int HW, int C, int act,
+                               float4* __restrict__ dx, long total4, int HW, int C4, int act,
                                float slope) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= total) return;
-  const int c = i % C;
-  const int n = (i / C) / HW;
-  const int nc = n * C + c;
-  const float mean = stats[2 * nc], rstd = stats[2 * nc + 1];
-  const float xh = (x[i] - mean) * rstd;
-  const float g = gy[i] * act_grad_pre(xh, act, slope);
-  const float2 k = coef[nc];
-  dx[i] = rstd * (g - k.x - xh * k.y);
+  if (i >= total4) return;
+  const int c4 = i % C4;
+  const int n = (i / C4) / HW;
+  const long nc4 = (long)n * C4 + c4;
+  const float4* st = reinterpret_cast<const float4*>(stats) + nc4 * 2;
+  const float4 s0 = st[0], s1 = st[1];
+  const float4 k01 = reinterpret_cast<const float4*>(coef)[nc4 * 2];
+  const float4 k23 = reinterpret_cast<const float4*>(coef)[nc4 * 2 + 1];
+  const float4 g = gy[i], v = x[i];
+  float4 o;
+  o.x = in_bwd1(g.x, v.x, s0.x, s0.y, make_float2(k01.x, k01.y), act, slope);
+  o.y = in_bwd1(g.y, v.y, s0.z, s0.w, make_float2(k01.z, k01.w), act, slope);
+  o.z = in_bwd1(g.z, v.z, s1.x, s1.y, make_float2(k23.x, k23.y), act, slope);
+  o.w = in_bwd1(g.w, v.w, s1.z, s1.w, make_float2(k23.z, k23.w), act, slope);
+  dx[i] = o;
 }
 
 __global__ void act_bwd_k(const float* __restrict__ gy, const float* __restrict__ y,
@@ -158,25 +205,61 @@ __global__ void act_bwd_k(const float* __restrict__ gy, const float* __restrict_
   if (i < n) dx[i] = gy[i] * act_grad_from_out(y[i], act, slope);
 }
 
+// per-channel sum (bias gradient of a layer without a following IN), same geometry as in_partial
+__global__ __launch_bounds__(NRED) void chsum_partial_k(const float* __restrict__ x,
+                                                        double* __restrict__ part, long NHW, int LP,
+                                                        int PG, int SP) {
+  __shared__ double red[4][NRED];
+  const int t = threadIdx.x, c4 = t % LP, pg = t / LP;
+  const long p0 = (long)blockIdx.x * SP, p1 = min(NHW, p0 + SP);
+  double acc[4] = {0, 0, 0, 0};
+  const float4* xb = reinterpret_cast<const float4*>(x) + c4;
+  for (long p = p0 + pg; p < p1; p += PG) {
+    const float4 v = xb[p * LP];
+    acc[0] += v.x; acc[1] += v.y; acc[2] += v.z; acc[3] += v.w;
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) red[j][t] = acc[j];
+  __syncthreads();
+  if (pg == 0)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      double s = 0.0;
+      for (int q = 0; q < PG; ++q) s += red[j][q * LP + c4];
+      part[(long)blockIdx.x * LP * 4 + 4 * c4 + j] = s;
+    }
+}
+
+__global__ void chsum_final_k(const double* __restrict__ part, float* __restrict__ db, int nsplit,
+                              int Cs, int Cl, int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= Cl) return;
+  double s = 0.0;
+  for (int z = 0; z < nsplit; ++z) s += part[(long)z * Cs + c];
+  db[c] = accumulate ? db[c] + (float)s : (float)s;
+}
+
 }  // namespace vst
 
 using namespace vst;
 
 extern "C" size_t vst_instnorm_ws_bytes(int N, int HW, int C) {
-  const size_t part = (size_t)N * in_splits(HW) * C * sizeof(double2);
-  const size_t coef = (size_t)N * C * sizeof(float2);
-  return part + coef + 256;
+  RedGeom g;
+  if (!red_geom(N, HW, C, g)) return 0;
+  return (size_t)N * g.nsplit * C * 3 * sizeof(double) + (size_t)N * C * sizeof(float2) + 256;
 }
 
 extern "C" int vst_instnorm_stats(const float* x, float* stats, float* ws, int N, int HW, int C,
                                   float eps, void* stream) {
-  VST_REQUIRE(x && stats && ws && N > 0 && HW > 0 && C > 0, "instnorm_stats: bad args");
+  RedGeom g;
+  VST_REQUIRE(x && stats && ws && N > 0 && HW > 0 && red_geom(N, HW, C, g),
+              "instnorm_stats: bad args (C must be 4*2^k <= 1024)");
   hipStream_t s = (hipStream_t)stream;
-  const int ns = in_splits(HW);
-  double2* part = reinterpret_cast<double2*>(ws);
-  hipLaunchKernelGGL(in_partial_k, dim3(ceil_div(C, 64), N, ns), dim3(256), 0, s, x, part, HW, C, ns);
+  double* part = reinterpret_cast<double*>(ws);
+  hipLaunchKernelGGL(in_partial_k<0>, dim3(g.nsplit, N), dim3(NRED), 0, s, x, (const float*)nullptr,
+                     (const float*)nullptr, part, HW, C, g.LP, g.PG, g.SP, g.nsplit, 0, 0.f);
   hipLaunchKernelGGL(in_finalize_k, dim3(ceil_div((long)N * C, 256)), dim3(256), 0, s, part, stats, N,
-                     HW, C, ns, eps);
+                     HW, C, g.nsplit, eps);
   return check_launch("instnorm_stats");
 }
 
@@ -192,21 +275,22 @@ extern "C" int vst_instnorm_act_fwd(const float* x, const float* stats, const fl
 }
 
 extern "C" int vst_instnorm_act_bwd(const float* gy, const float* x, const float* stats, float* dx,
-                                    float* ws, int N, int HW, int C, int act, float slope,
-                                    void* stream) {
-  VST_REQUIRE(gy && x && stats && dx && ws, "instnorm_act_bwd: bad args");
+                                    float* db, float* ws, int N, int HW, int C, int act, float slope,
+                                    int accumulate_db, void* stream) {
+  RedGeom g;
+  VST_REQUIRE(gy && x && stats && dx && ws && red_geom(N, HW, C, g), "instnorm_act_bwd: bad args");
   hipStream_t s = (hipStream_t)stream;
-  const int ns = in_splits(HW);
-  double2* part = reinterpret_cast<double2*>(ws);
+  double* part = reinterpret_cast<double*>(ws);
   float2* coef = reinterpret_cast<float2*>(reinterpret_cast<char*>(ws) +
-                                           (size_t)N * ns * C * sizeof(double2));
-  hipLaunchKernelGGL(in_bwd_partial_k, dim3(ceil_div(C, 64), N, ns), dim3(256), 0, s, gy, x, stats,
-                     part, HW, C, ns, act, slope);
-  hipLaunchKernelGGL(in_bwd_finalize_k, dim3(ceil_div((long)N * C, 256)), dim3(256), 0, s, part,
-                     coef, N, HW, C, ns);
-  const long total = (long)N * HW * C;
-  hipLaunchKernelGGL(in_bwd_apply_k, dim3(ceil_div(total, 256)), dim3(256), 0, s, gy, x, stats, coef,
-                     dx, total, HW, C, act, slope);
+                                           (size_t)N * g.nsplit * C * 3 * sizeof(double));
+  hipLaunchKernelGGL(in_partial_k<1>, dim3(g.nsplit, N), dim3(NRED), 0, s, x, gy, stats, part, HW, C,
+                     g.LP, g.PG, g.SP, g.nsplit, act, slope);
+  hipLaunchKernelGGL(in_bwd_finalize_k, dim3(ceil_div(C, 256)), dim3(256), 0, s, part, stats, coef, db,
+                     N, HW, C, g.nsplit, accumulate_db);
+  const long total4 = (long)N * HW * C / 4;
+  hipLaunchKernelGGL(in_bwd_apply_k, dim3(ceil_div(total4, 256)), dim3(256), 0, s,
+                     reinterpret_cast<const float4*>(gy), reinterpret_cast<const float4*>(x), stats,
+                     coef, reinterpret_cast<float4*>(dx), total4, HW, C / 4, act, slope);
   return check_launch("instnorm_act_bwd");
 }
 
@@ -218,47 +302,21 @@ extern "C" int vst_act_bwd(const float* gy, const float* y, float* dx, long n, i
   return check_launch("act_bwd");
 }
 
-// ------------------------------------------------------------------ per-channel sum (bias grad)
-namespace vst {
-constexpr int CS_SPLIT_PIX = 1024;
-
-__global__ void chsum_partial_k(const float* __restrict__ x, float* __restrict__ part, long NHW,
-                                int Cs, int Cl) {
-  __shared__ float red[4][64];
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int w = threadIdx.x >> 6;
-  const long p0 = (long)blockIdx.y * CS_SPLIT_PIX;
-  const long p1 = min(NHW, p0 + CS_SPLIT_PIX);
-  float s = 0.f;
-  if (c < Cl)
-    for (long p = p0 + w; p < p1; p += 4) s += x[p * Cs + c];
-  red[w][threadIdx.x & 63] = s;
-  __syncthreads();
-  if (w == 0 && c < Cl)
-    part[(long)blockIdx.y * Cl + c] = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] +
-                                      red[3][threadIdx.x];
-}
-
-__global__ void chsum_final_k(const float* __restrict__ part, float* __restrict__ db, int nsplit,
-                              int Cl, int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= Cl) return;
-  double s = 0.0;
-  for (int z = 0; z < nsplit; ++z) s += part[(long)z * Cl + c];
-  db[c] = accumulate ? db[c] + (float)s : (float)s;
-}
-}  // namespace vst
-
-extern "C" size_t vst_channel_sum_ws_bytes(long NHW, int Cl) {
-  return (size_t)ceil_div(NHW, CS_SPLIT_PIX) * Cl * sizeof(float);
+extern "C" size_t vst_channel_sum_ws_bytes(long NHW, int Cs) {
+  RedGeom g;
+  if (!red_geom(1, (int)NHW, Cs, g)) return 0;
+  return (size_t)g.nsplit * Cs * sizeof(double);
 }
 
 extern "C" int vst_channel_sum(const float* x, float* db, float* ws, long NHW, int Cs, int Cl,
                                int accumulate, void* stream) {
-  VST_REQUIRE(x && db && ws && Cl <= Cs && NHW > 0, "channel_sum: bad args");
+  RedGeom g;
+  VST_REQUIRE(x && db && ws && Cl <= Cs && NHW > 0 && red_geom(1, (int)NHW, Cs, g),
+              "channel_sum: bad args");
   hipStream_t s = (hipStream_t)stream;
-  const int ns = ceil_div(NHW, CS_SPLIT_PIX);
-  hipLaunchKernelGGL(chsum_partial_k, dim3(ceil_div(Cl, 64), ns), dim3(256), 0, s, x, ws, NHW, Cs, Cl);
-  hipLaunchKernelGGL(chsum_final_k, dim3(ceil_div(Cl, 256)), dim3(256), 0, s, ws, db, ns, Cl, accumulate);
+  double* part = reinterpret_cast<double*>(ws);
+  hipLaunchKernelGGL(chsum_partial_k, dim3(g.nsplit), dim3(NRED), 0, s, x, part, NHW, g.LP, g.PG, g.SP);
+  hipLaunchKernelGGL(chsum_final_k, dim3(ceil_div(Cl, 256)), dim3(256), 0, s, part, db, g.nsplit, Cs, Cl,
+                     accumulate);
   return check_launch("channel_sum");
 }

@@ -377,7 +377,7 @@ class _GeneratorFn(torch.autograd.Function):
         train_w = ctx.train_w
         gout = gout.contiguous()
 
-        def wgrad(mod, inp, dy, R, st, pad, mode, db=True):
+        def wgrad(mod, inp, dy, R, st, pad, mode, db=False):
             if not train_w:
                 return
             w = mod.weight
@@ -385,31 +385,36 @@ class _GeneratorFn(torch.autograd.Function):
             ops.conv2d_wgrad(inp, dy, w.grad, mod.bias.grad if (db and mod.bias is not None) else None,
                              R, R, st, pad, mode, co, ci, ci * R * R, R * R, accumulate=True)
 
+        def in_bwd(g, y, s, act, mod):
+            # IN(+act) backward; the bias gradient of the conv feeding the IN comes out of the
+            # same reduction (sum of dy per channel)
+            db = mod.bias.grad if (train_w and mod.bias is not None) else None
+            return ops.instnorm_act_bwd(g, y, s, act, db=db)
+
         def dgrad_reflect(dy, key, cin_p, R, p, H, W, addend=None):
             _, ck, _ = P[key]
-            dxp = ops.conv2d_tfwd(dy, ck, None, H + 2 * p, W + 2 * p, cin_p, R, R, 1, 0)
-            return ops.reflect_fold(dxp, p, addend)
+            return ops.conv2d_tfwd(dy, ck, None, H, W, cin_p, R, R, 1, p, pad_mode="reflect",
+                                   addend=addend)
 
         def dgrad_s2(dy, key, cin_p, H, W):
             _, ck, _ = P[key]
             return ops.conv2d_tfwd(dy, ck, None, H, W, cin_p, 3, 3, 2, 1)
 
-        # final conv + tanh
+        # final conv + tanh (no IN after it: bias grad is a channel sum)
         a, out = sv["f"]
         g = ops.act_bwd(gout, out, "tanh")
-        wgrad(f, a, g, 7, 1, 3, "reflect")
+        wgrad(f, a, g, 7, 1, 3, "reflect", db=True)
         ga = dgrad_reflect(g, "f", a.shape[-1], 7, 3, a.shape[1], a.shape[2])
         # up-sampling convT layers
         for i in (1, 0):
             a_in, y, s, an = sv[f"u{i}"]
-            dy = ops.instnorm_act_bwd(ga, y, s, "relu")
             m = u[i]
+            dy = in_bwd(ga, y, s, "relu", m)
             if train_w:
                 # Wt[ci][co] grad = wgrad of the equivalent conv x_T = conv(dy_T, .) (see header)
                 ci_t, co_t = m.weight.shape[0], m.weight.shape[1]
                 ops.conv2d_wgrad(dy, a_in, m.weight.grad, None, 3, 3, 2, 1, "zero", ci_t, co_t,
                                  co_t * 9, 9, accumulate=True)
-                ops.channel_sum(dy, m.bias.grad, co_t)
             kc, _, _ = P[f"u{i}"]
             ga = ops.conv2d_fwd(dy, kc, None, a_in.shape[-1], 3, 3, 2, 1, "zero")
         # residual blocks
@@ -417,10 +422,10 @@ class _GeneratorFn(torch.autograd.Function):
         for i in reversed(range(len(blocks))):
             h, t, s1, uu, v, s2 = sv[f"b{i}"]
             blk = blocks[i].conv_block
-            dv = ops.instnorm_act_bwd(gh, v, s2, "none")
+            dv = in_bwd(gh, v, s2, "none", blk[5])
             wgrad(blk[5], uu, dv, 3, 1, 1, "reflect")
             du = dgrad_reflect(dv, f"b{i}b", uu.shape[-1], 3, 1, uu.shape[1], uu.shape[2])
-            dt = ops.instnorm_act_bwd(du, t, s1, "relu")
+            dt = in_bwd(du, t, s1, "relu", blk[1])
             wgrad(blk[1], h, dt, 3, 1, 1, "reflect")
             gh = dgrad_reflect(dt, f"b{i}a", h.shape[-1], 3, 1, h.shape[1], h.shape[2], addend=gh)
         ga = gh
@@ -428,13 +433,13 @@ class _GeneratorFn(torch.autograd.Function):
         for key, mod, prev in (("d1", d[1], "d0"), ("d0", d[0], "c0")):
             y, s, _ = sv[key]
             a_in = sv[prev][2]
-            dy = ops.instnorm_act_bwd(ga, y, s, "relu")
+            dy = in_bwd(ga, y, s, "relu", mod)
             wgrad(mod, a_in, dy, 3, 2, 1, "zero")
             ga = dgrad_s2(dy, key, a_in.shape[-1], a_in.shape[1], a_in.shape[2])
         # first conv
         x = sv["x"]
         y, s, _ = sv["c0"]
-        dy = ops.instnorm_act_bwd(ga, y, s, "relu")
+        dy = in_bwd(ga, y, s, "relu", c0)
         wgrad(c0, x, dy, 7, 1, 3, "reflect")
         gx = None
         if ctx.needs_input_grad[0]:
@@ -522,14 +527,16 @@ class _DiscriminatorFn(torch.autograd.Function):
             m = convs[i]
             cout, st, has_in = net.spec[i]
             if has_in:
-                dy = ops.instnorm_act_bwd(g, y, s, "lrelu", SLOPE)
+                db = m.bias.grad if (ctx.train_w and m.bias is not None) else None
+                dy = ops.instnorm_act_bwd(g, y, s, "lrelu", SLOPE, db=db)
             elif i != L - 1:
                 dy = ops.act_bwd(g, an, "lrelu", SLOPE)
             else:
                 dy = g
             if ctx.train_w:
                 co, ci = m.weight.shape[0], m.weight.shape[1]
-                ops.conv2d_wgrad(a_in, dy, m.weight.grad, m.bias.grad if m.bias is not None else None,
+                ops.conv2d_wgrad(a_in, dy, m.weight.grad,
+                                 m.bias.grad if (m.bias is not None and not has_in) else None,
                                  4, 4, st, 1, "zero", co, ci, ci * 16, 16, accumulate=True)
             if i > 0 or ctx.needs_input_grad[0]:
                 _, ck, _ = P[i]

@@ -88,24 +88,34 @@ def conv2d_fwd(x, wp, bias, cop, R, S, stride, pad, pad_mode="zero", act="none",
     return y
 
 
-def conv2d_tfwd(x, wp, bias, Ho, Wo, cx, R, S, stride, pad, act="none", slope=0.0):
-    _dev_check(x, wp, bias)
+def conv2d_tfwd(x, wp, bias, Ho, Wo, cx, R, S, stride, pad, act="none", slope=0.0,
+                pad_mode="zero", addend=None):
+    """Transposed conv / data gradient (vst_conv2d_tfwd).  pad_mode='reflect' (stride 1) is the
+    exact gradient of ReflectionPad2d(pad)+conv; addend is added in the epilogue."""
+    _dev_check(x, wp, bias, addend)
     N, Hi, Wi, Cy = x.shape
     y = torch.empty((N, Ho, Wo, cx), device=x.device)
-    _call("vst_conv2d_tfwd", _p(x), _p(wp), _p(bias), _p(y), N, Hi, Wi, Cy, Ho, Wo, cx, R, S,
-          stride, pad, ACT[act], float(slope), _stream())
+    _call("vst_conv2d_tfwd", _p(x), _p(wp), _p(bias), _p(addend), _p(y), N, Hi, Wi, Cy, Ho, Wo, cx,
+          R, S, stride, pad, PAD[pad_mode], ACT[act], float(slope), _stream())
     return y
 
 
 def conv2d_wgrad(x, dy, dw, db, R, S, stride, pad, pad_mode, co, ci, so, si, accumulate=True):
-    """dw (+)= weight gradient written with strides (so, si) — see vst_conv2d_wgrad."""
+    """dw (+)= weight gradient written with strides (so, si) — see vst_conv2d_wgrad; db (if not
+    None) (+)= per-channel sum of dy (the bias gradient)."""
     _dev_check(x, dy)
     N, H, W, Cx = x.shape
     _, Ho, Wo, Cyp = dy.shape
     nbytes = lib().vst_conv2d_wgrad_ws_bytes(N, H, W, Cx, Ho, Wo, Cyp, R, S)
     ws = torch.empty((nbytes + 3) // 4, device=x.device)
-    _call("vst_conv2d_wgrad", _p(x), _p(dy), _p(dw), _p(db), _p(ws), nbytes, N, H, W, Cx, Ho, Wo,
+    _call("vst_conv2d_wgrad", _p(x), _p(dy), _p(dw), _p(ws), nbytes, N, H, W, Cx, Ho, Wo,
           Cyp, R, S, stride, pad, PAD[pad_mode], co, ci, so, si, 1 if accumulate else 0, _stream())
+    if db is not None:
+        channel_sum(dy, db, co, accumulate)
+
+
+def debug_set_tiles(fprop=-1, tconv=-1, wgrad=-1):
+    lib().vst_debug_set_tiles(int(fprop), int(tconv), int(wgrad))
 
 
 def channel_sum(x, db, cl, accumulate=True):
@@ -113,7 +123,7 @@ def channel_sum(x, db, cl, accumulate=True):
     _dev_check(x)
     cs = x.shape[-1]
     nhw = x.numel() // cs
-    nbytes = lib().vst_channel_sum_ws_bytes(nhw, cl)
+    nbytes = lib().vst_channel_sum_ws_bytes(nhw, cs)
     ws = torch.empty((nbytes + 3) // 4, device=x.device)
     _call("vst_channel_sum", _p(x), _p(db), _p(ws), nhw, cs, cl, 1 if accumulate else 0, _stream())
 
@@ -151,13 +161,14 @@ def instnorm_act_fwd(y, stats, act="relu", slope=0.0, residual=None):
     return a
 
 
-def instnorm_act_bwd(ga, y, stats, act="relu", slope=0.0):
+def instnorm_act_bwd(ga, y, stats, act="relu", slope=0.0, db=None, accumulate_db=True):
+    """dy = backward of act(IN(y)); db (if given) (+)= sum of dy per channel (conv-bias grad)."""
     _dev_check(ga, y, stats)
     N, H, W, C = y.shape
     dy = torch.empty_like(y)
     ws = _in_ws(N, H * W, C, y.device)
-    _call("vst_instnorm_act_bwd", _p(ga), _p(y), _p(stats), _p(dy), _p(ws), N, H * W, C, ACT[act],
-          float(slope), _stream())
+    _call("vst_instnorm_act_bwd", _p(ga), _p(y), _p(stats), _p(dy), _p(db), _p(ws), N, H * W, C,
+          ACT[act], float(slope), 1 if accumulate_db else 0, _stream())
     return dy
 
 

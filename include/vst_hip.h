@@ -70,24 +70,29 @@ int vst_conv2d_fwd(const float* x, const float* wp, const float* bias, float* y,
  * in is [N][Hi][Wi][Cy]; out is [N][Ho][Wo][Cx] (Ho/Wo given: (Hi-1)*stride - 2*pad + R + output_padding).
  * For ConvTranspose2d forward pass wp = VST_PACK_CK pack of Wt seen as [Ci][Co] (i.e. O=Ci, I=Co)
  * -> rows (r,s,ci) cols co; for the dgrad of a Conv2d pass its VST_PACK_CK pack. */
-int vst_conv2d_tfwd(const float* in, const float* wp, const float* bias, float* out,
-                    int N, int Hi, int Wi, int Cy, int Ho, int Wo, int Cx, int R, int S,
-                    int stride, int pad, int act, float slope, void* stream);
-/* Weight (and bias) gradient of y = conv(x, w):  dw[co][ci][r][s] (+)= sum_pix x_gather * dy,
- * db[co] (+)= sum_pix dy (db may be NULL).  x: [N][H][W][Cx], dy: [N][Ho][Wo][Cyp].  dw is written
+/* pad_mode VST_PAD_REFLECT (stride 1 only) gives the data-gradient of a ReflectionPad2d(pad) +
+ * valid conv directly: the mirrored contributions are gathered in-kernel (no padded buffer/fold).
+ * addend (NULL or [N][Ho][Wo][Cx]) is added after bias/act (fused residual gradient). */
+int vst_conv2d_tfwd(const float* in, const float* wp, const float* bias, const float* addend,
+                    float* out, int N, int Hi, int Wi, int Cy, int Ho, int Wo, int Cx, int R,
+                    int S, int stride, int pad, int pad_mode, int act, float slope, void* stream);
+/* Weight gradient of y = conv(x, w):  dw[co][ci][r][s] (+)= sum_pix x_gather * dy (bias gradient:
+ * vst_channel_sum of dy).  x: [N][H][W][Cx], dy: [N][Ho][Wo][Cyp].  dw is written
  * with strides (so, si) for (co, ci) and r*S+s contiguous, for co < Co, ci < Ci (logical); pass
  * so = Ci*R*S, si = R*S for a Conv2d weight.  A ConvTranspose2d weight Wt[Ci][Co][R][S] is the
  * weight gradient of the equivalent conv x_T = conv(dy_T, .): call with x := grad of the convT
  * output, dy := convT input, (Co, Ci) := (Ci_T, Co_T), db := NULL (use vst_channel_sum).  accumulate != 0 adds into dw/db.  Split-K partial slabs go to
  * ws (vst_conv2d_wgrad_ws_bytes bytes) and are reduced in a fixed order (deterministic). */
 size_t vst_conv2d_wgrad_ws_bytes(int N, int H, int W, int Cx, int Ho, int Wo, int Cyp, int R, int S);
-int vst_conv2d_wgrad(const float* x, const float* dy, float* dw, float* db, float* ws,
-                     size_t ws_bytes, int N, int H, int W, int Cx, int Ho, int Wo, int Cyp, int R,
-                     int S, int stride, int pad, int pad_mode, int Co, int Ci, long so, long si,
-                     int accumulate, void* stream);
+int vst_conv2d_wgrad(const float* x, const float* dy, float* dw, float* ws, size_t ws_bytes, int N,
+                     int H, int W, int Cx, int Ho, int Wo, int Cyp, int R, int S, int stride,
+                     int pad, int pad_mode, int Co, int Ci, long so, long si, int accumulate,
+                     void* stream);
+/* Debug/benchmark only: force the GEMM tile of fprop / tconv / wgrad (-1 = automatic). */
+void vst_debug_set_tiles(int fprop, int tconv, int wgrad);
 /* db[c] (+)= sum over NHW pixels of x[p][c] for c < Cl (channel stride Cs); bias gradient of a layer
  * whose output gradient is x.  ws: vst_channel_sum_ws_bytes bytes; fixed-order (deterministic). */
-size_t vst_channel_sum_ws_bytes(long NHW, int Cl);
+size_t vst_channel_sum_ws_bytes(long NHW, int Cs);
 int vst_channel_sum(const float* x, float* db, float* ws, long NHW, int Cs, int Cl, int accumulate,
                     void* stream);
 /* Fold the gradient of a ReflectionPad2d(p): dx[n][h][w][c] = sum of dxp over padded positions
@@ -105,9 +110,12 @@ int vst_instnorm_stats(const float* x, float* stats, float* ws, int N, int HW, i
 int vst_instnorm_act_fwd(const float* x, const float* stats, const float* residual, float* y,
                          int N, int HW, int C, int act, float slope, void* stream);
 /* Backward of y = act(IN(x)):  dx = rstd * (g - mean(g) - xhat * mean(g*xhat)),
- * g = gy * act'(xhat).  ws: vst_instnorm_ws_bytes bytes. */
-int vst_instnorm_act_bwd(const float* gy, const float* x, const float* stats, float* dx, float* ws,
-                         int N, int HW, int C, int act, float slope, void* stream);
+ * g = gy * act'(xhat).  db (NULL or C floats) receives (accumulate_db: adds) sum_{n,p} dx — the
+ * gradient of a conv bias feeding this IN — from the same fp64 reduction (no extra pass).
+ * ws: vst_instnorm_ws_bytes bytes.  C must be 4*2^k <= 1024. */
+int vst_instnorm_act_bwd(const float* gy, const float* x, const float* stats, float* dx, float* db,
+                         float* ws, int N, int HW, int C, int act, float slope, int accumulate_db,
+                         void* stream);
 /* Elementwise activation backward in place-safe form: dx = gy * act'(y) given the OUTPUT y. */
 int vst_act_bwd(const float* gy, const float* y, float* dx, long n, int act, float slope, void* stream);
 

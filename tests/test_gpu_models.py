@@ -88,7 +88,9 @@ def _oracle_fp64_losses(g):
         m.optimize_parameters()
         cur = m.get_current_losses()
         out.append([cur[n] for n in names])
-    return np.array(out)
+    with torch.no_grad():
+        probe = m.G_A(torch.from_numpy(g["probe"]).double()).float().numpy()
+    return np.array(out), probe
 
 
 def test_train_step_vs_reference_golden(gb, golden):
@@ -101,7 +103,8 @@ def test_train_step_vs_reference_golden(gb, golden):
     m, data = _load_step_model(gb, g)
     names = [str(n) for n in g["loss_names"]]
     ref_all = g["losses"]
-    band = (np.abs(_oracle_fp64_losses(g) - ref_all) / np.abs(ref_all)).max(axis=1)
+    l64, probe64 = _oracle_fp64_losses(g)
+    band = (np.abs(l64 - ref_all) / np.abs(ref_all)).max(axis=1)
     for s in range(ref_all.shape[0]):
         m.set_input_fc2(data)
         m.optimize_parameters()
@@ -112,7 +115,9 @@ def test_train_step_vs_reference_golden(gb, golden):
         assert rel.max() <= tol, (s, rel, band[s])
     with torch.no_grad():
         out = m.forward_eval(torch.from_numpy(g["probe"])).cpu().numpy()
-    assert np.abs(out - g["probe_out"]).max() < 5e-3
+    # G_A(probe) after 3 Adam steps: same rule (1e-3, or 3x the exact-arithmetic deviation)
+    dev64 = np.abs(probe64 - g["probe_out"]).max()
+    assert np.abs(out - g["probe_out"]).max() <= max(1e-3, 3 * dev64), (np.abs(out - g["probe_out"]).max(), dev64)
 
 
 def test_full_size_generator_vs_oracle(gb):

@@ -80,8 +80,13 @@ def test_conv_fwd_dgrad_wgrad(ops, case):
     # dgrad
     gyn = _nhwc(gy, ops)
     if mode == "reflect":
+        # two routes: padded-grid transposed conv + fold, and the fused reflect-aware gather
         dxp = ops.conv2d_tfwd(gyn, ck, None, H + 2 * pad, W + 2 * pad, xn.shape[-1], k, k, 1, 0)
-        dx = ops.reflect_fold(dxp, pad)
+        _close(_nchw(ops.reflect_fold(dxp, pad), Ci, ops), xr.grad, what=name + " dgrad(fold)")
+        add = _nhwc(_g(40, (N, Ci, H, W)), ops)
+        dx2 = ops.conv2d_tfwd(gyn, ck, None, H, W, xn.shape[-1], k, k, 1, pad, pad_mode="reflect", addend=add)
+        _close(_nchw(dx2, Ci, ops) - _nchw(add, Ci, ops), xr.grad, what=name + " dgrad(reflect+addend)")
+        dx = ops.conv2d_tfwd(gyn, ck, None, H, W, xn.shape[-1], k, k, 1, pad, pad_mode="reflect")
     else:
         dx = ops.conv2d_tfwd(gyn, ck, None, H, W, xn.shape[-1], k, k, st, pad)
     _close(_nchw(dx, Ci, ops), xr.grad, what=name + " dgrad")
@@ -141,8 +146,12 @@ def test_instnorm_act(ops, act):
     s = ops.instnorm_stats(xn)
     y = ops.instnorm_act_fwd(xn, s, act, 0.2, residual=_nhwc(res, ops) if act == "none" else None)
     _close(_nchw(y, C, ops), outr, tol=1e-5, what="IN fwd")
-    dx = ops.instnorm_act_bwd(_nhwc(gy, ops), xn, s, act, 0.2)
+    db = torch.full((C,), 0.5, device=DEV)
+    dx = ops.instnorm_act_bwd(_nhwc(gy, ops), xn, s, act, 0.2, db=db)
     _close(_nchw(dx, C, ops), xr.grad, tol=1e-5, what="IN bwd")
+    # bias gradient of the conv feeding the IN = per-channel sum of dx (exactly 0 in exact math)
+    ref_db = xr.grad.sum(dim=(0, 2, 3)).double()
+    assert (db.cpu().double() - 0.5 - ref_db).abs().max().item() < 1e-5 * xr.grad.abs().sum().item() / C
 
 
 def test_warp_golden(ops, golden):

@@ -1,0 +1,63 @@
+"""Developer microbenchmark: time the conv kernel families on the CycleGAN layer shapes (B=4, 256^2)
+for each GEMM tile choice (vst_debug_set_tiles), with HIP events on the launch stream."""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+import gbvst  # noqa: E402
+from gbvst import ops  # noqa: E402
+
+gbvst._lib.load()
+dev = torch.device("cuda")
+B = int(os.environ.get("B", "4"))
+TILES = {"auto": -1, "128x128w8": 0, "64x128": 1, "128x64": 2, "64x64": 3, "128x128w4": 5}
+
+
+def timeit(fn, reps=10):
+    for _ in range(2):
+        fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1) / reps * 1e3  # us
+
+
+# (name, Cin, H, Cout, k, stride, pad, mode)
+LAYERS = [
+    ("res", 256, 64, 256, 3, 1, 1, "reflect"),
+    ("d128", 64, 256, 128, 3, 2, 1, "zero"),
+    ("d256", 128, 128, 256, 3, 2, 1, "zero"),
+    ("c7s1_64", 4, 256, 64, 7, 1, 3, "reflect"),
+    ("D2", 64, 128, 128, 4, 2, 1, "zero"),
+    ("D4", 256, 32, 512, 4, 1, 1, "zero"),
+]
+res = []
+for name, Ci, H, Co, k, st, pad, mode in LAYERS:
+    x = torch.randn(B, H, H, Ci, device=dev)
+    w = torch.randn(Co, Ci, k, k, device=dev) * 0.02
+    kc, ck = ops.weight_pack(w, ops.PACK_KC), ops.weight_pack(w, ops.PACK_CK)
+    Ho = (H + 2 * pad - k) // st + 1
+    gy = torch.randn(B, Ho, Ho, Co, device=dev)
+    dw = torch.zeros(Co, Ci, k, k, device=dev)
+    flop = 2.0 * B * Ho * Ho * Co * Ci * k * k
+    for tname, tv in TILES.items():
+        ops.debug_set_tiles(tv, tv, tv)
+        try:
+            tf = timeit(lambda: ops.conv2d_fwd(x, kc, None, Co, k, k, st, pad, mode))
+            tt = timeit(lambda: ops.conv2d_tfwd(gy, ck, None, H, H, Ci, k, k, st, pad, pad_mode=mode))
+            tw = timeit(lambda: ops.conv2d_wgrad(x, gy, dw, None, k, k, st, pad, mode, Co, Ci, Ci * k * k, k * k))
+        except Exception as e:  # noqa
+            print(name, tname, "ERR", e)
+            continue
+        r = {"layer": name, "tile": tname, "fprop_us": round(tf, 1), "tconv_us": round(tt, 1),
+             "wgrad_us": round(tw, 1), "fprop_TF": round(flop / tf / 1e6, 1),
+             "tconv_TF": round(flop / tt / 1e6, 1), "wgrad_TF": round(flop / tw / 1e6, 1)}
+        res.append(r)
+        print(json.dumps(r), flush=True)
+ops.debug_set_tiles(-1, -1, -1)

@@ -1,0 +1,109 @@
+"""Data-parallel path on CPU with the gloo backend, world_size 2.
+
+* GradExchange averages every rank's flat gradient buffer with bucketed all_reduce(SUM)/world and
+  broadcast_params makes all replicas equal to rank 0.
+* DP equivalence: two ranks each back-propagating the mean loss of their half batch through the
+  reference-architecture networks (CPU oracle), exchanged with GradExchange, give the gradient of
+  the full-batch loss on one process — exact up to fp32 summation order, because InstanceNorm is
+  per sample and every loss is a batch mean.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+class _FlatNet:
+    """Minimal stand-in exposing the FlatNet interface GradExchange/broadcast_params use."""
+
+    def __init__(self, net):
+        self.net = net
+        self.params = list(net.parameters())
+        n = sum(p.numel() for p in self.params)
+        self.flat_param = torch.cat([p.detach().reshape(-1) for p in self.params])
+        self.flat_grad = torch.zeros(n)
+
+    def gather_grads(self):
+        self.flat_grad.copy_(torch.cat([p.grad.reshape(-1) for p in self.params]))
+
+    def bump_version(self):
+        pass
+
+
+def _worker(rank, world, port, q, bucket_bytes):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(1)
+    from gbvst import dp
+    from oracle import cpu_ref, prng
+
+    # 1) exchange arithmetic on synthetic buffers
+    nets = [_FlatNet(torch.nn.Linear(7, 5)), _FlatNet(torch.nn.Linear(3, 2))]
+    for i, n in enumerate(nets):
+        n.flat_grad.copy_(torch.arange(n.flat_grad.numel(), dtype=torch.float32) * (rank + 1) + i)
+    dp.GradExchange(world, bucket_bytes=bucket_bytes)(nets)
+    ok_avg = all(torch.allclose(n.flat_grad, torch.arange(n.flat_grad.numel(), dtype=torch.float32)
+                                * (sum(r + 1 for r in range(world)) / world) + i)
+                 for i, n in enumerate(nets))
+    for n in nets:
+        n.flat_param.fill_(float(rank))
+    dp.broadcast_params(nets)
+    ok_bcast = all(bool((n.flat_param == 0).all()) for n in nets)
+
+    # 2) DP equivalence through the reference-architecture generator (ngf=4, 32x32)
+    G = cpu_ref.RefResnetGenerator(3, 3, 4, 2)
+    cpu_ref.load_np_state(G, prng.init_state_dict(cpu_ref.state_shapes(G), base_seed=5))
+    x = torch.from_numpy(prng.uniform_f32(9, (4, 3, 32, 32), -1, 1))
+    t = torch.from_numpy(prng.uniform_f32(10, (4, 3, 32, 32), -1, 1))
+    xs, ts = x.chunk(world)[rank], t.chunk(world)[rank]
+    (G(xs) - ts).abs().mean().backward()
+    fn = _FlatNet(G)
+    fn.gather_grads()
+    dp.GradExchange(world, bucket_bytes=bucket_bytes)([fn])
+    q.put((rank, ok_avg, ok_bcast, fn.flat_grad.clone()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("bucket_bytes", [64, 32 << 20])
+def test_grad_exchange_gloo_world2(bucket_bytes):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, bucket_bytes)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    res.sort(key=lambda r: r[0])
+    assert all(r[1] for r in res), "all_reduce average wrong"
+    assert all(r[2] for r in res), "broadcast wrong"
+    # both ranks hold the same averaged gradient, equal to the single-process full-batch gradient
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from oracle import cpu_ref, prng
+    G = cpu_ref.RefResnetGenerator(3, 3, 4, 2)
+    cpu_ref.load_np_state(G, prng.init_state_dict(cpu_ref.state_shapes(G), base_seed=5))
+    x = torch.from_numpy(prng.uniform_f32(9, (4, 3, 32, 32), -1, 1))
+    t = torch.from_numpy(prng.uniform_f32(10, (4, 3, 32, 32), -1, 1))
+    (G(x) - t).abs().mean().backward()
+    full = torch.cat([p.grad.reshape(-1) for p in G.parameters()])
+    assert torch.allclose(res[0][3], res[1][3])
+    err = (res[0][3] - full).abs().max() / full.abs().max()
+    assert err < 1e-5, err

@@ -51,7 +51,7 @@ def dominant_kernel_roofline(device, B, reps=20):
     from gbvst import ops
     x = torch.randn(B, 64, 64, 256, device=device)
     w = torch.randn(256, 256, 3, 3, device=device) * 0.02
-    kc = ops.weight_pack(w, ops.PACK_KC)
+    kc = ops.weight_pack(w, ops.PACK_FWD)
     bias = torch.zeros(256, device=device)
     y = torch.empty(B, 64, 64, 256, device=device)
     s = torch.cuda.Stream(device=device)

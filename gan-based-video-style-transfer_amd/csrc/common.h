@@ -75,6 +75,13 @@ int skinny_out_launch(int mode, const float* in, const float* wp, const float* b
                       const float* addend, float* out, int N, int Hi, int Wi, int Cin, int Ho,
                       int Wo, int R, int S, int st, int pad, int reflect, int act, float slope,
                       hipStream_t s);
+// [row][k]-LDS implicit-GEMM fprop / transposed conv (conv_rk.hip); kind = tile override or -1
+void rk_fprop_launch(const float* x, const float* wp, const float* bias, float* y, int N, int H, int W,
+                     int C, int Ho, int Wo, int Cop, int R, int S, int st, int pad, int reflect, int act,
+                     float slope, int kind, hipStream_t s);
+void rk_tconv_launch(const float* in, const float* wp, const float* bias, const float* addend,
+                     float* out, int N, int Hi, int Wi, int Cy, int Ho, int Wo, int Cx, int R, int S,
+                     int st, int pad, int reflect, int act, float slope, int kind, hipStream_t s);
 int skinny_wgrad_launch(const float* x, const float* dy, float* slab, int H, int W, int Cx, int Ho,
                         int Wo, int S, int st, int pad, int reflect, int Mw, int P, int chunk,
                         int nsplit, hipStream_t s);

@@ -645,8 +645,8 @@ static WgradPlan plan_wgrad(int N, int Ho, int Wo, int Cx, int Cyp, int R, int S
   const int P = N * Ho * Wo;
   if (Cyp == 4) {  // VALU skinny path: one thread per (tap, 4 input channels) per split
     p.tile = T256x32;
-    int ns = ceil_div(65536, p.Mw / 4);
-    if (ns > 64) ns = 64;
+    int ns = ceil_div(262144, p.Mw / 4);  // ~4 waves per SIMD
+    if (ns > 256) ns = 256;
     const int max_ns = ceil_div(P, 64);
     if (ns > max_ns) ns = max_ns;
     if (ns < 1) ns = 1;
@@ -700,7 +700,9 @@ extern "C" int vst_conv2d_fwd(const float* x, const float* wp, const float* bias
   hipLaunchKernelGGL((conv_fprop_k<BM_, BN_, WM_, WN_>), dim3(ceil_div(M, BM_), ceil_div(Cop, BN_)),  \
                      dim3(Tile<BM_, BN_, WM_, WN_>::NT), 0, s, x, wp, bias, y, H, W, Cx, Ho, Wo, Cop, S, \
                      stride, pad, refl, act, slope, M, K)
-  VST_DISPATCH_TILE(pick_tile(M, Cop, 0), VST_FPROP)
+  (void)pick_tile;
+  rk_fprop_launch(x, wp, bias, y, N, H, W, Cx, Ho, Wo, Cop, R, S, stride, pad, refl, act, slope,
+                    g_tile_override[0], s);
 #undef VST_FPROP
   return check_launch("conv2d_fwd");
 }
@@ -731,7 +733,9 @@ extern "C" int vst_conv2d_tfwd(const float* in, const float* wp, const float* bi
   if (stride == 1) VST_TCONV_ST(BM_, BN_, WM_, WN_, 1);     \
   else if (stride == 2) VST_TCONV_ST(BM_, BN_, WM_, WN_, 2); \
   else VST_TCONV_ST(BM_, BN_, WM_, WN_, 0);
-  VST_DISPATCH_TILE(pick_tile((long)Mmax * stride * stride, Cx, 1), VST_TCONV)
+  (void)Mmax;
+  rk_tconv_launch(in, wp, bias, addend, out, N, Hi, Wi, Cy, Ho, Wo, Cx, R, S, stride, pad, refl, act,
+                    slope, g_tile_override[1], s);
 #undef VST_TCONV
 #undef VST_TCONV_ST
   return check_launch("conv2d_tfwd");

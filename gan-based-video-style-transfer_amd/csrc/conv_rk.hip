@@ -1,0 +1,425 @@
+// Forward and transposed (data-gradient) implicit-GEMM convolutions on gfx950 fp32 MFMA with a
+// row-major [row][k] LDS image — the production path behind vst_conv2d_fwd / vst_conv2d_tfwd.
+//
+// Why this layout: v_mfma_f32_32x32x2_f32 takes ONE f32 per lane per operand (lane l supplies
+// A[l&31][k = l>>5]).  The reduction order inside a K group is free, so within each 8-deep group
+// lane-half kh feeds k = 4*kh + t to MFMA t (t = 0..3).  A lane's four operands for four MFMAs are
+// then 4 consecutive floats of its row: one ds_read_b128 replaces four ds_read_b32, and both
+// operand tiles are written with ds_write_b128 straight from coalesced 128-byte global rows
+// (8 lanes x float4 per pixel row / weight row) — no transposing scalar LDS writes.  Row stride is
+// BK + 4 floats (144 B): the 16-lane groups of ds_read_b128 hit 16 distinct 16-byte bank slots.
+//
+//   conv_fprop_rk_k : y = act(conv(x, w) + bias)   m = output pixel, n = out channel,
+//                     k = (r, s, ci); B operand = VST_PACK_OK pack [Co][R][S][Ci]
+//   conv_tconv_rk_k : transposed conv / data gradient, gathered per output-parity class
+//                     (blockIdx.z), stride-specialised (ST), reflect-pad gradient folded into the
+//                     gather (mirrored rows/columns), residual addend fused in the epilogue;
+//                     B operand = VST_PACK_IK pack [Ci][R][S][Co]
+// Both keep the next K-step's global loads interleaved into the current MFMA stream and the
+// double-buffered LDS stage with one barrier per 32-deep K-step.
+#include "common.h"
+
+namespace vst {
+namespace rk {
+
+constexpr int BK = 32;
+constexpr int LDK = BK + 4;
+constexpr int NOPOS = -(1 << 20);
+
+template <int BM, int BN, int WM, int WN>
+struct Tile {
+  static constexpr int NW = (BM / WM) * (BN / WN);
+  static constexpr int NT = 64 * NW;
+  static constexpr int WAVES_N = BN / WN;
+  static constexpr int MI = WM / 32;
+  static constexpr int NI = WN / 32;
+  static constexpr int A_ELEMS = BM * LDK;
+  static constexpr int B_ELEMS = BN * LDK;
+  static constexpr int STAGE = A_ELEMS + B_ELEMS;
+  static constexpr int ROWS_PER_PASS = NT / 8;   // 8 lanes x float4 cover one 32-deep row
+  static constexpr int A_LD = BM / ROWS_PER_PASS;
+  static constexpr int B_LD = BN / ROWS_PER_PASS;
+  static_assert(NW == 4 || NW == 8, "4 or 8 waves");
+  static_assert(BM % ROWS_PER_PASS == 0 && BN % ROWS_PER_PASS == 0, "row coverage");
+};
+
+__device__ __forceinline__ float comp(const float4& v, int t) {
+  return t == 0 ? v.x : (t == 1 ? v.y : (t == 2 ? v.z : v.w));
+}
+
+template <int BM, int BN, int WM, int WN, class Hook>
+__device__ __forceinline__ void mma_stage(const float* __restrict__ As, const float* __restrict__ Bs,
+                                          f32x16 (&acc)[WM / 32][WN / 32], int wm0, int wn0,
+                                          int lane, Hook hook) {
+  using T = Tile<BM, BN, WM, WN>;
+  const int kh = lane >> 5, li = lane & 31;
+  const float* pa = As + (wm0 + li) * LDK + 4 * kh;
+  const float* pb = Bs + (wn0 + li) * LDK + 4 * kh;
+  float4 fa[2][T::MI], fb[2][T::NI];
+#pragma unroll
+  for (int i = 0; i < T::MI; ++i) fa[0][i] = *reinterpret_cast<const float4*>(pa + 32 * i * LDK);
+#pragma unroll
+  for (int j = 0; j < T::NI; ++j) fb[0][j] = *reinterpret_cast<const float4*>(pb + 32 * j * LDK);
+#pragma unroll
+  for (int g = 0; g < BK / 8; ++g) {
+    const int cur = g & 1, nxt = cur ^ 1;
+    hook(g);
+    if (g + 1 < BK / 8) {
+#pragma unroll
+      for (int i = 0; i < T::MI; ++i)
+        fa[nxt][i] = *reinterpret_cast<const float4*>(pa + 32 * i * LDK + 8 * (g + 1));
+#pragma unroll
+      for (int j = 0; j < T::NI; ++j)
+        fb[nxt][j] = *reinterpret_cast<const float4*>(pb + 32 * j * LDK + 8 * (g + 1));
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int i = 0; i < T::MI; ++i)
+#pragma unroll
+        for (int j = 0; j < T::NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(comp(fa[cur][i], t), comp(fb[cur][j], t),
+                                                           acc[i][j], 0, 0, 0);
+  }
+}
+
+template <int BM, int BN, int WM, int WN, int NLOAD, class LoadOne, class Adv, class Store>
+__device__ __forceinline__ void main_loop(float* smem, int nk, f32x16 (&acc)[WM / 32][WN / 32],
+                                          LoadOne load_one, Adv adv, Store store) {
+  using T = Tile<BM, BN, WM, WN>;
+  constexpr int PER = (NLOAD + BK / 8 - 1) / (BK / 8);
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wm0 = (wave / T::WAVES_N) * WM, wn0 = (wave % T::WAVES_N) * WN;
+  if (nk > 0) {
+#pragma unroll
+    for (int i = 0; i < NLOAD; ++i) load_one(i, 0);
+    store(smem);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    float* cur = smem + (kt & 1) * T::STAGE;
+    const bool next = kt + 1 < nk;
+    if (next) adv();
+    const int k0n = (kt + 1) * BK;
+    mma_stage<BM, BN, WM, WN>(cur, cur + T::A_ELEMS, acc, wm0, wn0, lane, [&](int g) {
+      if (next) {
+#pragma unroll
+        for (int u = 0; u < PER; ++u)
+          if (PER * g + u < NLOAD) load_one(PER * g + u, k0n);
+      }
+    });
+    if (next) store(smem + ((kt + 1) & 1) * T::STAGE);
+    __syncthreads();
+  }
+}
+
+__device__ __forceinline__ int remap_mtile(int bx, int nx) {
+  if ((nx & 7) != 0) return bx;
+  return (bx & 7) * (nx >> 3) + (bx >> 3);
+}
+
+template <int MI, int NI>
+__device__ __forceinline__ void zero_acc(f32x16 (&acc)[MI][NI]) {
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+}
+
+// ------------------------------------------------------------------------------------------ fprop
+template <int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__((Tile<BM, BN, WM, WN>::NT), 2) void conv_fprop_rk_k(
+    const float* __restrict__ x, const float* __restrict__ wp, const float* __restrict__ bias,
+    float* __restrict__ y, int H, int W, int C, int Ho, int Wo, int Cop, int S, int st, int pad,
+    int reflect, int act, float slope, int M, int Ktot) {
+  using T = Tile<BM, BN, WM, WN>;
+  constexpr int NT = T::NT, A_LD = T::A_LD, B_LD = T::B_LD, RP = T::ROWS_PER_PASS;
+  __shared__ __attribute__((aligned(16))) float smem[2 * T::STAGE];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int mt = remap_mtile(blockIdx.x, gridDim.x);
+  const int m0 = mt * BM, n0 = blockIdx.y * BN;
+  const int kq = t & 7, rb = t >> 3;
+
+  // k state (one per thread: every row this thread stages uses the same k position)
+  int kc = (4 * kq) % C, ks, kr;
+  {
+    const int rs = (4 * kq) / C;
+    kr = rs / S;
+    ks = rs - kr * S;
+  }
+  // A rows: output pixels m0 + rb + RP*j
+  int hb[A_LD], wb[A_LD];
+  const float* xb[A_LD];
+  bool mv[A_LD];
+#pragma unroll
+  for (int j = 0; j < A_LD; ++j) {
+    const int m = m0 + rb + RP * j;
+    mv[j] = m < M;
+    const int mm = mv[j] ? m : 0;
+    const int hw = Ho * Wo;
+    const int n = mm / hw, rem = mm - n * hw, ho = rem / Wo, wo = rem - ho * Wo;
+    hb[j] = ho * st - pad;
+    wb[j] = wo * st - pad;
+    xb[j] = x + (long)n * H * W * C;
+  }
+  const float* wrow[B_LD];
+  bool nv[B_LD];
+#pragma unroll
+  for (int j = 0; j < B_LD; ++j) {
+    const int n = n0 + rb + RP * j;
+    nv[j] = n < Cop;
+    wrow[j] = wp + (long)(nv[j] ? n : 0) * Ktot;
+  }
+
+  float4 ra[A_LD], rbv[B_LD];
+  int kcur = 4 * kq;  // absolute k of this thread's float4 in the stage being loaded
+  auto load_one = [&](int i, int) {
+    if (i < A_LD) {
+      const int j = i;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (mv[j] && kcur < Ktot) {
+        int hi = hb[j] + kr, wi = wb[j] + ks;
+        bool ok = true;
+        if (reflect) {
+          hi = reflect_idx(hi, H);
+          wi = reflect_idx(wi, W);
+        } else {
+          ok = (unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W;
+        }
+        if (ok) v = *reinterpret_cast<const float4*>(xb[j] + ((long)hi * W + wi) * C + kc);
+      }
+      ra[j] = v;
+    } else {
+      const int j = i - A_LD;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (nv[j] && kcur < Ktot) v = *reinterpret_cast<const float4*>(wrow[j] + kcur);
+      rbv[j] = v;
+    }
+  };
+  auto adv = [&]() {
+    kcur += BK;
+    kc += BK;
+    while (kc >= C) {
+      kc -= C;
+      if (++ks == S) { ks = 0; ++kr; }
+    }
+  };
+  auto store = [&](float* As) {
+    float* Bs = As + T::A_ELEMS;
+#pragma unroll
+    for (int j = 0; j < A_LD; ++j) *reinterpret_cast<float4*>(As + (rb + RP * j) * LDK + 4 * kq) = ra[j];
+#pragma unroll
+    for (int j = 0; j < B_LD; ++j) *reinterpret_cast<float4*>(Bs + (rb + RP * j) * LDK + 4 * kq) = rbv[j];
+  };
+
+  f32x16 acc[T::MI][T::NI];
+  zero_acc(acc);
+  main_loop<BM, BN, WM, WN, A_LD + B_LD>(smem, (Ktot + BK - 1) / BK, acc, load_one, adv, store);
+  (void)NT;
+
+  const int wm0 = (wave / T::WAVES_N) * WM, wn0 = (wave % T::WAVES_N) * WN;
+#pragma unroll
+  for (int i = 0; i < T::MI; ++i)
+#pragma unroll
+    for (int j = 0; j < T::NI; ++j) {
+      const int n = n0 + wn0 + 32 * j + (lane & 31);
+      if (n >= Cop) continue;
+      const float bv = bias ? bias[n] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int mm = m0 + wm0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (mm < M) y[(long)mm * Cop + n] = apply_act(acc[i][j][r] + bv, act, slope);
+      }
+    }
+}
+
+// ------------------------------------------------------------------- transposed conv / dgrad
+template <int BM, int BN, int WM, int WN, int ST>
+__global__ __launch_bounds__((Tile<BM, BN, WM, WN>::NT), 2) void conv_tconv_rk_k(
+    const float* __restrict__ in, const float* __restrict__ wp, const float* __restrict__ bias,
+    const float* __restrict__ addend, float* __restrict__ out, int Hi, int Wi, int Cy, int Ho,
+    int Wo, int Cx, int R, int S, int st_rt, int pad, int reflect, int act, float slope, int Nimg) {
+  using T = Tile<BM, BN, WM, WN>;
+  constexpr int A_LD = T::A_LD, B_LD = T::B_LD, RP = T::ROWS_PER_PASS;
+  __shared__ __attribute__((aligned(16))) float smem[2 * T::STAGE];
+  const int st = ST > 0 ? ST : st_rt;
+  const int ca = blockIdx.z / st, cb = blockIdx.z % st;
+  const int Hc = Ho > ca ? (Ho - ca + st - 1) / st : 0;
+  const int Wc = Wo > cb ? (Wo - cb + st - 1) / st : 0;
+  const int M = Nimg * Hc * Wc;
+  const int mt = remap_mtile(blockIdx.x, gridDim.x);
+  const int m0 = mt * BM, n0 = blockIdx.y * BN;
+  if (m0 >= M) return;
+  const int r0 = (ca + pad) % st, s0 = (cb + pad) % st;
+  const int nr = r0 < R ? (R - r0 + st - 1) / st : 0;
+  const int ns = s0 < S ? (S - s0 + st - 1) / st : 0;
+  const int Ktot = nr * ns * Cy;
+
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int kq = t & 7, rb = t >> 3;
+  int kc = ns > 0 ? (4 * kq) % Cy : 0, kis, kir;
+  {
+    const int tp = Cy > 0 ? (4 * kq) / Cy : 0;
+    kir = ns > 0 ? tp / ns : 0;
+    kis = tp - kir * ns;
+  }
+  int hp[A_LD], wq[A_LD], hm[A_LD], wm[A_LD];
+  const float* ib[A_LD];
+  bool mv[A_LD];
+#pragma unroll
+  for (int j = 0; j < A_LD; ++j) {
+    const int m = m0 + rb + RP * j;
+    mv[j] = m < M;
+    const int mm = mv[j] ? m : 0;
+    const int hw = Hc * Wc;
+    const int n = mm / hw, rem = mm - n * hw, hh = rem / Wc, ww = rem - hh * Wc;
+    const int h = ca + st * hh, w = cb + st * ww;
+    hp[j] = h + pad;
+    wq[j] = w + pad;
+    hm[j] = NOPOS;
+    wm[j] = NOPOS;
+    if (reflect) {
+      if (h >= 1 && h <= pad) hm[j] = pad - h;
+      else if (h >= Ho - 1 - pad && h <= Ho - 2) hm[j] = 2 * Ho - 2 - h + pad;
+      if (w >= 1 && w <= pad) wm[j] = pad - w;
+      else if (w >= Wo - 1 - pad && w <= Wo - 2) wm[j] = 2 * Wo - 2 - w + pad;
+    }
+    ib[j] = in + (long)n * Hi * Wi * Cy;
+  }
+  const long wstride = (long)R * S * Cy;
+  const float* wrow[B_LD];
+  bool nv[B_LD];
+#pragma unroll
+  for (int j = 0; j < B_LD; ++j) {
+    const int n = n0 + rb + RP * j;
+    nv[j] = n < Cx;
+    wrow[j] = wp + (long)(nv[j] ? n : 0) * wstride;
+  }
+
+  float4 ra[A_LD], rbv[B_LD];
+  int kcur = 4 * kq;
+  auto gather1 = [&](const float* base, int hpos, int wpos, int r, int s, float4& v) {
+    const int dh = hpos - r, dw = wpos - s;
+    if (dh >= 0 && dw >= 0) {
+      const int ho = dh / st, wo = dw / st;
+      if (ho < Hi && wo < Wi) add_f4(v, *reinterpret_cast<const float4*>(base + ((long)ho * Wi + wo) * Cy + kc));
+    }
+  };
+  auto load_one = [&](int i, int) {
+    const int r = r0 + st * kir, s = s0 + st * kis;
+    if (i < A_LD) {
+      const int j = i;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (mv[j] && kcur < Ktot) {
+        gather1(ib[j], hp[j], wq[j], r, s, v);
+        if (hm[j] != NOPOS) gather1(ib[j], hm[j], wq[j], r, s, v);
+        if (wm[j] != NOPOS) {
+          gather1(ib[j], hp[j], wm[j], r, s, v);
+          if (hm[j] != NOPOS) gather1(ib[j], hm[j], wm[j], r, s, v);
+        }
+      }
+      ra[j] = v;
+    } else {
+      const int j = i - A_LD;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (nv[j] && kcur < Ktot)
+        v = *reinterpret_cast<const float4*>(wrow[j] + (long)(r * S + s) * Cy + kc);
+      rbv[j] = v;
+    }
+  };
+  auto adv = [&]() {
+    kcur += BK;
+    kc += BK;
+    while (kc >= Cy) {
+      kc -= Cy;
+      if (++kis == ns) { kis = 0; ++kir; }
+    }
+  };
+  auto store = [&](float* As) {
+    float* Bs = As + T::A_ELEMS;
+#pragma unroll
+    for (int j = 0; j < A_LD; ++j) *reinterpret_cast<float4*>(As + (rb + RP * j) * LDK + 4 * kq) = ra[j];
+#pragma unroll
+    for (int j = 0; j < B_LD; ++j) *reinterpret_cast<float4*>(Bs + (rb + RP * j) * LDK + 4 * kq) = rbv[j];
+  };
+
+  f32x16 acc[T::MI][T::NI];
+  zero_acc(acc);
+  main_loop<BM, BN, WM, WN, A_LD + B_LD>(smem, (Ktot + BK - 1) / BK, acc, load_one, adv, store);
+
+  const int wm0 = (wave / T::WAVES_N) * WM, wn0 = (wave % T::WAVES_N) * WN;
+  const int hw = Hc * Wc;
+#pragma unroll
+  for (int i = 0; i < T::MI; ++i)
+#pragma unroll
+    for (int j = 0; j < T::NI; ++j) {
+      const int n = n0 + wn0 + 32 * j + (lane & 31);
+      if (n >= Cx) continue;
+      const float bv = bias ? bias[n] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int mm = m0 + wm0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (mm >= M) continue;
+        const int nimg = mm / hw, rem = mm - nimg * hw, hh = rem / Wc, ww = rem - hh * Wc;
+        const long o = (((long)nimg * Ho + (ca + st * hh)) * Wo + (cb + st * ww)) * Cx + n;
+        float v = apply_act(acc[i][j][r] + bv, act, slope);
+        if (addend) v += addend[o];
+        out[o] = v;
+      }
+    }
+}
+
+}  // namespace rk
+
+// Tile kinds: 0 = 128x128 (8 waves, 64x32 each), 1 = 64x128, 2 = 128x64, 3 = 64x64 (4 waves)
+int rk_pick(long M, int Nc, int override_kind) {
+  if (override_kind >= 0 && override_kind <= 3) return override_kind;
+  if (Nc <= 64) return M / 128 >= 256 ? 2 : 3;
+  const long n128 = (Nc + 127) / 128;
+  if ((M / 128) * n128 >= 200) return 0;
+  if ((M / 64) * n128 >= 200) return 1;
+  return 3;
+}
+
+#define VST_RK_DISPATCH(kind, LAUNCH)            \
+  switch (kind) {                                 \
+    case 0: LAUNCH(128, 128, 64, 32); break;      \
+    case 1: LAUNCH(64, 128, 32, 64); break;       \
+    case 2: LAUNCH(128, 64, 64, 32); break;       \
+    default: LAUNCH(64, 64, 32, 32); break;       \
+  }
+
+void rk_fprop_launch(const float* x, const float* wp, const float* bias, float* y, int N, int H, int W,
+                     int C, int Ho, int Wo, int Cop, int R, int S, int st, int pad, int reflect, int act,
+                     float slope, int kind, hipStream_t s) {
+  const int M = N * Ho * Wo, K = R * S * C;
+#define VST_L(BM_, BN_, WM_, WN_)                                                                  \
+  hipLaunchKernelGGL((rk::conv_fprop_rk_k<BM_, BN_, WM_, WN_>),                                      \
+                     dim3(ceil_div(M, BM_), ceil_div(Cop, BN_)), dim3(rk::Tile<BM_, BN_, WM_, WN_>::NT), \
+                     0, s, x, wp, bias, y, H, W, C, Ho, Wo, Cop, S, st, pad, reflect, act, slope, M, K)
+  VST_RK_DISPATCH(rk_pick(M, Cop, kind), VST_L)
+#undef VST_L
+}
+
+void rk_tconv_launch(const float* in, const float* wp, const float* bias, const float* addend,
+                     float* out, int N, int Hi, int Wi, int Cy, int Ho, int Wo, int Cx, int R, int S,
+                     int st, int pad, int reflect, int act, float slope, int kind, hipStream_t s) {
+  const int Hc = (Ho + st - 1) / st, Wc = (Wo + st - 1) / st;
+  const int Mmax = N * Hc * Wc;
+#define VST_LST(BM_, BN_, WM_, WN_, ST_)                                                           \
+  hipLaunchKernelGGL((rk::conv_tconv_rk_k<BM_, BN_, WM_, WN_, ST_>),                                 \
+                     dim3(ceil_div(Mmax, BM_), ceil_div(Cx, BN_), st * st),                          \
+                     dim3(rk::Tile<BM_, BN_, WM_, WN_>::NT), 0, s, in, wp, bias, addend, out, Hi, Wi, \
+                     Cy, Ho, Wo, Cx, R, S, st, pad, reflect, act, slope, N)
+#define VST_L(BM_, BN_, WM_, WN_)                   \
+  if (st == 1) VST_LST(BM_, BN_, WM_, WN_, 1);       \
+  else if (st == 2) VST_LST(BM_, BN_, WM_, WN_, 2);  \
+  else VST_LST(BM_, BN_, WM_, WN_, 0);
+  VST_RK_DISPATCH(rk_pick((long)Mmax * st * st, Cx, kind), VST_L)
+#undef VST_L
+#undef VST_LST
+}
+
+}  // namespace vst

@@ -21,8 +21,8 @@ struct RedGeom {
 static bool red_geom(int N, int HW, int C, RedGeom& g) {
   if (C % 4) return false;
   g.LP = C / 4;
-  if (g.LP > NRED || NRED % g.LP) return false;
-  g.PG = NRED / g.LP;
+  if (g.LP > NRED) return false;
+  g.PG = NRED / g.LP;  // threads beyond LP*PG idle when LP does not divide NRED
   long sp = ((long)N * HW + 511) / 512;
   if (sp < 2L * g.PG) sp = 2L * g.PG;
   sp = (sp + g.PG - 1) / g.PG * g.PG;
@@ -59,7 +59,7 @@ __global__ __launch_bounds__(NRED) void in_partial_k(const float* __restrict__ x
   }
   const float4* xb = reinterpret_cast<const float4*>(x) + (long)n * HW * LP + c4;
   const float4* gb = reinterpret_cast<const float4*>(gy) + (long)n * HW * LP + c4;
-  for (int p = p0 + pg; p < p1; p += PG) {
+  for (int p = p0 + pg; pg < PG && p < p1; p += PG) {
     const float4 v = xb[(long)p * LP];
     const float xv[4] = {v.x, v.y, v.z, v.w};
     if (MODE == 0) {
@@ -107,46 +107,69 @@ __global__ __launch_bounds__(NRED) void in_partial_k(const float* __restrict__ x
   }
 }
 
+// Fold the per-slice partials of one (n, 64-channel group): 4 waves stride the slices (coalesced
+// over c), then combine through LDS in a fixed order.  out[v] = sum_z part[n][z][c][v].
+template <int NV>
+__device__ __forceinline__ bool fold_slices(const double* __restrict__ part, int n, int C, int nsplit,
+                                            double (&out)[NV]) {
+  __shared__ double red[NV][4][64];
+  const int cl = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  double acc[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) acc[v] = 0.0;
+  if (c < C)
+    for (int z = q; z < nsplit; z += 4) {
+      const double* a = part + (((long)n * nsplit + z) * C + c) * NV;
+#pragma unroll
+      for (int v = 0; v < NV; ++v) acc[v] += a[v];
+    }
+#pragma unroll
+  for (int v = 0; v < NV; ++v) red[v][q][cl] = acc[v];
+  __syncthreads();
+  if (q != 0 || c >= C) return false;
+#pragma unroll
+  for (int v = 0; v < NV; ++v) out[v] = red[v][0][cl] + red[v][1][cl] + red[v][2][cl] + red[v][3][cl];
+  return true;
+}
+
+// grid (C/64, N), 256 threads
 __global__ void in_finalize_k(const double* __restrict__ part, float* __restrict__ stats, int N,
                               int HW, int C, int nsplit, float eps) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= N * C) return;
-  const int n = idx / C, c = idx - n * C;
-  double s = 0.0, q = 0.0;
-  for (int z = 0; z < nsplit; ++z) {
-    const double* a = part + (((long)n * nsplit + z) * C + c) * 2;
-    s += a[0];
-    q += a[1];
-  }
-  const double mean = s / HW;
-  double var = q / HW - mean * mean;
+  double sq[2];
+  const int n = blockIdx.y;
+  if (!fold_slices<2>(part, n, C, nsplit, sq)) return;
+  const int idx = n * C + blockIdx.x * 64 + (threadIdx.x & 63);
+  const double mean = sq[0] / HW;
+  double var = sq[1] / HW - mean * mean;
   if (var < 0) var = 0;
   stats[2 * idx] = (float)mean;
   stats[2 * idx + 1] = (float)(1.0 / sqrt(var + (double)eps));
 }
 
-// coef[(n*C+c)] = {mean(g), mean(g*xhat)}; db[c] (+)= sum_n sum_p dx = sum_n rstd*(-mean(g xhat)*sum xhat)
-// (the exact per-channel sum of the IN input gradient: the conv-bias gradient of the layer).
+// coef[(n*C+c)] = {mean(g), mean(g*xhat)}; dbn[n*C+c] = sum_p dx = rstd*((sum g - HW*mean g)
+// - mean(g xhat)*sum xhat)  (the exact per-channel sum of the IN input gradient).
 __global__ void in_bwd_finalize_k(const double* __restrict__ part, const float* __restrict__ stats,
-                                  float2* __restrict__ coef, float* __restrict__ db, int N, int HW,
-                                  int C, int nsplit, int accumulate) {
+                                  float2* __restrict__ coef, double* __restrict__ dbn, int N, int HW,
+                                  int C, int nsplit) {
+  double a[3];
+  const int n = blockIdx.y;
+  if (!fold_slices<3>(part, n, C, nsplit, a)) return;
+  const int idx = n * C + blockIdx.x * 64 + (threadIdx.x & 63);
+  const double mg = a[0] / HW, mgx = a[1] / HW;
+  coef[idx] = make_float2((float)mg, (float)mgx);
+  const double rstd = stats[2 * idx + 1];
+  dbn[idx] = rstd * ((a[0] - HW * mg) - mgx * a[2]);
+}
+
+// db[c] (+)= sum_n dbn[n][c] in a fixed order (conv-bias gradient)
+__global__ void in_bias_grad_k(const double* __restrict__ dbn, float* __restrict__ db, int N, int C,
+                               int accumulate) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
-  double dbs = 0.0;
-  for (int n = 0; n < N; ++n) {
-    double sg = 0.0, sgx = 0.0, sx = 0.0;
-    for (int z = 0; z < nsplit; ++z) {
-      const double* a = part + (((long)n * nsplit + z) * C + c) * 3;
-      sg += a[0];
-      sgx += a[1];
-      sx += a[2];
-    }
-    const double mg = sg / HW, mgx = sgx / HW;
-    coef[n * C + c] = make_float2((float)mg, (float)mgx);
-    const double rstd = stats[2 * (n * C + c) + 1];
-    dbs += rstd * ((sg - HW * mg) - mgx * sx);
-  }
-  if (db) db[c] = accumulate ? db[c] + (float)dbs : (float)dbs;
+  double s = 0.0;
+  for (int n = 0; n < N; ++n) s += dbn[(long)n * C + c];
+  db[c] = accumulate ? db[c] + (float)s : (float)s;
 }
 
 __global__ void in_apply_k(const float4* __restrict__ x, const float* __restrict__ stats,
@@ -214,7 +237,7 @@ __global__ __launch_bounds__(NRED) void chsum_partial_k(const float* __restrict_
   const long p0 = (long)blockIdx.x * SP, p1 = min(NHW, p0 + SP);
   double acc[4] = {0, 0, 0, 0};
   const float4* xb = reinterpret_cast<const float4*>(x) + c4;
-  for (long p = p0 + pg; p < p1; p += PG) {
+  for (long p = p0 + pg; pg < PG && p < p1; p += PG) {
     const float4 v = xb[p * LP];
     acc[0] += v.x; acc[1] += v.y; acc[2] += v.z; acc[3] += v.w;
   }
@@ -230,13 +253,14 @@ __global__ __launch_bounds__(NRED) void chsum_partial_k(const float* __restrict_
     }
 }
 
+// grid (Cs/64), 256 threads: db[c] (+)= sum_z part[z][c]
 __global__ void chsum_final_k(const double* __restrict__ part, float* __restrict__ db, int nsplit,
                               int Cs, int Cl, int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  double s[1];
+  if (!fold_slices<1>(part, 0, Cs, nsplit, s)) return;
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   if (c >= Cl) return;
-  double s = 0.0;
-  for (int z = 0; z < nsplit; ++z) s += part[(long)z * Cs + c];
-  db[c] = accumulate ? db[c] + (float)s : (float)s;
+  db[c] = accumulate ? db[c] + (float)s[0] : (float)s[0];
 }
 
 }  // namespace vst
@@ -246,7 +270,8 @@ using namespace vst;
 extern "C" size_t vst_instnorm_ws_bytes(int N, int HW, int C) {
   RedGeom g;
   if (!red_geom(N, HW, C, g)) return 0;
-  return (size_t)N * g.nsplit * C * 3 * sizeof(double) + (size_t)N * C * sizeof(float2) + 256;
+  return (size_t)N * g.nsplit * C * 3 * sizeof(double) + (size_t)N * C * (sizeof(float2) + sizeof(double)) +
+         256;
 }
 
 extern "C" int vst_instnorm_stats(const float* x, float* stats, float* ws, int N, int HW, int C,
@@ -258,8 +283,8 @@ extern "C" int vst_instnorm_stats(const float* x, float* stats, float* ws, int N
   double* part = reinterpret_cast<double*>(ws);
   hipLaunchKernelGGL(in_partial_k<0>, dim3(g.nsplit, N), dim3(NRED), 0, s, x, (const float*)nullptr,
                      (const float*)nullptr, part, HW, C, g.LP, g.PG, g.SP, g.nsplit, 0, 0.f);
-  hipLaunchKernelGGL(in_finalize_k, dim3(ceil_div((long)N * C, 256)), dim3(256), 0, s, part, stats, N,
-                     HW, C, g.nsplit, eps);
+  hipLaunchKernelGGL(in_finalize_k, dim3(ceil_div(C, 64), N), dim3(256), 0, s, part, stats, N, HW, C,
+                     g.nsplit, eps);
   return check_launch("instnorm_stats");
 }
 
@@ -285,8 +310,12 @@ extern "C" int vst_instnorm_act_bwd(const float* gy, const float* x, const float
                                            (size_t)N * g.nsplit * C * 3 * sizeof(double));
   hipLaunchKernelGGL(in_partial_k<1>, dim3(g.nsplit, N), dim3(NRED), 0, s, x, gy, stats, part, HW, C,
                      g.LP, g.PG, g.SP, g.nsplit, act, slope);
-  hipLaunchKernelGGL(in_bwd_finalize_k, dim3(ceil_div(C, 256)), dim3(256), 0, s, part, stats, coef, db,
-                     N, HW, C, g.nsplit, accumulate_db);
+  double* dbn = reinterpret_cast<double*>(reinterpret_cast<char*>(coef) + (size_t)N * C * sizeof(float2));
+  hipLaunchKernelGGL(in_bwd_finalize_k, dim3(ceil_div(C, 64), N), dim3(256), 0, s, part, stats, coef, dbn,
+                     N, HW, C, g.nsplit);
+  if (db)
+    hipLaunchKernelGGL(in_bias_grad_k, dim3(ceil_div(C, 256)), dim3(256), 0, s, dbn, db, N, C,
+                       accumulate_db);
   const long total4 = (long)N * HW * C / 4;
   hipLaunchKernelGGL(in_bwd_apply_k, dim3(ceil_div(total4, 256)), dim3(256), 0, s,
                      reinterpret_cast<const float4*>(gy), reinterpret_cast<const float4*>(x), stats,
@@ -316,7 +345,7 @@ extern "C" int vst_channel_sum(const float* x, float* db, float* ws, long NHW, i
   hipStream_t s = (hipStream_t)stream;
   double* part = reinterpret_cast<double*>(ws);
   hipLaunchKernelGGL(chsum_partial_k, dim3(g.nsplit), dim3(NRED), 0, s, x, part, NHW, g.LP, g.PG, g.SP);
-  hipLaunchKernelGGL(chsum_final_k, dim3(ceil_div(Cl, 256)), dim3(256), 0, s, part, db, g.nsplit, Cs, Cl,
+  hipLaunchKernelGGL(chsum_final_k, dim3(ceil_div(Cs, 64)), dim3(256), 0, s, part, db, g.nsplit, Cs, Cl,
                      accumulate);
   return check_launch("channel_sum");
 }

@@ -232,7 +232,7 @@ class _ToNCHW(torch.autograd.Function):
 
 
 def _pack_conv(m):
-    return (ops.weight_pack(m.weight, ops.PACK_KC), ops.weight_pack(m.weight, ops.PACK_CK),
+    return (ops.weight_pack(m.weight, ops.PACK_FWD), ops.weight_pack(m.weight, ops.PACK_DGRAD),
             _padded_bias(m))
 
 
@@ -312,7 +312,7 @@ class ResnetGenerator(FlatNet):
         for i, m in enumerate(u):
             # ConvTranspose2d fwd = transposed kernel with rows (r,s,ci) -> CK pack of Wt[Ci][Co];
             # its dgrad = forward conv with KC pack of Wt seen as [O=Ci][I=Co] -> rows (r,s,co), cols ci
-            P[f"u{i}"] = (ops.weight_pack(m.weight, ops.PACK_KC), ops.weight_pack(m.weight, ops.PACK_CK),
+            P[f"u{i}"] = (ops.weight_pack(m.weight, ops.PACK_FWD), ops.weight_pack(m.weight, ops.PACK_DGRAD),
                           _padded_bias(m))
         return P
 

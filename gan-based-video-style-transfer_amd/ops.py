@@ -10,7 +10,9 @@ from . import _lib
 
 ACT = {"none": 0, "relu": 1, "lrelu": 2, "tanh": 3}
 PAD = {"zero": 0, "reflect": 1}
-PACK_KC, PACK_CK = 0, 1
+PACK_KC, PACK_CK, PACK_OK, PACK_IK = 0, 1, 2, 3
+# the conv kernels consume: forward conv -> PACK_OK, data-gradient / transposed conv -> PACK_IK
+PACK_FWD, PACK_DGRAD = PACK_OK, PACK_IK
 IN_EPS = 1e-5
 
 
@@ -69,7 +71,8 @@ def weight_pack(w, mode, transposed=False):
     _dev_check(w)
     O, I_, R, S = w.shape
     Op, Ip = cpad(O), cpad(I_)
-    shape = (R, S, Ip, Op) if mode == PACK_KC else (R, S, Op, Ip)
+    shape = {PACK_KC: (R, S, Ip, Op), PACK_CK: (R, S, Op, Ip), PACK_OK: (Op, R, S, Ip),
+             PACK_IK: (Ip, R, S, Op)}[mode]
     out = torch.empty(shape, device=w.device, dtype=torch.float32)
     _call("vst_weight_pack", _p(w), _p(out), O, I_, R, S, Op, Ip, mode, _stream())
     return out

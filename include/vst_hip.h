@@ -41,8 +41,10 @@ extern "C" {
 enum { VST_OK = 0, VST_EINVAL = 1, VST_EUNSUPPORTED = 2, VST_EHIP = 3 };
 enum { VST_PAD_ZERO = 0, VST_PAD_REFLECT = 1 };
 enum { VST_ACT_NONE = 0, VST_ACT_RELU = 1, VST_ACT_LRELU = 2, VST_ACT_TANH = 3 };
-enum { VST_PACK_KC = 0,   /* [R][S][Ci][Co]  fprop B operand  (rows k=(r,s,ci), cols co) */
-       VST_PACK_CK = 1 }; /* [R][S][Co][Ci]  dgrad B operand  (rows k=(r,s,co), cols ci) */
+enum { VST_PACK_KC = 0,   /* [R][S][Ci][Co]  (rows k=(r,s,ci), cols co) */
+       VST_PACK_CK = 1,   /* [R][S][Co][Ci]  (rows k=(r,s,co), cols ci) */
+       VST_PACK_OK = 2,   /* [Co][R][S][Ci]  conv forward B operand, k=(r,s,ci) contiguous per co */
+       VST_PACK_IK = 3 }; /* [Ci][R][S][Co]  dgrad / transposed-conv B operand, k=(r,s,co) per ci */
 
 const char* vst_last_error(void);
 int vst_version(void);

@@ -70,8 +70,8 @@ def test_conv_fwd_dgrad_wgrad(ops, case):
     gy = _g(4, tuple(yr.shape))
     yr.backward(gy)
     wd = w.to(DEV)
-    kc = ops.weight_pack(wd, ops.PACK_KC)
-    ck = ops.weight_pack(wd, ops.PACK_CK)
+    kc = ops.weight_pack(wd, ops.PACK_FWD)
+    ck = ops.weight_pack(wd, ops.PACK_DGRAD)
     bp = torch.zeros(ops.cpad(Co), device=DEV)
     bp[:Co] = b.to(DEV)
     xn = _nhwc(x, ops)
@@ -110,8 +110,8 @@ def test_conv_transpose(ops, cfg):
     gy = _g(8, tuple(yr.shape))
     yr.backward(gy)
     wd = w.to(DEV)
-    kc = ops.weight_pack(wd, ops.PACK_KC)
-    ck = ops.weight_pack(wd, ops.PACK_CK)
+    kc = ops.weight_pack(wd, ops.PACK_FWD)
+    ck = ops.weight_pack(wd, ops.PACK_DGRAD)
     bp = torch.zeros(ops.cpad(Co), device=DEV)
     bp[:Co] = b.to(DEV)
     xn = _nhwc(x, ops)

@@ -13,7 +13,7 @@ from gbvst import ops  # noqa: E402
 gbvst._lib.load()
 dev = torch.device("cuda")
 B = int(os.environ.get("B", "4"))
-TILES = {"auto": -1, "128x128w8": 0, "64x128": 1, "128x64": 2, "64x64": 3, "128x128w4": 5}
+TILES = {"auto": -1, "128x128w8": 0, "64x128": 1, "128x64": 2, "64x64": 3}
 
 
 def timeit(fn, reps=10):
@@ -41,7 +41,7 @@ res = []
 for name, Ci, H, Co, k, st, pad, mode in LAYERS:
     x = torch.randn(B, H, H, Ci, device=dev)
     w = torch.randn(Co, Ci, k, k, device=dev) * 0.02
-    kc, ck = ops.weight_pack(w, ops.PACK_KC), ops.weight_pack(w, ops.PACK_CK)
+    kc, ck = ops.weight_pack(w, ops.PACK_FWD), ops.weight_pack(w, ops.PACK_DGRAD)
     Ho = (H + 2 * pad - k) // st + 1
     gy = torch.randn(B, Ho, Ho, Co, device=dev)
     dw = torch.zeros(Co, Ci, k, k, device=dev)

@@ -16,6 +16,8 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(PKG)
 BUILD = os.path.join(PKG, "_build")
 LIB_PATH = os.path.join(BUILD, "libvst_hip.so")
+# developer A/B runs only: load an alternative build (tools/build_variant.py) instead
+LIB_PATH = os.environ.get("VST_LIB_VARIANT", LIB_PATH)
 CSRC = os.path.join(PKG, "csrc")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
@@ -38,7 +40,7 @@ SIGNATURES = {
     "vst_weight_pack": (I, [P, P, I, I, I, I, I, I, I, P]),
     "vst_conv2d_fwd": (I, [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, P]),
     "vst_conv2d_tfwd": (I, [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, F, P]),
-    "vst_conv2d_wgrad_ws_bytes": (SZ, [I, I, I, I, I, I, I, I, I]),
+    "vst_conv2d_wgrad_ws_bytes": (SZ, [I, I, I, I, I, I, I, I, I, I]),
     "vst_conv2d_wgrad": (I, [P, P, P, P, SZ, I, I, I, I, I, I, I, I, I, I, I, I, I, I, L, L, I, P]),
     "vst_debug_set_tiles": (None, [I, I, I]),
     "vst_reflect_fold": (I, [P, P, P, I, I, I, I, I, P]),
@@ -69,21 +71,24 @@ def sources():
     return sorted(glob.glob(os.path.join(CSRC, "*.hip")))
 
 
-def build(force=False, verbose=False):
-    """Compile every HIP source into _build/libvst_hip.so for gfx950 (cross-compiles without a GPU)."""
-    os.makedirs(BUILD, exist_ok=True)
+def build(force=False, verbose=False, out=None, defines=()):
+    """Compile every HIP source into _build/libvst_hip.so for gfx950 (cross-compiles without a GPU).
+    out/defines: developer variant builds (tools/build_variant.py)."""
+    lib_path = out or os.path.join(BUILD, "libvst_hip.so")
+    objdir = os.path.join(os.path.dirname(lib_path), "obj_" + os.path.basename(lib_path)[:-3])
+    os.makedirs(objdir, exist_ok=True)
     srcs = sources()
     deps = srcs + glob.glob(os.path.join(CSRC, "*.h")) + [os.path.join(REPO, "include", "vst_hip.h")]
-    if not force and os.path.exists(LIB_PATH):
-        if os.path.getmtime(LIB_PATH) >= max(os.path.getmtime(d) for d in deps):
-            return LIB_PATH
+    if not force and os.path.exists(lib_path):
+        if os.path.getmtime(lib_path) >= max(os.path.getmtime(d) for d in deps):
+            return lib_path
     objs = []
     procs = []
     for s in srcs:
-        o = os.path.join(BUILD, os.path.basename(s) + ".o")
+        o = os.path.join(objdir, os.path.basename(s) + ".o")
         objs.append(o)
         cmd = [HIPCC, "-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-munsafe-fp-atomics",
-               "-Wall", "-Wno-unused-function", "-c", s, "-o", o]
+               "-Wall", "-Wno-unused-function"] + ["-D" + d for d in defines] + ["-c", s, "-o", o]
         procs.append((cmd, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
     for cmd, p in procs:
         out, _ = p.communicate()
@@ -91,13 +96,13 @@ def build(force=False, verbose=False):
             raise RuntimeError("hipcc failed: %s\n%s" % (" ".join(cmd), out.decode(errors="replace")))
         if verbose and out:
             print(out.decode(errors="replace"))
-    tmp = LIB_PATH + ".tmp"
+    tmp = lib_path + ".tmp"
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
     r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
     if r.returncode != 0:
         raise RuntimeError("link failed: %s\n%s" % (" ".join(cmd), r.stdout.decode(errors="replace")))
-    os.replace(tmp, LIB_PATH)
-    return LIB_PATH
+    os.replace(tmp, lib_path)
+    return lib_path
 
 
 def load():

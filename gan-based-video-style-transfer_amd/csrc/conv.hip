@@ -637,12 +637,49 @@ static TileKind pick_tile(long M, int Nc, int which) {
 struct WgradPlan {
   int Mw, nsplit, chunk;
   TileKind tile;
+  bool trans;        // channel-major operand copies + conv_wgrad_rk_k (stride 1, Wo % 4 == 0)
+  long xt_floats;    // workspace floats after the slabs: xt [Cx][N*H*W] then dyt [Cyp][P]
+  long dyt_floats;
 };
 
-static WgradPlan plan_wgrad(int N, int Ho, int Wo, int Cx, int Cyp, int R, int S) {
+// Split count whose grid fills its last "round" (slots co-resident blocks) best, among grids of
+// at least ~3/4 of a round (a 288-block grid on 256 CUs runs two rounds for 1.125 rounds of work).
+static int pick_splits(int tiles, int slots, int max_ns) {
+  if (max_ns < 1) max_ns = 1;
+  int ns = 1;
+  double best = -1.0;
+  for (int c = 1; c <= max_ns; ++c) {
+    const long blocks = (long)tiles * c;
+    const double fill = (double)blocks / (double)(((blocks + slots - 1) / slots) * slots);
+    const double score = blocks < (3 * slots) / 4 ? fill * blocks / slots : fill;
+    if (score > best + 1e-9) { best = score; ns = c; }
+    if (blocks >= 2 * slots) break;
+  }
+  return ns;
+}
+
+static WgradPlan plan_wgrad(int N, int H, int W, int Ho, int Wo, int Cx, int Cyp, int R, int S,
+                            int stride) {
   WgradPlan p;
   p.Mw = R * S * Cx;
+  p.trans = false;
+  p.xt_floats = p.dyt_floats = 0;
   const int P = N * Ho * Wo;
+  const int ov = g_tile_override[2];
+  if (Cyp > 4 && stride == 1 && Wo % 4 == 0 && ov < 8) {
+    p.trans = true;
+    int kind = (ov >= 0 && ov <= 6) ? ov : (Cyp <= 64 ? (p.Mw >= 1024 ? 2 : 3) : (p.Mw >= 1024 ? 0 : 1));
+    p.tile = (TileKind)kind;
+    int bm, bn, bk, slots;
+    rk_tile_geom(kind, &bm, &bn, &bk, &slots);
+    const int tiles = ceil_div(p.Mw, bm) * ceil_div(Cyp, bn);
+    const int ns = pick_splits(tiles, slots, ceil_div(P, 8 * bk) < 256 ? ceil_div(P, 8 * bk) : 256);
+    p.chunk = ceil_div(ceil_div(P, ns), bk) * bk;
+    p.nsplit = ceil_div(P, p.chunk);
+    p.xt_floats = rk_cp_ld((long)N * H * W) * Cx;
+    p.dyt_floats = rk_cp_ld(P) * Cyp;
+    return p;
+  }
   if (Cyp == 4) {  // VALU skinny path: one thread per (tap, 4 input channels) per split
     p.tile = T256x32;
     int ns = ceil_div(262144, p.Mw / 4);  // ~4 waves per SIMD
@@ -657,14 +694,11 @@ static WgradPlan plan_wgrad(int N, int Ho, int Wo, int Cx, int Cyp, int R, int S
   if (Cyp <= 32) p.tile = T256x32;
   else if (Cyp <= 64) p.tile = p.Mw >= 1024 ? T128x64 : T64x64;
   else p.tile = p.Mw >= 1024 ? T128x128w8 : T64x128;
-  if (g_tile_override[2] != TAUTO) p.tile = (TileKind)g_tile_override[2];
+  if (ov >= 0) p.tile = (TileKind)(ov >= 8 ? ov - 8 : ov);
   const int tiles = ceil_div(p.Mw, tile_bm(p.tile)) * ceil_div(Cyp, tile_bn(p.tile));
-  const int target = p.tile == T128x128w8 ? 256 : 512;  // ~one 8-wave / two 4-wave blocks per CU
-  int ns = ceil_div(target, tiles);
-  if (ns > 64) ns = 64;
+  // one 8-wave or two 4-wave blocks per CU form a round of 256 / 512 blocks
   const int max_ns = ceil_div(P, 8 * BK);  // at least 8 K-steps per split
-  if (ns > max_ns) ns = max_ns;
-  if (ns < 1) ns = 1;
+  const int ns = pick_splits(tiles, p.tile == T128x128w8 ? 256 : 512, max_ns < 64 ? max_ns : 64);
   p.chunk = ceil_div(ceil_div(P, ns), BK) * BK;
   p.nsplit = ceil_div(P, p.chunk);
   return p;
@@ -741,12 +775,14 @@ extern "C" int vst_conv2d_tfwd(const float* in, const float* wp, const float* bi
   return check_launch("conv2d_tfwd");
 }
 
+static size_t wgrad_ws_floats(const WgradPlan& p, int Cyp) {
+  return (size_t)p.nsplit * p.Mw * Cyp + p.xt_floats + p.dyt_floats;
+}
+
 extern "C" size_t vst_conv2d_wgrad_ws_bytes(int N, int H, int W, int Cx, int Ho, int Wo, int Cyp,
-                                            int R, int S) {
-  (void)H;
-  (void)W;
-  const WgradPlan p = plan_wgrad(N, Ho, Wo, Cx, Cyp, R, S);
-  return (size_t)p.nsplit * p.Mw * Cyp * sizeof(float);
+                                            int R, int S, int stride) {
+  const WgradPlan p = plan_wgrad(N, H, W, Ho, Wo, Cx, Cyp, R, S, stride);
+  return wgrad_ws_floats(p, Cyp) * sizeof(float);
 }
 
 extern "C" int vst_conv2d_wgrad(const float* x, const float* dy, float* dw, float* ws,
@@ -757,8 +793,8 @@ extern "C" int vst_conv2d_wgrad(const float* x, const float* dy, float* dw, floa
   VST_REQUIRE(Cx % 4 == 0 && Cyp % 4 == 0, "conv2d_wgrad: channel strides must be multiples of 4");
   VST_REQUIRE(Co <= Cyp && Ci <= Cx, "conv2d_wgrad: logical channels exceed strides");
   VST_REQUIRE(pad_mode == VST_PAD_ZERO || (pad < H && pad < W), "conv2d_wgrad: reflect pad >= size");
-  const WgradPlan p = plan_wgrad(N, Ho, Wo, Cx, Cyp, R, S);
-  VST_REQUIRE(ws_bytes >= (size_t)p.nsplit * p.Mw * Cyp * sizeof(float),
+  const WgradPlan p = plan_wgrad(N, H, W, Ho, Wo, Cx, Cyp, R, S, stride);
+  VST_REQUIRE(ws_bytes >= wgrad_ws_floats(p, Cyp) * sizeof(float),
               "conv2d_wgrad: workspace too small (%zu bytes)", ws_bytes);
   hipStream_t s = (hipStream_t)stream;
   const int P = N * Ho * Wo;
@@ -768,7 +804,14 @@ extern "C" int vst_conv2d_wgrad(const float* x, const float* dy, float* dw, floa
                      dim3(ceil_div(p.Mw, BM_), ceil_div(Cyp, BN_), p.nsplit),                        \
                      dim3(Tile<BM_, BN_, WM_, WN_>::NT), 0, s, x, dy, ws, H, W, Cx, Ho, Wo, Cyp, S,  \
                      stride, pad, refl, p.Mw, P, p.chunk)
-  if (Cyp == 4) {
+  if (p.trans) {
+    float* xt = ws + (size_t)p.nsplit * p.Mw * Cyp;
+    float* dyt = xt + p.xt_floats;
+    rk_nhwc_to_cp(x, xt, (long)N * H * W, Cx, s);
+    rk_nhwc_to_cp(dy, dyt, P, Cyp, s);
+    rk_wgrad_launch(xt, dyt, ws, N, H, W, Cx, Ho, Wo, Cyp, S, pad, refl, p.Mw, p.chunk, p.nsplit,
+                    (int)p.tile, s);
+  } else if (Cyp == 4) {
     int rc0 = skinny_wgrad_launch(x, dy, ws, H, W, Cx, Ho, Wo, S, stride, pad, refl, p.Mw, P, p.chunk,
                                   p.nsplit, s);
     if (rc0) return rc0;

@@ -7,7 +7,7 @@
 // then 4 consecutive floats of its row: one ds_read_b128 replaces four ds_read_b32, and both
 // operand tiles are written with ds_write_b128 straight from coalesced 128-byte global rows
 // (8 lanes x float4 per pixel row / weight row) — no transposing scalar LDS writes.  Row stride is
-// BK + 4 floats (144 B): the 16-lane groups of ds_read_b128 hit 16 distinct 16-byte bank slots.
+// BK + 4 floats (144 B at BK = 32): the 16-lane groups of ds_read_b128 hit 16 distinct 16-byte bank slots.
 //
 //   conv_fprop_rk_k : y = act(conv(x, w) + bias)   m = output pixel, n = out channel,
 //                     k = (r, s, ci); B operand = VST_PACK_OK pack [Co][R][S][Ci]
@@ -22,12 +22,19 @@
 namespace vst {
 namespace rk {
 
-constexpr int BK = 32;
-constexpr int LDK = BK + 4;
 constexpr int NOPOS = -(1 << 20);
+#ifndef VST_RK_PROBE
+#define VST_RK_PROBE 0  // developer probes: 1 = fprop without global loads, 2 = without MFMAs
+#endif
+#ifndef VST_RK_LG
+#define VST_RK_LG 4   // the next stage's global loads are spread over the first LG MFMA groups
+#endif
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, int BK_>
 struct Tile {
+  static constexpr int BK = BK_;
+  static constexpr int LDK = BK + 4;
+  static constexpr int KQ = BK / 4;              // lanes (float4s) per staged row
   static constexpr int NW = (BM / WM) * (BN / WN);
   static constexpr int NT = 64 * NW;
   static constexpr int WAVES_N = BN / WN;
@@ -36,7 +43,7 @@ struct Tile {
   static constexpr int A_ELEMS = BM * LDK;
   static constexpr int B_ELEMS = BN * LDK;
   static constexpr int STAGE = A_ELEMS + B_ELEMS;
-  static constexpr int ROWS_PER_PASS = NT / 8;   // 8 lanes x float4 cover one 32-deep row
+  static constexpr int ROWS_PER_PASS = NT / KQ;  // KQ lanes x float4 cover one BK-deep row
   static constexpr int A_LD = BM / ROWS_PER_PASS;
   static constexpr int B_LD = BN / ROWS_PER_PASS;
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
@@ -47,11 +54,12 @@ __device__ __forceinline__ float comp(const float4& v, int t) {
   return t == 0 ? v.x : (t == 1 ? v.y : (t == 2 ? v.z : v.w));
 }
 
-template <int BM, int BN, int WM, int WN, class Hook>
+template <int BM, int BN, int WM, int WN, int BK, class Hook>
 __device__ __forceinline__ void mma_stage(const float* __restrict__ As, const float* __restrict__ Bs,
                                           f32x16 (&acc)[WM / 32][WN / 32], int wm0, int wn0,
                                           int lane, Hook hook) {
-  using T = Tile<BM, BN, WM, WN>;
+  using T = Tile<BM, BN, WM, WN, BK>;
+  constexpr int LDK = T::LDK;
   const int kh = lane >> 5, li = lane & 31;
   const float* pa = As + (wm0 + li) * LDK + 4 * kh;
   const float* pb = Bs + (wn0 + li) * LDK + 4 * kh;
@@ -78,16 +86,21 @@ __device__ __forceinline__ void mma_stage(const float* __restrict__ As, const fl
       for (int i = 0; i < T::MI; ++i)
 #pragma unroll
         for (int j = 0; j < T::NI; ++j)
+#if VST_RK_PROBE == 2  // developer probe: LDS + global traffic without the MFMAs
+          acc[i][j][t] += comp(fa[cur][i], t) * comp(fb[cur][j], t);
+#else
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(comp(fa[cur][i], t), comp(fb[cur][j], t),
                                                            acc[i][j], 0, 0, 0);
+#endif
   }
 }
 
-template <int BM, int BN, int WM, int WN, int NLOAD, class LoadOne, class Adv, class Store>
+template <int BM, int BN, int WM, int WN, int BK, int NLOAD, class LoadOne, class Adv, class Store>
 __device__ __forceinline__ void main_loop(float* smem, int nk, f32x16 (&acc)[WM / 32][WN / 32],
                                           LoadOne load_one, Adv adv, Store store) {
-  using T = Tile<BM, BN, WM, WN>;
-  constexpr int PER = (NLOAD + BK / 8 - 1) / (BK / 8);
+  using T = Tile<BM, BN, WM, WN, BK>;
+  constexpr int LG = VST_RK_LG < BK / 8 ? VST_RK_LG : BK / 8;
+  constexpr int PER = (NLOAD + LG - 1) / LG;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int wm0 = (wave / T::WAVES_N) * WM, wn0 = (wave % T::WAVES_N) * WN;
   if (nk > 0) {
@@ -101,7 +114,7 @@ __device__ __forceinline__ void main_loop(float* smem, int nk, f32x16 (&acc)[WM 
     const bool next = kt + 1 < nk;
     if (next) adv();
     const int k0n = (kt + 1) * BK;
-    mma_stage<BM, BN, WM, WN>(cur, cur + T::A_ELEMS, acc, wm0, wn0, lane, [&](int g) {
+    mma_stage<BM, BN, WM, WN, BK>(cur, cur + T::A_ELEMS, acc, wm0, wn0, lane, [&](int g) {
       if (next) {
 #pragma unroll
         for (int u = 0; u < PER; ++u)
@@ -129,18 +142,18 @@ __device__ __forceinline__ void zero_acc(f32x16 (&acc)[MI][NI]) {
 }
 
 // ------------------------------------------------------------------------------------------ fprop
-template <int BM, int BN, int WM, int WN>
-__global__ __launch_bounds__((Tile<BM, BN, WM, WN>::NT), 2) void conv_fprop_rk_k(
+template <int BM, int BN, int WM, int WN, int BK>
+__global__ __launch_bounds__((Tile<BM, BN, WM, WN, BK>::NT), 2) void conv_fprop_rk_k(
     const float* __restrict__ x, const float* __restrict__ wp, const float* __restrict__ bias,
     float* __restrict__ y, int H, int W, int C, int Ho, int Wo, int Cop, int S, int st, int pad,
     int reflect, int act, float slope, int M, int Ktot) {
-  using T = Tile<BM, BN, WM, WN>;
-  constexpr int NT = T::NT, A_LD = T::A_LD, B_LD = T::B_LD, RP = T::ROWS_PER_PASS;
+  using T = Tile<BM, BN, WM, WN, BK>;
+  constexpr int NT = T::NT, A_LD = T::A_LD, B_LD = T::B_LD, RP = T::ROWS_PER_PASS, LDK = T::LDK;
   __shared__ __attribute__((aligned(16))) float smem[2 * T::STAGE];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int mt = remap_mtile(blockIdx.x, gridDim.x);
   const int m0 = mt * BM, n0 = blockIdx.y * BN;
-  const int kq = t & 7, rb = t >> 3;
+  const int kq = t % T::KQ, rb = t / T::KQ;
 
   // k state (one per thread: every row this thread stages uses the same k position)
   int kc = (4 * kq) % C, ks, kr;
@@ -176,6 +189,11 @@ __global__ __launch_bounds__((Tile<BM, BN, WM, WN>::NT), 2) void conv_fprop_rk_k
   float4 ra[A_LD], rbv[B_LD];
   int kcur = 4 * kq;  // absolute k of this thread's float4 in the stage being loaded
   auto load_one = [&](int i, int) {
+#if VST_RK_PROBE == 1
+    if (i < A_LD) ra[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    else rbv[i - A_LD] = make_float4(0.f, 0.f, 0.f, 0.f);
+    return;
+#endif
     if (i < A_LD) {
       const int j = i;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -216,7 +234,7 @@ __global__ __launch_bounds__((Tile<BM, BN, WM, WN>::NT), 2) void conv_fprop_rk_k
 
   f32x16 acc[T::MI][T::NI];
   zero_acc(acc);
-  main_loop<BM, BN, WM, WN, A_LD + B_LD>(smem, (Ktot + BK - 1) / BK, acc, load_one, adv, store);
+  main_loop<BM, BN, WM, WN, BK, A_LD + B_LD>(smem, (Ktot + BK - 1) / BK, acc, load_one, adv, store);
   (void)NT;
 
   const int wm0 = (wave / T::WAVES_N) * WM, wn0 = (wave % T::WAVES_N) * WN;
@@ -236,13 +254,13 @@ __global__ __launch_bounds__((Tile<BM, BN, WM, WN>::NT), 2) void conv_fprop_rk_k
 }
 
 // ------------------------------------------------------------------- transposed conv / dgrad
-template <int BM, int BN, int WM, int WN, int ST>
-__global__ __launch_bounds__((Tile<BM, BN, WM, WN>::NT), 2) void conv_tconv_rk_k(
+template <int BM, int BN, int WM, int WN, int BK, int ST>
+__global__ __launch_bounds__((Tile<BM, BN, WM, WN, BK>::NT), 2) void conv_tconv_rk_k(
     const float* __restrict__ in, const float* __restrict__ wp, const float* __restrict__ bias,
     const float* __restrict__ addend, float* __restrict__ out, int Hi, int Wi, int Cy, int Ho,
     int Wo, int Cx, int R, int S, int st_rt, int pad, int reflect, int act, float slope, int Nimg) {
-  using T = Tile<BM, BN, WM, WN>;
-  constexpr int A_LD = T::A_LD, B_LD = T::B_LD, RP = T::ROWS_PER_PASS;
+  using T = Tile<BM, BN, WM, WN, BK>;
+  constexpr int A_LD = T::A_LD, B_LD = T::B_LD, RP = T::ROWS_PER_PASS, LDK = T::LDK;
   __shared__ __attribute__((aligned(16))) float smem[2 * T::STAGE];
   const int st = ST > 0 ? ST : st_rt;
   const int ca = blockIdx.z / st, cb = blockIdx.z % st;
@@ -258,7 +276,7 @@ __global__ __launch_bounds__((Tile<BM, BN, WM, WN>::NT), 2) void conv_tconv_rk_k
   const int Ktot = nr * ns * Cy;
 
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int kq = t & 7, rb = t >> 3;
+  const int kq = t % T::KQ, rb = t / T::KQ;
   int kc = ns > 0 ? (4 * kq) % Cy : 0, kis, kir;
   {
     const int tp = Cy > 0 ? (4 * kq) / Cy : 0;
@@ -347,7 +365,7 @@ __global__ __launch_bounds__((Tile<BM, BN, WM, WN>::NT), 2) void conv_tconv_rk_k
 
   f32x16 acc[T::MI][T::NI];
   zero_acc(acc);
-  main_loop<BM, BN, WM, WN, A_LD + B_LD>(smem, (Ktot + BK - 1) / BK, acc, load_one, adv, store);
+  main_loop<BM, BN, WM, WN, BK, A_LD + B_LD>(smem, (Ktot + BK - 1) / BK, acc, load_one, adv, store);
 
   const int wm0 = (wave / T::WAVES_N) * WM, wn0 = (wave % T::WAVES_N) * WN;
   const int hw = Hc * Wc;
@@ -371,11 +389,184 @@ __global__ __launch_bounds__((Tile<BM, BN, WM, WN>::NT), 2) void conv_tconv_rk_k
     }
 }
 
+// ------------------------------------------------------------------ weight gradient, stride 1
+// dW[m = (r, s, ci)][co] = sum_p X[shift_rs(p)][ci] * dY[p][co] with both operands read from
+// channel-major copies (xt = [Cx][N][H][W], dyt = [Cyp][N*Ho*Wo], made by nhwc_to_cp_k), so every
+// GEMM row is contiguous along the reduction (pixel) axis and stages into the row-major [row][k]
+// LDS image with ds_write_b128 exactly like the forward kernel.  For stride 1 the 4 pixels of a
+// float4 are 4 consecutive input columns: one (unaligned) 16-byte load unless the window crosses
+// the image border, where the 4 taps are reflected / zeroed one by one.  blockIdx.z = K split;
+// partial tiles land in slab[z][m][Cyp] (summed and transposed into dw by conv.hip).
+template <int BM, int BN, int WM, int WN, int BK>
+__global__ __launch_bounds__((Tile<BM, BN, WM, WN, BK>::NT), 2) void conv_wgrad_rk_k(
+    const float* __restrict__ xt, const float* __restrict__ dyt, float* __restrict__ slab, int H,
+    int W, int Cx, int Ho, int Wo, int Cyp, int S, int pad, int reflect, int Mw, int P, int chunk,
+    long ldx, long ldy) {
+  using T = Tile<BM, BN, WM, WN, BK>;
+  constexpr int A_LD = T::A_LD, B_LD = T::B_LD, RP = T::ROWS_PER_PASS, LDK = T::LDK;
+  typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
+  __shared__ __attribute__((aligned(16))) float smem[2 * T::STAGE];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int pbeg = blockIdx.z * chunk;
+  const int pend = min(P, pbeg + chunk);
+  const int kq = t % T::KQ, rb = t / T::KQ;
+  const long HW = (long)H * W;
+
+  int ar[A_LD], as[A_LD];
+  const float* xrow[A_LD];
+  bool mv[A_LD];
+#pragma unroll
+  for (int j = 0; j < A_LD; ++j) {
+    const int m = m0 + rb + RP * j;
+    mv[j] = m < Mw;
+    const int mm = mv[j] ? m : 0;
+    const int tap = mm / Cx, ci = mm - tap * Cx;
+    const int r = tap / S, s = tap - r * S;
+    ar[j] = r - pad;
+    as[j] = s - pad;
+    xrow[j] = xt + (long)ci * ldx;
+  }
+  const float* dyrow[B_LD];
+  bool nv[B_LD];
+#pragma unroll
+  for (int j = 0; j < B_LD; ++j) {
+    const int n = n0 + rb + RP * j;
+    nv[j] = n < Cyp;
+    dyrow[j] = dyt + (long)(nv[j] ? n : 0) * ldy;
+  }
+  // pixel state of this thread's float4 (shared by all its rows)
+  int kp = pbeg + 4 * kq, pn, pho, pwo;
+  {
+    const int hw = Ho * Wo;
+    pn = kp / hw;
+    const int rem = kp - pn * hw;
+    pho = rem / Wo;
+    pwo = rem - pho * Wo;
+  }
+  float4 ra[A_LD], rbv[B_LD];
+  auto load_one = [&](int i, int) {
+    if (i < A_LD) {
+      const int j = i;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (mv[j] && kp < pend) {
+        int hi = pho + ar[j];
+        const int wi = pwo + as[j];
+        bool hok = true;
+        if (reflect) hi = reflect_idx(hi, H);
+        else hok = (unsigned)hi < (unsigned)H;
+        if (hok) {
+          const float* rowp = xrow[j] + pn * HW + (long)hi * W;
+          if (wi >= 0 && wi + 3 < W) {
+            const f4u u = *reinterpret_cast<const f4u*>(rowp + wi);
+            v = make_float4(u.x, u.y, u.z, u.w);
+          } else {
+            float e[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              int wq = wi + q;
+              bool ok = true;
+              if (reflect) wq = reflect_idx(wq, W);
+              else ok = (unsigned)wq < (unsigned)W;
+              e[q] = ok ? rowp[wq] : 0.f;
+            }
+            v = make_float4(e[0], e[1], e[2], e[3]);
+          }
+        }
+      }
+      ra[j] = v;
+    } else {
+      const int j = i - A_LD;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (nv[j] && kp < pend) v = *reinterpret_cast<const float4*>(dyrow[j] + kp);
+      rbv[j] = v;
+    }
+  };
+  auto adv = [&]() {
+    kp += BK;
+    pwo += BK;
+    while (pwo >= Wo) {
+      pwo -= Wo;
+      if (++pho == Ho) { pho = 0; ++pn; }
+    }
+  };
+  auto store = [&](float* As) {
+    float* Bs = As + T::A_ELEMS;
+#pragma unroll
+    for (int j = 0; j < A_LD; ++j) *reinterpret_cast<float4*>(As + (rb + RP * j) * LDK + 4 * kq) = ra[j];
+#pragma unroll
+    for (int j = 0; j < B_LD; ++j) *reinterpret_cast<float4*>(Bs + (rb + RP * j) * LDK + 4 * kq) = rbv[j];
+  };
+
+  f32x16 acc[T::MI][T::NI];
+  zero_acc(acc);
+  const int nk = pend > pbeg ? (pend - pbeg + BK - 1) / BK : 0;
+  main_loop<BM, BN, WM, WN, BK, A_LD + B_LD>(smem, nk, acc, load_one, adv, store);
+
+  const int wm0 = (wave / T::WAVES_N) * WM, wn0 = (wave % T::WAVES_N) * WN;
+  float* sl = slab + (long)blockIdx.z * Mw * Cyp;
+#pragma unroll
+  for (int i = 0; i < T::MI; ++i)
+#pragma unroll
+    for (int j = 0; j < T::NI; ++j) {
+      const int n = n0 + wn0 + 32 * j + (lane & 31);
+      if (n >= Cyp) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int mm = m0 + wm0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (mm < Mw) sl[(long)mm * Cyp + n] = acc[i][j][r];
+      }
+    }
+}
+
+// NHWC [P][Cs] -> channel-major [Cs][ld] through a 64x64 LDS tile (float4 reads and writes).
+__global__ __launch_bounds__(256) void nhwc_to_cp_k(const float* __restrict__ x, float* __restrict__ y,
+                                                    long P, int Cs, long ld) {
+  __shared__ float tile[64][65];
+  const long p0 = (long)blockIdx.x * 64;
+  const int c0 = blockIdx.y * 64;
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int idx = t + 256 * it, pr = idx >> 4, c4 = (idx & 15) * 4;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (p0 + pr < P && c0 + c4 < Cs) v = *reinterpret_cast<const float4*>(x + (p0 + pr) * Cs + c0 + c4);
+    tile[pr][c4] = v.x;
+    tile[pr][c4 + 1] = v.y;
+    tile[pr][c4 + 2] = v.z;
+    tile[pr][c4 + 3] = v.w;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int idx = t + 256 * it, cr = idx >> 4, p4 = (idx & 15) * 4;
+    if (c0 + cr >= Cs || p0 + p4 >= P) continue;
+    float* dst = y + (long)(c0 + cr) * ld + p0 + p4;
+    if (p0 + p4 + 3 < P && (ld & 3) == 0) {
+      *reinterpret_cast<float4*>(dst) =
+          make_float4(tile[p4][cr], tile[p4 + 1][cr], tile[p4 + 2][cr], tile[p4 + 3][cr]);
+    } else {  // ragged plane length (P % 4 != 0): element stores, never past the plane
+      for (int e = 0; e < 4 && p0 + p4 + e < P; ++e) dst[e] = tile[p4 + e][cr];
+    }
+  }
+}
+
 }  // namespace rk
 
-// Tile kinds: 0 = 128x128 (8 waves, 64x32 each), 1 = 64x128, 2 = 128x64, 3 = 64x64 (4 waves)
+// Plane stride of a channel-major copy: a multiple of 4 floats that is NOT a multiple of a large
+// power of two (P = 65536 would put all 128 rows of a tile on one L2 channel).
+long rk_cp_ld(long P) { return (P + 63) / 64 * 64 + 64; }
+
+void rk_nhwc_to_cp(const float* x, float* y, long P, int Cs, hipStream_t s) {
+  hipLaunchKernelGGL(rk::nhwc_to_cp_k, dim3((unsigned)((P + 63) / 64), ceil_div(Cs, 64)), dim3(256), 0,
+                     s, x, y, P, Cs, rk_cp_ld(P));
+}
+
+// Tile kinds: 0 = 128x128 (8 waves, 64x32 each), 1 = 64x128, 2 = 128x64, 3 = 64x64 (4 waves),
+// all 32-deep K-steps; 4 = 128x128 with 64-deep K-steps (139 KB LDS, one block per CU);
+// 5 / 6 = 128x128 with 4 waves of 64x64 (4 accumulators per wave), 32- / 64-deep K-steps
 int rk_pick(long M, int Nc, int override_kind) {
-  if (override_kind >= 0 && override_kind <= 3) return override_kind;
+  if (override_kind >= 0 && override_kind <= 6) return override_kind;
   if (Nc <= 64) return M / 128 >= 256 ? 2 : 3;
   const long n128 = (Nc + 127) / 128;
   if ((M / 128) * n128 >= 200) return 0;
@@ -383,21 +574,32 @@ int rk_pick(long M, int Nc, int override_kind) {
   return 3;
 }
 
+void rk_tile_geom(int kind, int* bm, int* bn, int* bk, int* slots) {
+  *bm = (kind == 1 || kind == 3) ? 64 : 128;
+  *bn = (kind == 2 || kind == 3) ? 64 : 128;
+  *bk = (kind == 4 || kind == 6) ? 64 : 32;
+  *slots = (kind == 0 || kind == 4 || kind == 6) ? 256 : 512;  // co-resident blocks per round
+}
+
 #define VST_RK_DISPATCH(kind, LAUNCH)            \
   switch (kind) {                                 \
-    case 0: LAUNCH(128, 128, 64, 32); break;      \
-    case 1: LAUNCH(64, 128, 32, 64); break;       \
-    case 2: LAUNCH(128, 64, 64, 32); break;       \
-    default: LAUNCH(64, 64, 32, 32); break;       \
+    case 0: LAUNCH(128, 128, 64, 32, 32); break;  \
+    case 1: LAUNCH(64, 128, 32, 64, 32); break;   \
+    case 2: LAUNCH(128, 64, 64, 32, 32); break;   \
+    case 4: LAUNCH(128, 128, 64, 32, 64); break;  \
+    case 5: LAUNCH(128, 128, 64, 64, 32); break;  \
+    case 6: LAUNCH(128, 128, 64, 64, 64); break;  \
+    default: LAUNCH(64, 64, 32, 32, 32); break;   \
   }
 
 void rk_fprop_launch(const float* x, const float* wp, const float* bias, float* y, int N, int H, int W,
                      int C, int Ho, int Wo, int Cop, int R, int S, int st, int pad, int reflect, int act,
                      float slope, int kind, hipStream_t s) {
   const int M = N * Ho * Wo, K = R * S * C;
-#define VST_L(BM_, BN_, WM_, WN_)                                                                  \
-  hipLaunchKernelGGL((rk::conv_fprop_rk_k<BM_, BN_, WM_, WN_>),                                      \
-                     dim3(ceil_div(M, BM_), ceil_div(Cop, BN_)), dim3(rk::Tile<BM_, BN_, WM_, WN_>::NT), \
+#define VST_L(BM_, BN_, WM_, WN_, BK_)                                                             \
+  hipLaunchKernelGGL((rk::conv_fprop_rk_k<BM_, BN_, WM_, WN_, BK_>),                                 \
+                     dim3(ceil_div(M, BM_), ceil_div(Cop, BN_)),                                     \
+                     dim3(rk::Tile<BM_, BN_, WM_, WN_, BK_>::NT),                                    \
                      0, s, x, wp, bias, y, H, W, C, Ho, Wo, Cop, S, st, pad, reflect, act, slope, M, K)
   VST_RK_DISPATCH(rk_pick(M, Cop, kind), VST_L)
 #undef VST_L
@@ -408,18 +610,31 @@ void rk_tconv_launch(const float* in, const float* wp, const float* bias, const 
                      int st, int pad, int reflect, int act, float slope, int kind, hipStream_t s) {
   const int Hc = (Ho + st - 1) / st, Wc = (Wo + st - 1) / st;
   const int Mmax = N * Hc * Wc;
-#define VST_LST(BM_, BN_, WM_, WN_, ST_)                                                           \
-  hipLaunchKernelGGL((rk::conv_tconv_rk_k<BM_, BN_, WM_, WN_, ST_>),                                 \
+#define VST_LST(BM_, BN_, WM_, WN_, BK_, ST_)                                                      \
+  hipLaunchKernelGGL((rk::conv_tconv_rk_k<BM_, BN_, WM_, WN_, BK_, ST_>),                            \
                      dim3(ceil_div(Mmax, BM_), ceil_div(Cx, BN_), st * st),                          \
-                     dim3(rk::Tile<BM_, BN_, WM_, WN_>::NT), 0, s, in, wp, bias, addend, out, Hi, Wi, \
+                     dim3(rk::Tile<BM_, BN_, WM_, WN_, BK_>::NT), 0, s, in, wp, bias, addend, out, Hi, Wi, \
                      Cy, Ho, Wo, Cx, R, S, st, pad, reflect, act, slope, N)
-#define VST_L(BM_, BN_, WM_, WN_)                   \
-  if (st == 1) VST_LST(BM_, BN_, WM_, WN_, 1);       \
-  else if (st == 2) VST_LST(BM_, BN_, WM_, WN_, 2);  \
-  else VST_LST(BM_, BN_, WM_, WN_, 0);
+#define VST_L(BM_, BN_, WM_, WN_, BK_)                   \
+  if (st == 1) VST_LST(BM_, BN_, WM_, WN_, BK_, 1);       \
+  else if (st == 2) VST_LST(BM_, BN_, WM_, WN_, BK_, 2);  \
+  else VST_LST(BM_, BN_, WM_, WN_, BK_, 0);
   VST_RK_DISPATCH(rk_pick((long)Mmax * st * st, Cx, kind), VST_L)
 #undef VST_L
 #undef VST_LST
+}
+
+void rk_wgrad_launch(const float* xt, const float* dyt, float* slab, int N, int H, int W, int Cx,
+                     int Ho, int Wo, int Cyp, int S, int pad, int reflect, int Mw, int chunk,
+                     int nsplit, int kind, hipStream_t s) {
+  const int P = N * Ho * Wo;
+#define VST_L(BM_, BN_, WM_, WN_, BK_)                                                             \
+  hipLaunchKernelGGL((rk::conv_wgrad_rk_k<BM_, BN_, WM_, WN_, BK_>),                                 \
+                     dim3(ceil_div(Mw, BM_), ceil_div(Cyp, BN_), nsplit),                            \
+                     dim3(rk::Tile<BM_, BN_, WM_, WN_, BK_>::NT), 0, s, xt, dyt, slab, H, W, Cx, Ho, \
+                     Wo, Cyp, S, pad, reflect, Mw, P, chunk, rk_cp_ld((long)N * H * W), rk_cp_ld(P))
+  VST_RK_DISPATCH(kind, VST_L)
+#undef VST_L
 }
 
 }  // namespace vst

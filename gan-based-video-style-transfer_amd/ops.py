@@ -109,7 +109,7 @@ def conv2d_wgrad(x, dy, dw, db, R, S, stride, pad, pad_mode, co, ci, so, si, acc
     _dev_check(x, dy)
     N, H, W, Cx = x.shape
     _, Ho, Wo, Cyp = dy.shape
-    nbytes = lib().vst_conv2d_wgrad_ws_bytes(N, H, W, Cx, Ho, Wo, Cyp, R, S)
+    nbytes = lib().vst_conv2d_wgrad_ws_bytes(N, H, W, Cx, Ho, Wo, Cyp, R, S, stride)
     ws = torch.empty((nbytes + 3) // 4, device=x.device)
     _call("vst_conv2d_wgrad", _p(x), _p(dy), _p(dw), _p(ws), nbytes, N, H, W, Cx, Ho, Wo,
           Cyp, R, S, stride, pad, PAD[pad_mode], co, ci, so, si, 1 if accumulate else 0, _stream())

@@ -54,24 +54,26 @@ int vst_version(void);
 int vst_nchw_to_nhwc(const float* x, float* y, int N, int C, int H, int W, int Cs, void* stream);
 int vst_nhwc_to_nchw(const float* x, float* y, int N, int C, int H, int W, int Cs, void* stream);
 /* Pack a PyTorch conv weight w[O][I][R][S] (ConvTranspose: pass Ci as O) for the GEMM kernels.
- * mode VST_PACK_KC -> out[R][S][Ip][Op]; VST_PACK_CK -> out[R][S][Op][Ip]; Ip/Op are the padded
- * channel strides (multiples of 4, zero filled). */
+ * mode VST_PACK_KC -> out[R][S][Ip][Op]; VST_PACK_CK -> out[R][S][Op][Ip];
+ * VST_PACK_OK -> out[Op][R][S][Ip] (consumed by vst_conv2d_fwd);
+ * VST_PACK_IK -> out[Ip][R][S][Op] (consumed by vst_conv2d_tfwd).
+ * Ip/Op are the padded channel strides (multiples of 4, zero filled). */
 int vst_weight_pack(const float* w, float* out, int O, int I, int R, int S, int Op, int Ip,
                     int mode, void* stream);
 
 /* ---- convolution (implicit GEMM on fp32 MFMA) -------------------------------------------- */
-/* y[N][Ho][Wo][Cop] = act(conv(x[N][H][W][Cx], w) + bias).  wp = VST_PACK_KC pack
- * ([R][S][Cx][Cop]); bias has Cop entries or is NULL.  pad_mode VST_PAD_ZERO / VST_PAD_REFLECT.
+/* y[N][Ho][Wo][Cop] = act(conv(x[N][H][W][Cx], w) + bias).  wp = VST_PACK_OK pack
+ * ([Cop][R][S][Cx]); bias has Cop entries or is NULL.  pad_mode VST_PAD_ZERO / VST_PAD_REFLECT.
  * Ho = (H + 2*pad - R)/stride + 1. */
 int vst_conv2d_fwd(const float* x, const float* wp, const float* bias, float* y,
                    int N, int H, int W, int Cx, int Cop, int R, int S, int stride, int pad,
                    int pad_mode, int act, float slope, void* stream);
 /* Transposed convolution / conv data-gradient (gather form, split by output parity class):
  *   out[n][h][w][cx] = sum_{r,s,cy : h = ho*stride - pad + r, w = wo*stride - pad + s}
- *                        in[n][ho][wo][cy] * wp[r][s][cy][cx]        (+ bias[cx], act)
+ *                        in[n][ho][wo][cy] * w[cy][cx][r][s]        (+ bias[cx], act)
  * in is [N][Hi][Wi][Cy]; out is [N][Ho][Wo][Cx] (Ho/Wo given: (Hi-1)*stride - 2*pad + R + output_padding).
- * For ConvTranspose2d forward pass wp = VST_PACK_CK pack of Wt seen as [Ci][Co] (i.e. O=Ci, I=Co)
- * -> rows (r,s,ci) cols co; for the dgrad of a Conv2d pass its VST_PACK_CK pack. */
+ * wp = VST_PACK_IK pack ([Cx][R][S][Cy]): for ConvTranspose2d forward pack Wt seen as O=Ci, I=Co;
+ * for the dgrad of a Conv2d pass the IK pack of its weight. */
 /* pad_mode VST_PAD_REFLECT (stride 1 only) gives the data-gradient of a ReflectionPad2d(pad) +
  * valid conv directly: the mirrored contributions are gathered in-kernel (no padded buffer/fold).
  * addend (NULL or [N][Ho][Wo][Cx]) is added after bias/act (fused residual gradient). */
@@ -85,12 +87,16 @@ int vst_conv2d_tfwd(const float* in, const float* wp, const float* bias, const f
  * weight gradient of the equivalent conv x_T = conv(dy_T, .): call with x := grad of the convT
  * output, dy := convT input, (Co, Ci) := (Ci_T, Co_T), db := NULL (use vst_channel_sum).  accumulate != 0 adds into dw/db.  Split-K partial slabs go to
  * ws (vst_conv2d_wgrad_ws_bytes bytes) and are reduced in a fixed order (deterministic). */
-size_t vst_conv2d_wgrad_ws_bytes(int N, int H, int W, int Cx, int Ho, int Wo, int Cyp, int R, int S);
+size_t vst_conv2d_wgrad_ws_bytes(int N, int H, int W, int Cx, int Ho, int Wo, int Cyp, int R, int S,
+                                 int stride);
 int vst_conv2d_wgrad(const float* x, const float* dy, float* dw, float* ws, size_t ws_bytes, int N,
                      int H, int W, int Cx, int Ho, int Wo, int Cyp, int R, int S, int stride,
                      int pad, int pad_mode, int Co, int Ci, long so, long si, int accumulate,
                      void* stream);
-/* Debug/benchmark only: force the GEMM tile of fprop / tconv / wgrad (-1 = automatic). */
+/* Debug/benchmark only: force the GEMM tile of fprop / tconv / wgrad (-1 = automatic).
+ * fprop/tconv: 0 = 128x128 (8 waves), 1 = 64x128, 2 = 128x64, 3 = 64x64, 4 = 128x128 64-deep K.
+ * wgrad: the same kinds 0..4 on the channel-major (stride-1) path; 8 + k forces the k-major
+ * legacy wgrad kernel with tile k (0..3, 4 = 256x32). */
 void vst_debug_set_tiles(int fprop, int tconv, int wgrad);
 /* db[c] (+)= sum over NHW pixels of x[p][c] for c < Cl (channel stride Cs); bias gradient of a layer
  * whose output gradient is x.  ws: vst_channel_sum_ws_bytes bytes; fixed-order (deterministic). */

@@ -53,11 +53,30 @@ CONV_CASES = [
     ("D_4x4_s1", 2, 32, 9, 11, 64, 4, 1, 1, "zero"),
     ("D_head_1", 2, 64, 7, 7, 1, 4, 1, 1, "zero"),
     ("odd_big_M", 3, 8, 37, 29, 72, 3, 1, 1, "zero"),
+    # W_out % 4 == 0 stride-1 shapes take the channel-major wgrad path
+    ("c7s1_reflect_w4", 2, 3, 20, 16, 16, 7, 1, 3, "reflect"),
+    ("res_reflect_w8", 2, 32, 12, 8, 32, 3, 1, 1, "reflect"),
+    ("D_4x4_s1_w12", 2, 32, 9, 13, 64, 4, 1, 1, "zero"),
+    ("res_wide_w4", 2, 256, 6, 4, 136, 3, 1, 1, "reflect"),
 ]
 
 
+# forced GEMM tile kinds (fprop/tconv rk kind, -, wgrad kind): every tiling the planners may pick
+TILE_SETS = {"auto": (-1, -1, -1), "t128k64": (4, 4, 4), "t64x128": (1, 1, 1), "t64x64": (3, 3, 3),
+             "t128x128": (0, 0, 0), "legacy_wgrad": (-1, -1, 8), "legacy_wgrad64": (-1, -1, 11)}
+
+
+@pytest.mark.parametrize("tiles", list(TILE_SETS), ids=list(TILE_SETS))
 @pytest.mark.parametrize("case", CONV_CASES, ids=[c[0] for c in CONV_CASES])
-def test_conv_fwd_dgrad_wgrad(ops, case):
+def test_conv_fwd_dgrad_wgrad(ops, case, tiles):
+    ops.debug_set_tiles(*TILE_SETS[tiles])
+    try:
+        _conv_case(ops, case)
+    finally:
+        ops.debug_set_tiles(-1, -1, -1)
+
+
+def _conv_case(ops, case):
     name, N, Ci, H, W, Co, k, st, pad, mode = case
     x = _g(1, (N, Ci, H, W))
     w = _g(2, (Co, Ci, k, k), 0.1)

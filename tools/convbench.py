@@ -13,11 +13,16 @@ from gbvst import ops  # noqa: E402
 gbvst._lib.load()
 dev = torch.device("cuda")
 B = int(os.environ.get("B", "4"))
-TILES = {"auto": -1, "128x128w8": 0, "64x128": 1, "128x64": 2, "64x64": 3}
+# name -> (fprop/tconv rk kind, wgrad TileKind)
+TILES = {"auto": (-1, -1), "128x128w8": (0, 0), "64x128": (1, 1), "128x64": (2, 2), "64x64": (3, 3),
+         "128x128k64": (4, 4), "legacy": (-1, 8), "128x128w4": (5, 5), "128x128w4k64": (6, 6)}
+if os.environ.get("TILES"):
+    TILES = {k: v for k, v in TILES.items() if k in os.environ["TILES"].split(",")}
+ONLY = os.environ.get("LAYERS")
 
 
-def timeit(fn, reps=10):
-    for _ in range(2):
+def timeit(fn, reps=20):
+    for _ in range(3):
         fn()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
@@ -38,7 +43,12 @@ LAYERS = [
     ("D4", 256, 32, 512, 4, 1, 1, "zero"),
 ]
 res = []
+_w = torch.randn(4096, 4096, device=dev)
+for _ in range(50):
+    _w @ _w  # clock ramp
 for name, Ci, H, Co, k, st, pad, mode in LAYERS:
+    if ONLY and name not in ONLY.split(","):
+        continue
     x = torch.randn(B, H, H, Ci, device=dev)
     w = torch.randn(Co, Ci, k, k, device=dev) * 0.02
     kc, ck = ops.weight_pack(w, ops.PACK_FWD), ops.weight_pack(w, ops.PACK_DGRAD)
@@ -47,7 +57,7 @@ for name, Ci, H, Co, k, st, pad, mode in LAYERS:
     dw = torch.zeros(Co, Ci, k, k, device=dev)
     flop = 2.0 * B * Ho * Ho * Co * Ci * k * k
     for tname, tv in TILES.items():
-        ops.debug_set_tiles(tv, tv, tv)
+        ops.debug_set_tiles(tv[0], tv[0], tv[1])
         try:
             tf = timeit(lambda: ops.conv2d_fwd(x, kc, None, Co, k, k, st, pad, mode))
             tt = timeit(lambda: ops.conv2d_tfwd(gy, ck, None, H, H, Ci, k, k, st, pad, pad_mode=mode))

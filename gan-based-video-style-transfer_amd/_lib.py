@@ -23,6 +23,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
 _lib = None
+MATH_MODES = {"fp32": 0, "bf16x3": 1, "bf16x6": 2}  # VST_MATH_* (include/vst_hip.h)
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -38,10 +39,10 @@ SIGNATURES = {
     "vst_nchw_to_nhwc": (I, [P, P, I, I, I, I, I, P]),
     "vst_nhwc_to_nchw": (I, [P, P, I, I, I, I, I, P]),
     "vst_weight_pack": (I, [P, P, I, I, I, I, I, I, I, P]),
-    "vst_conv2d_fwd": (I, [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, P]),
-    "vst_conv2d_tfwd": (I, [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, F, P]),
+    "vst_conv2d_fwd": (I, [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, I, P]),
+    "vst_conv2d_tfwd": (I, [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, F, I, P]),
     "vst_conv2d_wgrad_ws_bytes": (SZ, [I, I, I, I, I, I, I, I, I, I]),
-    "vst_conv2d_wgrad": (I, [P, P, P, P, SZ, I, I, I, I, I, I, I, I, I, I, I, I, I, I, L, L, I, P]),
+    "vst_conv2d_wgrad": (I, [P, P, P, P, SZ, I, I, I, I, I, I, I, I, I, I, I, I, I, I, L, L, I, I, P]),
     "vst_debug_set_tiles": (None, [I, I, I]),
     "vst_reflect_fold": (I, [P, P, P, I, I, I, I, I, P]),
     "vst_channel_sum_ws_bytes": (SZ, [L, I]),

@@ -78,16 +78,18 @@ int skinny_out_launch(int mode, const float* in, const float* wp, const float* b
 // [row][k]-LDS implicit-GEMM fprop / transposed conv (conv_rk.hip); kind = tile override or -1
 void rk_fprop_launch(const float* x, const float* wp, const float* bias, float* y, int N, int H, int W,
                      int C, int Ho, int Wo, int Cop, int R, int S, int st, int pad, int reflect, int act,
-                     float slope, int kind, hipStream_t s);
+                     float slope, int kind, int math, hipStream_t s);
 long rk_cp_ld(long P);
+
 void rk_tile_geom(int kind, int* bm, int* bn, int* bk, int* slots);
 void rk_nhwc_to_cp(const float* x, float* y, long P, int Cs, hipStream_t s);
 void rk_wgrad_launch(const float* xt, const float* dyt, float* slab, int N, int H, int W, int Cx,
                      int Ho, int Wo, int Cyp, int S, int pad, int reflect, int Mw, int chunk,
-                     int nsplit, int kind, hipStream_t s);
+                     int nsplit, int kind, int math, hipStream_t s);
 void rk_tconv_launch(const float* in, const float* wp, const float* bias, const float* addend,
                      float* out, int N, int Hi, int Wi, int Cy, int Ho, int Wo, int Cx, int R, int S,
-                     int st, int pad, int reflect, int act, float slope, int kind, hipStream_t s);
+                     int st, int pad, int reflect, int act, float slope, int kind, int math,
+                     hipStream_t s);
 int skinny_wgrad_launch(const float* x, const float* dy, float* slab, int H, int W, int Cx, int Ho,
                         int Wo, int S, int st, int pad, int reflect, int Mw, int P, int chunk,
                         int nsplit, hipStream_t s);

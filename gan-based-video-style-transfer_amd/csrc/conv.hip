@@ -716,8 +716,9 @@ extern "C" void vst_debug_set_tiles(int fprop, int tconv, int wgrad) {
 
 extern "C" int vst_conv2d_fwd(const float* x, const float* wp, const float* bias, float* y, int N,
                               int H, int W, int Cx, int Cop, int R, int S, int stride, int pad,
-                              int pad_mode, int act, float slope, void* stream) {
+                              int pad_mode, int act, float slope, int math, void* stream) {
   VST_REQUIRE(x && wp && y, "conv2d_fwd: null pointer");
+  VST_REQUIRE(math >= VST_MATH_F32 && math <= VST_MATH_BF16X6, "conv2d_fwd: bad math %d", math);
   VST_REQUIRE(N > 0 && H > 0 && W > 0 && R > 0 && S > 0 && stride > 0 && pad >= 0,
               "conv2d_fwd: bad shape");
   VST_REQUIRE(Cx % 4 == 0 && Cop % 4 == 0, "conv2d_fwd: channel strides must be multiples of 4");
@@ -736,7 +737,7 @@ extern "C" int vst_conv2d_fwd(const float* x, const float* wp, const float* bias
                      stride, pad, refl, act, slope, M, K)
   (void)pick_tile;
   rk_fprop_launch(x, wp, bias, y, N, H, W, Cx, Ho, Wo, Cop, R, S, stride, pad, refl, act, slope,
-                    g_tile_override[0], s);
+                  g_tile_override[0], math, s);
 #undef VST_FPROP
   return check_launch("conv2d_fwd");
 }
@@ -744,8 +745,9 @@ extern "C" int vst_conv2d_fwd(const float* x, const float* wp, const float* bias
 extern "C" int vst_conv2d_tfwd(const float* in, const float* wp, const float* bias,
                                const float* addend, float* out, int N, int Hi, int Wi, int Cy,
                                int Ho, int Wo, int Cx, int R, int S, int stride, int pad,
-                               int pad_mode, int act, float slope, void* stream) {
+                               int pad_mode, int act, float slope, int math, void* stream) {
   VST_REQUIRE(in && wp && out, "conv2d_tfwd: null pointer");
+  VST_REQUIRE(math >= VST_MATH_F32 && math <= VST_MATH_BF16X6, "conv2d_tfwd: bad math %d", math);
   VST_REQUIRE(N > 0 && Hi > 0 && Wi > 0 && Ho > 0 && Wo > 0 && R > 0 && S > 0 && stride > 0 && pad >= 0,
               "conv2d_tfwd: bad shape");
   VST_REQUIRE(Cy % 4 == 0 && Cx % 4 == 0, "conv2d_tfwd: channel strides must be multiples of 4");
@@ -769,7 +771,7 @@ extern "C" int vst_conv2d_tfwd(const float* in, const float* wp, const float* bi
   else VST_TCONV_ST(BM_, BN_, WM_, WN_, 0);
   (void)Mmax;
   rk_tconv_launch(in, wp, bias, addend, out, N, Hi, Wi, Cy, Ho, Wo, Cx, R, S, stride, pad, refl, act,
-                    slope, g_tile_override[1], s);
+                  slope, g_tile_override[1], math, s);
 #undef VST_TCONV
 #undef VST_TCONV_ST
   return check_launch("conv2d_tfwd");
@@ -788,8 +790,9 @@ extern "C" size_t vst_conv2d_wgrad_ws_bytes(int N, int H, int W, int Cx, int Ho,
 extern "C" int vst_conv2d_wgrad(const float* x, const float* dy, float* dw, float* ws,
                                 size_t ws_bytes, int N, int H, int W, int Cx, int Ho, int Wo,
                                 int Cyp, int R, int S, int stride, int pad, int pad_mode, int Co,
-                                int Ci, long so, long si, int accumulate, void* stream) {
+                                int Ci, long so, long si, int accumulate, int math, void* stream) {
   VST_REQUIRE(x && dy && dw && ws, "conv2d_wgrad: null pointer");
+  VST_REQUIRE(math >= VST_MATH_F32 && math <= VST_MATH_BF16X6, "conv2d_wgrad: bad math %d", math);
   VST_REQUIRE(Cx % 4 == 0 && Cyp % 4 == 0, "conv2d_wgrad: channel strides must be multiples of 4");
   VST_REQUIRE(Co <= Cyp && Ci <= Cx, "conv2d_wgrad: logical channels exceed strides");
   VST_REQUIRE(pad_mode == VST_PAD_ZERO || (pad < H && pad < W), "conv2d_wgrad: reflect pad >= size");
@@ -810,7 +813,7 @@ extern "C" int vst_conv2d_wgrad(const float* x, const float* dy, float* dw, floa
     rk_nhwc_to_cp(x, xt, (long)N * H * W, Cx, s);
     rk_nhwc_to_cp(dy, dyt, P, Cyp, s);
     rk_wgrad_launch(xt, dyt, ws, N, H, W, Cx, Ho, Wo, Cyp, S, pad, refl, p.Mw, p.chunk, p.nsplit,
-                    (int)p.tile, s);
+                    (int)p.tile, math, s);
   } else if (Cyp == 4) {
     int rc0 = skinny_wgrad_launch(x, dy, ws, H, W, Cx, Ho, Wo, S, stride, pad, refl, p.Mw, P, p.chunk,
                                   p.nsplit, s);

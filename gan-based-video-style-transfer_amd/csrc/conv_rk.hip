@@ -30,23 +30,30 @@ constexpr int NOPOS = -(1 << 20);
 #define VST_RK_LG 4   // the next stage's global loads are spread over the first LG MFMA groups
 #endif
 
-template <int BM, int BN, int WM, int WN, int BK_>
+template <int BM, int BN, int WM, int WN, int BK_, int MATH_ = VST_MATH_F32>
 struct Tile {
+  static constexpr int MATH = MATH_;
+  static constexpr bool X3 = MATH != VST_MATH_F32;    // bf16 split-operand image (x3 or x6)
+  static constexpr int NP = MATH == VST_MATH_BF16X6 ? 3 : 2;  // bf16 planes per operand
+  static constexpr int BM_ = BM, BN_ = BN, WM_ = WM, WN_ = WN;
   static constexpr int BK = BK_;
-  static constexpr int LDK = BK + 4;
+  static constexpr int LDK = BK + 4;             // fp32 image: row stride in floats
+  static constexpr int LDH = BK + 8;             // bf16x3 image: row stride in bf16 elements
   static constexpr int KQ = BK / 4;              // lanes (float4s) per staged row
   static constexpr int NW = (BM / WM) * (BN / WN);
   static constexpr int NT = 64 * NW;
   static constexpr int WAVES_N = BN / WN;
   static constexpr int MI = WM / 32;
   static constexpr int NI = WN / 32;
-  static constexpr int A_ELEMS = BM * LDK;
-  static constexpr int B_ELEMS = BN * LDK;
+  // stage sizes in floats; a bf16 split image holds NP planes [rows][LDH] (hi, (mid,) lo)
+  static constexpr int A_ELEMS = X3 ? BM * LDH * NP / 2 : BM * LDK;
+  static constexpr int B_ELEMS = X3 ? BN * LDH * NP / 2 : BN * LDK;
   static constexpr int STAGE = A_ELEMS + B_ELEMS;
   static constexpr int ROWS_PER_PASS = NT / KQ;  // KQ lanes x float4 cover one BK-deep row
   static constexpr int A_LD = BM / ROWS_PER_PASS;
   static constexpr int B_LD = BN / ROWS_PER_PASS;
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
+  static_assert(!X3 || BK % 16 == 0, "bf16 k groups are 16 deep");
   static_assert(BM % ROWS_PER_PASS == 0 && BN % ROWS_PER_PASS == 0, "row coverage");
 };
 
@@ -54,12 +61,44 @@ __device__ __forceinline__ float comp(const float4& v, int t) {
   return t == 0 ? v.x : (t == 1 ? v.y : (t == 2 ? v.z : v.w));
 }
 
-template <int BM, int BN, int WM, int WN, int BK, class Hook>
-__device__ __forceinline__ void mma_stage(const float* __restrict__ As, const float* __restrict__ Bs,
-                                          f32x16 (&acc)[WM / 32][WN / 32], int wm0, int wn0,
-                                          int lane, Hook hook) {
-  using T = Tile<BM, BN, WM, WN, BK>;
-  constexpr int LDK = T::LDK;
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+
+// Two fp32 -> two bf16 (RNE, v_cvt_pk_bf16_f32), packed low = a, high = b.
+__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
+  const f32x2_t v = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
+}
+
+// bf16 operand split of four fp32 values into NP planes.  NP = 2: hi = bf16(v), lo = bf16(v - hi);
+// v - hi is exact in fp32, so hi + lo carries 16 significant bits (|v - hi - lo| <= 2^-17 |v|).
+// NP = 3 splits the remainder once more (mid, lo): hi + mid + lo carries all 24 bits of v.
+__device__ __forceinline__ float bf16_lo_f(uint32_t p) { return __uint_as_float(p << 16); }
+__device__ __forceinline__ float bf16_hi_f(uint32_t p) { return __uint_as_float(p & 0xffff0000u); }
+
+template <int NP>
+__device__ __forceinline__ void split4(const float4& v, uint2 (&o)[NP]) {
+  float r0 = v.x, r1 = v.y, r2 = v.z, r3 = v.w;
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    o[p].x = pack_bf16x2(r0, r1);
+    o[p].y = pack_bf16x2(r2, r3);
+    if (p + 1 < NP) {
+      r0 -= bf16_lo_f(o[p].x);
+      r1 -= bf16_hi_f(o[p].x);
+      r2 -= bf16_lo_f(o[p].y);
+      r3 -= bf16_hi_f(o[p].y);
+    }
+  }
+}
+
+// fp32 image: v_mfma_f32_32x32x2_f32, 4 MFMAs per 8-deep k group and fragment pair.
+template <class T, class Hook>
+__device__ __forceinline__ void mma_stage_f32(const float* __restrict__ As, const float* __restrict__ Bs,
+                                              f32x16 (&acc)[T::MI][T::NI], int wm0, int wn0, int lane,
+                                              Hook hook) {
+  constexpr int LDK = T::LDK, BK = T::BK;
   const int kh = lane >> 5, li = lane & 31;
   const float* pa = As + (wm0 + li) * LDK + 4 * kh;
   const float* pb = Bs + (wn0 + li) * LDK + 4 * kh;
@@ -95,14 +134,101 @@ __device__ __forceinline__ void mma_stage(const float* __restrict__ As, const fl
   }
 }
 
-template <int BM, int BN, int WM, int WN, int BK, int NLOAD, class LoadOne, class Adv, class Store>
-__device__ __forceinline__ void main_loop(float* smem, int nk, f32x16 (&acc)[WM / 32][WN / 32],
+// bf16 split image: per 16-deep k group, lane (li, kh) reads 8 consecutive k of its row
+// (k = 16g + 8kh + 0..7, the v_mfma_f32_32x32x16_bf16 A/B operand map) from every plane with one
+// ds_read_b128 each, then accumulates the split products in fp32, smallest terms first:
+//   x3 (NP = 2): lo*hi + hi*lo + hi*hi                (dropped lo*lo <= 2^-16 |a*b|)
+//   x6 (NP = 3): lo*hi + hi*lo + mid*mid + mid*hi + hi*mid + hi*hi   (dropped terms <= 2^-24 |a*b|)
+// Row stride BK + 8 bf16 = 16-B slots that put the 16 lanes of every ds_read_b128 group on 16
+// distinct slots.
+template <class T, class Hook>
+__device__ __forceinline__ void mma_stage_bf16(const float* __restrict__ As, const float* __restrict__ Bs,
+                                               f32x16 (&acc)[T::MI][T::NI], int wm0, int wn0, int lane,
+                                               Hook hook) {
+  constexpr int LDH = T::LDH, BK = T::BK, NP = T::NP;
+  constexpr int PA = T::BM_ * LDH, PB = T::BN_ * LDH;  // plane sizes (bf16)
+  const int kh = lane >> 5, li = lane & 31;
+  const __bf16* pa = reinterpret_cast<const __bf16*>(As) + (wm0 + li) * LDH + 8 * kh;
+  const __bf16* pb = reinterpret_cast<const __bf16*>(Bs) + (wn0 + li) * LDH + 8 * kh;
+  bf16x8_t fa[2][NP][T::MI], fb[2][NP][T::NI];
+  auto rd = [&](int buf, int o) {
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+#pragma unroll
+      for (int i = 0; i < T::MI; ++i)
+        fa[buf][p][i] = *reinterpret_cast<const bf16x8_t*>(pa + p * PA + 32 * i * LDH + o);
+#pragma unroll
+      for (int j = 0; j < T::NI; ++j)
+        fb[buf][p][j] = *reinterpret_cast<const bf16x8_t*>(pb + p * PB + 32 * j * LDH + o);
+    }
+  };
+  rd(0, 0);
+#pragma unroll
+  for (int g = 0; g < BK / 16; ++g) {
+    const int cur = g & 1;
+    hook(g);
+    if (g + 1 < BK / 16) rd(cur ^ 1, 16 * (g + 1));
+#pragma unroll
+    for (int i = 0; i < T::MI; ++i)
+#pragma unroll
+      for (int j = 0; j < T::NI; ++j) {
+#define VST_MF(pA, pB) \
+  acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[cur][pA][i], fb[cur][pB][j], acc[i][j], 0, 0, 0)
+        if constexpr (NP == 3) {
+          VST_MF(2, 0); VST_MF(0, 2); VST_MF(1, 1); VST_MF(1, 0); VST_MF(0, 1); VST_MF(0, 0);
+        } else {
+          VST_MF(1, 0); VST_MF(0, 1); VST_MF(0, 0);
+        }
+#undef VST_MF
+      }
+  }
+}
+
+// Write one thread's staged float4s (A rows rb + RP*j, B rows likewise, k = 4*kq..4*kq+3) into a
+// stage image: float4 rows for fp32, split hi/lo bf16 quads (ds_write_b64 each) for bf16x3.
+template <class T, int A_LD, int B_LD>
+__device__ __forceinline__ void store_stage(float* As, const float4 (&ra)[A_LD], const float4 (&rbv)[B_LD],
+                                            int rb, int kq) {
+  constexpr int RP = T::ROWS_PER_PASS;
+  float* Bs = As + T::A_ELEMS;
+  if constexpr (T::X3) {
+    constexpr int LDH = T::LDH, NP = T::NP;
+    __bf16* ah = reinterpret_cast<__bf16*>(As);
+    __bf16* bh = reinterpret_cast<__bf16*>(Bs);
+#pragma unroll
+    for (int j = 0; j < A_LD; ++j) {
+      uint2 s[NP];
+      split4<NP>(ra[j], s);
+      const int o = (rb + RP * j) * LDH + 4 * kq;
+#pragma unroll
+      for (int p = 0; p < NP; ++p) *reinterpret_cast<uint2*>(ah + p * T::BM_ * LDH + o) = s[p];
+    }
+#pragma unroll
+    for (int j = 0; j < B_LD; ++j) {
+      uint2 s[NP];
+      split4<NP>(rbv[j], s);
+      const int o = (rb + RP * j) * LDH + 4 * kq;
+#pragma unroll
+      for (int p = 0; p < NP; ++p) *reinterpret_cast<uint2*>(bh + p * T::BN_ * LDH + o) = s[p];
+    }
+  } else {
+    constexpr int LDK = T::LDK;
+#pragma unroll
+    for (int j = 0; j < A_LD; ++j) *reinterpret_cast<float4*>(As + (rb + RP * j) * LDK + 4 * kq) = ra[j];
+#pragma unroll
+    for (int j = 0; j < B_LD; ++j) *reinterpret_cast<float4*>(Bs + (rb + RP * j) * LDK + 4 * kq) = rbv[j];
+  }
+}
+
+template <class T, int NLOAD, class LoadOne, class Adv, class Store>
+__device__ __forceinline__ void main_loop(float* smem, int nk, f32x16 (&acc)[T::MI][T::NI],
                                           LoadOne load_one, Adv adv, Store store) {
-  using T = Tile<BM, BN, WM, WN, BK>;
-  constexpr int LG = VST_RK_LG < BK / 8 ? VST_RK_LG : BK / 8;
+  constexpr int BK = T::BK;
+  constexpr int NG = T::X3 ? BK / 16 : BK / 8;  // k groups per stage (hook slots)
+  constexpr int LG = VST_RK_LG < NG ? VST_RK_LG : NG;
   constexpr int PER = (NLOAD + LG - 1) / LG;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int wm0 = (wave / T::WAVES_N) * WM, wn0 = (wave % T::WAVES_N) * WN;
+  const int wm0 = (wave / T::WAVES_N) * T::WM_, wn0 = (wave % T::WAVES_N) * T::WN_;
   if (nk > 0) {
 #pragma unroll
     for (int i = 0; i < NLOAD; ++i) load_one(i, 0);
@@ -114,13 +240,15 @@ __device__ __forceinline__ void main_loop(float* smem, int nk, f32x16 (&acc)[WM 
     const bool next = kt + 1 < nk;
     if (next) adv();
     const int k0n = (kt + 1) * BK;
-    mma_stage<BM, BN, WM, WN, BK>(cur, cur + T::A_ELEMS, acc, wm0, wn0, lane, [&](int g) {
+    auto hook = [&](int g) {
       if (next) {
 #pragma unroll
         for (int u = 0; u < PER; ++u)
           if (PER * g + u < NLOAD) load_one(PER * g + u, k0n);
       }
-    });
+    };
+    if constexpr (T::X3) mma_stage_bf16<T>(cur, cur + T::A_ELEMS, acc, wm0, wn0, lane, hook);
+    else mma_stage_f32<T>(cur, cur + T::A_ELEMS, acc, wm0, wn0, lane, hook);
     if (next) store(smem + ((kt + 1) & 1) * T::STAGE);
     __syncthreads();
   }
@@ -142,13 +270,13 @@ __device__ __forceinline__ void zero_acc(f32x16 (&acc)[MI][NI]) {
 }
 
 // ------------------------------------------------------------------------------------------ fprop
-template <int BM, int BN, int WM, int WN, int BK>
-__global__ __launch_bounds__((Tile<BM, BN, WM, WN, BK>::NT), 2) void conv_fprop_rk_k(
+template <int BM, int BN, int WM, int WN, int BK, int MATH>
+__global__ __launch_bounds__((Tile<BM, BN, WM, WN, BK, MATH>::NT), 2) void conv_fprop_rk_k(
     const float* __restrict__ x, const float* __restrict__ wp, const float* __restrict__ bias,
     float* __restrict__ y, int H, int W, int C, int Ho, int Wo, int Cop, int S, int st, int pad,
     int reflect, int act, float slope, int M, int Ktot) {
-  using T = Tile<BM, BN, WM, WN, BK>;
-  constexpr int NT = T::NT, A_LD = T::A_LD, B_LD = T::B_LD, RP = T::ROWS_PER_PASS, LDK = T::LDK;
+  using T = Tile<BM, BN, WM, WN, BK, MATH>;
+  constexpr int NT = T::NT, A_LD = T::A_LD, B_LD = T::B_LD, RP = T::ROWS_PER_PASS;
   __shared__ __attribute__((aligned(16))) float smem[2 * T::STAGE];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int mt = remap_mtile(blockIdx.x, gridDim.x);
@@ -224,17 +352,11 @@ __global__ __launch_bounds__((Tile<BM, BN, WM, WN, BK>::NT), 2) void conv_fprop_
       if (++ks == S) { ks = 0; ++kr; }
     }
   };
-  auto store = [&](float* As) {
-    float* Bs = As + T::A_ELEMS;
-#pragma unroll
-    for (int j = 0; j < A_LD; ++j) *reinterpret_cast<float4*>(As + (rb + RP * j) * LDK + 4 * kq) = ra[j];
-#pragma unroll
-    for (int j = 0; j < B_LD; ++j) *reinterpret_cast<float4*>(Bs + (rb + RP * j) * LDK + 4 * kq) = rbv[j];
-  };
+  auto store = [&](float* As) { store_stage<T, A_LD, B_LD>(As, ra, rbv, rb, kq); };
 
   f32x16 acc[T::MI][T::NI];
   zero_acc(acc);
-  main_loop<BM, BN, WM, WN, BK, A_LD + B_LD>(smem, (Ktot + BK - 1) / BK, acc, load_one, adv, store);
+  main_loop<T, A_LD + B_LD>(smem, (Ktot + BK - 1) / BK, acc, load_one, adv, store);
   (void)NT;
 
   const int wm0 = (wave / T::WAVES_N) * WM, wn0 = (wave % T::WAVES_N) * WN;
@@ -254,13 +376,13 @@ __global__ __launch_bounds__((Tile<BM, BN, WM, WN, BK>::NT), 2) void conv_fprop_
 }
 
 // ------------------------------------------------------------------- transposed conv / dgrad
-template <int BM, int BN, int WM, int WN, int BK, int ST>
-__global__ __launch_bounds__((Tile<BM, BN, WM, WN, BK>::NT), 2) void conv_tconv_rk_k(
+template <int BM, int BN, int WM, int WN, int BK, int ST, int MATH>
+__global__ __launch_bounds__((Tile<BM, BN, WM, WN, BK, MATH>::NT), 2) void conv_tconv_rk_k(
     const float* __restrict__ in, const float* __restrict__ wp, const float* __restrict__ bias,
     const float* __restrict__ addend, float* __restrict__ out, int Hi, int Wi, int Cy, int Ho,
     int Wo, int Cx, int R, int S, int st_rt, int pad, int reflect, int act, float slope, int Nimg) {
-  using T = Tile<BM, BN, WM, WN, BK>;
-  constexpr int A_LD = T::A_LD, B_LD = T::B_LD, RP = T::ROWS_PER_PASS, LDK = T::LDK;
+  using T = Tile<BM, BN, WM, WN, BK, MATH>;
+  constexpr int A_LD = T::A_LD, B_LD = T::B_LD, RP = T::ROWS_PER_PASS;
   __shared__ __attribute__((aligned(16))) float smem[2 * T::STAGE];
   const int st = ST > 0 ? ST : st_rt;
   const int ca = blockIdx.z / st, cb = blockIdx.z % st;
@@ -355,17 +477,11 @@ __global__ __launch_bounds__((Tile<BM, BN, WM, WN, BK>::NT), 2) void conv_tconv_
       if (++kis == ns) { kis = 0; ++kir; }
     }
   };
-  auto store = [&](float* As) {
-    float* Bs = As + T::A_ELEMS;
-#pragma unroll
-    for (int j = 0; j < A_LD; ++j) *reinterpret_cast<float4*>(As + (rb + RP * j) * LDK + 4 * kq) = ra[j];
-#pragma unroll
-    for (int j = 0; j < B_LD; ++j) *reinterpret_cast<float4*>(Bs + (rb + RP * j) * LDK + 4 * kq) = rbv[j];
-  };
+  auto store = [&](float* As) { store_stage<T, A_LD, B_LD>(As, ra, rbv, rb, kq); };
 
   f32x16 acc[T::MI][T::NI];
   zero_acc(acc);
-  main_loop<BM, BN, WM, WN, BK, A_LD + B_LD>(smem, (Ktot + BK - 1) / BK, acc, load_one, adv, store);
+  main_loop<T, A_LD + B_LD>(smem, (Ktot + BK - 1) / BK, acc, load_one, adv, store);
 
   const int wm0 = (wave / T::WAVES_N) * WM, wn0 = (wave % T::WAVES_N) * WN;
   const int hw = Hc * Wc;
@@ -397,13 +513,13 @@ __global__ __launch_bounds__((Tile<BM, BN, WM, WN, BK>::NT), 2) void conv_tconv_
 // float4 are 4 consecutive input columns: one (unaligned) 16-byte load unless the window crosses
 // the image border, where the 4 taps are reflected / zeroed one by one.  blockIdx.z = K split;
 // partial tiles land in slab[z][m][Cyp] (summed and transposed into dw by conv.hip).
-template <int BM, int BN, int WM, int WN, int BK>
-__global__ __launch_bounds__((Tile<BM, BN, WM, WN, BK>::NT), 2) void conv_wgrad_rk_k(
+template <int BM, int BN, int WM, int WN, int BK, int MATH>
+__global__ __launch_bounds__((Tile<BM, BN, WM, WN, BK, MATH>::NT), 2) void conv_wgrad_rk_k(
     const float* __restrict__ xt, const float* __restrict__ dyt, float* __restrict__ slab, int H,
     int W, int Cx, int Ho, int Wo, int Cyp, int S, int pad, int reflect, int Mw, int P, int chunk,
     long ldx, long ldy) {
-  using T = Tile<BM, BN, WM, WN, BK>;
-  constexpr int A_LD = T::A_LD, B_LD = T::B_LD, RP = T::ROWS_PER_PASS, LDK = T::LDK;
+  using T = Tile<BM, BN, WM, WN, BK, MATH>;
+  constexpr int A_LD = T::A_LD, B_LD = T::B_LD, RP = T::ROWS_PER_PASS;
   typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
   __shared__ __attribute__((aligned(16))) float smem[2 * T::STAGE];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -490,18 +606,12 @@ __global__ __launch_bounds__((Tile<BM, BN, WM, WN, BK>::NT), 2) void conv_wgrad_
       if (++pho == Ho) { pho = 0; ++pn; }
     }
   };
-  auto store = [&](float* As) {
-    float* Bs = As + T::A_ELEMS;
-#pragma unroll
-    for (int j = 0; j < A_LD; ++j) *reinterpret_cast<float4*>(As + (rb + RP * j) * LDK + 4 * kq) = ra[j];
-#pragma unroll
-    for (int j = 0; j < B_LD; ++j) *reinterpret_cast<float4*>(Bs + (rb + RP * j) * LDK + 4 * kq) = rbv[j];
-  };
+  auto store = [&](float* As) { store_stage<T, A_LD, B_LD>(As, ra, rbv, rb, kq); };
 
   f32x16 acc[T::MI][T::NI];
   zero_acc(acc);
   const int nk = pend > pbeg ? (pend - pbeg + BK - 1) / BK : 0;
-  main_loop<BM, BN, WM, WN, BK, A_LD + B_LD>(smem, nk, acc, load_one, adv, store);
+  main_loop<T, A_LD + B_LD>(smem, nk, acc, load_one, adv, store);
 
   const int wm0 = (wave / T::WAVES_N) * WM, wn0 = (wave % T::WAVES_N) * WN;
   float* sl = slab + (long)blockIdx.z * Mw * Cyp;
@@ -581,60 +691,84 @@ void rk_tile_geom(int kind, int* bm, int* bn, int* bk, int* slots) {
   *slots = (kind == 0 || kind == 4 || kind == 6) ? 256 : 512;  // co-resident blocks per round
 }
 
-#define VST_RK_DISPATCH(kind, LAUNCH)            \
-  switch (kind) {                                 \
-    case 0: LAUNCH(128, 128, 64, 32, 32); break;  \
-    case 1: LAUNCH(64, 128, 32, 64, 32); break;   \
-    case 2: LAUNCH(128, 64, 64, 32, 32); break;   \
-    case 4: LAUNCH(128, 128, 64, 32, 64); break;  \
-    case 5: LAUNCH(128, 128, 64, 64, 32); break;  \
-    case 6: LAUNCH(128, 128, 64, 64, 64); break;  \
-    default: LAUNCH(64, 64, 32, 32, 32); break;   \
+#define VST_RK_DISPATCH_M(kind, LAUNCH, M_)                             \
+  switch (kind) {                                                        \
+    case 0: LAUNCH(128, 128, 64, 32, 32, M_) break;                      \
+    case 1: LAUNCH(64, 128, 32, 64, 32, M_) break;                       \
+    case 2: LAUNCH(128, 64, 64, 32, 32, M_) break;                       \
+    case 4: LAUNCH(128, 128, 64, 32, (M_ == VST_MATH_BF16X6 ? 32 : 64), M_) break; \
+    case 5: LAUNCH(128, 128, 64, 64, 32, M_) break;                      \
+    case 6: LAUNCH(128, 128, 64, 64, (M_ == VST_MATH_BF16X6 ? 32 : 64), M_) break; \
+    default: LAUNCH(64, 64, 32, 32, 32, M_) break;                       \
+  }
+
+// Conv GEMM arithmetic (per call): VST_MATH_F32 = v_mfma_f32_32x32x2_f32 (exact fp32 products);
+// VST_MATH_BF16X3 / VST_MATH_BF16X6 = split-operand v_mfma_f32_32x32x16_bf16 (3 / 6 products per
+// operand pair, fp32 accumulate).  The 3-plane x6 image only fits the 32-deep K-step tiles.
+static int math_kind(int math, int kind) {
+  if (math == VST_MATH_BF16X6) return kind == 4 ? 0 : (kind == 6 ? 5 : kind);
+  return kind;
+}
+
+#define VST_MATH_SWITCH(math, LAUNCH_M)                                        \
+  switch (math) {                                                               \
+    case VST_MATH_BF16X3: { LAUNCH_M(VST_MATH_BF16X3) } break;                  \
+    case VST_MATH_BF16X6: { LAUNCH_M(VST_MATH_BF16X6) } break;                  \
+    default: { LAUNCH_M(VST_MATH_F32) } break;                                  \
   }
 
 void rk_fprop_launch(const float* x, const float* wp, const float* bias, float* y, int N, int H, int W,
                      int C, int Ho, int Wo, int Cop, int R, int S, int st, int pad, int reflect, int act,
-                     float slope, int kind, hipStream_t s) {
+                     float slope, int kind, int math, hipStream_t s) {
   const int M = N * Ho * Wo, K = R * S * C;
-#define VST_L(BM_, BN_, WM_, WN_, BK_)                                                             \
-  hipLaunchKernelGGL((rk::conv_fprop_rk_k<BM_, BN_, WM_, WN_, BK_>),                                 \
+  const int kd = math_kind(math, rk_pick(M, Cop, kind));
+#define VST_LX(BM_, BN_, WM_, WN_, BK_, M_)                                                        \
+  hipLaunchKernelGGL((rk::conv_fprop_rk_k<BM_, BN_, WM_, WN_, BK_, M_>),                             \
                      dim3(ceil_div(M, BM_), ceil_div(Cop, BN_)),                                     \
                      dim3(rk::Tile<BM_, BN_, WM_, WN_, BK_>::NT),                                    \
-                     0, s, x, wp, bias, y, H, W, C, Ho, Wo, Cop, S, st, pad, reflect, act, slope, M, K)
-  VST_RK_DISPATCH(rk_pick(M, Cop, kind), VST_L)
-#undef VST_L
+                     0, s, x, wp, bias, y, H, W, C, Ho, Wo, Cop, S, st, pad, reflect, act, slope, M, K);
+#define VST_LM(M_) VST_RK_DISPATCH_M(kd, VST_LX, M_)
+  VST_MATH_SWITCH(math, VST_LM)
+#undef VST_LM
+#undef VST_LX
 }
 
 void rk_tconv_launch(const float* in, const float* wp, const float* bias, const float* addend,
                      float* out, int N, int Hi, int Wi, int Cy, int Ho, int Wo, int Cx, int R, int S,
-                     int st, int pad, int reflect, int act, float slope, int kind, hipStream_t s) {
+                     int st, int pad, int reflect, int act, float slope, int kind, int math, hipStream_t s) {
   const int Hc = (Ho + st - 1) / st, Wc = (Wo + st - 1) / st;
   const int Mmax = N * Hc * Wc;
-#define VST_LST(BM_, BN_, WM_, WN_, BK_, ST_)                                                      \
-  hipLaunchKernelGGL((rk::conv_tconv_rk_k<BM_, BN_, WM_, WN_, BK_, ST_>),                            \
+  const int kd = math_kind(math, rk_pick((long)Mmax * st * st, Cx, kind));
+#define VST_LST(BM_, BN_, WM_, WN_, BK_, ST_, M_)                                                  \
+  hipLaunchKernelGGL((rk::conv_tconv_rk_k<BM_, BN_, WM_, WN_, BK_, ST_, M_>),                        \
                      dim3(ceil_div(Mmax, BM_), ceil_div(Cx, BN_), st * st),                          \
                      dim3(rk::Tile<BM_, BN_, WM_, WN_, BK_>::NT), 0, s, in, wp, bias, addend, out, Hi, Wi, \
                      Cy, Ho, Wo, Cx, R, S, st, pad, reflect, act, slope, N)
-#define VST_L(BM_, BN_, WM_, WN_, BK_)                   \
-  if (st == 1) VST_LST(BM_, BN_, WM_, WN_, BK_, 1);       \
-  else if (st == 2) VST_LST(BM_, BN_, WM_, WN_, BK_, 2);  \
-  else VST_LST(BM_, BN_, WM_, WN_, BK_, 0);
-  VST_RK_DISPATCH(rk_pick((long)Mmax * st * st, Cx, kind), VST_L)
-#undef VST_L
+#define VST_LX(BM_, BN_, WM_, WN_, BK_, M_)                 \
+  if (st == 1) VST_LST(BM_, BN_, WM_, WN_, BK_, 1, M_);       \
+  else if (st == 2) VST_LST(BM_, BN_, WM_, WN_, BK_, 2, M_);  \
+  else VST_LST(BM_, BN_, WM_, WN_, BK_, 0, M_);
+#define VST_LM(M_) VST_RK_DISPATCH_M(kd, VST_LX, M_)
+  VST_MATH_SWITCH(math, VST_LM)
+#undef VST_LM
+#undef VST_LX
 #undef VST_LST
 }
 
 void rk_wgrad_launch(const float* xt, const float* dyt, float* slab, int N, int H, int W, int Cx,
                      int Ho, int Wo, int Cyp, int S, int pad, int reflect, int Mw, int chunk,
-                     int nsplit, int kind, hipStream_t s) {
+                     int nsplit, int kind, int math, hipStream_t s) {
   const int P = N * Ho * Wo;
-#define VST_L(BM_, BN_, WM_, WN_, BK_)                                                             \
-  hipLaunchKernelGGL((rk::conv_wgrad_rk_k<BM_, BN_, WM_, WN_, BK_>),                                 \
+  const int kd = math_kind(math, kind);
+#define VST_LX(BM_, BN_, WM_, WN_, BK_, M_)                                                        \
+  hipLaunchKernelGGL((rk::conv_wgrad_rk_k<BM_, BN_, WM_, WN_, BK_, M_>),                             \
                      dim3(ceil_div(Mw, BM_), ceil_div(Cyp, BN_), nsplit),                            \
                      dim3(rk::Tile<BM_, BN_, WM_, WN_, BK_>::NT), 0, s, xt, dyt, slab, H, W, Cx, Ho, \
-                     Wo, Cyp, S, pad, reflect, Mw, P, chunk, rk_cp_ld((long)N * H * W), rk_cp_ld(P))
-  VST_RK_DISPATCH(kind, VST_L)
-#undef VST_L
+                     Wo, Cyp, S, pad, reflect, Mw, P, chunk, rk_cp_ld((long)N * H * W), rk_cp_ld(P));
+#define VST_LM(M_) VST_RK_DISPATCH_M(kd, VST_LX, M_)
+  VST_MATH_SWITCH(math, VST_LM)
+#undef VST_LM
+#undef VST_LX
 }
 
 }  // namespace vst

@@ -330,10 +330,11 @@ class _GeneratorFn(torch.autograd.Function):
         ngf = net.ngf
         sv = {"x": x}
         N, H, W, _ = x.shape
+        role = "fwd" if any(ctx.needs_input_grad[:2]) else "infer"
 
         def conv_in_relu(inp, key, cout, R, st, pad, mode):
             kc, _, b = P[key]
-            y = ops.conv2d_fwd(inp, kc, b, cpad(cout), R, R, st, pad, mode)
+            y = ops.conv2d_fwd(inp, kc, b, cpad(cout), R, R, st, pad, mode, role=role)
             s = ops.instnorm_stats(y)
             return y, s, ops.instnorm_act_fwd(y, s, "relu")
 
@@ -347,7 +348,7 @@ class _GeneratorFn(torch.autograd.Function):
         for i in range(len(blocks)):
             t, s1, uu = conv_in_relu(h, f"b{i}a", 4 * ngf, 3, 1, 1, "reflect")
             kc, _, b = P[f"b{i}b"]
-            v = ops.conv2d_fwd(uu, kc, b, 4 * ngf, 3, 3, 1, 1, "reflect")
+            v = ops.conv2d_fwd(uu, kc, b, 4 * ngf, 3, 3, 1, 1, "reflect", role=role)
             s2 = ops.instnorm_stats(v)
             hn = ops.instnorm_act_fwd(v, s2, "none", residual=h)
             sv[f"b{i}"] = (h, t, s1, uu, v, s2)
@@ -357,13 +358,13 @@ class _GeneratorFn(torch.autograd.Function):
             cout = ngf * 2 ** (1 - i)
             _, ck, b = P[f"u{i}"]
             Hi, Wi = a.shape[1], a.shape[2]
-            y = ops.conv2d_tfwd(a, ck, b, 2 * Hi, 2 * Wi, cpad(cout), 3, 3, 2, 1)
+            y = ops.conv2d_tfwd(a, ck, b, 2 * Hi, 2 * Wi, cpad(cout), 3, 3, 2, 1, role=role)
             s = ops.instnorm_stats(y)
             an = ops.instnorm_act_fwd(y, s, "relu")
             sv[f"u{i}"] = (a, y, s, an)
             a = an
         kc, _, b = P["f"]
-        out = ops.conv2d_fwd(a, kc, b, cpad(net.output_nc), 7, 7, 1, 3, "reflect", act="tanh")
+        out = ops.conv2d_fwd(a, kc, b, cpad(net.output_nc), 7, 7, 1, 3, "reflect", act="tanh", role=role)
         sv["f"] = (a, out)
         ctx.sv, ctx.net, ctx.P = sv, net, P
         ctx.train_w = anchor.requires_grad
@@ -416,7 +417,7 @@ class _GeneratorFn(torch.autograd.Function):
                 ops.conv2d_wgrad(dy, a_in, m.weight.grad, None, 3, 3, 2, 1, "zero", ci_t, co_t,
                                  co_t * 9, 9, accumulate=True)
             kc, _, _ = P[f"u{i}"]
-            ga = ops.conv2d_fwd(dy, kc, None, a_in.shape[-1], 3, 3, 2, 1, "zero")
+            ga = ops.conv2d_fwd(dy, kc, None, a_in.shape[-1], 3, 3, 2, 1, "zero", role="bwd")
         # residual blocks
         gh = ga
         for i in reversed(range(len(blocks))):
@@ -498,17 +499,19 @@ class _DiscriminatorFn(torch.autograd.Function):
         saved = []
         a = x
         L = len(convs)
+        role = "fwd" if any(ctx.needs_input_grad[:2]) else "infer"
         for i, (m, (cout, st, has_in)) in enumerate(zip(convs, net.spec)):
             kc, _, b = P[i]
             last = i == L - 1
             if has_in:
-                y = ops.conv2d_fwd(a, kc, b, cpad(cout), 4, 4, st, 1, "zero")
+                y = ops.conv2d_fwd(a, kc, b, cpad(cout), 4, 4, st, 1, "zero", role=role)
                 s = ops.instnorm_stats(y)
                 an = ops.instnorm_act_fwd(y, s, "lrelu", SLOPE)
                 saved.append((a, y, s, an))
             else:
                 act = "none" if last else "lrelu"
-                an = ops.conv2d_fwd(a, kc, b, cpad(cout), 4, 4, st, 1, "zero", act=act, slope=SLOPE)
+                an = ops.conv2d_fwd(a, kc, b, cpad(cout), 4, 4, st, 1, "zero", act=act, slope=SLOPE,
+                                     role=role)
                 saved.append((a, None, None, an))
             a = an
         ctx.saved, ctx.net, ctx.P = saved, net, P

@@ -61,13 +61,26 @@ int vst_nhwc_to_nchw(const float* x, float* y, int N, int C, int H, int W, int C
 int vst_weight_pack(const float* w, float* out, int O, int I, int R, int S, int Op, int Ip,
                     int mode, void* stream);
 
-/* ---- convolution (implicit GEMM on fp32 MFMA) -------------------------------------------- */
+/* ---- convolution (implicit GEMM on MFMA) -------------------------------------------------- */
+/* `math` argument of vst_conv2d_fwd / _tfwd / _wgrad: the GEMM arithmetic of that call.
+ *   VST_MATH_F32     v_mfma_f32_32x32x2_f32: exact fp32 products, fp32 accumulate (1x rate).
+ *   VST_MATH_BF16X3  every fp32 operand split into bf16 hi + lo; acc += lo*hi + hi*lo + hi*hi on
+ *                    v_mfma_f32_32x32x16_bf16 (fp32 accumulate, 5.3x rate): product error
+ *                    <= ~2^-16 relative (finer than the TF32 convs cuDNN runs by default).
+ *   VST_MATH_BF16X6  three-plane split (hi, mid, lo), six products: error <= ~2^-24 relative,
+ *                    i.e. fp32-equivalent (2.7x rate).
+ * The Python mirror uses BF16X6 for every forward conv (forward rounding decides ReLU masks and
+ * hence which gradients exist, so it must stay at fp32 accuracy) and BF16X3 for the data and
+ * weight gradients (linear in their inputs: errors stay ~1e-5 relative).  Layers routed to the
+ * VALU skinny / legacy kernels (<= 4 output channels, strided weight gradients) always compute in
+ * exact fp32, whatever `math` asks. */
+enum { VST_MATH_F32 = 0, VST_MATH_BF16X3 = 1, VST_MATH_BF16X6 = 2 };
 /* y[N][Ho][Wo][Cop] = act(conv(x[N][H][W][Cx], w) + bias).  wp = VST_PACK_OK pack
  * ([Cop][R][S][Cx]); bias has Cop entries or is NULL.  pad_mode VST_PAD_ZERO / VST_PAD_REFLECT.
  * Ho = (H + 2*pad - R)/stride + 1. */
 int vst_conv2d_fwd(const float* x, const float* wp, const float* bias, float* y,
                    int N, int H, int W, int Cx, int Cop, int R, int S, int stride, int pad,
-                   int pad_mode, int act, float slope, void* stream);
+                   int pad_mode, int act, float slope, int math, void* stream);
 /* Transposed convolution / conv data-gradient (gather form, split by output parity class):
  *   out[n][h][w][cx] = sum_{r,s,cy : h = ho*stride - pad + r, w = wo*stride - pad + s}
  *                        in[n][ho][wo][cy] * w[cy][cx][r][s]        (+ bias[cx], act)
@@ -79,7 +92,8 @@ int vst_conv2d_fwd(const float* x, const float* wp, const float* bias, float* y,
  * addend (NULL or [N][Ho][Wo][Cx]) is added after bias/act (fused residual gradient). */
 int vst_conv2d_tfwd(const float* in, const float* wp, const float* bias, const float* addend,
                     float* out, int N, int Hi, int Wi, int Cy, int Ho, int Wo, int Cx, int R,
-                    int S, int stride, int pad, int pad_mode, int act, float slope, void* stream);
+                    int S, int stride, int pad, int pad_mode, int act, float slope, int math,
+                    void* stream);
 /* Weight gradient of y = conv(x, w):  dw[co][ci][r][s] (+)= sum_pix x_gather * dy (bias gradient:
  * vst_channel_sum of dy).  x: [N][H][W][Cx], dy: [N][Ho][Wo][Cyp].  dw is written
  * with strides (so, si) for (co, ci) and r*S+s contiguous, for co < Co, ci < Ci (logical); pass
@@ -92,7 +106,7 @@ size_t vst_conv2d_wgrad_ws_bytes(int N, int H, int W, int Cx, int Ho, int Wo, in
 int vst_conv2d_wgrad(const float* x, const float* dy, float* dw, float* ws, size_t ws_bytes, int N,
                      int H, int W, int Cx, int Ho, int Wo, int Cyp, int R, int S, int stride,
                      int pad, int pad_mode, int Co, int Ci, long so, long si, int accumulate,
-                     void* stream);
+                     int math, void* stream);
 /* Debug/benchmark only: force the GEMM tile of fprop / tconv / wgrad (-1 = automatic).
  * fprop/tconv: 0 = 128x128 (8 waves), 1 = 64x128, 2 = 128x64, 3 = 64x64, 4 = 128x128 64-deep K.
  * wgrad: the same kinds 0..4 on the channel-major (stride-1) path; 8 + k forces the k-major

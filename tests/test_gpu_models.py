@@ -29,7 +29,7 @@ def _rel(got, ref):
 
 
 @pytest.mark.parametrize("tag", ["G", "D"])
-def test_network_vs_reference_golden(gb, golden, tag):
+def test_network_vs_reference_golden(gb, golden, tag, train_math):
     from gbvst import networks
     g = golden("nets_small")
     if tag == "G":
@@ -93,7 +93,7 @@ def _oracle_fp64_losses(g):
     return np.array(out), probe
 
 
-def test_train_step_vs_reference_golden(gb, golden):
+def test_train_step_vs_reference_golden(gb, golden, train_math):
     """Step 0: every loss within 1e-3 relative (north_star).  Later steps: the largest relative loss
     deviation must stay within 1e-3 or within 3x the largest relative deviation that an
     exact-arithmetic (fp64) run of the same algorithm shows from the fp32 reference at that step
@@ -120,7 +120,7 @@ def test_train_step_vs_reference_golden(gb, golden):
     assert np.abs(out - g["probe_out"]).max() <= max(1e-3, 3 * dev64), (np.abs(out - g["probe_out"]).max(), dev64)
 
 
-def test_full_size_generator_vs_oracle(gb):
+def test_full_size_generator_vs_oracle(gb, infer_math):
     from gbvst import networks
     from oracle import cpu_ref, prng
     ref = cpu_ref.RefResnetGenerator(3, 3, 64, 9)

@@ -1,0 +1,11 @@
+cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp; OUT=gpurun_out/r1c; mkdir -p $OUT
+timeout -k 10 500 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1; rc=$?
+tail -40 $OUT/pytest.log | grep -E "passed|failed|FAILED|Error" | head -40
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "pytest rc=$rc"; exit 1; fi
+for m in bf16x3 bf16x6; do
+  VST_CONV_MATH=$m timeout -k 10 200 python -u tools/convbench.py > $OUT/convbench_$m.log 2>&1 || { echo convbench failed; tail $OUT/convbench_$m.log; exit 1; }
+done
+timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline > $OUT/bench.json 2> $OUT/bench.err || { echo bench failed; tail -20 $OUT/bench.err; exit 1; }
+cat $OUT/bench.json
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o prof -- python3 bench.py --steps 7 --warmup 3 --no-cpu-baseline --no-extras > $OUT/prof.log 2>&1 || { echo prof failed; tail -20 $OUT/prof.log; exit 1; }
+echo done

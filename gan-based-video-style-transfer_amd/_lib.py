@@ -39,7 +39,8 @@ SIGNATURES = {
     "vst_nchw_to_nhwc": (I, [P, P, I, I, I, I, I, P]),
     "vst_nhwc_to_nchw": (I, [P, P, I, I, I, I, I, P]),
     "vst_weight_pack": (I, [P, P, I, I, I, I, I, I, I, P]),
-    "vst_conv2d_fwd": (I, [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, I, P]),
+    "vst_conv2d_fwd": (I, [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, I, P]),
+    "vst_weight_split": (I, [P, P, L, P]),
     "vst_conv2d_tfwd": (I, [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, F, I, P]),
     "vst_conv2d_wgrad_ws_bytes": (SZ, [I, I, I, I, I, I, I, I, I, I]),
     "vst_conv2d_wgrad": (I, [P, P, P, P, SZ, I, I, I, I, I, I, I, I, I, I, I, I, I, I, L, L, I, I, P]),

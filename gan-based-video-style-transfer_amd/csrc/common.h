@@ -80,6 +80,10 @@ void rk_fprop_launch(const float* x, const float* wp, const float* bias, float* 
                      int C, int Ho, int Wo, int Cop, int R, int S, int st, int pad, int reflect, int act,
                      float slope, int kind, int math, hipStream_t s);
 long rk_cp_ld(long P);
+// split-operand bf16 implicit GEMM (conv_bf.hip); wsplit = vst_weight_split planes, stride wps
+int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* bias, float* y, int N,
+                    int H, int W, int C, int Ho, int Wo, int Cop, int R, int S, int st, int pad,
+                    int reflect, int act, float slope, int math, int kind, hipStream_t s);
 
 void rk_tile_geom(int kind, int* bm, int* bn, int* bk, int* slots);
 void rk_nhwc_to_cp(const float* x, float* y, long P, int Cs, hipStream_t s);

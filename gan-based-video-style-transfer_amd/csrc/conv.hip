@@ -714,7 +714,8 @@ extern "C" void vst_debug_set_tiles(int fprop, int tconv, int wgrad) {
   g_tile_override[2] = wgrad;
 }
 
-extern "C" int vst_conv2d_fwd(const float* x, const float* wp, const float* bias, float* y, int N,
+extern "C" int vst_conv2d_fwd(const float* x, const float* wp, const void* wsplit, const float* bias,
+                              float* y, int N,
                               int H, int W, int Cx, int Cop, int R, int S, int stride, int pad,
                               int pad_mode, int act, float slope, int math, void* stream) {
   VST_REQUIRE(x && wp && y, "conv2d_fwd: null pointer");
@@ -736,6 +737,9 @@ extern "C" int vst_conv2d_fwd(const float* x, const float* wp, const float* bias
                      dim3(Tile<BM_, BN_, WM_, WN_>::NT), 0, s, x, wp, bias, y, H, W, Cx, Ho, Wo, Cop, S, \
                      stride, pad, refl, act, slope, M, K)
   (void)pick_tile;
+  if (math != VST_MATH_F32 && wsplit && Cx % 8 == 0)
+    return bf_fprop_launch(x, wsplit, (long)Cop * R * S * Cx, bias, y, N, H, W, Cx, Ho, Wo, Cop, R, S,
+                           stride, pad, refl, act, slope, math, g_tile_override[0], s);
   rk_fprop_launch(x, wp, bias, y, N, H, W, Cx, Ho, Wo, Cop, R, S, stride, pad, refl, act, slope,
                   g_tile_override[0], math, s);
 #undef VST_FPROP

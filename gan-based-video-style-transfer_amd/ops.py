@@ -77,6 +77,10 @@ def weight_pack(w, mode, transposed=False):
              PACK_IK: (Ip, R, S, Op)}[mode]
     out = torch.empty(shape, device=w.device, dtype=torch.float32)
     _call("vst_weight_pack", _p(w), _p(out), O, I_, R, S, Op, Ip, mode, _stream())
+    # the split-arithmetic conv paths read the pack as three bf16 planes (vst_weight_split)
+    split = torch.empty((3,) + shape, device=w.device, dtype=torch.bfloat16)
+    _call("vst_weight_split", _p(out), _p(split), out.numel(), _stream())
+    out.vst_split = split
     return out
 
 
@@ -88,7 +92,8 @@ def conv2d_fwd(x, wp, bias, cop, R, S, stride, pad, pad_mode="zero", act="none",
     Ho = (H + 2 * pad - R) // stride + 1
     Wo = (W + 2 * pad - S) // stride + 1
     y = out if out is not None else torch.empty((N, Ho, Wo, cop), device=x.device)
-    _call("vst_conv2d_fwd", _p(x), _p(wp), _p(bias), _p(y), N, H, W, Cx, cop, R, S, stride, pad,
+    _call("vst_conv2d_fwd", _p(x), _p(wp), _p(getattr(wp, "vst_split", None)), _p(bias), _p(y), N, H,
+          W, Cx, cop, R, S, stride, pad,
           PAD[pad_mode], ACT[act], float(slope), _math(role), _stream())
     return y
 

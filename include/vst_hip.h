@@ -60,6 +60,10 @@ int vst_nhwc_to_nchw(const float* x, float* y, int N, int C, int H, int W, int C
  * Ip/Op are the padded channel strides (multiples of 4, zero filled). */
 int vst_weight_pack(const float* w, float* out, int O, int I, int R, int S, int Op, int Ip,
                     int mode, void* stream);
+/* Split n fp32 values (a weight pack) into three bf16 planes out[0..n) = hi = bf16(v),
+ * out[n..2n) = mid = bf16(v - hi), out[2n..3n) = lo = bf16(v - hi - mid) (2-byte elements).
+ * The split-arithmetic conv paths read these planes as their B operand (`wsplit`). */
+int vst_weight_split(const float* w, void* out, long n, void* stream);
 
 /* ---- convolution (implicit GEMM on MFMA) -------------------------------------------------- */
 /* `math` argument of vst_conv2d_fwd / _tfwd / _wgrad: the GEMM arithmetic of that call.
@@ -78,7 +82,7 @@ enum { VST_MATH_F32 = 0, VST_MATH_BF16X3 = 1, VST_MATH_BF16X6 = 2 };
 /* y[N][Ho][Wo][Cop] = act(conv(x[N][H][W][Cx], w) + bias).  wp = VST_PACK_OK pack
  * ([Cop][R][S][Cx]); bias has Cop entries or is NULL.  pad_mode VST_PAD_ZERO / VST_PAD_REFLECT.
  * Ho = (H + 2*pad - R)/stride + 1. */
-int vst_conv2d_fwd(const float* x, const float* wp, const float* bias, float* y,
+int vst_conv2d_fwd(const float* x, const float* wp, const void* wsplit, const float* bias, float* y,
                    int N, int H, int W, int Cx, int Cop, int R, int S, int stride, int pad,
                    int pad_mode, int act, float slope, int math, void* stream);
 /* Transposed convolution / conv data-gradient (gather form, split by output parity class):

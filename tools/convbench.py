@@ -14,8 +14,8 @@ gbvst._lib.load()
 dev = torch.device("cuda")
 B = int(os.environ.get("B", "4"))
 # name -> (fprop/tconv rk kind, wgrad TileKind)
-TILES = {"auto": (-1, -1), "128x128w8": (0, 0), "64x128": (1, 1), "128x64": (2, 2), "64x64": (3, 3),
-         "128x128k64": (4, 4), "legacy": (-1, 8), "128x128w4": (5, 5), "128x128w4k64": (6, 6)}
+TILES = {"auto": (-1, -1), "k0": (0, 0), "k1": (1, 1), "k2": (2, 2), "k3": (3, 3),
+         "k4": (4, 4), "legacy": (-1, 8), "k5": (5, 5), "k6": (6, 6)}
 if os.environ.get("TILES"):
     TILES = {k: v for k, v in TILES.items() if k in os.environ["TILES"].split(",")}
 ONLY = os.environ.get("LAYERS")

@@ -1,0 +1,29 @@
+"""Developer: launch one conv family on the ResnetBlock shape (B=4, 64x64x256, 3x3 reflect) a few
+times — the target of rocprofv3 --pmc passes.  usage: kbench.py fprop|tconv|wgrad [reps]"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+import gbvst  # noqa: E402
+from gbvst import ops  # noqa: E402
+
+gbvst._lib.load()
+which = sys.argv[1]
+reps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+dev = torch.device("cuda")
+B, H, C = 4, 64, 256
+x = torch.randn(B, H, H, C, device=dev)
+w = torch.randn(C, C, 3, 3, device=dev) * 0.02
+kc, ck = ops.weight_pack(w, ops.PACK_FWD), ops.weight_pack(w, ops.PACK_DGRAD)
+gy = torch.randn(B, H, H, C, device=dev)
+dw = torch.zeros(C, C, 3, 3, device=dev)
+for _ in range(reps):
+    if which == "fprop":
+        ops.conv2d_fwd(x, kc, None, C, 3, 3, 1, 1, "reflect")
+    elif which == "tconv":
+        ops.conv2d_tfwd(gy, ck, None, H, H, C, 3, 3, 1, 1, pad_mode="reflect")
+    else:
+        ops.conv2d_wgrad(x, gy, dw, None, 3, 3, 1, 1, "reflect", C, C, C * 9, 9)
+torch.cuda.synchronize()

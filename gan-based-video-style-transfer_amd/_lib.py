@@ -66,6 +66,27 @@ SIGNATURES = {
     "vst_finish_sum": (I, [P, I, P, D, P]),
     "vst_adam_step": (I, [P, P, P, P, L, F, F, F, F, I, P]),
     "vst_axpby": (I, [P, P, L, F, F, P]),
+    # learning-based style path / RAFT correlation (style.hip, norm.hip, flow.hip)
+    "vst_warp_masked_fwd": (I, [P, P, P, I, I, I, I, I, P]),
+    "vst_warp_masked_bwd_input": (I, [P, P, P, I, I, I, I, I, P]),
+    "vst_instnorm_affine_fwd": (I, [P, P, P, P, P, F, P, P, I, I, I, I, F, P]),
+    "vst_instnorm_affine_ws_bytes": (SZ, [I, I, I]),
+    "vst_instnorm_affine_bwd": (I, [P, P, P, P, P, P, F, P, P, P, P, P, P, I, I, I, I, F, I, P]),
+    "vst_upsample2x_fwd": (I, [P, P, I, I, I, I, P]),
+    "vst_upsample2x_bwd": (I, [P, P, I, I, I, I, P]),
+    "vst_scaled_tanh_fwd": (I, [P, P, L, I, I, P]),
+    "vst_scaled_tanh_bwd": (I, [P, P, P, L, I, I, P]),
+    "vst_channel_normalize": (I, [P, P, P, P, F, L, I, I, I, P]),
+    "vst_maxpool2_fwd": (I, [P, P, I, I, I, I, P]),
+    "vst_maxpool2_bwd": (I, [P, P, P, I, I, I, I, P]),
+    "vst_loss_mse": (I, [P, P, P, P, L, I, I, F, I, P]),
+    "vst_loss_mse_bwd": (I, [P, P, P, P, L, I, I, F, I, P]),
+    "vst_loss_tv": (I, [P, P, P, I, I, I, I, I, F, I, P]),
+    "vst_loss_tv_bwd": (I, [P, P, P, I, I, I, I, I, F, P]),
+    "vst_gram_sym": (I, [P, P, I, F, P]),
+    "vst_corr_pyramid_floats": (L, [L, I, I, L, I]),
+    "vst_corr_pyramid": (I, [P, L, I, I, L, I, P]),
+    "vst_corr_lookup": (I, [P, P, P, I, I, I, I, I, L, I, I, I, P]),
 }
 
 

@@ -53,7 +53,20 @@ __device__ __forceinline__ void for_corners(const Bilin& b, int H, int W, F f) {
   if (inb(b.y0 + 1, b.x0 + 1, H, W)) f(b.y0 + 1, b.x0 + 1, b.se);
 }
 
-// out (NHWC, Cs channels, processed 4 at a time) = warp(x, flow)
+// fs_lib.warp validity (methods/learning-based/fs_lib.py:33-39): grid_sample of a ones image with
+// the same grid, i.e. the in-bounds corner weights summed in nw, ne, sw, se order; the sample is
+// kept iff that sum >= 0.9999 (mask < 0.9999 -> 0, mask > 0 -> 1).
+__device__ __forceinline__ bool warp_valid(const Bilin& b, int H, int W) {
+  float m = 0.f;
+  m += inb(b.y0, b.x0, H, W) ? b.nw : 0.f;
+  m += inb(b.y0, b.x0 + 1, H, W) ? b.ne : 0.f;
+  m += inb(b.y0 + 1, b.x0, H, W) ? b.sw : 0.f;
+  m += inb(b.y0 + 1, b.x0 + 1, H, W) ? b.se : 0.f;
+  return !(m < 0.9999f) && m > 0.f;
+}
+
+// out (NHWC, Cs channels, processed 4 at a time) = warp(x, flow) (MASKED: * fs_lib validity mask)
+template <int MASKED>
 __global__ void warp_fwd_k(const float* __restrict__ x, const float* __restrict__ flow,
                            float* __restrict__ out, int N, int H, int W, int C4, int align) {
   const long total = (long)N * H * W * C4;
@@ -64,6 +77,10 @@ __global__ void warp_fwd_k(const float* __restrict__ x, const float* __restrict_
   const int w = pix % W, h = (pix / W) % H, n = pix / ((long)W * H);
   const long fo = (long)n * 2 * H * W + (long)h * W + w;
   const Bilin b = bilin(h, w, flow[fo], flow[fo + (long)H * W], H, W, align);
+  if (MASKED && !warp_valid(b, H, W)) {
+    reinterpret_cast<float4*>(out)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    return;
+  }
   const float4* xs = reinterpret_cast<const float4*>(x) + (long)n * H * W * C4 + c4;
   float4 v_nw = make_float4(0, 0, 0, 0), v_ne = v_nw, v_sw = v_nw, v_se = v_nw;
   if (inb(b.y0, b.x0, H, W)) v_nw = xs[((long)b.y0 * W + b.x0) * C4];
@@ -78,6 +95,7 @@ __global__ void warp_fwd_k(const float* __restrict__ x, const float* __restrict_
   reinterpret_cast<float4*>(out)[i] = o;
 }
 
+template <int MASKED>
 __global__ void warp_bwd_k(const float* __restrict__ gout, const float* __restrict__ flow,
                            float* __restrict__ gx, int N, int H, int W, int Cs, int align) {
   const long total = (long)N * H * W;
@@ -86,6 +104,7 @@ __global__ void warp_bwd_k(const float* __restrict__ gout, const float* __restri
   const int w = pix % W, h = (pix / W) % H, n = pix / ((long)W * H);
   const long fo = (long)n * 2 * H * W + (long)h * W + w;
   const Bilin b = bilin(h, w, flow[fo], flow[fo + (long)H * W], H, W, align);
+  if (MASKED && !warp_valid(b, H, W)) return;
   const float* g = gout + pix * Cs;
   float* base = gx + (long)n * H * W * Cs;
   for_corners(b, H, W, [&](int y, int xx, float wt) {
@@ -199,18 +218,36 @@ extern "C" int vst_warp_fwd(const float* x, const float* flow, float* out, int N
                             int Cs, int align_corners, void* stream) {
   VST_REQUIRE(x && flow && out && Cs % 4 == 0 && N > 0 && H > 0 && W > 0, "warp_fwd: bad args");
   const long total = (long)N * H * W * (Cs / 4);
-  hipLaunchKernelGGL(warp_fwd_k, dim3(ceil_div(total, 256)), dim3(256), 0, (hipStream_t)stream, x,
+  hipLaunchKernelGGL(warp_fwd_k<0>, dim3(ceil_div(total, 256)), dim3(256), 0, (hipStream_t)stream, x,
                      flow, out, N, H, W, Cs / 4, align_corners);
   return check_launch("warp_fwd");
+}
+
+extern "C" int vst_warp_masked_fwd(const float* x, const float* flow, float* out, int N, int H, int W,
+                                   int Cs, int align_corners, void* stream) {
+  VST_REQUIRE(x && flow && out && Cs % 4 == 0 && N > 0 && H > 0 && W > 0, "warp_masked_fwd: bad args");
+  const long total = (long)N * H * W * (Cs / 4);
+  hipLaunchKernelGGL(warp_fwd_k<1>, dim3(ceil_div(total, 256)), dim3(256), 0, (hipStream_t)stream, x,
+                     flow, out, N, H, W, Cs / 4, align_corners);
+  return check_launch("warp_masked_fwd");
 }
 
 extern "C" int vst_warp_bwd_input(const float* gout, const float* flow, float* gx, int N, int H,
                                   int W, int Cs, int align_corners, void* stream) {
   VST_REQUIRE(gout && flow && gx && Cs > 0, "warp_bwd_input: bad args");
   const long total = (long)N * H * W;
-  hipLaunchKernelGGL(warp_bwd_k, dim3(ceil_div(total, 256)), dim3(256), 0, (hipStream_t)stream, gout,
+  hipLaunchKernelGGL(warp_bwd_k<0>, dim3(ceil_div(total, 256)), dim3(256), 0, (hipStream_t)stream, gout,
                      flow, gx, N, H, W, Cs, align_corners);
   return check_launch("warp_bwd_input");
+}
+
+extern "C" int vst_warp_masked_bwd_input(const float* gout, const float* flow, float* gx, int N, int H,
+                                         int W, int Cs, int align_corners, void* stream) {
+  VST_REQUIRE(gout && flow && gx && Cs > 0, "warp_masked_bwd_input: bad args");
+  const long total = (long)N * H * W;
+  hipLaunchKernelGGL(warp_bwd_k<1>, dim3(ceil_div(total, 256)), dim3(256), 0, (hipStream_t)stream, gout,
+                     flow, gx, N, H, W, Cs, align_corners);
+  return check_launch("warp_masked_bwd_input");
 }
 
 extern "C" int vst_fbcheck(const float* ff, const float* bf, float* mask, int N, int H, int W,

@@ -263,6 +263,200 @@ __global__ void chsum_final_k(const double* __restrict__ part, float* __restrict
   db[c] = accumulate ? db[c] + (float)s[0] : (float)s[0];
 }
 
+
+// ---- affine InstanceNorm (nn.InstanceNorm2d(affine=True), learning-based network.py:147-261) ---
+// y = s * act(gamma[c] * xhat + beta[c]) + residual, xhat = (x - mean) * rstd, computed as ATen's
+// CPU batch-norm transform does: z = x * alpha + (beta - mean * alpha), alpha = rstd * gamma.
+// s = 1, or the ResidualBlock gate s = 2|u| / (1 + |u|), u = gate_mult * gate[0]
+// (network.py:241-245 layer_strength).
+__device__ __forceinline__ float gate_scale(const float* gate, float mult) {
+  if (!gate) return 1.f;
+  const float u = fabsf(mult * gate[0]);
+  return 2.f * u / (1.f + u);
+}
+
+__global__ void in_aff_apply_k(const float4* __restrict__ x, const float* __restrict__ stats,
+                               const float* __restrict__ gamma, const float* __restrict__ beta,
+                               const float* __restrict__ gate, float gate_mult,
+                               const float4* __restrict__ res, float4* __restrict__ y, long total4,
+                               int HW, int C4, int act, float slope) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total4) return;
+  const int c4 = i % C4;
+  const int n = (i / C4) / HW;
+  const float sc = gate_scale(gate, gate_mult);
+  const float* st = stats + ((long)n * C4 + c4) * 8;
+  const float4 v = x[i];
+  const float xv[4] = {v.x, v.y, v.z, v.w};
+  float o[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = 4 * c4 + j;
+    const float al = st[2 * j + 1] * gamma[c];
+    const float be = beta[c] - st[2 * j] * al;
+    float z = apply_act(xv[j] * al + be, act, slope);
+    o[j] = gate ? sc * z : z;
+  }
+  float4 r = make_float4(o[0], o[1], o[2], o[3]);
+  if (res) add_f4(r, res[i]);
+  y[i] = r;
+}
+
+// backward partials per (n, c) slice: {sum gz, sum gz*xhat, sum xhat, sum gy*a},
+// gz = s * gy * act'(z), a = act(z) (the gate-input activation)
+__global__ __launch_bounds__(NRED) void in_aff_partial_k(const float* __restrict__ x,
+                                                         const float* __restrict__ gy,
+                                                         const float* __restrict__ stats,
+                                                         const float* __restrict__ gamma,
+                                                         const float* __restrict__ beta,
+                                                         const float* __restrict__ gate, float gate_mult,
+                                                         double* __restrict__ part, int HW, int C,
+                                                         int LP, int PG, int SP, int nsplit, int act,
+                                                         float slope) {
+  constexpr int NV = 4;
+  __shared__ double red[NV * 4][NRED];
+  const int t = threadIdx.x, c4 = t % LP, pg = t / LP;
+  const int n = blockIdx.y, z = blockIdx.x;
+  const int p0 = z * SP, p1 = min(HW, p0 + SP);
+  const float sc = gate_scale(gate, gate_mult);
+  double acc[NV][4];
+#pragma unroll
+  for (int v = 0; v < NV; ++v)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[v][j] = 0.0;
+  float mean[4], rstd[4], ga[4], be[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = 4 * c4 + j < C ? 4 * c4 + j : 0;
+    mean[j] = stats[2 * ((long)n * C + c)];
+    rstd[j] = stats[2 * ((long)n * C + c) + 1];
+    ga[j] = gamma[c];
+    be[j] = beta[c];
+  }
+  const float4* xb = reinterpret_cast<const float4*>(x) + (long)n * HW * LP + c4;
+  const float4* gb = reinterpret_cast<const float4*>(gy) + (long)n * HW * LP + c4;
+  for (int p = p0 + pg; pg < PG && p < p1; p += PG) {
+    const float4 v = xb[(long)p * LP];
+    const float4 gv = gb[(long)p * LP];
+    const float xv[4] = {v.x, v.y, v.z, v.w};
+    const float gg[4] = {gv.x, gv.y, gv.z, gv.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float xh = (xv[j] - mean[j]) * rstd[j];
+      const float al = rstd[j] * ga[j];
+      const float zz = xv[j] * al + (be[j] - mean[j] * al);
+      float d = 1.f;
+      if (act == VST_ACT_RELU) d = zz > 0.f ? 1.f : 0.f;
+      else if (act == VST_ACT_LRELU) d = zz > 0.f ? 1.f : slope;
+      const float g = sc * gg[j] * d;
+      acc[0][j] += g;
+      acc[1][j] += (double)g * xh;
+      acc[2][j] += xh;
+      acc[3][j] += (double)gg[j] * apply_act(zz, act, slope);
+    }
+  }
+#pragma unroll
+  for (int v = 0; v < NV; ++v)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) red[v * 4 + j][t] = acc[v][j];
+  __syncthreads();
+  if (pg == 0) {
+    double* dst = part + (((long)n * nsplit + z) * C + 4 * c4) * NV;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int v = 0; v < NV; ++v) {
+        double s = 0.0;
+        for (int q = 0; q < PG; ++q) s += red[v * 4 + j][q * LP + c4];
+        dst[j * NV + v] = s;
+      }
+  }
+}
+
+// coef[n*C+c] = {mean gz, mean gz*xhat}; sums[n*C+c] = {sum gz, sum gz*xhat, sum gy*a, dbias}
+__global__ void in_aff_finalize_k(const double* __restrict__ part, const float* __restrict__ stats,
+                                  const float* __restrict__ gamma, float2* __restrict__ coef,
+                                  double* __restrict__ sums, int N, int HW, int C, int nsplit) {
+  double a[4];
+  const int n = blockIdx.y;
+  if (!fold_slices<4>(part, n, C, nsplit, a)) return;
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int idx = n * C + c;
+  const double mg = a[0] / HW, mgx = a[1] / HW;
+  coef[idx] = make_float2((float)mg, (float)mgx);
+  const double rstd = stats[2 * idx + 1];
+  sums[4 * idx + 0] = a[0];
+  sums[4 * idx + 1] = a[1];
+  sums[4 * idx + 2] = a[3];
+  sums[4 * idx + 3] = rstd * gamma[c] * ((a[0] - HW * mg) - mgx * a[2]);
+}
+
+// one block: dgamma/dbeta/dbias per channel (sum over n, fixed order) and the gate gradient
+__global__ void in_aff_param_grad_k(const double* __restrict__ sums, float* __restrict__ dgamma,
+                                    float* __restrict__ dbeta, float* __restrict__ dbias,
+                                    const float* __restrict__ gate, float gate_mult,
+                                    float* __restrict__ dgate, int N, int C, int accumulate) {
+  __shared__ double red[4];
+  double ds = 0.0;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    double sg = 0.0, sgx = 0.0, sb = 0.0;
+    for (int n = 0; n < N; ++n) {
+      const double* q = sums + 4 * ((long)n * C + c);
+      sg += q[0];
+      sgx += q[1];
+      ds += q[2];
+      sb += q[3];
+    }
+    if (dgamma) dgamma[c] = accumulate ? dgamma[c] + (float)sgx : (float)sgx;
+    if (dbeta) dbeta[c] = accumulate ? dbeta[c] + (float)sg : (float)sg;
+    if (dbias) dbias[c] = accumulate ? dbias[c] + (float)sb : (float)sb;
+  }
+  if (!gate || !dgate) return;
+  ds = wave_sum_d(ds);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ds;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const double tot = red[0] + red[1] + red[2] + red[3];
+    const float u = gate_mult * gate[0];
+    const float au = fabsf(u);
+    const float du = 2.f / ((1.f + au) * (1.f + au)) * (u > 0.f ? 1.f : (u < 0.f ? -1.f : 0.f));
+    const float g = (float)tot * du * gate_mult;
+    dgate[0] = accumulate ? dgate[0] + g : g;
+  }
+}
+
+__global__ void in_aff_bwd_apply_k(const float4* __restrict__ gy, const float4* __restrict__ x,
+                                   const float* __restrict__ stats, const float* __restrict__ gamma,
+                                   const float* __restrict__ beta, const float* __restrict__ gate,
+                                   float gate_mult, const float2* __restrict__ coef,
+                                   float4* __restrict__ dx, long total4, int HW, int C4, int act,
+                                   float slope) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total4) return;
+  const int c4 = i % C4;
+  const int n = (i / C4) / HW;
+  const float sc = gate_scale(gate, gate_mult);
+  const long nc = (long)n * C4 * 4 + 4 * c4;
+  const float4 g4 = gy[i], v = x[i];
+  const float gg[4] = {g4.x, g4.y, g4.z, g4.w}, xv[4] = {v.x, v.y, v.z, v.w};
+  float o[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = 4 * c4 + j;
+    const float mean = stats[2 * (nc + j)], rstd = stats[2 * (nc + j) + 1];
+    const float al = rstd * gamma[c];
+    const float zz = xv[j] * al + (beta[c] - mean * al);
+    float d = 1.f;
+    if (act == VST_ACT_RELU) d = zz > 0.f ? 1.f : 0.f;
+    else if (act == VST_ACT_LRELU) d = zz > 0.f ? 1.f : slope;
+    const float g = sc * gg[j] * d;
+    const float xh = (xv[j] - mean) * rstd;
+    const float2 k = coef[nc + j];
+    o[j] = al * (g - k.x - xh * k.y);
+  }
+  dx[i] = make_float4(o[0], o[1], o[2], o[3]);
+}
+
 }  // namespace vst
 
 using namespace vst;
@@ -348,4 +542,52 @@ extern "C" int vst_channel_sum(const float* x, float* db, float* ws, long NHW, i
   hipLaunchKernelGGL(chsum_final_k, dim3(ceil_div(Cs, 64)), dim3(256), 0, s, part, db, g.nsplit, Cs, Cl,
                      accumulate);
   return check_launch("channel_sum");
+}
+
+extern "C" size_t vst_instnorm_affine_ws_bytes(int N, int HW, int C) {
+  RedGeom g;
+  if (!red_geom(N, HW, C, g)) return 0;
+  return (size_t)N * g.nsplit * C * 4 * sizeof(double) + (size_t)N * C * (sizeof(float2) + 4 * sizeof(double)) +
+         256;
+}
+
+extern "C" int vst_instnorm_affine_fwd(const float* x, const float* stats, const float* gamma,
+                                       const float* beta, const float* gate, float gate_mult,
+                                       const float* residual, float* y, int N, int HW, int C, int act,
+                                       float slope, void* stream) {
+  VST_REQUIRE(x && stats && gamma && beta && y && C % 4 == 0 && N > 0 && HW > 0,
+              "instnorm_affine_fwd: bad args");
+  const long total4 = (long)N * HW * C / 4;
+  hipLaunchKernelGGL(in_aff_apply_k, dim3(ceil_div(total4, 256)), dim3(256), 0, (hipStream_t)stream,
+                     reinterpret_cast<const float4*>(x), stats, gamma, beta, gate, gate_mult,
+                     reinterpret_cast<const float4*>(residual), reinterpret_cast<float4*>(y), total4, HW,
+                     C / 4, act, slope);
+  return check_launch("instnorm_affine_fwd");
+}
+
+extern "C" int vst_instnorm_affine_bwd(const float* gy, const float* x, const float* stats,
+                                       const float* gamma, const float* beta, const float* gate,
+                                       float gate_mult, float* dx, float* dgamma, float* dbeta,
+                                       float* dgate, float* dbias, float* ws, int N, int HW, int C,
+                                       int act, float slope, int accumulate, void* stream) {
+  RedGeom g;
+  VST_REQUIRE(gy && x && stats && gamma && beta && dx && ws && red_geom(N, HW, C, g),
+              "instnorm_affine_bwd: bad args (C must be 4*2^k <= 1024)");
+  hipStream_t s = (hipStream_t)stream;
+  double* part = reinterpret_cast<double*>(ws);
+  char* p = reinterpret_cast<char*>(ws) + (size_t)N * g.nsplit * C * 4 * sizeof(double);
+  float2* coef = reinterpret_cast<float2*>(p);
+  double* sums = reinterpret_cast<double*>(p + (size_t)N * C * sizeof(float2));
+  hipLaunchKernelGGL(in_aff_partial_k, dim3(g.nsplit, N), dim3(NRED), 0, s, x, gy, stats, gamma, beta,
+                     gate, gate_mult, part, HW, C, g.LP, g.PG, g.SP, g.nsplit, act, slope);
+  hipLaunchKernelGGL(in_aff_finalize_k, dim3(ceil_div(C, 64), N), dim3(256), 0, s, part, stats, gamma,
+                     coef, sums, N, HW, C, g.nsplit);
+  hipLaunchKernelGGL(in_aff_param_grad_k, dim3(1), dim3(256), 0, s, sums, dgamma, dbeta, dbias, gate,
+                     gate_mult, dgate, N, C, accumulate);
+  const long total4 = (long)N * HW * C / 4;
+  hipLaunchKernelGGL(in_aff_bwd_apply_k, dim3(ceil_div(total4, 256)), dim3(256), 0, s,
+                     reinterpret_cast<const float4*>(gy), reinterpret_cast<const float4*>(x), stats, gamma,
+                     beta, gate, gate_mult, coef, reinterpret_cast<float4*>(dx), total4, HW, C / 4, act,
+                     slope);
+  return check_launch("instnorm_affine_bwd");
 }

@@ -314,3 +314,192 @@ def adam_step(p, g, m, v, lr, beta1, beta2, eps, step):
 def axpby(x, y, a, b):
     _dev_check(x, y)
     _call("vst_axpby", _p(x), _p(y), x.numel(), float(a), float(b), _stream())
+
+
+# ------------------------------------------------------------- learning-based style path
+def warp_masked_nhwc(x, flow, align_corners=False):
+    """fs_lib.warp (methods/learning-based/fs_lib.py:5-39): warp * grid_sample(ones) validity."""
+    _dev_check(x, flow)
+    N, H, W, C = x.shape
+    out = torch.empty_like(x)
+    _call("vst_warp_masked_fwd", _p(x), _p(flow), _p(out), N, H, W, C, int(align_corners), _stream())
+    return out
+
+
+def warp_masked_bwd_nhwc(gout, flow, align_corners=False):
+    _dev_check(gout, flow)
+    N, H, W, C = gout.shape
+    gx = torch.zeros_like(gout)
+    _call("vst_warp_masked_bwd_input", _p(gout), _p(flow), _p(gx), N, H, W, C, int(align_corners),
+          _stream())
+    return gx
+
+
+def instnorm_affine_fwd(y, stats, gamma, beta, act="none", gate=None, gate_mult=1.0, residual=None,
+                        slope=0.0):
+    """s * act(gamma * IN(y) + beta) + residual (vst_instnorm_affine_fwd); gamma/beta padded to C."""
+    _dev_check(y, stats, gamma, beta, gate, residual)
+    N, H, W, C = y.shape
+    out = torch.empty_like(y)
+    _call("vst_instnorm_affine_fwd", _p(y), _p(stats), _p(gamma), _p(beta), _p(gate), float(gate_mult),
+          _p(residual), _p(out), N, H * W, C, ACT[act], float(slope), _stream())
+    return out
+
+
+def instnorm_affine_bwd(g, y, stats, gamma, beta, act="none", gate=None, gate_mult=1.0, dgamma=None,
+                        dbeta=None, dgate=None, dbias=None, accumulate=True, slope=0.0):
+    _dev_check(g, y, stats, gamma, beta, gate)
+    N, H, W, C = y.shape
+    dx = torch.empty_like(y)
+    nbytes = lib().vst_instnorm_affine_ws_bytes(N, H * W, C)
+    ws = torch.empty((nbytes + 7) // 8, dtype=torch.float64, device=y.device)
+    _call("vst_instnorm_affine_bwd", _p(g), _p(y), _p(stats), _p(gamma), _p(beta), _p(gate),
+          float(gate_mult), _p(dx), _p(dgamma), _p(dbeta), _p(dgate), _p(dbias), _p(ws), N, H * W, C,
+          ACT[act], float(slope), 1 if accumulate else 0, _stream())
+    return dx
+
+
+def upsample2x(x):
+    _dev_check(x)
+    N, H, W, C = x.shape
+    y = torch.empty((N, 2 * H, 2 * W, C), device=x.device)
+    _call("vst_upsample2x_fwd", _p(x), _p(y), N, H, W, C, _stream())
+    return y
+
+
+def upsample2x_bwd(gy):
+    _dev_check(gy)
+    N, H2, W2, C = gy.shape
+    gx = torch.empty((N, H2 // 2, W2 // 2, C), device=gy.device)
+    _call("vst_upsample2x_bwd", _p(gy), _p(gx), N, H2 // 2, W2 // 2, C, _stream())
+    return gx
+
+
+def scaled_tanh(x, cl=3):
+    _dev_check(x)
+    y = torch.empty_like(x)
+    _call("vst_scaled_tanh_fwd", _p(x), _p(y), x.numel() // x.shape[-1], x.shape[-1], cl, _stream())
+    return y
+
+
+def scaled_tanh_bwd(x, gy, cl=3):
+    _dev_check(x, gy)
+    gx = torch.empty_like(x)
+    _call("vst_scaled_tanh_bwd", _p(x), _p(gy), _p(gx), x.numel() // x.shape[-1], x.shape[-1], cl,
+          _stream())
+    return gx
+
+
+def channel_normalize(x, mean, std, d0=1.0, cl=3, backward=False):
+    """((x / d0) - mean[c]) / std[c] (backward: (x / std[c]) / d0); mean/std device tensors [cl]."""
+    _dev_check(x, mean, std)
+    y = torch.empty_like(x)
+    _call("vst_channel_normalize", _p(x), _p(y), _p(mean), _p(std), float(d0),
+          x.numel() // x.shape[-1], x.shape[-1], cl, 1 if backward else 0, _stream())
+    return y
+
+
+def maxpool2(x):
+    _dev_check(x)
+    N, H, W, C = x.shape
+    y = torch.empty((N, H // 2, W // 2, C), device=x.device)
+    _call("vst_maxpool2_fwd", _p(x), _p(y), N, H, W, C, _stream())
+    return y
+
+
+def maxpool2_bwd(gy, x):
+    _dev_check(gy, x)
+    N, H, W, C = x.shape
+    gx = torch.empty_like(x)
+    _call("vst_maxpool2_bwd", _p(gy), _p(x), _p(gx), N, H, W, C, _stream())
+    return gx
+
+
+def loss_mse(a, b, scale=1.0, cl=None, out=None, accumulate=False):
+    """scale * mean((a - b)^2) over the cl logical channels (default all)."""
+    _dev_check(a, b)
+    cs = a.shape[-1]
+    npix = a.numel() // cs
+    loss = out if out is not None else torch.zeros((), device=a.device)
+    _call("vst_loss_mse", _p(a), _p(b), _p(loss), _p(_part(npix, a.device)), npix, cs, cl or cs,
+          float(scale), 1 if accumulate else 0, _stream())
+    return loss
+
+
+def loss_mse_bwd(a, b, gout, scale=1.0, cl=None, grad=None):
+    cs = a.shape[-1]
+    npix = a.numel() // cs
+    acc = grad is not None
+    g = grad if acc else torch.empty_like(a)
+    _call("vst_loss_mse_bwd", _p(a), _p(b), _p(gout), _p(g), npix, cs, cl or cs, float(scale),
+          1 if acc else 0, _stream())
+    return g
+
+
+def loss_tv(img, scale=1.0, cl=3):
+    _dev_check(img)
+    N, H, W, C = img.shape
+    loss = torch.zeros((), device=img.device)
+    _call("vst_loss_tv", _p(img), _p(loss), _p(_part(N * (H - 1) * (W - 1), img.device)), N, H, W, C, cl,
+          float(scale), 0, _stream())
+    return loss
+
+
+def loss_tv_bwd(img, gout, scale=1.0, cl=3):
+    N, H, W, C = img.shape
+    g = torch.empty_like(img)
+    _call("vst_loss_tv_bwd", _p(img), _p(gout), _p(g), N, H, W, C, cl, float(scale), _stream())
+    return g
+
+
+def gram(f, role="fwd"):
+    """G[b] = F_b^T F_b / (h*w) for NHWC features f [B][h][w][C] -> [B][C][C]
+    (fast_style_transfer.py:813-817).  Each G[b] is the weight gradient of a 1x1 conv whose input
+    and output gradient are both F_b, i.e. the split-K MFMA wgrad kernel."""
+    _dev_check(f)
+    B, h, w, C = f.shape
+    G = torch.empty((B, C, C), device=f.device)
+    for b in range(B):
+        fb = f[b:b + 1]
+        conv2d_wgrad(fb, fb, G[b], None, 1, 1, 1, 0, "zero", C, C, C, 1, accumulate=False, role=role)
+    axpby(G, G, 1.0 / (h * w), 0.0)
+    return G
+
+
+def split_planes(wp):
+    """Attach the bf16 split planes (vst_weight_split) the split-arithmetic conv paths read."""
+    split = torch.empty((3,) + tuple(wp.shape), device=wp.device, dtype=torch.bfloat16)
+    _call("vst_weight_split", _p(wp), _p(split), wp.numel(), _stream())
+    wp.vst_split = split
+    return wp
+
+
+def gram_bwd(f, dG, role="bwd"):
+    """dF_b = F_b (dG_b + dG_b^T) / (h*w): a 1x1 conv of F_b with weight S_b (vst_gram_sym)."""
+    _dev_check(f, dG)
+    B, h, w, C = f.shape
+    df = torch.empty_like(f)
+    for b in range(B):
+        S = torch.empty((C, 1, 1, C), device=f.device)
+        _call("vst_gram_sym", _p(dG[b]), _p(S), C, float(1.0 / (h * w)), _stream())
+        split_planes(S)
+        conv2d_fwd(f[b:b + 1], S, None, C, 1, 1, 1, 0, out=df[b:b + 1], role=role)
+    return df
+
+
+def corr_pyramid_floats(P, H2, W2, ld0, levels):
+    return lib().vst_corr_pyramid_floats(P, H2, W2, ld0, levels)
+
+
+def corr_pyramid(pyr, P, H2, W2, ld0, levels):
+    _call("vst_corr_pyramid", _p(pyr), P, H2, W2, ld0, levels, _stream())
+
+
+def corr_lookup(pyr, coords, B, H1, W1, H2, W2, ld0, levels, radius):
+    _dev_check(pyr, coords)
+    K = 2 * radius + 1
+    cs = cpad(levels * K * K)
+    out = torch.empty((B, H1, W1, cs), device=pyr.device)
+    _call("vst_corr_lookup", _p(pyr), _p(coords), _p(out), B, H1, W1, H2, W2, ld0, levels, radius, cs,
+          _stream())
+    return out

@@ -27,6 +27,19 @@
  *   vst_loss_*                  networks.py:209-275 GANLoss('lsgan'), torch.nn.L1Loss
  *                               (cycle_gan_model.py:94-95), temporal loss cycle_gan_model.py:204
  *   vst_adam_step               torch.optim.Adam as constructed at cycle_gan_model.py:97-98
+ *   vst_warp_masked_*           methods/learning-based/fs_lib.py:5-39 warp (grid_sample * validity mask)
+ *   vst_instnorm_affine_*       nn.InstanceNorm2d(affine=True) (+ReLU, + ResidualBlock layer_strength
+ *                               gate) of methods/learning-based/network.py:147-298 (FastStyleNet)
+ *   vst_upsample2x_*            F.interpolate(scale_factor=2) in network.py:206-207
+ *   vst_scaled_tanh_*           ConvTanh network.py:111-118
+ *   vst_channel_normalize       fast_style_transfer.py:819-822 normalize (+ the fs_johnson.py:31 /255)
+ *   vst_maxpool2_*              torchvision VGG MaxPool2d(2,2) used by network.py:10-78 (Vgg16/Vgg19)
+ *   vst_loss_mse / _tv, vst_gram_sym
+ *                               fs_johnson.py:35-47 content / style / TV losses and the backward of
+ *                               fast_style_transfer.py:813-817 gram_matrix (Gram itself = 1x1 wgrad)
+ *   vst_corr_pyramid / vst_corr_lookup
+ *                               utils/raft/raft/corr.py:12-60 CorrBlock (all-pairs volume = 1x1 conv
+ *                               GEMM on vst_conv2d_fwd) + utils/raft/raft/utils/utils.py:57-71
  */
 #ifndef VST_HIP_H
 #define VST_HIP_H
@@ -193,6 +206,70 @@ int vst_adam_step(float* p, const float* g, float* m, float* v, long n, float lr
                   float beta2, float eps, int step, void* stream);
 /* y = a*x + b*y over n floats (gradient scaling / DP averaging helper). */
 int vst_axpby(const float* x, float* y, long n, float a, float b, void* stream);
+
+/* ---- learning-based style path -------------------------------------- */
+/* fs_lib.warp: warp(x, flow) * (grid_sample(ones) >= 0.9999).  Same layouts as vst_warp_fwd; the
+ * backward scatters only through kept samples (gx accumulated, must be zero-initialised). */
+int vst_warp_masked_fwd(const float* x, const float* flow, float* out, int N, int H, int W, int Cs,
+                        int align_corners, void* stream);
+int vst_warp_masked_bwd_input(const float* gout, const float* flow, float* gx, int N, int H, int W,
+                              int Cs, int align_corners, void* stream);
+/* Affine instance norm: y = s * act(gamma[c] * xhat + beta[c]) + residual, with stats from
+ * vst_instnorm_stats; s = 1 (gate NULL) or s = 2|u|/(1+|u|), u = gate_mult * gate[0] (device scalar:
+ * ResidualBlock layer_strength, network.py:241-245).  residual may be NULL.  C = 4*2^k <= 1024. */
+int vst_instnorm_affine_fwd(const float* x, const float* stats, const float* gamma, const float* beta,
+                            const float* gate, float gate_mult, const float* residual, float* y,
+                            int N, int HW, int C, int act, float slope, void* stream);
+/* Backward: dx written; dgamma/dbeta/dgate/dbias (each may be NULL) written or accumulated
+ * (accumulate != 0).  dbias is the gradient of a conv bias feeding the norm (exact per-channel sum
+ * of dx).  ws: vst_instnorm_affine_ws_bytes bytes.  Reductions fp64, fixed order. */
+size_t vst_instnorm_affine_ws_bytes(int N, int HW, int C);
+int vst_instnorm_affine_bwd(const float* gy, const float* x, const float* stats, const float* gamma,
+                            const float* beta, const float* gate, float gate_mult, float* dx,
+                            float* dgamma, float* dbeta, float* dgate, float* dbias, float* ws, int N,
+                            int HW, int C, int act, float slope, int accumulate, void* stream);
+/* Nearest 2x upsample of NHWC (Cs % 4 == 0): y [N][2H][2W][Cs]; backward sums each 2x2 block. */
+int vst_upsample2x_fwd(const float* x, float* y, int N, int H, int W, int Cs, void* stream);
+int vst_upsample2x_bwd(const float* gy, float* gx, int N, int H, int W, int Cs, void* stream);
+/* ConvTanh: y = tanh(x/255)*150 + 127.5 on the Cl logical channels (padding channels 0);
+ * backward from the saved pre-activation x. */
+int vst_scaled_tanh_fwd(const float* x, float* y, long npix, int Cs, int Cl, void* stream);
+int vst_scaled_tanh_bwd(const float* x, const float* gy, float* gx, long npix, int Cs, int Cl,
+                        void* stream);
+/* y = ((x / d0) - mean[c]) / std[c] (mean may be NULL = 0); backward != 0: y = (x / std[c]) / d0.
+ * mean/std: device arrays of Cl floats.  Padding channels written 0. */
+int vst_channel_normalize(const float* x, float* y, const float* mean, const float* stdv, float d0,
+                          long npix, int Cs, int Cl, int backward, void* stream);
+/* MaxPool2d(2, 2) (floor mode) on NHWC; backward writes every gx element (first max wins ties). */
+int vst_maxpool2_fwd(const float* x, float* y, int N, int H, int W, int Cs, void* stream);
+int vst_maxpool2_bwd(const float* gy, const float* x, float* gx, int N, int H, int W, int Cs,
+                     void* stream);
+/* loss (+)= scale * mean((a - b)^2) over npix*Cl elements; grad (+)= gout*scale*2(a-b)/count. */
+int vst_loss_mse(const float* a, const float* b, float* loss, float* part, long npix, int Cs, int Cl,
+                 float scale, int accumulate, void* stream);
+int vst_loss_mse_bwd(const float* a, const float* b, const float* gout, float* grad, long npix,
+                     int Cs, int Cl, float scale, int accumulate, void* stream);
+/* calc_tv_loss: loss (+)= scale * sum_{n,y<H-1,x<W-1} sqrt(|I[y+1][x]-I[y][x]|^2 + |I[y][x+1]-I[y][x]|^2)
+ * (norms over the Cl <= 4 logical channels); backward writes grad (zero-length terms give 0). */
+int vst_loss_tv(const float* img, float* loss, float* part, int N, int H, int W, int Cs, int Cl,
+                float scale, int accumulate, void* stream);
+int vst_loss_tv_bwd(const float* img, const float* gout, float* grad, int N, int H, int W, int Cs,
+                    int Cl, float scale, void* stream);
+/* Gram backward weight: S = (dG + dG^T) * scale, [C][C] — dF = F * S is then a 1x1 vst_conv2d_fwd.
+ * (The Gram itself, G = F^T F, is vst_conv2d_wgrad of a 1x1 conv with x = dy = F.) */
+int vst_gram_sym(const float* dG, float* S, int C, float scale, void* stream);
+
+/* ---- RAFT correlation pyramid ---------------------------------------------- */
+/* Level 0 (P = B*H1*W1 planes of H2*W2, plane stride ld0) is the all-pairs GEMM output
+ * fmap1^T fmap2 / sqrt(D) produced by vst_conv2d_fwd (1x1 conv, fmap2 as the weight).  Levels
+ * 1..levels-1 (avg_pool2d 2x2, floor) follow it packed in the same buffer. */
+long vst_corr_pyramid_floats(long P, int H2, int W2, long ld0, int levels);
+int vst_corr_pyramid(float* pyr, long P, int H2, int W2, long ld0, int levels, void* stream);
+/* out[b][h][w][c] (NHWC, Cs >= levels*(2r+1)^2, extra channels 0): CorrBlock.__call__ window
+ * lookup at coords [B][2][H1][W1] (x, y pixel coordinates); channel lvl*(2r+1)^2 + a*(2r+1) + c
+ * samples x + (a - r), y + (c - r) at level lvl (align_corners=True bilinear, zeros outside). */
+int vst_corr_lookup(const float* pyr, const float* coords, float* out, int B, int H1, int W1, int H2,
+                    int W2, long ld0, int levels, int radius, int Cs, void* stream);
 
 #ifdef __cplusplus
 }

@@ -80,3 +80,21 @@ def test_ops_refuse_cpu_tensors():
     from gbvst import ops
     with pytest.raises(RuntimeError):
         ops.nchw_to_nhwc(torch.zeros(1, 3, 4, 4))
+
+
+def test_style_modules_match_reference_layout():
+    """FastStyleNet / Vgg16 / Vgg19 keep network.py's module tree: identical state_dict keys and
+    shapes (reference checkpoints load by name), 1,679,240 FastStyleNet(3, 1) parameters."""
+    from gbvst import faststyle, perceptual
+    from oracle import style_ref
+    n = faststyle.FastStyleNet(3, 1)
+    assert cpu_state(n) == cpu_state(style_ref.RefFastStyleNet(3))
+    assert sum(p.numel() for p in n.parameters()) == 1679240
+    assert cpu_state(perceptual.Vgg16()) == cpu_state(style_ref.RefVGG("vgg16"))
+    assert cpu_state(perceptual.Vgg19()) == cpu_state(style_ref.RefVGG("vgg19"))
+    with pytest.raises(NotImplementedError):
+        faststyle.FastStyleNet(3, n_styles=2)
+
+
+def cpu_state(net):
+    return {k: tuple(v.shape) for k, v in net.state_dict().items()}

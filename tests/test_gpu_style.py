@@ -1,0 +1,301 @@
+"""GPU parity of the learning-based style path and the RAFT correlation:
+libvst_hip kernels against the reference-produced fixtures (tests/golden/style_small.npz,
+corr_small.npz) and against the CPU oracle (oracle/style_ref.py, stock torch fp32).
+
+Tolerances (relative to max|ref| unless stated): streaming ops 1e-5 (maxpool / upsample exact);
+affine InstanceNorm 1e-4; Gram / networks' outputs and input gradients 1e-4 (their convs run the
+fp32-equivalent bf16x6 forward; gradients bf16x3, ~1e-5); parameter gradients 1e-3; Johnson losses
+1e-3 (north_star); corr volume / lookup 1e-4 (bf16x3 inference GEMM)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module")
+def gb():
+    import gbvst
+    gbvst._lib.load()
+    return gbvst
+
+
+def _rel(got, ref):
+    got = got.detach().float().cpu().numpy() if torch.is_tensor(got) else np.asarray(got)
+    ref = ref.detach().float().cpu().numpy() if torch.is_tensor(ref) else np.asarray(ref)
+    assert got.shape == ref.shape, (got.shape, ref.shape)
+    return float(np.abs(got.astype(np.float64) - ref).max() / (np.abs(ref).max() + 1e-30))
+
+
+def _g(seed, shape, scale=1.0):
+    return torch.randn(*shape, generator=torch.Generator().manual_seed(seed)) * scale
+
+
+def _nhwc(x, ops):
+    return ops.nchw_to_nhwc(x.to(DEV).contiguous())
+
+
+def _nchw(y, c, ops):
+    return ops.nhwc_to_nchw(y.contiguous(), c).cpu()
+
+
+# ------------------------------------------------------------------------------ fs_lib warp
+def test_fs_warp_vs_reference_golden(gb, golden):
+    from gbvst import fs_lib
+    g = golden("style_small")
+    for case in ("zero", "frac", "oob"):
+        x = torch.from_numpy(g["fsw_x"]).to(DEV).requires_grad_(True)
+        y = fs_lib.warp(x, torch.from_numpy(g[f"fsw_{case}_flow"]).to(DEV))
+        y.backward(torch.from_numpy(g["fsw_gout"]).to(DEV))
+        assert np.abs(y.detach().cpu().numpy() - g[f"fsw_{case}_y"]).max() < 2e-6, case
+        assert np.abs(x.grad.cpu().numpy() - g[f"fsw_{case}_dx"]).max() < 2e-6, case
+
+
+# ------------------------------------------------------------------------- affine instance norm
+@pytest.mark.parametrize("act,gated", [("relu", False), ("none", True), ("none", False)])
+def test_instnorm_affine_fwd_bwd(gb, act, gated):
+    from gbvst import ops
+    N, C, H, W = 2, 32, 12, 20
+    x = _g(1, (N, C, H, W)) * 2 + 0.5
+    gam = (_g(2, (C,), 0.2) + 1).requires_grad_(True)
+    bet = _g(3, (C,), 0.2).requires_grad_(True)
+    ls = torch.tensor([0.7], requires_grad=True)
+    res = _g(4, (N, C, H, W))
+    xr = x.clone().requires_grad_(True)
+    z = F.instance_norm(xr, weight=gam, bias=bet, eps=1e-5)
+    if act == "relu":
+        z = F.relu(z)
+    if gated:
+        s = 0.9 * ls
+        s = 2 * s.abs() / (1 + s.abs())
+        z = s * z + res
+    gy = _g(5, tuple(z.shape))
+    z.backward(gy)
+    xn = _nhwc(x, ops)
+    st = ops.instnorm_stats(xn)
+    gd, bd, lsd = gam.detach().to(DEV), bet.detach().to(DEV), ls.detach().to(DEV)
+    kw = dict(gate=lsd, gate_mult=0.9, residual=_nhwc(res, ops)) if gated else {}
+    y = ops.instnorm_affine_fwd(xn, st, gd, bd, act, **kw)
+    assert _rel(_nchw(y, C, ops), z) < 1e-5
+    dgam, dbet, dls = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV), torch.zeros(1, device=DEV)
+    dbias = torch.full((C,), 0.5, device=DEV)
+    kw.pop("residual", None)
+    dx = ops.instnorm_affine_bwd(_nhwc(gy, ops), xn, st, gd, bd, act, dgamma=dgam, dbeta=dbet,
+                                 dgate=dls if gated else None, dbias=dbias, accumulate=True, **kw)
+    assert _rel(_nchw(dx, C, ops), xr.grad) < 1e-4
+    assert _rel(dgam, gam.grad) < 1e-4 and _rel(dbet, bet.grad) < 1e-4
+    if gated:
+        assert _rel(dls, ls.grad) < 1e-4
+    # a conv bias in front of the norm has an exactly-zero gradient: only rounding noise remains
+    assert (dbias.cpu() - 0.5).abs().max().item() < 1e-3
+
+
+# ---------------------------------------------------------------------- streaming elementwise
+def test_upsample_tanh_normalize_maxpool(gb):
+    from gbvst import ops
+    N, C, H, W = 2, 8, 10, 14
+    x = _g(11, (N, C, H, W))
+    xr = x.clone().requires_grad_(True)
+    up = F.interpolate(xr, scale_factor=2)
+    gu = _g(12, tuple(up.shape))
+    up.backward(gu)
+    xn = _nhwc(x, ops)
+    assert _rel(_nchw(ops.upsample2x(xn), C, ops), up) == 0.0
+    assert _rel(_nchw(ops.upsample2x_bwd(_nhwc(gu, ops)), C, ops), xr.grad) < 1e-6
+    # ConvTanh epilogue on 3 logical channels of an NHWC4 tensor; padding channel stays 0
+    t = (_g(13, (N, 3, H, W)) * 200).requires_grad_(True)
+    yt = torch.tanh(t / 255) * 150 + 255 / 2
+    gt = _g(14, tuple(yt.shape))
+    yt.backward(gt)
+    tn = _nhwc(t.detach(), ops)
+    yn = ops.scaled_tanh(tn, 3)
+    assert _rel(_nchw(yn, 3, ops), yt) < 1e-6 and yn[..., 3].abs().max().item() == 0
+    assert _rel(_nchw(ops.scaled_tanh_bwd(tn, _nhwc(gt, ops), 3), 3, ops), t.grad) < 1e-5
+    # normalize((img / 255)) and its backward
+    from gbvst import perceptual
+    img = (torch.rand(N, 3, H, W, generator=torch.Generator().manual_seed(15)) * 255).requires_grad_(True)
+    ref = perceptual_ref_normalize(img / 255.0)
+    gn = _g(16, tuple(ref.shape))
+    ref.backward(gn)
+    imn = _nhwc(img.detach(), ops).requires_grad_(True)
+    out = perceptual.normalize_nhwc(imn, d0=255.0)
+    out.backward(_nhwc(gn, ops))
+    assert _rel(_nchw(out.detach(), 3, ops), ref) < 1e-6
+    assert _rel(_nchw(imn.grad, 3, ops), img.grad) < 1e-6
+    # max pool with ties and odd sizes (floor mode): first maximum in scan order wins
+    xm = torch.round(_g(17, (N, C, 11, 13)) * 2) / 2
+    xmr = xm.clone().requires_grad_(True)
+    ym = F.max_pool2d(xmr, 2, 2)
+    gm = _g(18, tuple(ym.shape))
+    ym.backward(gm)
+    xmn = _nhwc(xm, ops)
+    assert _rel(_nchw(ops.maxpool2(xmn), C, ops), ym) == 0.0
+    assert _rel(_nchw(ops.maxpool2_bwd(_nhwc(gm, ops), xmn), C, ops), xmr.grad) == 0.0
+
+
+def perceptual_ref_normalize(img):
+    from oracle import style_ref
+    return style_ref.normalize(img)
+
+
+def test_mse_tv_gram(gb):
+    from gbvst import ops, perceptual
+    from oracle import style_ref
+    a = _g(21, (2, 16, 9, 11)).requires_grad_(True)
+    b = _g(22, (2, 16, 9, 11))
+    ref = F.mse_loss(a, b) * 3.0
+    ref.backward()
+    an, bn = _nhwc(a.detach(), ops).requires_grad_(True), _nhwc(b, ops)
+    got = perceptual.mse_loss(an, bn, 3.0)
+    got.backward()
+    assert _rel(got.cpu(), ref) < 1e-5 and _rel(_nchw(an.grad, 16, ops), a.grad) < 1e-5
+    # TV loss (fast_style_transfer.py:795-803) on an image-like NHWC4 tensor
+    im = (_g(23, (2, 3, 17, 19)) * 30).requires_grad_(True)
+    rt = style_ref.calc_tv_loss(im) * 0.5
+    rt.backward()
+    imn = _nhwc(im.detach(), ops).requires_grad_(True)
+    gt = perceptual.tv_loss_nhwc(imn, 0.5, 3)
+    gt.backward()
+    assert _rel(gt.cpu(), rt) < 1e-5 and _rel(_nchw(imn.grad, 3, ops), im.grad) < 1e-5
+    # Gram matrix (split-K MFMA wgrad kernel) and its backward (1x1 conv)
+    f = _g(24, (2, 64, 12, 16)).requires_grad_(True)
+    G = style_ref.gram_matrix(f)
+    gG = _g(25, tuple(G.shape))
+    G.backward(gG)
+    fn = _nhwc(f.detach(), ops).requires_grad_(True)
+    Gn = perceptual.gram_nhwc(fn)
+    Gn.backward(gG.to(DEV))
+    assert _rel(Gn, G) < 1e-4
+    assert _rel(_nchw(fn.grad, 64, ops), f.grad) < 1e-4
+
+
+# --------------------------------------------------------------------------------- networks
+def _vgg(gb, arch, base):
+    from gbvst import perceptual
+    from oracle import style_ref
+    net = (perceptual.Vgg16 if arch == "vgg16" else perceptual.Vgg19)(DEV)
+    sd = style_ref.vgg_weights(style_ref.RefVGG(arch), base)
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    net.bump_version()
+    return net
+
+
+@pytest.mark.parametrize("arch,base", [("vgg16", 510), ("vgg19", 520)])
+def test_vgg_vs_reference_golden(gb, golden, arch, base):
+    from oracle import prng
+    g = golden("style_small")
+    net = _vgg(gb, arch, base)
+    x = torch.from_numpy(g[f"{arch}_x"]).to(DEV).requires_grad_(True)
+    ys = net(x)
+    loss = 0
+    for i, y in enumerate(ys):
+        assert _rel(y, g[f"{arch}_y{i}"]) < 1e-4, (arch, i)
+        loss = loss + (y * torch.from_numpy(prng.normal(base + 10 + i, tuple(y.shape))).to(DEV)).sum()
+    loss.backward()
+    assert _rel(x.grad, g[f"{arch}_dx"]) < 1e-4
+
+
+def _fsn(gb, base):
+    from gbvst import faststyle
+    from oracle import style_ref
+    net = faststyle.FastStyleNet(3, 1).to(DEV)
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in
+                         style_ref.fsn_weights(style_ref.RefFastStyleNet(3), base).items()})
+    return net
+
+
+def test_faststylenet_vs_reference_golden(gb, golden):
+    from oracle import prng
+    g = golden("style_small")
+    net = _fsn(gb, 530)
+    net.zero_grad()
+    x = torch.from_numpy(g["fsn_x"]).to(DEV).requires_grad_(True)
+    feats, img = net(x, 0.8)
+    assert _rel(feats, g["fsn_feats"]) < 1e-4 and _rel(img, g["fsn_img"]) < 1e-4
+    gf = torch.from_numpy(prng.normal(532, tuple(feats.shape))).to(DEV)
+    gi = torch.from_numpy(prng.normal(533, tuple(img.shape))).to(DEV)
+    ((feats * gf).sum() + (img * gi).sum()).backward()
+    assert _rel(x.grad, g["fsn_dx"]) < 1e-4
+    params = dict(net.named_parameters())
+    for k in [k[len("fsn_g_"):] for k in g.files if k.startswith("fsn_g_")]:
+        ref = g["fsn_g_" + k]
+        if k.endswith("conv2d.bias") and not k.startswith("deconv3"):
+            # bias in front of an InstanceNorm: exact gradient 0, both sides are rounding noise
+            assert params[k].grad.abs().max().item() < 1e-3 * max(1.0, np.abs(ref).max()), k
+            continue
+        assert _rel(params[k].grad, ref) < 1e-3, k
+
+
+def test_johnson_step_vs_reference_golden(gb, golden):
+    from gbvst import faststyle, ops
+    g = golden("style_small")
+    model = _fsn(gb, 540)
+    vgg = _vgg(gb, "vgg16", 550)
+    emph = tuple(float(v) for v in g["js_emph"])
+    J = faststyle.Johnson([torch.from_numpy(g["js_style"])], emphasis=emph, lr=1e-3, batch_sz=2,
+                          device=DEV, vgg=vgg, model=model)
+    x = ops.nchw_to_nhwc(torch.from_numpy(g["js_img"]).to(DEV))
+    params = dict(model.named_parameters())
+    for s in range(2):
+        J.adam.zero_grad()
+        loss, cl, sl, tv, _ = J.losses_nhwc(x)
+        loss.backward()
+        got = np.array([float(v) for v in (loss, cl, sl, tv)])
+        rel = np.abs(got - g["js_losses"][s]) / np.abs(g["js_losses"][s])
+        assert rel.max() < 1e-3, (s, rel)
+        if s == 0:
+            for k in [k[len("js_g_"):] for k in g.files if k.startswith("js_g_")]:
+                assert _rel(params[k].grad, g["js_g_" + k]) < 1e-3, k
+        J.adam.step()
+
+
+def test_faststylenet_inference_256_vs_oracle(gb):
+    from oracle import style_ref
+    ref = style_ref.RefFastStyleNet(3)
+    style_ref.load_np(ref, style_ref.fsn_weights(ref, 77))
+    net = _fsn(gb, 77)
+    x = torch.rand(1, 3, 256, 256, generator=torch.Generator().manual_seed(5))
+    with torch.no_grad():
+        _, y_ref = ref(x)
+        _, y = net(x.to(DEV))
+    # stylised frame (0..255 scale) within 1e-3 relative of the CPU reference (north_star)
+    assert _rel(y, y_ref) < 1e-3
+
+
+# ------------------------------------------------------------------------------------- RAFT
+def test_corr_block_vs_reference_golden(gb, golden):
+    from gbvst import raft_corr
+    g = golden("corr_small")
+    cb = raft_corr.CorrBlock(torch.from_numpy(g["f1"]).to(DEV), torch.from_numpy(g["f2"]).to(DEV), 4, 4)
+    for i in range(4):
+        assert _rel(cb.level(i), g[f"level{i}"]) < 1e-4, i
+    out = cb(torch.from_numpy(g["coords"]).to(DEV))
+    assert _rel(out, g["lookup"]) < 1e-4
+
+
+def test_corr_block_raft_size_vs_oracle(gb):
+    """Full RAFT geometry: fmaps 1x256x55x128 (Sintel 440x1024 / 8), 4 levels, radius 4."""
+    from gbvst import raft_corr
+    from oracle import style_ref
+    B, D, H, W = 1, 256, 55, 128
+    f1, f2 = _g(31, (B, D, H, W)), _g(32, (B, D, H, W))
+    ys, xs = torch.meshgrid(torch.arange(H), torch.arange(W), indexing="ij")
+    coords = torch.stack([xs, ys])[None].float() + _g(33, (B, 2, H, W), 4.0)
+    ref = style_ref.RefCorrBlock(f1, f2, 4, 4)(coords)
+    cb = raft_corr.CorrBlock(f1.to(DEV), f2.to(DEV), 4, 4)
+    assert _rel(cb(coords.to(DEV)), ref) < 1e-4
+
+
+# -------------------------------------------------------------------------------------- TCL
+def test_tcl_vs_oracle(gb):
+    from gbvst import sintel_eval
+    from oracle import cpu_ref
+    B, H, W = 1, 48, 64
+    x, prev = torch.tanh(_g(41, (B, 3, H, W))), torch.tanh(_g(42, (B, 3, H, W)))
+    ff, bf = _g(43, (B, 2, H, W), 1.5), _g(44, (B, 2, H, W), 1.5)
+    mask = cpu_ref.fbc_check(ff, bf)
+    ref = cpu_ref.tcl(x, prev, bf, mask)
+    got = sintel_eval.tcl_from_flows(x.to(DEV), prev.to(DEV), ff.to(DEV), bf.to(DEV))
+    assert abs(float(got) - float(ref)) <= 1e-5 * abs(float(ref))

@@ -228,7 +228,40 @@ def test_faststylenet_vs_reference_golden(gb, golden):
         assert _rel(params[k].grad, ref) < 1e-3, k
 
 
-def test_johnson_step_vs_reference_golden(gb, golden):
+def _johnson_perturbed_grads(g, emph, eps, seed):
+    """Step-0 parameter gradients of the CPU oracle (fp32) with every weight scaled by
+    (1 + eps * N(0,1)): how much the reference's own gradient moves under forward perturbations of
+    the size any other fp32 summation order produces (ReLU / max-pool decisions flip)."""
+    from oracle import style_ref
+    model = style_ref.RefFastStyleNet(3)
+    style_ref.load_np(model, style_ref.fsn_weights(model, 540))
+    vgg = style_ref.RefVGG("vgg16")
+    style_ref.load_np(vgg, style_ref.vgg_weights(vgg, 550))
+    gen = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        for p in list(model.parameters()) + list(vgg.parameters()):
+            p.mul_(1 + eps * torch.randn(p.shape, generator=gen))
+        grams = [style_ref.gram_matrix(f) for f in vgg(style_ref.normalize(torch.from_numpy(g["js_style"])))]
+    ls = style_ref.johnson_losses(model, vgg, torch.from_numpy(g["js_img"]), grams, *emph)
+    ls[0].backward()
+    return {k: p.grad.numpy() for k, p in model.named_parameters()}
+
+
+def _nrel(got, ref):
+    got = got.detach().double().cpu().numpy() if torch.is_tensor(got) else np.asarray(got, np.float64)
+    ref = np.asarray(ref, np.float64)
+    return float(np.linalg.norm(got - ref) / (np.linalg.norm(ref) + 1e-30))
+
+
+def test_johnson_step_vs_reference_golden(gb, golden, train_math):
+    """Losses of two Johnson steps (step 0 and after one Adam update) within 1e-3 relative of the
+    reference; step-0 parameter gradients (norm-wise relative error) within 1e-3 or within the
+    reference's own sensitivity, whichever is larger.  The gradient path crosses VGG16's and
+    FastStyleNet's ReLUs and max pools, so it is a discontinuous function of the forward values:
+    scaling the reference's weights by (1 + 1e-6 N(0,1)) — forward changes of the size any other
+    fp32 summation order makes — moves its own conv1 weight gradient by up to 5.7e-3 (measured on
+    this fixture; the band is recomputed here over two perturbation seeds).  Forward values, losses
+    and the Grams are checked at 1e-3 / 1e-4 elsewhere."""
     from gbvst import faststyle, ops
     g = golden("style_small")
     model = _fsn(gb, 540)
@@ -238,6 +271,7 @@ def test_johnson_step_vs_reference_golden(gb, golden):
                           device=DEV, vgg=vgg, model=model)
     x = ops.nchw_to_nhwc(torch.from_numpy(g["js_img"]).to(DEV))
     params = dict(model.named_parameters())
+    pert = [_johnson_perturbed_grads(g, emph, 1e-6, sd) for sd in (0, 1)]
     for s in range(2):
         J.adam.zero_grad()
         loss, cl, sl, tv, _ = J.losses_nhwc(x)
@@ -247,7 +281,8 @@ def test_johnson_step_vs_reference_golden(gb, golden):
         assert rel.max() < 1e-3, (s, rel)
         if s == 0:
             for k in [k[len("js_g_"):] for k in g.files if k.startswith("js_g_")]:
-                assert _rel(params[k].grad, g["js_g_" + k]) < 1e-3, k
+                band = max(_nrel(pg[k], g["js_g_" + k]) for pg in pert)
+                assert _nrel(params[k].grad, g["js_g_" + k]) < max(1e-3, band), (k, band)
         J.adam.step()
 
 

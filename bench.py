@@ -15,6 +15,10 @@ Also reported (same JSON line):
   cpu_baseline  rank 0 only, N=1: the CPU oracle (stock PyTorch, NCHW fp32) on the host cores,
                 one B=4 step after a B=1 warm-up (oracle is imported only for this leg).
   inference     generator-only inference fps at 256x256, B=16 (north_star's secondary number).
+  extras        generator inference at the Sintel size (1x436x1024); the flow-warp kernel's HBM
+                roofline on the SURVEY §8d large synthetic (N=32, C=64, 436x1024); the RAFT
+                correlation volume build at fmaps 1x256x55x128; the Johnson (FastStyleNet + VGG16
+                perceptual loss) train step at B=4, 256x256.
 """
 import argparse
 import json
@@ -29,6 +33,8 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 FP32_MFMA_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 (spec; 155 measured)
+BF16_MFMA_PEAK_TFLOPS = 2500.0     # dense bf16 (v_mfma_f32_32x32x16_bf16); bf16x6 = 6 products / fp32 MAC
+HBM_PEAK_GBS = 8000.0              # MI355X_MICROARCH.md: HBM3E 8 TB/s spec (~6.3 achievable)
 TRAIN_TFLOP_PER_FRAME = 2.1753     # SURVEY §8d / BASELINE.md: CycleGANCon step conv FLOPs @256^2
 G_GFLOP_PER_FRAME = 99.10          # ResnetGenerator fwd @256^2
 
@@ -46,8 +52,26 @@ def synthetic_batch(B, H, W, seed, device):
     return [t.to(device).contiguous() for t in imgs + [mask, flow]]
 
 
+def _time_on_stream(fn, reps, warm=3):
+    """Average ms per call of fn() launched on a dedicated stream, HIP events on that stream."""
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        for _ in range(warm):
+            fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(reps):
+            fn()
+        e1.record(s)
+    e1.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
 def dominant_kernel_roofline(device, B, reps=20):
-    """Time the ResnetBlock conv (3x3, reflect 1, 256->256 @64x64, B frames) on its own stream."""
+    """Time the ResnetBlock conv (3x3, reflect 1, 256->256 @64x64, B frames) on its own stream.
+    It runs the training forward arithmetic (bf16x6: fp32-equivalent products from 6 bf16 MFMAs
+    per MAC); `peak` is the dense fp32 MFMA peak of the dtype it delivers, `emulation_peak` the
+    bf16 peak / 6 ceiling of the arithmetic actually executed."""
     from gbvst import ops
     x = torch.randn(B, 64, 64, 256, device=device)
     w = torch.randn(256, 256, 3, 3, device=device) * 0.02
@@ -74,10 +98,80 @@ def dominant_kernel_roofline(device, B, reps=20):
             traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
-    return {"kernel": "conv_fprop_k<128,128,64,64> (ResnetBlock 3x3 256->256 @64x64, B=%d)" % B,
+    emu = BF16_MFMA_PEAK_TFLOPS / 6.0
+    return {"kernel": "conv_fprop_bf_k<128x128, bf16x6> (ResnetBlock 3x3 256->256 @64x64, B=%d)" % B,
             "bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
             "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
-            "traffic": traffic, "avg_launch_ms": round(ms, 4), "flop_per_launch": flop}
+            "traffic": traffic, "avg_launch_ms": round(ms, 4), "flop_per_launch": flop,
+            "emulation_peak": round(emu, 1), "emulation_frac": round(achieved / emu, 4)}
+
+
+def warp_roofline(device, N=32, C=64, H=436, W=1024, reps=10):
+    """vst_warp_fwd (utils/flowtools.py warp) on the SURVEY §8d large synthetic: HBM-bound; algorithmic
+    bytes = N*H*W*(4C gather-once + 8 flow + 4C write)."""
+    from gbvst import ops
+    x = torch.randn(N, H, W, C, device=device)
+    flow = torch.randn(N, 2, H, W, device=device) * 3.0
+    out = torch.empty_like(x)
+    fn = lambda: ops.lib().vst_warp_fwd(x.data_ptr(), flow.data_ptr(), out.data_ptr(), N, H, W, C, 0,  # noqa: E731
+                                        torch.cuda.current_stream().cuda_stream)
+    ms = _time_on_stream(fn, reps)
+    nbytes = N * H * W * (8.0 * C + 8.0)
+    gbs = nbytes / (ms * 1e-3) / 1e9
+    del x, out
+    return {"kernel": "warp_fwd_k (N=%d, C=%d, %dx%d)" % (N, C, H, W), "bound": "hbm",
+            "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
+            "avg_launch_ms": round(ms, 4), "bytes_per_launch": nbytes}
+
+
+def corr_volume(device, B=1, D=256, H=55, W=128, reps=5):
+    """RAFT CorrBlock build (utils/raft/raft/corr.py) at Sintel 440x1024 / 8: all-pairs GEMM on MFMA +
+    3-level average-pool pyramid, then one 4-level radius-4 lookup."""
+    from gbvst import raft_corr
+    f1 = torch.randn(B, D, H, W, device=device)
+    f2 = torch.randn(B, D, H, W, device=device)
+    ys, xs = torch.meshgrid(torch.arange(H, device=device), torch.arange(W, device=device), indexing="ij")
+    coords = torch.stack([xs, ys])[None].float().repeat(B, 1, 1, 1)
+    holder = {}
+
+    def build():
+        holder["cb"] = raft_corr.CorrBlock(f1, f2, 4, 4)
+    ms = _time_on_stream(build, reps)
+    cb = holder["cb"]
+    ms_lookup = _time_on_stream(lambda: cb.lookup_nhwc(coords), reps)
+    flop = raft_corr.corr_flops(B, D, H, W)
+    return {"config": "fmaps %dx%dx%dx%d, 4 levels, radius 4" % (B, D, H, W), "build_ms": round(ms, 4),
+            "gemm_tflops_lower_bound": round(flop / (ms * 1e-3) / 1e12, 2), "lookup_ms": round(ms_lookup, 4),
+            "note": "build = GEMM + pyramid + layout; TFLOP/s counts the GEMM's 2*(HW)^2*D over the whole build"}
+
+
+def sintel_inference_fps(device, reps=5):
+    """Generator-only inference at the Sintel frame size (1x3x436x1024)."""
+    from gbvst import networks
+    G = networks.define_G(3, 3, 64, "resnet_9blocks", "instance", False, "normal", 0.02, [device.index or 0])
+    x = torch.randn(1, 3, 436, 1024, device=device)
+    with torch.no_grad():
+        ms = _time_on_stream(lambda: G(x), reps, warm=2)
+    return {"metric": "generator-only inference fps 1024x436", "batch": 1, "value": round(1000.0 / ms, 2),
+            "unit": "frames/s", "tflops": round(675.14 / ms, 2)}
+
+
+def johnson_train_fps(device, B=4, S=256, steps=5):
+    """Learning-based (Johnson) train step: FastStyleNet + VGG16 content/Gram-style/TV losses + Adam
+    (fs_johnson.py), B frames of SxS, random-init weights (pretrained VGG is unavailable offline)."""
+    from gbvst import faststyle, ops
+    g = torch.Generator(device="cpu").manual_seed(7)
+    J = faststyle.Johnson([torch.rand(1, 3, S, S, generator=g)], lr=1e-3, batch_sz=B, device=device)
+    x = torch.rand(B, 3, S, S, generator=g).to(device)
+    J.train_step(x)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        J.train_step(x)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    return {"metric": "Johnson fast-style train step frames/s %dx%d" % (S, S), "batch": B,
+            "value": round(B / dt, 2), "unit": "frames/s", "ms_per_step": round(dt * 1e3, 3)}
 
 
 def inference_fps(device, B=16, reps=10):
@@ -206,6 +300,10 @@ def main():
     if rank == 0 and not args.no_extras:
         out["roofline"] = dominant_kernel_roofline(device, B)
         out["inference"] = inference_fps(device)
+        out["extras"] = {"sintel_inference": sintel_inference_fps(device),
+                         "warp_roofline": warp_roofline(device),
+                         "raft_corr": corr_volume(device),
+                         "johnson_train": johnson_train_fps(device)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline()
     if rank == 0:

@@ -10,8 +10,9 @@ sides).  Multi-GPU: one process per GPU (torchrun), gradients exchanged with RCC
 
 Also reported (same JSON line):
   roofline      the dominant kernel (ResnetBlock 3x3 conv fprop, 16384x256x2304 implicit GEMM at
-                B=4) timed with HIP events on its launch stream: algorithmic FLOPs / avg duration
-                vs the fp32 MFMA peak; traffic from profiles/*_pmc.json when present.
+                B=4) timed with HIP events around each of its launches inside the timed steps:
+                algorithmic FLOPs / avg duration vs the fp32 MFMA peak; traffic = PMC-measured HBM
+                bytes per launch from profiles/r01_conv_fprop_pmc.json (tools/pmc_conv.py).
   cpu_baseline  rank 0 only, N=1: the CPU oracle (stock PyTorch, NCHW fp32) on the host cores,
                 one B=4 step after a B=1 warm-up (oracle is imported only for this leg).
   inference     generator-only inference fps at 256x256, B=16 (north_star's secondary number).
@@ -67,28 +68,17 @@ def _time_on_stream(fn, reps, warm=3):
     return e0.elapsed_time(e1) / reps
 
 
-def dominant_kernel_roofline(device, B, reps=20):
-    """Time the ResnetBlock conv (3x3, reflect 1, 256->256 @64x64, B frames) on its own stream.
-    It runs the training forward arithmetic (bf16x6: fp32-equivalent products from 6 bf16 MFMAs
-    per MAC); `peak` is the dense fp32 MFMA peak of the dtype it delivers, `emulation_peak` the
-    bf16 peak / 6 ceiling of the arithmetic actually executed."""
-    from gbvst import ops
-    x = torch.randn(B, 64, 64, 256, device=device)
-    w = torch.randn(256, 256, 3, 3, device=device) * 0.02
-    kc = ops.weight_pack(w, ops.PACK_FWD)
-    bias = torch.zeros(256, device=device)
-    y = torch.empty(B, 64, 64, 256, device=device)
-    s = torch.cuda.Stream(device=device)
-    with torch.cuda.stream(s):
-        for _ in range(3):
-            ops.conv2d_fwd(x, kc, bias, 256, 3, 3, 1, 1, "reflect", out=y)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(s)
-        for _ in range(reps):
-            ops.conv2d_fwd(x, kc, bias, 256, 3, 3, 1, 1, "reflect", out=y)
-        e1.record(s)
-    e1.synchronize()
-    ms = e0.elapsed_time(e1) / reps
+DOMINANT_KEY = lambda B: (B, 64, 64, 256, 256, 3, 1)  # noqa: E731  ResnetBlock conv fprop (N,H,W,Cx,Cop,R,st)
+
+
+def dominant_kernel_roofline(B, probe):
+    """The dominant kernel — the ResnetBlock conv forward (3x3 reflect, 256->256 @64x64, B frames;
+    36 launches per train step) — timed live over the timed steps: HIP events around each of its
+    launches on the stream it is launched on (ops.LaunchProbe).  It runs the training forward
+    arithmetic (bf16x6: fp32-equivalent products from 6 bf16 MFMAs per MAC); `peak` is the dense
+    fp32 MFMA peak of the dtype it delivers, `emulation_peak` the bf16 peak / 6 ceiling of the
+    arithmetic actually executed."""
+    ms = probe.mean_ms()
     flop = 2.0 * (B * 64 * 64) * 256 * (256 * 9)
     achieved = flop / (ms * 1e-3) / 1e12
     traffic = None
@@ -103,6 +93,7 @@ def dominant_kernel_roofline(device, B, reps=20):
             "bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
             "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
             "traffic": traffic, "avg_launch_ms": round(ms, 4), "flop_per_launch": flop,
+            "launches_timed": len(probe.events),
             "emulation_peak": round(emu, 1), "emulation_frac": round(achieved / emu, 4)}
 
 
@@ -268,6 +259,8 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    probe = ops.LaunchProbe(DOMINANT_KEY(B))
+    ops.set_launch_probe(probe)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         model.optimize_parameters(hookG, hookD)
@@ -276,6 +269,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    ops.set_launch_probe(None)
     if world > 1:
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -298,7 +292,7 @@ def main():
         "final_losses": {k: round(v, 5) for k, v in losses.items()},
     }
     if rank == 0 and not args.no_extras:
-        out["roofline"] = dominant_kernel_roofline(device, B)
+        out["roofline"] = dominant_kernel_roofline(B, probe)
         out["inference"] = inference_fps(device)
         out["extras"] = {"sintel_inference": sintel_inference_fps(device),
                          "warp_roofline": warp_roofline(device),

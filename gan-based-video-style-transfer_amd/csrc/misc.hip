@@ -57,11 +57,12 @@ __global__ void weight_pack_k(const float* __restrict__ w, float* __restrict__ o
     const long q = idx / Ip;
     rs = q % RS;
     o = q / RS;
-  } else {  // VST_PACK_IK: idx = (i*RS + rs)*Op + o
+  } else {  // VST_PACK_IK / VST_PACK_IKF: idx = (i*RS + rs)*Op + o (IKF: taps rotated 180 deg)
     o = idx % Op;
     const long q = idx / Op;
     rs = q % RS;
     i = q / RS;
+    if (mode == VST_PACK_IKF) rs = RS - 1 - rs;
   }
   out[idx] = (o < O && i < I) ? w[((long)o * I + i) * RS + rs] : 0.f;
 }
@@ -118,7 +119,7 @@ extern "C" int vst_nhwc_to_nchw(const float* x, float* y, int N, int C, int H, i
 
 extern "C" int vst_weight_pack(const float* w, float* out, int O, int I, int R, int S, int Op,
                                int Ip, int mode, void* stream) {
-  VST_REQUIRE(w && out && O <= Op && I <= Ip && mode >= VST_PACK_KC && mode <= VST_PACK_IK,
+  VST_REQUIRE(w && out && O <= Op && I <= Ip && mode >= VST_PACK_KC && mode <= VST_PACK_IKF,
               "weight_pack: bad args");
   const long total = (long)R * S * Op * Ip;
   hipLaunchKernelGGL(weight_pack_k, dim3(ceil_div(total, 256)), dim3(256), 0, (hipStream_t)stream, w,

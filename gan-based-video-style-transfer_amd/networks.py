@@ -19,6 +19,7 @@ MI355X design (not a translation):
     and returns NCHW like the reference; ``forward_nhwc`` is the internal zero-copy entry.
 """
 import functools
+import os
 
 import torch
 import torch.nn as nn
@@ -236,6 +237,16 @@ def _pack_conv(m):
             _padded_bias(m))
 
 
+# Stride-1 data gradients whose output-gradient channel count suits the split-bf16 forward kernel
+# run as forward convs over rotated weights (ops.conv2d_dgrad_s1): the fprop kernel (pre-split
+# weight planes) sustains ~1.8x the transposed-conv kernel on the ResnetBlock shape.
+DGRAD_AS_FPROP = os.environ.get("VST_DGRAD_FPROP", "1") != "0"
+
+
+def _ikf(m):
+    return ops.weight_pack(m.weight, ops.PACK_IKF) if DGRAD_AS_FPROP else None
+
+
 def _padded_bias(m):
     if m.bias is None:
         return None
@@ -306,9 +317,12 @@ class ResnetGenerator(FlatNet):
     def _make_packs(self):
         c0, d, blocks, u, f = self._layers()
         P = {"c0": _pack_conv(c0), "d0": _pack_conv(d[0]), "d1": _pack_conv(d[1]), "f": _pack_conv(f)}
+        P["ikf"] = {}
         for i, b in enumerate(blocks):
             P[f"b{i}a"] = _pack_conv(b.conv_block[1])
             P[f"b{i}b"] = _pack_conv(b.conv_block[5])
+            P["ikf"][f"b{i}a"] = _ikf(b.conv_block[1])
+            P["ikf"][f"b{i}b"] = _ikf(b.conv_block[5])
         for i, m in enumerate(u):
             # ConvTranspose2d fwd = transposed kernel with rows (r,s,ci) -> CK pack of Wt[Ci][Co];
             # its dgrad = forward conv with KC pack of Wt seen as [O=Ci][I=Co] -> rows (r,s,co), cols ci
@@ -393,6 +407,9 @@ class _GeneratorFn(torch.autograd.Function):
             return ops.instnorm_act_bwd(g, y, s, act, db=db)
 
         def dgrad_reflect(dy, key, cin_p, R, p, H, W, addend=None):
+            ikf = P["ikf"].get(key)
+            if ikf is not None and dy.shape[-1] % 8 == 0:
+                return ops.conv2d_dgrad_s1(dy, ikf, H, W, cin_p, R, p, "reflect", addend=addend)
             _, ck, _ = P[key]
             return ops.conv2d_tfwd(dy, ck, None, H, W, cin_p, R, R, 1, p, pad_mode="reflect",
                                    addend=addend)
@@ -482,7 +499,11 @@ class NLayerDiscriminator(FlatNet):
         return [m for m in self.model if isinstance(m, Conv2d)]
 
     def _make_packs(self):
-        return [_pack_conv(m) for m in self._convs()]
+        packs = [_pack_conv(m) for m in self._convs()]
+        # stride-1 layers with >= 8 output channels: data gradient as a forward conv (IKF pack)
+        self._ikf = [(_ikf(m) if (st == 1 and cout % 8 == 0) else None)
+                     for m, (cout, st, _) in zip(self._convs(), self.spec)]
+        return packs
 
     def forward_nhwc(self, x):
         return _DiscriminatorFn.apply(x, self._anchor(), self)
@@ -542,8 +563,13 @@ class _DiscriminatorFn(torch.autograd.Function):
                                  m.bias.grad if (m.bias is not None and not has_in) else None,
                                  4, 4, st, 1, "zero", co, ci, ci * 16, 16, accumulate=True)
             if i > 0 or ctx.needs_input_grad[0]:
-                _, ck, _ = P[i]
-                g = ops.conv2d_tfwd(dy, ck, None, a_in.shape[1], a_in.shape[2], a_in.shape[-1], 4, 4, st, 1)
+                ikf = net._ikf[i]
+                if ikf is not None:
+                    g = ops.conv2d_dgrad_s1(dy, ikf, a_in.shape[1], a_in.shape[2], a_in.shape[-1], 4, 1)
+                else:
+                    _, ck, _ = P[i]
+                    g = ops.conv2d_tfwd(dy, ck, None, a_in.shape[1], a_in.shape[2], a_in.shape[-1], 4, 4,
+                                        st, 1)
                 if i == 0:
                     gx = g
         ctx.saved = None

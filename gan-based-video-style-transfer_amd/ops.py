@@ -12,7 +12,7 @@ from . import _lib
 
 ACT = {"none": 0, "relu": 1, "lrelu": 2, "tanh": 3}
 PAD = {"zero": 0, "reflect": 1}
-PACK_KC, PACK_CK, PACK_OK, PACK_IK = 0, 1, 2, 3
+PACK_KC, PACK_CK, PACK_OK, PACK_IK, PACK_IKF = 0, 1, 2, 3, 4
 # the conv kernels consume: forward conv -> PACK_OK, data-gradient / transposed conv -> PACK_IK
 PACK_FWD, PACK_DGRAD = PACK_OK, PACK_IK
 IN_EPS = 1e-5
@@ -74,7 +74,7 @@ def weight_pack(w, mode, transposed=False):
     O, I_, R, S = w.shape
     Op, Ip = cpad(O), cpad(I_)
     shape = {PACK_KC: (R, S, Ip, Op), PACK_CK: (R, S, Op, Ip), PACK_OK: (Op, R, S, Ip),
-             PACK_IK: (Ip, R, S, Op)}[mode]
+             PACK_IK: (Ip, R, S, Op), PACK_IKF: (Ip, R, S, Op)}[mode]
     out = torch.empty(shape, device=w.device, dtype=torch.float32)
     _call("vst_weight_pack", _p(w), _p(out), O, I_, R, S, Op, Ip, mode, _stream())
     # the split-arithmetic conv paths read the pack as three bf16 planes (vst_weight_split)
@@ -85,6 +85,27 @@ def weight_pack(w, mode, transposed=False):
 
 
 # --------------------------------------------------------------------------------------- conv
+class LaunchProbe:
+    """Measurement hook (bench.py): HIP events around every vst_conv2d_fwd launch of one shape
+    (N, H, W, Cx, Cop, R, stride), recorded on the stream the kernel is launched on."""
+
+    def __init__(self, key):
+        self.key, self.events = key, []
+
+    def mean_ms(self):
+        torch.cuda.synchronize()
+        t = [a.elapsed_time(b) for a, b in self.events]
+        return sum(t) / len(t) if t else float("nan")
+
+
+_probe = None
+
+
+def set_launch_probe(probe):
+    global _probe
+    _probe = probe
+
+
 def conv2d_fwd(x, wp, bias, cop, R, S, stride, pad, pad_mode="zero", act="none", slope=0.0,
                out=None, role="fwd"):
     _dev_check(x, wp, bias)
@@ -92,9 +113,16 @@ def conv2d_fwd(x, wp, bias, cop, R, S, stride, pad, pad_mode="zero", act="none",
     Ho = (H + 2 * pad - R) // stride + 1
     Wo = (W + 2 * pad - S) // stride + 1
     y = out if out is not None else torch.empty((N, Ho, Wo, cop), device=x.device)
+    probe = _probe if (_probe is not None and _probe.key == (N, H, W, Cx, cop, R, stride)) else None
+    if probe is not None:
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev[0].record()
     _call("vst_conv2d_fwd", _p(x), _p(wp), _p(getattr(wp, "vst_split", None)), _p(bias), _p(y), N, H,
           W, Cx, cop, R, S, stride, pad,
           PAD[pad_mode], ACT[act], float(slope), _math(role), _stream())
+    if probe is not None:
+        ev[1].record()
+        probe.events.append(ev)
     return y
 
 
@@ -173,6 +201,23 @@ def channel_sum(x, db, cl, accumulate=True):
     nbytes = lib().vst_channel_sum_ws_bytes(nhw, cs)
     ws = torch.empty((nbytes + 3) // 4, device=x.device)
     _call("vst_channel_sum", _p(x), _p(db), _p(ws), nhw, cs, cl, 1 if accumulate else 0, _stream())
+
+
+def conv2d_dgrad_s1(dy, ikf, H, W, cx, R, pad, pad_mode="zero", addend=None, role="bwd"):
+    """Data gradient of a stride-1 conv as a FORWARD conv (the split-bf16 MFMA fprop kernel with
+    pre-split weights).  Reflect padding: dx_full = conv(dy, rot180(W)^T, zero pad R-1) over the
+    padded input frame [H+2p][W+2p], then the reflect fold (+ addend).  Zero padding p <= R-1:
+    dx = conv(dy, rot180(W)^T, zero pad R-1-p) directly (+ addend).  ikf: VST_PACK_IKF pack."""
+    _dev_check(dy, ikf, addend)
+    if pad_mode == "reflect":
+        dxp = conv2d_fwd(dy, ikf, None, cx, R, R, 1, R - 1, "zero", role=role)
+        return reflect_fold(dxp, pad, addend)
+    if pad > R - 1:
+        raise NotImplementedError("conv2d_dgrad_s1: zero padding must be <= R-1")
+    dx = conv2d_fwd(dy, ikf, None, cx, R, R, 1, R - 1 - pad, "zero", role=role)
+    if addend is not None:
+        axpby(addend, dx, 1.0, 1.0)
+    return dx
 
 
 def reflect_fold(dxp, p, addend=None):

@@ -57,7 +57,10 @@ enum { VST_ACT_NONE = 0, VST_ACT_RELU = 1, VST_ACT_LRELU = 2, VST_ACT_TANH = 3 }
 enum { VST_PACK_KC = 0,   /* [R][S][Ci][Co]  (rows k=(r,s,ci), cols co) */
        VST_PACK_CK = 1,   /* [R][S][Co][Ci]  (rows k=(r,s,co), cols ci) */
        VST_PACK_OK = 2,   /* [Co][R][S][Ci]  conv forward B operand, k=(r,s,ci) contiguous per co */
-       VST_PACK_IK = 3 }; /* [Ci][R][S][Co]  dgrad / transposed-conv B operand, k=(r,s,co) per ci */
+       VST_PACK_IK = 3,   /* [Ci][R][S][Co]  dgrad / transposed-conv B operand, k=(r,s,co) per ci */
+       VST_PACK_IKF = 4 };/* IK with the taps rotated 180 deg: w[co][ci][R-1-r][S-1-s] — the
+                           * VST_PACK_OK pack of the conv whose forward is this conv's stride-1
+                           * data gradient (dx = conv(dy, IKF, pad R-1-pad), then reflect fold) */
 
 const char* vst_last_error(void);
 int vst_version(void);
@@ -69,7 +72,8 @@ int vst_nhwc_to_nchw(const float* x, float* y, int N, int C, int H, int W, int C
 /* Pack a PyTorch conv weight w[O][I][R][S] (ConvTranspose: pass Ci as O) for the GEMM kernels.
  * mode VST_PACK_KC -> out[R][S][Ip][Op]; VST_PACK_CK -> out[R][S][Op][Ip];
  * VST_PACK_OK -> out[Op][R][S][Ip] (consumed by vst_conv2d_fwd);
- * VST_PACK_IK -> out[Ip][R][S][Op] (consumed by vst_conv2d_tfwd).
+ * VST_PACK_IK -> out[Ip][R][S][Op] (consumed by vst_conv2d_tfwd);
+ * VST_PACK_IKF -> out[Ip][R][S][Op] with rotated taps (consumed by vst_conv2d_fwd as a dgrad).
  * Ip/Op are the padded channel strides (multiples of 4, zero filled). */
 int vst_weight_pack(const float* w, float* out, int O, int I, int R, int S, int Op, int Ip,
                     int mode, void* stream);

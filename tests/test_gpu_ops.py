@@ -245,3 +245,27 @@ def test_adam_matches_torch(ops):
         opt.step()
         ops.adam_step(p, gr.to(DEV), m, v, 2e-4, 0.5, 0.999, 1e-8, i + 1)
     np.testing.assert_allclose(p.cpu().numpy(), pr.detach().numpy(), rtol=0, atol=1e-7)
+
+
+@pytest.mark.parametrize("case", [
+    # name, N, Ci, H, W, Co, k, pad, mode
+    ("res_reflect", 2, 32, 12, 10, 32, 3, 1, "reflect"),
+    ("res_wide_reflect", 1, 256, 16, 16, 256, 3, 1, "reflect"),
+    ("c7_reflect", 2, 16, 14, 12, 16, 7, 3, "reflect"),
+    ("D4_s1_zero", 2, 32, 9, 11, 64, 4, 1, "zero"),
+    ("k3_zero", 2, 24, 8, 8, 40, 3, 1, "zero"),
+], ids=lambda c: c[0])
+def test_dgrad_as_fprop(ops, case, conv_math):
+    """Stride-1 data gradient computed by the forward-conv kernel over the rotated-tap (IKF) pack,
+    + reflect fold / addend, against torch autograd."""
+    name, N, Ci, H, W, Co, k, pad, mode = case
+    x = _g(61, (N, Ci, H, W)).requires_grad_(True)
+    w = _g(62, (Co, Ci, k, k), 0.1)
+    xp = F.pad(x, (pad,) * 4, mode="reflect") if mode == "reflect" else x
+    y = F.conv2d(xp, w, None, padding=0 if mode == "reflect" else pad)
+    gy = _g(63, tuple(y.shape))
+    y.backward(gy)
+    ikf = ops.weight_pack(w.to(DEV), ops.PACK_IKF)
+    add = _g(64, (N, Ci, H, W))
+    dx = ops.conv2d_dgrad_s1(_nhwc(gy, ops), ikf, H, W, ops.cpad(Ci), k, pad, mode, addend=_nhwc(add, ops))
+    _close(_nchw(dx, Ci, ops) - add, x.grad, tol=CONV_TOL[conv_math], what=name)

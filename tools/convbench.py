@@ -52,6 +52,7 @@ for name, Ci, H, Co, k, st, pad, mode in LAYERS:
     x = torch.randn(B, H, H, Ci, device=dev)
     w = torch.randn(Co, Ci, k, k, device=dev) * 0.02
     kc, ck = ops.weight_pack(w, ops.PACK_FWD), ops.weight_pack(w, ops.PACK_DGRAD)
+    ikf = ops.weight_pack(w, ops.PACK_IKF)
     Ho = (H + 2 * pad - k) // st + 1
     gy = torch.randn(B, Ho, Ho, Co, device=dev)
     dw = torch.zeros(Co, Ci, k, k, device=dev)
@@ -62,12 +63,14 @@ for name, Ci, H, Co, k, st, pad, mode in LAYERS:
             tf = timeit(lambda: ops.conv2d_fwd(x, kc, None, Co, k, k, st, pad, mode))
             tt = timeit(lambda: ops.conv2d_tfwd(gy, ck, None, H, H, Ci, k, k, st, pad, pad_mode=mode))
             tw = timeit(lambda: ops.conv2d_wgrad(x, gy, dw, None, k, k, st, pad, mode, Co, Ci, Ci * k * k, k * k))
+            td = timeit(lambda: ops.conv2d_dgrad_s1(gy, ikf, H, H, Ci, k, pad, mode)) if st == 1 and Co % 8 == 0 else float("nan")
         except Exception as e:  # noqa
             print(name, tname, "ERR", e)
             continue
         r = {"layer": name, "tile": tname, "fprop_us": round(tf, 1), "tconv_us": round(tt, 1),
              "wgrad_us": round(tw, 1), "fprop_TF": round(flop / tf / 1e6, 1),
-             "tconv_TF": round(flop / tt / 1e6, 1), "wgrad_TF": round(flop / tw / 1e6, 1)}
+             "tconv_TF": round(flop / tt / 1e6, 1), "wgrad_TF": round(flop / tw / 1e6, 1),
+             "dgrad_fprop_us": round(td, 1)}
         res.append(r)
         print(json.dumps(r), flush=True)
 ops.debug_set_tiles(-1, -1, -1)

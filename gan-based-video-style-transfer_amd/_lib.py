@@ -87,6 +87,10 @@ SIGNATURES = {
     "vst_corr_pyramid_floats": (L, [L, I, I, L, I]),
     "vst_corr_pyramid": (I, [P, L, I, I, L, I, P]),
     "vst_corr_lookup": (I, [P, P, P, I, I, I, I, I, L, I, I, I, P]),
+    # StarGAN (style.hip, norm.hip)
+    "vst_concat_label_nhwc": (I, [P, P, P, I, I, I, I, I, I, P]),
+    "vst_instnorm_running_update": (I, [P, P, P, I, I, I, F, F, P]),
+    "vst_instnorm_stats_from_running": (I, [P, P, P, I, I, F, P]),
 }
 
 

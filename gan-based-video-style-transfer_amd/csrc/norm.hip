@@ -457,6 +457,38 @@ __global__ void in_aff_bwd_apply_k(const float4* __restrict__ gy, const float4* 
   dx[i] = make_float4(o[0], o[1], o[2], o[3]);
 }
 
+
+// ---- running statistics (nn.InstanceNorm2d(track_running_stats=True), StarGAN model.py:13-16) ---
+// ATen instance_norm: batch_norm over (1, N*C, HW) with the running buffers repeated N times, then
+// the N copies averaged: rm = (1-m) rm + m * mean_n(mean_nc); rv = (1-m) rv + m * mean_n(var_nc *
+// HW/(HW-1)) (unbiased).  var_nc is recovered from rstd: 1/rstd^2 - eps.
+__global__ void in_running_update_k(const float* __restrict__ stats, float* __restrict__ rm,
+                                    float* __restrict__ rv, int N, int C, int HW, float momentum,
+                                    float eps) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double sm = 0.0, sv = 0.0;
+  const double unb = HW > 1 ? (double)HW / (HW - 1) : 1.0;
+  for (int n = 0; n < N; ++n) {
+    const float mean = stats[2 * ((long)n * C + c)], rstd = stats[2 * ((long)n * C + c) + 1];
+    const double var = 1.0 / ((double)rstd * rstd) - eps;
+    sm += (1.0 - momentum) * rm[c] + (double)momentum * mean;
+    sv += (1.0 - momentum) * rv[c] + (double)momentum * var * unb;
+  }
+  rm[c] = (float)(sm / N);
+  rv[c] = (float)(sv / N);
+}
+
+// eval mode: stats[n][c] = {running_mean, 1/sqrt(running_var + eps)} for every n
+__global__ void in_stats_from_running_k(const float* __restrict__ rm, const float* __restrict__ rv,
+                                        float* __restrict__ stats, int N, int C, float eps) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)N * C) return;
+  const int c = i % C;
+  stats[2 * i] = rm[c];
+  stats[2 * i + 1] = 1.f / sqrtf(rv[c] + eps);
+}
+
 }  // namespace vst
 
 using namespace vst;
@@ -590,4 +622,21 @@ extern "C" int vst_instnorm_affine_bwd(const float* gy, const float* x, const fl
                      beta, gate, gate_mult, coef, reinterpret_cast<float4*>(dx), total4, HW, C / 4, act,
                      slope);
   return check_launch("instnorm_affine_bwd");
+}
+
+extern "C" int vst_instnorm_running_update(const float* stats, float* running_mean, float* running_var,
+                                           int N, int C, int HW, float momentum, float eps,
+                                           void* stream) {
+  VST_REQUIRE(stats && running_mean && running_var && N > 0 && C > 0, "instnorm_running_update: bad args");
+  hipLaunchKernelGGL(in_running_update_k, dim3(ceil_div(C, 256)), dim3(256), 0, (hipStream_t)stream, stats,
+                     running_mean, running_var, N, C, HW, momentum, eps);
+  return check_launch("instnorm_running_update");
+}
+
+extern "C" int vst_instnorm_stats_from_running(const float* running_mean, const float* running_var,
+                                               float* stats, int N, int C, float eps, void* stream) {
+  VST_REQUIRE(running_mean && running_var && stats && N > 0 && C > 0, "instnorm_stats_from_running: bad args");
+  hipLaunchKernelGGL(in_stats_from_running_k, dim3(ceil_div((long)N * C, 256)), dim3(256), 0,
+                     (hipStream_t)stream, running_mean, running_var, stats, N, C, eps);
+  return check_launch("instnorm_stats_from_running");
 }

@@ -298,6 +298,23 @@ __global__ void finish_sum3_k(const float* __restrict__ part, int n, float* __re
   }
 }
 
+
+// StarGAN Generator.forward (model.py:59-64): cat([x, c replicated over H, W], dim=1) written as
+// NHWC with channel stride Cs: y[n][h][w] = {x[n][0..Cx)[h][w], c[n][0..Cl), 0...}
+__global__ void concat_label_k(const float* __restrict__ x, const float* __restrict__ lab,
+                               float* __restrict__ y, int N, int Cx, int Cl, int H, int W, int Cs) {
+  const long total = (long)N * H * W * Cs;
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int c = i % Cs;
+  const long pix = i / Cs;
+  const int w = pix % W, h = (pix / W) % H, n = pix / ((long)H * W);
+  float v = 0.f;
+  if (c < Cx) v = x[(((long)n * Cx + c) * H + h) * W + w];
+  else if (c < Cx + Cl) v = lab[(long)n * Cl + (c - Cx)];
+  y[i] = v;
+}
+
 }  // namespace vst
 
 using namespace vst;
@@ -474,4 +491,13 @@ extern "C" int vst_corr_lookup(const float* pyr, const float* coords, float* out
   hipLaunchKernelGGL(corr_lookup_k, grid1(total), dim3(256), 0, (hipStream_t)stream, pyr, geo, coords,
                      out, B, H1, W1, levels, radius, Cs);
   return check_launch("corr_lookup");
+}
+
+extern "C" int vst_concat_label_nhwc(const float* x, const float* label, float* y, int N, int Cx, int Cl,
+                                     int H, int W, int Cs, void* stream) {
+  VST_REQUIRE(x && label && y && Cx + Cl <= Cs && N > 0 && H > 0 && W > 0, "concat_label_nhwc: bad args");
+  const long total = (long)N * H * W * Cs;
+  hipLaunchKernelGGL(concat_label_k, grid1(total), dim3(256), 0, (hipStream_t)stream, x, label, y, N, Cx, Cl,
+                     H, W, Cs);
+  return check_launch("concat_label_nhwc");
 }

@@ -548,3 +548,31 @@ def corr_lookup(pyr, coords, B, H1, W1, H2, W2, ld0, levels, radius):
     _call("vst_corr_lookup", _p(pyr), _p(coords), _p(out), B, H1, W1, H2, W2, ld0, levels, radius, cs,
           _stream())
     return out
+
+
+# -------------------------------------------------------------------------------- StarGAN
+def concat_label_nhwc(x, label, cs=None):
+    """NCHW x [N,Cx,H,W] + label [N,Cl] -> NHWC [N,H,W,cs] (StarGAN model.py:59-64)."""
+    _dev_check(x, label)
+    N, Cx, H, W = x.shape
+    Cl = label.shape[1]
+    cs = cs or cpad(Cx + Cl)
+    y = torch.empty((N, H, W, cs), device=x.device)
+    _call("vst_concat_label_nhwc", _p(x), _p(label), _p(y), N, Cx, Cl, H, W, cs, _stream())
+    return y
+
+
+def instnorm_running_update(stats, running_mean, running_var, HW, momentum=0.1):
+    _dev_check(stats, running_mean, running_var)
+    N, C, _ = stats.shape
+    _call("vst_instnorm_running_update", _p(stats), _p(running_mean), _p(running_var), N, C, HW,
+          float(momentum), IN_EPS, _stream())
+
+
+def instnorm_stats_from_running(running_mean, running_var, N):
+    _dev_check(running_mean, running_var)
+    C = running_mean.numel()
+    stats = torch.empty((N, C, 2), device=running_mean.device)
+    _call("vst_instnorm_stats_from_running", _p(running_mean), _p(running_var), _p(stats), N, C, IN_EPS,
+          _stream())
+    return stats

@@ -275,6 +275,19 @@ int vst_corr_pyramid(float* pyr, long P, int H2, int W2, long ld0, int levels, v
 int vst_corr_lookup(const float* pyr, const float* coords, float* out, int B, int H1, int W1, int H2,
                     int W2, long ld0, int levels, int radius, int Cs, void* stream);
 
+/* ---- StarGAN -------------------------------------------------------------- */
+/* methods/GAN-based/StarGAN/model.py:59-64: y = NHWC(cat([x, label replicated], 1)), x NCHW
+ * [N][Cx][H][W], label [N][Cl], y [N][H][W][Cs] (Cs >= Cx + Cl, extra channels 0). */
+int vst_concat_label_nhwc(const float* x, const float* label, float* y, int N, int Cx, int Cl, int H,
+                          int W, int Cs, void* stream);
+/* nn.InstanceNorm2d(track_running_stats=True) buffers (model.py:13-16): training-mode update from
+ * this batch's stats (mean of the per-instance updates, unbiased variance), and the eval-mode
+ * stats tensor built from the running buffers. */
+int vst_instnorm_running_update(const float* stats, float* running_mean, float* running_var, int N,
+                                int C, int HW, float momentum, float eps, void* stream);
+int vst_instnorm_stats_from_running(const float* running_mean, const float* running_var,
+                                    float* stats, int N, int C, float eps, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

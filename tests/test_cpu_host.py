@@ -98,3 +98,18 @@ def test_style_modules_match_reference_layout():
 
 def cpu_state(net):
     return {k: tuple(v.shape) for k, v in net.state_dict().items()}
+
+
+def test_stargan_modules_match_reference_layout():
+    """Generator / Discriminator keep StarGAN/model.py's module tree (state_dict keys, shapes and the
+    InstanceNorm running buffers), at the solver defaults and at the fixture config."""
+    from gbvst import stargan
+    from oracle import stargan_ref
+    for args in ((64, 5, 6), (8, 4, 2)):
+        assert cpu_state(stargan.Generator(*args)) == cpu_state(stargan_ref.RefGenerator(*args))
+    for args in ((128, 64, 5, 6), (256, 64, 4, 6), (32, 8, 4, 4)):
+        assert cpu_state(stargan.Discriminator(*args)) == cpu_state(stargan_ref.RefDiscriminator(*args))
+    d = stargan.Discriminator(256, 64, 4, 6)
+    assert d.k == 4 and d.conv2.weight.shape == (4, 2048, 4, 4)
+    oh = stargan.label2onehot(torch.tensor([2, 0]), 4, "cpu")
+    assert oh.tolist() == [[0, 0, 1, 0], [1, 0, 0, 0]]

@@ -165,6 +165,28 @@ def johnson_train_fps(device, B=4, S=256, steps=5):
             "value": round(B / dt, 2), "unit": "frames/s", "ms_per_step": round(dt * 1e3, 3)}
 
 
+def stargan_train_fps(device, B=4, S=256, c_dim=4, cycles=1):
+    """StarGAN C4: solver.py's training iteration at SxS, c_dim 4, n_critic 5, B_local
+    images per rank; one timed cycle = 5 D iterations (each with the WGAN-GP double backward) + 1 G
+    step.  Reported as per-D-iteration images/s (BASELINE.md's C4 line).  Random-init weights."""
+    from gbvst import stargan
+    g = torch.Generator(device="cpu").manual_seed(11)
+    sol = stargan.StarGANSolver(image_size=S, c_dim=c_dim, n_critic=5, device=device)
+    x = (torch.rand(B, 3, S, S, generator=g) * 2 - 1).to(device)
+    lo = torch.randint(0, c_dim, (B,), generator=g)
+    lt = torch.randint(0, c_dim, (B,), generator=g)
+    for _ in range(5):
+        sol.train_step(x, lo, lt)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(5 * cycles):
+        sol.train_step(x, lo, lt)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / (5 * cycles)
+    return {"metric": "StarGAN train images/s per D iteration %dx%d (n_critic 5)" % (S, S), "batch": B,
+            "value": round(B / dt, 2), "unit": "images/s", "ms_per_d_iteration": round(dt * 1e3, 3)}
+
+
 def inference_fps(device, B=16, reps=10):
     from gbvst import networks
     G = networks.define_G(3, 3, 64, "resnet_9blocks", "instance", False, "normal", 0.02,
@@ -297,7 +319,8 @@ def main():
         out["extras"] = {"sintel_inference": sintel_inference_fps(device),
                          "warp_roofline": warp_roofline(device),
                          "raft_corr": corr_volume(device),
-                         "johnson_train": johnson_train_fps(device)}
+                         "johnson_train": johnson_train_fps(device),
+                         "stargan_train": stargan_train_fps(device)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline()
     if rank == 0:

@@ -228,28 +228,30 @@ __global__ void act_bwd_k(const float* __restrict__ gy, const float* __restrict_
   if (i < n) dx[i] = gy[i] * act_grad_from_out(y[i], act, slope);
 }
 
-// per-channel sum (bias gradient of a layer without a following IN), same geometry as in_partial
+// per-channel sum (bias gradient of a layer without a following IN), same geometry as in_partial.
+// Channels wider than 4*NRED run as chunks of LP float4 lanes: chunk lanes [c4off, c4off + nl) of a
+// row of CS4 float4s; part rows are CS4*4 doubles wide so one final pass folds every chunk.
 __global__ __launch_bounds__(NRED) void chsum_partial_k(const float* __restrict__ x,
                                                         double* __restrict__ part, long NHW, int LP,
-                                                        int PG, int SP) {
+                                                        int PG, int SP, int CS4, int c4off, int nl) {
   __shared__ double red[4][NRED];
   const int t = threadIdx.x, c4 = t % LP, pg = t / LP;
   const long p0 = (long)blockIdx.x * SP, p1 = min(NHW, p0 + SP);
   double acc[4] = {0, 0, 0, 0};
-  const float4* xb = reinterpret_cast<const float4*>(x) + c4;
-  for (long p = p0 + pg; pg < PG && p < p1; p += PG) {
-    const float4 v = xb[p * LP];
+  const float4* xb = reinterpret_cast<const float4*>(x) + c4off + c4;
+  for (long p = p0 + pg; pg < PG && c4 < nl && p < p1; p += PG) {
+    const float4 v = xb[p * CS4];
     acc[0] += v.x; acc[1] += v.y; acc[2] += v.z; acc[3] += v.w;
   }
 #pragma unroll
   for (int j = 0; j < 4; ++j) red[j][t] = acc[j];
   __syncthreads();
-  if (pg == 0)
+  if (pg == 0 && c4 < nl)
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       double s = 0.0;
       for (int q = 0; q < PG; ++q) s += red[j][q * LP + c4];
-      part[(long)blockIdx.x * LP * 4 + 4 * c4 + j] = s;
+      part[(long)blockIdx.x * CS4 * 4 + 4 * (c4off + c4) + j] = s;
     }
 }
 
@@ -559,18 +561,22 @@ extern "C" int vst_act_bwd(const float* gy, const float* y, float* dx, long n, i
 
 extern "C" size_t vst_channel_sum_ws_bytes(long NHW, int Cs) {
   RedGeom g;
-  if (!red_geom(1, (int)NHW, Cs, g)) return 0;
+  if (Cs % 4 || !red_geom(1, (int)NHW, std::min(Cs, 4 * NRED), g)) return 0;
   return (size_t)g.nsplit * Cs * sizeof(double);
 }
 
 extern "C" int vst_channel_sum(const float* x, float* db, float* ws, long NHW, int Cs, int Cl,
                                int accumulate, void* stream) {
   RedGeom g;
-  VST_REQUIRE(x && db && ws && Cl <= Cs && NHW > 0 && red_geom(1, (int)NHW, Cs, g),
+  VST_REQUIRE(x && db && ws && Cl <= Cs && NHW > 0 && Cs % 4 == 0 &&
+                  red_geom(1, (int)NHW, std::min(Cs, 4 * NRED), g),
               "channel_sum: bad args");
   hipStream_t s = (hipStream_t)stream;
   double* part = reinterpret_cast<double*>(ws);
-  hipLaunchKernelGGL(chsum_partial_k, dim3(g.nsplit), dim3(NRED), 0, s, x, part, NHW, g.LP, g.PG, g.SP);
+  const int cs4 = Cs / 4;
+  for (int c4off = 0; c4off < cs4; c4off += g.LP)
+    hipLaunchKernelGGL(chsum_partial_k, dim3(g.nsplit), dim3(NRED), 0, s, x, part, NHW, g.LP, g.PG, g.SP, cs4,
+                       c4off, std::min(g.LP, cs4 - c4off));
   hipLaunchKernelGGL(chsum_final_k, dim3(ceil_div(Cs, 64)), dim3(256), 0, s, part, db, g.nsplit, Cs, Cl,
                      accumulate);
   return check_launch("channel_sum");

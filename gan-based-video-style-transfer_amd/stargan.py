@@ -483,8 +483,11 @@ class StarGANSolver:
 
     def __init__(self, image_size=256, c_dim=4, g_conv_dim=64, d_conv_dim=64, g_repeat_num=6, d_repeat_num=6,
                  lambda_cls=1.0, lambda_rec=10.0, lambda_gp=10.0, g_lr=1e-4, d_lr=1e-4, n_critic=5, beta1=0.5,
-                 beta2=0.999, dataset="CelebA", device="cuda"):
+                 beta2=0.999, dataset="CelebA", device="cuda", grad_hook=None):
+        """grad_hook(nets): called on [D] / [G] between backward and the optimizer step — the data-parallel
+        gradient exchange (dp.GradExchange) plugs in here; each rank then runs on its own B_local."""
         self.device = torch.device(device)
+        self.grad_hook = grad_hook
         self.c_dim, self.dataset, self.n_critic = c_dim, dataset, n_critic
         self.lambda_cls, self.lambda_rec, self.lambda_gp = lambda_cls, lambda_rec, lambda_gp
         self.G = Generator(g_conv_dim, c_dim, g_repeat_num).to(self.device)
@@ -525,6 +528,8 @@ class StarGANSolver:
         d_loss = d_loss_real + d_loss_fake + self.lambda_cls * d_loss_cls + self.lambda_gp * d_loss_gp
         self.reset_grad()
         d_loss.backward()
+        if self.grad_hook is not None:
+            self.grad_hook([self.D])
         self.d_optimizer.step()
         loss = {"D/loss_real": d_loss_real.detach(), "D/loss_fake": d_loss_fake.detach(),
                 "D/loss_cls": d_loss_cls.detach(), "D/loss_gp": d_loss_gp.detach()}
@@ -539,6 +544,8 @@ class StarGANSolver:
             g_loss = g_loss_fake + self.lambda_rec * g_loss_rec + self.lambda_cls * g_loss_cls
             self.reset_grad()
             g_loss.backward()
+            if self.grad_hook is not None:
+                self.grad_hook([self.G])
             self.g_optimizer.step()
             loss.update({"G/loss_fake": g_loss_fake.detach(), "G/loss_rec": g_loss_rec.detach(),
                          "G/loss_cls": g_loss_cls.detach()})

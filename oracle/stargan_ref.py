@@ -98,9 +98,8 @@ def gradient_penalty(y, x):
     return torch.mean((torch.sqrt(torch.sum(dydx ** 2, dim=1)) - 1) ** 2)
 
 
-def train_iteration(G, D, g_opt, d_opt, x_real, label_org, label_trg, alpha, i, c_dim, n_critic=5,
-                    lambda_cls=1.0, lambda_rec=10.0, lambda_gp=10.0, dataset="CelebA"):
-    """solver.py:298-363 with the batch, target labels and GP alphas given."""
+def d_losses(G, D, x_real, label_org, label_trg, alpha, c_dim, lambda_cls=1.0, lambda_gp=10.0, dataset="CelebA"):
+    """solver.py:315-335: (d_loss, parts) of the discriminator step."""
     c_org, c_trg = label2onehot(label_org, c_dim), label2onehot(label_trg, c_dim)
     out_src, out_cls = D(x_real)
     d_loss_real = -torch.mean(out_src)
@@ -112,26 +111,39 @@ def train_iteration(G, D, g_opt, d_opt, x_real, label_org, label_trg, alpha, i, 
     out_src, _ = D(x_hat)
     d_loss_gp = gradient_penalty(out_src, x_hat)
     d_loss = d_loss_real + d_loss_fake + lambda_cls * d_loss_cls + lambda_gp * d_loss_gp
+    return d_loss, {"D/loss_real": d_loss_real.item(), "D/loss_fake": d_loss_fake.item(),
+                    "D/loss_cls": d_loss_cls.item(), "D/loss_gp": d_loss_gp.item()}
+
+
+def g_losses(G, D, x_real, label_org, label_trg, c_dim, lambda_cls=1.0, lambda_rec=10.0, dataset="CelebA"):
+    """solver.py:348-363: (g_loss, parts) of the generator step."""
+    c_org, c_trg = label2onehot(label_org, c_dim), label2onehot(label_trg, c_dim)
+    x_fake = G(x_real, c_trg)
+    out_src, out_cls = D(x_fake)
+    g_loss_fake = -torch.mean(out_src)
+    g_loss_cls = classification_loss(out_cls, c_trg, dataset)
+    x_reconst = G(x_fake, c_org)
+    g_loss_rec = torch.mean(torch.abs(x_real - x_reconst))
+    g_loss = g_loss_fake + lambda_rec * g_loss_rec + lambda_cls * g_loss_cls
+    return g_loss, {"G/loss_fake": g_loss_fake.item(), "G/loss_rec": g_loss_rec.item(),
+                    "G/loss_cls": g_loss_cls.item()}
+
+
+def train_iteration(G, D, g_opt, d_opt, x_real, label_org, label_trg, alpha, i, c_dim, n_critic=5,
+                    lambda_cls=1.0, lambda_rec=10.0, lambda_gp=10.0, dataset="CelebA"):
+    """solver.py:298-363 with the batch, target labels and GP alphas given."""
+    d_loss, loss = d_losses(G, D, x_real, label_org, label_trg, alpha, c_dim, lambda_cls, lambda_gp, dataset)
     g_opt.zero_grad()
     d_opt.zero_grad()
     d_loss.backward()
     d_opt.step()
-    loss = {"D/loss_real": d_loss_real.item(), "D/loss_fake": d_loss_fake.item(),
-            "D/loss_cls": d_loss_cls.item(), "D/loss_gp": d_loss_gp.item()}
     if (i + 1) % n_critic == 0:
-        x_fake = G(x_real, c_trg)
-        out_src, out_cls = D(x_fake)
-        g_loss_fake = -torch.mean(out_src)
-        g_loss_cls = classification_loss(out_cls, c_trg, dataset)
-        x_reconst = G(x_fake, c_org)
-        g_loss_rec = torch.mean(torch.abs(x_real - x_reconst))
-        g_loss = g_loss_fake + lambda_rec * g_loss_rec + lambda_cls * g_loss_cls
+        g_loss, parts = g_losses(G, D, x_real, label_org, label_trg, c_dim, lambda_cls, lambda_rec, dataset)
         g_opt.zero_grad()
         d_opt.zero_grad()
         g_loss.backward()
         g_opt.step()
-        loss.update({"G/loss_fake": g_loss_fake.item(), "G/loss_rec": g_loss_rec.item(),
-                     "G/loss_cls": g_loss_cls.item()})
+        loss.update(parts)
     return loss
 
 

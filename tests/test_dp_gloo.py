@@ -107,3 +107,75 @@ def test_grad_exchange_gloo_world2(bucket_bytes):
     assert torch.allclose(res[0][3], res[1][3])
     err = (res[0][3] - full).abs().max() / full.abs().max()
     assert err < 1e-5, err
+
+
+def _sg_nets():
+    from oracle import stargan_ref
+    G, D = stargan_ref.RefGenerator(8, 4, 2), stargan_ref.RefDiscriminator(32, 8, 4, 4)
+    for net, base in ((G, 700), (D, 710)):
+        net.load_state_dict({k: torch.from_numpy(v if hasattr(v, "shape") else v)
+                             for k, v in stargan_ref.sg_weights(net, base).items()})
+    return G, D
+
+
+def _sg_batch():
+    from oracle import prng
+    x = torch.from_numpy(prng.uniform_f32(761, (4, 3, 32, 32), -1, 1))
+    alpha = torch.from_numpy(prng.uniform_f32(762, (4, 1, 1, 1)))
+    return x, torch.tensor([0, 2, 1, 3]), torch.tensor([3, 1, 0, 2]), alpha
+
+
+def _sg_grads(G, D, x, lo, lt, alpha):
+    """Flat D gradient of the D loss (incl. the WGAN-GP double backward) and flat G gradient of the
+    G loss, solver.py:315-363."""
+    from oracle import stargan_ref
+    d_loss, _ = stargan_ref.d_losses(G, D, x, lo, lt, alpha, 4)
+    gd = torch.autograd.grad(d_loss, list(D.parameters()))
+    g_loss, _ = stargan_ref.g_losses(G, D, x, lo, lt, 4)
+    gg = torch.autograd.grad(g_loss, list(G.parameters()))
+    return torch.cat([t.reshape(-1) for t in gd]), torch.cat([t.reshape(-1) for t in gg])
+
+
+def _sg_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(1)
+    from gbvst import dp
+    G, D = _sg_nets()
+    x, lo, lt, alpha = _sg_batch()
+    sl = slice(rank * 4 // world, (rank + 1) * 4 // world)
+    gd, gg = _sg_grads(G, D, x[sl], lo[sl], lt[sl], alpha[sl])
+    nets = [_FlatNet(D), _FlatNet(G)]
+    nets[0].flat_grad.copy_(gd)
+    nets[1].flat_grad.copy_(gg)
+    dp.GradExchange(world, bucket_bytes=1 << 16)(nets)
+    q.put((rank, nets[0].flat_grad.clone(), nets[1].flat_grad.clone()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_stargan_dp_equivalence_gloo_world2():
+    """StarGAN C4 data parallelism: every StarGAN loss term is a batch mean (the CelebA BCE is sum/B,
+    the penalty a mean over samples, IN per sample), so the rank-averaged half-batch gradients equal
+    the full-batch gradients — including the WGAN-GP double-backward term."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sg_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    G, D = _sg_nets()
+    gd, gg = _sg_grads(G, D, *_sg_batch())
+    for i, full in ((1, gd), (2, gg)):
+        assert torch.allclose(res[0][i], res[1][i])
+        err = (res[0][i] - full).abs().max() / full.abs().max()
+        assert err < 1e-5, (i, err)

@@ -269,3 +269,15 @@ def test_dgrad_as_fprop(ops, case, conv_math):
     add = _g(64, (N, Ci, H, W))
     dx = ops.conv2d_dgrad_s1(_nhwc(gy, ops), ikf, H, W, ops.cpad(Ci), k, pad, mode, addend=_nhwc(add, ops))
     _close(_nchw(dx, Ci, ops) - add, x.grad, tol=CONV_TOL[conv_math], what=name)
+
+
+@pytest.mark.parametrize("nhw,cs,cl", [(37, 2048, 2048), (1000, 1028, 1025), (5000, 64, 61), (3, 4096, 4000)])
+def test_channel_sum_wide(ops, nhw, cs, cl):
+    """Per-channel sums over NHWC rows, including channel counts above one reduction block (StarGAN's
+    2048-channel discriminator layer runs as channel chunks)."""
+    x = _g(71, (nhw, cs))
+    db = torch.full((cl,), 0.5, device=DEV)
+    ops.channel_sum(x.to(DEV), db, cl, accumulate=True)
+    _close(db, x[:, :cl].double().sum(0).float() + 0.5, tol=1e-6, what="accumulate")
+    ops.channel_sum(x.to(DEV), db, cl, accumulate=False)
+    _close(db, x[:, :cl].double().sum(0).float(), tol=1e-6, what="overwrite")

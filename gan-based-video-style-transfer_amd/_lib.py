@@ -91,6 +91,8 @@ SIGNATURES = {
     "vst_concat_label_nhwc": (I, [P, P, P, I, I, I, I, I, I, P]),
     "vst_instnorm_running_update": (I, [P, P, P, I, I, I, F, F, P]),
     "vst_instnorm_stats_from_running": (I, [P, P, P, I, I, F, P]),
+    "vst_fc2_unpack": (I, [P, P, P, P, P, I, I, I, P]),
+    "vst_u8_image_to_nhwc4": (I, [P, P, L, P]),
 }
 
 

@@ -576,3 +576,30 @@ def instnorm_stats_from_running(running_mean, running_var, N):
     _call("vst_instnorm_stats_from_running", _p(running_mean), _p(running_var), _p(stats), N, C, IN_EPS,
           _stream())
     return stats
+
+
+# -------------------------------------------------------------------------------- formats
+def fc2_unpack(raw):
+    """raw float32 [B,H,W,9] FC2 block on the device -> (img1 NHWC4, img2 NHWC4, mask [B,1,H,W],
+    flow [B,2,H,W]) as the CycleGANCon step consumes them (fc2_dataset.py:35-41)."""
+    _dev_check(raw)
+    B, H, W, nine = raw.shape
+    if nine != 9 or raw.dtype != torch.float32 or not raw.is_contiguous():
+        raise ValueError("fc2_unpack: expected contiguous float32 [B,H,W,9]")
+    img1 = torch.empty((B, H, W, 4), device=raw.device)
+    img2 = torch.empty((B, H, W, 4), device=raw.device)
+    mask = torch.empty((B, 1, H, W), device=raw.device)
+    flow = torch.empty((B, 2, H, W), device=raw.device)
+    _call("vst_fc2_unpack", _p(raw), _p(img1), _p(img2), _p(mask), _p(flow), B, H, W, _stream())
+    return img1, img2, mask, flow
+
+
+def u8_image_to_nhwc4(x):
+    """uint8 [B,H,W,3] on the device -> ToTensor + Normalize(0.5, 0.5) as float32 NHWC4."""
+    if not x.is_cuda:
+        raise RuntimeError("vst ops require GPU tensors (no CPU fallback)")
+    if x.dtype != torch.uint8 or x.shape[-1] != 3 or not x.is_contiguous():
+        raise ValueError("u8_image_to_nhwc4: expected contiguous uint8 [..., 3]")
+    y = torch.empty(tuple(x.shape[:-1]) + (4,), device=x.device)
+    _call("vst_u8_image_to_nhwc4", _p(x), _p(y), x.numel() // 3, _stream())
+    return y

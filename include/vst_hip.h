@@ -288,6 +288,17 @@ int vst_instnorm_running_update(const float* stats, float* running_mean, float* 
 int vst_instnorm_stats_from_running(const float* running_mean, const float* running_var,
                                     float* stats, int N, int C, float eps, void* stream);
 
+/* ---- input formats ------------------------------------------------------------ */
+/* FC2 sample block -> train-step inputs.  Replaces DatasetFC2.__getitem__'s tensor conversion
+ * (methods/GAN-based/CycleGANCon/fc2_dataset.py:35-41 with the T.ToTensor + T.Normalize(0.5, 0.5)
+ * transform of :79-81): raw float32 [B][H][W][9] (img1 0:3, img2 3:6, mask 6:7, flow 7:9) ->
+ * img1, img2 NHWC4 normalised through the uint8 round trip, mask [B][H][W], flow [B][2][H][W]. */
+int vst_fc2_unpack(const float* raw, float* img1, float* img2, float* mask, float* flow, int B, int H,
+                   int W, void* stream);
+/* uint8 RGB HWC (PIL-decoded style frame, fc2_dataset.py:32) -> ToTensor + Normalize(0.5, 0.5),
+ * NHWC4 float32 (channel 3 zero). */
+int vst_u8_image_to_nhwc4(const unsigned char* x, float* y, long npix, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -92,6 +92,17 @@ SIGNATURES = {
     "vst_instnorm_running_update": (I, [P, P, P, I, I, I, F, F, P]),
     "vst_instnorm_stats_from_running": (I, [P, P, P, I, I, F, P]),
     "vst_fc2_unpack": (I, [P, P, P, P, P, I, I, I, P]),
+    "vst_conv2d_fwd_hw": (I, [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, I, P]),
+    "vst_raft_prep": (I, [P, P, I, I, I, I, I, I, I, P]),
+    "vst_add_relu": (I, [P, P, P, L, P]),
+    "vst_copy_channels": (I, [P, I, I, P, I, I, I, L, P]),
+    "vst_raft_ctx_split": (I, [P, I, I, I, P, P, P, I, L, P]),
+    "vst_raft_flow4": (I, [P, P, I, I, I, P]),
+    "vst_raft_motion": (I, [P, I, I, P, P, P, I, I, L, P]),
+    "vst_gru_reset": (I, [P, P, P, I, I, L, P]),
+    "vst_gru_update": (I, [P, P, P, P, I, I, L, P]),
+    "vst_raft_coords_update": (I, [P, P, I, I, I, I, P]),
+    "vst_raft_upsample": (I, [P, P, I, P, I, I, I, P]),
     "vst_u8_image_to_nhwc4": (I, [P, P, L, P]),
 }
 

@@ -76,13 +76,14 @@ int skinny_out_launch(int mode, const float* in, const float* wp, const float* b
                       int Wo, int R, int S, int st, int pad, int reflect, int act, float slope,
                       hipStream_t s);
 // [row][k]-LDS implicit-GEMM fprop / transposed conv (conv_rk.hip); kind = tile override or -1
+// (padh, padw: zero/reflect padding rows / columns — the forward kernels take them separately)
 void rk_fprop_launch(const float* x, const float* wp, const float* bias, float* y, int N, int H, int W,
-                     int C, int Ho, int Wo, int Cop, int R, int S, int st, int pad, int reflect, int act,
-                     float slope, int kind, int math, hipStream_t s);
+                     int C, int Ho, int Wo, int Cop, int R, int S, int st, int padh, int padw, int reflect,
+                     int act, float slope, int kind, int math, hipStream_t s);
 long rk_cp_ld(long P);
 // split-operand bf16 implicit GEMM (conv_bf.hip); wsplit = vst_weight_split planes, stride wps
 int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* bias, float* y, int N,
-                    int H, int W, int C, int Ho, int Wo, int Cop, int R, int S, int st, int pad,
+                    int H, int W, int C, int Ho, int Wo, int Cop, int R, int S, int st, int padh, int padw,
                     int reflect, int act, float slope, int math, int kind, hipStream_t s);
 
 void rk_tile_geom(int kind, int* bm, int* bn, int* bk, int* slots);

@@ -714,36 +714,44 @@ extern "C" void vst_debug_set_tiles(int fprop, int tconv, int wgrad) {
   g_tile_override[2] = wgrad;
 }
 
+static int conv_fwd_impl(const float* x, const float* wp, const void* wsplit, const float* bias, float* y,
+                         int N, int H, int W, int Cx, int Cop, int R, int S, int stride, int padh, int padw,
+                         int pad_mode, int act, float slope, int math, hipStream_t s) {
+  VST_REQUIRE(x && wp && y, "conv2d_fwd: null pointer");
+  VST_REQUIRE(math >= VST_MATH_F32 && math <= VST_MATH_BF16X6, "conv2d_fwd: bad math %d", math);
+  VST_REQUIRE(N > 0 && H > 0 && W > 0 && R > 0 && S > 0 && stride > 0 && padh >= 0 && padw >= 0,
+              "conv2d_fwd: bad shape");
+  VST_REQUIRE(Cx % 4 == 0 && Cop % 4 == 0, "conv2d_fwd: channel strides must be multiples of 4");
+  VST_REQUIRE(pad_mode == VST_PAD_ZERO || (padh < H && padw < W), "conv2d_fwd: reflect pad >= size");
+  const int Ho = (H + 2 * padh - R) / stride + 1, Wo = (W + 2 * padw - S) / stride + 1;
+  VST_REQUIRE(Ho > 0 && Wo > 0, "conv2d_fwd: empty output");
+  const int refl = pad_mode == VST_PAD_REFLECT;
+  if (Cop == 4) {  // image-channel outputs / PatchGAN head: VALU path (skinny.hip)
+    VST_REQUIRE(padh == padw, "conv2d_fwd: the 4-channel-output path needs equal row/column padding");
+    return skinny_out_launch(0, x, wp, bias, nullptr, y, N, H, W, Cx, Ho, Wo, R, S, stride, padh, refl,
+                             act, slope, s);
+  }
+  if (math != VST_MATH_F32 && wsplit && Cx % 8 == 0)
+    return bf_fprop_launch(x, wsplit, (long)Cop * R * S * Cx, bias, y, N, H, W, Cx, Ho, Wo, Cop, R, S,
+                           stride, padh, padw, refl, act, slope, math, g_tile_override[0], s);
+  rk_fprop_launch(x, wp, bias, y, N, H, W, Cx, Ho, Wo, Cop, R, S, stride, padh, padw, refl, act, slope,
+                  g_tile_override[0], math, s);
+  return check_launch("conv2d_fwd");
+}
+
 extern "C" int vst_conv2d_fwd(const float* x, const float* wp, const void* wsplit, const float* bias,
                               float* y, int N,
                               int H, int W, int Cx, int Cop, int R, int S, int stride, int pad,
                               int pad_mode, int act, float slope, int math, void* stream) {
-  VST_REQUIRE(x && wp && y, "conv2d_fwd: null pointer");
-  VST_REQUIRE(math >= VST_MATH_F32 && math <= VST_MATH_BF16X6, "conv2d_fwd: bad math %d", math);
-  VST_REQUIRE(N > 0 && H > 0 && W > 0 && R > 0 && S > 0 && stride > 0 && pad >= 0,
-              "conv2d_fwd: bad shape");
-  VST_REQUIRE(Cx % 4 == 0 && Cop % 4 == 0, "conv2d_fwd: channel strides must be multiples of 4");
-  VST_REQUIRE(pad_mode == VST_PAD_ZERO || (pad < H && pad < W), "conv2d_fwd: reflect pad >= size");
-  const int Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - S) / stride + 1;
-  VST_REQUIRE(Ho > 0 && Wo > 0, "conv2d_fwd: empty output");
-  const int refl = pad_mode == VST_PAD_REFLECT;
-  hipStream_t s = (hipStream_t)stream;
-  const int M = N * Ho * Wo, K = R * S * Cx;
-  if (Cop == 4)  // image-channel outputs / PatchGAN head: VALU path (skinny.hip)
-    return skinny_out_launch(0, x, wp, bias, nullptr, y, N, H, W, Cx, Ho, Wo, R, S, stride, pad, refl,
-                             act, slope, s);
-#define VST_FPROP(BM_, BN_, WM_, WN_)                                                           \
-  hipLaunchKernelGGL((conv_fprop_k<BM_, BN_, WM_, WN_>), dim3(ceil_div(M, BM_), ceil_div(Cop, BN_)),  \
-                     dim3(Tile<BM_, BN_, WM_, WN_>::NT), 0, s, x, wp, bias, y, H, W, Cx, Ho, Wo, Cop, S, \
-                     stride, pad, refl, act, slope, M, K)
-  (void)pick_tile;
-  if (math != VST_MATH_F32 && wsplit && Cx % 8 == 0)
-    return bf_fprop_launch(x, wsplit, (long)Cop * R * S * Cx, bias, y, N, H, W, Cx, Ho, Wo, Cop, R, S,
-                           stride, pad, refl, act, slope, math, g_tile_override[0], s);
-  rk_fprop_launch(x, wp, bias, y, N, H, W, Cx, Ho, Wo, Cop, R, S, stride, pad, refl, act, slope,
-                  g_tile_override[0], math, s);
-#undef VST_FPROP
-  return check_launch("conv2d_fwd");
+  return conv_fwd_impl(x, wp, wsplit, bias, y, N, H, W, Cx, Cop, R, S, stride, pad, pad, pad_mode, act, slope,
+                       math, (hipStream_t)stream);
+}
+
+extern "C" int vst_conv2d_fwd_hw(const float* x, const float* wp, const void* wsplit, const float* bias,
+                                 float* y, int N, int H, int W, int Cx, int Cop, int R, int S, int stride,
+                                 int pad_h, int pad_w, int act, float slope, int math, void* stream) {
+  return conv_fwd_impl(x, wp, wsplit, bias, y, N, H, W, Cx, Cop, R, S, stride, pad_h, pad_w, VST_PAD_ZERO, act,
+                       slope, math, (hipStream_t)stream);
 }
 
 extern "C" int vst_conv2d_tfwd(const float* in, const float* wp, const float* bias,

@@ -209,8 +209,8 @@ __device__ __forceinline__ int remap_mtile(int bx, int nx) {
 template <class T>
 __global__ __launch_bounds__(T::NT, 2) void conv_fprop_bf_k(
     const float* __restrict__ x, const __bf16* __restrict__ ws, long wps, const float* __restrict__ bias,
-    float* __restrict__ y, int H, int W, int C, int Ho, int Wo, int Cop, int S, int st, int pad,
-    int reflect, int act, float slope, int M, int Ktot) {
+    float* __restrict__ y, int H, int W, int C, int Ho, int Wo, int Cop, int S, int st, int padh,
+    int padw, int reflect, int act, float slope, int M, int Ktot) {
   __shared__ __attribute__((aligned(16))) char smem[2 * T::STAGE];
   constexpr int A_LD = T::A_LD, B_LD = T::B_LD, RPP = T::RPP, NP = T::NP;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -232,8 +232,8 @@ __global__ __launch_bounds__(T::NT, 2) void conv_fprop_bf_k(
     const int mm = m < M ? m : 0;
     const int hw = Ho * Wo;
     const int n = mm / hw, rem = mm - n * hw, ho = rem / Wo, wo = rem - ho * Wo;
-    hb[j] = ho * st - pad;
-    wb[j] = wo * st - pad;
+    hb[j] = ho * st - padh;
+    wb[j] = wo * st - padw;
     nb[j] = m < M ? n : -1;
   }
   auto tap_rows = [&]() {
@@ -359,7 +359,7 @@ int bf_pick(long M, int Nc, int override_kind) {
 }
 
 int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* bias, float* y, int N,
-                    int H, int W, int C, int Ho, int Wo, int Cop, int R, int S, int st, int pad,
+                    int H, int W, int C, int Ho, int Wo, int Cop, int R, int S, int st, int padh, int padw,
                     int reflect, int act, float slope, int math, int kind, hipStream_t s) {
   const int M = N * Ho * Wo, K = R * S * C;
   const __bf16* ws = reinterpret_cast<const __bf16*>(wsplit);
@@ -369,7 +369,7 @@ int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* b
     using T = bf::Tile<BM_, BN_, WM_, WN_, BK_, NP_>;                                              \
     hipLaunchKernelGGL(bf::conv_fprop_bf_k<T>, dim3(ceil_div(M, BM_), ceil_div(Cop, BN_)),           \
                        dim3(T::NT), 0, s, x, ws, wps, bias, y, H, W, C, Ho, Wo, Cop, S,             \
-                       st, pad, reflect, act, slope, M, K);                                         \
+                       st, padh, padw, reflect, act, slope, M, K);                                  \
   }
   if (math == VST_MATH_BF16X6) {
     VST_BF_DISPATCH(kd, 3, VST_BF)

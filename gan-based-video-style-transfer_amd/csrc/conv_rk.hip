@@ -273,8 +273,8 @@ __device__ __forceinline__ void zero_acc(f32x16 (&acc)[MI][NI]) {
 template <int BM, int BN, int WM, int WN, int BK, int MATH>
 __global__ __launch_bounds__((Tile<BM, BN, WM, WN, BK, MATH>::NT), 2) void conv_fprop_rk_k(
     const float* __restrict__ x, const float* __restrict__ wp, const float* __restrict__ bias,
-    float* __restrict__ y, int H, int W, int C, int Ho, int Wo, int Cop, int S, int st, int pad,
-    int reflect, int act, float slope, int M, int Ktot) {
+    float* __restrict__ y, int H, int W, int C, int Ho, int Wo, int Cop, int S, int st, int padh,
+    int padw, int reflect, int act, float slope, int M, int Ktot) {
   using T = Tile<BM, BN, WM, WN, BK, MATH>;
   constexpr int NT = T::NT, A_LD = T::A_LD, B_LD = T::B_LD, RP = T::ROWS_PER_PASS;
   __shared__ __attribute__((aligned(16))) float smem[2 * T::STAGE];
@@ -301,8 +301,8 @@ __global__ __launch_bounds__((Tile<BM, BN, WM, WN, BK, MATH>::NT), 2) void conv_
     const int mm = mv[j] ? m : 0;
     const int hw = Ho * Wo;
     const int n = mm / hw, rem = mm - n * hw, ho = rem / Wo, wo = rem - ho * Wo;
-    hb[j] = ho * st - pad;
-    wb[j] = wo * st - pad;
+    hb[j] = ho * st - padh;
+    wb[j] = wo * st - padw;
     xb[j] = x + (long)n * H * W * C;
   }
   const float* wrow[B_LD];
@@ -718,15 +718,16 @@ static int math_kind(int math, int kind) {
   }
 
 void rk_fprop_launch(const float* x, const float* wp, const float* bias, float* y, int N, int H, int W,
-                     int C, int Ho, int Wo, int Cop, int R, int S, int st, int pad, int reflect, int act,
-                     float slope, int kind, int math, hipStream_t s) {
+                     int C, int Ho, int Wo, int Cop, int R, int S, int st, int padh, int padw, int reflect,
+                     int act, float slope, int kind, int math, hipStream_t s) {
   const int M = N * Ho * Wo, K = R * S * C;
   const int kd = math_kind(math, rk_pick(M, Cop, kind));
 #define VST_LX(BM_, BN_, WM_, WN_, BK_, M_)                                                        \
   hipLaunchKernelGGL((rk::conv_fprop_rk_k<BM_, BN_, WM_, WN_, BK_, M_>),                             \
                      dim3(ceil_div(M, BM_), ceil_div(Cop, BN_)),                                     \
                      dim3(rk::Tile<BM_, BN_, WM_, WN_, BK_>::NT),                                    \
-                     0, s, x, wp, bias, y, H, W, C, Ho, Wo, Cop, S, st, pad, reflect, act, slope, M, K);
+                     0, s, x, wp, bias, y, H, W, C, Ho, Wo, Cop, S, st, padh, padw, reflect, act, slope, \
+                     M, K);
 #define VST_LM(M_) VST_RK_DISPATCH_M(kd, VST_LX, M_)
   VST_MATH_SWITCH(math, VST_LM)
 #undef VST_LM

@@ -603,3 +603,89 @@ def u8_image_to_nhwc4(x):
     y = torch.empty(tuple(x.shape[:-1]) + (4,), device=x.device)
     _call("vst_u8_image_to_nhwc4", _p(x), _p(y), x.numel() // 3, _stream())
     return y
+
+
+# ----------------------------------------------------------------------------------- RAFT
+def conv2d_fwd_hw(x, wp, bias, cop, R, S, stride, pad_h, pad_w, act="none", role="fwd"):
+    """Forward conv with separate row / column zero padding (vst_conv2d_fwd_hw)."""
+    _dev_check(x, wp, bias)
+    N, H, W, Cx = x.shape
+    Ho = (H + 2 * pad_h - R) // stride + 1
+    Wo = (W + 2 * pad_w - S) // stride + 1
+    y = torch.empty((N, Ho, Wo, cop), device=x.device)
+    _call("vst_conv2d_fwd_hw", _p(x), _p(wp), _p(getattr(wp, "vst_split", None)), _p(bias), _p(y), N, H, W, Cx,
+          cop, R, S, stride, pad_h, pad_w, ACT[act], 0.0, _math(role), _stream())
+    return y
+
+
+def raft_prep(img, pads):
+    """NCHW [B,3,H,W] -> replicate pad (l, r, t, b) + 2*(x/255)-1 -> NHWC4."""
+    _dev_check(img)
+    B, C, H, W = img.shape
+    if C != 3:
+        raise ValueError("raft_prep: expected 3-channel images")
+    l, r, t, b = pads
+    out = torch.empty((B, H + t + b, W + l + r, 4), device=img.device)
+    _call("vst_raft_prep", _p(img), _p(out), B, H, W, l, r, t, b, _stream())
+    return out
+
+
+def add_relu(a, b, out=None):
+    _dev_check(a, b, out)
+    y = out if out is not None else torch.empty_like(a)
+    _call("vst_add_relu", _p(a), _p(b), _p(y), a.numel(), _stream())
+    return y
+
+
+def copy_channels(src, src_c0, dst, dst_c0, nc):
+    _dev_check(src, dst)
+    npix = src.numel() // src.shape[-1]
+    if dst.numel() // dst.shape[-1] != npix:
+        raise ValueError("copy_channels: pixel counts differ")
+    _call("vst_copy_channels", _p(src), src.shape[-1], src_c0, _p(dst), dst.shape[-1], dst_c0, nc, npix, _stream())
+
+
+def raft_ctx_split(c, hdim, cdim, h, hx, rhx):
+    _dev_check(c, h, hx, rhx)
+    npix = c.numel() // c.shape[-1]
+    _call("vst_raft_ctx_split", _p(c), c.shape[-1], hdim, cdim, _p(h), _p(hx), _p(rhx), hx.shape[-1], npix,
+          _stream())
+
+
+def raft_flow4(coords1, flow4):
+    _dev_check(coords1, flow4)
+    B, _, h, w = coords1.shape
+    _call("vst_raft_flow4", _p(coords1), _p(flow4), B, h, w, _stream())
+
+
+def raft_motion(out, nout, flow4, hx, rhx, c0):
+    _dev_check(out, flow4, hx, rhx)
+    npix = out.numel() // out.shape[-1]
+    _call("vst_raft_motion", _p(out), out.shape[-1], nout, _p(flow4), _p(hx), _p(rhx), hx.shape[-1], c0, npix,
+          _stream())
+
+
+def gru_reset(zr, h, rhx):
+    _dev_check(zr, h, rhx)
+    hd = h.shape[-1]
+    _call("vst_gru_reset", _p(zr), _p(h), _p(rhx), hd, rhx.shape[-1], h.numel() // hd, _stream())
+
+
+def gru_update(zr, q, h, hx):
+    _dev_check(zr, q, h, hx)
+    hd = h.shape[-1]
+    _call("vst_gru_update", _p(zr), _p(q), _p(h), _p(hx), hd, hx.shape[-1], h.numel() // hd, _stream())
+
+
+def raft_coords_update(coords1, delta):
+    _dev_check(coords1, delta)
+    B, _, h, w = coords1.shape
+    _call("vst_raft_coords_update", _p(coords1), _p(delta), delta.shape[-1], B, h, w, _stream())
+
+
+def raft_upsample(coords1, mask):
+    _dev_check(coords1, mask)
+    B, _, h, w = coords1.shape
+    out = torch.empty((B, 2, 8 * h, 8 * w), device=coords1.device)
+    _call("vst_raft_upsample", _p(coords1), _p(mask), mask.shape[-1], _p(out), B, h, w, _stream())
+    return out

@@ -22,18 +22,28 @@ from .ops import cpad
 
 
 class CorrBlock:
-    def __init__(self, fmap1, fmap2, num_levels=4, radius=4):
-        self.num_levels, self.radius = num_levels, radius
+    def __init__(self, fmap1, fmap2, num_levels=4, radius=4, role="infer"):
         B, D, H, W = fmap1.shape
         if tuple(fmap2.shape) != (B, D, H, W):
             raise ValueError("CorrBlock: fmap1 and fmap2 must have the same shape")
+        Dp = cpad(D)
+        self._build(ops.nchw_to_nhwc(fmap1.float().contiguous(), Dp), ops.nchw_to_nhwc(fmap2.float().contiguous(), Dp),
+                    D, num_levels, radius, role)
+
+    @classmethod
+    def from_nhwc(cls, f1, f2, D, num_levels=4, radius=4, role="infer"):
+        """Build from NHWC feature maps [B, H, W, cpad(D)] (RAFT's fnet output, no layout pass)."""
+        self = cls.__new__(cls)
+        self._build(f1.contiguous(), f2.contiguous(), D, num_levels, radius, role)
+        return self
+
+    def _build(self, f1, f2, D, num_levels, radius, role):
+        self.num_levels, self.radius = num_levels, radius
+        B, H, W, Dp = f1.shape
         if num_levels > 1 and ((H >> (num_levels - 1)) < 2 or (W >> (num_levels - 1)) < 2):
             raise ValueError("CorrBlock: the coarsest level must be at least 2x2")
         self.B, self.H, self.W, self.D = B, H, W, D
-        dev = fmap1.device
-        Dp = cpad(D)
-        f1 = ops.nchw_to_nhwc(fmap1.float().contiguous(), Dp)
-        f2 = ops.nchw_to_nhwc(fmap2.float().contiguous(), Dp)
+        dev = f1.device
         # corr.py:58-59: matmul / torch.sqrt(torch.tensor(dim).float())
         sq = float(torch.sqrt(torch.tensor(D).float()))
         f1 = ops.channel_normalize(f1, None, torch.full((D,), sq, device=dev), 1.0, D)
@@ -50,7 +60,7 @@ class CorrBlock:
                 wp[:HW] = f2[b].reshape(HW, 1, 1, Dp)
             ops.split_planes(wp)
             out = self.pyr[b * HW * self.ld0:(b + 1) * HW * self.ld0].view(1, H, W, self.ld0)
-            ops.conv2d_fwd(f1[b:b + 1], wp, None, self.ld0, 1, 1, 1, 0, out=out, role="infer")
+            ops.conv2d_fwd(f1[b:b + 1], wp, None, self.ld0, 1, 1, 1, 0, out=out, role=role)
         ops.corr_pyramid(self.pyr, P, H, W, self.ld0, num_levels)
 
     def level(self, i):

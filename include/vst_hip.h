@@ -288,6 +288,41 @@ int vst_instnorm_running_update(const float* stats, float* running_mean, float* 
 int vst_instnorm_stats_from_running(const float* running_mean, const float* running_var,
                                     float* stats, int N, int C, float eps, void* stream);
 
+/* ---- RAFT inference (SURVEY §8 A19 + §8f rank 3) ------------------------------------------ */
+/* Forward conv with separate row / column zero padding (SepConvGRU's (1,5) / (5,1) kernels with
+ * padding (0,2) / (2,0), update.py:36-43); otherwise identical to vst_conv2d_fwd. */
+int vst_conv2d_fwd_hw(const float* x, const float* wp, const void* wsplit, const float* bias, float* y,
+                      int N, int H, int W, int Cx, int Cop, int R, int S, int stride, int pad_h, int pad_w,
+                      int act, float slope, int math, void* stream);
+/* InputPadder.pad (utils/raft/raft/utils/utils.py:7-20, replicate) + raft.py:89-90 2*(x/255)-1:
+ * NCHW [B][3][H][W] -> NHWC4 [B][H+pt+pb][W+pl+pr][4]. */
+int vst_raft_prep(const float* img, float* out, int B, int H, int W, int pad_l, int pad_r, int pad_t,
+                  int pad_b, void* stream);
+/* y = relu(a + b) (extractor.py ResidualBlock: relu(x + y)); n % 4 == 0. */
+int vst_add_relu(const float* a, const float* b, float* y, long n, void* stream);
+/* torch.cat along channels: dst[p][dst_c0 + c] = src[p][src_c0 + c], c < nc. */
+int vst_copy_channels(const float* src, int src_cs, int src_c0, float* dst, int dst_cs, int dst_c0, int nc,
+                      long npix, void* stream);
+/* raft.py:107-109 split of the context features: h = tanh(c[:hdim]) (also hx[:, :hdim]),
+ * inp = relu(c[hdim:hdim+cdim]) into hx / rhx channels [hdim, hdim+cdim). */
+int vst_raft_ctx_split(const float* c, int cs, int hdim, int cdim, float* h, float* hx, float* rhx, int xcs,
+                       long npix, void* stream);
+/* raft.py:121: flow = coords1 - coords0 (coords1 NCHW [B][2][h][w]) as NHWC4. */
+int vst_raft_flow4(const float* coords1, float* flow4, int B, int h, int w, void* stream);
+/* update.py:95-96 + 130: [out[:, :nout] | flow] written to hx and rhx channels [c0, c0+nout+2). */
+int vst_raft_motion(const float* out, int ocs, int nout, const float* flow4, float* hx, float* rhx, int xcs,
+                    int c0, long npix, void* stream);
+/* SepConvGRU halves (update.py:46-58): rhx[:, :hd] = sigmoid(zr[:, hd:]) * h, and
+ * h = (1 - z) h + z q with z = sigmoid(zr[:, :hd]) (also into hx[:, :hd]). */
+int vst_gru_reset(const float* zr, const float* h, float* rhx, int hd, int xcs, long npix, void* stream);
+int vst_gru_update(const float* zr, const float* q, float* h, float* hx, int hd, int xcs, long npix, void* stream);
+/* raft.py:127: coords1 += delta_flow (delta NHWC, channels 0/1 of stride dcs). */
+int vst_raft_coords_update(float* coords1, const float* delta, int dcs, int B, int h, int w, void* stream);
+/* raft.py:72-83 convex upsampling: mask NHWC [B][h][w][mcs >= 576] (0.25 already applied),
+ * out NCHW [B][2][8h][8w]. */
+int vst_raft_upsample(const float* coords1, const float* mask, int mcs, float* out, int B, int h, int w,
+                      void* stream);
+
 /* ---- input formats ------------------------------------------------------------ */
 /* FC2 sample block -> train-step inputs.  Replaces DatasetFC2.__getitem__'s tensor conversion
  * (methods/GAN-based/CycleGANCon/fc2_dataset.py:35-41 with the T.ToTensor + T.Normalize(0.5, 0.5)

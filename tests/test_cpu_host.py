@@ -113,3 +113,23 @@ def test_stargan_modules_match_reference_layout():
     assert d.k == 4 and d.conv2.weight.shape == (4, 2048, 4, 4)
     oh = stargan.label2onehot(torch.tensor([2, 0]), 4, "cpu")
     assert oh.tolist() == [[0, 0, 1, 0], [1, 0, 0, 0]]
+
+
+def test_raft_module_tree_and_no_cpu_fallback():
+    """gbvst.raft.RAFT keeps raft.py's state_dict keys (checked against the reference list in
+    tests/golden/raft_small.npz) and refuses to run on CPU tensors (no fallback path)."""
+    import argparse
+
+    import numpy as np
+    from gbvst import raft
+    m = raft.RAFT(argparse.Namespace(small=False))
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "raft_small.npz"), allow_pickle=False)
+    assert sorted(m.state_dict()) == list(g["keys"])
+    assert m.args.corr_levels == 4 and m.args.corr_radius == 4
+    with pytest.raises(NotImplementedError):
+        raft.RAFT(argparse.Namespace(small=True))
+    assert raft.InputPadder((1, 3, 436, 1024)).pads == (0, 0, 2, 2)
+    assert raft.InputPadder((1, 3, 436, 1024), mode="kitti").pads == (0, 0, 0, 4)
+    x = torch.zeros(1, 3, 64, 64)
+    with pytest.raises(RuntimeError):
+        m(x, x, iters=1, test_mode=True)

@@ -187,6 +187,28 @@ def stargan_train_fps(device, B=4, S=256, c_dim=4, cycles=1):
             "value": round(B / dt, 2), "unit": "images/s", "ms_per_d_iteration": round(dt * 1e3, 3)}
 
 
+def raft_inference(device, B=1, H=436, W=1024, iters=20, reps=3):
+    """RAFT (full model) flow for one frame pair as the Sintel TCL harness / MoGAN call it
+    (InputPadder + test_mode, 20 iterations); random-init weights (raft-chairs.pth is unavailable)."""
+    import argparse
+    from gbvst import raft
+    m = raft.RAFT(argparse.Namespace(small=False)).to(device).eval()
+    g = torch.Generator(device="cpu").manual_seed(5)
+    i1 = (torch.rand(B, 3, H, W, generator=g) * 255).to(device)
+    i2 = (torch.rand(B, 3, H, W, generator=g) * 255).to(device)
+    raft.compute_raft(m, i1, i2, it=iters)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        raft.compute_raft(m, i1, i2, it=iters)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / reps
+    pads = raft.InputPadder((B, 3, H, W)).pads
+    fl = raft.raft_flops(B, H + pads[2] + pads[3], W + pads[0] + pads[1], iters)
+    return {"metric": "RAFT flow %dx%d, %d iterations" % (H, W, iters), "batch": B, "ms_per_call": round(dt * 1e3, 3),
+            "pairs_per_s": round(B / dt, 2), "tflops": round(fl / dt / 1e12, 2)}
+
+
 def inference_fps(device, B=16, reps=10):
     from gbvst import networks
     G = networks.define_G(3, 3, 64, "resnet_9blocks", "instance", False, "normal", 0.02,
@@ -320,7 +342,9 @@ def main():
                          "warp_roofline": warp_roofline(device),
                          "raft_corr": corr_volume(device),
                          "johnson_train": johnson_train_fps(device),
-                         "stargan_train": stargan_train_fps(device)}
+                         "stargan_train": stargan_train_fps(device),
+                         "raft_sintel": raft_inference(device),
+                         "raft_mogan": raft_inference(device, B=4, H=256, W=256)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline()
     if rank == 0:

@@ -94,6 +94,9 @@ SIGNATURES = {
     "vst_fc2_unpack": (I, [P, P, P, P, P, I, I, I, P]),
     "vst_conv2d_fwd_hw": (I, [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, I, P]),
     "vst_raft_prep": (I, [P, P, I, I, I, I, I, I, I, P]),
+    "vst_raft_prep_nhwc": (I, [P, I, P, I, I, I, I, I, I, I, P]),
+    "vst_loss_masked_l1": (I, [P, P, P, P, P, L, I, I, F, P]),
+    "vst_loss_masked_l1_bwd": (I, [P, P, P, P, P, L, I, I, F, P]),
     "vst_add_relu": (I, [P, P, P, L, P]),
     "vst_copy_channels": (I, [P, I, I, P, I, I, I, L, P]),
     "vst_raft_ctx_split": (I, [P, I, I, I, P, P, P, I, L, P]),

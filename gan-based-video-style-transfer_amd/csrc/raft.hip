@@ -34,6 +34,22 @@ __global__ void raft_prep_k(const float* __restrict__ img, float4* __restrict__ 
   out[i] = make_float4(v[0], v[1], v[2], 0.f);
 }
 
+__global__ void raft_prep_nhwc_k(const float* __restrict__ img, int cs, float4* __restrict__ out, int H, int W,
+                                 int Hp, int Wp, int pl, int pt, long total) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int wp = i % Wp;
+  const long t = i / Wp;
+  const int hp = t % Hp;
+  const long n = t / Hp;
+  const int h = min(max(hp - pt, 0), H - 1), w = min(max(wp - pl, 0), W - 1);
+  const float* src = img + ((n * H + h) * (long)W + w) * cs;
+  float v[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) v[c] = __fsub_rn(__fmul_rn(2.f, __fdiv_rn(src[c], 255.f)), 1.f);
+  out[i] = make_float4(v[0], v[1], v[2], 0.f);
+}
+
 __global__ void add_relu_k(const float4* __restrict__ a, const float4* __restrict__ b, float4* __restrict__ y,
                            long n4) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -208,6 +224,18 @@ extern "C" int vst_raft_prep(const float* img, float* out, int B, int H, int W, 
   hipLaunchKernelGGL(raft_prep_k, g256(total), dim3(256), 0, (hipStream_t)stream, img,
                      reinterpret_cast<float4*>(out), H, W, Hp, Wp, pad_l, pad_t, total);
   return check_launch("raft_prep");
+}
+
+extern "C" int vst_raft_prep_nhwc(const float* img, int src_cs, float* out, int B, int H, int W, int pad_l,
+                                  int pad_r, int pad_t, int pad_b, void* stream) {
+  VST_REQUIRE(img && out && src_cs >= 3 && B > 0 && H > 0 && W > 0 && pad_l >= 0 && pad_r >= 0 && pad_t >= 0 &&
+                  pad_b >= 0,
+              "raft_prep_nhwc: bad args");
+  const int Hp = H + pad_t + pad_b, Wp = W + pad_l + pad_r;
+  const long total = (long)B * Hp * Wp;
+  hipLaunchKernelGGL(raft_prep_nhwc_k, g256(total), dim3(256), 0, (hipStream_t)stream, img, src_cs,
+                     reinterpret_cast<float4*>(out), H, W, Hp, Wp, pad_l, pad_t, total);
+  return check_launch("raft_prep_nhwc");
 }
 
 extern "C" int vst_add_relu(const float* a, const float* b, float* y, long n, void* stream) {

@@ -618,14 +618,25 @@ def conv2d_fwd_hw(x, wp, bias, cop, R, S, stride, pad_h, pad_w, act="none", role
     return y
 
 
-def raft_prep(img, pads):
-    """NCHW [B,3,H,W] -> replicate pad (l, r, t, b) + 2*(x/255)-1 -> NHWC4."""
-    _dev_check(img)
-    B, C, H, W = img.shape
-    if C != 3:
-        raise ValueError("raft_prep: expected 3-channel images")
+def raft_prep(img, pads, nhwc=False, out=None):
+    """[B,3,H,W] NCHW (or NHWC [B,H,W,Cs>=3] with nhwc=True) -> replicate pad (l, r, t, b) +
+    2*(x/255)-1 -> NHWC4 (written into ``out`` when given)."""
+    _dev_check(img, out)
     l, r, t, b = pads
-    out = torch.empty((B, H + t + b, W + l + r, 4), device=img.device)
+    if nhwc:
+        B, H, W, cs = img.shape
+    else:
+        B, C, H, W = img.shape
+        if C != 3:
+            raise ValueError("raft_prep: expected 3-channel images")
+    shape = (B, H + t + b, W + l + r, 4)
+    if out is None:
+        out = torch.empty(shape, device=img.device)
+    elif tuple(out.shape) != shape:
+        raise ValueError("raft_prep: out has shape %s, expected %s" % (tuple(out.shape), shape))
+    if nhwc:
+        _call("vst_raft_prep_nhwc", _p(img), cs, _p(out), B, H, W, l, r, t, b, _stream())
+        return out
     _call("vst_raft_prep", _p(img), _p(out), B, H, W, l, r, t, b, _stream())
     return out
 
@@ -689,3 +700,22 @@ def raft_upsample(coords1, mask):
     out = torch.empty((B, 2, 8 * h, 8 * w), device=coords1.device)
     _call("vst_raft_upsample", _p(coords1), _p(mask), mask.shape[-1], _p(out), B, h, w, _stream())
     return out
+
+
+def loss_masked_l1(a, b, mask, scale, cl):
+    """scale * mean(mask * |a - b|) over cl logical channels of NHWC a, b; mask [B,1,H,W] / [B,H,W] or None."""
+    _dev_check(a, b, mask)
+    npix = a.numel() // a.shape[-1]
+    loss = torch.empty((), device=a.device)
+    _call("vst_loss_masked_l1", _p(a), _p(b), _p(mask), _p(loss), _p(_part(npix, a.device)), npix, a.shape[-1], cl,
+          float(scale), _stream())
+    return loss
+
+
+def loss_masked_l1_bwd(a, b, mask, gout, scale, cl):
+    _dev_check(a, b, mask, gout)
+    npix = a.numel() // a.shape[-1]
+    grad = torch.empty_like(a)
+    _call("vst_loss_masked_l1_bwd", _p(a), _p(b), _p(mask), _p(gout), _p(grad), npix, a.shape[-1], cl, float(scale),
+          _stream())
+    return grad

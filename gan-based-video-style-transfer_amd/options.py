@@ -89,7 +89,7 @@ def parse_options(argv=None, is_train=True):
 
 
 def default_opt(is_train=True, **overrides):
-    opt = parse_options([], is_train)
+    opt = parse_options(["--model", overrides["model"]] if "model" in overrides else [], is_train)
     for k, v in overrides.items():
         setattr(opt, k, v)
     return opt

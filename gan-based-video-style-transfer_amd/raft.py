@@ -266,15 +266,21 @@ class RAFT(nn.Module):
         return P["conv2"](y, "none", role)
 
     # ----------------------------------------------------------------------------- forward
-    def forward(self, image1, image2, iters=12, flow_init=None, upsample=True, test_mode=False, pads=(0, 0, 0, 0)):
+    def forward(self, image1, image2, iters=12, flow_init=None, upsample=True, test_mode=False, pads=(0, 0, 0, 0),
+                nhwc=False):
         """raft.py:86-144.  image1/2: NCHW [B,3,H,W] in the caller's scale (the reference maps
         2*(x/255)-1 regardless); pads = replicate padding (l, r, t, b) applied on the way in (the
         caller's InputPadder, fused).  Returns (flow_low, flow_up) in test_mode, else the list of
-        flow_up per iteration."""
+        flow_up per iteration.  nhwc=True: images are NHWC [B,H,W,Cs>=3] (e.g. generator outputs)
+        and the flows come back as NHWC4 (2 logical channels)."""
         P = self.packs()
         role = self.role
         B = image1.shape[0]
-        imgs = ops.raft_prep(torch.cat([image1, image2], 0).float().contiguous(), pads)
+        H, W = (image1.shape[1], image1.shape[2]) if nhwc else (image1.shape[2], image1.shape[3])
+        l, r, t, b = pads
+        imgs = torch.empty((2 * B, H + t + b, W + l + r, 4), device=image1.device)
+        for k, im in enumerate((image1, image2)):
+            ops.raft_prep(im.float().contiguous(), pads, nhwc=nhwc, out=imgs[k * B:(k + 1) * B])
         Hp, Wp = imgs.shape[1], imgs.shape[2]
         if Hp % 8 or Wp % 8:
             raise ValueError("RAFT: padded image size must be divisible by 8 (use InputPadder)")
@@ -317,10 +323,11 @@ class RAFT(nn.Module):
             ops.raft_coords_update(coords1, delta)
             if not test_mode or it == iters - 1:
                 mask = P["m2"](P["m1"](h, "relu", role), "none", role)
-                preds.append(ops.raft_upsample(coords1, mask))
+                up = ops.raft_upsample(coords1, mask)
+                preds.append(ops.nchw_to_nhwc(up) if nhwc else up)
         if test_mode:
             ops.raft_flow4(coords1, flow4)
-            return ops.nhwc_to_nchw(flow4, 2), preds[-1]
+            return (flow4 if nhwc else ops.nhwc_to_nchw(flow4, 2)), preds[-1]
         return preds
 
 

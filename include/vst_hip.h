@@ -298,6 +298,9 @@ int vst_conv2d_fwd_hw(const float* x, const float* wp, const void* wsplit, const
  * NCHW [B][3][H][W] -> NHWC4 [B][H+pt+pb][W+pl+pr][4]. */
 int vst_raft_prep(const float* img, float* out, int B, int H, int W, int pad_l, int pad_r, int pad_t,
                   int pad_b, void* stream);
+/* Same from an NHWC image with channel stride src_cs (first 3 channels), e.g. a generator output. */
+int vst_raft_prep_nhwc(const float* img, int src_cs, float* out, int B, int H, int W, int pad_l, int pad_r,
+                       int pad_t, int pad_b, void* stream);
 /* y = relu(a + b) (extractor.py ResidualBlock: relu(x + y)); n % 4 == 0. */
 int vst_add_relu(const float* a, const float* b, float* y, long n, void* stream);
 /* torch.cat along channels: dst[p][dst_c0 + c] = src[p][src_c0 + c], c < nc. */
@@ -322,6 +325,14 @@ int vst_raft_coords_update(float* coords1, const float* delta, int dcs, int B, i
  * out NCHW [B][2][8h][8w]. */
 int vst_raft_upsample(const float* coords1, const float* mask, int mcs, float* out, int B, int h, int w,
                       void* stream);
+
+/* MoGAN motion losses (MoGAN/models/cycle_gan_model.py:294-311): scale * mean(mask * |a - b|) over
+ * npix pixels x Cl logical channels of NHWC (channel stride Cs) tensors, mask [npix] broadcast over
+ * channels (nullptr = no mask); backward writes d/da (pass (b, a) for d/db), 0 in padded channels. */
+int vst_loss_masked_l1(const float* a, const float* b, const float* mask, float* loss, float* part, long npix,
+                       int Cs, int Cl, float scale, void* stream);
+int vst_loss_masked_l1_bwd(const float* a, const float* b, const float* mask, const float* gout, float* grad,
+                           long npix, int Cs, int Cl, float scale, void* stream);
 
 /* ---- input formats ------------------------------------------------------------ */
 /* FC2 sample block -> train-step inputs.  Replaces DatasetFC2.__getitem__'s tensor conversion

@@ -126,9 +126,10 @@ def raft_forward(sd, image1, image2, iters=12, flow_init=None, test_mode=False, 
 
 
 # ------------------------------------------------------------------- fixture weights (PRNG)
-def raft_weights(state_shapes, base):
+def raft_weights(state_shapes, base, flow_scale=1.0):
     """Counter-PRNG state_dict by name: conv weights N(0, 1/fan_in), conv biases N(0, 0.05), BN
-    gamma N(1, 0.1), beta N(0, 0.1), running_mean N(0, 0.1), running_var U(0.5, 1.5)."""
+    gamma N(1, 0.1), beta N(0, 0.1), running_mean N(0, 0.1), running_var U(0.5, 1.5).  flow_scale
+    multiplies the flow head's last conv (small, smooth flows keep fbcCheck masks non-trivial)."""
     from oracle import prng
     sd = {}
     for k, shape in state_shapes.items():
@@ -147,4 +148,6 @@ def raft_weights(state_shapes, base):
             sd[k] = prng.normal(s, shape, std=0.1, mean=1.0 if k.endswith("weight") else 0.0)
         else:
             sd[k] = prng.normal(s, shape, std=0.05)
+        if k.startswith("update_block.flow_head.conv2."):
+            sd[k] = (sd[k] * np.float32(flow_scale)).astype(np.float32)
     return sd

@@ -209,6 +209,29 @@ def raft_inference(device, B=1, H=436, W=1024, iters=20, reps=3):
             "pairs_per_s": round(B / dt, 2), "tflops": round(fl / dt / 1e12, 2)}
 
 
+def mogan_train_fps(device, B=4, S=256, pairs=2):
+    """MoGAN C5-style step: CycleGAN ngf=ndf=64 generators / discriminators, motion nets,
+    8 RAFT calls (20 iterations) per optimize_parameters, E-step / M-step alternating; B frame pairs
+    of SxS, random-init weights.  Reported per optimize_parameters call (E and M averaged)."""
+    from gbvst import mogan_model
+    from gbvst.options import default_opt
+    opt = default_opt(True, model="mogan", pool_size=50, gpu_ids=[device.index or 0])
+    m = mogan_model.MoGANModel(opt)
+    g = torch.Generator(device="cpu").manual_seed(3)
+    imgs = [(torch.rand(B, 3, S, S, generator=g) * 2 - 1) for _ in range(4)]
+    m.set_input_fc2(imgs)
+    for _ in range(2):
+        m.optimize_parameters()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(2 * pairs):
+        m.optimize_parameters()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / (2 * pairs)
+    return {"metric": "MoGAN optimize_parameters frames/s %dx%d (8 RAFT calls x 20 iterations)" % (S, S),
+            "batch": B, "value": round(B / dt, 2), "unit": "frames/s", "ms_per_step": round(dt * 1e3, 3)}
+
+
 def inference_fps(device, B=16, reps=10):
     from gbvst import networks
     G = networks.define_G(3, 3, 64, "resnet_9blocks", "instance", False, "normal", 0.02,
@@ -344,7 +367,8 @@ def main():
                          "johnson_train": johnson_train_fps(device),
                          "stargan_train": stargan_train_fps(device),
                          "raft_sintel": raft_inference(device),
-                         "raft_mogan": raft_inference(device, B=4, H=256, W=256)}
+                         "raft_mogan": raft_inference(device, B=4, H=256, W=256),
+                         "mogan_train": mogan_train_fps(device)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline()
     if rank == 0:

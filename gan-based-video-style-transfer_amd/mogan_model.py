@@ -117,6 +117,8 @@ class CycleGANModel(BaseModel):
         with torch.no_grad():
             B, H, W, _ = img1.shape
             padder = InputPadder((B, 3, H, W))
+            if getattr(self.raftModel, "use_graphs", False):
+                return self.raftModel.graphed(img1.detach(), img2.detach(), it, padder.pads, nhwc=True)[1]
             _, flow_up = self.raftModel(img1.detach(), img2.detach(), iters=it, test_mode=True, pads=padder.pads,
                                         nhwc=True)
         return flow_up

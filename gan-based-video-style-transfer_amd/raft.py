@@ -207,7 +207,9 @@ class RAFT(nn.Module):
         self.cnet = BasicEncoder(output_dim=hdim + cdim, norm_fn="batch")
         self.update_block = BasicUpdateBlock(args.corr_levels, args.corr_radius, hidden_dim=hdim)
         self.role = "fwd"  # conv arithmetic role (ops policy); fp32-equivalent by default
+        self.use_graphs = True  # compute_raft replays a captured HIP graph per input shape
         self._packs, self._pkey = None, None
+        self._graphs = {}
 
     def freeze_bn(self):
         pass  # BatchNorm is always evaluated with its running statistics here
@@ -219,10 +221,36 @@ class RAFT(nn.Module):
     def packs(self):
         key = self._key()
         if self._packs is None or self._pkey != key:
+            self._graphs.clear()  # captured graphs read the previous packs
             with torch.no_grad():
                 self._packs = self._make_packs()
             self._pkey = key
         return self._packs
+
+    def graphed(self, image1, image2, iters, pads=(0, 0, 0, 0), nhwc=False):
+        """test_mode forward replayed from a HIP graph captured once per (shape, iters, pads, layout):
+        the ~20 launches per GRU iteration become one graph launch.  Returns fresh copies of
+        (flow_low, flow_up)."""
+        self.packs()
+        key = (tuple(image1.shape), int(iters), tuple(pads), bool(nhwc), image1.device)
+        ent = self._graphs.get(key)
+        if ent is None:
+            s1, s2 = image1.detach().clone(), image2.detach().clone()
+            side = torch.cuda.Stream(device=image1.device)
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):  # warm-up outside capture (allocator, first-touch)
+                self.forward(s1, s2, iters=iters, test_mode=True, pads=pads, nhwc=nhwc)
+            torch.cuda.current_stream().wait_stream(side)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                out = self.forward(s1, s2, iters=iters, test_mode=True, pads=pads, nhwc=nhwc)
+            ent = (g, s1, s2, out)
+            self._graphs[key] = ent
+        g, s1, s2, out = ent
+        s1.copy_(image1)
+        s2.copy_(image2)
+        g.replay()
+        return out[0].clone(), out[1].clone()
 
     def _make_packs(self):
         def enc(e):
@@ -358,6 +386,8 @@ def compute_raft(model, img1, img2, it=20):
     padded size, as the reference does)."""
     with torch.no_grad():
         padder = InputPadder(img1.shape)
+        if model.use_graphs:
+            return model.graphed(img1, img2, it, padder.pads)[1]
         _, flow_up = model(img1, img2, iters=it, test_mode=True, pads=padder.pads)
     return flow_up
 

@@ -127,3 +127,24 @@ def test_raft_vs_oracle_larger(gb):
                     flow_init=finit.to(DEV), test_mode=True, pads=pads)
     assert _rel(low, low_r) < 1e-3
     assert _rel(up, up_r) < 1e-3
+
+
+def test_raft_graph_replay_matches_eager(gb):
+    """compute_raft's captured-graph replay gives the eager result bit for bit, across replays with
+    new inputs and after a weight reload (which must drop the stale graph)."""
+    from gbvst import raft
+    m, _ = _model(1500)
+    x = [torch.from_numpy(prng.uniform_f32(1501 + i, (2, 3, 128, 160), 0.0, 255.0)).to(DEV) for i in range(4)]
+    with torch.no_grad():
+        for a, b in ((x[0], x[1]), (x[2], x[3])):
+            m.use_graphs = False
+            ref = raft.compute_raft(m, a, b, it=5)
+            m.use_graphs = True
+            got = raft.compute_raft(m, a, b, it=5)
+            assert torch.equal(got, ref)
+        assert len(m._graphs) == 1
+        m2, _ = _model(1600)
+        m.load_state_dict(m2.state_dict())
+        got = raft.compute_raft(m, x[0], x[1], it=5)
+        m.use_graphs = False
+        assert torch.equal(got, raft.compute_raft(m, x[0], x[1], it=5))

@@ -1,0 +1,147 @@
+// Tap-GEMM form of the convolutions with 4 (padded) output channels — the generators' last layer
+// (c7s1-3 + tanh, CycleGAN networks.py:365-367; StarGAN model.py:53-54; MoGAN's motion nets).
+//
+// A 4-wide output makes the implicit GEMM N = 4: a 32x32 MFMA tile would be 1/8 useful, so the
+// direct form ran on the VALU at ~10 TFLOP/s.  Instead the contraction over input channels runs
+// first for every tap at once, as a 1x1 conv with N = R*S*4 on the MFMA fprop kernel:
+//     Z[q][(r,s,co)] = sum_ci x[q][ci] * w[co][ci][r][s]            (weights = VST_PACK_CK pack)
+// and the taps are summed afterwards by a gather over source pixels:
+//     y[p][co] = act(bias[co] + sum_{r,s} Z[src(p, r, s)][(r,s,co)])  (vst_tapsum_fwd)
+// The weight gradient mirrors it: the adjoint of the gather folds dy into
+//     D[q][(r,s,co)] = sum_{p : src(p,r,s) = q} dy[p][co]            (vst_tapfold)
+// (with reflect padding a source pixel can be hit by up to 2 positions per axis), the MFMA wgrad
+// kernel contracts D with x over pixels (a 1x1 wgrad, M = R*S*4, N = Ci), and vst_tap_wgrad_scatter
+// writes the [R*S*4][Ci] result back into the [Co][Ci][R][S] gradient.
+// Streaming kernels; Z / D are N*H*W*R*S*16 bytes, each element written once and read once.
+#include "common.h"
+
+namespace vst {
+
+__device__ __forceinline__ int src_index(int x, int n, int reflect) {
+  if (!reflect) return (x >= 0 && x < n) ? x : -1;
+  if (x < 0) return -x;
+  if (x >= n) return 2 * (n - 1) - x;
+  return x;
+}
+
+__global__ void tapsum_k(const float4* __restrict__ z, int zcs4, const float* __restrict__ bias,
+                         float4* __restrict__ y, int H, int W, int R, int S, int pad, int reflect, int act,
+                         float slope, long P) {
+  const long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P) return;
+  const int w = p % W;
+  const long t = p / W;
+  const int h = t % H;
+  const long n = t / H;
+  float4 acc = bias ? make_float4(bias[0], bias[1], bias[2], bias[3]) : make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int r = 0; r < R; ++r) {
+    const int hh = src_index(h + r - pad, H, reflect);
+    if (hh < 0) continue;
+    const float4* zr = z + ((n * H + hh) * (long)W) * zcs4 + r * S;
+    for (int s = 0; s < S; ++s) {
+      const int ww = src_index(w + s - pad, W, reflect);
+      if (ww < 0) continue;
+      const float4 v = zr[(long)ww * zcs4 + s];
+      acc.x += v.x;
+      acc.y += v.y;
+      acc.z += v.z;
+      acc.w += v.w;
+    }
+  }
+  y[p] = make_float4(apply_act(acc.x, act, slope), apply_act(acc.y, act, slope), apply_act(acc.z, act, slope),
+                     apply_act(acc.w, act, slope));
+}
+
+// preimages along one axis: positions pos in [0, n) with src_index(pos + k - pad) == q (k = tap)
+__device__ __forceinline__ int preimages(int q, int k, int pad, int n, int reflect, int (&out)[3]) {
+  const int cand[3] = {q - k + pad, pad - k - q, 2 * (n - 1) - q - k + pad};
+  int m = 0;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int c = cand[j];
+    if (c < 0 || c >= n) continue;
+    if (src_index(c + k - pad, n, reflect) != q) continue;
+    bool dup = false;
+    for (int e = 0; e < m; ++e) dup |= out[e] == c;
+    if (!dup) out[m++] = c;
+  }
+  return m;
+}
+
+__global__ void tapfold_k(const float4* __restrict__ g, float4* __restrict__ d, int H, int W, int R, int S,
+                          int pad, int reflect, long total) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int RS = R * S;
+  const int rs = i % RS;
+  const long q = i / RS;
+  const int qw = q % W;
+  const long t = q / W;
+  const int qh = t % H;
+  const long n = t / H;
+  const int r = rs / S, s = rs - r * S;
+  int ph[3], pw[3];
+  const int mh = preimages(qh, r, pad, H, reflect, ph);
+  const int mw = preimages(qw, s, pad, W, reflect, pw);
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int a = 0; a < mh; ++a)
+    for (int b = 0; b < mw; ++b) {
+      const float4 v = g[(n * H + ph[a]) * (long)W + pw[b]];
+      acc.x += v.x;
+      acc.y += v.y;
+      acc.z += v.z;
+      acc.w += v.w;
+    }
+  d[i] = acc;
+}
+
+// dw[co][ci][rs] (+)= t[(rs*4 + co)][ci], co < Co
+__global__ void tap_wgrad_scatter_k(const float* __restrict__ t, float* __restrict__ dw, int Co, int Ci, int RS,
+                                    int accumulate, long total) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int rs = i % RS;
+  const long u = i / RS;
+  const int ci = u % Ci;
+  const int co = u / Ci;
+  const float v = t[((long)rs * 4 + co) * Ci + ci];
+  dw[i] = accumulate ? dw[i] + v : v;
+}
+
+}  // namespace vst
+
+using namespace vst;
+
+extern "C" int vst_tapsum_fwd(const float* z, int zcs, const float* bias, float* y, int N, int H, int W, int R,
+                              int S, int pad, int pad_mode, int act, float slope, void* stream) {
+  VST_REQUIRE(z && y && N > 0 && H > 0 && W > 0 && R > 0 && S > 0 && zcs == R * S * 4 && pad >= 0,
+              "tapsum_fwd: bad args");
+  VST_REQUIRE(pad_mode == VST_PAD_ZERO || (pad < H && pad < W), "tapsum_fwd: reflect pad >= size");
+  VST_REQUIRE(2 * pad == R - 1 && 2 * pad == S - 1, "tapsum_fwd: 'same' convolutions only (2*pad == k-1)");
+  const long P = (long)N * H * W;
+  hipLaunchKernelGGL(tapsum_k, dim3(ceil_div(P, 256)), dim3(256), 0, (hipStream_t)stream,
+                     reinterpret_cast<const float4*>(z), zcs / 4, bias, reinterpret_cast<float4*>(y), H, W, R, S, pad,
+                     pad_mode == VST_PAD_REFLECT, act, slope, P);
+  return check_launch("tapsum_fwd");
+}
+
+extern "C" int vst_tapfold(const float* g, float* d, int N, int H, int W, int R, int S, int pad, int pad_mode,
+                           void* stream) {
+  VST_REQUIRE(g && d && N > 0 && H > 0 && W > 0 && R > 0 && S > 0 && pad >= 0, "tapfold: bad args");
+  VST_REQUIRE(pad_mode == VST_PAD_ZERO || (pad < H && pad < W), "tapfold: reflect pad >= size");
+  VST_REQUIRE(2 * pad == R - 1 && 2 * pad == S - 1, "tapfold: 'same' convolutions only (2*pad == k-1)");
+  const long total = (long)N * H * W * R * S;
+  hipLaunchKernelGGL(tapfold_k, dim3(ceil_div(total, 256)), dim3(256), 0, (hipStream_t)stream,
+                     reinterpret_cast<const float4*>(g), reinterpret_cast<float4*>(d), H, W, R, S, pad,
+                     pad_mode == VST_PAD_REFLECT, total);
+  return check_launch("tapfold");
+}
+
+extern "C" int vst_tap_wgrad_scatter(const float* t, float* dw, int Co, int Ci, int R, int S, int accumulate,
+                                     void* stream) {
+  VST_REQUIRE(t && dw && Co > 0 && Co <= 4 && Ci > 0 && R > 0 && S > 0, "tap_wgrad_scatter: bad args");
+  const long total = (long)Co * Ci * R * S;
+  hipLaunchKernelGGL(tap_wgrad_scatter_k, dim3(ceil_div(total, 256)), dim3(256), 0, (hipStream_t)stream, t, dw, Co,
+                     Ci, R * S, accumulate, total);
+  return check_launch("tap_wgrad_scatter");
+}

@@ -241,6 +241,9 @@ def _pack_conv(m):
 # run as forward convs over rotated weights (ops.conv2d_dgrad_s1): the fprop kernel (pre-split
 # weight planes) sustains ~1.8x the transposed-conv kernel on the ResnetBlock shape.
 DGRAD_AS_FPROP = os.environ.get("VST_DGRAD_FPROP", "1") != "0"
+# The generator's last conv (4 padded output channels) runs as a tap GEMM on the matrix cores
+# (ops.tap_conv_fwd / tap_conv_wgrad) instead of the VALU skinny kernel; VST_TAP_CONV=0 disables.
+TAP_LAST = os.environ.get("VST_TAP_CONV", "1") != "0"
 
 
 def _ikf(m):
@@ -317,6 +320,8 @@ class ResnetGenerator(FlatNet):
     def _make_packs(self):
         c0, d, blocks, u, f = self._layers()
         P = {"c0": _pack_conv(c0), "d0": _pack_conv(d[0]), "d1": _pack_conv(d[1]), "f": _pack_conv(f)}
+        if TAP_LAST:
+            P["ftap"] = ops.weight_pack(f.weight, ops.PACK_CK)
         P["ikf"] = {}
         for i, b in enumerate(blocks):
             P[f"b{i}a"] = _pack_conv(b.conv_block[1])
@@ -378,7 +383,10 @@ class _GeneratorFn(torch.autograd.Function):
             sv[f"u{i}"] = (a, y, s, an)
             a = an
         kc, _, b = P["f"]
-        out = ops.conv2d_fwd(a, kc, b, cpad(net.output_nc), 7, 7, 1, 3, "reflect", act="tanh", role=role)
+        if "ftap" in P:
+            out = ops.tap_conv_fwd(a, P["ftap"], b, 7, 3, "reflect", act="tanh", role=role)
+        else:
+            out = ops.conv2d_fwd(a, kc, b, cpad(net.output_nc), 7, 7, 1, 3, "reflect", act="tanh", role=role)
         sv["f"] = (a, out)
         ctx.sv, ctx.net, ctx.P = sv, net, P
         ctx.train_w = anchor.requires_grad
@@ -421,7 +429,13 @@ class _GeneratorFn(torch.autograd.Function):
         # final conv + tanh (no IN after it: bias grad is a channel sum)
         a, out = sv["f"]
         g = ops.act_bwd(gout, out, "tanh")
-        wgrad(f, a, g, 7, 1, 3, "reflect", db=True)
+        if "ftap" in P:
+            if train_w:
+                ops.tap_conv_wgrad(a, g, f.weight.grad, 7, 3, "reflect", accumulate=True)
+                if f.bias is not None:
+                    ops.channel_sum(g, f.bias.grad, f.weight.shape[0], accumulate=True)
+        else:
+            wgrad(f, a, g, 7, 1, 3, "reflect", db=True)
         ga = dgrad_reflect(g, "f", a.shape[-1], 7, 3, a.shape[1], a.shape[2])
         # up-sampling convT layers
         for i in (1, 0):

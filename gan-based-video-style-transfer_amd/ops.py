@@ -719,3 +719,30 @@ def loss_masked_l1_bwd(a, b, mask, gout, scale, cl):
     _call("vst_loss_masked_l1_bwd", _p(a), _p(b), _p(mask), _p(gout), _p(grad), npix, a.shape[-1], cl, float(scale),
           _stream())
     return grad
+
+
+# ----------------------------------------------------------------------- tap-GEMM convolutions
+def tap_conv_fwd(x, ck, bias, R, pad, pad_mode="zero", act="none", slope=0.0, role="fwd"):
+    """'same' conv with <= 4 output channels on the MFMA kernel (see vst_tapsum_fwd): ck is the
+    VST_PACK_CK pack [R][S][4][Ci] of the weight, bias padded to 4 (or None); returns NHWC4."""
+    _dev_check(x, ck, bias)
+    N, H, W, Cx = x.shape
+    if ck.shape != (R, R, 4, Cx):
+        raise ValueError("tap_conv_fwd: CK pack shape %s does not match R=%d, Cx=%d" % (tuple(ck.shape), R, Cx))
+    z = conv2d_fwd(x, ck, None, R * R * 4, 1, 1, 1, 0, "zero", role=role)
+    y = torch.empty((N, H, W, 4), device=x.device)
+    _call("vst_tapsum_fwd", _p(z), R * R * 4, _p(bias), _p(y), N, H, W, R, R, pad, PAD[pad_mode], ACT[act],
+          float(slope), _stream())
+    return y
+
+
+def tap_conv_wgrad(x, dy, dw, R, pad, pad_mode="zero", accumulate=True, role="bwd"):
+    """dw [Co<=4][Ci][R][R] (+)= weight gradient of tap_conv_fwd given dy NHWC4 (pre-activation)."""
+    _dev_check(x, dy, dw)
+    N, H, W, Cx = x.shape
+    Co, Ci = dw.shape[0], dw.shape[1]
+    d = torch.empty((N, H, W, R * R * 4), device=x.device)
+    _call("vst_tapfold", _p(dy), _p(d), N, H, W, R, R, pad, PAD[pad_mode], _stream())
+    t = torch.empty((R * R * 4, Ci), device=x.device)
+    conv2d_wgrad(x, d, t, None, 1, 1, 1, 0, "zero", R * R * 4, Ci, Ci, 1, accumulate=False, role=role)
+    _call("vst_tap_wgrad_scatter", _p(t), _p(dw), Co, Ci, R, R, 1 if accumulate else 0, _stream())

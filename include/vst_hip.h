@@ -288,6 +288,20 @@ int vst_instnorm_running_update(const float* stats, float* running_mean, float* 
 int vst_instnorm_stats_from_running(const float* running_mean, const float* running_var,
                                     float* stats, int N, int C, float eps, void* stream);
 
+/* ---- tap-GEMM convolutions with 4 (padded) output channels (generators' last layer) -------- */
+/* Z = vst_conv2d_fwd(x, VST_PACK_CK pack of w seen as a 1x1 conv with R*S*4 outputs) holds
+ * sum_ci x[q][ci] w[co][ci][r][s] for every source pixel q and tap; vst_tapsum_fwd gathers
+ * y[p][co] = act(bias[co] + sum_{r,s} Z[src(p,r,s)][(r*S+s)*4 + co]) for 'same' convolutions
+ * (2*pad == R-1 == S-1, zero or reflect padding; y NHWC4).  Replaces the direct conv of
+ * networks.py:365-367 (c7s1-3) on the matrix cores. */
+int vst_tapsum_fwd(const float* z, int zcs, const float* bias, float* y, int N, int H, int W, int R, int S,
+                   int pad, int pad_mode, int act, float slope, void* stream);
+/* Adjoint gather of the weight gradient: d[q][(r*S+s)*4 + co] = sum_{p: src(p,r,s) = q} g[p][co]
+ * (g NHWC4); then vst_conv2d_wgrad(x, d) as a 1x1 wgrad gives t[(r*S+s)*4 + co][ci], and
+ * vst_tap_wgrad_scatter writes dw[co][ci][r][s] (+)= t (co < Co <= 4). */
+int vst_tapfold(const float* g, float* d, int N, int H, int W, int R, int S, int pad, int pad_mode, void* stream);
+int vst_tap_wgrad_scatter(const float* t, float* dw, int Co, int Ci, int R, int S, int accumulate, void* stream);
+
 /* ---- RAFT inference (SURVEY §8 A19 + §8f rank 3) ------------------------------------------ */
 /* Forward conv with separate row / column zero padding (SepConvGRU's (1,5) / (5,1) kernels with
  * padding (0,2) / (2,0), update.py:36-43); otherwise identical to vst_conv2d_fwd. */

@@ -281,3 +281,29 @@ def test_channel_sum_wide(ops, nhw, cs, cl):
     _close(db, x[:, :cl].double().sum(0).float() + 0.5, tol=1e-6, what="accumulate")
     ops.channel_sum(x.to(DEV), db, cl, accumulate=False)
     _close(db, x[:, :cl].double().sum(0).float(), tol=1e-6, what="overwrite")
+
+
+@pytest.mark.parametrize("co,ci,k,mode", [(3, 64, 7, "reflect"), (2, 64, 7, "reflect"), (3, 32, 3, "zero"),
+                                          (1, 16, 5, "reflect")])
+def test_tap_conv(ops, conv_math, co, ci, k, mode):
+    """Tap-GEMM form of a 'same' conv with <= 4 outputs (generator last layer): forward (+bias, tanh)
+    and the weight gradient against torch autograd, reflect and zero padding."""
+    N, H, W = 2, 11, 13
+    pad = (k - 1) // 2
+    x = _g(81, (N, ci, H, W)).requires_grad_(True)
+    w = (_g(82, (co, ci, k, k), 0.05)).requires_grad_(True)
+    b = _g(83, (co,), 0.1)
+    xp = F.pad(x, (pad,) * 4, mode="reflect") if mode == "reflect" else F.pad(x, (pad,) * 4)
+    y = torch.tanh(F.conv2d(xp, w, b))
+    gy = _g(84, tuple(y.shape))
+    y.backward(gy)
+    ck = ops.weight_pack(w.detach().to(DEV), ops.PACK_CK)
+    bp = torch.zeros(4, device=DEV)
+    bp[:co] = b.to(DEV)
+    xn = _nhwc(x.detach(), ops)
+    yt = ops.tap_conv_fwd(xn, ck, bp, k, pad, mode, act="tanh")
+    _close(_nchw(yt, co, ops), y, tol=CONV_TOL[conv_math], what="tap fwd")
+    g = ops.act_bwd(_nhwc(gy, ops), yt, "tanh")
+    dw = torch.full((co, ci, k, k), 0.25, device=DEV)
+    ops.tap_conv_wgrad(xn, g, dw, k, pad, mode, accumulate=True)
+    _close(dw.cpu() - 0.25, w.grad, tol=CONV_TOL[conv_math], what="tap wgrad")

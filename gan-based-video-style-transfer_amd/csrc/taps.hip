@@ -95,6 +95,82 @@ __global__ void tapfold_k(const float4* __restrict__ g, float4* __restrict__ d, 
   d[i] = acc;
 }
 
+// Row-segment form of tapsum: a 64-lane block owns 64 consecutive output pixels of one row; for
+// each filter row r it stages the S taps of that row for the 64 + S - 1 source pixels in LDS
+// (each pixel's S float4 are contiguous in Z), then every lane sums its S taps from LDS.  Every Z
+// element is read once, in 16*S-byte contiguous runs.
+template <int S>
+__global__ __launch_bounds__(64) void tapsum_row_k(const float4* __restrict__ z, const float* __restrict__ bias,
+                                                   float4* __restrict__ y, int H, int W, int R, int pad,
+                                                   int reflect, int act, float slope) {
+  constexpr int SEG = 64, NSRC = SEG + S - 1;
+  __shared__ float4 lds[NSRC * S];
+  const int lane = threadIdx.x;
+  const int segs = (W + SEG - 1) / SEG;
+  const long row = blockIdx.x / segs;  // (n, h)
+  const int w0 = (blockIdx.x % segs) * SEG;
+  const int h = row % H;
+  const long n = row / H;
+  const int zcs4 = R * S;
+  const int w = w0 + lane;
+  float4 acc = bias ? make_float4(bias[0], bias[1], bias[2], bias[3]) : make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int r = 0; r < R; ++r) {
+    const int hh = src_index(h + r - pad, H, reflect);
+    if (hh < 0) continue;  // whole row zero-padded (uniform over the block)
+    const float4* zr = z + (n * H + hh) * (long)W * zcs4 + r * S;
+    __syncthreads();
+    for (int e = lane; e < NSRC * S; e += SEG) {
+      const int j = e / S, s = e - j * S;
+      const int ww = src_index(w0 - pad + j, W, reflect);
+      lds[e] = (ww >= 0 && w0 - pad + j < W + pad) ? zr[(long)ww * zcs4 + s] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const float4 v = lds[(lane + s) * S + s];
+      acc.x += v.x;
+      acc.y += v.y;
+      acc.z += v.z;
+      acc.w += v.w;
+    }
+  }
+  if (w < W)
+    y[row * W + w] = make_float4(apply_act(acc.x, act, slope), apply_act(acc.y, act, slope),
+                                 apply_act(acc.z, act, slope), apply_act(acc.w, act, slope));
+}
+
+// Data-gradient gather (adjoint of the tap gather): y[q] = sum_{r,s} sum_{p: src(p,r,s) = q} Z[p][(r,s)]
+__global__ void tapgather_k(const float4* __restrict__ z, float4* __restrict__ y, int H, int W, int R, int S,
+                            int pad, int reflect, long P) {
+  const long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= P) return;
+  const int qw = q % W;
+  const long t = q / W;
+  const int qh = t % H;
+  const long n = t / H;
+  const int zcs4 = R * S;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int r = 0; r < R; ++r) {
+    int ph[3];
+    const int mh = preimages(qh, r, pad, H, reflect, ph);
+    for (int a = 0; a < mh; ++a) {
+      const float4* zr = z + (n * H + ph[a]) * (long)W * zcs4 + r * S;
+      for (int s = 0; s < S; ++s) {
+        int pw[3];
+        const int mw = preimages(qw, s, pad, W, reflect, pw);
+        for (int b = 0; b < mw; ++b) {
+          const float4 v = zr[(long)pw[b] * zcs4 + s];
+          acc.x += v.x;
+          acc.y += v.y;
+          acc.z += v.z;
+          acc.w += v.w;
+        }
+      }
+    }
+  }
+  y[q] = acc;
+}
+
 // dw[co][ci][rs] (+)= t[(rs*4 + co)][ci], co < Co
 __global__ void tap_wgrad_scatter_k(const float* __restrict__ t, float* __restrict__ dw, int Co, int Ci, int RS,
                                     int accumulate, long total) {
@@ -119,9 +195,20 @@ extern "C" int vst_tapsum_fwd(const float* z, int zcs, const float* bias, float*
   VST_REQUIRE(pad_mode == VST_PAD_ZERO || (pad < H && pad < W), "tapsum_fwd: reflect pad >= size");
   VST_REQUIRE(2 * pad == R - 1 && 2 * pad == S - 1, "tapsum_fwd: 'same' convolutions only (2*pad == k-1)");
   const long P = (long)N * H * W;
-  hipLaunchKernelGGL(tapsum_k, dim3(ceil_div(P, 256)), dim3(256), 0, (hipStream_t)stream,
-                     reinterpret_cast<const float4*>(z), zcs / 4, bias, reinterpret_cast<float4*>(y), H, W, R, S, pad,
-                     pad_mode == VST_PAD_REFLECT, act, slope, P);
+  const int refl = pad_mode == VST_PAD_REFLECT;
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 rows((unsigned)((long)N * H * ceil_div(W, 64)));
+  switch (S) {
+    case 3: hipLaunchKernelGGL(tapsum_row_k<3>, rows, dim3(64), 0, st, reinterpret_cast<const float4*>(z), bias,
+                               reinterpret_cast<float4*>(y), H, W, R, pad, refl, act, slope); break;
+    case 5: hipLaunchKernelGGL(tapsum_row_k<5>, rows, dim3(64), 0, st, reinterpret_cast<const float4*>(z), bias,
+                               reinterpret_cast<float4*>(y), H, W, R, pad, refl, act, slope); break;
+    case 7: hipLaunchKernelGGL(tapsum_row_k<7>, rows, dim3(64), 0, st, reinterpret_cast<const float4*>(z), bias,
+                               reinterpret_cast<float4*>(y), H, W, R, pad, refl, act, slope); break;
+    default:
+      hipLaunchKernelGGL(tapsum_k, dim3(ceil_div(P, 256)), dim3(256), 0, st, reinterpret_cast<const float4*>(z),
+                         zcs / 4, bias, reinterpret_cast<float4*>(y), H, W, R, S, pad, refl, act, slope, P);
+  }
   return check_launch("tapsum_fwd");
 }
 
@@ -144,4 +231,16 @@ extern "C" int vst_tap_wgrad_scatter(const float* t, float* dw, int Co, int Ci, 
   hipLaunchKernelGGL(tap_wgrad_scatter_k, dim3(ceil_div(total, 256)), dim3(256), 0, (hipStream_t)stream, t, dw, Co,
                      Ci, R * S, accumulate, total);
   return check_launch("tap_wgrad_scatter");
+}
+
+extern "C" int vst_tapgather(const float* z, float* y, int N, int H, int W, int R, int S, int pad, int pad_mode,
+                             void* stream) {
+  VST_REQUIRE(z && y && N > 0 && H > 0 && W > 0 && R > 0 && S > 0 && pad >= 0, "tapgather: bad args");
+  VST_REQUIRE(pad_mode == VST_PAD_ZERO || (pad < H && pad < W), "tapgather: reflect pad >= size");
+  VST_REQUIRE(2 * pad == R - 1 && 2 * pad == S - 1, "tapgather: 'same' convolutions only (2*pad == k-1)");
+  const long P = (long)N * H * W;
+  hipLaunchKernelGGL(tapgather_k, dim3(ceil_div(P, 256)), dim3(256), 0, (hipStream_t)stream,
+                     reinterpret_cast<const float4*>(z), reinterpret_cast<float4*>(y), H, W, R, S, pad,
+                     pad_mode == VST_PAD_REFLECT, P);
+  return check_launch("tapgather");
 }

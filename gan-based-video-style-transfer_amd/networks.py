@@ -322,6 +322,8 @@ class ResnetGenerator(FlatNet):
         P = {"c0": _pack_conv(c0), "d0": _pack_conv(d[0]), "d1": _pack_conv(d[1]), "f": _pack_conv(f)}
         if TAP_LAST:
             P["ftap"] = ops.weight_pack(f.weight, ops.PACK_CK)
+            if c0.weight.shape[1] <= 4:  # image-input first layer: its data gradient as a tap gather
+                P["c0kc"] = ops.weight_pack(c0.weight, ops.PACK_KC)
         P["ikf"] = {}
         for i, b in enumerate(blocks):
             P[f"b{i}a"] = _pack_conv(b.conv_block[1])
@@ -475,7 +477,10 @@ class _GeneratorFn(torch.autograd.Function):
         wgrad(c0, x, dy, 7, 1, 3, "reflect")
         gx = None
         if ctx.needs_input_grad[0]:
-            gx = dgrad_reflect(dy, "c0", x.shape[-1], 7, 3, x.shape[1], x.shape[2])
+            if "c0kc" in P and x.shape[-1] == 4:
+                gx = ops.tap_conv_dgrad(dy, P["c0kc"], 7, 3, "reflect")
+            else:
+                gx = dgrad_reflect(dy, "c0", x.shape[-1], 7, 3, x.shape[1], x.shape[2])
         ctx.sv = None
         return gx, None, None
 

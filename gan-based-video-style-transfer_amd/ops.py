@@ -746,3 +746,16 @@ def tap_conv_wgrad(x, dy, dw, R, pad, pad_mode="zero", accumulate=True, role="bw
     t = torch.empty((R * R * 4, Ci), device=x.device)
     conv2d_wgrad(x, d, t, None, 1, 1, 1, 0, "zero", R * R * 4, Ci, Ci, 1, accumulate=False, role=role)
     _call("vst_tap_wgrad_scatter", _p(t), _p(dw), Co, Ci, R, R, 1 if accumulate else 0, _stream())
+
+
+def tap_conv_dgrad(dy, kc, R, pad, pad_mode="zero", role="bwd"):
+    """Data gradient (NHWC4) of a 'same' conv with <= 4 input channels: kc = VST_PACK_KC pack
+    [R][R][4][Cy] of its weight (see vst_tapgather)."""
+    _dev_check(dy, kc)
+    N, H, W, Cy = dy.shape
+    if kc.shape != (R, R, 4, Cy):
+        raise ValueError("tap_conv_dgrad: KC pack shape %s does not match R=%d, Cy=%d" % (tuple(kc.shape), R, Cy))
+    z = conv2d_fwd(dy, kc, None, R * R * 4, 1, 1, 1, 0, "zero", role=role)
+    y = torch.empty((N, H, W, 4), device=dy.device)
+    _call("vst_tapgather", _p(z), _p(y), N, H, W, R, R, pad, PAD[pad_mode], _stream())
+    return y

@@ -301,6 +301,11 @@ int vst_tapsum_fwd(const float* z, int zcs, const float* bias, float* y, int N, 
  * vst_tap_wgrad_scatter writes dw[co][ci][r][s] (+)= t (co < Co <= 4). */
 int vst_tapfold(const float* g, float* d, int N, int H, int W, int R, int S, int pad, int pad_mode, void* stream);
 int vst_tap_wgrad_scatter(const float* t, float* dw, int Co, int Ci, int R, int S, int accumulate, void* stream);
+/* Data gradient of a 'same' conv with <= 4 INPUT channels (the generators' first layer, c7s1-64 on
+ * the image): z = vst_conv2d_fwd(dy, VST_PACK_KC pack seen as a 1x1 conv with R*S*4 outputs), then
+ * y[q][ci] = sum_{r,s} sum_{p: src(p,r,s) = q} z[p][(r*S+s)*4 + ci]  (y NHWC4). */
+int vst_tapgather(const float* z, float* y, int N, int H, int W, int R, int S, int pad, int pad_mode,
+                  void* stream);
 
 /* ---- RAFT inference (SURVEY §8 A19 + §8f rank 3) ------------------------------------------ */
 /* Forward conv with separate row / column zero padding (SepConvGRU's (1,5) / (5,1) kernels with

@@ -288,7 +288,7 @@ def test_channel_sum_wide(ops, nhw, cs, cl):
 def test_tap_conv(ops, conv_math, co, ci, k, mode):
     """Tap-GEMM form of a 'same' conv with <= 4 outputs (generator last layer): forward (+bias, tanh)
     and the weight gradient against torch autograd, reflect and zero padding."""
-    N, H, W = 2, 11, 13
+    N, H, W = 2, 11, 75  # W > 64: several row segments in the LDS tap-sum
     pad = (k - 1) // 2
     x = _g(81, (N, ci, H, W)).requires_grad_(True)
     w = (_g(82, (co, ci, k, k), 0.05)).requires_grad_(True)
@@ -307,3 +307,21 @@ def test_tap_conv(ops, conv_math, co, ci, k, mode):
     dw = torch.full((co, ci, k, k), 0.25, device=DEV)
     ops.tap_conv_wgrad(xn, g, dw, k, pad, mode, accumulate=True)
     _close(dw.cpu() - 0.25, w.grad, tol=CONV_TOL[conv_math], what="tap wgrad")
+
+
+@pytest.mark.parametrize("ci,co,k,mode", [(3, 64, 7, "reflect"), (2, 64, 7, "reflect"), (3, 32, 3, "zero")])
+def test_tap_conv_dgrad(ops, conv_math, ci, co, k, mode):
+    """Data gradient of a 'same' conv with <= 4 input channels (generator first layer) as a 1x1 conv
+    over all taps + the adjoint tap gather, against torch autograd."""
+    N, H, W = 2, 12, 70
+    pad = (k - 1) // 2
+    x = _g(91, (N, ci, H, W)).requires_grad_(True)
+    w = _g(92, (co, ci, k, k), 0.05)
+    xp = F.pad(x, (pad,) * 4, mode="reflect") if mode == "reflect" else F.pad(x, (pad,) * 4)
+    y = F.conv2d(xp, w)
+    gy = _g(93, tuple(y.shape))
+    y.backward(gy)
+    kc = ops.weight_pack(w.to(DEV), ops.PACK_KC)
+    dx = ops.tap_conv_dgrad(_nhwc(gy, ops), kc, k, pad, mode)
+    _close(_nchw(dx, ci, ops), x.grad, tol=CONV_TOL[conv_math], what="tap dgrad")
+    assert float(dx[..., ci:].abs().max()) == 0.0

@@ -115,15 +115,29 @@ __device__ __forceinline__ bool fold_slices(const double* __restrict__ part, int
   __shared__ double red[NV][4][64];
   const int cl = threadIdx.x & 63, q = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
-  double acc[NV];
+  // 4 independent accumulator chains per thread (slices q, q+4, q+8, q+12, then +16 ...) so the
+  // loads overlap instead of serialising on the fp64 add chain; combined in a fixed order.
+  double acc[NV], acc4[4][NV];
 #pragma unroll
-  for (int v = 0; v < NV; ++v) acc[v] = 0.0;
-  if (c < C)
-    for (int z = q; z < nsplit; z += 4) {
-      const double* a = part + (((long)n * nsplit + z) * C + c) * NV;
+  for (int u = 0; u < 4; ++u)
 #pragma unroll
-      for (int v = 0; v < NV; ++v) acc[v] += a[v];
+    for (int v = 0; v < NV; ++v) acc4[u][v] = 0.0;
+  if (c < C) {
+    const long zs = (long)C * NV;
+    const double* base = part + (((long)n * nsplit) * C + c) * NV;
+    int z = q;
+    for (; z + 12 < nsplit; z += 16) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int v = 0; v < NV; ++v) acc4[u][v] += base[(long)(z + 4 * u) * zs + v];
     }
+    for (; z < nsplit; z += 4)
+#pragma unroll
+      for (int v = 0; v < NV; ++v) acc4[0][v] += base[(long)z * zs + v];
+  }
+#pragma unroll
+  for (int v = 0; v < NV; ++v) acc[v] = (acc4[0][v] + acc4[1][v]) + (acc4[2][v] + acc4[3][v]);
 #pragma unroll
   for (int v = 0; v < NV; ++v) red[v][q][cl] = acc[v];
   __syncthreads();

@@ -75,9 +75,9 @@ def dominant_kernel_roofline(B, probe):
     """The dominant kernel — the ResnetBlock conv forward (3x3 reflect, 256->256 @64x64, B frames;
     36 launches per train step) — timed live over the timed steps: HIP events around each of its
     launches on the stream it is launched on (ops.LaunchProbe).  It runs the training forward
-    arithmetic (bf16x6: fp32-equivalent products from 6 bf16 MFMAs per MAC); `peak` is the dense
-    fp32 MFMA peak of the dtype it delivers, `emulation_peak` the bf16 peak / 6 ceiling of the
-    arithmetic actually executed."""
+    arithmetic (bf16x6: fp32-equivalent products from 6 bf16 MFMAs per MAC), so its hardware
+    ceiling — `peak` — is the dense bf16 MFMA peak / 6 in fp32-equivalent FLOP/s; the fp32 MFMA
+    peak (the ceiling of a native-fp32 kernel, which this one exceeds) is reported beside it."""
     ms = probe.mean_ms()
     flop = 2.0 * (B * 64 * 64) * 256 * (256 * 9)
     achieved = flop / (ms * 1e-3) / 1e12
@@ -90,11 +90,13 @@ def dominant_kernel_roofline(B, probe):
             traffic = None
     emu = BF16_MFMA_PEAK_TFLOPS / 6.0
     return {"kernel": "conv_fprop_bf_k<128x128, bf16x6> (ResnetBlock 3x3 256->256 @64x64, B=%d)" % B,
-            "bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
-            "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
+            "bound": "mfma", "achieved": round(achieved, 2), "peak": round(emu, 1),
+            "unit": "TFLOP/s", "frac": round(achieved / emu, 4),
+            "peak_basis": "dense bf16 MFMA %.0f TFLOP/s / 6 bf16 products per fp32-equivalent MAC" %
+                          BF16_MFMA_PEAK_TFLOPS,
             "traffic": traffic, "avg_launch_ms": round(ms, 4), "flop_per_launch": flop,
             "launches_timed": len(probe.events),
-            "emulation_peak": round(emu, 1), "emulation_frac": round(achieved / emu, 4)}
+            "fp32_mfma_peak": FP32_MFMA_PEAK_TFLOPS, "frac_of_fp32_mfma_peak": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4)}
 
 
 def warp_roofline(device, N=32, C=64, H=436, W=1024, reps=10):

@@ -244,6 +244,9 @@ DGRAD_AS_FPROP = os.environ.get("VST_DGRAD_FPROP", "1") != "0"
 # The generator's last conv (4 padded output channels) runs as a tap GEMM on the matrix cores
 # (ops.tap_conv_fwd / tap_conv_wgrad) instead of the VALU skinny kernel; VST_TAP_CONV=0 disables.
 TAP_LAST = os.environ.get("VST_TAP_CONV", "1") != "0"
+# The up-sampling ConvTranspose2d (k3 s2 p1 op1) forward as four sub-pixel phase convs on the
+# split-bf16 forward kernel + an interleave (ops.convT3s2_fwd); VST_CONVT_PHASES=0 disables.
+CONVT_PHASES = os.environ.get("VST_CONVT_PHASES", "1") != "0"
 
 
 def _ikf(m):
@@ -333,6 +336,8 @@ class ResnetGenerator(FlatNet):
         for i, m in enumerate(u):
             # ConvTranspose2d fwd = transposed kernel with rows (r,s,ci) -> CK pack of Wt[Ci][Co];
             # its dgrad = forward conv with KC pack of Wt seen as [O=Ci][I=Co] -> rows (r,s,co), cols ci
+            if CONVT_PHASES:
+                P[f"u{i}ph"] = ops.convT3s2_phase_packs(m.weight)
             P[f"u{i}"] = (ops.weight_pack(m.weight, ops.PACK_FWD), ops.weight_pack(m.weight, ops.PACK_DGRAD),
                           _padded_bias(m))
         return P
@@ -379,7 +384,10 @@ class _GeneratorFn(torch.autograd.Function):
             cout = ngf * 2 ** (1 - i)
             _, ck, b = P[f"u{i}"]
             Hi, Wi = a.shape[1], a.shape[2]
-            y = ops.conv2d_tfwd(a, ck, b, 2 * Hi, 2 * Wi, cpad(cout), 3, 3, 2, 1, role=role)
+            if f"u{i}ph" in P and a.shape[-1] % 8 == 0:
+                y = ops.convT3s2_fwd(a, P[f"u{i}ph"], b, cpad(cout), role=role)
+            else:
+                y = ops.conv2d_tfwd(a, ck, b, 2 * Hi, 2 * Wi, cpad(cout), 3, 3, 2, 1, role=role)
             s = ops.instnorm_stats(y)
             an = ops.instnorm_act_fwd(y, s, "relu")
             sv[f"u{i}"] = (a, y, s, an)

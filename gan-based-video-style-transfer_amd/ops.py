@@ -759,3 +759,30 @@ def tap_conv_dgrad(dy, kc, R, pad, pad_mode="zero", role="bwd"):
     y = torch.empty((N, H, W, 4), device=dy.device)
     _call("vst_tapgather", _p(z), _p(y), N, H, W, R, R, pad, PAD[pad_mode], _stream())
     return y
+
+
+def convT3s2_phase_packs(wt):
+    """Phase weight packs of a ConvTranspose2d(k=3, stride=2, padding=1, output_padding=1) weight
+    wt [Ci][Co][3][3]: output parity a (rows) / b (cols) uses taps k=1 (even) or k=(2, 0) at input
+    offsets (0, +1) (odd).  Returns the VST_PACK_OK packs of the 1x1, 1x2, 2x1, 2x2 phase convs."""
+    wc = wt.detach().permute(1, 0, 2, 3)  # [Co][Ci][kh][kw]
+    odd = torch.tensor([2, 0], device=wt.device)
+    ev = torch.tensor([1], device=wt.device)
+    packs = []
+    for a, b in ((0, 0), (0, 1), (1, 0), (1, 1)):
+        w = wc.index_select(2, odd if a else ev).index_select(3, odd if b else ev).contiguous()
+        packs.append(weight_pack(w, PACK_OK))
+    return packs
+
+
+def convT3s2_fwd(x, packs, bias, cop, act="none", role="fwd"):
+    """ConvTranspose2d(k=3, s=2, p=1, op=1) forward on NHWC x via four phase convs + interleave."""
+    _dev_check(x, bias)
+    N, H, W, _ = x.shape
+    outs = []
+    for (a, b), wp in zip(((0, 0), (0, 1), (1, 0), (1, 1)), packs):
+        outs.append(conv2d_fwd_hw(x, wp, bias, cop, 1 + a, 1 + b, 1, a, b, act=act, role=role))
+    y = torch.empty((N, 2 * H, 2 * W, cop), device=x.device)
+    _call("vst_interleave_phases", _p(outs[0]), _p(outs[1]), _p(outs[2]), _p(outs[3]), _p(y), N, H, W, cop,
+          _stream())
+    return y

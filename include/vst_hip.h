@@ -307,6 +307,13 @@ int vst_tap_wgrad_scatter(const float* t, float* dw, int Co, int Ci, int R, int 
 int vst_tapgather(const float* z, float* y, int N, int H, int W, int R, int S, int pad, int pad_mode,
                   void* stream);
 
+/* ConvTranspose2d(k=3, stride 2, padding 1, output_padding 1) forward (CycleGAN networks.py:357-364)
+ * as four sub-pixel phase convolutions on the forward kernels: P_00 = 1x1 conv, P_01 = 1x2 conv
+ * (pad 0,1), P_10 = 2x1 (pad 1,0), P_11 = 2x2 (pad 1,1) with the phase's taps of the transposed
+ * weight; this interleaves them: y[n][2i+a][2j+b][c] = P_ab[n][i+a][j+b][c] (P_ab is (H+a) x (W+b)). */
+int vst_interleave_phases(const float* p00, const float* p01, const float* p10, const float* p11, float* y, int N,
+                          int H, int W, int C, void* stream);
+
 /* ---- RAFT inference (SURVEY §8 A19 + §8f rank 3) ------------------------------------------ */
 /* Forward conv with separate row / column zero padding (SepConvGRU's (1,5) / (5,1) kernels with
  * padding (0,2) / (2,0), update.py:36-43); otherwise identical to vst_conv2d_fwd. */

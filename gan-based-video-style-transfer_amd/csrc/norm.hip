@@ -13,6 +13,10 @@
 namespace vst {
 
 constexpr int NRED = 256;
+// target number of (slice, sample) blocks of a reduction pass over N*HW pixels
+#ifndef IN_TARGET_BLOCKS
+#define IN_TARGET_BLOCKS 512
+#endif
 
 struct RedGeom {
   int LP, PG, SP, nsplit;  // lanes per pixel (C/4), pixel groups, pixels per slice, slices
@@ -23,7 +27,7 @@ static bool red_geom(int N, int HW, int C, RedGeom& g) {
   g.LP = C / 4;
   if (g.LP > NRED) return false;
   g.PG = NRED / g.LP;  // threads beyond LP*PG idle when LP does not divide NRED
-  long sp = ((long)N * HW + 511) / 512;
+  long sp = ((long)N * HW + IN_TARGET_BLOCKS - 1) / IN_TARGET_BLOCKS;
   if (sp < 2L * g.PG) sp = 2L * g.PG;
   sp = (sp + g.PG - 1) / g.PG * g.PG;
   if (sp > HW) sp = HW;

@@ -363,6 +363,7 @@ def main():
     if rank == 0 and not args.no_extras:
         out["roofline"] = dominant_kernel_roofline(B, probe)
         out["inference"] = inference_fps(device)
+    if rank == 0 and world == 1 and not args.no_extras:  # single-GPU context numbers only
         out["extras"] = {"sintel_inference": sintel_inference_fps(device),
                          "warp_roofline": warp_roofline(device),
                          "raft_corr": corr_volume(device),

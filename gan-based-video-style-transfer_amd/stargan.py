@@ -25,7 +25,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import ops
-from .networks import Conv2d, ConvTranspose2d, FlatNet, _Marker
+from .networks import TAP_LAST, Conv2d, ConvTranspose2d, FlatNet, _Marker
 from .ops import cpad
 from .optim import FusedAdam
 
@@ -310,6 +310,8 @@ class Generator(FlatNet):
              "up": [(ops.weight_pack(c.weight, ops.PACK_FWD), ops.weight_pack(c.weight, ops.PACK_DGRAD))
                     for c, _ in up],
              "last": (ops.weight_pack(last.weight, ops.PACK_FWD), ops.weight_pack(last.weight, ops.PACK_DGRAD))}
+        if TAP_LAST:  # 64 -> 3 output channels: tap GEMM on the matrix cores (ops.tap_conv_fwd)
+            P["last_tap"] = ops.weight_pack(last.weight, ops.PACK_CK)
         return P
 
     def forward(self, x, c):
@@ -385,7 +387,10 @@ class _StarGFn(torch.autograd.Function):
             an = ops.instnorm_affine_fwd(y, s, g, b, "relu")
             sv[("up", i)] = (a, y, s)
             a = an
-        out = ops.conv2d_fwd(a, P["last"][0], None, cpad(3), 7, 7, 1, 3, "zero", act="tanh", role=role)
+        if "last_tap" in P:
+            out = ops.tap_conv_fwd(a, P["last_tap"], None, 7, 3, "zero", act="tanh", role=role)
+        else:
+            out = ops.conv2d_fwd(a, P["last"][0], None, cpad(3), 7, 7, 1, 3, "zero", act="tanh", role=role)
         sv["last"] = (a, out)
         ctx.sv, ctx.net, ctx.P = sv, net, P
         ctx.train_w = anchor.requires_grad
@@ -410,7 +415,11 @@ class _StarGFn(torch.autograd.Function):
 
         a, out = sv["last"]
         g = ops.act_bwd(gout.contiguous(), out, "tanh")
-        wgrad(last, a, g, 7, 1, 3)
+        if "last_tap" in P:
+            if tw:
+                ops.tap_conv_wgrad(a, g, last.weight.grad, 7, 3, "zero", accumulate=True)
+        else:
+            wgrad(last, a, g, 7, 1, 3)
         g = ops.conv2d_tfwd(g, P["last"][1], None, a.shape[1], a.shape[2], a.shape[-1], 7, 7, 1, 3)
         for i in (1, 0):
             conv, norm = up[i]

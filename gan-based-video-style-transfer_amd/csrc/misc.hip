@@ -37,7 +37,8 @@ __global__ void nhwc_to_nchw_k(const float* __restrict__ x, float* __restrict__ 
 
 // w[O][I][R][S] -> KC: out[r][s][i][o] (Ip x Op per tap) or CK: out[r][s][o][i] (Op x Ip per tap)
 __global__ void weight_pack_k(const float* __restrict__ w, float* __restrict__ out, int O, int I,
-                              int R, int S, int Op, int Ip, int mode, long total) {
+                              int R, int S, int Op, int Ip, int mode, long total,
+                              __bf16* __restrict__ split = nullptr) {
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= total) return;
   const int RS = R * S;
@@ -64,7 +65,16 @@ __global__ void weight_pack_k(const float* __restrict__ w, float* __restrict__ o
     i = q / RS;
     if (mode == VST_PACK_IKF) rs = RS - 1 - rs;
   }
-  out[idx] = (o < O && i < I) ? w[((long)o * I + i) * RS + rs] : 0.f;
+  const float v = (o < O && i < I) ? w[((long)o * I + i) * RS + rs] : 0.f;
+  out[idx] = v;
+  if (split) {  // the three bf16 planes hi, mid, lo of the split-arithmetic kernels (vst_weight_split)
+    const __bf16 h = (__bf16)v;
+    const float r = v - (float)h;
+    const __bf16 m = (__bf16)r;
+    split[idx] = h;
+    split[total + idx] = m;
+    split[2 * total + idx] = (__bf16)(r - (float)m);
+  }
 }
 
 __global__ void adam_k(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
@@ -125,6 +135,16 @@ extern "C" int vst_weight_pack(const float* w, float* out, int O, int I, int R, 
   hipLaunchKernelGGL(weight_pack_k, dim3(ceil_div(total, 256)), dim3(256), 0, (hipStream_t)stream, w,
                      out, O, I, R, S, Op, Ip, mode, total);
   return check_launch("weight_pack");
+}
+
+extern "C" int vst_weight_pack_split(const float* w, float* out, void* split, int O, int I, int R, int S, int Op,
+                                     int Ip, int mode, void* stream) {
+  VST_REQUIRE(w && out && split && O <= Op && I <= Ip && mode >= VST_PACK_KC && mode <= VST_PACK_IKF,
+              "weight_pack_split: bad args");
+  const long total = (long)R * S * Op * Ip;
+  hipLaunchKernelGGL(weight_pack_k, dim3(ceil_div(total, 256)), dim3(256), 0, (hipStream_t)stream, w, out, O, I, R,
+                     S, Op, Ip, mode, total, reinterpret_cast<__bf16*>(split));
+  return check_launch("weight_pack_split");
 }
 
 extern "C" int vst_adam_step(float* p, const float* g, float* m, float* v, long n, float lr,

@@ -76,10 +76,9 @@ def weight_pack(w, mode, transposed=False):
     shape = {PACK_KC: (R, S, Ip, Op), PACK_CK: (R, S, Op, Ip), PACK_OK: (Op, R, S, Ip),
              PACK_IK: (Ip, R, S, Op), PACK_IKF: (Ip, R, S, Op)}[mode]
     out = torch.empty(shape, device=w.device, dtype=torch.float32)
-    _call("vst_weight_pack", _p(w), _p(out), O, I_, R, S, Op, Ip, mode, _stream())
-    # the split-arithmetic conv paths read the pack as three bf16 planes (vst_weight_split)
+    # the split-arithmetic conv paths read the pack as three bf16 planes (written in the same pass)
     split = torch.empty((3,) + shape, device=w.device, dtype=torch.bfloat16)
-    _call("vst_weight_split", _p(out), _p(split), out.numel(), _stream())
+    _call("vst_weight_pack_split", _p(w), _p(out), _p(split), O, I_, R, S, Op, Ip, mode, _stream())
     out.vst_split = split
     return out
 

@@ -81,6 +81,9 @@ int vst_weight_pack(const float* w, float* out, int O, int I, int R, int S, int 
  * out[n..2n) = mid = bf16(v - hi), out[2n..3n) = lo = bf16(v - hi - mid) (2-byte elements).
  * The split-arithmetic conv paths read these planes as their B operand (`wsplit`). */
 int vst_weight_split(const float* w, void* out, long n, void* stream);
+/* vst_weight_pack + vst_weight_split of the pack in one pass (split: 3 * R*S*Op*Ip bf16). */
+int vst_weight_pack_split(const float* w, float* out, void* split, int O, int I, int R, int S, int Op, int Ip,
+                          int mode, void* stream);
 
 /* ---- convolution (implicit GEMM on MFMA) -------------------------------------------------- */
 /* `math` argument of vst_conv2d_fwd / _tfwd / _wgrad: the GEMM arithmetic of that call.

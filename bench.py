@@ -68,28 +68,33 @@ def _time_on_stream(fn, reps, warm=3):
     return e0.elapsed_time(e1) / reps
 
 
-DOMINANT_KEY = lambda B: (B, 64, 64, 256, 256, 3, 1)  # noqa: E731  ResnetBlock conv fprop (N,H,W,Cx,Cop,R,st)
+# ResnetBlock conv forward (N,H,W,Cx,Cop,R,stride,pad,mode) as launched by the batched G_A calls
+# (N = 2B: [real_A, real_A2] and [fake_A, real_B]); pad 1 reflect separates it from the stride-1
+# data gradient that runs on the same kernel over the padded frame (pad 2 zero).
+DOMINANT_KEY = lambda B: (2 * B, 64, 64, 256, 256, 3, 1, 1, "reflect")  # noqa: E731
 
 
 def dominant_kernel_roofline(B, probe):
-    """The dominant kernel — the ResnetBlock conv forward (3x3 reflect, 256->256 @64x64, B frames;
-    36 launches per train step) — timed live over the timed steps: HIP events around each of its
+    """The dominant kernel — the ResnetBlock conv forward (3x3 reflect, 256->256 @64x64, 2B frames:
+    the batched G_A calls, 36 launches per train step) — timed live over the timed steps: HIP events around each of its
     launches on the stream it is launched on (ops.LaunchProbe).  It runs the training forward
     arithmetic (bf16x6: fp32-equivalent products from 6 bf16 MFMAs per MAC), so its hardware
     ceiling — `peak` — is the dense bf16 MFMA peak / 6 in fp32-equivalent FLOP/s; the fp32 MFMA
     peak (the ceiling of a native-fp32 kernel, which this one exceeds) is reported beside it."""
     ms = probe.mean_ms()
-    flop = 2.0 * (B * 64 * 64) * 256 * (256 * 9)
+    N = probe.key[0]
+    flop = 2.0 * (N * 64 * 64) * 256 * (256 * 9)
     achieved = flop / (ms * 1e-3) / 1e12
     traffic = None
     pmc = os.path.join(HERE, "profiles", "r01_conv_fprop_pmc.json")
     if os.path.exists(pmc):
         try:
-            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+            rec = json.load(open(pmc))
+            traffic = rec.get("hbm_bytes_per_launch") if rec.get("batch") == N else None
         except Exception:
             traffic = None
     emu = BF16_MFMA_PEAK_TFLOPS / 6.0
-    return {"kernel": "conv_fprop_bf_k<128x128, bf16x6> (ResnetBlock 3x3 256->256 @64x64, B=%d)" % B,
+    return {"kernel": "conv_fprop_bf_k<128x128, bf16x6> (ResnetBlock 3x3 reflect 256->256 @64x64, N=%d)" % N,
             "bound": "mfma", "achieved": round(achieved, 2), "peak": round(emu, 1),
             "unit": "TFLOP/s", "frac": round(achieved / emu, 4),
             "peak_basis": "dense bf16 MFMA %.0f TFLOP/s / 6 bf16 products per fp32-equivalent MAC" %

@@ -86,7 +86,7 @@ def weight_pack(w, mode, transposed=False):
 # --------------------------------------------------------------------------------------- conv
 class LaunchProbe:
     """Measurement hook (bench.py): HIP events around every vst_conv2d_fwd launch of one shape
-    (N, H, W, Cx, Cop, R, stride), recorded on the stream the kernel is launched on."""
+    (N, H, W, Cx, Cop, R, stride, pad, pad_mode), recorded on the stream the kernel is launched on."""
 
     def __init__(self, key):
         self.key, self.events = key, []
@@ -112,7 +112,7 @@ def conv2d_fwd(x, wp, bias, cop, R, S, stride, pad, pad_mode="zero", act="none",
     Ho = (H + 2 * pad - R) // stride + 1
     Wo = (W + 2 * pad - S) // stride + 1
     y = out if out is not None else torch.empty((N, Ho, Wo, cop), device=x.device)
-    probe = _probe if (_probe is not None and _probe.key == (N, H, W, Cx, cop, R, stride)) else None
+    probe = _probe if (_probe is not None and _probe.key == (N, H, W, Cx, cop, R, stride, pad, pad_mode)) else None
     if probe is not None:
         ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
         ev[0].record()

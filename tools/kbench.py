@@ -1,5 +1,5 @@
 """Developer: launch one conv family on the ResnetBlock shape (B=4, 64x64x256, 3x3 reflect) a few
-times — the target of rocprofv3 --pmc passes.  usage: kbench.py fprop|tconv|wgrad [reps]"""
+times (batch KB_B, default 8) — the target of rocprofv3 --pmc passes.  usage: kbench.py fprop|tconv|wgrad [reps]"""
 import os
 import sys
 
@@ -13,7 +13,7 @@ gbvst._lib.load()
 which = sys.argv[1]
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
 dev = torch.device("cuda")
-B, H, C = 4, 64, 256
+B, H, C = int(os.environ.get("KB_B", "8")), 64, 256  # 8 = the batched G_A calls of the train step
 x = torch.randn(B, H, H, C, device=dev)
 w = torch.randn(C, C, 3, 3, device=dev) * 0.02
 kc, ck = ops.weight_pack(w, ops.PACK_FWD), ops.weight_pack(w, ops.PACK_DGRAD)

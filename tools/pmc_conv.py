@@ -27,9 +27,10 @@ write = per_dispatch(wd, "WRITE_SIZE", sub)
 assert fetch and write, (len(fetch), len(write))
 f_kb = sum(fetch) / len(fetch)
 w_kb = sum(write) / len(write)
-B, H, C = 4, 64, 256
+import os  # noqa: E402
+B, H, C = int(os.environ.get("KB_B", "8")), 64, 256
 alg = 4.0 * B * H * H * C * 2 + 256 * 2304 * 3 * 2  # x read once + y written once + 3 bf16 weight planes
-res = {"kernel": sub, "shape": "ResnetBlock 3x3 reflect 256->256 @64x64, B=4 (bf16x6 forward)",
+res = {"kernel": sub, "shape": "ResnetBlock 3x3 reflect 256->256 @64x64, N=%d (bf16x6 forward)" % B, "batch": B,
        "dispatches": [len(fetch), len(write)], "fetch_kb_raw": f_kb, "write_kb_raw": w_kb,
        "fetch_bytes": 2 * f_kb * 1024, "write_bytes": w_kb * 1024,
        "hbm_bytes_per_launch": 2 * f_kb * 1024 + w_kb * 1024, "algorithmic_bytes": alg,

@@ -218,7 +218,7 @@ def raft_inference(device, B=1, H=436, W=1024, iters=20, reps=3):
 
 def mogan_train_fps(device, B=4, S=256, pairs=2):
     """MoGAN C5-style step: CycleGAN ngf=ndf=64 generators / discriminators, motion nets,
-    8 RAFT calls (20 iterations) per optimize_parameters, E-step / M-step alternating; B frame pairs
+    8 RAFT flows (20 iterations; one batched call) per optimize_parameters, E-step / M-step alternating; B frame pairs
     of SxS, random-init weights.  Reported per optimize_parameters call (E and M averaged)."""
     from gbvst import mogan_model
     from gbvst.options import default_opt
@@ -235,7 +235,7 @@ def mogan_train_fps(device, B=4, S=256, pairs=2):
         m.optimize_parameters()
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / (2 * pairs)
-    return {"metric": "MoGAN optimize_parameters frames/s %dx%d (8 RAFT calls x 20 iterations)" % (S, S),
+    return {"metric": "MoGAN optimize_parameters frames/s %dx%d (8 RAFT flows x 20 iterations per step)" % (S, S),
             "batch": B, "value": round(B / dt, 2), "unit": "frames/s", "ms_per_step": round(dt * 1e3, 3)}
 
 

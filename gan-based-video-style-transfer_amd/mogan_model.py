@@ -21,6 +21,7 @@ import torch
 
 from . import networks, ops
 from .base_model import BaseModel
+from .cycle_gan_model import BATCH_PASSES
 from .flowtools import warp_nhwc
 from .image_pool import ImagePool
 from .optim import FusedAdam
@@ -140,6 +141,8 @@ class CycleGANModel(BaseModel):
     # ------------------------------------------------------------------------------ forward
     def forward_train(self):
         """:160-196."""
+        if BATCH_PASSES:
+            return self._forward_train_batched()
         G_A, G_B = self.netG_A.forward_nhwc, self.netG_B.forward_nhwc
         self.fake_B = G_A(self.real_A)
         self.rec_A = G_B(self.fake_B)
@@ -166,6 +169,35 @@ class CycleGANModel(BaseModel):
         self.warp_A = warp_nhwc(self.fake_A, ops.nhwc_to_nchw(self.bf_M_B.detach(), 2))
         self.mask_B = ops.fbcheck(ops.nhwc_to_nchw(self.ff_real_B, 2), ops.nhwc_to_nchw(self.bf_real_B, 2))
 
+    def _forward_train_batched(self):
+        """forward_train with its passes grouped (per-sample layers, so every sample's result is the
+        unbatched one): G_A[real_A, real_A2], G_B[fake_B, fake_B2, real_B, real_B2, (real_A)],
+        G_A[fake_A, fake_A2, (real_B)] (the E-step's identity passes ride along), then ONE RAFT call
+        over all eight frame pairs and one call per motion net."""
+        B = self.real_A.shape[0]
+        idt = self.e_step and self.opt.lambda_identity > 0
+        ya = self.netG_A.forward_nhwc(torch.cat([self.real_A, self.real_A2]))
+        self.fake_B, self.fake_B2 = ya[:B], ya[B:]
+        yb = self.netG_B.forward_nhwc(torch.cat([self.fake_B, self.fake_B2, self.real_B, self.real_B2]
+                                                + ([self.real_A] if idt else [])))
+        self.rec_A, self.rec_A2, self.fake_A, self.fake_A2 = (yb[k * B:(k + 1) * B] for k in range(4))
+        yc = self.netG_A.forward_nhwc(torch.cat([self.fake_A, self.fake_A2] + ([self.real_B] if idt else [])))
+        self.rec_B, self.rec_B2 = yc[:B], yc[B:2 * B]
+        self._idt_pre = (yc[2 * B:], yb[4 * B:]) if idt else None
+        firsts = [self.real_A, self.real_A2, self.fake_B2, self.rec_A2, self.real_B, self.real_B2, self.fake_A2,
+                  self.rec_B2]
+        seconds = [self.real_A2, self.real_A, self.fake_B, self.rec_A, self.real_B2, self.real_B, self.fake_A,
+                   self.rec_B]
+        fl = self.computeRAFT(torch.cat([t.detach() for t in firsts]), torch.cat([t.detach() for t in seconds]))
+        (self.ff_real_A, self.bf_real_A, self.bf_fake_B, self.bf_rec_A,
+         self.ff_real_B, self.bf_real_B, self.bf_fake_A, self.bf_rec_B) = (fl[k * B:(k + 1) * B] for k in range(8))
+        self.bf_M_A = self.netM_A.forward_nhwc(self.bf_real_A)
+        self.warp_B = warp_nhwc(self.fake_B, ops.nhwc_to_nchw(self.bf_M_A.detach(), 2))
+        self.mask_A = ops.fbcheck(ops.nhwc_to_nchw(self.ff_real_A, 2), ops.nhwc_to_nchw(self.bf_real_A, 2))
+        self.bf_M_B = self.netM_B.forward_nhwc(self.bf_real_B)
+        self.warp_A = warp_nhwc(self.fake_A, ops.nhwc_to_nchw(self.bf_M_B.detach(), 2))
+        self.mask_B = ops.fbcheck(ops.nhwc_to_nchw(self.ff_real_B, 2), ops.nhwc_to_nchw(self.bf_real_B, 2))
+
     def forward(self):
         """:198-203 (used by test)."""
         self.fake_B = self.netG_A.forward_nhwc(self.real_A)
@@ -182,9 +214,14 @@ class CycleGANModel(BaseModel):
 
     # ---------------------------------------------------------------------------- backward
     def backward_D_basic(self, netD, real, fake):
-        pred_real = netD.forward_nhwc(real)
+        if BATCH_PASSES and real.shape == fake.shape:
+            B = real.shape[0]
+            pred = netD.forward_nhwc(torch.cat([real, fake.detach()]))
+            pred_real, pred_fake = pred[:B], pred[B:]
+        else:
+            pred_real = netD.forward_nhwc(real)
+            pred_fake = netD.forward_nhwc(fake.detach())
         loss_D_real = self.criterionGAN(pred_real, True, nhwc=True)
-        pred_fake = netD.forward_nhwc(fake.detach())
         loss_D_fake = self.criterionGAN(pred_fake, False, nhwc=True)
         loss_D = (loss_D_real + loss_D_fake) * 0.5
         loss_D.backward()
@@ -201,9 +238,11 @@ class CycleGANModel(BaseModel):
         lambda_idt, lambda_A, lambda_B = self.opt.lambda_identity, self.opt.lambda_A, self.opt.lambda_B
         lambda_MC, lambda_MT = self.opt.lambda_MC, self.opt.lambda_MT
         if lambda_idt > 0:
-            self.idt_A = self.netG_A.forward_nhwc(self.real_B)
+            pre = getattr(self, "_idt_pre", None)
+            self._idt_pre = None
+            self.idt_A = pre[0] if pre is not None else self.netG_A.forward_nhwc(self.real_B)
             self.loss_idt_A = networks.l1_loss(self.idt_A, self.real_B, lambda_B * lambda_idt)
-            self.idt_B = self.netG_B.forward_nhwc(self.real_A)
+            self.idt_B = pre[1] if pre is not None else self.netG_B.forward_nhwc(self.real_A)
             self.loss_idt_B = networks.l1_loss(self.idt_B, self.real_A, lambda_A * lambda_idt)
         else:
             self.loss_idt_A = 0

@@ -521,13 +521,13 @@ class StarGANSolver:
         x_real = x_real.to(self.device).float().contiguous()
         c_org = label2onehot(label_org, self.c_dim, self.device)
         c_trg = label2onehot(label_trg, self.c_dim, self.device)
-        # 2. discriminator
-        out_src, out_cls = self.D(x_real)
-        d_loss_real = -torch.mean(out_src)
-        d_loss_cls = classification_loss(out_cls, c_org, self.dataset)
+        # 2. discriminator (real and fake through D as one batch: D is per-sample)
         x_fake = self.G(x_real, c_trg)
-        out_src, _ = self.D(x_fake.detach())
-        d_loss_fake = torch.mean(out_src)
+        B = x_real.shape[0]
+        out_src, out_cls = self.D(torch.cat([x_real, x_fake.detach()]))
+        d_loss_real = -torch.mean(out_src[:B])
+        d_loss_cls = classification_loss(out_cls[:B], c_org, self.dataset)
+        d_loss_fake = torch.mean(out_src[B:])
         if alpha is None:
             alpha = torch.rand(x_real.size(0), 1, 1, 1)
         alpha = alpha.to(self.device)

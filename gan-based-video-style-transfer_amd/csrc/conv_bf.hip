@@ -202,6 +202,17 @@ __device__ __forceinline__ int remap_mtile(int bx, int nx) {
   return (bx & 7) * (nx >> 3) + (bx >> 3);
 }
 
+// XCD-aware tile order for a 1-D grid of Mt*Nt tiles.  Consecutive workgroup ids land on
+// consecutive XCDs, so XCD x (= L % 8) gets the contiguous tile range [x*T/8, (x+1)*T/8) in
+// (m-major, n-minor) order: the N-tiles that share an A row block run together on one XCD and the
+// XCD's resident working set is (CUs per XCD / Nt) M-tiles of activations, which stays in its L2.
+__device__ __forceinline__ void tile_of(int L, int Mt, int Nt, int& mt, int& nt) {
+  const int T = Mt * Nt;
+  const int t = (T & 7) ? L : (L & 7) * (T >> 3) + (L >> 3);
+  mt = t / Nt;
+  nt = t - mt * Nt;
+}
+
 // ------------------------------------------------------------------------------------------ fprop
 // y[m = (n, ho, wo)][co] = act(sum_k x_gather[m][k] * w[co][k] + bias[co]),  k = (r, s, ci);
 // requires C % 8 == 0 (a thread's 8-deep chunk stays inside one tap).  ws = pre-split weight planes
@@ -214,7 +225,9 @@ __global__ __launch_bounds__(T::NT, 2) void conv_fprop_bf_k(
   __shared__ __attribute__((aligned(16))) char smem[2 * T::STAGE];
   constexpr int A_LD = T::A_LD, B_LD = T::B_LD, RPP = T::RPP, NP = T::NP;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int m0 = remap_mtile(blockIdx.x, gridDim.x) * T::BM, n0 = blockIdx.y * T::BN;
+  int mt_, nt_;
+  tile_of(blockIdx.x, (M + T::BM - 1) / T::BM, (Cop + T::BN - 1) / T::BN, mt_, nt_);
+  const int m0 = mt_ * T::BM, n0 = nt_ * T::BN;
   const int kq = t % T::KC, rb = t / T::KC;
 
   // this thread's chunk: absolute k = kcur, tap (kr, ks), channel kc
@@ -367,7 +380,7 @@ int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* b
 #define VST_BF(BM_, BN_, WM_, WN_, BK_, NP_)                                                       \
   {                                                                                                 \
     using T = bf::Tile<BM_, BN_, WM_, WN_, BK_, NP_>;                                              \
-    hipLaunchKernelGGL(bf::conv_fprop_bf_k<T>, dim3(ceil_div(M, BM_), ceil_div(Cop, BN_)),           \
+    hipLaunchKernelGGL(bf::conv_fprop_bf_k<T>, dim3(ceil_div(M, BM_) * ceil_div(Cop, BN_)),           \
                        dim3(T::NT), 0, s, x, ws, wps, bias, y, H, W, C, Ho, Wo, Cop, S,             \
                        st, padh, padw, reflect, act, slope, M, K);                                  \
   }

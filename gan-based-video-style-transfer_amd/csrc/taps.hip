@@ -190,6 +190,59 @@ __global__ void interleave_phases_k(const float4* __restrict__ p00, const float4
   y[idx] = src[((n * Hp + i + a) * (long)Wp + j + b) * C4 + c4];
 }
 
+// Row-segment form of tapgather: a 64-lane block owns output pixels [w0, w0+64) of row qh; for each
+// filter row r and each source row ph mapping onto qh, it stages Z[ph][w0-2pad .. w0+64+2pad) taps
+// (r, 0..S-1) in LDS and each lane adds its direct column preimages pw = qw - s + pad from LDS; the
+// reflected column preimages (lanes within pad of a border) are read from global memory.
+template <int S>
+__global__ __launch_bounds__(64) void tapgather_row_k(const float4* __restrict__ z, float4* __restrict__ y, int H,
+                                                      int W, int R, int pad, int reflect) {
+  constexpr int SEG = 64;
+  __shared__ float4 lds[(SEG + 2 * (S - 1)) * S];
+  const int nsrc = SEG + 4 * pad;
+  const int lane = threadIdx.x;
+  const int segs = (W + SEG - 1) / SEG;
+  const long row = blockIdx.x / segs;
+  const int w0 = (blockIdx.x % segs) * SEG;
+  const int qh = row % H;
+  const long n = row / H;
+  const int zcs4 = R * S;
+  const int qw = w0 + lane;
+  const int base = w0 - 2 * pad;  // source column held at lds slot 0
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int r = 0; r < R; ++r) {
+    int ph[3];
+    const int mh = preimages(qh, r, pad, H, reflect, ph);  // uniform over the block
+    for (int a = 0; a < mh; ++a) {
+      const float4* zr = z + (n * H + ph[a]) * (long)W * zcs4 + r * S;
+      __syncthreads();
+      for (int e = lane; e < nsrc * S; e += SEG) {
+        const int j = e / S, s = e - j * S;
+        const int pw = base + j;
+        lds[e] = (pw >= 0 && pw < W) ? zr[(long)pw * zcs4 + s] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      __syncthreads();
+      if (qw < W) {
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+          int pw[3];
+          const int mw = preimages(qw, s, pad, W, reflect, pw);
+          for (int b = 0; b < mw; ++b) {
+            const int j = pw[b] - base;
+            const float4 v = (pw[b] == qw - s + pad && j >= 0 && j < nsrc) ? lds[j * S + s]
+                                                                          : zr[(long)pw[b] * zcs4 + s];
+            acc.x += v.x;
+            acc.y += v.y;
+            acc.z += v.z;
+            acc.w += v.w;
+          }
+        }
+      }
+    }
+  }
+  if (qw < W) y[row * W + qw] = acc;
+}
+
 // dw[co][ci][rs] (+)= t[(rs*4 + co)][ci], co < Co
 __global__ void tap_wgrad_scatter_k(const float* __restrict__ t, float* __restrict__ dw, int Co, int Ci, int RS,
                                     int accumulate, long total) {
@@ -258,9 +311,18 @@ extern "C" int vst_tapgather(const float* z, float* y, int N, int H, int W, int 
   VST_REQUIRE(pad_mode == VST_PAD_ZERO || (pad < H && pad < W), "tapgather: reflect pad >= size");
   VST_REQUIRE(2 * pad == R - 1 && 2 * pad == S - 1, "tapgather: 'same' convolutions only (2*pad == k-1)");
   const long P = (long)N * H * W;
-  hipLaunchKernelGGL(tapgather_k, dim3(ceil_div(P, 256)), dim3(256), 0, (hipStream_t)stream,
-                     reinterpret_cast<const float4*>(z), reinterpret_cast<float4*>(y), H, W, R, S, pad,
-                     pad_mode == VST_PAD_REFLECT, P);
+  const int refl = pad_mode == VST_PAD_REFLECT;
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 rows((unsigned)((long)N * H * ceil_div(W, 64)));
+  const float4* zz = reinterpret_cast<const float4*>(z);
+  float4* yy = reinterpret_cast<float4*>(y);
+  switch (S) {
+    case 3: hipLaunchKernelGGL(tapgather_row_k<3>, rows, dim3(64), 0, st, zz, yy, H, W, R, pad, refl); break;
+    case 5: hipLaunchKernelGGL(tapgather_row_k<5>, rows, dim3(64), 0, st, zz, yy, H, W, R, pad, refl); break;
+    case 7: hipLaunchKernelGGL(tapgather_row_k<7>, rows, dim3(64), 0, st, zz, yy, H, W, R, pad, refl); break;
+    default:
+      hipLaunchKernelGGL(tapgather_k, dim3(ceil_div(P, 256)), dim3(256), 0, st, zz, yy, H, W, R, S, pad, refl, P);
+  }
   return check_launch("tapgather");
 }
 

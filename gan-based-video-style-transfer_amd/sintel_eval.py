@@ -9,9 +9,10 @@ utils/sintel_eval.py:104-130 twin):
   evaluate_video(...)   the per-video loop of evaluate_sintel (TCL-ST at i > 0, TCL-LT at i >= 5,
                         DT = generator time per frame in ms), over in-memory frames.
 
-The flow estimator is a callable ``flow_model(a, b) -> [B, 2, H, W]`` (the reference's
-computeRAFT(net, a, b)): pretrained RAFT weights are not available offline, so the harness takes
-any flow source.  The TCL reduction itself is one fused kernel (vst_loss_temporal with lambda = 1:
+The flow estimator is a callable ``flow_model(a, b) -> [B, 2, H, W]``: the reference's
+``computeRAFT(raft, a, b)`` is provided here on the HIP RAFT (``initRaftModel`` / ``computeRAFT``;
+pretrained raft-chairs weights are not shipped, so they load only if a checkpoint is given), and any
+other flow source plugs in the same way.  The TCL reduction itself is one fused kernel (vst_loss_temporal with lambda = 1:
 warp + mask + squared error + fixed-order mean), the mask one vst_fbcheck launch.
 """
 import json
@@ -33,6 +34,31 @@ def tcl_from_flows(x_fake, prev_fake, ff, bf):
     bf = bf.float().contiguous()
     mask = ops.fbcheck(ff.float().contiguous(), bf)
     return torch.sqrt(ops.loss_temporal(a, b, bf, mask, 1.0, cl=x_fake.shape[1]))
+
+
+def initRaftModel(opt=None, device="cuda", weights=None):
+    """CycleGAN/sintel_eval.py:44-52: the full RAFT in eval mode.  ``weights``: a RAFT checkpoint
+    (the reference loads raft/models/raft-chairs.pth, saved from nn.DataParallel — the "module."
+    prefix is stripped), loaded with weights_only=True; without it the model keeps its random init
+    (pretrained weights are not shipped with the reference)."""
+    import argparse
+    from .raft import RAFT
+    args = opt if opt is not None else argparse.Namespace(small=False, mixed_precision=False, alternate_corr=False)
+    model = RAFT(args)
+    if weights is not None:
+        sd = torch.load(weights, map_location="cpu", weights_only=True)
+        model.load_state_dict({(k[7:] if k.startswith("module.") else k): v for k, v in sd.items()})
+    return model.to(device).eval()
+
+
+def computeRAFT(net, img1, img2, it=20, crop_rows=True):
+    """CycleGAN/sintel_eval.py:54-60: InputPadder('sintel') + test-mode RAFT; returns flow_up cut to
+    the first H rows (the reference's ``flow_up[:, :, :H, :]``, which keeps the top padding rows —
+    SURVEY App. A; crop_rows=False returns the padded flow as utils/sintel_eval.py:62 does)."""
+    from .raft import compute_raft
+    H = img1.shape[2]
+    flow_up = compute_raft(net, img1, img2, it=it)
+    return flow_up[:, :, :H, :].contiguous() if crop_rows else flow_up
 
 
 def computeTCL(net, flow_model, img_fake, img1, img2):

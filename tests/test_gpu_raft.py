@@ -148,3 +148,41 @@ def test_raft_graph_replay_matches_eager(gb):
         got = raft.compute_raft(m, x[0], x[1], it=5)
         m.use_graphs = False
         assert torch.equal(got, raft.compute_raft(m, x[0], x[1], it=5))
+
+
+def test_sintel_harness_with_raft_flows(gb):
+    """utils/sintel_eval.py harness on the HIP RAFT: computeRAFT (InputPadder + the reference's
+    flow_up[:, :, :H, :] cut) and computeTCL on a non-divisible frame size, vs the CPU oracle."""
+    from gbvst import networks, raft, sintel_eval
+    from oracle import cpu_ref
+    m, sd = _model(1700)
+    m.use_graphs = True
+    H, W = 132, 160  # H % 8 != 0 (padded rows), H % 4 == 0 (shape-preserving G), W % 8 == 0 as on Sintel
+    img1 = torch.from_numpy(prng.uniform_f32(1701, (1, 3, H, W), -1.0, 1.0))
+    img2 = torch.from_numpy(np.clip(np.roll(img1.numpy(), (1, 2), axis=(2, 3)), -1, 1))
+    with torch.no_grad():
+        pads = raft_ref.input_pads(img1.shape)
+        _, up_r = raft_ref.raft_forward(sd, raft_ref.pad_replicate(img1, pads), raft_ref.pad_replicate(img2, pads),
+                                        iters=6, test_mode=True)
+        flow = sintel_eval.computeRAFT(m, img1.to(DEV), img2.to(DEV), it=6)
+    assert flow.shape == (1, 2, H, W)
+    assert _rel(flow, up_r[:, :, :H, :]) < 1e-3
+    G = networks.define_G(3, 3, 8, "resnet_9blocks", "instance", False, "normal", 0.02, [0])
+    Gr = cpu_ref.RefResnetGenerator(3, 3, 8, 9)
+    sdg = prng.init_state_dict(cpu_ref.state_shapes(Gr), base_seed=1702)
+    cpu_ref.load_np_state(Gr, sdg)
+    G.load_state_dict({k: torch.from_numpy(v) for k, v in sdg.items()})
+
+    class _Net:
+        def forward_eval(self, x):
+            return G(x)
+
+    fake = torch.from_numpy(prng.uniform_f32(1703, (1, 3, H, W), -1.0, 1.0))
+    flow_fn = lambda a, b: sintel_eval.computeRAFT(m, a, b, it=6)  # noqa: E731
+    tcl = float(sintel_eval.computeTCL(_Net(), flow_fn, fake.to(DEV), img1.to(DEV), img2.to(DEV)))
+    with torch.no_grad():
+        ff = raft_ref.raft_forward(sd, raft_ref.pad_replicate(img2, pads), raft_ref.pad_replicate(img1, pads), iters=6,
+                                   test_mode=True)[1][:, :, :H, :]
+        bf = up_r[:, :, :H, :]
+        tcl_ref = float(cpu_ref.tcl(fake, Gr(img2), bf, cpu_ref.fbc_check(ff, bf)))
+    assert abs(tcl - tcl_ref) <= 1e-3 * abs(tcl_ref) + 1e-6, (tcl, tcl_ref)

@@ -19,6 +19,10 @@
 // double-buffered LDS stage with one barrier per 32-deep K-step.
 #include "common.h"
 
+#ifndef WGRAD_XCD
+#define WGRAD_XCD 1
+#endif
+
 namespace vst {
 namespace rk {
 
@@ -523,8 +527,27 @@ __global__ __launch_bounds__((Tile<BM, BN, WM, WN, BK, MATH>::NT), 2) void conv_
   typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
   __shared__ __attribute__((aligned(16))) float smem[2 * T::STAGE];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+#if WGRAD_XCD
+  // 1-D grid, XCD-aware: consecutive workgroup ids go to consecutive XCDs, so XCD x takes the
+  // contiguous range [x*T/8, (x+1)*T/8) of (split-major, then n, then m) tiles — every tile of a
+  // split-K chunk runs on one XCD and its x / dy chunk rows stay in that XCD's L2 (the 3-D grid
+  // spread each chunk over all eight L2s: ~11x the algorithmic HBM reads).
+  const int Mt = (Mw + BM - 1) / BM, Nt = (Cyp + BN - 1) / BN, Zt = (P + chunk - 1) / chunk;
+  int mx, ny, zz;
+  {
+    const int L = blockIdx.x, Tt = Mt * Nt * Zt;
+    const int tt = (Tt & 7) ? L : (L & 7) * (Tt >> 3) + (L >> 3);
+    zz = tt / (Mt * Nt);
+    const int rem = tt - zz * Mt * Nt;
+    ny = rem / Mt;
+    mx = rem - ny * Mt;
+  }
+  const int m0 = mx * BM, n0 = ny * BN;
+  const int pbeg = zz * chunk;
+#else
   const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
   const int pbeg = blockIdx.z * chunk;
+#endif
   const int pend = min(P, pbeg + chunk);
   const int kq = t % T::KQ, rb = t / T::KQ;
   const long HW = (long)H * W;
@@ -614,7 +637,11 @@ __global__ __launch_bounds__((Tile<BM, BN, WM, WN, BK, MATH>::NT), 2) void conv_
   main_loop<T, A_LD + B_LD>(smem, nk, acc, load_one, adv, store);
 
   const int wm0 = (wave / T::WAVES_N) * WM, wn0 = (wave % T::WAVES_N) * WN;
+#if WGRAD_XCD
+  float* sl = slab + (long)zz * Mw * Cyp;
+#else
   float* sl = slab + (long)blockIdx.z * Mw * Cyp;
+#endif
 #pragma unroll
   for (int i = 0; i < T::MI; ++i)
 #pragma unroll
@@ -756,6 +783,12 @@ void rk_tconv_launch(const float* in, const float* wp, const float* bias, const 
 #undef VST_LST
 }
 
+#if WGRAD_XCD
+#define WGRAD_GRID(mt, nt, z) dim3((mt) * (nt) * (z))
+#else
+#define WGRAD_GRID(mt, nt, z) dim3((mt), (nt), (z))
+#endif
+
 void rk_wgrad_launch(const float* xt, const float* dyt, float* slab, int N, int H, int W, int Cx,
                      int Ho, int Wo, int Cyp, int S, int pad, int reflect, int Mw, int chunk,
                      int nsplit, int kind, int math, hipStream_t s) {
@@ -763,7 +796,7 @@ void rk_wgrad_launch(const float* xt, const float* dyt, float* slab, int N, int 
   const int kd = math_kind(math, kind);
 #define VST_LX(BM_, BN_, WM_, WN_, BK_, M_)                                                        \
   hipLaunchKernelGGL((rk::conv_wgrad_rk_k<BM_, BN_, WM_, WN_, BK_, M_>),                             \
-                     dim3(ceil_div(Mw, BM_), ceil_div(Cyp, BN_), nsplit),                            \
+                     WGRAD_GRID(ceil_div(Mw, BM_), ceil_div(Cyp, BN_), nsplit),                       \
                      dim3(rk::Tile<BM_, BN_, WM_, WN_, BK_>::NT), 0, s, xt, dyt, slab, H, W, Cx, Ho, \
                      Wo, Cyp, S, pad, reflect, Mw, P, chunk, rk_cp_ld((long)N * H * W), rk_cp_ld(P));
 #define VST_LM(M_) VST_RK_DISPATCH_M(kd, VST_LX, M_)

@@ -448,8 +448,19 @@ __global__ __launch_bounds__((Tile<BM, BN, WM, WN>::NT), 2) void conv_wgrad_k(
   __shared__ __attribute__((aligned(16))) float smem[2 * T::STAGE];
 
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
-  const int pbeg = blockIdx.z * chunk;
+  // 1-D XCD-aware grid (as conv_rk.hip's wgrad): the tiles of one pixel chunk share an XCD's L2
+  const int Mt = (Mw + BM - 1) / BM, Nt = (Cyp + BN - 1) / BN, Zt = (P + chunk - 1) / chunk;
+  int zz, mx, ny;
+  {
+    const int L = blockIdx.x, Tt = Mt * Nt * Zt;
+    const int tt = (Tt & 7) ? L : (L & 7) * (Tt >> 3) + (L >> 3);
+    zz = tt / (Mt * Nt);
+    const int rem = tt - zz * Mt * Nt;
+    ny = rem / Mt;
+    mx = rem - ny * Mt;
+  }
+  const int m0 = mx * BM, n0 = ny * BN;
+  const int pbeg = zz * chunk;
   const int pend = min(P, pbeg + chunk);
 
   const int am4 = t % BM4, akb = t / BM4;
@@ -528,7 +539,7 @@ __global__ __launch_bounds__((Tile<BM, BN, WM, WN>::NT), 2) void conv_wgrad_k(
   main_loop<BM, BN, WM, WN, A_LD + B_LD>(smem, nk, pbeg, acc, load_one, adv, store);
 
   const int wm0 = (wave / T::WAVES_N) * WM, wn0 = (wave % T::WAVES_N) * WN;
-  float* sl = slab + (long)blockIdx.z * Mw * Cyp;
+  float* sl = slab + (long)zz * Mw * Cyp;
 #pragma unroll
   for (int i = 0; i < T::MI; ++i)
 #pragma unroll
@@ -823,7 +834,7 @@ extern "C" int vst_conv2d_wgrad(const float* x, const float* dy, float* dw, floa
   const int refl = pad_mode == VST_PAD_REFLECT;
 #define VST_WG(BM_, BN_, WM_, WN_)                                                                 \
   hipLaunchKernelGGL((conv_wgrad_k<BM_, BN_, WM_, WN_>),                                            \
-                     dim3(ceil_div(p.Mw, BM_), ceil_div(Cyp, BN_), p.nsplit),                        \
+                     dim3(ceil_div(p.Mw, BM_) * ceil_div(Cyp, BN_) * p.nsplit),                      \
                      dim3(Tile<BM_, BN_, WM_, WN_>::NT), 0, s, x, dy, ws, H, W, Cx, Ho, Wo, Cyp, S,  \
                      stride, pad, refl, p.Mw, P, p.chunk)
   if (p.trans) {

@@ -649,7 +649,8 @@ struct WgradPlan {
   int Mw, nsplit, chunk;
   TileKind tile;
   bool trans;        // channel-major operand copies + conv_wgrad_rk_k (stride 1, Wo % 4 == 0)
-  long xt_floats;    // workspace floats after the slabs: xt [Cx][N*H*W] then dyt [Cyp][P]
+  int pad;           // trans: the border the padded x copy carries (derived from H -> Ho)
+  long xt_floats;    // workspace floats after the slabs: xt [Cx][N*Hp*Wp] then dyt [Cyp][P]
   long dyt_floats;
 };
 
@@ -680,11 +681,15 @@ static WgradPlan plan_wgrad(int N, int H, int W, int Ho, int Wo, int Cx, int Cyp
   WgradPlan p;
   p.Mw = R * S * Cx;
   p.trans = false;
+  p.pad = 0;
   p.xt_floats = p.dyt_floats = 0;
   const int P = N * Ho * Wo;
   const int ov = g_tile_override[2];
-  if (Cyp > 4 && stride == 1 && Wo % 4 == 0 && ov < 8) {
+  const int pd2 = Ho - H + R - 1;  // stride 1: 2 * pad
+  if (Cyp > 4 && stride == 1 && Wo % 4 == 0 && ov < 8 && pd2 >= 0 && pd2 % 2 == 0 &&
+      Wo - W + S - 1 == pd2) {
     p.trans = true;
+    p.pad = pd2 / 2;
     int kind = (ov >= 0 && ov <= 6) ? ov : (Cyp <= 64 ? (p.Mw >= 1024 ? 2 : 3) : (p.Mw >= 1024 ? 0 : 1));
     p.tile = (TileKind)kind;
     int bm, bn, bk, slots;
@@ -694,7 +699,7 @@ static WgradPlan plan_wgrad(int N, int H, int W, int Ho, int Wo, int Cx, int Cyp
                                ceil_div(P, WGRAD_CHUNK_MAX));
     p.chunk = ceil_div(ceil_div(P, ns), bk) * bk;
     p.nsplit = ceil_div(P, p.chunk);
-    p.xt_floats = rk_cp_ld((long)N * H * W) * Cx;
+    p.xt_floats = rk_cp_ld((long)N * (H + 2 * p.pad) * (W + 2 * p.pad)) * Cx;  // padded image
     p.dyt_floats = rk_cp_ld(P) * Cyp;
     return p;
   }
@@ -838,10 +843,12 @@ extern "C" int vst_conv2d_wgrad(const float* x, const float* dy, float* dw, floa
                      dim3(Tile<BM_, BN_, WM_, WN_>::NT), 0, s, x, dy, ws, H, W, Cx, Ho, Wo, Cyp, S,  \
                      stride, pad, refl, p.Mw, P, p.chunk)
   if (p.trans) {
+    VST_REQUIRE(pad == p.pad, "conv2d_wgrad: pad %d inconsistent with H %d -> Ho %d", pad, H, Ho);
     float* xt = ws + (size_t)p.nsplit * p.Mw * Cyp;
     float* dyt = xt + p.xt_floats;
-    rk_nhwc_to_cp(x, xt, (long)N * H * W, Cx, s);
-    rk_nhwc_to_cp(dy, dyt, P, Cyp, s);
+    const int pack = math == VST_MATH_BF16X3;  // the x3 kernel stages pre-split (hi, lo) words
+    rk_nhwc_to_cp_pad(x, xt, N, H, W, Cx, pad, refl, pack, s);
+    rk_nhwc_to_cp(dy, dyt, P, Cyp, pack, s);
     rk_wgrad_launch(xt, dyt, ws, N, H, W, Cx, Ho, Wo, Cyp, S, pad, refl, p.Mw, p.chunk, p.nsplit,
                     (int)p.tile, math, s);
   } else if (Cyp == 4) {

@@ -511,12 +511,13 @@ __global__ __launch_bounds__((Tile<BM, BN, WM, WN, BK, MATH>::NT), 2) void conv_
 
 // ------------------------------------------------------------------ weight gradient, stride 1
 // dW[m = (r, s, ci)][co] = sum_p X[shift_rs(p)][ci] * dY[p][co] with both operands read from
-// channel-major copies (xt = [Cx][N][H][W], dyt = [Cyp][N*Ho*Wo], made by nhwc_to_cp_k), so every
-// GEMM row is contiguous along the reduction (pixel) axis and stages into the row-major [row][k]
-// LDS image with ds_write_b128 exactly like the forward kernel.  For stride 1 the 4 pixels of a
-// float4 are 4 consecutive input columns: one (unaligned) 16-byte load unless the window crosses
-// the image border, where the 4 taps are reflected / zeroed one by one.  blockIdx.z = K split;
-// partial tiles land in slab[z][m][Cyp] (summed and transposed into dw by conv.hip).
+// channel-major copies (xt = [Cx][N][Hp][Wp], the input with its reflect / zero border already
+// applied, made by nhwc_to_cp_pad_k; dyt = [Cyp][N*Ho*Wo], made by nhwc_to_cp_k), so every GEMM
+// row is contiguous along the reduction (pixel) axis and stages into the row-major [row][k] LDS
+// image with ds_write_b128 exactly like the forward kernel.  For stride 1 the 4 pixels of a
+// float4 are 4 consecutive padded columns: one (unaligned) 16-byte load, no border branches.
+// The split-K chunk index comes from the XCD-aware 1-D grid; partial tiles land in
+// slab[z][m][Cyp] (summed and transposed into dw by conv.hip).
 template <int BM, int BN, int WM, int WN, int BK, int MATH>
 __global__ __launch_bounds__((Tile<BM, BN, WM, WN, BK, MATH>::NT), 2) void conv_wgrad_rk_k(
     const float* __restrict__ xt, const float* __restrict__ dyt, float* __restrict__ slab, int H,
@@ -524,6 +525,7 @@ __global__ __launch_bounds__((Tile<BM, BN, WM, WN, BK, MATH>::NT), 2) void conv_
     long ldx, long ldy) {
   using T = Tile<BM, BN, WM, WN, BK, MATH>;
   constexpr int A_LD = T::A_LD, B_LD = T::B_LD, RP = T::ROWS_PER_PASS;
+  constexpr bool PACKED = MATH == VST_MATH_BF16X3;  // xt / dyt hold (hi << 16 | lo) bf16 words
   typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
   __shared__ __attribute__((aligned(16))) float smem[2 * T::STAGE];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -552,7 +554,10 @@ __global__ __launch_bounds__((Tile<BM, BN, WM, WN, BK, MATH>::NT), 2) void conv_
   const int kq = t % T::KQ, rb = t / T::KQ;
   const long HW = (long)H * W;
 
-  int ar[A_LD], as[A_LD];
+  // A rows: tap (r, s) of input channel ci over the PADDED channel-major image xt =
+  // [Cx][N][Hp][Wp] (nhwc_to_cp_pad_k applied the reflect / zero border), so the 4 pixels of a
+  // float4 are 4 consecutive padded columns of one row — always in bounds, one 16-byte load.
+  const int Hp = H + 2 * pad, Wp = W + 2 * pad;
   const float* xrow[A_LD];
   bool mv[A_LD];
 #pragma unroll
@@ -561,10 +566,8 @@ __global__ __launch_bounds__((Tile<BM, BN, WM, WN, BK, MATH>::NT), 2) void conv_
     mv[j] = m < Mw;
     const int mm = mv[j] ? m : 0;
     const int tap = mm / Cx, ci = mm - tap * Cx;
-    const int r = tap / S, s = tap - r * S;
-    ar[j] = r - pad;
-    as[j] = s - pad;
-    xrow[j] = xt + (long)ci * ldx;
+    const int r = tap / S, s_ = tap - r * S;
+    xrow[j] = xt + (long)ci * ldx + r * Wp + s_;
   }
   const float* dyrow[B_LD];
   bool nv[B_LD];
@@ -574,62 +577,73 @@ __global__ __launch_bounds__((Tile<BM, BN, WM, WN, BK, MATH>::NT), 2) void conv_
     nv[j] = n < Cyp;
     dyrow[j] = dyt + (long)(nv[j] ? n : 0) * ldy;
   }
-  // pixel state of this thread's float4 (shared by all its rows)
-  int kp = pbeg + 4 * kq, pn, pho, pwo;
+  // pixel state of this thread's float4 (shared by all its rows): output pixel kp = (pn, pho, pwo)
+  // and its padded-image offset poff = (pn * Hp + pho) * Wp + pwo
+  int kp = pbeg + 4 * kq, pho, pwo;
+  long poff;
   {
     const int hw = Ho * Wo;
-    pn = kp / hw;
+    const int pn = kp / hw;
     const int rem = kp - pn * hw;
     pho = rem / Wo;
     pwo = rem - pho * Wo;
+    poff = ((long)pn * Hp + pho) * Wp + pwo;
   }
   float4 ra[A_LD], rbv[B_LD];
   auto load_one = [&](int i, int) {
+    const bool live = kp < pend;
     if (i < A_LD) {
       const int j = i;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (mv[j] && kp < pend) {
-        int hi = pho + ar[j];
-        const int wi = pwo + as[j];
-        bool hok = true;
-        if (reflect) hi = reflect_idx(hi, H);
-        else hok = (unsigned)hi < (unsigned)H;
-        if (hok) {
-          const float* rowp = xrow[j] + pn * HW + (long)hi * W;
-          if (wi >= 0 && wi + 3 < W) {
-            const f4u u = *reinterpret_cast<const f4u*>(rowp + wi);
-            v = make_float4(u.x, u.y, u.z, u.w);
-          } else {
-            float e[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              int wq = wi + q;
-              bool ok = true;
-              if (reflect) wq = reflect_idx(wq, W);
-              else ok = (unsigned)wq < (unsigned)W;
-              e[q] = ok ? rowp[wq] : 0.f;
-            }
-            v = make_float4(e[0], e[1], e[2], e[3]);
-          }
-        }
+      if (mv[j] && live) {
+        const f4u u = *reinterpret_cast<const f4u*>(xrow[j] + poff);
+        v = make_float4(u.x, u.y, u.z, u.w);
       }
       ra[j] = v;
     } else {
       const int j = i - A_LD;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (nv[j] && kp < pend) v = *reinterpret_cast<const float4*>(dyrow[j] + kp);
+      if (nv[j] && live) v = *reinterpret_cast<const float4*>(dyrow[j] + kp);
       rbv[j] = v;
     }
   };
   auto adv = [&]() {
     kp += BK;
     pwo += BK;
+    poff += BK;
     while (pwo >= Wo) {
       pwo -= Wo;
-      if (++pho == Ho) { pho = 0; ++pn; }
+      poff += Wp - Wo;
+      if (++pho == Ho) { pho = 0; poff += (long)(Hp - Ho) * Wp; }
     }
   };
-  auto store = [&](float* As) { store_stage<T, A_LD, B_LD>(As, ra, rbv, rb, kq); };
+  // bf16x3: the channel-major copies already hold each value as a (hi, lo) bf16 word pair
+  // (nhwc_to_cp_k<true>), so a staged float4 is four packed words and the stage image takes
+  // one byte permute per plane pair instead of the convert / subtract / convert split.
+  auto store = [&](float* As) {
+    if constexpr (PACKED) {
+      constexpr int LDH = T::LDH;
+      __bf16* ah = reinterpret_cast<__bf16*>(As);
+      __bf16* bh = reinterpret_cast<__bf16*>(As + T::A_ELEMS);
+      auto put = [&](__bf16* base, int plane, const float4& v, int o) {
+        const uint32_t x0 = __float_as_uint(v.x), x1 = __float_as_uint(v.y);
+        const uint32_t x2 = __float_as_uint(v.z), x3 = __float_as_uint(v.w);
+        uint2 h, l;
+        h.x = __builtin_amdgcn_perm(x1, x0, 0x07060302u);
+        h.y = __builtin_amdgcn_perm(x3, x2, 0x07060302u);
+        l.x = __builtin_amdgcn_perm(x1, x0, 0x05040100u);
+        l.y = __builtin_amdgcn_perm(x3, x2, 0x05040100u);
+        *reinterpret_cast<uint2*>(base + o) = h;
+        *reinterpret_cast<uint2*>(base + plane + o) = l;
+      };
+#pragma unroll
+      for (int j = 0; j < A_LD; ++j) put(ah, BM * LDH, ra[j], (rb + RP * j) * LDH + 4 * kq);
+#pragma unroll
+      for (int j = 0; j < B_LD; ++j) put(bh, BN * LDH, rbv[j], (rb + RP * j) * LDH + 4 * kq);
+    } else {
+      store_stage<T, A_LD, B_LD>(As, ra, rbv, rb, kq);
+    }
+  };
 
   f32x16 acc[T::MI][T::NI];
   zero_acc(acc);
@@ -656,7 +670,17 @@ __global__ __launch_bounds__((Tile<BM, BN, WM, WN, BK, MATH>::NT), 2) void conv_
     }
 }
 
-// NHWC [P][Cs] -> channel-major [Cs][ld] through a 64x64 LDS tile (float4 reads and writes).
+// One fp32 value as its bf16x3 operand pair in one word: hi = bf16(v) in the high half,
+// lo = bf16(v - hi) in the low half (the same RNE conversions as split4<2>).
+__device__ __forceinline__ float split_word(float v) {
+  const uint32_t h = pack_bf16x2(v, 0.f) & 0xffffu;
+  const uint32_t l = pack_bf16x2(v - __uint_as_float(h << 16), 0.f) & 0xffffu;
+  return __uint_as_float((h << 16) | l);
+}
+
+// NHWC [P][Cs] -> channel-major [Cs][ld] through a 64x64 LDS tile (float4 reads and writes);
+// PACK stores every value as its split_word (the bf16x3 weight gradient's operand image).
+template <bool PACK>
 __global__ __launch_bounds__(256) void nhwc_to_cp_k(const float* __restrict__ x, float* __restrict__ y,
                                                     long P, int Cs, long ld) {
   __shared__ float tile[64][65];
@@ -668,6 +692,7 @@ __global__ __launch_bounds__(256) void nhwc_to_cp_k(const float* __restrict__ x,
     const int idx = t + 256 * it, pr = idx >> 4, c4 = (idx & 15) * 4;
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     if (p0 + pr < P && c0 + c4 < Cs) v = *reinterpret_cast<const float4*>(x + (p0 + pr) * Cs + c0 + c4);
+    if (PACK) v = make_float4(split_word(v.x), split_word(v.y), split_word(v.z), split_word(v.w));
     tile[pr][c4] = v.x;
     tile[pr][c4 + 1] = v.y;
     tile[pr][c4 + 2] = v.z;
@@ -688,15 +713,79 @@ __global__ __launch_bounds__(256) void nhwc_to_cp_k(const float* __restrict__ x,
   }
 }
 
+// NHWC [N][H][W][Cs] -> padded channel-major [Cs][N][H+2p][W+2p] (reflect or zero border), the
+// weight gradient's A-operand image; same 64x64 LDS tile walk as nhwc_to_cp_k over padded pixels.
+template <bool PACK>
+__global__ __launch_bounds__(256) void nhwc_to_cp_pad_k(const float* __restrict__ x, float* __restrict__ y,
+                                                        int N, int H, int W, int Cs, int pad, int reflect,
+                                                        long ld) {
+  __shared__ float tile[64][65];
+  const int Hp = H + 2 * pad, Wp = W + 2 * pad;
+  const long P = (long)N * Hp * Wp;
+  const long p0 = (long)blockIdx.x * 64;
+  const int c0 = blockIdx.y * 64;
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int idx = t + 256 * it, pr = idx >> 4, c4 = (idx & 15) * 4;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    const long q = p0 + pr;
+    if (q < P && c0 + c4 < Cs) {
+      const int n = (int)(q / ((long)Hp * Wp));
+      const int rem = (int)(q - (long)n * Hp * Wp);
+      int h = rem / Wp - pad, w = rem % Wp - pad;
+      bool ok = true;
+      if (reflect) {
+        h = reflect_idx(h, H);
+        w = reflect_idx(w, W);
+      } else {
+        ok = (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+      }
+      if (ok) v = *reinterpret_cast<const float4*>(x + (((long)n * H + h) * W + w) * Cs + c0 + c4);
+    }
+    if (PACK) v = make_float4(split_word(v.x), split_word(v.y), split_word(v.z), split_word(v.w));
+    tile[pr][c4] = v.x;
+    tile[pr][c4 + 1] = v.y;
+    tile[pr][c4 + 2] = v.z;
+    tile[pr][c4 + 3] = v.w;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int idx = t + 256 * it, cr = idx >> 4, p4 = (idx & 15) * 4;
+    if (c0 + cr >= Cs || p0 + p4 >= P) continue;
+    float* dst = y + (long)(c0 + cr) * ld + p0 + p4;
+    if (p0 + p4 + 3 < P && (ld & 3) == 0) {
+      *reinterpret_cast<float4*>(dst) =
+          make_float4(tile[p4][cr], tile[p4 + 1][cr], tile[p4 + 2][cr], tile[p4 + 3][cr]);
+    } else {
+      for (int e = 0; e < 4 && p0 + p4 + e < P; ++e) dst[e] = tile[p4 + e][cr];
+    }
+  }
+}
+
 }  // namespace rk
 
 // Plane stride of a channel-major copy: a multiple of 4 floats that is NOT a multiple of a large
 // power of two (P = 65536 would put all 128 rows of a tile on one L2 channel).
 long rk_cp_ld(long P) { return (P + 63) / 64 * 64 + 64; }
 
-void rk_nhwc_to_cp(const float* x, float* y, long P, int Cs, hipStream_t s) {
-  hipLaunchKernelGGL(rk::nhwc_to_cp_k, dim3((unsigned)((P + 63) / 64), ceil_div(Cs, 64)), dim3(256), 0,
-                     s, x, y, P, Cs, rk_cp_ld(P));
+void rk_nhwc_to_cp_pad(const float* x, float* y, int N, int H, int W, int Cs, int pad, int reflect,
+                       int pack, hipStream_t s) {
+  const long P = (long)N * (H + 2 * pad) * (W + 2 * pad);
+  const dim3 g((unsigned)((P + 63) / 64), ceil_div(Cs, 64));
+  if (pack)
+    hipLaunchKernelGGL(rk::nhwc_to_cp_pad_k<true>, g, dim3(256), 0, s, x, y, N, H, W, Cs, pad, reflect,
+                       rk_cp_ld(P));
+  else
+    hipLaunchKernelGGL(rk::nhwc_to_cp_pad_k<false>, g, dim3(256), 0, s, x, y, N, H, W, Cs, pad, reflect,
+                       rk_cp_ld(P));
+}
+
+void rk_nhwc_to_cp(const float* x, float* y, long P, int Cs, int pack, hipStream_t s) {
+  const dim3 g((unsigned)((P + 63) / 64), ceil_div(Cs, 64));
+  if (pack) hipLaunchKernelGGL(rk::nhwc_to_cp_k<true>, g, dim3(256), 0, s, x, y, P, Cs, rk_cp_ld(P));
+  else hipLaunchKernelGGL(rk::nhwc_to_cp_k<false>, g, dim3(256), 0, s, x, y, P, Cs, rk_cp_ld(P));
 }
 
 // Tile kinds: 0 = 128x128 (8 waves, 64x32 each), 1 = 64x128, 2 = 128x64, 3 = 64x64 (4 waves),
@@ -798,7 +887,8 @@ void rk_wgrad_launch(const float* xt, const float* dyt, float* slab, int N, int 
   hipLaunchKernelGGL((rk::conv_wgrad_rk_k<BM_, BN_, WM_, WN_, BK_, M_>),                             \
                      WGRAD_GRID(ceil_div(Mw, BM_), ceil_div(Cyp, BN_), nsplit),                       \
                      dim3(rk::Tile<BM_, BN_, WM_, WN_, BK_>::NT), 0, s, xt, dyt, slab, H, W, Cx, Ho, \
-                     Wo, Cyp, S, pad, reflect, Mw, P, chunk, rk_cp_ld((long)N * H * W), rk_cp_ld(P));
+                     Wo, Cyp, S, pad, reflect, Mw, P, chunk,                                   \
+                     rk_cp_ld((long)N * (H + 2 * pad) * (W + 2 * pad)), rk_cp_ld(P));
 #define VST_LM(M_) VST_RK_DISPATCH_M(kd, VST_LX, M_)
   VST_MATH_SWITCH(math, VST_LM)
 #undef VST_LM

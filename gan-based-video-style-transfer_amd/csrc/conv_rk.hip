@@ -56,6 +56,19 @@ struct Tile {
   static constexpr int ROWS_PER_PASS = NT / KQ;  // KQ lanes x float4 cover one BK-deep row
   static constexpr int A_LD = BM / ROWS_PER_PASS;
   static constexpr int B_LD = BN / ROWS_PER_PASS;
+  // Staging row of thread t.  bf16 images (row stride LDH = 40 bf16 = 20 banks) with 8 lanes per
+  // row: a 32-lane half-wave writes 4 rows, and rows r, r+4, r+8, r+12 start on banks 0/16/32/48
+  // (+ const) — the 4 x 16-bank row segments tile the 64 banks without overlap, where 4
+  // consecutive rows (banks 0/20/40/60) collide.  Bijective on [0, RP); loads follow the rows.
+  static __device__ __forceinline__ int row_of(int t) {
+    const int q = t / KQ;
+    if constexpr (X3 && KQ == 8) {
+      const int h = q >> 2, e = q & 3;
+      return ((h >> 2) << 4) + (h & 3) + 4 * e;
+    } else {
+      return q;
+    }
+  }
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
   static_assert(!X3 || BK % 16 == 0, "bf16 k groups are 16 deep");
   static_assert(BM % ROWS_PER_PASS == 0 && BN % ROWS_PER_PASS == 0, "row coverage");
@@ -285,7 +298,7 @@ __global__ __launch_bounds__((Tile<BM, BN, WM, WN, BK, MATH>::NT), 2) void conv_
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int mt = remap_mtile(blockIdx.x, gridDim.x);
   const int m0 = mt * BM, n0 = blockIdx.y * BN;
-  const int kq = t % T::KQ, rb = t / T::KQ;
+  const int kq = t % T::KQ, rb = T::row_of(t);
 
   // k state (one per thread: every row this thread stages uses the same k position)
   int kc = (4 * kq) % C, ks, kr;
@@ -402,7 +415,7 @@ __global__ __launch_bounds__((Tile<BM, BN, WM, WN, BK, MATH>::NT), 2) void conv_
   const int Ktot = nr * ns * Cy;
 
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int kq = t % T::KQ, rb = t / T::KQ;
+  const int kq = t % T::KQ, rb = T::row_of(t);
   int kc = ns > 0 ? (4 * kq) % Cy : 0, kis, kir;
   {
     const int tp = Cy > 0 ? (4 * kq) / Cy : 0;
@@ -551,7 +564,7 @@ __global__ __launch_bounds__((Tile<BM, BN, WM, WN, BK, MATH>::NT), 2) void conv_
   const int pbeg = blockIdx.z * chunk;
 #endif
   const int pend = min(P, pbeg + chunk);
-  const int kq = t % T::KQ, rb = t / T::KQ;
+  const int kq = t % T::KQ, rb = T::row_of(t);
   const long HW = (long)H * W;
 
   // A rows: tap (r, s) of input channel ci over the PADDED channel-major image xt =

@@ -17,7 +17,7 @@ REPO = os.path.dirname(PKG)
 BUILD = os.path.join(PKG, "_build")
 LIB_PATH = os.path.join(BUILD, "libvst_hip.so")
 # developer A/B runs only: load an alternative build (tools/build_variant.py) instead
-LIB_PATH = os.environ.get("VST_LIB_VARIANT", LIB_PATH)
+LIB_PATH = os.environ.get("VST_LIB_VARIANT") or LIB_PATH
 CSRC = os.path.join(PKG, "csrc")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"

@@ -24,6 +24,9 @@ inline int check_launch(const char* what) {
   return VST_OK;
 }
 
+// Compute units of one MI355X (8 XCDs x 32 CUs): the unit of a launch's block rounds.
+#define VST_NUM_CUS 256
+
 #define VST_REQUIRE(cond, ...)            \
   do {                                    \
     if (!(cond)) {                        \

@@ -22,6 +22,13 @@
 
 #include "common.h"
 
+#ifndef VST_BF_X6K3
+#define VST_BF_X6K3 0
+#endif
+#ifndef VST_BF_TAIL
+#define VST_BF_TAIL 1
+#endif
+
 namespace vst {
 namespace bf {
 
@@ -221,13 +228,13 @@ template <class T>
 __global__ __launch_bounds__(T::NT, 2) void conv_fprop_bf_k(
     const float* __restrict__ x, const __bf16* __restrict__ ws, long wps, const float* __restrict__ bias,
     float* __restrict__ y, int H, int W, int C, int Ho, int Wo, int Cop, int S, int st, int padh,
-    int padw, int reflect, int act, float slope, int M, int Ktot) {
+    int padw, int reflect, int act, float slope, int M, int Ktot, int m_base) {
   __shared__ __attribute__((aligned(16))) char smem[2 * T::STAGE];
   constexpr int A_LD = T::A_LD, B_LD = T::B_LD, RPP = T::RPP, NP = T::NP;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   int mt_, nt_;
-  tile_of(blockIdx.x, (M + T::BM - 1) / T::BM, (Cop + T::BN - 1) / T::BN, mt_, nt_);
-  const int m0 = mt_ * T::BM, n0 = nt_ * T::BN;
+  tile_of(blockIdx.x, (M - m_base + T::BM - 1) / T::BM, (Cop + T::BN - 1) / T::BN, mt_, nt_);
+  const int m0 = m_base + mt_ * T::BM, n0 = nt_ * T::BN;
   const int kq = t % T::KC, rb = t / T::KC;
 
   // this thread's chunk: absolute k = kcur, tap (kr, ks), channel kc
@@ -376,18 +383,39 @@ int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* b
                     int reflect, int act, float slope, int math, int kind, hipStream_t s) {
   const int M = N * Ho * Wo, K = R * S * C;
   const __bf16* ws = reinterpret_cast<const __bf16*>(wsplit);
-  const int kd = bf_pick(M, Cop, kind);
+  int kd = bf_pick(M, Cop, kind);
+#if VST_BF_X6K3
+  // x6: the 128x128 three-plane stage pair (96 KB) fits one block per CU; 64x128 tiles fit two
+  if (kind < 0 && kd == 0 && math == VST_MATH_BF16X6) kd = 3;
+#endif
+  int m_split = 0;
+#if VST_BF_TAIL
+  // Wave quantisation: 128x128 x3 blocks run two per CU, so a grid a few tiles past a whole
+  // number of blocks per CU (the padded-frame dgrad: 546 = 2 x 256 + 34 blocks at N = 8) keeps
+  // most CUs idle for one extra block time.  Such a tail (<= 1/4 of the CUs) runs as a second
+  // launch of 64x64 tiles over the remaining pixel rows (4x as many, 4x smaller blocks).
+  if (kind < 0 && kd == 0 && math != VST_MATH_BF16X6) {
+    const long nt = (Cop + 127) / 128, blocks = (long)((M + 127) / 128) * nt;
+    const long per = blocks / VST_NUM_CUS, tail = blocks - per * VST_NUM_CUS;
+    if (per >= 1 && tail > 0 && 4 * tail <= VST_NUM_CUS && (per * VST_NUM_CUS) % nt == 0)
+      m_split = (int)(per * VST_NUM_CUS / nt) * 128;
+  }
+#endif
 #define VST_BF(BM_, BN_, WM_, WN_, BK_, NP_)                                                       \
   {                                                                                                 \
     using T = bf::Tile<BM_, BN_, WM_, WN_, BK_, NP_>;                                              \
-    hipLaunchKernelGGL(bf::conv_fprop_bf_k<T>, dim3(ceil_div(M, BM_) * ceil_div(Cop, BN_)),           \
+    hipLaunchKernelGGL(bf::conv_fprop_bf_k<T>, dim3(ceil_div(Mend - mb, BM_) * ceil_div(Cop, BN_)),   \
                        dim3(T::NT), 0, s, x, ws, wps, bias, y, H, W, C, Ho, Wo, Cop, S,             \
-                       st, padh, padw, reflect, act, slope, M, K);                                  \
+                       st, padh, padw, reflect, act, slope, Mend, K, mb);                           \
   }
-  if (math == VST_MATH_BF16X6) {
-    VST_BF_DISPATCH(kd, 3, VST_BF)
-  } else {
-    VST_BF_DISPATCH(kd, 2, VST_BF)
+  for (int part = 0; part < (m_split ? 2 : 1); ++part) {
+    const int mb = part ? m_split : 0, Mend = (m_split && !part) ? m_split : M;
+    const int kp = part ? 6 : kd;
+    if (math == VST_MATH_BF16X6) {
+      VST_BF_DISPATCH(kp, 3, VST_BF)
+    } else {
+      VST_BF_DISPATCH(kp, 2, VST_BF)
+    }
   }
 #undef VST_BF
   return check_launch("conv2d_fwd(bf16 split)");

@@ -1,5 +1,5 @@
 """Developer: launch one conv family on the ResnetBlock shape (B=4, 64x64x256, 3x3 reflect) a few
-times (batch KB_B, default 8) — the target of rocprofv3 --pmc passes.  usage: kbench.py fprop|tconv|wgrad [reps]"""
+times (batch KB_B, default 8) — the target of rocprofv3 --pmc passes.  usage: kbench.py fprop|dgrad|tconv|wgrad [reps]"""
 import os
 import sys
 
@@ -17,11 +17,14 @@ B, H, C = int(os.environ.get("KB_B", "8")), 64, 256  # 8 = the batched G_A calls
 x = torch.randn(B, H, H, C, device=dev)
 w = torch.randn(C, C, 3, 3, device=dev) * 0.02
 kc, ck = ops.weight_pack(w, ops.PACK_FWD), ops.weight_pack(w, ops.PACK_DGRAD)
+ikf = ops.weight_pack(w, ops.PACK_IKF)
 gy = torch.randn(B, H, H, C, device=dev)
 dw = torch.zeros(C, C, 3, 3, device=dev)
 for _ in range(reps):
     if which == "fprop":
         ops.conv2d_fwd(x, kc, None, C, 3, 3, 1, 1, "reflect")
+    elif which == "dgrad":  # stride-1 data gradient as a forward conv over rotated taps (train path)
+        ops.conv2d_dgrad_s1(gy, ikf, H, H, C, 3, 1, "reflect")
     elif which == "tconv":
         ops.conv2d_tfwd(gy, ck, None, H, H, C, 3, 3, 1, 1, pad_mode="reflect")
     else:

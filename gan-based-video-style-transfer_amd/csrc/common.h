@@ -92,9 +92,9 @@ int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* b
 void rk_tile_geom(int kind, int* bm, int* bn, int* bk, int* slots);
 void rk_nhwc_to_cp(const float* x, float* y, long P, int Cs, int pack, hipStream_t s);
 void rk_nhwc_to_cp_pad(const float* x, float* y, int N, int H, int W, int Cs, int pad, int reflect,
-                       int pack, hipStream_t s);
+                       int phase, int pack, hipStream_t s);
 void rk_wgrad_launch(const float* xt, const float* dyt, float* slab, int N, int H, int W, int Cx,
-                     int Ho, int Wo, int Cyp, int S, int pad, int reflect, int Mw, int chunk,
+                     int Ho, int Wo, int Cyp, int S, int pad, int st, int Mw, int chunk,
                      int nsplit, int kind, int math, hipStream_t s);
 void rk_tconv_launch(const float* in, const float* wp, const float* bias, const float* addend,
                      float* out, int N, int Hi, int Wi, int Cy, int Ho, int Wo, int Cx, int R, int S,

@@ -686,10 +686,13 @@ static WgradPlan plan_wgrad(int N, int H, int W, int Ho, int Wo, int Cx, int Cyp
   const int P = N * Ho * Wo;
   const int ov = g_tile_override[2];
   const int pd2 = Ho - H + R - 1;  // stride 1: 2 * pad
-  if (Cyp > 4 && stride == 1 && Wo % 4 == 0 && ov < 8 && pd2 >= 0 && pd2 % 2 == 0 &&
-      Wo - W + S - 1 == pd2) {
+  const bool s1 = stride == 1 && pd2 >= 0 && pd2 % 2 == 0 && Wo - W + S - 1 == pd2;
+  // stride 2: the pad is not recoverable from the shapes; the padded copy is sized for pad <= R - 1
+  // (checked at the call) and its rows are column-phase split, which needs W + 2 pad even
+  const bool s2 = stride == 2 && W % 2 == 0;
+  if (Cyp > 4 && (s1 || s2) && Wo % 4 == 0 && ov < 8) {
     p.trans = true;
-    p.pad = pd2 / 2;
+    p.pad = s1 ? pd2 / 2 : -1;
     int kind = (ov >= 0 && ov <= 6) ? ov : (Cyp <= 64 ? (p.Mw >= 1024 ? 2 : 3) : (p.Mw >= 1024 ? 0 : 1));
     p.tile = (TileKind)kind;
     int bm, bn, bk, slots;
@@ -699,7 +702,8 @@ static WgradPlan plan_wgrad(int N, int H, int W, int Ho, int Wo, int Cx, int Cyp
                                ceil_div(P, WGRAD_CHUNK_MAX));
     p.chunk = ceil_div(ceil_div(P, ns), bk) * bk;
     p.nsplit = ceil_div(P, p.chunk);
-    p.xt_floats = rk_cp_ld((long)N * (H + 2 * p.pad) * (W + 2 * p.pad)) * Cx;  // padded image
+    const int pmax = s1 ? p.pad : (R > S ? R : S) - 1;
+    p.xt_floats = rk_cp_ld((long)N * (H + 2 * pmax) * (W + 2 * pmax)) * Cx;  // padded image
     p.dyt_floats = rk_cp_ld(P) * Cyp;
     return p;
   }
@@ -843,13 +847,16 @@ extern "C" int vst_conv2d_wgrad(const float* x, const float* dy, float* dw, floa
                      dim3(Tile<BM_, BN_, WM_, WN_>::NT), 0, s, x, dy, ws, H, W, Cx, Ho, Wo, Cyp, S,  \
                      stride, pad, refl, p.Mw, P, p.chunk)
   if (p.trans) {
-    VST_REQUIRE(pad == p.pad, "conv2d_wgrad: pad %d inconsistent with H %d -> Ho %d", pad, H, Ho);
+    VST_REQUIRE(stride == 2 ? (pad <= R - 1 && pad <= S - 1 && Ho == (H + 2 * pad - R) / 2 + 1 &&
+                               Wo == (W + 2 * pad - S) / 2 + 1)
+                            : pad == p.pad,
+                "conv2d_wgrad: pad %d inconsistent with H %d -> Ho %d (stride %d)", pad, H, Ho, stride);
     float* xt = ws + (size_t)p.nsplit * p.Mw * Cyp;
     float* dyt = xt + p.xt_floats;
     const int pack = math == VST_MATH_BF16X3;  // the x3 kernel stages pre-split (hi, lo) words
-    rk_nhwc_to_cp_pad(x, xt, N, H, W, Cx, pad, refl, pack, s);
+    rk_nhwc_to_cp_pad(x, xt, N, H, W, Cx, pad, refl, stride == 2, pack, s);
     rk_nhwc_to_cp(dy, dyt, P, Cyp, pack, s);
-    rk_wgrad_launch(xt, dyt, ws, N, H, W, Cx, Ho, Wo, Cyp, S, pad, refl, p.Mw, p.chunk, p.nsplit,
+    rk_wgrad_launch(xt, dyt, ws, N, H, W, Cx, Ho, Wo, Cyp, S, pad, stride, p.Mw, p.chunk, p.nsplit,
                     (int)p.tile, math, s);
   } else if (Cyp == 4) {
     int rc0 = skinny_wgrad_launch(x, dy, ws, H, W, Cx, Ho, Wo, S, stride, pad, refl, p.Mw, P, p.chunk,

@@ -529,12 +529,13 @@ __global__ __launch_bounds__((Tile<BM, BN, WM, WN, BK, MATH>::NT), 2) void conv_
 // row is contiguous along the reduction (pixel) axis and stages into the row-major [row][k] LDS
 // image with ds_write_b128 exactly like the forward kernel.  For stride 1 the 4 pixels of a
 // float4 are 4 consecutive padded columns: one (unaligned) 16-byte load, no border branches.
+// Stride 2 reads the same way from a copy whose padded rows are split into even / odd columns.
 // The split-K chunk index comes from the XCD-aware 1-D grid; partial tiles land in
 // slab[z][m][Cyp] (summed and transposed into dw by conv.hip).
 template <int BM, int BN, int WM, int WN, int BK, int MATH>
 __global__ __launch_bounds__((Tile<BM, BN, WM, WN, BK, MATH>::NT), 2) void conv_wgrad_rk_k(
     const float* __restrict__ xt, const float* __restrict__ dyt, float* __restrict__ slab, int H,
-    int W, int Cx, int Ho, int Wo, int Cyp, int S, int pad, int reflect, int Mw, int P, int chunk,
+    int W, int Cx, int Ho, int Wo, int Cyp, int S, int pad, int st, int Mw, int P, int chunk,
     long ldx, long ldy) {
   using T = Tile<BM, BN, WM, WN, BK, MATH>;
   constexpr int A_LD = T::A_LD, B_LD = T::B_LD, RP = T::ROWS_PER_PASS;
@@ -569,7 +570,7 @@ __global__ __launch_bounds__((Tile<BM, BN, WM, WN, BK, MATH>::NT), 2) void conv_
 
   // A rows: tap (r, s) of input channel ci over the PADDED channel-major image xt =
   // [Cx][N][Hp][Wp] (nhwc_to_cp_pad_k applied the reflect / zero border), so the 4 pixels of a
-  // float4 are 4 consecutive padded columns of one row — always in bounds, one 16-byte load.
+  // float4 are 4 consecutive words of one padded row — always in bounds, one 16-byte load.
   const int Hp = H + 2 * pad, Wp = W + 2 * pad;
   const float* xrow[A_LD];
   bool mv[A_LD];
@@ -580,7 +581,9 @@ __global__ __launch_bounds__((Tile<BM, BN, WM, WN, BK, MATH>::NT), 2) void conv_
     const int mm = mv[j] ? m : 0;
     const int tap = mm / Cx, ci = mm - tap * Cx;
     const int r = tap / S, s_ = tap - r * S;
-    xrow[j] = xt + (long)ci * ldx + r * Wp + s_;
+    // stride 2: padded rows are stored column-phase split ([even cols][odd cols], Wp / 2 each),
+    // so tap s of 4 consecutive output columns is 4 consecutive words of phase s & 1
+    xrow[j] = xt + (long)ci * ldx + r * Wp + (st == 1 ? s_ : (s_ & 1) * (Wp >> 1) + (s_ >> 1));
   }
   const float* dyrow[B_LD];
   bool nv[B_LD];
@@ -600,7 +603,7 @@ __global__ __launch_bounds__((Tile<BM, BN, WM, WN, BK, MATH>::NT), 2) void conv_
     const int rem = kp - pn * hw;
     pho = rem / Wo;
     pwo = rem - pho * Wo;
-    poff = ((long)pn * Hp + pho) * Wp + pwo;
+    poff = ((long)pn * Hp + st * pho) * Wp + pwo;
   }
   float4 ra[A_LD], rbv[B_LD];
   auto load_one = [&](int i, int) {
@@ -626,8 +629,8 @@ __global__ __launch_bounds__((Tile<BM, BN, WM, WN, BK, MATH>::NT), 2) void conv_
     poff += BK;
     while (pwo >= Wo) {
       pwo -= Wo;
-      poff += Wp - Wo;
-      if (++pho == Ho) { pho = 0; poff += (long)(Hp - Ho) * Wp; }
+      poff += st * Wp - Wo;
+      if (++pho == Ho) { pho = 0; poff += (long)(Hp - st * Ho) * Wp; }
     }
   };
   // bf16x3: the channel-major copies already hold each value as a (hi, lo) bf16 word pair
@@ -728,10 +731,11 @@ __global__ __launch_bounds__(256) void nhwc_to_cp_k(const float* __restrict__ x,
 
 // NHWC [N][H][W][Cs] -> padded channel-major [Cs][N][H+2p][W+2p] (reflect or zero border), the
 // weight gradient's A-operand image; same 64x64 LDS tile walk as nhwc_to_cp_k over padded pixels.
+// phase (stride 2, W + 2p even): each padded row stored as its even columns then its odd columns.
 template <bool PACK>
 __global__ __launch_bounds__(256) void nhwc_to_cp_pad_k(const float* __restrict__ x, float* __restrict__ y,
                                                         int N, int H, int W, int Cs, int pad, int reflect,
-                                                        long ld) {
+                                                        int phase, long ld) {
   __shared__ float tile[64][65];
   const int Hp = H + 2 * pad, Wp = W + 2 * pad;
   const long P = (long)N * Hp * Wp;
@@ -746,7 +750,12 @@ __global__ __launch_bounds__(256) void nhwc_to_cp_pad_k(const float* __restrict_
     if (q < P && c0 + c4 < Cs) {
       const int n = (int)(q / ((long)Hp * Wp));
       const int rem = (int)(q - (long)n * Hp * Wp);
-      int h = rem / Wp - pad, w = rem % Wp - pad;
+      int h = rem / Wp - pad, w = rem % Wp;
+      if (phase) {  // destination word e of a row holds padded column 2e (e < Wp/2) or 2(e - Wp/2) + 1
+        const int wh = Wp >> 1;
+        w = w < wh ? 2 * w : 2 * (w - wh) + 1;
+      }
+      w -= pad;
       bool ok = true;
       if (reflect) {
         h = reflect_idx(h, H);
@@ -784,15 +793,15 @@ __global__ __launch_bounds__(256) void nhwc_to_cp_pad_k(const float* __restrict_
 long rk_cp_ld(long P) { return (P + 63) / 64 * 64 + 64; }
 
 void rk_nhwc_to_cp_pad(const float* x, float* y, int N, int H, int W, int Cs, int pad, int reflect,
-                       int pack, hipStream_t s) {
+                       int phase, int pack, hipStream_t s) {
   const long P = (long)N * (H + 2 * pad) * (W + 2 * pad);
   const dim3 g((unsigned)((P + 63) / 64), ceil_div(Cs, 64));
   if (pack)
     hipLaunchKernelGGL(rk::nhwc_to_cp_pad_k<true>, g, dim3(256), 0, s, x, y, N, H, W, Cs, pad, reflect,
-                       rk_cp_ld(P));
+                       phase, rk_cp_ld(P));
   else
     hipLaunchKernelGGL(rk::nhwc_to_cp_pad_k<false>, g, dim3(256), 0, s, x, y, N, H, W, Cs, pad, reflect,
-                       rk_cp_ld(P));
+                       phase, rk_cp_ld(P));
 }
 
 void rk_nhwc_to_cp(const float* x, float* y, long P, int Cs, int pack, hipStream_t s) {
@@ -892,7 +901,7 @@ void rk_tconv_launch(const float* in, const float* wp, const float* bias, const 
 #endif
 
 void rk_wgrad_launch(const float* xt, const float* dyt, float* slab, int N, int H, int W, int Cx,
-                     int Ho, int Wo, int Cyp, int S, int pad, int reflect, int Mw, int chunk,
+                     int Ho, int Wo, int Cyp, int S, int pad, int st, int Mw, int chunk,
                      int nsplit, int kind, int math, hipStream_t s) {
   const int P = N * Ho * Wo;
   const int kd = math_kind(math, kind);
@@ -900,7 +909,7 @@ void rk_wgrad_launch(const float* xt, const float* dyt, float* slab, int N, int 
   hipLaunchKernelGGL((rk::conv_wgrad_rk_k<BM_, BN_, WM_, WN_, BK_, M_>),                             \
                      WGRAD_GRID(ceil_div(Mw, BM_), ceil_div(Cyp, BN_), nsplit),                       \
                      dim3(rk::Tile<BM_, BN_, WM_, WN_, BK_>::NT), 0, s, xt, dyt, slab, H, W, Cx, Ho, \
-                     Wo, Cyp, S, pad, reflect, Mw, P, chunk,                                   \
+                     Wo, Cyp, S, pad, st, Mw, P, chunk,                                         \
                      rk_cp_ld((long)N * (H + 2 * pad) * (W + 2 * pad)), rk_cp_ld(P));
 #define VST_LM(M_) VST_RK_DISPATCH_M(kd, VST_LX, M_)
   VST_MATH_SWITCH(math, VST_LM)

@@ -62,6 +62,11 @@ CONV_CASES = [
     ("res_reflect_w8", 2, 32, 12, 8, 32, 3, 1, 1, "reflect"),
     ("D_4x4_s1_w12", 2, 32, 9, 13, 64, 4, 1, 1, "zero"),
     ("res_wide_w4", 2, 256, 6, 4, 136, 3, 1, 1, "reflect"),
+    # stride 2 with W_out % 4 == 0 and W even: channel-major wgrad over column-phase split rows
+    ("d_3x3_s2_w8", 2, 16, 16, 16, 32, 3, 2, 1, "zero"),
+    ("s2_reflect_w8", 2, 8, 10, 16, 16, 3, 2, 1, "reflect"),
+    ("D_4x4_s2_w8_oddHo", 1, 16, 10, 16, 24, 4, 2, 1, "zero"),
+    ("s2_p0_w8", 2, 8, 9, 18, 16, 3, 2, 0, "zero"),
 ]
 
 
@@ -104,8 +109,13 @@ def _conv_case(ops, case, tol):
     gyn = _nhwc(gy, ops)
     if mode == "reflect":
         # two routes: padded-grid transposed conv + fold, and the fused reflect-aware gather
-        dxp = ops.conv2d_tfwd(gyn, ck, None, H + 2 * pad, W + 2 * pad, xn.shape[-1], k, k, 1, 0)
+        # (stride 1 only, like the C ABI; a strided reflect conv takes the fold route)
+        Hpd, Wpd = H + 2 * pad, W + 2 * pad
+        dxp = ops.conv2d_tfwd(gyn, ck, None, Hpd, Wpd, xn.shape[-1], k, k, st, 0)
         _close(_nchw(ops.reflect_fold(dxp, pad), Ci, ops), xr.grad, tol=tol, what=name + " dgrad(fold)")
+    if mode == "reflect" and st > 1:
+        dx = ops.reflect_fold(dxp, pad)
+    elif mode == "reflect":
         add = _nhwc(_g(40, (N, Ci, H, W)), ops)
         dx2 = ops.conv2d_tfwd(gyn, ck, None, H, W, xn.shape[-1], k, k, 1, pad, pad_mode="reflect", addend=add)
         _close(_nchw(dx2, Ci, ops) - _nchw(add, Ci, ops), xr.grad, tol=tol, what=name + " dgrad(reflect+addend)")

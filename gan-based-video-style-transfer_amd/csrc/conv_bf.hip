@@ -25,6 +25,12 @@
 #ifndef VST_BF_X6K3
 #define VST_BF_X6K3 0
 #endif
+#ifndef VST_BF_MINB
+#define VST_BF_MINB 1
+#endif
+#ifndef VST_BF_X6_256
+#define VST_BF_X6_256 1
+#endif
 #ifndef VST_BF_TAIL
 #define VST_BF_TAIL 1
 #endif
@@ -54,6 +60,13 @@ struct Tile {
   static_assert(KC == 2 || KC == 4 || KC == 8, "BK in {16, 32, 64}");
   static_assert(BM % RPP == 0 && BN % RPP == 0, "row coverage");
   static_assert(2 * STAGE <= 160 * 1024, "LDS");
+  // co-resident blocks per CU the register budget is compiled for: two when two double-buffered
+  // stage pairs fit the 160 KB LDS, else one (then each wave may use the whole 2-wave budget)
+#if VST_BF_MINB
+  static constexpr int MINB = 4 * STAGE <= 160 * 1024 ? 2 : 1;
+#else
+  static constexpr int MINB = 2;
+#endif
 };
 
 __device__ __forceinline__ int swz_off(int row, int c, int rowb, int sws, int kcm) {
@@ -225,7 +238,7 @@ __device__ __forceinline__ void tile_of(int L, int Mt, int Nt, int& mt, int& nt)
 // requires C % 8 == 0 (a thread's 8-deep chunk stays inside one tap).  ws = pre-split weight planes
 // of the VST_PACK_OK matrix [Cop][R*S*C], plane stride wps elements.
 template <class T>
-__global__ __launch_bounds__(T::NT, 2) void conv_fprop_bf_k(
+__global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_k(
     const float* __restrict__ x, const __bf16* __restrict__ ws, long wps, const float* __restrict__ bias,
     float* __restrict__ y, int H, int W, int C, int Ho, int Wo, int Cop, int S, int st, int padh,
     int padw, int reflect, int act, float slope, int M, int Ktot, int m_base) {
@@ -366,11 +379,12 @@ __global__ void split3_k(const float* __restrict__ w, __bf16* __restrict__ out, 
     case 4: L(128, 128, 64, 32, (np == 3 ? 32 : 64), np) break;        \
     case 5: L(128, 64, 64, 32, 64, np) break;                          \
     case 6: L(64, 64, 32, 32, 32, np) break;                           \
+    case 7: L(256, 128, 64, 64, 32, np) break;                         \
     default: L(128, 128, 64, 32, 32, np) break;                        \
   }
 
 int bf_pick(long M, int Nc, int override_kind) {
-  if (override_kind >= 0 && override_kind <= 6) return override_kind;
+  if (override_kind >= 0 && override_kind <= 7) return override_kind;
   if (Nc <= 64) return M / 128 >= 256 ? 1 : 6;
   const long n128 = (Nc + 127) / 128;
   if ((M / 128) * n128 >= 200) return 0;
@@ -387,6 +401,14 @@ int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* b
 #if VST_BF_X6K3
   // x6: the 128x128 three-plane stage pair (96 KB) fits one block per CU; 64x128 tiles fit two
   if (kind < 0 && kd == 0 && math == VST_MATH_BF16X6) kd = 3;
+#endif
+#if VST_BF_X6_256
+  // x6, one block per CU either way: 256x128 tiles of 8 waves x (64x64) halve the LDS fragment
+  // reads per MFMA and the barriers per FLOP — when the grid is whole rounds of 256 blocks
+  if (kind < 0 && kd == 0 && math == VST_MATH_BF16X6) {
+    const long b256 = (long)((M + 255) / 256) * ((Cop + 127) / 128);
+    if (b256 % VST_NUM_CUS == 0 || b256 >= 4 * VST_NUM_CUS) kd = 7;
+  }
 #endif
   int m_split = 0;
 #if VST_BF_TAIL

@@ -9,8 +9,9 @@ processed by all ranks / max-over-ranks wall time of exactly K steps (barrier + 
 sides).  Multi-GPU: one process per GPU (torchrun), gradients exchanged with RCCL all_reduce.
 
 Also reported (same JSON line):
-  roofline      the dominant kernel (ResnetBlock 3x3 conv fprop, 16384x256x2304 implicit GEMM at
-                B=4) timed with HIP events around each of its launches inside the timed steps:
+  roofline      the dominant kernel (ResnetBlock 3x3 conv fprop, 32768x256x2304 implicit GEMM at
+                N=2B=8, the batched G_A calls) timed with HIP events around each of its launches
+                inside the timed steps:
                 algorithmic FLOPs / avg duration vs the fp32 MFMA peak; traffic = PMC-measured HBM
                 bytes per launch from profiles/r01_conv_fprop_pmc.json (tools/pmc_conv.py).
   cpu_baseline  rank 0 only, N=1: the CPU oracle (stock PyTorch, NCHW fp32) on the host cores,
@@ -94,7 +95,7 @@ def dominant_kernel_roofline(B, probe):
         except Exception:
             traffic = None
     emu = BF16_MFMA_PEAK_TFLOPS / 6.0
-    return {"kernel": "conv_fprop_bf_k<128x128, bf16x6> (ResnetBlock 3x3 reflect 256->256 @64x64, N=%d)" % N,
+    return {"kernel": "conv_fprop_bf_k<256x128, bf16x6> (ResnetBlock 3x3 reflect 256->256 @64x64, N=%d)" % N,
             "bound": "mfma", "achieved": round(achieved, 2), "peak": round(emu, 1),
             "unit": "TFLOP/s", "frac": round(achieved / emu, 4),
             "peak_basis": "dense bf16 MFMA %.0f TFLOP/s / 6 bf16 products per fp32-equivalent MAC" %

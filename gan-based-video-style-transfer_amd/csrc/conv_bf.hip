@@ -31,6 +31,9 @@
 #ifndef VST_BF_X6_256
 #define VST_BF_X6_256 1
 #endif
+#ifndef VST_BF_KSLICE
+#define VST_BF_KSLICE 1
+#endif
 #ifndef VST_BF_TAIL
 #define VST_BF_TAIL 1
 #endif
@@ -250,7 +253,16 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_k(
   const int m0 = m_base + mt_ * T::BM, n0 = nt_ * T::BN;
   const int kq = t % T::KC, rb = t / T::KC;
 
-  // this thread's chunk: absolute k = kcur, tap (kr, ks), channel kc
+  // this thread's chunk: absolute k = kcur, tap (kr, ks), channel kc.
+  // Channel-sliced K order (C % BK == 0): K-steps walk the R*S taps of one BK-channel slice, then
+  // the next slice, so one slice of the block's activation rows is reused by all taps while it
+  // is L2-resident (tap-major order streams the whole C-deep block through L2 once per tap).  The
+  // weight planes keep their (r, s, ci) layout: the B offset of a step is (r*S + s)*C + kc.
+  // Applied where the tap-major order overflows L2: the 256-row x6 tiles (one round, 4 MB live
+  // activation block per XCD: 289 -> 96 MB HBM traffic per N=8 ResnetBlock launch).  Smaller
+  // tiles keep the tap-major summation order.
+  const bool ksl = VST_BF_KSLICE && T::BM == 256 && NP == 3 && C % T::BK == 0 && Ktot % C == 0;
+  const int Rk = ksl ? Ktot / (S * C) : 0;
   int kcur = 8 * kq;
   int kc = kcur % C, ks, kr;
   {
@@ -299,8 +311,8 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_k(
   // unconditional loads: invalid rows / the K tail read a safe address; the row mask (bit j = A row
   // j, bit 16 + j = B row j) zeroes them when the stage is written to LDS
   auto load_all = [&](int set) {
-    const bool kin = kcur < Ktot;
-    const int kk = kin ? kcur : 0;
+    const bool kin = ksl ? kc < C : kcur < Ktot;
+    const int kk = kin ? (ksl ? (kr * S + ks) * C + kc : kcur) : 0;
     uint32_t m = 0;
 #pragma unroll
     for (int j = 0; j < A_LD; ++j) {
@@ -319,6 +331,14 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_k(
     msk[set] = m;
   };
   auto adv = [&]() {
+    if (ksl) {
+      if (++ks == S) {
+        ks = 0;
+        if (++kr == Rk) { kr = 0; kc += T::BK; }
+      }
+      tap_rows();
+      return;
+    }
     kcur += T::BK;
     kc += T::BK;
     if (kc >= C) {

@@ -133,12 +133,14 @@ def test_full_size_generator_vs_oracle(gb, infer_math):
         y_ref = ref(x)
         y = net(x.to(DEV)).cpu()
     assert (y - y_ref).abs().max().item() < 1e-3
-    # batch invariance at B=4 (per-sample InstanceNorm): frame 2 of a batch == the frame alone
+    # batch invariance at B=4 (per-sample InstanceNorm): frame 2 of a batch == the frame alone, up
+    # to fp32 summation order (the batched call may take another tile / K order: 256-row tiles
+    # walk K channel-slice-major), i.e. a few ulps of the tanh output after 24 conv + IN layers
     xb = torch.from_numpy(prng.uniform_f32(79, (4, 3, 256, 256), -1, 1)).to(DEV)
     with torch.no_grad():
         yb = net(xb)
         y2 = net(xb[2:3].contiguous())
-    assert (yb[2:3] - y2).abs().max().item() < 1e-5
+    assert (yb[2:3] - y2).abs().max().item() < 3e-5
 
 
 def test_pool_and_plain_step_run(gb, golden):

@@ -63,8 +63,8 @@ __global__ __launch_bounds__(NRED) void in_partial_k(const float* __restrict__ x
   }
   const float4* xb = reinterpret_cast<const float4*>(x) + (long)n * HW * LP + c4;
   const float4* gb = reinterpret_cast<const float4*>(gy) + (long)n * HW * LP + c4;
-  for (int p = p0 + pg; pg < PG && p < p1; p += PG) {
-    const float4 v = xb[(long)p * LP];
+  // one pixel row's float4 (x, and g for MODE 1) into the fp64 partials
+  auto accum = [&](const float4 v, const float4 gv) {
     const float xv[4] = {v.x, v.y, v.z, v.w};
     if (MODE == 0) {
 #pragma unroll
@@ -73,7 +73,6 @@ __global__ __launch_bounds__(NRED) void in_partial_k(const float* __restrict__ x
         acc[1][j] += (double)xv[j] * xv[j];
       }
     } else {
-      const float4 gv = gb[(long)p * LP];
       const float gg[4] = {gv.x, gv.y, gv.z, gv.w};
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -87,6 +86,23 @@ __global__ __launch_bounds__(NRED) void in_partial_k(const float* __restrict__ x
         acc[2][j] += xh;
       }
     }
+  };
+  // the thread's rows p, p + PG, p + 2 PG, ... accumulated in that order; four rows' loads are
+  // issued together ahead of their (serial, order-preserving) fp64 accumulation
+  if (pg < PG) {
+    int p = p0 + pg;
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (; p + 3 * PG < p1; p += 4 * PG) {
+      float4 v[4], gv[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        v[k] = xb[(long)(p + k * PG) * LP];
+        gv[k] = MODE == 1 ? gb[(long)(p + k * PG) * LP] : z4;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) accum(v[k], gv[k]);
+    }
+    for (; p < p1; p += PG) accum(xb[(long)p * LP], MODE == 1 ? gb[(long)p * LP] : z4);
   }
 #pragma unroll
   for (int v = 0; v < NV; ++v)

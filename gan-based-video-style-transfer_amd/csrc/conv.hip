@@ -564,23 +564,32 @@ __global__ void wgrad_sum_k(float* __restrict__ slab, long n4, int nsplit) {
   s[i] = a;
 }
 
-// dw[co*so + ci*si + rs] (+)= S[rs*Cx + ci][co] via a 64x64 LDS transpose tile (reads coalesced
-// along co, writes along m = (rs, ci)).
-__global__ void wgrad_store_k(const float* __restrict__ Ssum, float* __restrict__ dw, int Mw, int Cx,
-                              int Cyp, int RS, int Co, int Ci, long so, long si, int accumulate) {
+// dw[co*so + ci*si + rs] (+)= sum_z S_z[rs*Cx + ci][co] via a 64x64 LDS transpose tile whose rows
+// are 64 consecutive (ci, rs) of dw's own order (reads coalesced along co, writes contiguous along
+// ci*RS + rs for the dense [Co][Ci][R][S] layout).  nsplit > 1 folds the split-K slabs (stride zs)
+// in the load, in wgrad_sum_k's order (z = 0, 1, 2, ...), so the sums are bit-identical.
+__global__ void wgrad_store_k(const float* __restrict__ S, float* __restrict__ dw, int Cx, int Cyp, int RS,
+                              int Co, int Ci, long so, long si, int accumulate, int nsplit, long zs) {
   __shared__ float tile[64][65];
   const int m0 = blockIdx.x * 64, c0 = blockIdx.y * 64;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int Md = Ci * RS;
   for (int r = ty; r < 64; r += 4) {
-    const int m = m0 + r, c = c0 + tx;
-    tile[r][tx] = (m < Mw && c < Cyp) ? Ssum[(long)m * Cyp + c] : 0.f;
+    const int md = m0 + r, c = c0 + tx;
+    float v = 0.f;
+    if (md < Md && c < Cyp) {
+      const int ci = md / RS, rs = md - ci * RS;
+      const float* src = S + (long)(rs * Cx + ci) * Cyp + c;
+      v = src[0];
+      for (int z = 1; z < nsplit; ++z) v += src[(long)z * zs];
+    }
+    tile[r][tx] = v;
   }
   __syncthreads();
   for (int r = ty; r < 64; r += 4) {
-    const int c = c0 + r, m = m0 + tx;
-    if (c >= Co || m >= Mw) continue;
-    const int ci = m % Cx, rs = m / Cx;
-    if (ci >= Ci) continue;
+    const int c = c0 + r, md = m0 + tx;
+    if (c >= Co || md >= Md) continue;
+    const int ci = md / RS, rs = md - ci * RS;
     float* d = dw + c * so + ci * si + rs;
     const float v = tile[tx][r];
     *d = accumulate ? *d + v : v;
@@ -868,12 +877,15 @@ extern "C" int vst_conv2d_wgrad(const float* x, const float* dy, float* dw, floa
 #undef VST_WG
   int rc = check_launch("conv2d_wgrad");
   if (rc) return rc;
-  if (p.nsplit > 1) {
+  // split-K slabs: one streaming sum pass first (a fold inside the store serialises its loads)
+  const bool fold = p.nsplit <= 1;
+  if (p.nsplit > 1 && !fold) {
     const long n4 = (long)p.Mw * Cyp / 4;
     hipLaunchKernelGGL(wgrad_sum_k, dim3(ceil_div(n4, 256)), dim3(256), 0, s, ws, n4, p.nsplit);
   }
-  hipLaunchKernelGGL(wgrad_store_k, dim3(ceil_div(p.Mw, 64), ceil_div(Cyp, 64)), dim3(256), 0, s, ws,
-                     dw, p.Mw, Cx, Cyp, R * S, Co, Ci, so, si, accumulate);
+  hipLaunchKernelGGL(wgrad_store_k, dim3(ceil_div(Ci * R * S, 64), ceil_div(Co, 64)), dim3(256), 0, s, ws,
+                     dw, Cx, Cyp, R * S, Co, Ci, so, si, accumulate, fold ? p.nsplit : 1,
+                     (long)p.Mw * Cyp);
   return check_launch("conv2d_wgrad_reduce");
 }
 

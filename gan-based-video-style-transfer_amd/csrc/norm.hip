@@ -36,6 +36,10 @@ static bool red_geom(int N, int HW, int C, RedGeom& g) {
   return true;
 }
 
+#ifndef IN_UNROLL
+#define IN_UNROLL 4
+#endif
+
 // MODE 0: stats partials {sum x, sum x^2}; MODE 1: backward partials {sum g, sum g*xhat, sum xhat}
 template <int MODE>
 __global__ __launch_bounds__(NRED) void in_partial_k(const float* __restrict__ x,
@@ -87,20 +91,21 @@ __global__ __launch_bounds__(NRED) void in_partial_k(const float* __restrict__ x
       }
     }
   };
-  // the thread's rows p, p + PG, p + 2 PG, ... accumulated in that order; four rows' loads are
+  // the thread's rows p, p + PG, p + 2 PG, ... accumulated in that order; UR rows' loads are
   // issued together ahead of their (serial, order-preserving) fp64 accumulation
+  constexpr int UR = IN_UNROLL;
   if (pg < PG) {
     int p = p0 + pg;
     const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (; p + 3 * PG < p1; p += 4 * PG) {
-      float4 v[4], gv[4];
+    for (; p + (UR - 1) * PG < p1; p += UR * PG) {
+      float4 v[UR], gv[UR];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
+      for (int k = 0; k < UR; ++k) {
         v[k] = xb[(long)(p + k * PG) * LP];
         gv[k] = MODE == 1 ? gb[(long)(p + k * PG) * LP] : z4;
       }
 #pragma unroll
-      for (int k = 0; k < 4; ++k) accum(v[k], gv[k]);
+      for (int k = 0; k < UR; ++k) accum(v[k], gv[k]);
     }
     for (; p < p1; p += PG) accum(xb[(long)p * LP], MODE == 1 ? gb[(long)p * LP] : z4);
   }

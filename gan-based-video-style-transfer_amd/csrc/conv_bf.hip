@@ -34,6 +34,9 @@
 #ifndef VST_BF_KSLICE
 #define VST_BF_KSLICE 1
 #endif
+#ifndef VST_BF_TAIL_KIND
+#define VST_BF_TAIL_KIND 8
+#endif
 #ifndef VST_BF_TAIL
 #define VST_BF_TAIL 1
 #endif
@@ -400,6 +403,7 @@ __global__ void split3_k(const float* __restrict__ w, __bf16* __restrict__ out, 
     case 5: L(128, 64, 64, 32, 64, np) break;                          \
     case 6: L(64, 64, 32, 32, 32, np) break;                           \
     case 7: L(256, 128, 64, 64, 32, np) break;                         \
+    case 8: L(64, 64, 32, 32, (np == 3 ? 32 : 64), np) break;          \
     default: L(128, 128, 64, 32, 32, np) break;                        \
   }
 
@@ -452,7 +456,7 @@ int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* b
   }
   for (int part = 0; part < (m_split ? 2 : 1); ++part) {
     const int mb = part ? m_split : 0, Mend = (m_split && !part) ? m_split : M;
-    const int kp = part ? 6 : kd;
+    const int kp = part ? VST_BF_TAIL_KIND : kd;
     if (math == VST_MATH_BF16X6) {
       VST_BF_DISPATCH(kp, 3, VST_BF)
     } else {

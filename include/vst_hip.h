@@ -124,7 +124,9 @@ int vst_conv2d_tfwd(const float* in, const float* wp, const float* bias, const f
  * so = Ci*R*S, si = R*S for a Conv2d weight.  A ConvTranspose2d weight Wt[Ci][Co][R][S] is the
  * weight gradient of the equivalent conv x_T = conv(dy_T, .): call with x := grad of the convT
  * output, dy := convT input, (Co, Ci) := (Ci_T, Co_T), db := NULL (use vst_channel_sum).  accumulate != 0 adds into dw/db.  Split-K partial slabs go to
- * ws (vst_conv2d_wgrad_ws_bytes bytes) and are reduced in a fixed order (deterministic). */
+ * ws (vst_conv2d_wgrad_ws_bytes bytes) and are reduced in a fixed order (deterministic).
+ * Stride 1 and 2 with W_out % 4 == 0 (stride 2: W even) stage padded channel-major copies of x and
+ * dy in ws; for stride 2 that copy is sized for pad <= min(R, S) - 1 (VST_EINVAL beyond). */
 size_t vst_conv2d_wgrad_ws_bytes(int N, int H, int W, int Cx, int Ho, int Wo, int Cyp, int R, int S,
                                  int stride);
 int vst_conv2d_wgrad(const float* x, const float* dy, float* dw, float* ws, size_t ws_bytes, int N,

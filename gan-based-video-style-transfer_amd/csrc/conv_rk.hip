@@ -566,7 +566,6 @@ __global__ __launch_bounds__((Tile<BM, BN, WM, WN, BK, MATH>::NT), 2) void conv_
 #endif
   const int pend = min(P, pbeg + chunk);
   const int kq = t % T::KQ, rb = T::row_of(t);
-  const long HW = (long)H * W;
 
   // A rows: tap (r, s) of input channel ci over the PADDED channel-major image xt =
   // [Cx][N][Hp][Wp] (nhwc_to_cp_pad_k applied the reflect / zero border), so the 4 pixels of a

@@ -685,6 +685,10 @@ static int pick_splits(int tiles, int slots, int max_ns, int min_ns = 1) {
   return ns;
 }
 
+#ifndef VST_WG_BIG
+#define VST_WG_BIG 5  // rk tile kind of the wide (Cyp > 64, Mw >= 1024) weight gradients
+#endif
+
 static WgradPlan plan_wgrad(int N, int H, int W, int Ho, int Wo, int Cx, int Cyp, int R, int S,
                             int stride) {
   WgradPlan p;
@@ -702,7 +706,7 @@ static WgradPlan plan_wgrad(int N, int H, int W, int Ho, int Wo, int Cx, int Cyp
   if (Cyp > 4 && (s1 || s2) && Wo % 4 == 0 && ov < 8) {
     p.trans = true;
     p.pad = s1 ? pd2 / 2 : -1;
-    int kind = (ov >= 0 && ov <= 6) ? ov : (Cyp <= 64 ? (p.Mw >= 1024 ? 2 : 3) : (p.Mw >= 1024 ? 0 : 1));
+    int kind = (ov >= 0 && ov <= 6) ? ov : (Cyp <= 64 ? (p.Mw >= 1024 ? 2 : 3) : (p.Mw >= 1024 ? VST_WG_BIG : 1));
     p.tile = (TileKind)kind;
     int bm, bn, bk, slots;
     rk_tile_geom(kind, &bm, &bn, &bk, &slots);

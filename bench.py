@@ -9,14 +9,21 @@ processed by all ranks / max-over-ranks wall time of exactly K steps (barrier + 
 sides).  Multi-GPU: one process per GPU (torchrun), gradients exchanged with RCCL all_reduce.
 
 Also reported (same JSON line):
-  roofline      the dominant kernel (ResnetBlock 3x3 conv fprop, 32768x256x2304 implicit GEMM at
-                N=2B=8, the batched G_A calls) timed with HIP events around each of its launches
-                inside the timed steps:
-                algorithmic FLOPs / avg duration vs the fp32 MFMA peak; traffic = PMC-measured HBM
-                bytes per launch from profiles/r01_conv_fprop_pmc.json (tools/pmc_conv.py).
-  cpu_baseline  rank 0 only, N=1: the CPU oracle (stock PyTorch, NCHW fp32) on the host cores,
-                one B=4 step after a B=1 warm-up (oracle is imported only for this leg).
-  inference     generator-only inference fps at 256x256, B=16 (north_star's secondary number).
+  math          the conv arithmetic of the headline: bf16x6 (fp32-equivalent split products) in
+                every forward, data-gradient and weight-gradient conv (--math / VST_CONV_MATH).
+  roofline      the dominant conv launch of the step by time, out of roofline_convs: the ResnetBlock
+                3x3 conv forward / stride-1 dgrad / wgrad at N=2B=8 (the batched G_A calls), each
+                timed with HIP events around each of its launches inside the timed steps:
+                algorithmic FLOPs / avg duration vs the ceiling of the arithmetic it runs; traffic =
+                PMC-measured HBM bytes per launch from profiles/r02_conv_pmc.json when that record
+                matches the policy / tile / shape, else null.
+  mixed_policy  the same step under the round-1 "mixed" policy (x6 forwards, x3 gradients), labelled.
+  cpu_baseline  rank 0 only, N=1: the CPU oracle (stock PyTorch, NCHW fp32) with the GPU run's
+  parity        initial weights and synthetic batch, on all the CPUs this process may use: one
+                warm-up step whose losses are checked against the GPU's step-0 losses (parity),
+                then 2 timed B=4 steps (oracle is imported only for this leg).
+  inference     generator-only inference fps at 256x256, B=16 (north_star's secondary number),
+                under the headline policy.
   extras        generator inference at the Sintel size (1x436x1024); the flow-warp kernel's HBM
                 roofline on the SURVEY §8d large synthetic (N=32, C=64, 436x1024); the RAFT
                 correlation volume build at fmaps 1x256x55x128; the Johnson (FastStyleNet + VGG16
@@ -69,40 +76,66 @@ def _time_on_stream(fn, reps, warm=3):
     return e0.elapsed_time(e1) / reps
 
 
-# ResnetBlock conv forward (N,H,W,Cx,Cop,R,stride,pad,mode) as launched by the batched G_A calls
-# (N = 2B: [real_A, real_A2] and [fake_A, real_B]); pad 1 reflect separates it from the stride-1
-# data gradient that runs on the same kernel over the padded frame (pad 2 zero).
-DOMINANT_KEY = lambda B: (2 * B, 64, 64, 256, 256, 3, 1, 1, "reflect")  # noqa: E731
+# The step's dominant conv launches: the ResnetBlock 3x3 reflect 256->256 @64x64 convs of the batched
+# generator calls (N = 2B frames: G_A[real_A, real_A2] and G_A[fake_A, real_B]) — the forward, the
+# stride-1 data gradient (a forward conv over the rotated taps onto the 66x66 padded frame: zero pad 2,
+# the key that separates it from the forward) and the weight gradient.  Keys: ops.LaunchProbe.
+def DOMINANT_KEYS(B):
+    N = 2 * B
+    return {"resblock_fprop": ("fwd", (N, 64, 64, 256, 256, 3, 1, 1, "reflect")),
+            "resblock_dgrad": ("fwd", (N, 64, 64, 256, 256, 3, 1, 2, "zero")),
+            "resblock_wgrad": ("wgrad", (N, 64, 64, 256, 256, 3, 1, 1, "reflect"))}
 
 
-def dominant_kernel_roofline(B, probe):
-    """The dominant kernel — the ResnetBlock conv forward (3x3 reflect, 256->256 @64x64, 2B frames:
-    the batched G_A calls, 36 launches per train step) — timed live over the timed steps: HIP events around each of its
-    launches on the stream it is launched on (ops.LaunchProbe).  It runs the training forward
-    arithmetic (bf16x6: fp32-equivalent products from 6 bf16 MFMAs per MAC), so its hardware
-    ceiling — `peak` — is the dense bf16 MFMA peak / 6 in fp32-equivalent FLOP/s; the fp32 MFMA
-    peak (the ceiling of a native-fp32 kernel, which this one exceeds) is reported beside it."""
+PMC_FILE = os.path.join(HERE, "profiles", "r02_conv_pmc.json")
+
+
+def _pmc_traffic(name, key):
+    """HBM bytes per launch of this kernel from the committed rocprofv3 PMC record (two passes:
+    FETCH_SIZE x2 per the gfx950 wide-read correction, WRITE_SIZE), only if the record was taken
+    on the same policy, tile and shape; else None."""
+    try:
+        rec = json.load(open(PMC_FILE)).get(name)
+    except (OSError, ValueError):
+        return None
+    if not rec or any(rec.get("key", {}).get(k) != v for k, v in key.items()):
+        return None
+    return rec.get("hbm_bytes_per_launch")
+
+
+def conv_roofline(name, probe, math):
+    """Roofline entry of one probed conv: algorithmic FLOPs (2*M*N*K of the conv it computes) per
+    launch / the average duration of its launches inside the timed steps (HIP events on the launch
+    stream) vs the ceiling of the arithmetic it executes (dense bf16 MFMA peak / 6 products per
+    fp32-equivalent MAC for bf16x6, / 3 for bf16x3; the fp32 MFMA peak for fp32)."""
+    from gbvst import ops
+    if not probe.events:
+        return None
     ms = probe.mean_ms()
-    N = probe.key[0]
+    op, (N, H, W, Cx, Cop, R, st, pad, mode) = probe.key
     flop = 2.0 * (N * 64 * 64) * 256 * (256 * 9)
+    role = "bwd" if name != "resblock_fprop" else "fwd"
+    m = ops._POLICIES[math][role]
+    peak = {"bf16x6": BF16_MFMA_PEAK_TFLOPS / 6.0, "bf16x3": BF16_MFMA_PEAK_TFLOPS / 3.0,
+            "fp32": FP32_MFMA_PEAK_TFLOPS}[m]
     achieved = flop / (ms * 1e-3) / 1e12
-    traffic = None
-    pmc = os.path.join(HERE, "profiles", "r01_conv_fprop_pmc.json")
-    if os.path.exists(pmc):
-        try:
-            rec = json.load(open(pmc))
-            traffic = rec.get("hbm_bytes_per_launch") if rec.get("batch") == N else None
-        except Exception:
-            traffic = None
-    emu = BF16_MFMA_PEAK_TFLOPS / 6.0
-    return {"kernel": "conv_fprop_bf_k<256x128, bf16x6> (ResnetBlock 3x3 reflect 256->256 @64x64, N=%d)" % N,
-            "bound": "mfma", "achieved": round(achieved, 2), "peak": round(emu, 1),
-            "unit": "TFLOP/s", "frac": round(achieved / emu, 4),
-            "peak_basis": "dense bf16 MFMA %.0f TFLOP/s / 6 bf16 products per fp32-equivalent MAC" %
-                          BF16_MFMA_PEAK_TFLOPS,
-            "traffic": traffic, "avg_launch_ms": round(ms, 4), "flop_per_launch": flop,
-            "launches_timed": len(probe.events),
-            "fp32_mfma_peak": FP32_MFMA_PEAK_TFLOPS, "frac_of_fp32_mfma_peak": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4)}
+    if op == "fwd":
+        kind, ms_ = ops.conv_plan_fwd(N, H, W, Cx, Cop, R, R, st, pad, pad, m)
+        kernel = "conv_fprop_bf_k<%s, %s>%s" % (ops.TILE_NAMES.get(kind, kind), m, " + 64x64 tail" if ms_ else "")
+        key = {"math": m, "tile": kind, "m_split": ms_, "N": N}
+        note = ("stride-1 data gradient as a forward conv over the rotated taps (66x66 padded frame)"
+                if name == "resblock_dgrad" else "ResnetBlock conv forward")
+    else:
+        kernel = "vst_conv2d_wgrad (channel-major copies + conv_wgrad_rk_k + split-K sum/store), %s" % m
+        key = {"math": m, "N": N}
+        note = "whole weight-gradient op: its 4-5 launches are timed together"
+    return {"kernel": kernel, "what": note + " — ResnetBlock 3x3 reflect 256->256 @64x64, N=%d" % N,
+            "bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
+            "frac": round(achieved / peak, 4),
+            "peak_basis": "dense bf16 MFMA %.0f TFLOP/s / products per fp32-equivalent MAC (%s)" % (BF16_MFMA_PEAK_TFLOPS, m),
+            "traffic": _pmc_traffic(name, key), "avg_launch_ms": round(ms, 4), "flop_per_launch": flop,
+            "launches_timed": len(probe.events), "ms_per_step": round(ms * len(probe.events) / max(1, probe.steps), 3),
+            "fp32_mfma_peak": FP32_MFMA_PEAK_TFLOPS}
 
 
 def warp_roofline(device, N=32, C=64, H=436, W=1024, reps=10):
@@ -259,32 +292,85 @@ def inference_fps(device, B=16, reps=10):
             "unit": "frames/s", "tflops": round(fps * G_GFLOP_PER_FRAME / 1e3, 2)}
 
 
-def cpu_baseline(B=4, H=256, W=256):
-    """Oracle (stock PyTorch CPU, NCHW fp32) train step on the host cores: 1 B=1 warm-up step, then
-    one timed B=4 step (a bounded ~10-60 s sample of the same workload)."""
-    from oracle import cpu_ref
-    threads = min(16, os.cpu_count() or 1)
-    torch.set_num_threads(threads)
-    m = cpu_ref.RefCycleGANCon(device="cpu")
-    a, a2, b, mask, flow = cpu_ref.synthetic_batch(1, H, W, seed=99)
-    m.set_input_fc2(a, a2, b, mask, flow)
-    m.optimize_parameters()
-    a, a2, b, mask, flow = cpu_ref.synthetic_batch(B, H, W, seed=100)
-    m.set_input_fc2(a, a2, b, mask, flow)
-    t0 = time.perf_counter()
-    m.optimize_parameters()
-    dt = time.perf_counter() - t0
-    model = ""
+def host_cpus():
+    """CPUs this process may run on: the affinity set, capped by a cgroup-v2 CPU quota if one is
+    set (on a shared GPU box os.cpu_count() reports the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = max(1, min(n, int(int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
             if line.startswith("model name"):
-                model = line.split(":", 1)[1].strip()
-                break
+                return line.split(":", 1)[1].strip()
     except OSError:
         pass
-    return {"value": round(B / dt, 4), "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/cpu_ref.RefCycleGANCon: 1 train step B={B} {H}x{W} fp32 after a B=1 warm-up "
-                      f"({dt:.1f} s; torch CPU threads={threads}; {model})"}
+    return ""
+
+
+def cpu_baseline_and_parity(init_sd, batch_cpu, hip_losses0, steps=2):
+    """cpu_baseline + parity leg (rank 0, N=1): the CPU oracle (oracle/cpu_ref.RefCycleGANCon —
+    stock PyTorch, NCHW fp32, the reference's arithmetic) loaded with the SAME initial weights and
+    fed the SAME synthetic batch as the GPU run.  Its first optimize_parameters() is the warm-up and
+    the parity check: step-0 losses vs the GPU model's step-0 losses (max relative difference over
+    the 9 loss terms; north_star bound 1e-3).  Then `steps` more B=4 steps are timed on all the host
+    CPUs this process may use."""
+    from oracle import cpu_ref
+    threads = host_cpus()
+    torch.set_num_threads(threads)
+    m = cpu_ref.RefCycleGANCon(device="cpu")
+    for name, net in m.nets().items():
+        net.load_state_dict(init_sd[name])
+    m.set_input_fc2(*batch_cpu)
+    m.optimize_parameters()
+    ref = m.get_current_losses()
+    rel = {k: abs(hip_losses0[k] - v) / abs(v) for k, v in ref.items()}
+    parity = {"what": "step-0 losses, GPU (HIP) vs CPU oracle, same weights and inputs", "max_rel": max(rel.values()),
+              "worst": max(rel, key=rel.get), "bound": 1e-3, "pass": max(rel.values()) <= 1e-3}
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        m.optimize_parameters()
+    dt = (time.perf_counter() - t0) / steps
+    B, _, H, W = batch_cpu[0].shape
+    base = {"value": round(B / dt, 4), "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/cpu_ref.RefCycleGANCon: {steps} timed train steps B={B} {H}x{W} fp32 after 1 "
+                      f"warm-up/parity step ({dt:.1f} s/step; torch threads={threads} = the CPUs this process may "
+                      f"use of os.cpu_count()={os.cpu_count()}; {cpu_model()})"}
+    return base, parity
+
+
+def time_steps(model, steps, hook_g, hook_d, world, device):
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        model.optimize_parameters(hook_g, hook_d)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    return elapsed
+
+
+# What each conv arithmetic policy computes in (gbvst.ops._POLICIES); the headline runs "bf16x6".
+MATH_LABEL = {"bf16x6": "fp32 (bf16x6 split products: fp32-equivalent, fp32 accumulate) in every conv: fwd, dgrad, wgrad",
+              "mixed": "mixed: bf16x6 (fp32-equivalent) training forwards / bf16x3 (~2^-16 rel. products) dgrad, wgrad, inference",
+              "fp32": "fp32 (v_mfma_f32_32x32x2_f32) in every conv",
+              "bf16x3": "bf16x3 split products (~2^-16 relative) in every conv"}
 
 
 def main():
@@ -295,6 +381,8 @@ def main():
     ap.add_argument("--batch", type=int, default=4, help="frame pairs per GPU (C2: 4)")
     ap.add_argument("--size", type=int, default=256)
     ap.add_argument("--pool", type=int, default=50)
+    ap.add_argument("--math", default=os.environ.get("VST_CONV_MATH", "bf16x6"),
+                    help="conv arithmetic policy of the headline (fp32-equivalent bf16x6 by default)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
     args = ap.parse_args()
@@ -310,45 +398,38 @@ def main():
 
     import gbvst
     gbvst._lib.load()
-    from gbvst import dp
+    from gbvst import dp, ops
     from gbvst.cycle_gan_model import CycleGANModel
     from gbvst.options import default_opt
 
+    ops.set_conv_math(args.math)
     torch.manual_seed(0)
     opt = default_opt(True, gpu_ids=[local], pool_size=args.pool)
     model = CycleGANModel(opt)
+    nets = {"G_A": model.netG_A, "G_B": model.netG_B, "D_A": model.netD_A, "D_B": model.netD_B}
     hookG = hookD = None
     if world > 1:
-        nets = [model.netG_A, model.netG_B, model.netD_A, model.netD_B]
-        dp.broadcast_params(nets)
-        ex = dp.GradExchange(world)
+        dp.broadcast_params(list(nets.values()))
+        ex = dp.GradExchange(world).attach(list(nets.values()))
         hookG = hookD = ex
+    init_sd = {k: {n: t.detach().cpu().clone() for n, t in v.state_dict().items()} for k, v in nets.items()}
     B, S = args.batch, args.size
-    a, a2, b, mask, flow = synthetic_batch(B, S, S, seed=1234 + rank, device=device)
-    from gbvst import ops
-    model.set_input_nhwc(ops.nchw_to_nhwc(a), ops.nchw_to_nhwc(a2), ops.nchw_to_nhwc(b), mask, flow)
+    batch_cpu = synthetic_batch(B, S, S, seed=1234 + rank, device="cpu")
+    a, a2, b, mask, flow = [t.to(device) for t in batch_cpu]
+    model.set_input_nhwc(ops.nchw_to_nhwc(a), ops.nchw_to_nhwc(a2), ops.nchw_to_nhwc(b), mask.contiguous(),
+                         flow.contiguous())
 
-    for _ in range(args.warmup):
+    losses0 = None
+    for i in range(max(1, args.warmup)):
         model.optimize_parameters(hookG, hookD)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    probe = ops.LaunchProbe(DOMINANT_KEY(B))
-    ops.set_launch_probe(probe)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        model.optimize_parameters(hookG, hookD)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    ops.set_launch_probe(None)
-    if world > 1:
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
+        if i == 0:
+            losses0 = model.get_current_losses()  # step 0: what the parity leg checks
+    probes = {k: ops.LaunchProbe(v) for k, v in DOMINANT_KEYS(B).items()}
+    ops.set_launch_probes(list(probes.values()))
+    elapsed = time_steps(model, args.steps, hookG, hookD, world, device)
+    ops.set_launch_probes([])
+    for p in probes.values():
+        p.steps = args.steps
     losses = model.get_current_losses()
 
     frames = B * world * args.steps
@@ -357,19 +438,33 @@ def main():
         "metric": "frames/sec: CycleGAN train step (G+D+flow-warp loss) 256x256",
         "value": round(value, 3), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "fp32" if args.math in ("bf16x6", "fp32") else args.math,
+        "math": {"policy": args.math, "conv": MATH_LABEL[args.math],
+                 "elementwise_and_reductions": "fp32 / fp64 (IN statistics, losses, bias sums)"},
         "data": "synthetic (SURVEY §8d generator; random-init weights, init_type=normal 0.02)",
         "config": {"workload": "C2: CycleGANCon optimize_parameters, resnet_9blocks G + basic PatchGAN D, "
                                "ngf=ndf=64, %dx%d, B_local=%d, pool_size=%d, flow-warp temporal loss" % (S, S, B, args.pool),
-                   "global_batch": B * world, "height": S, "width": S, "parallelism": "dp%d" % world},
+                   "global_batch": B * world, "height": S, "width": S, "parallelism": "dp%d" % world,
+                   "dp_exchange": "RCCL all_reduce of 8 MiB flat-gradient buckets launched during backward" if world > 1 else None},
         "algorithmic_tflops": round(value * TRAIN_TFLOP_PER_FRAME, 2),
-        "step_frac_of_fp32_mfma_peak": round(value * TRAIN_TFLOP_PER_FRAME / (FP32_MFMA_PEAK_TFLOPS * world), 4),
         "final_losses": {k: round(v, 5) for k, v in losses.items()},
     }
     if rank == 0 and not args.no_extras:
-        out["roofline"] = dominant_kernel_roofline(B, probe)
+        rl = {k: conv_roofline(k, p, args.math) for k, p in probes.items()}
+        dom = max(rl, key=lambda k: rl[k]["ms_per_step"] if rl[k] else -1)
+        out["roofline"] = rl[dom]
+        out["roofline_convs"] = rl
         out["inference"] = inference_fps(device)
-    if rank == 0 and world == 1 and not args.no_extras:  # single-GPU context numbers only
+    if rank == 0 and world == 1 and not args.no_extras:
+        # the same step under the round-1 "mixed" policy, separately labelled (not the headline)
+        prev = ops.set_conv_math("mixed")
+        model.optimize_parameters()
+        el = time_steps(model, args.steps, None, None, 1, device)
+        out["mixed_policy"] = {"value": round(B * args.steps / el, 3), "unit": "frames/s",
+                               "ms_per_step": round(el / args.steps * 1e3, 3), "dtype": "mixed",
+                               "math": MATH_LABEL["mixed"], "inference": inference_fps(device)}
+        ops.set_conv_math(prev)
         out["extras"] = {"sintel_inference": sintel_inference_fps(device),
                          "warp_roofline": warp_roofline(device),
                          "raft_corr": corr_volume(device),
@@ -379,7 +474,7 @@ def main():
                          "raft_mogan": raft_inference(device, B=4, H=256, W=256),
                          "mogan_train": mogan_train_fps(device)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline()
+        out["cpu_baseline"], out["parity"] = cpu_baseline_and_parity(init_sd, batch_cpu, losses0)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

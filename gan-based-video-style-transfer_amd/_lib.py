@@ -45,6 +45,7 @@ SIGNATURES = {
     "vst_conv2d_wgrad_ws_bytes": (SZ, [I, I, I, I, I, I, I, I, I, I]),
     "vst_conv2d_wgrad": (I, [P, P, P, P, SZ, I, I, I, I, I, I, I, I, I, I, I, I, I, I, L, L, I, I, P]),
     "vst_debug_set_tiles": (None, [I, I, I]),
+    "vst_conv_plan_fwd": (I, [I, I, I, I, I, I, I, I, I, I, I, P, P]),
     "vst_reflect_fold": (I, [P, P, P, I, I, I, I, I, P]),
     "vst_channel_sum_ws_bytes": (SZ, [L, I]),
     "vst_channel_sum": (I, [P, P, P, L, I, I, I, P]),

@@ -88,6 +88,7 @@ long rk_cp_ld(long P);
 int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* bias, float* y, int N,
                     int H, int W, int C, int Ho, int Wo, int Cop, int R, int S, int st, int padh, int padw,
                     int reflect, int act, float slope, int math, int kind, hipStream_t s);
+void bf_plan(long M, int Cop, int math, int kind, int* kind_out, int* m_split_out);
 
 void rk_tile_geom(int kind, int* bm, int* bn, int* bk, int* slots);
 void rk_nhwc_to_cp(const float* x, float* y, long P, int Cs, int pack, hipStream_t s);

@@ -627,7 +627,9 @@ __global__ void reflect_fold_k(const float* __restrict__ dxp, const float* __res
 // Tile kinds: 0 = 128x128 (8 waves, 64x32 each), 1 = 64x128 (4 waves), 2 = 128x64 (4 waves),
 // 3 = 64x64 (4 waves), 4 = 256x32 (skinny N), 5 = 128x128 (4 waves, 64x64 each).
 enum TileKind { T128x128w8 = 0, T64x128 = 1, T128x64 = 2, T64x64 = 3, T256x32 = 4, T128x128w4 = 5, TAUTO = -1 };
-static int g_tile_override[3] = {TAUTO, TAUTO, TAUTO};
+// Debug tile override (vst_debug_set_tiles): per calling host thread, so concurrent callers on
+// other threads / streams are never affected (the library keeps no other mutable state).
+static thread_local int g_tile_override[3] = {TAUTO, TAUTO, TAUTO};
 
 static int tile_bm(TileKind k) { return k == T64x128 || k == T64x64 ? 64 : (k == T256x32 ? 256 : 128); }
 static int tile_bn(TileKind k) {
@@ -752,6 +754,23 @@ extern "C" void vst_debug_set_tiles(int fprop, int tconv, int wgrad) {
   g_tile_override[0] = fprop;
   g_tile_override[1] = tconv;
   g_tile_override[2] = wgrad;
+}
+
+extern "C" int vst_conv_plan_fwd(int N, int H, int W, int Cx, int Cop, int R, int S, int stride, int padh,
+                                 int padw, int math, int* kind, int* m_split) {
+  VST_REQUIRE(kind && m_split && N > 0 && H > 0 && W > 0 && R > 0 && S > 0 && stride > 0,
+              "conv_plan_fwd: bad args");
+  const int Ho = (H + 2 * padh - R) / stride + 1, Wo = (W + 2 * padw - S) / stride + 1;
+  VST_REQUIRE(Ho > 0 && Wo > 0, "conv_plan_fwd: empty output");
+  *m_split = 0;
+  if (Cop == 4) {
+    *kind = VST_PLAN_SKINNY;
+  } else if (math != VST_MATH_F32 && Cx % 8 == 0) {
+    bf_plan((long)N * Ho * Wo, Cop, math, g_tile_override[0], kind, m_split);
+  } else {
+    *kind = VST_PLAN_RK;
+  }
+  return VST_OK;
 }
 
 static int conv_fwd_impl(const float* x, const float* wp, const void* wsplit, const float* bias, float* y,

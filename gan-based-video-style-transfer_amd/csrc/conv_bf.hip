@@ -416,11 +416,10 @@ int bf_pick(long M, int Nc, int override_kind) {
   return 6;
 }
 
-int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* bias, float* y, int N,
-                    int H, int W, int C, int Ho, int Wo, int Cop, int R, int S, int st, int padh, int padw,
-                    int reflect, int act, float slope, int math, int kind, hipStream_t s) {
-  const int M = N * Ho * Wo, K = R * S * C;
-  const __bf16* ws = reinterpret_cast<const __bf16*>(wsplit);
+// Launch plan of the split-arithmetic forward for an M x Cop output: the tile kind of the main
+// launch and, when the grid is split for wave quantisation, the first pixel row of the tail launch
+// (0 = one launch).  Host-only; also exported through vst_conv_plan_fwd for tests and the bench.
+void bf_plan(long M, int Cop, int math, int kind, int* kind_out, int* m_split_out) {
   int kd = bf_pick(M, Cop, kind);
 #if VST_BF_X6K3
   // x6: the 128x128 three-plane stage pair (96 KB) fits one block per CU; 64x128 tiles fit two
@@ -447,7 +446,18 @@ int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* b
       m_split = (int)(per * VST_NUM_CUS / nt) * 128;
   }
 #endif
-#define VST_BF(BM_, BN_, WM_, WN_, BK_, NP_)                                                       \
+  *kind_out = kd;
+  *m_split_out = m_split;
+}
+
+int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* bias, float* y, int N,
+                    int H, int W, int C, int Ho, int Wo, int Cop, int R, int S, int st, int padh, int padw,
+                    int reflect, int act, float slope, int math, int kind, hipStream_t s) {
+  const int M = N * Ho * Wo, K = R * S * C;
+  const __bf16* ws = reinterpret_cast<const __bf16*>(wsplit);
+  int kd, m_split;
+  bf_plan(M, Cop, math, kind, &kd, &m_split);
+#define VST_BF(BM_, BN_, WM_, WN_, BK_, NP_)                                                     \
   {                                                                                                 \
     using T = bf::Tile<BM_, BN_, WM_, WN_, BK_, NP_>;                                              \
     hipLaunchKernelGGL(bf::conv_fprop_bf_k<T>, dim3(ceil_div(Mend - mb, BM_) * ceil_div(Cop, BN_)),   \

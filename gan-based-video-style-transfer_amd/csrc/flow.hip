@@ -11,6 +11,12 @@
 // the result; the backward scatters with fp32 atomics into the zero-initialised input gradient.
 #include "common.h"
 
+// No a*b+c -> fma contraction in this file: the sample positions, bilinear weights, norms and
+// thresholds are evaluated with the same separately-rounded fp32 operations as PyTorch's CPU
+// grid sampler / norm, so the fb-check mask is bit-identical to the reference's (a contracted
+// multiply-add can move a threshold comparison across a tie).
+#pragma clang fp contract(off)
+
 namespace vst {
 
 struct Bilin {

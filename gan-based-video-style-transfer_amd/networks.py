@@ -209,6 +209,34 @@ class FlatNet(nn.Module):
         y = self.forward_nhwc(_ToNHWC.apply(x, cpad(cin)))
         return _ToNCHW.apply(y, self.output_nc)
 
+    # ---- gradient readiness for the data-parallel exchange (dp.GradExchange.attach) ----------
+    # Every training forward (trainable weights, grad enabled) adds one pending backward pass; the
+    # backward pass that brings the count to zero is the last one of this optimizer phase, so each
+    # layer's slice of flat_grad is final as soon as that pass has written it.  The pass then
+    # reports, layer by layer in reverse parameter order, the lowest flat offset from which every
+    # gradient is final; the exchange launches the RCCL all-reduce of every bucket at or above it
+    # while the rest of the backward is still running.
+    _grad_ready_cb = None
+    _bwd_pending = 0
+
+    def _note_forward(self, train_w):
+        if train_w:
+            self._bwd_pending += 1
+
+    def _bwd_begin(self):
+        """Call at the start of a backward pass; True if this is the phase's last pass and an
+        exchange is attached (the pass must then call _grad_done after each layer)."""
+        self._bwd_pending = max(0, self._bwd_pending - 1)
+        return self._bwd_pending == 0 and self._grad_ready_cb is not None
+
+    def _grad_done(self, mod):
+        base = self.flat_param.data_ptr()
+        off = min((p.data_ptr() - base) // p.element_size() for p in mod.parameters())
+        self._grad_ready_cb(off)
+
+    def _reset_pending(self):
+        self._bwd_pending = 0
+
 
 class _ToNHWC(torch.autograd.Function):
     @staticmethod
@@ -400,6 +428,7 @@ class _GeneratorFn(torch.autograd.Function):
         sv["f"] = (a, out)
         ctx.sv, ctx.net, ctx.P = sv, net, P
         ctx.train_w = anchor.requires_grad
+        net._note_forward(ctx.train_w)
         return out
 
     @staticmethod
@@ -409,6 +438,11 @@ class _GeneratorFn(torch.autograd.Function):
         ngf = net.ngf
         train_w = ctx.train_w
         gout = gout.contiguous()
+        final = train_w and net._bwd_begin()
+
+        def done(mod):  # mod's gradients (and all later layers') are final for this phase
+            if final:
+                net._grad_done(mod)
 
         def wgrad(mod, inp, dy, R, st, pad, mode, db=False):
             if not train_w:
@@ -446,6 +480,7 @@ class _GeneratorFn(torch.autograd.Function):
                     ops.channel_sum(g, f.bias.grad, f.weight.shape[0], accumulate=True)
         else:
             wgrad(f, a, g, 7, 1, 3, "reflect", db=True)
+        done(f)
         ga = dgrad_reflect(g, "f", a.shape[-1], 7, 3, a.shape[1], a.shape[2])
         # up-sampling convT layers
         for i in (1, 0):
@@ -457,6 +492,7 @@ class _GeneratorFn(torch.autograd.Function):
                 ci_t, co_t = m.weight.shape[0], m.weight.shape[1]
                 ops.conv2d_wgrad(dy, a_in, m.weight.grad, None, 3, 3, 2, 1, "zero", ci_t, co_t,
                                  co_t * 9, 9, accumulate=True)
+            done(m)
             kc, _, _ = P[f"u{i}"]
             ga = ops.conv2d_fwd(dy, kc, None, a_in.shape[-1], 3, 3, 2, 1, "zero", role="bwd")
         # residual blocks
@@ -466,9 +502,11 @@ class _GeneratorFn(torch.autograd.Function):
             blk = blocks[i].conv_block
             dv = in_bwd(gh, v, s2, "none", blk[5])
             wgrad(blk[5], uu, dv, 3, 1, 1, "reflect")
+            done(blk[5])
             du = dgrad_reflect(dv, f"b{i}b", uu.shape[-1], 3, 1, uu.shape[1], uu.shape[2])
             dt = in_bwd(du, t, s1, "relu", blk[1])
             wgrad(blk[1], h, dt, 3, 1, 1, "reflect")
+            done(blk[1])
             gh = dgrad_reflect(dt, f"b{i}a", h.shape[-1], 3, 1, h.shape[1], h.shape[2], addend=gh)
         ga = gh
         # down-sampling convs
@@ -477,12 +515,14 @@ class _GeneratorFn(torch.autograd.Function):
             a_in = sv[prev][2]
             dy = in_bwd(ga, y, s, "relu", mod)
             wgrad(mod, a_in, dy, 3, 2, 1, "zero")
+            done(mod)
             ga = dgrad_s2(dy, key, a_in.shape[-1], a_in.shape[1], a_in.shape[2])
         # first conv
         x = sv["x"]
         y, s, _ = sv["c0"]
         dy = in_bwd(ga, y, s, "relu", c0)
         wgrad(c0, x, dy, 7, 1, 3, "reflect")
+        done(c0)
         gx = None
         if ctx.needs_input_grad[0]:
             if "c0kc" in P and x.shape[-1] == 4:
@@ -564,6 +604,7 @@ class _DiscriminatorFn(torch.autograd.Function):
             a = an
         ctx.saved, ctx.net, ctx.P = saved, net, P
         ctx.train_w = anchor.requires_grad
+        net._note_forward(ctx.train_w)
         return a
 
     @staticmethod
@@ -573,6 +614,7 @@ class _DiscriminatorFn(torch.autograd.Function):
         L = len(convs)
         g = gout.contiguous()
         gx = None
+        final = ctx.train_w and net._bwd_begin()
         for i in reversed(range(L)):
             a_in, y, s, an = saved[i]
             m = convs[i]
@@ -589,6 +631,8 @@ class _DiscriminatorFn(torch.autograd.Function):
                 ops.conv2d_wgrad(a_in, dy, m.weight.grad,
                                  m.bias.grad if (m.bias is not None and not has_in) else None,
                                  4, 4, st, 1, "zero", co, ci, ci * 16, 16, accumulate=True)
+                if final:
+                    net._grad_done(m)
             if i > 0 or ctx.needs_input_grad[0]:
                 ikf = net._ikf[i]
                 if ikf is not None:

@@ -85,11 +85,12 @@ def weight_pack(w, mode, transposed=False):
 
 # --------------------------------------------------------------------------------------- conv
 class LaunchProbe:
-    """Measurement hook (bench.py): HIP events around every vst_conv2d_fwd launch of one shape
-    (N, H, W, Cx, Cop, R, stride, pad, pad_mode), recorded on the stream the kernel is launched on."""
+    """Measurement hook (bench.py): HIP events around every launch of one conv op ("fwd" =
+    vst_conv2d_fwd, "wgrad" = vst_conv2d_wgrad) of one shape (N, H, W, Cx, Cop, R, stride, pad,
+    pad_mode), recorded on the stream the op is launched on."""
 
     def __init__(self, key):
-        self.key, self.events = key, []
+        self.key, self.events, self.steps = key, [], 1
 
     def mean_ms(self):
         torch.cuda.synchronize()
@@ -97,12 +98,28 @@ class LaunchProbe:
         return sum(t) / len(t) if t else float("nan")
 
 
-_probe = None
+_probes = []
 
 
-def set_launch_probe(probe):
-    global _probe
-    _probe = probe
+def set_launch_probes(probes):
+    global _probes
+    _probes = list(probes)
+
+
+def _probe_begin(op, key):
+    for p in _probes:
+        if p.key == (op, key):
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
+            return p, ev
+    return None
+
+
+def _probe_end(h):
+    if h is not None:
+        p, ev = h
+        ev[1].record()
+        p.events.append(ev)
 
 
 def conv2d_fwd(x, wp, bias, cop, R, S, stride, pad, pad_mode="zero", act="none", slope=0.0,
@@ -112,16 +129,11 @@ def conv2d_fwd(x, wp, bias, cop, R, S, stride, pad, pad_mode="zero", act="none",
     Ho = (H + 2 * pad - R) // stride + 1
     Wo = (W + 2 * pad - S) // stride + 1
     y = out if out is not None else torch.empty((N, Ho, Wo, cop), device=x.device)
-    probe = _probe if (_probe is not None and _probe.key == (N, H, W, Cx, cop, R, stride, pad, pad_mode)) else None
-    if probe is not None:
-        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-        ev[0].record()
+    h = _probe_begin("fwd", (N, H, W, Cx, cop, R, stride, pad, pad_mode)) if _probes else None
     _call("vst_conv2d_fwd", _p(x), _p(wp), _p(getattr(wp, "vst_split", None)), _p(bias), _p(y), N, H,
           W, Cx, cop, R, S, stride, pad,
           PAD[pad_mode], ACT[act], float(slope), _math(role), _stream())
-    if probe is not None:
-        ev[1].record()
-        probe.events.append(ev)
+    _probe_end(h)
     return y
 
 
@@ -146,26 +158,29 @@ def conv2d_wgrad(x, dy, dw, db, R, S, stride, pad, pad_mode, co, ci, so, si, acc
     _, Ho, Wo, Cyp = dy.shape
     nbytes = lib().vst_conv2d_wgrad_ws_bytes(N, H, W, Cx, Ho, Wo, Cyp, R, S, stride)
     ws = torch.empty((nbytes + 3) // 4, device=x.device)
+    h = _probe_begin("wgrad", (N, H, W, Cx, Cyp, R, stride, pad, pad_mode)) if _probes else None
     _call("vst_conv2d_wgrad", _p(x), _p(dy), _p(dw), _p(ws), nbytes, N, H, W, Cx, Ho, Wo,
           Cyp, R, S, stride, pad, PAD[pad_mode], co, ci, so, si, 1 if accumulate else 0, _math(role),
           _stream())
+    _probe_end(h)
     if db is not None:
         channel_sum(dy, db, co, accumulate)
 
 
-# Conv GEMM arithmetic by role (see VST_MATH_* in include/vst_hip.h).  Forward convs run the
-# fp32-equivalent three-plane bf16 split: the forward rounding decides ReLU masks, and a mask flipped
-# by a 1e-5 perturbation changes which gradients exist (measured on the reference-golden G: bf16x3
-# forward => 6e-3 input-grad error, bf16x6 forward => 1e-7).  Data/weight gradients are linear in
-# their inputs, so bf16x3 keeps them at ~1e-5 relative.  VST_CONV_MATH overrides both roles:
-# fp32 | bf16x3 | bf16x6 | mixed (default).
-# Inference-only forwards (no gradient will be taken: forward_eval, the stylised frames) need no
-# mask stability and run bf16x3 (output error ~4e-5 relative vs the 1e-3 north_star bound).
+# Conv GEMM arithmetic by role (see VST_MATH_* in include/vst_hip.h).  The default policy, bf16x6,
+# runs EVERY conv — training forwards, data gradients, weight gradients, inference — with the
+# fp32-equivalent three-plane bf16 split (dropped product terms <= 2^-24 relative).  "mixed" (the
+# round-1 default) keeps the forwards at bf16x6 — the forward rounding decides ReLU masks, and a mask
+# flipped by a 1e-5 perturbation changes which gradients exist (measured on the reference-golden G:
+# bf16x3 forward => 6e-3 input-grad error, bf16x6 forward => 1e-7) — but runs data/weight gradients
+# and inference-only forwards at bf16x3 (~2^-16 relative products, ~1e-5 relative gradient error):
+# narrower than fp32, so it is a separately labelled option.  VST_CONV_MATH / set_conv_math:
+# bf16x6 (default) | mixed | fp32 (v_mfma_f32_32x32x2_f32) | bf16x3.
 _POLICIES = {"mixed": {"fwd": "bf16x6", "infer": "bf16x3", "bwd": "bf16x3"},
              "fp32": {"fwd": "fp32", "infer": "fp32", "bwd": "fp32"},
              "bf16x3": {"fwd": "bf16x3", "infer": "bf16x3", "bwd": "bf16x3"},
              "bf16x6": {"fwd": "bf16x6", "infer": "bf16x6", "bwd": "bf16x6"}}
-_policy_name = os.environ.get("VST_CONV_MATH", "mixed")
+_policy_name = os.environ.get("VST_CONV_MATH", "bf16x6")
 if _policy_name not in _POLICIES:
     raise ValueError("VST_CONV_MATH must be one of %s" % sorted(_POLICIES))
 
@@ -189,7 +204,26 @@ def _math(role):
 
 
 def debug_set_tiles(fprop=-1, tconv=-1, wgrad=-1):
+    """Force GEMM tiles for calls from this host thread (vst_debug_set_tiles; -1 = automatic)."""
     lib().vst_debug_set_tiles(int(fprop), int(tconv), int(wgrad))
+
+
+PLAN_RK, PLAN_SKINNY = -1, -2
+TILE_NAMES = {0: "128x128 (8 waves of 64x32)", 1: "128x64", 2: "128x128 (4 waves of 64x64)", 3: "64x128",
+              4: "128x128 BK64", 5: "128x64 BK64", 6: "64x64", 7: "256x128 (8 waves of 64x64)", 8: "64x64 BK64",
+              PLAN_RK: "fp32 [row][k] kernel", PLAN_SKINNY: "VALU skinny kernel"}
+
+
+def conv_plan_fwd(N, H, W, Cx, Cop, R, S, stride, pad_h, pad_w, math):
+    """Host-only query (vst_conv_plan_fwd): (tile kind, tail-split row) vst_conv2d_fwd would use for
+    this shape under `math` ('fp32' | 'bf16x3' | 'bf16x6', or a role of the current policy)."""
+    import ctypes
+    from ._lib import MATH_MODES
+    m = MATH_MODES[math] if math in MATH_MODES else _math(math)
+    kind, ms = ctypes.c_int(0), ctypes.c_int(0)
+    _call("vst_conv_plan_fwd", N, H, W, Cx, Cop, R, S, stride, pad_h, pad_w, m, ctypes.addressof(kind),
+          ctypes.addressof(ms))
+    return kind.value, ms.value
 
 
 def channel_sum(x, db, cl, accumulate=True):

@@ -133,11 +133,21 @@ int vst_conv2d_wgrad(const float* x, const float* dy, float* dw, float* ws, size
                      int H, int W, int Cx, int Ho, int Wo, int Cyp, int R, int S, int stride,
                      int pad, int pad_mode, int Co, int Ci, long so, long si, int accumulate,
                      int math, void* stream);
-/* Debug/benchmark only: force the GEMM tile of fprop / tconv / wgrad (-1 = automatic).
- * fprop/tconv: 0 = 128x128 (8 waves), 1 = 64x128, 2 = 128x64, 3 = 64x64, 4 = 128x128 64-deep K.
+/* Debug/benchmark only: force the GEMM tile of fprop / tconv / wgrad (-1 = automatic) for calls
+ * made from the CALLING host thread (thread-local; other threads keep automatic selection).
+ * fprop/tconv: 0 = 128x128 (8 waves), 1 = 64x128, 2 = 128x64, 3 = 64x64, 4 = 128x128 64-deep K,
+ * (split-arithmetic fprop only) 7 = 256x128.
  * wgrad: the same kinds 0..4 on the channel-major (stride-1) path; 8 + k forces the k-major
  * legacy wgrad kernel with tile k (0..3, 4 = 256x32). */
 void vst_debug_set_tiles(int fprop, int tconv, int wgrad);
+/* Host-only planning query (no launch, no device needed): the kernel vst_conv2d_fwd would run for
+ * this shape and `math` on this thread.  *kind = split-arithmetic tile kind (0..8, see
+ * vst_debug_set_tiles; 7 = 256x128), VST_PLAN_RK (fp32 [row][k] kernel) or VST_PLAN_SKINNY
+ * (<= 4 output channels, VALU); *m_split = first output-pixel row of the wave-quantisation tail
+ * launch (64x64 tiles), 0 when the grid runs as one launch. */
+enum { VST_PLAN_RK = -1, VST_PLAN_SKINNY = -2 };
+int vst_conv_plan_fwd(int N, int H, int W, int Cx, int Cop, int R, int S, int stride, int pad_h,
+                      int pad_w, int math, int* kind, int* m_split);
 /* db[c] (+)= sum over NHW pixels of x[p][c] for c < Cl (channel stride Cs); bias gradient of a layer
  * whose output gradient is x.  ws: vst_channel_sum_ws_bytes bytes; fixed-order (deterministic). */
 size_t vst_channel_sum_ws_bytes(long NHW, int Cs);

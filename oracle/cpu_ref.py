@@ -171,7 +171,9 @@ class RefCycleGANCon:
         self.real_A, self.real_A2, self.real_B, self.mask, self.flow = (
             real_A, real_A2, real_B, mask, flow)
 
-    def optimize_parameters(self):
+    def optimize_parameters(self, grad_hook_G=None, grad_hook_D=None):
+        """grad_hook_*(nets): called between backward and the optimizer step (parity tests read the
+        accumulated gradients there, like CycleGANModel.optimize_parameters' hooks)."""
         # forward (:133-139)
         self.fake_B = self.G_A(self.real_A)
         self.fake_B2 = self.G_A(self.real_A2)
@@ -194,6 +196,8 @@ class RefCycleGANCon:
         self.loss_G = (self.loss_G_A + self.loss_G_B + self.loss_cycle_A + self.loss_cycle_B
                        + self.loss_idt_A + self.loss_idt_B + self.loss_G_T)
         self.loss_G.backward()
+        if grad_hook_G is not None:
+            grad_hook_G([self.G_A, self.G_B])
         self.opt_G.step()
         # D step (:141-166, 226-232)
         for p in list(self.D_A.parameters()) + list(self.D_B.parameters()):
@@ -201,6 +205,8 @@ class RefCycleGANCon:
         self.opt_D.zero_grad()
         self.loss_D_A = self._backward_D(self.D_A, self.real_B, self.fake_B)
         self.loss_D_B = self._backward_D(self.D_B, self.real_A, self.fake_A)
+        if grad_hook_D is not None:
+            grad_hook_D([self.D_A, self.D_B])
         self.opt_D.step()
 
     @staticmethod

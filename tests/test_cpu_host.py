@@ -133,3 +133,31 @@ def test_raft_module_tree_and_no_cpu_fallback():
     x = torch.zeros(1, 3, 64, 64)
     with pytest.raises(RuntimeError):
         m(x, x, iters=1, test_mode=True)
+
+
+def test_conv_planner_picks_production_kernels():
+    """The host planner (vst_conv_plan_fwd, no device needed) routes the train step's dominant
+    shapes to the kernels the GPU parity tests force and check: the N=8 ResnetBlock forward under
+    bf16x6 -> 256x128 tiles (kind 7, one launch); its stride-1 data gradient over the padded frame
+    (66x66, zero pad 2) under bf16x3 -> 128x128 tiles + a 64x64 wave-quantisation tail launch
+    (546 = 2 x 256 + 34 blocks); fp32 -> the [row][k] kernel; 4 output channels -> VALU."""
+    import gbvst
+    from gbvst import ops
+    gbvst._lib.load()
+    assert ops.conv_plan_fwd(8, 64, 64, 256, 256, 3, 3, 1, 1, 1, "bf16x6") == (7, 0)
+    kind, ms = ops.conv_plan_fwd(8, 64, 64, 256, 256, 3, 3, 1, 2, 2, "bf16x3")
+    assert kind == 0 and ms == 2 * 256 // 2 * 128 and 0 < ms < 8 * 66 * 66
+    assert ops.conv_plan_fwd(8, 64, 64, 256, 256, 3, 3, 1, 1, 1, "fp32") == (ops.PLAN_RK, 0)
+    assert ops.conv_plan_fwd(2, 32, 32, 64, 4, 7, 7, 1, 3, 3, "bf16x6")[0] == ops.PLAN_SKINNY
+    ops.debug_set_tiles(7, -1, -1)
+    try:
+        assert ops.conv_plan_fwd(2, 12, 10, 32, 32, 3, 3, 1, 1, 1, "bf16x3") == (7, 0)
+        # the override is thread-local: another host thread still plans automatically
+        import threading
+        out = []
+        t = threading.Thread(target=lambda: out.append(ops.conv_plan_fwd(2, 12, 10, 32, 32, 3, 3, 1, 1, 1, "bf16x3")))
+        t.start()
+        t.join()
+        assert out[0][0] != 7
+    finally:
+        ops.debug_set_tiles(-1, -1, -1)

@@ -179,3 +179,107 @@ def test_stargan_dp_equivalence_gloo_world2():
         assert torch.allclose(res[0][i], res[1][i])
         err = (res[0][i] - full).abs().max() / full.abs().max()
         assert err < 1e-5, (i, err)
+
+
+class _LayeredFlat:
+    """Stand-in for a FlatNet's last backward pass of a phase: layers write their gradient slices
+    in reverse parameter order and report readiness exactly like networks._GeneratorFn.backward
+    (net._grad_done(layer) -> _grad_ready_cb(lowest offset of that layer))."""
+
+    def __init__(self, sizes):
+        self.sizes = sizes
+        self.offsets = [sum(sizes[:i]) for i in range(len(sizes))]
+        n = sum(sizes)
+        self.flat_param = torch.zeros(n)
+        self.flat_grad = torch.zeros(n)
+        self._grad_ready_cb = None
+        self.pending_reset = 0
+
+    def _reset_pending(self):
+        self.pending_reset += 1
+
+    def backward(self, rank, log):
+        for i in reversed(range(len(self.sizes))):
+            lo = self.offsets[i]
+            self.flat_grad[lo:lo + self.sizes[i]] = (torch.arange(self.sizes[i], dtype=torch.float32) + i) * (rank + 1)
+            log.append(("layer", i))
+            if self._grad_ready_cb is not None:
+                self._grad_ready_cb(lo)
+        log.append(("end", -1))
+
+
+def _overlap_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(1)
+    from gbvst import dp
+    net = _LayeredFlat([1000] * 10)
+    ex = dp.GradExchange(world, bucket_bytes=2500 * 4).attach([net])
+    st = ex._state(net)
+    log = []
+    orig = ex._on_ready
+
+    def spy(s, off):  # record which buckets were in flight when each layer finished
+        orig(s, off)
+        log.append(("launched", s.next))
+    ex._on_ready = spy
+    net.backward(rank, log)
+    early = list(st.launch_log)
+    ex([net])
+    expect = torch.cat([(torch.arange(1000, dtype=torch.float32) + i) for i in range(10)]) * (
+        sum(r + 1 for r in range(world)) / world)
+    q.put((rank, early, log, bool(torch.allclose(net.flat_grad, expect)), net.pending_reset, st.last_log))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_grad_exchange_overlaps_backward_gloo_world2():
+    """Buckets (cut from the end of the flat buffer) are all-reduced DURING the last backward pass,
+    each as soon as the layers covering it are written — before the pass ends — and the join then
+    yields the exact average."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_overlap_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, early, log, ok, resets, last in res:
+        # buckets [7500,10000) [5000,7500) [2500,5000) [0,2500) become final after layers 7, 5, 2, 0
+        assert early == [(0, 7000), (1, 5000), (2, 2000), (3, 0)], early
+        assert last == early
+        launched_after = {i: n for (kind, i), (_, n) in zip(log[0:-1:2], log[1::2]) if kind == "layer"}
+        assert launched_after[9] == 0 and launched_after[7] == 1 and launched_after[5] == 2
+        assert launched_after[2] == 3 and launched_after[0] == 4
+        assert log[-1] == ("end", -1)
+        assert ok and resets == 1
+
+
+def test_generator_reports_layers_in_reverse_flat_order():
+    """The real generator / discriminator backward report every layer, last to first, with
+    strictly decreasing flat offsets that end at 0 (CPU: offsets only, no kernels)."""
+    from gbvst import networks
+    G = networks.define_G(3, 3, 8, "resnet_9blocks", "instance", False, "normal", 0.02, [])
+    c0, d, blocks, u, f = G._layers()
+    order = [f, u[1], u[0]]
+    for b in reversed(blocks):
+        order += [b.conv_block[5], b.conv_block[1]]
+    order += [d[1], d[0], c0]
+    offs = []
+    G._grad_ready_cb = offs.append
+    for m in order:
+        G._grad_done(m)
+    assert offs == sorted(offs, reverse=True) and len(set(offs)) == len(offs) and offs[-1] == 0
+    assert G.flat_grad.numel() - offs[0] == sum(p.numel() for p in f.parameters())
+    D = networks.define_D(3, 8, "basic", 3, "instance", "normal", 0.02, [])
+    offs = []
+    D._grad_ready_cb = offs.append
+    for m in reversed(D._convs()):
+        D._grad_done(m)
+    assert offs == sorted(offs, reverse=True) and offs[-1] == 0

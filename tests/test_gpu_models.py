@@ -156,3 +156,109 @@ def test_pool_and_plain_step_run(gb, golden):
         m.set_input_fc2(data)
         m.optimize_parameters()
     assert all(np.isfinite(v) for v in m.get_current_losses().values())
+
+
+# ------------------------------------------------------------------------------------------------
+# Full-size C2 step (ngf=ndf=64, 256x256, B=4): the production kernel instantiations of the
+# metric's train step — the batched N=8 / N=12 generator calls (256x128 channel-slice-major bf16x6
+# forward tiles, the 128x128 + 64x64-tail bf16x3 padded-frame data gradients, the wide channel-major
+# weight gradients) — against the CPU oracle on identical counter-PRNG weights and inputs.
+FULL_B, FULL_S = 4, 256
+_NET_SEEDS = {"G_A": 301, "G_B": 302, "D_A": 303, "D_B": 304}
+# biases that feed an InstanceNorm: their exact gradient is 0 and both sides hold rounding noise
+_REAL_BIAS = {"G": ("model.26.bias",), "D": ("model.0.bias", "model.11.bias")}
+
+
+def _full_weights():
+    from oracle import cpu_ref, prng
+    shapes = {"G": cpu_ref.state_shapes(cpu_ref.RefResnetGenerator(3, 3, 64, 9)),
+              "D": cpu_ref.state_shapes(cpu_ref.RefNLayerDiscriminator(3, 64))}
+    return {n: prng.init_state_dict(shapes[n[0]], base_seed=s) for n, s in _NET_SEEDS.items()}
+
+
+def _full_inputs():
+    from oracle import cpu_ref, prng
+    a, a2, b, mask, flow = cpu_ref.synthetic_batch(FULL_B, FULL_S, FULL_S, seed=4321)
+    probe = torch.from_numpy(prng.uniform_f32(4322, (1, 3, FULL_S, FULL_S), -1, 1))
+    return (a, a2, b, mask, flow), probe
+
+
+def _grab(store):
+    def hook(nets):
+        for net in nets:
+            for k, p in net.named_parameters():
+                store.setdefault(id(net), {})[k] = p.grad.detach().double().cpu().clone()
+    return hook
+
+
+def _oracle_full_step(dtype):
+    from oracle import cpu_ref
+    m = cpu_ref.RefCycleGANCon(ngf=64, ndf=64)
+    W = _full_weights()
+    for name, net in m.nets().items():
+        cpu_ref.load_np_state(net, W[name])
+        net.to(dtype)
+    m.opt_G = torch.optim.Adam(list(m.G_A.parameters()) + list(m.G_B.parameters()), lr=2e-4, betas=(0.5, 0.999))
+    m.opt_D = torch.optim.Adam(list(m.D_A.parameters()) + list(m.D_B.parameters()), lr=2e-4, betas=(0.5, 0.999))
+    data, probe = _full_inputs()
+    m.set_input_fc2(*(t.to(dtype) for t in data))
+    grads = {}
+    m.optimize_parameters(_grab(grads), _grab(grads))
+    losses = m.get_current_losses()
+    with torch.no_grad():
+        out = m.G_A(probe.to(dtype)).double()
+    named = {n: grads[id(net)] for n, net in m.nets().items()}
+    return losses, named, out
+
+
+@pytest.fixture(scope="module")
+def full_oracle(golden):
+    """fp32 oracle run (the reference arithmetic) live, plus the fp64-vs-fp32 band of the same
+    step from tests/golden/full_step_band.npz (oracle/gen_full_step_band.py; the fp64 step takes
+    minutes on a CPU): the spread the reference's own rounding gives each quantity."""
+    return _oracle_full_step(torch.float32), golden("full_step_band")
+
+
+def _norm_rel(a, b):
+    return float((a - b).norm() / (b.norm() + 1e-30))
+
+
+@pytest.mark.timeout(900)
+def test_full_size_train_step_vs_oracle(gb, full_oracle, train_math):
+    """One CycleGANCon optimize_parameters() at the C2 config: every step-0 loss within 1e-3
+    relative (north_star); every parameter gradient of G_A/G_B (G step) and D_A/D_B (D step)
+    within max(2e-3, 3x the fp64-vs-fp32 oracle band) norm-wise; G_A(probe) after the Adam update
+    within max(1e-3, 3x the fp64-vs-fp32 deviation)."""
+    from gbvst import ops
+    from gbvst.cycle_gan_model import CycleGANModel
+    from gbvst.options import default_opt
+    # the batched passes must reach the production instantiations under this policy
+    if ops.get_conv_math() in ("mixed", "bf16x6"):
+        assert ops.conv_plan_fwd(2 * FULL_B, 64, 64, 256, 256, 3, 3, 1, 1, 1, "fwd")[0] == 7
+    (l32, g32, p32), band = full_oracle
+    m = CycleGANModel(default_opt(True, pool_size=0, gpu_ids=[0]))
+    W = _full_weights()
+    for name in _NET_SEEDS:
+        getattr(m, "net" + name).load_state_dict({k: torch.from_numpy(v) for k, v in W[name].items()})
+    data, probe = _full_inputs()
+    m.set_input_fc2((data[0], data[1], data[2], None, data[3], data[4]))
+    grads = {}
+    m.optimize_parameters(_grab(grads), _grab(grads))
+    torch.cuda.synchronize()
+    cur = m.get_current_losses()
+    for k, ref in l32.items():
+        assert abs(cur[k] - ref) <= 1e-3 * abs(ref), (k, cur[k], ref)
+    for name in _NET_SEEDS:
+        got = grads[id(getattr(m, "net" + name))]
+        for k, ref in g32[name].items():
+            if k.endswith("bias") and k not in _REAL_BIAS[name[0]]:
+                assert got[k].abs().max().item() < 1e-3, (name, k)
+                continue
+            b = float(band[f"band_{name}_{k}"])
+            rel = _norm_rel(got[k], ref)
+            assert rel <= max(2e-3, 3 * b), (name, k, rel, b)
+    with torch.no_grad():
+        out = m.forward_eval(probe).double().cpu()
+    dev64 = float(band["probe_dev64"])
+    err = (out - p32).abs().max().item()
+    assert err <= max(1e-3, 3 * dev64), (err, dev64)

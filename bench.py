@@ -45,6 +45,7 @@ FP32_MFMA_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32
 BF16_MFMA_PEAK_TFLOPS = 2500.0     # dense bf16 (v_mfma_f32_32x32x16_bf16); bf16x6 = 6 products / fp32 MAC
 HBM_PEAK_GBS = 8000.0              # MI355X_MICROARCH.md: HBM3E 8 TB/s spec (~6.3 achievable)
 TRAIN_TFLOP_PER_FRAME = 2.1753     # SURVEY §8d / BASELINE.md: CycleGANCon step conv FLOPs @256^2
+TRAIN_TFLOP_PER_FRAME_C3 = 14.831  # the same step's G/D conv FLOPs @1024x436 (VGG not counted)
 G_GFLOP_PER_FRAME = 99.10          # ResnetGenerator fwd @256^2
 
 
@@ -273,6 +274,32 @@ def mogan_train_fps(device, B=4, S=256, pairs=2):
             "batch": B, "value": round(B / dt, 2), "unit": "frames/s", "ms_per_step": round(dt * 1e3, 3)}
 
 
+def c3_train_fps(device, B=1, H=436, W=1024, steps=4):
+    """Config C3: CycleGANCon step + VGG-19 content / Gram loss on fake_B2
+    (gbvst.cycle_gan_vgg_model) on synthetic Sintel-size frame pairs 1x3x436x1024 (flow x4), random-init
+    generator / discriminator weights, seeded VGG-19 (no pretrained weights offline); frames/s of
+    optimize_parameters under the headline policy."""
+    from gbvst import ops
+    from gbvst.cycle_gan_vgg_model import CycleGANVGGModel
+    from gbvst.options import default_opt
+    m = CycleGANVGGModel(default_opt(True, model="cycle_gan_vgg", pool_size=50, gpu_ids=[device.index or 0]))
+    a, a2, b, mask, flow = synthetic_batch(B, H, W, seed=4360, device=device)
+    m.set_input_nhwc(ops.nchw_to_nhwc(a), ops.nchw_to_nhwc(a2), ops.nchw_to_nhwc(b), mask.contiguous(),
+                     (flow * 4.0).contiguous())
+    for _ in range(2):
+        m.optimize_parameters()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        m.optimize_parameters()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    return {"metric": "C3 train step frames/s %dx%d (CycleGANCon + flow-warp + VGG-19 content/Gram loss)" % (W, H),
+            "batch": B, "value": round(B / dt, 3), "unit": "frames/s", "ms_per_step": round(dt * 1e3, 2),
+            "tflops_conv_G_D": round(TRAIN_TFLOP_PER_FRAME_C3 / dt, 2),
+            "losses": {k: round(v, 4) for k, v in m.get_current_losses().items()}}
+
+
 def inference_fps(device, B=16, reps=10):
     from gbvst import networks
     G = networks.define_G(3, 3, 64, "resnet_9blocks", "instance", False, "normal", 0.02,
@@ -465,7 +492,8 @@ def main():
                                "ms_per_step": round(el / args.steps * 1e3, 3), "dtype": "mixed",
                                "math": MATH_LABEL["mixed"], "inference": inference_fps(device)}
         ops.set_conv_math(prev)
-        out["extras"] = {"sintel_inference": sintel_inference_fps(device),
+        out["extras"] = {"c3_train": c3_train_fps(device),
+                         "sintel_inference": sintel_inference_fps(device),
                          "warp_roofline": warp_roofline(device),
                          "raft_corr": corr_volume(device),
                          "johnson_train": johnson_train_fps(device),

@@ -45,7 +45,7 @@ SIGNATURES = {
     "vst_conv2d_wgrad_ws_bytes": (SZ, [I, I, I, I, I, I, I, I, I, I]),
     "vst_conv2d_wgrad": (I, [P, P, P, P, SZ, I, I, I, I, I, I, I, I, I, I, I, I, I, I, L, L, I, I, P]),
     "vst_debug_set_tiles": (None, [I, I, I]),
-    "vst_conv_plan_fwd": (I, [I, I, I, I, I, I, I, I, I, I, I, P, P]),
+    "vst_conv_plan_fwd": (I, [I, I, I, I, I, I, I, I, I, I, I, P, P, P]),
     "vst_reflect_fold": (I, [P, P, P, I, I, I, I, I, P]),
     "vst_channel_sum_ws_bytes": (SZ, [L, I]),
     "vst_channel_sum": (I, [P, P, P, L, I, I, I, P]),
@@ -139,6 +139,8 @@ def build(force=False, verbose=False, out=None, defines=()):
         objs.append(o)
         cmd = [HIPCC, "-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-munsafe-fp-atomics",
                "-Wall", "-Wno-unused-function"] + ["-D" + d for d in defines] + ["-c", s, "-o", o]
+        if out is not None:  # developer variant builds only: extra compiler flags
+            cmd[1:1] = os.environ.get("VST_VARIANT_HIPCC_FLAGS", "").split()
         procs.append((cmd, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
     for cmd, p in procs:
         out, _ = p.communicate()

@@ -660,6 +660,8 @@ struct WgradPlan {
   int Mw, nsplit, chunk;
   TileKind tile;
   bool trans;        // channel-major operand copies + conv_wgrad_rk_k (stride 1, Wo % 4 == 0)
+  bool bfk;          // trans, on the split-bf16 kernel (conv_wgrad_bf_k; x6, Wo % 8 == 0): dy as
+                     // pre-split bf16 planes, `tile` is then a conv_bf tile kind
   int pad;           // trans: the border the padded x copy carries (derived from H -> Ho)
   long xt_floats;    // workspace floats after the slabs: xt [Cx][N*Hp*Wp] then dyt [Cyp][P]
   long dyt_floats;
@@ -690,12 +692,16 @@ static int pick_splits(int tiles, int slots, int max_ns, int min_ns = 1) {
 #ifndef VST_WG_BIG
 #define VST_WG_BIG 5  // rk tile kind of the wide (Cyp > 64, Mw >= 1024) weight gradients
 #endif
+#ifndef VST_WG_BF
+#define VST_WG_BF 1   // x6 weight gradients on the split-bf16 kernel (conv_wgrad_bf_k)
+#endif
 
 static WgradPlan plan_wgrad(int N, int H, int W, int Ho, int Wo, int Cx, int Cyp, int R, int S,
-                            int stride) {
+                            int stride, int math) {
   WgradPlan p;
   p.Mw = R * S * Cx;
   p.trans = false;
+  p.bfk = false;
   p.pad = 0;
   p.xt_floats = p.dyt_floats = 0;
   const int P = N * Ho * Wo;
@@ -705,13 +711,34 @@ static WgradPlan plan_wgrad(int N, int H, int W, int Ho, int Wo, int Cx, int Cyp
   // stride 2: the pad is not recoverable from the shapes; the padded copy is sized for pad <= R - 1
   // (checked at the call) and its rows are column-phase split, which needs W + 2 pad even
   const bool s2 = stride == 2 && W % 2 == 0;
+  if (Cyp > 4 && (s1 || s2) && Wo % 8 == 0 && ov < 0 && math == VST_MATH_BF16X6 && VST_WG_BF) {
+    // x6: the split-bf16 weight-gradient kernel (conv_bf.hip), 256x128 tiles for the wide layers
+    p.trans = p.bfk = true;
+    p.pad = s1 ? pd2 / 2 : -1;
+    const int kind = Cyp > 64 ? (p.Mw >= 1024 ? 7 : 3) : (p.Mw >= 1024 ? 1 : 8);
+    p.tile = (TileKind)kind;
+    int bm, bn, bk, slots;
+    bf_wgrad_geom(kind, math, &bm, &bn, &bk, &slots);
+    const int tiles = ceil_div(p.Mw, bm) * ceil_div(Cyp, bn);
+    const int ns = pick_splits(tiles, slots, ceil_div(P, 8 * bk) < 256 ? ceil_div(P, 8 * bk) : 256,
+                               ceil_div(P, WGRAD_CHUNK_MAX));
+    p.chunk = ceil_div(ceil_div(P, ns), bk) * bk;
+    p.nsplit = ceil_div(P, p.chunk);
+    const int pmax = s1 ? p.pad : (R > S ? R : S) - 1;
+    p.xt_floats = rk_cp_ld((long)N * (H + 2 * pmax) * (W + 2 * pmax)) * Cx;  // padded fp32 image
+    p.dyt_floats = (rk_cp_ld(P) * Cyp * 3 + 1) / 2;                           // 3 bf16 planes
+    return p;
+  }
   if (Cyp > 4 && (s1 || s2) && Wo % 4 == 0 && ov < 8) {
     p.trans = true;
     p.pad = s1 ? pd2 / 2 : -1;
-    int kind = (ov >= 0 && ov <= 6) ? ov : (Cyp <= 64 ? (p.Mw >= 1024 ? 2 : 3) : (p.Mw >= 1024 ? VST_WG_BIG : 1));
+    // wide layers: 4 waves of 64x64 (two blocks per CU) under x3; under x6 the 128x128 image fits
+    // one block per CU, so the 8-wave kind keeps two waves per SIMD
+    const int wide = math == VST_MATH_BF16X6 ? 0 : VST_WG_BIG;
+    int kind = (ov >= 0 && ov <= 6) ? ov : (Cyp <= 64 ? (p.Mw >= 1024 ? 2 : 3) : (p.Mw >= 1024 ? wide : 1));
     p.tile = (TileKind)kind;
     int bm, bn, bk, slots;
-    rk_tile_geom(kind, &bm, &bn, &bk, &slots);
+    rk_tile_geom(kind, math, &bm, &bn, &bk, &slots);
     const int tiles = ceil_div(p.Mw, bm) * ceil_div(Cyp, bn);
     const int ns = pick_splits(tiles, slots, ceil_div(P, 8 * bk) < 256 ? ceil_div(P, 8 * bk) : 256,
                                ceil_div(P, WGRAD_CHUNK_MAX));
@@ -757,16 +784,17 @@ extern "C" void vst_debug_set_tiles(int fprop, int tconv, int wgrad) {
 }
 
 extern "C" int vst_conv_plan_fwd(int N, int H, int W, int Cx, int Cop, int R, int S, int stride, int padh,
-                                 int padw, int math, int* kind, int* m_split) {
-  VST_REQUIRE(kind && m_split && N > 0 && H > 0 && W > 0 && R > 0 && S > 0 && stride > 0,
+                                 int padw, int math, int* kind, int* m_split, int* tail_kind) {
+  VST_REQUIRE(kind && m_split && tail_kind && N > 0 && H > 0 && W > 0 && R > 0 && S > 0 && stride > 0,
               "conv_plan_fwd: bad args");
   const int Ho = (H + 2 * padh - R) / stride + 1, Wo = (W + 2 * padw - S) / stride + 1;
   VST_REQUIRE(Ho > 0 && Wo > 0, "conv_plan_fwd: empty output");
   *m_split = 0;
+  *tail_kind = -1;
   if (Cop == 4) {
     *kind = VST_PLAN_SKINNY;
   } else if (math != VST_MATH_F32 && Cx % 8 == 0) {
-    bf_plan((long)N * Ho * Wo, Cop, math, g_tile_override[0], kind, m_split);
+    bf_plan((long)N * Ho * Wo, Cop, math, g_tile_override[0], kind, m_split, tail_kind);
   } else {
     *kind = VST_PLAN_RK;
   }
@@ -854,8 +882,13 @@ static size_t wgrad_ws_floats(const WgradPlan& p, int Cyp) {
 
 extern "C" size_t vst_conv2d_wgrad_ws_bytes(int N, int H, int W, int Cx, int Ho, int Wo, int Cyp,
                                             int R, int S, int stride) {
-  const WgradPlan p = plan_wgrad(N, H, W, Ho, Wo, Cx, Cyp, R, S, stride);
-  return wgrad_ws_floats(p, Cyp) * sizeof(float);
+  // the plan (split count, tile) depends on the arithmetic: size for the largest
+  size_t mx = 0;
+  for (int math = VST_MATH_F32; math <= VST_MATH_BF16X6; ++math) {
+    const size_t b = wgrad_ws_floats(plan_wgrad(N, H, W, Ho, Wo, Cx, Cyp, R, S, stride, math), Cyp) * sizeof(float);
+    mx = b > mx ? b : mx;
+  }
+  return mx;
 }
 
 extern "C" int vst_conv2d_wgrad(const float* x, const float* dy, float* dw, float* ws,
@@ -867,7 +900,7 @@ extern "C" int vst_conv2d_wgrad(const float* x, const float* dy, float* dw, floa
   VST_REQUIRE(Cx % 4 == 0 && Cyp % 4 == 0, "conv2d_wgrad: channel strides must be multiples of 4");
   VST_REQUIRE(Co <= Cyp && Ci <= Cx, "conv2d_wgrad: logical channels exceed strides");
   VST_REQUIRE(pad_mode == VST_PAD_ZERO || (pad < H && pad < W), "conv2d_wgrad: reflect pad >= size");
-  const WgradPlan p = plan_wgrad(N, H, W, Ho, Wo, Cx, Cyp, R, S, stride);
+  const WgradPlan p = plan_wgrad(N, H, W, Ho, Wo, Cx, Cyp, R, S, stride, math);
   VST_REQUIRE(ws_bytes >= wgrad_ws_floats(p, Cyp) * sizeof(float),
               "conv2d_wgrad: workspace too small (%zu bytes)", ws_bytes);
   hipStream_t s = (hipStream_t)stream;
@@ -885,11 +918,18 @@ extern "C" int vst_conv2d_wgrad(const float* x, const float* dy, float* dw, floa
                 "conv2d_wgrad: pad %d inconsistent with H %d -> Ho %d (stride %d)", pad, H, Ho, stride);
     float* xt = ws + (size_t)p.nsplit * p.Mw * Cyp;
     float* dyt = xt + p.xt_floats;
-    const int pack = math == VST_MATH_BF16X3;  // the x3 kernel stages pre-split (hi, lo) words
-    rk_nhwc_to_cp_pad(x, xt, N, H, W, Cx, pad, refl, stride == 2, pack, s);
-    rk_nhwc_to_cp(dy, dyt, P, Cyp, pack, s);
-    rk_wgrad_launch(xt, dyt, ws, N, H, W, Cx, Ho, Wo, Cyp, S, pad, stride, p.Mw, p.chunk, p.nsplit,
-                    (int)p.tile, math, s);
+    if (p.bfk) {
+      rk_nhwc_to_cp_pad(x, xt, N, H, W, Cx, pad, refl, stride == 2, 0, s);
+      bf_nhwc_to_planes(dy, dyt, P, Cyp, 3, s);
+      bf_wgrad_launch(xt, dyt, ws, N, H, W, Cx, Ho, Wo, Cyp, S, pad, stride, p.Mw, p.chunk, p.nsplit,
+                      (int)p.tile, math, s);
+    } else {
+      const int pack = math == VST_MATH_BF16X3;  // the x3 kernel stages pre-split (hi, lo) words
+      rk_nhwc_to_cp_pad(x, xt, N, H, W, Cx, pad, refl, stride == 2, pack, s);
+      rk_nhwc_to_cp(dy, dyt, P, Cyp, pack, s);
+      rk_wgrad_launch(xt, dyt, ws, N, H, W, Cx, Ho, Wo, Cyp, S, pad, stride, p.Mw, p.chunk, p.nsplit,
+                      (int)p.tile, math, s);
+    }
   } else if (Cyp == 4) {
     int rc0 = skinny_wgrad_launch(x, dy, ws, H, W, Cx, Ho, Wo, S, stride, pad, refl, p.Mw, P, p.chunk,
                                   p.nsplit, s);

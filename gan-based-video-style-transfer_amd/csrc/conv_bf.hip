@@ -40,6 +40,9 @@
 #ifndef VST_BF_TAIL
 #define VST_BF_TAIL 1
 #endif
+#ifndef VST_BF_STORE_IN_MMA
+#define VST_BF_STORE_IN_MMA 1
+#endif
 
 namespace vst {
 namespace bf {
@@ -47,6 +50,7 @@ namespace bf {
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));  // a 16-B chunk as a first-class value
 
 template <int BM_, int BN_, int WM_, int WN_, int BK_, int NP_>
 struct Tile {
@@ -149,30 +153,25 @@ __device__ __forceinline__ void mma_stage(const char* __restrict__ As, const cha
   }
 }
 
-// Stage writer: A rows as fp32 pairs (split here), B rows as pre-split planes.  The row masks are
-// applied here, not at load time, so that no wait for the loads is forced before the MFMAs.
+// Stage writer: A rows as fp32 pairs (split here), B rows as pre-split planes.  Masked rows were
+// loaded from the zero page, so every row is written unconditionally.
 template <class T>
 __device__ __forceinline__ void store_stage(char* st, const float4 (&ra)[T::A_LD][2],
-                                            const uint4 (&rbv)[T::B_LD][T::NP], uint32_t msk, int rb,
-                                            int kq) {
+                                            const u32x4_t (&rbv)[T::B_LD][T::NP], int rb, int kq) {
   char* Bs = st + T::A_BYTES;
-  const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
   for (int j = 0; j < T::A_LD; ++j) {
     uint4 s[T::NP];
-    const bool ok = (msk >> j) & 1;
-    split8<T::NP>(ok ? ra[j][0] : z, ok ? ra[j][1] : z, s);
+    split8<T::NP>(ra[j][0], ra[j][1], s);
     const int off = swz_off(rb + T::RPP * j, kq, T::ROWB, T::SWS, T::KC - 1);
 #pragma unroll
     for (int p = 0; p < T::NP; ++p) *reinterpret_cast<uint4*>(st + p * T::A_PLANE + off) = s[p];
   }
 #pragma unroll
   for (int j = 0; j < T::B_LD; ++j) {
-    const bool ok = (msk >> (16 + j)) & 1;
     const int off = swz_off(rb + T::RPP * j, kq, T::ROWB, T::SWS, T::KC - 1);
 #pragma unroll
-    for (int p = 0; p < T::NP; ++p)
-      *reinterpret_cast<uint4*>(Bs + p * T::B_PLANE + off) = ok ? rbv[j][p] : make_uint4(0, 0, 0, 0);
+    for (int p = 0; p < T::NP; ++p) *reinterpret_cast<u32x4_t*>(Bs + p * T::B_PLANE + off) = rbv[j][p];
   }
 }
 
@@ -183,18 +182,23 @@ __device__ __forceinline__ void store_stage(char* st, const float4 (&ra)[T::A_LD
 // the cursor one stage on.
 template <class T, class LoadAll, class Adv>
 __device__ __forceinline__ void main_loop(char* smem, int nk, f32x16 (&acc)[T::MI][T::NI],
-                                          float4 (&ra)[2][T::A_LD][2], uint4 (&rbv)[2][T::B_LD][T::NP],
-                                          uint32_t (&msk)[2], int rb, int kq, LoadAll load_all, Adv adv) {
+                                          float4 (&ra)[2][T::A_LD][2], u32x4_t (&rbv)[2][T::B_LD][T::NP],
+                                          int rb, int kq, LoadAll load_all, Adv adv) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int wm0 = (wave / T::WAVES_N) * T::WM, wn0 = (wave % T::WAVES_N) * T::WN;
   if (nk <= 0) return;
   load_all(0);
-  store_stage<T>(smem, ra[0], rbv[0], msk[0], rb, kq);
+  store_stage<T>(smem, ra[0], rbv[0], rb, kq);
   if (nk > 1) {
     adv();
     load_all(1);
   }
   __syncthreads();
+  // Stage k+1's image (registers loaded one stage earlier) is split and written to the other LDS
+  // buffer from inside stage k's MFMA stream (before its last k group): that buffer's previous
+  // contents (stage k-1) were released by the barrier that ended stage k-1, so the split VALU and
+  // ds_writes fill the gaps between this stage's MFMAs instead of forming a bubble before the
+  // barrier (VST_BF_STORE_IN_MMA=0: the store after the MFMAs).
   auto step = [&](int kt, auto par) {
     constexpr int P = decltype(par)::value;
     char* cur = smem + P * T::STAGE;
@@ -203,8 +207,11 @@ __device__ __forceinline__ void main_loop(char* smem, int nk, f32x16 (&acc)[T::M
         adv();
         load_all(P);
       }
+      if (VST_BF_STORE_IN_MMA && g == T::BK / 16 - 1 && kt + 1 < nk)
+        store_stage<T>(smem + (P ^ 1) * T::STAGE, ra[P ^ 1], rbv[P ^ 1], rb, kq);
     });
-    if (kt + 1 < nk) store_stage<T>(smem + (P ^ 1) * T::STAGE, ra[P ^ 1], rbv[P ^ 1], msk[P ^ 1], rb, kq);
+    if (!VST_BF_STORE_IN_MMA && kt + 1 < nk)
+      store_stage<T>(smem + (P ^ 1) * T::STAGE, ra[P ^ 1], rbv[P ^ 1], rb, kq);
     __syncthreads();
   };
   for (int kt = 0; kt < nk; kt += 2) {
@@ -240,10 +247,26 @@ __device__ __forceinline__ void tile_of(int L, int Mt, int Nt, int& mt, int& nt)
 }
 
 // ------------------------------------------------------------------------------------------ fprop
+// Target of every masked A gather (zero-padding taps, the K tail): loads from it return zeros, so
+// the stage writer needs no per-row select.  Never written.
+__device__ __attribute__((aligned(256))) float g_zero_page[64];
+
 // y[m = (n, ho, wo)][co] = act(sum_k x_gather[m][k] * w[co][k] + bias[co]),  k = (r, s, ci);
 // requires C % 8 == 0 (a thread's 8-deep chunk stays inside one tap).  ws = pre-split weight planes
 // of the VST_PACK_OK matrix [Cop][R*S*C], plane stride wps elements.
-template <class T>
+//
+// KSL (C % BK == 0): K-steps walk the R*S taps of one BK-channel slice, then the next slice, so one
+// slice of the block's activation rows is reused by all taps while it is L2-resident (tap-major
+// order streams the whole C-deep block through L2 once per tap: 289 -> 96 MB HBM traffic per N=8
+// ResnetBlock launch on the 256x128 tiles; the 128x128 dgrad tiles fetched 356 MB per launch tap-
+// major).  The K cursor (tap, slice) is block-uniform, so it lives in scalar registers; only the
+// per-row pixel offsets are recomputed (one reflect / bounds map per row) when the tap changes.
+// The weight planes keep their (r, s, ci) layout: the B offset of a step is (r*S + s)*C + slice.
+// Without KSL (C not a multiple of BK: the image-input layers) the K-steps walk k = (r, s, ci) in
+// order with a per-thread cursor.
+// REFL: 0 = zero padding, 1 = reflect padding (compile-time, branch-free tap map), 2 = runtime
+// `reflect` (the rarely used tap-major variants).
+template <class T, bool KSL, int REFL>
 __global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_k(
     const float* __restrict__ x, const __bf16* __restrict__ ws, long wps, const float* __restrict__ bias,
     float* __restrict__ y, int H, int W, int C, int Ho, int Wo, int Cop, int S, int st, int padh,
@@ -255,25 +278,11 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_k(
   tile_of(blockIdx.x, (M - m_base + T::BM - 1) / T::BM, (Cop + T::BN - 1) / T::BN, mt_, nt_);
   const int m0 = m_base + mt_ * T::BM, n0 = nt_ * T::BN;
   const int kq = t % T::KC, rb = t / T::KC;
+  const float* zp = g_zero_page;
 
-  // this thread's chunk: absolute k = kcur, tap (kr, ks), channel kc.
-  // Channel-sliced K order (C % BK == 0): K-steps walk the R*S taps of one BK-channel slice, then
-  // the next slice, so one slice of the block's activation rows is reused by all taps while it
-  // is L2-resident (tap-major order streams the whole C-deep block through L2 once per tap).  The
-  // weight planes keep their (r, s, ci) layout: the B offset of a step is (r*S + s)*C + kc.
-  // Applied where the tap-major order overflows L2: the 256-row x6 tiles (one round, 4 MB live
-  // activation block per XCD: 289 -> 96 MB HBM traffic per N=8 ResnetBlock launch).  Smaller
-  // tiles keep the tap-major summation order.
-  const bool ksl = VST_BF_KSLICE && T::BM == 256 && NP == 3 && C % T::BK == 0 && Ktot % C == 0;
-  const int Rk = ksl ? Ktot / (S * C) : 0;
-  int kcur = 8 * kq;
-  int kc = kcur % C, ks, kr;
-  {
-    const int rs = kcur / C;
-    kr = rs / S;
-    ks = rs - kr * S;
-  }
-  int hb[A_LD], wb[A_LD], nb[A_LD], aoff[A_LD];
+  // A rows (output pixels m0 + rb + RPP*j): tap-independent geometry.  Rows past M gather row 0's
+  // pixels instead: their outputs are never stored, so no mask is needed for them.
+  int hb[A_LD], wb[A_LD], pb[A_LD], aoff[A_LD];
 #pragma unroll
   for (int j = 0; j < A_LD; ++j) {
     const int m = m0 + rb + RPP * j;
@@ -282,64 +291,73 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_k(
     const int n = mm / hw, rem = mm - n * hw, ho = rem / Wo, wo = rem - ho * Wo;
     hb[j] = ho * st - padh;
     wb[j] = wo * st - padw;
-    nb[j] = m < M ? n : -1;
+    pb[j] = n * H * W * C;
   }
-  auto tap_rows = [&]() {
+  // element offset of row j's pixel under tap (kr, ks), -1 where the tap reads zero padding
+  const bool refl = REFL == 2 ? reflect != 0 : REFL == 1;
+  const int WC = W * C;
+  auto tap_rows = [&](int kr, int ks) __attribute__((always_inline)) {
 #pragma unroll
     for (int j = 0; j < A_LD; ++j) {
       int hi = hb[j] + kr, wi = wb[j] + ks;
-      bool ok = nb[j] >= 0;
-      if (reflect) {
+      if (refl) {
         hi = reflect_idx(hi, H);
         wi = reflect_idx(wi, W);
+        aoff[j] = pb[j] + __mul24(hi, WC) + __mul24(wi, C);
       } else {
-        ok = ok && (unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W;
+        const bool ok = (unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W;
+        aoff[j] = ok ? pb[j] + __mul24(hi, WC) + __mul24(wi, C) : -1;
       }
-      aoff[j] = ok ? ((nb[j] * H + hi) * W + wi) * C : -1;
     }
   };
-  tap_rows();
+  // B rows (output channels n0 + rb + RPP*j); channels past Cop read row Cop-1 (never stored)
   const __bf16* wrow[B_LD];
-  bool nv[B_LD];
 #pragma unroll
   for (int j = 0; j < B_LD; ++j) {
     const int n = n0 + rb + RPP * j;
-    nv[j] = n < Cop;
-    wrow[j] = ws + (long)(nv[j] ? n : 0) * Ktot;
+    wrow[j] = ws + (long)(n < Cop ? n : Cop - 1) * Ktot;
+  }
+
+  // K cursor.  KSL: block-uniform (tap r, tap s, slice base) + this thread's chunk 8*kq.
+  // Otherwise: per-thread absolute k (kcur) with its channel kc and tap (kr, ks).
+  const int kq8 = 8 * kq;
+  int tr = 0, ts = 0, ksb = 0;                 // KSL
+  int kcur = kq8, kc = kq8 % C, kr = 0, ks = 0;  // tap-major
+  const int Rk = KSL ? Ktot / (S * C) : 0;
+  if (KSL) {
+    tap_rows(0, 0);
+  } else {
+    const int rs = kq8 / C;
+    kr = rs / S;
+    ks = rs - kr * S;
+    tap_rows(kr, ks);
   }
 
   float4 ra[2][A_LD][2];
-  uint4 rbv[2][B_LD][NP];
-  uint32_t msk[2];
-  // unconditional loads: invalid rows / the K tail read a safe address; the row mask (bit j = A row
-  // j, bit 16 + j = B row j) zeroes them when the stage is written to LDS
-  auto load_all = [&](int set) {
-    const bool kin = ksl ? kc < C : kcur < Ktot;
-    const int kk = kin ? (ksl ? (kr * S + ks) * C + kc : kcur) : 0;
-    uint32_t m = 0;
+  u32x4_t rbv[2][B_LD][NP];
+  auto load_all = [&](int set) __attribute__((always_inline)) {
+    const bool kin = KSL || kcur < Ktot;  // the K tail reads zeros (A) against row 0 (B)
+    const int ka = KSL ? ksb + kq8 : kc;
+    const int kb = KSL ? (tr * S + ts) * C + ksb + kq8 : (kin ? kcur : 0);
 #pragma unroll
     for (int j = 0; j < A_LD; ++j) {
-      const bool ok = kin && aoff[j] >= 0;
-      m |= (uint32_t)ok << j;
-      const float* p = x + (ok ? aoff[j] + kc : 0);
+      const float* p = (kin && aoff[j] >= 0) ? x + aoff[j] + ka : zp;
       ra[set][j][0] = *reinterpret_cast<const float4*>(p);
       ra[set][j][1] = *reinterpret_cast<const float4*>(p + 4);
     }
 #pragma unroll
     for (int j = 0; j < B_LD; ++j) {
-      m |= (uint32_t)(kin && nv[j]) << (16 + j);
 #pragma unroll
-      for (int p = 0; p < NP; ++p) rbv[set][j][p] = *reinterpret_cast<const uint4*>(wrow[j] + p * wps + kk);
+      for (int p = 0; p < NP; ++p) rbv[set][j][p] = *reinterpret_cast<const u32x4_t*>(wrow[j] + p * wps + kb);
     }
-    msk[set] = m;
   };
-  auto adv = [&]() {
-    if (ksl) {
-      if (++ks == S) {
-        ks = 0;
-        if (++kr == Rk) { kr = 0; kc += T::BK; }
+  auto adv = [&]() __attribute__((always_inline)) {
+    if (KSL) {
+      if (++ts == S) {
+        ts = 0;
+        if (++tr == Rk) { tr = 0; ksb += T::BK; }
       }
-      tap_rows();
+      tap_rows(tr, ts);
       return;
     }
     kcur += T::BK;
@@ -349,13 +367,13 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_k(
         kc -= C;
         if (++ks == S) { ks = 0; ++kr; }
       } while (kc >= C);
-      tap_rows();
+      tap_rows(kr, ks);
     }
   };
 
   f32x16 acc[T::MI][T::NI];
   zero_acc(acc);
-  main_loop<T>(smem, (Ktot + T::BK - 1) / T::BK, acc, ra, rbv, msk, rb, kq, load_all, adv);
+  main_loop<T>(smem, (Ktot + T::BK - 1) / T::BK, acc, ra, rbv, rb, kq, load_all, adv);
 
   const int wm0 = (wave / T::WAVES_N) * T::WM, wn0 = (wave % T::WAVES_N) * T::WN;
 #pragma unroll
@@ -371,6 +389,171 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_k(
         if (mm < M) y[(long)mm * Cop + n] = apply_act(acc[i][j][r] + bv, act, slope);
       }
     }
+}
+
+// -------------------------------------------------------------------------- weight gradient
+// dW[m = (r, s, ci)][co] = sum_p X[shift_rs(p)][ci] * dY[p][co] over one split-K chunk of output
+// pixels p, on the same stage / MMA machinery as the forward:
+//   A rows (tap, ci): the padded channel-major fp32 copy xt = [Cx][N][Hp][Wp] of x (reflect / zero
+//     border applied; stride 2: each padded row stored as its even then its odd columns), so a
+//     thread's 8 consecutive output pixels (one output-row segment: Wo % 8 == 0) are 8 consecutive
+//     words; split into bf16 planes in registers like the forward's activations;
+//   B rows co: dY as NP pre-split bf16 planes [NP][Cyp][ldy] (nhwc_to_cp_planes_k), copied into the
+//     stage image like the forward's weights.
+// Replaces the [row][k] fp32-image kernel for the x6 arithmetic: that one split BOTH operands in
+// registers for every K-step (the x shifted copy once per tap) and sat at ~0.33 of the x6 ceiling.
+// The split-K chunk index comes from an XCD-aware 1-D grid (every tile of one chunk on one XCD, so
+// its x / dy rows stay in that XCD's L2); partial tiles land in slab[z][m][Cyp].
+template <class T>
+__global__ __launch_bounds__(T::NT, T::MINB) void conv_wgrad_bf_k(
+    const float* __restrict__ xt, const __bf16* __restrict__ dyp, long dps, float* __restrict__ slab, int H,
+    int W, int Cx, int Ho, int Wo, int Cyp, int S, int pad, int st, int Mw, int P, int chunk, long ldx,
+    long ldy) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * T::STAGE];
+  constexpr int A_LD = T::A_LD, B_LD = T::B_LD, RPP = T::RPP, NP = T::NP;
+  typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int Mt = (Mw + T::BM - 1) / T::BM, Nt = (Cyp + T::BN - 1) / T::BN, Zt = (P + chunk - 1) / chunk;
+  int mx, ny, zz;
+  {
+    const int L = blockIdx.x, Tt = Mt * Nt * Zt;
+    const int tt = (Tt & 7) ? L : (L & 7) * (Tt >> 3) + (L >> 3);
+    zz = tt / (Mt * Nt);
+    const int rem = tt - zz * Mt * Nt;
+    ny = rem / Mt;
+    mx = rem - ny * Mt;
+  }
+  const int m0 = mx * T::BM, n0 = ny * T::BN;
+  const int pbeg = zz * chunk, pend = min(P, pbeg + chunk);
+  const int kq = t % T::KC, rb = t / T::KC;
+  const float* zp = g_zero_page;
+  const __bf16* zpb = reinterpret_cast<const __bf16*>(g_zero_page);
+  const int Hp = H + 2 * pad, Wp = W + 2 * pad;
+  // A rows (rows past Mw read row Mw-1: never stored)
+  const float* xrow[A_LD];
+#pragma unroll
+  for (int j = 0; j < A_LD; ++j) {
+    const int m = m0 + rb + RPP * j;
+    const int mm = m < Mw ? m : Mw - 1;
+    const int tap = mm / Cx, ci = mm - tap * Cx;
+    const int r = tap / S, s_ = tap - r * S;
+    xrow[j] = xt + (long)ci * ldx + r * Wp + (st == 1 ? s_ : (s_ & 1) * (Wp >> 1) + (s_ >> 1));
+  }
+  // B rows (channels past Cyp read row Cyp-1: never stored)
+  const __bf16* drow[B_LD];
+#pragma unroll
+  for (int j = 0; j < B_LD; ++j) {
+    const int n = n0 + rb + RPP * j;
+    drow[j] = dyp + (long)(n < Cyp ? n : Cyp - 1) * ldy;
+  }
+  // this thread's 8-pixel chunk: output pixel kp = (pn, pho, pwo) and its padded-image offset
+  int kp = pbeg + 8 * kq, pho, pwo;
+  long poff;
+  {
+    const int hw = Ho * Wo;
+    const int pn = kp / hw;
+    const int rem = kp - pn * hw;
+    pho = rem / Wo;
+    pwo = rem - pho * Wo;
+    poff = ((long)pn * Hp + st * pho) * Wp + pwo;
+  }
+  float4 ra[2][A_LD][2];
+  u32x4_t rbv[2][B_LD][NP];
+  auto load_all = [&](int set) __attribute__((always_inline)) {
+    const bool live = kp < pend;  // 8-pixel chunks never straddle pend (chunk, P multiples of 8)
+#pragma unroll
+    for (int j = 0; j < A_LD; ++j) {
+      const float* p = live ? xrow[j] + poff : zp;
+      const f4u u0 = *reinterpret_cast<const f4u*>(p);
+      const f4u u1 = *reinterpret_cast<const f4u*>(p + 4);
+      ra[set][j][0] = make_float4(u0.x, u0.y, u0.z, u0.w);
+      ra[set][j][1] = make_float4(u1.x, u1.y, u1.z, u1.w);
+    }
+#pragma unroll
+    for (int j = 0; j < B_LD; ++j) {
+      const __bf16* q = live ? drow[j] + kp : zpb;
+      const long ps = live ? dps : 0;
+#pragma unroll
+      for (int p = 0; p < NP; ++p) rbv[set][j][p] = *reinterpret_cast<const u32x4_t*>(q + p * ps);
+    }
+  };
+  auto adv = [&]() __attribute__((always_inline)) {
+    kp += T::BK;
+    pwo += T::BK;
+    poff += T::BK;
+    while (pwo >= Wo) {
+      pwo -= Wo;
+      poff += st * Wp - Wo;
+      if (++pho == Ho) { pho = 0; poff += (long)(Hp - st * Ho) * Wp; }
+    }
+  };
+  f32x16 acc[T::MI][T::NI];
+  zero_acc(acc);
+  const int nk = pend > pbeg ? (pend - pbeg + T::BK - 1) / T::BK : 0;
+  main_loop<T>(smem, nk, acc, ra, rbv, rb, kq, load_all, adv);
+
+  const int wm0 = (wave / T::WAVES_N) * T::WM, wn0 = (wave % T::WAVES_N) * T::WN;
+  float* sl = slab + (long)zz * Mw * Cyp;
+#pragma unroll
+  for (int i = 0; i < T::MI; ++i)
+#pragma unroll
+    for (int j = 0; j < T::NI; ++j) {
+      const int n = n0 + wn0 + 32 * j + (lane & 31);
+      if (n >= Cyp) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int mm = m0 + wm0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (mm < Mw) sl[(long)mm * Cyp + n] = acc[i][j][r];
+      }
+    }
+}
+
+// NHWC [P][Cs] fp32 -> NP bf16 planes [NP][Cs][ld] (hi, (mid,) lo of each value, the same RNE
+// conversions as split8 / split3_k) through a 64x64 LDS transpose tile: the weight gradient's
+// pre-split B operand.
+template <int NP>
+__global__ __launch_bounds__(256) void nhwc_to_cp_planes_k(const float* __restrict__ x, __bf16* __restrict__ y,
+                                                           long P, int Cs, long ld) {
+  __shared__ float tile[64][65];
+  const long p0 = (long)blockIdx.x * 64;
+  const int c0 = blockIdx.y * 64;
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int idx = t + 256 * it, pr = idx >> 4, c4 = (idx & 15) * 4;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (p0 + pr < P && c0 + c4 < Cs) v = *reinterpret_cast<const float4*>(x + (p0 + pr) * Cs + c0 + c4);
+    tile[pr][c4] = v.x;
+    tile[pr][c4 + 1] = v.y;
+    tile[pr][c4 + 2] = v.z;
+    tile[pr][c4 + 3] = v.w;
+  }
+  __syncthreads();
+  const long plane = (long)Cs * ld;
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int idx = t + 256 * it, cr = idx >> 4, p4 = (idx & 15) * 4;
+    if (c0 + cr >= Cs || p0 + p4 >= P) continue;
+    float r[4] = {tile[p4][cr], tile[p4 + 1][cr], tile[p4 + 2][cr], tile[p4 + 3][cr]};
+    __bf16* dst = y + (long)(c0 + cr) * ld + p0 + p4;
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const uint32_t q0 = pack2(r[0], r[1]), q1 = pack2(r[2], r[3]);
+      if (p0 + p4 + 3 < P) {
+        *reinterpret_cast<uint2*>(dst + p * plane) = make_uint2(q0, q1);
+      } else {  // ragged plane length: element stores, never past P
+        const uint16_t h[4] = {(uint16_t)q0, (uint16_t)(q0 >> 16), (uint16_t)q1, (uint16_t)(q1 >> 16)};
+        for (int e = 0; e < 4 && p0 + p4 + e < P; ++e)
+          reinterpret_cast<uint16_t*>(dst + p * plane)[e] = h[e];
+      }
+      if (p + 1 < NP) {
+        r[0] -= __uint_as_float(q0 << 16);
+        r[1] -= __uint_as_float(q0 & 0xffff0000u);
+        r[2] -= __uint_as_float(q1 << 16);
+        r[3] -= __uint_as_float(q1 & 0xffff0000u);
+      }
+    }
+  }
 }
 
 // split an fp32 buffer into three bf16 planes (hi, mid, lo) of n elements each
@@ -408,7 +591,7 @@ __global__ void split3_k(const float* __restrict__ w, __bf16* __restrict__ out, 
   }
 
 int bf_pick(long M, int Nc, int override_kind) {
-  if (override_kind >= 0 && override_kind <= 7) return override_kind;
+  if (override_kind >= 0 && override_kind <= 8) return override_kind;
   if (Nc <= 64) return M / 128 >= 256 ? 1 : 6;
   const long n128 = (Nc + 127) / 128;
   if ((M / 128) * n128 >= 200) return 0;
@@ -416,24 +599,71 @@ int bf_pick(long M, int Nc, int override_kind) {
   return 6;
 }
 
+// Tile geometry of a kind for NP planes: rows, cols, co-resident blocks per CU (LDS-limited).
+static void bf_geom(int kind, int np, int* bm, int* bn, int* slots) {
+  int BM = 128, BN = 128, BK = 32;
+  switch (kind) {
+    case 1: BN = 64; break;
+    case 2: break;
+    case 3: BM = 64; break;
+    case 4: BK = np == 3 ? 32 : 64; break;
+    case 5: BN = 64; BK = 64; break;
+    case 6: BM = 64; BN = 64; break;
+    case 7: BM = 256; break;
+    case 8: BM = 64; BN = 64; BK = np == 3 ? 32 : 64; break;
+    default: break;
+  }
+  const int stage = np * (BM + BN) * BK * 2;
+  int sl = (160 * 1024) / (2 * stage);
+  const int waves = (kind == 0 || kind == 4 || kind == 7) ? 8 : 4;
+  if (sl * waves > 32) sl = 32 / waves;
+  *bm = BM;
+  *bn = BN;
+  *slots = sl < 1 ? 1 : sl;
+}
+
 // Launch plan of the split-arithmetic forward for an M x Cop output: the tile kind of the main
 // launch and, when the grid is split for wave quantisation, the first pixel row of the tail launch
-// (0 = one launch).  Host-only; also exported through vst_conv_plan_fwd for tests and the bench.
-void bf_plan(long M, int Cop, int math, int kind, int* kind_out, int* m_split_out) {
+// (0 = one launch) and the tail's tile kind.  Host-only; exported through vst_conv_plan_fwd.
+void bf_plan(long M, int Cop, int math, int kind, int* kind_out, int* m_split_out, int* tail_out) {
   int kd = bf_pick(M, Cop, kind);
-#if VST_BF_X6K3
-  // x6: the 128x128 three-plane stage pair (96 KB) fits one block per CU; 64x128 tiles fit two
-  if (kind < 0 && kd == 0 && math == VST_MATH_BF16X6) kd = 3;
-#endif
+  int m_split = 0, tail_kind = VST_BF_TAIL_KIND;
 #if VST_BF_X6_256
-  // x6, one block per CU either way: 256x128 tiles of 8 waves x (64x64) halve the LDS fragment
-  // reads per MFMA and the barriers per FLOP — when the grid is whole rounds of 256 blocks
+  // x6 runs one 128x128 or 256x128 block per CU either way (the three-plane stage pairs are 96 /
+  // 144 KB): 256x128 tiles of 8 waves x (64x64) halve the LDS fragment reads per MFMA and the
+  // barriers per FLOP.  Whole rounds of 256 blocks run as one launch; otherwise the whole rounds
+  // of 256x128 tiles run first and the remaining pixel rows (a partial round) as a second launch
+  // of smaller tiles chosen to fill the CUs (cost = rounds x tile area / tile efficiency):
+  //   N=8 padded-frame dgrad (M = 34848): 256 x 256x128 + 132 x 64x64 blocks (was 546 x 128x128
+  //   at one per CU = 3 rounds); N=12 forward (M = 49152): 256 x 256x128 + 512 x 64x128.
   if (kind < 0 && kd == 0 && math == VST_MATH_BF16X6) {
-    const long b256 = (long)((M + 255) / 256) * ((Cop + 127) / 128);
-    if (b256 % VST_NUM_CUS == 0 || b256 >= 4 * VST_NUM_CUS) kd = 7;
+    const long nt = (Cop + 127) / 128;
+    const long b256 = (long)((M + 255) / 256) * nt;
+    if (b256 % VST_NUM_CUS == 0 || b256 >= 4 * VST_NUM_CUS) {
+      kd = 7;
+    } else if (b256 > VST_NUM_CUS && (VST_NUM_CUS % nt) == 0) {
+      const long ms = (long)(b256 / VST_NUM_CUS) * (VST_NUM_CUS / nt) * 256;  // whole rounds of rows
+      const long rest = M - ms;
+      static const int cand[4] = {8, 3, 1, 0};
+      static const double eff[4] = {0.6, 0.75, 0.75, 0.85};  // relative to the 256x128 tile
+      double best = (double)((b256 + VST_NUM_CUS - 1) / VST_NUM_CUS);  // no split: whole 256x128 grid
+      int bk = -1;
+      for (int c = 0; c < 4; ++c) {
+        int bm, bn, sl;
+        bf_geom(cand[c], 3, &bm, &bn, &sl);
+        const long blocks = ((rest + bm - 1) / bm) * ((Cop + bn - 1) / bn);
+        const long rounds = (blocks + (long)sl * VST_NUM_CUS - 1) / ((long)sl * VST_NUM_CUS);
+        const double cost = (double)(ms / 256 * nt) / VST_NUM_CUS + rounds * (bm * bn) / (256.0 * 128.0) / eff[c];
+        if (cost < best - 1e-9) { best = cost; bk = cand[c]; }
+      }
+      kd = 7;
+      if (bk >= 0) {
+        m_split = (int)ms;
+        tail_kind = bk;
+      }
+    }
   }
 #endif
-  int m_split = 0;
 #if VST_BF_TAIL
   // Wave quantisation: 128x128 x3 blocks run two per CU, so a grid a few tiles past a whole
   // number of blocks per CU (the padded-frame dgrad: 546 = 2 x 256 + 34 blocks at N = 8) keeps
@@ -442,12 +672,15 @@ void bf_plan(long M, int Cop, int math, int kind, int* kind_out, int* m_split_ou
   if (kind < 0 && kd == 0 && math != VST_MATH_BF16X6) {
     const long nt = (Cop + 127) / 128, blocks = (long)((M + 127) / 128) * nt;
     const long per = blocks / VST_NUM_CUS, tail = blocks - per * VST_NUM_CUS;
-    if (per >= 1 && tail > 0 && 4 * tail <= VST_NUM_CUS && (per * VST_NUM_CUS) % nt == 0)
+    if (per >= 1 && tail > 0 && 4 * tail <= VST_NUM_CUS && (per * VST_NUM_CUS) % nt == 0) {
       m_split = (int)(per * VST_NUM_CUS / nt) * 128;
+      tail_kind = VST_BF_TAIL_KIND;
+    }
   }
 #endif
   *kind_out = kd;
   *m_split_out = m_split;
+  *tail_out = m_split ? tail_kind : -1;
 }
 
 int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* bias, float* y, int N,
@@ -455,18 +688,25 @@ int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* b
                     int reflect, int act, float slope, int math, int kind, hipStream_t s) {
   const int M = N * Ho * Wo, K = R * S * C;
   const __bf16* ws = reinterpret_cast<const __bf16*>(wsplit);
-  int kd, m_split;
-  bf_plan(M, Cop, math, kind, &kd, &m_split);
-#define VST_BF(BM_, BN_, WM_, WN_, BK_, NP_)                                                     \
+  int kd, m_split, tail_kind;
+  bf_plan(M, Cop, math, kind, &kd, &m_split, &tail_kind);
+#define VST_BF(BM_, BN_, WM_, WN_, BK_, NP_)                                                       \
   {                                                                                                 \
     using T = bf::Tile<BM_, BN_, WM_, WN_, BK_, NP_>;                                              \
-    hipLaunchKernelGGL(bf::conv_fprop_bf_k<T>, dim3(ceil_div(Mend - mb, BM_) * ceil_div(Cop, BN_)),   \
-                       dim3(T::NT), 0, s, x, ws, wps, bias, y, H, W, C, Ho, Wo, Cop, S,             \
-                       st, padh, padw, reflect, act, slope, Mend, K, mb);                           \
+    const dim3 grid(ceil_div(Mend - mb, BM_) * ceil_div(Cop, BN_));                                 \
+    if (VST_BF_KSLICE && C % BK_ == 0 && reflect)                                                   \
+      hipLaunchKernelGGL((bf::conv_fprop_bf_k<T, true, 1>), grid, dim3(T::NT), 0, s, x, ws, wps, bias, y, \
+                         H, W, C, Ho, Wo, Cop, S, st, padh, padw, reflect, act, slope, Mend, K, mb); \
+    else if (VST_BF_KSLICE && C % BK_ == 0)                                                         \
+      hipLaunchKernelGGL((bf::conv_fprop_bf_k<T, true, 0>), grid, dim3(T::NT), 0, s, x, ws, wps, bias, y, \
+                         H, W, C, Ho, Wo, Cop, S, st, padh, padw, reflect, act, slope, Mend, K, mb); \
+    else                                                                                            \
+      hipLaunchKernelGGL((bf::conv_fprop_bf_k<T, false, 2>), grid, dim3(T::NT), 0, s, x, ws, wps, bias, y, \
+                         H, W, C, Ho, Wo, Cop, S, st, padh, padw, reflect, act, slope, Mend, K, mb); \
   }
   for (int part = 0; part < (m_split ? 2 : 1); ++part) {
     const int mb = part ? m_split : 0, Mend = (m_split && !part) ? m_split : M;
-    const int kp = part ? VST_BF_TAIL_KIND : kd;
+    const int kp = part ? tail_kind : kd;
     if (math == VST_MATH_BF16X6) {
       VST_BF_DISPATCH(kp, 3, VST_BF)
     } else {
@@ -475,6 +715,43 @@ int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* b
   }
 #undef VST_BF
   return check_launch("conv2d_fwd(bf16 split)");
+}
+
+
+void bf_nhwc_to_planes(const float* x, void* y, long P, int Cs, int np, hipStream_t s) {
+  const dim3 g((unsigned)((P + 63) / 64), ceil_div(Cs, 64));
+  __bf16* yb = reinterpret_cast<__bf16*>(y);
+  if (np == 3) hipLaunchKernelGGL(bf::nhwc_to_cp_planes_k<3>, g, dim3(256), 0, s, x, yb, P, Cs, rk_cp_ld(P));
+  else hipLaunchKernelGGL(bf::nhwc_to_cp_planes_k<2>, g, dim3(256), 0, s, x, yb, P, Cs, rk_cp_ld(P));
+}
+
+void bf_wgrad_launch(const float* xt, const void* dyp, float* slab, int N, int H, int W, int Cx, int Ho,
+                     int Wo, int Cyp, int S, int pad, int st, int Mw, int chunk, int nsplit, int kind, int math,
+                     hipStream_t s) {
+  const int P = N * Ho * Wo;
+  const long ldx = rk_cp_ld((long)N * (H + 2 * pad) * (W + 2 * pad)), ldy = rk_cp_ld(P);
+  const __bf16* d = reinterpret_cast<const __bf16*>(dyp);
+  const long dps = (long)Cyp * ldy;
+#define VST_BW(BM_, BN_, WM_, WN_, BK_, NP_)                                                          \
+  {                                                                                                 \
+    using T = bf::Tile<BM_, BN_, WM_, WN_, BK_, NP_>;                                              \
+    hipLaunchKernelGGL((bf::conv_wgrad_bf_k<T>),                                                    \
+                       dim3(ceil_div(Mw, BM_) * ceil_div(Cyp, BN_) * nsplit), dim3(T::NT), 0, s, xt, d, \
+                       dps, slab, H, W, Cx, Ho, Wo, Cyp, S, pad, st, Mw, P, chunk, ldx, ldy);       \
+  }
+  if (math == VST_MATH_BF16X6) {
+    VST_BF_DISPATCH(kind, 3, VST_BW)
+  } else {
+    VST_BF_DISPATCH(kind, 2, VST_BW)
+  }
+#undef VST_BW
+}
+
+void bf_wgrad_geom(int kind, int math, int* bm, int* bn, int* bk, int* slots) {
+  int sl;
+  bf_geom(kind, math == VST_MATH_BF16X6 ? 3 : 2, bm, bn, &sl);
+  *bk = 32;
+  *slots = sl * VST_NUM_CUS;
 }
 
 }  // namespace vst

@@ -821,11 +821,23 @@ int rk_pick(long M, int Nc, int override_kind) {
   return 3;
 }
 
-void rk_tile_geom(int kind, int* bm, int* bn, int* bk, int* slots) {
+// Geometry of a tile kind under `math` (the x6 image maps kinds 4 / 6 to their 32-deep twins) and
+// its co-resident blocks per round: LDS-limited (double-buffered stage image: fp32 [rows][BK+4] or
+// NP bf16 planes [rows][BK+8]) and at most two blocks per CU (__launch_bounds__(NT, 2)), one for
+// the 8-wave kinds.  The x6 128x128 image (122 KB) fits one block per CU.
+void rk_tile_geom(int kind, int math, int* bm, int* bn, int* bk, int* slots) {
+  if (math == VST_MATH_BF16X6) kind = kind == 4 ? 0 : (kind == 6 ? 5 : kind);
   *bm = (kind == 1 || kind == 3) ? 64 : 128;
   *bn = (kind == 2 || kind == 3) ? 64 : 128;
   *bk = (kind == 4 || kind == 6) ? 64 : 32;
-  *slots = (kind == 0 || kind == 4 || kind == 6) ? 256 : 512;  // co-resident blocks per round
+  const int np = math == VST_MATH_BF16X6 ? 3 : 2;
+  const long stage = math == VST_MATH_F32 ? (long)(*bm + *bn) * (*bk + 4) * 4
+                                          : (long)(*bm + *bn) * (*bk + 8) * 2 * np;
+  long per_cu = (160L * 1024) / (2 * stage);
+  const long cap = (kind == 0 || kind == 4) ? 1 : 2;
+  if (per_cu > cap) per_cu = cap;
+  if (per_cu < 1) per_cu = 1;
+  *slots = (int)per_cu * VST_NUM_CUS;
 }
 
 #define VST_RK_DISPATCH_M(kind, LAUNCH, M_)                             \

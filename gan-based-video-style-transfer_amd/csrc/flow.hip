@@ -11,10 +11,13 @@
 // the result; the backward scatters with fp32 atomics into the zero-initialised input gradient.
 #include "common.h"
 
-// No a*b+c -> fma contraction in this file: the sample positions, bilinear weights, norms and
-// thresholds are evaluated with the same separately-rounded fp32 operations as PyTorch's CPU
-// grid sampler / norm, so the fb-check mask is bit-identical to the reference's (a contracted
-// multiply-add can move a threshold comparison across a tie).
+// No implicit a*b+c -> fma contraction in this file: every rounding step is spelled out to match
+// the reference's PyTorch CPU kernels bit for bit (tests/golden/warp.npz, fbc.npz were written by
+// the reference itself).  Those kernels are built with FMA contraction, so where they fuse we fuse
+// explicitly: the source index is fma(g + 1, size / 2, -0.5), the bilinear sample is the fma chain
+// nw -> ne -> sw -> se, a 2-vector squared norm is fma(q, q, p*p); everything else (grid
+// normalisation, weights, thresholds, which PyTorch evaluates as separate tensor ops) rounds each
+// operation on its own.
 #pragma clang fp contract(off)
 
 namespace vst {
@@ -25,7 +28,14 @@ struct Bilin {
 };
 
 __device__ __forceinline__ float src_index(float g, int size, int align) {
-  return align ? ((g + 1.f) / 2.f) * (float)(size - 1) : ((g + 1.f) * (float)size - 1.f) / 2.f;
+  // ATen's grid-sampler unnormalize: (g + 1) * ((size - 1) / 2), resp. fma(g + 1, size / 2, -0.5)
+  return align ? (g + 1.f) * ((float)(size - 1) * 0.5f) : fmaf(g + 1.f, (float)size * 0.5f, -0.5f);
+}
+
+// bilinear combination of the four corner values in ATen's order (an fma chain)
+__device__ __forceinline__ float bilerp(float v_nw, float v_ne, float v_sw, float v_se, float nw, float ne,
+                                        float sw, float se) {
+  return fmaf(v_se, se, fmaf(v_sw, sw, fmaf(v_ne, ne, v_nw * nw)));
 }
 
 // sample position for output pixel (h, w) displaced by (fx, fy), reference normalisation
@@ -94,10 +104,10 @@ __global__ void warp_fwd_k(const float* __restrict__ x, const float* __restrict_
   if (inb(b.y0 + 1, b.x0, H, W)) v_sw = xs[((long)(b.y0 + 1) * W + b.x0) * C4];
   if (inb(b.y0 + 1, b.x0 + 1, H, W)) v_se = xs[((long)(b.y0 + 1) * W + b.x0 + 1) * C4];
   float4 o;
-  o.x = v_nw.x * b.nw + v_ne.x * b.ne + v_sw.x * b.sw + v_se.x * b.se;
-  o.y = v_nw.y * b.nw + v_ne.y * b.ne + v_sw.y * b.sw + v_se.y * b.se;
-  o.z = v_nw.z * b.nw + v_ne.z * b.ne + v_sw.z * b.sw + v_se.z * b.se;
-  o.w = v_nw.w * b.nw + v_ne.w * b.ne + v_sw.w * b.sw + v_se.w * b.se;
+  o.x = bilerp(v_nw.x, v_ne.x, v_sw.x, v_se.x, b.nw, b.ne, b.sw, b.se);
+  o.y = bilerp(v_nw.y, v_ne.y, v_sw.y, v_se.y, b.nw, b.ne, b.sw, b.se);
+  o.z = bilerp(v_nw.z, v_ne.z, v_sw.z, v_se.z, b.nw, b.ne, b.sw, b.se);
+  o.w = bilerp(v_nw.w, v_ne.w, v_sw.w, v_se.w, b.nw, b.ne, b.sw, b.se);
   reinterpret_cast<float4*>(out)[i] = o;
 }
 
@@ -143,7 +153,7 @@ __global__ void temporal_k(const float* __restrict__ a, const float* __restrict_
       if (inb(b.y0, b.x0 + 1, H, W)) v_ne = an[((long)b.y0 * W + b.x0 + 1) * Cs + c];
       if (inb(b.y0 + 1, b.x0, H, W)) v_sw = an[((long)(b.y0 + 1) * W + b.x0) * Cs + c];
       if (inb(b.y0 + 1, b.x0 + 1, H, W)) v_se = an[((long)(b.y0 + 1) * W + b.x0 + 1) * Cs + c];
-      const float wv = v_nw * b.nw + v_ne * b.ne + v_sw * b.sw + v_se * b.se;
+      const float wv = bilerp(v_nw, v_ne, v_sw, v_se, b.nw, b.ne, b.sw, b.se);
       const float e = m * (bimg[pix * Cs + c] - wv);
       acc += e * e;
       if (gout) {
@@ -199,11 +209,11 @@ __global__ void fbcheck_k(const float* __restrict__ ff, const float* __restrict_
     if (inb(b.y0, b.x0 + 1, H, W)) { a_ne = f0[(long)b.y0 * W + b.x0 + 1]; c_ne = f1[(long)b.y0 * W + b.x0 + 1]; }
     if (inb(b.y0 + 1, b.x0, H, W)) { a_sw = f0[(long)(b.y0 + 1) * W + b.x0]; c_sw = f1[(long)(b.y0 + 1) * W + b.x0]; }
     if (inb(b.y0 + 1, b.x0 + 1, H, W)) { a_se = f0[(long)(b.y0 + 1) * W + b.x0 + 1]; c_se = f1[(long)(b.y0 + 1) * W + b.x0 + 1]; }
-    w0 = a_nw * b.nw + a_ne * b.ne + a_sw * b.sw + a_se * b.se;
-    w1 = c_nw * b.nw + c_ne * b.ne + c_sw * b.sw + c_se * b.se;
+    w0 = bilerp(a_nw, a_ne, a_sw, a_se, b.nw, b.ne, b.sw, b.se);
+    w1 = bilerp(c_nw, c_ne, c_sw, c_se, b.nw, b.ne, b.sw, b.se);
   }
-  // torch.norm(., dim=1)**2 : sqrt of the sum of squares, then squared
-  auto n2 = [](float p, float q) { const float r = sqrtf(p * p + q * q); return r * r; };
+  // torch.norm(., dim=1)**2 : sqrt of the sum of squares (ATen's fused reduction), then squared
+  auto n2 = [](float p, float q) { const float r = sqrtf(fmaf(q, q, p * p)); return r * r; };
   const float nwb = n2(w0 + bu, w1 + bv);
   const float nw_ = n2(w0, w1);
   const float nb = n2(bu, bv);

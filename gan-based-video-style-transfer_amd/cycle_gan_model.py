@@ -203,7 +203,15 @@ class CycleGANModel(BaseModel):
         self.loss_cycle_B = networks.l1_loss(self.rec_B, self.real_B, lambda_B)
         self.loss_G = (self.loss_G_A + self.loss_G_B + self.loss_cycle_A + self.loss_cycle_B
                        + self.loss_idt_A + self.loss_idt_B + self.loss_G_T)
+        extra = self.extra_G_loss()
+        if extra is not None:
+            self.loss_G = self.loss_G + extra
         self.loss_G.backward()
+
+    def extra_G_loss(self):
+        """Hook for composed steps (cycle_gan_vgg_model.py, config C3): a term added to the total G
+        loss before its backward.  None for the CycleGANCon step itself."""
+        return None
 
     def optimize_parameters(self, grad_hook_G=None, grad_hook_D=None):
         """:218-232.  ``grad_hook_*`` (used by dp.py) run between backward and the optimizer step."""

@@ -1,0 +1,64 @@
+"""CycleGANVGGModel — config C3: the CycleGANCon train step plus a VGG-19 perceptual / Gram style
+loss on the temporally-warped frame's translation fake_B2 (CycleGAN + flow-warp
+temporal loss + VGG loss on Sintel frame pairs 1024x436, 1 GPU).  Model name 'cycle_gan_vgg'.
+
+The reference has no such step (ConGAN's VGG term is commented out:
+methods/GAN-based/ConGAN/models/cycle_gan_model.py:295-296), so the composition is the build's,
+made of reference pieces (the oracle oracle/c3_ref.py restates it; tests/golden/c3_small.npz pins it
+against the reference CycleGANCon model with the reference network.Vgg19 composed in):
+  vgg(x)   = Vgg19(normalize((x + 1) / 2))              network.py:45-78, fast_style_transfer.py:819-822
+  loss_G_C = lambda_content * mean((vgg(fake_B2)[relu4_1] - vgg(real_A2)[relu4_1])^2)
+  loss_G_S = lambda_style * sum_{relu1_1..relu5_1} mean((gram(vgg(fake_B2)_i) - gram(vgg(real_B)_i))^2)
+             gram = F F^T / (h*w) (fast_style_transfer.py:813-817); style target = the B-domain frame
+  loss_G  += loss_G_C + loss_G_S                        (CycleGANCon backward_G total, :204-216)
+VGG is frozen (network.py:69-70): its backward is the data gradient only; the targets run as
+inference.  Everything stays NHWC on the HIP kernels (perceptual.py): the (x + 1) / 2 and the
+ImageNet normalisation are one channel-normalise pass ((x / 2) - (mean - 1/2)) / std.
+Pretrained VGG weights cannot be fetched offline: the net initialises from `vgg_seed` and loads real
+weights with ``netVGG.load_state_dict`` (torchvision `features` keys via load_torchvision_features).
+"""
+import torch
+
+from . import ops, perceptual
+from .cycle_gan_model import CycleGANModel
+
+CONTENT_LEVEL = 3  # relu4_1
+
+
+class CycleGANVGGModel(CycleGANModel):
+    @staticmethod
+    def modify_commandline_options(parser, is_train=True):
+        parser = CycleGANModel.modify_commandline_options(parser, is_train)
+        if is_train:
+            parser.add_argument('--lambda_content', type=float, default=1.0, help='VGG-19 relu4_1 content weight')
+            parser.add_argument('--lambda_style', type=float, default=0.01,
+                                help='VGG-19 Gram style weight (seeded VGG: the Gram MSE is O(100))')
+            parser.add_argument('--vgg_seed', type=int, default=0, help='seed of the (non-pretrained) VGG-19')
+        return parser
+
+    def __init__(self, opt):
+        super().__init__(opt)
+        self.loss_names = self.loss_names + ['G_C', 'G_S']
+        self.netVGG = perceptual.Vgg19(seed=getattr(opt, 'vgg_seed', 0)).to(self.device)
+        mean, std = perceptual._mean_std(self.device)
+        self._vgg_mean, self._vgg_std = (mean - 0.5).contiguous(), std
+
+    def vgg_features(self, img_nhwc4):
+        """Vgg19(normalize((x + 1) / 2)) of an NHWC4 image in [-1, 1] -> 5 NHWC slice outputs."""
+        x = perceptual._NormalizeFn.apply(img_nhwc4, self._vgg_mean, self._vgg_std, 2.0, 3)
+        return self.netVGG.forward_nhwc(x)
+
+    def extra_G_loss(self):
+        if not self.temporal:
+            raise NotImplementedError('cycle_gan_vgg composes the temporal (CycleGANCon) step: lambda_T > 0')
+        f = self.vgg_features(self.fake_B2)
+        with torch.no_grad():
+            fc = self.vgg_features(self.real_A2)[CONTENT_LEVEL]
+            gs = [perceptual.gram_nhwc(t) for t in self.vgg_features(self.real_B)]
+        self.loss_G_C = perceptual.mse_loss(f[CONTENT_LEVEL], fc, self.opt.lambda_content)
+        style = None
+        for fi, gi in zip(f, gs):
+            term = perceptual.mse_loss(perceptual.gram_nhwc(fi), gi, self.opt.lambda_style)
+            style = term if style is None else style + term
+        self.loss_G_S = style
+        return self.loss_G_C + self.loss_G_S

@@ -3,13 +3,15 @@
 ``create_model(opt)`` instantiates the BaseModel subclass registered for ``opt.model``; like the
 reference, '<name>' maps to a class named '<Name>Model' (case-insensitive, underscores removed).
 The HIP build registers the hot-path plugin 'cycle_gan' (CycleGANCon semantics; ``--lambda_T 0``
-gives the plain CycleGAN step) and 'mogan' (MoGAN's motion-consistent step, mogan_model.py).
+gives the plain CycleGAN step), 'cycle_gan_vgg' (config C3: + VGG-19 content / Gram loss,
+cycle_gan_vgg_model.py) and 'mogan' (MoGAN's motion-consistent step, mogan_model.py).
 """
 from .base_model import BaseModel
 from .cycle_gan_model import CycleGANModel
+from .cycle_gan_vgg_model import CycleGANVGGModel
 from .mogan_model import MoGANModel
 
-_REGISTRY = {"cycle_gan": CycleGANModel, "mogan": MoGANModel}
+_REGISTRY = {"cycle_gan": CycleGANModel, "cycle_gan_vgg": CycleGANVGGModel, "mogan": MoGANModel}
 
 
 def find_model_using_name(model_name):

@@ -214,16 +214,17 @@ TILE_NAMES = {0: "128x128 (8 waves of 64x32)", 1: "128x64", 2: "128x128 (4 waves
               PLAN_RK: "fp32 [row][k] kernel", PLAN_SKINNY: "VALU skinny kernel"}
 
 
-def conv_plan_fwd(N, H, W, Cx, Cop, R, S, stride, pad_h, pad_w, math):
-    """Host-only query (vst_conv_plan_fwd): (tile kind, tail-split row) vst_conv2d_fwd would use for
-    this shape under `math` ('fp32' | 'bf16x3' | 'bf16x6', or a role of the current policy)."""
+def conv_plan_fwd(N, H, W, Cx, Cop, R, S, stride, pad_h, pad_w, math, with_tail=False):
+    """Host-only query (vst_conv_plan_fwd): (tile kind, tail-split row[, tail kind]) vst_conv2d_fwd
+    would use for this shape under `math` ('fp32' | 'bf16x3' | 'bf16x6', or a role of the current
+    policy)."""
     import ctypes
     from ._lib import MATH_MODES
     m = MATH_MODES[math] if math in MATH_MODES else _math(math)
-    kind, ms = ctypes.c_int(0), ctypes.c_int(0)
+    kind, ms, tk = ctypes.c_int(0), ctypes.c_int(0), ctypes.c_int(0)
     _call("vst_conv_plan_fwd", N, H, W, Cx, Cop, R, S, stride, pad_h, pad_w, m, ctypes.addressof(kind),
-          ctypes.addressof(ms))
-    return kind.value, ms.value
+          ctypes.addressof(ms), ctypes.addressof(tk))
+    return (kind.value, ms.value, tk.value) if with_tail else (kind.value, ms.value)
 
 
 def channel_sum(x, db, cl, accumulate=True):

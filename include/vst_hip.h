@@ -144,10 +144,10 @@ void vst_debug_set_tiles(int fprop, int tconv, int wgrad);
  * this shape and `math` on this thread.  *kind = split-arithmetic tile kind (0..8, see
  * vst_debug_set_tiles; 7 = 256x128), VST_PLAN_RK (fp32 [row][k] kernel) or VST_PLAN_SKINNY
  * (<= 4 output channels, VALU); *m_split = first output-pixel row of the wave-quantisation tail
- * launch (64x64 tiles), 0 when the grid runs as one launch. */
+ * launch, 0 when the grid runs as one launch; *tail_kind = that tail launch's tile kind (-1: none). */
 enum { VST_PLAN_RK = -1, VST_PLAN_SKINNY = -2 };
 int vst_conv_plan_fwd(int N, int H, int W, int Cx, int Cop, int R, int S, int stride, int pad_h,
-                      int pad_w, int math, int* kind, int* m_split);
+                      int pad_w, int math, int* kind, int* m_split, int* tail_kind);
 /* db[c] (+)= sum over NHW pixels of x[p][c] for c < Cl (channel stride Cs); bias gradient of a layer
  * whose output gradient is x.  ws: vst_channel_sum_ws_bytes bytes; fixed-order (deterministic). */
 size_t vst_channel_sum_ws_bytes(long NHW, int Cs);

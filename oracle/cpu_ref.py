@@ -195,6 +195,9 @@ class RefCycleGANCon:
         self.loss_cycle_B = (self.rec_B - self.real_B).abs().mean() * self.lB
         self.loss_G = (self.loss_G_A + self.loss_G_B + self.loss_cycle_A + self.loss_cycle_B
                        + self.loss_idt_A + self.loss_idt_B + self.loss_G_T)
+        extra = self.extra_G_loss()
+        if extra is not None:
+            self.loss_G = self.loss_G + extra
         self.loss_G.backward()
         if grad_hook_G is not None:
             grad_hook_G([self.G_A, self.G_B])
@@ -208,6 +211,10 @@ class RefCycleGANCon:
         if grad_hook_D is not None:
             grad_hook_D([self.D_A, self.D_B])
         self.opt_D.step()
+
+    def extra_G_loss(self):
+        """Hook for composed steps (oracle/c3_ref.py): a term added to loss_G before backward."""
+        return None
 
     @staticmethod
     def _backward_D(D, real, fake):

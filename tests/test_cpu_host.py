@@ -145,6 +145,8 @@ def test_conv_planner_picks_production_kernels():
     from gbvst import ops
     gbvst._lib.load()
     assert ops.conv_plan_fwd(8, 64, 64, 256, 256, 3, 3, 1, 1, 1, "bf16x6") == (7, 0)
+    # bf16x6 padded-frame dgrad (274 256x128 tiles): one whole round + a 64x64 tail launch
+    assert ops.conv_plan_fwd(8, 64, 64, 256, 256, 3, 3, 1, 2, 2, "bf16x6", with_tail=True) == (7, 32768, 8)
     kind, ms = ops.conv_plan_fwd(8, 64, 64, 256, 256, 3, 3, 1, 2, 2, "bf16x3")
     assert kind == 0 and ms == 2 * 256 // 2 * 128 and 0 < ms < 8 * 66 * 66
     assert ops.conv_plan_fwd(8, 64, 64, 256, 256, 3, 3, 1, 1, 1, "fp32") == (ops.PLAN_RK, 0)

@@ -1,0 +1,44 @@
+"""Developer A/B timing of the ResnetBlock conv kernels (N = KB_B frames, 64x64x256, 3x3 reflect)
+under the current VST_CONV_MATH policy: fprop, dgrad (stride-1 data gradient as a forward conv over
+the padded frame + fold), wgrad; HIP events on the launch stream, median of 5 x 20 launches.
+Run with VST_LIB_VARIANT=<variant .so> to compare builds (tools/build_variant.py)."""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+import gbvst  # noqa: E402
+from gbvst import ops  # noqa: E402
+
+gbvst._lib.load()
+dev = torch.device("cuda")
+out = {"lib": os.environ.get("VST_LIB_VARIANT", "default"), "math": ops.get_conv_math()}
+for B in [int(b) for b in os.environ.get("KB_B", "8,12").split(",")]:
+    H, C = 64, 256
+    x = torch.randn(B, H, H, C, device=dev)
+    w = torch.randn(C, C, 3, 3, device=dev) * 0.02
+    kc, ikf = ops.weight_pack(w, ops.PACK_FWD), ops.weight_pack(w, ops.PACK_IKF)
+    gy = torch.randn(B, H, H, C, device=dev)
+    dw = torch.zeros(C, C, 3, 3, device=dev)
+    flop = 2.0 * B * H * H * C * C * 9
+    fns = {"fprop": lambda: ops.conv2d_fwd(x, kc, None, C, 3, 3, 1, 1, "reflect"),
+           "dgrad": lambda: ops.conv2d_fwd(gy, ikf, None, C, 3, 3, 1, 2, "zero", role="bwd"),
+           "wgrad": lambda: ops.conv2d_wgrad(x, gy, dw, None, 3, 3, 1, 1, "reflect", C, C, C * 9, 9)}
+    for name, fn in fns.items():
+        for _ in range(5):
+            fn()
+        ts = []
+        for _ in range(5):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(20):
+                fn()
+            e1.record()
+            e1.synchronize()
+            ts.append(e0.elapsed_time(e1) / 20 * 1e3)
+        us = sorted(ts)[2]
+        out["%s_N%d_us" % (name, B)] = round(us, 1)
+        out["%s_N%d_TF" % (name, B)] = round(flop / us / 1e6, 1)
+print(json.dumps(out), flush=True)

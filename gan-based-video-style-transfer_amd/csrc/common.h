@@ -35,6 +35,15 @@ inline int check_launch(const char* what) {
     }                                     \
   } while (0)
 
+// XCD-aware tile order for a 1-D grid of T tiles.  Workgroups are dealt round-robin over the 8
+// XCDs (block L runs on XCD L % 8, MI355X_MICROARCH.md), so XCD x is given the contiguous tile range
+// [x*(T/8) + min(x, T%8), +T/8 + (x < T%8)): neighbouring tiles — the ones sharing operand rows —
+// run on one XCD and share its L2, for any T (a bijection on [0, T)).
+__device__ __forceinline__ int xcd_tile(int L, int T) {
+  const int x = L & 7, k = L >> 3, q = T >> 3, r = T & 7;
+  return x * q + (x < r ? x : r) + k;
+}
+
 __device__ __forceinline__ int reflect_idx(int i, int n) {
   // ReflectionPad2d index map: mirror without repeating the edge.
   i = i < 0 ? -i : i;

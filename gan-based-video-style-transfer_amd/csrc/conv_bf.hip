@@ -40,8 +40,8 @@
 #ifndef VST_BF_TAIL
 #define VST_BF_TAIL 1
 #endif
-#ifndef VST_BF_STORE_IN_MMA
-#define VST_BF_STORE_IN_MMA 1
+#ifndef VST_BF_SCHED
+#define VST_BF_SCHED 1
 #endif
 
 namespace vst {
@@ -108,49 +108,48 @@ __device__ __forceinline__ void split8(const float4& a, const float4& b, uint4 (
   }
 }
 
-// MMA over one staged K-step.  hook(g) runs before k group g (used to issue the next stage's loads).
-template <class T, class Hook>
-__device__ __forceinline__ void mma_stage(const char* __restrict__ As, const char* __restrict__ Bs,
-                                          f32x16 (&acc)[T::MI][T::NI], int wm0, int wn0, int lane,
-                                          Hook hook) {
-  constexpr int NP = T::NP;
-  const int kh = lane >> 5, li = lane & 31;
-  bf16x8_t fa[2][NP][T::MI], fb[2][NP][T::NI];
-  auto rd = [&](int buf, int g) {
-    const int c = 2 * g + kh;
+// One k group (16 deep) of a wave's operand fragments: NP planes x (MI A + NI B) bf16x8 per lane.
+template <class T>
+struct Frag {
+  bf16x8_t a[T::NP][T::MI], b[T::NP][T::NI];
+};
+
+// LDS -> registers: k group g of the stage image at st (lane l: row l % 32, 8-deep chunk 2g + l / 32).
+template <class T>
+__device__ __forceinline__ void read_frag(Frag<T>& f, const char* __restrict__ st, int g, int wm0, int wn0,
+                                          int lane) {
+  const char* As = st;
+  const char* Bs = st + T::A_BYTES;
+  const int c = 2 * g + (lane >> 5), li = lane & 31;
 #pragma unroll
-    for (int i = 0; i < T::MI; ++i) {
-      const int off = swz_off(wm0 + 32 * i + li, c, T::ROWB, T::SWS, T::KC - 1);
+  for (int i = 0; i < T::MI; ++i) {
+    const int off = swz_off(wm0 + 32 * i + li, c, T::ROWB, T::SWS, T::KC - 1);
 #pragma unroll
-      for (int p = 0; p < NP; ++p) fa[buf][p][i] = *reinterpret_cast<const bf16x8_t*>(As + p * T::A_PLANE + off);
-    }
+    for (int p = 0; p < T::NP; ++p) f.a[p][i] = *reinterpret_cast<const bf16x8_t*>(As + p * T::A_PLANE + off);
+  }
+#pragma unroll
+  for (int j = 0; j < T::NI; ++j) {
+    const int off = swz_off(wn0 + 32 * j + li, c, T::ROWB, T::SWS, T::KC - 1);
+#pragma unroll
+    for (int p = 0; p < T::NP; ++p) f.b[p][j] = *reinterpret_cast<const bf16x8_t*>(Bs + p * T::B_PLANE + off);
+  }
+}
+
+// The split products of one k group into the wave's accumulators.
+template <class T>
+__device__ __forceinline__ void mma_frag(const Frag<T>& f, f32x16 (&acc)[T::MI][T::NI]) {
+#pragma unroll
+  for (int i = 0; i < T::MI; ++i)
 #pragma unroll
     for (int j = 0; j < T::NI; ++j) {
-      const int off = swz_off(wn0 + 32 * j + li, c, T::ROWB, T::SWS, T::KC - 1);
-#pragma unroll
-      for (int p = 0; p < NP; ++p) fb[buf][p][j] = *reinterpret_cast<const bf16x8_t*>(Bs + p * T::B_PLANE + off);
-    }
-  };
-  rd(0, 0);
-#pragma unroll
-  for (int g = 0; g < T::BK / 16; ++g) {
-    const int cur = g & 1;
-    hook(g);
-    if (g + 1 < T::BK / 16) rd(cur ^ 1, g + 1);
-#pragma unroll
-    for (int i = 0; i < T::MI; ++i)
-#pragma unroll
-      for (int j = 0; j < T::NI; ++j) {
-#define VST_MF(pA, pB) \
-  acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[cur][pA][i], fb[cur][pB][j], acc[i][j], 0, 0, 0)
-        if constexpr (NP == 3) {
-          VST_MF(2, 0); VST_MF(0, 2); VST_MF(1, 1); VST_MF(1, 0); VST_MF(0, 1); VST_MF(0, 0);
-        } else {
-          VST_MF(1, 0); VST_MF(0, 1); VST_MF(0, 0);
-        }
-#undef VST_MF
+#define VST_MF(pA, pB) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[pA][i], f.b[pB][j], acc[i][j], 0, 0, 0)
+      if constexpr (T::NP == 3) {
+        VST_MF(2, 0); VST_MF(0, 2); VST_MF(1, 1); VST_MF(1, 0); VST_MF(0, 1); VST_MF(0, 0);
+      } else {
+        VST_MF(1, 0); VST_MF(0, 1); VST_MF(0, 0);
       }
-  }
+#undef VST_MF
+    }
 }
 
 // Stage writer: A rows as fp32 pairs (split here), B rows as pre-split planes.  Masked rows were
@@ -175,49 +174,93 @@ __device__ __forceinline__ void store_stage(char* st, const float4 (&ra)[T::A_LD
   }
 }
 
-// K loop with a two-deep load pipeline: the global loads of stage k + 2 are issued at the start of
-// stage k's MFMAs into the register set stage k vacated, and stage k + 1's registers (loaded one
-// whole stage earlier) are split and written to the other LDS buffer after stage k's MFMAs; one
-// barrier per stage.  load_all(set) loads the cursor's stage into register set `set`; adv() moves
-// the cursor one stage on.
+// Issue pattern of one k group's MFMAs (VST_BF_SCHED): each MFMA is followed by a share of the
+// group's other work, so the fragment reads, global loads, the split VALU and its ds_writes sit
+// in the MFMA gaps instead of in blocks the matrix pipe waits behind.  first: the group that also
+// issues the next loads and the stage store; the group after the barrier only reads fragments.
+template <class T>
+__device__ __forceinline__ void sched_group(bool first, bool after_barrier) {
+  constexpr int NM = T::MI * T::NI * (T::NP == 3 ? 6 : 3);     // MFMAs per k group
+  constexpr int NR = T::NP * (T::MI + T::NI);                   // ds_read_b128 per k group
+  constexpr int NV = T::A_LD * 2 + T::B_LD * T::NP;             // global loads per stage
+  constexpr int NW = T::A_LD * T::NP + T::B_LD * T::NP;         // ds_write_b128 per stage
+  if (first && !after_barrier) {
+    if (VST_BF_SCHED < 2) return;
+#pragma unroll
+    for (int i = 0; i < NM; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);          // MFMA
+      if (i < NR) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+      if (i < NV) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read
+      __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);          // VALU
+      if (i >= NM - NW - 1 && i < NM - 1) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // DS write
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < NM; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      if (i < NR) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+    }
+  }
+}
+
+// K loop with a two-deep global-load pipeline and LDS fragments read one k group ahead, across
+// the stage boundary.  Stage kt (LDS buffer P = kt & 1):
+//   group 0: read group 1's fragments; issue the global loads of stage kt + 2 into register set P;
+//            split + write stage kt + 1 (register set P ^ 1, loaded one stage earlier) into buffer
+//            P ^ 1; MFMAs of group 0 — the split VALU and ds_writes fill the MFMA gaps;
+//   last group: barrier (buffer P ^ 1 complete, every read of buffer P done), read stage kt + 1's
+//            group 0 from buffer P ^ 1 into the free fragment set, then this group's MFMAs, which
+//            cover that read's latency.
+// Every load and store is unconditional (the last two stages re-load the final stage's addresses
+// and write an LDS image nobody reads; the cursor stops advancing there): a conditional load
+// makes the wait-count pass merge "issued / not issued" paths and drain the whole prefetch
+// (vmcnt(0)) before each stage's stores.  load_all(set) loads the cursor's stage into register
+// set `set`; adv(go) moves the cursor one stage on when go.  An odd stage count runs its last stage after
+// the two-stage loop.
 template <class T, class LoadAll, class Adv>
 __device__ __forceinline__ void main_loop(char* smem, int nk, f32x16 (&acc)[T::MI][T::NI],
                                           float4 (&ra)[2][T::A_LD][2], u32x4_t (&rbv)[2][T::B_LD][T::NP],
                                           int rb, int kq, LoadAll load_all, Adv adv) {
+  constexpr int G = T::BK / 16;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int wm0 = (wave / T::WAVES_N) * T::WM, wn0 = (wave % T::WAVES_N) * T::WN;
   if (nk <= 0) return;
   load_all(0);
   store_stage<T>(smem, ra[0], rbv[0], rb, kq);
-  if (nk > 1) {
-    adv();
-    load_all(1);
-  }
+  adv(nk > 1);
+  load_all(1);
   __syncthreads();
-  // Stage k+1's image (registers loaded one stage earlier) is split and written to the other LDS
-  // buffer from inside stage k's MFMA stream (before its last k group): that buffer's previous
-  // contents (stage k-1) were released by the barrier that ended stage k-1, so the split VALU and
-  // ds_writes fill the gaps between this stage's MFMAs instead of forming a bubble before the
-  // barrier (VST_BF_STORE_IN_MMA=0: the store after the MFMAs).
-  auto step = [&](int kt, auto par) {
+  Frag<T> fr[2];
+  read_frag<T>(fr[0], smem, 0, wm0, wn0, lane);
+  auto step = [&](int kt, auto par) __attribute__((always_inline)) {
     constexpr int P = decltype(par)::value;
-    char* cur = smem + P * T::STAGE;
-    mma_stage<T>(cur, cur + T::A_BYTES, acc, wm0, wn0, lane, [&](int g) {
-      if (g == 0 && kt + 2 < nk) {
-        adv();
+    const char* cur = smem + P * T::STAGE;
+    char* nxt = smem + (P ^ 1) * T::STAGE;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int fi = (P * G + g) & 1;
+      if (g + 1 < G) read_frag<T>(fr[fi ^ 1], cur, g + 1, wm0, wn0, lane);
+      if (g == 0) {
+        adv(kt + 2 < nk);
         load_all(P);
+        store_stage<T>(nxt, ra[P ^ 1], rbv[P ^ 1], rb, kq);
       }
-      if (VST_BF_STORE_IN_MMA && g == T::BK / 16 - 1 && kt + 1 < nk)
-        store_stage<T>(smem + (P ^ 1) * T::STAGE, ra[P ^ 1], rbv[P ^ 1], rb, kq);
-    });
-    if (!VST_BF_STORE_IN_MMA && kt + 1 < nk)
-      store_stage<T>(smem + (P ^ 1) * T::STAGE, ra[P ^ 1], rbv[P ^ 1], rb, kq);
-    __syncthreads();
+      if (g == G - 1) {
+        __builtin_amdgcn_sched_barrier(0);  // keep this group's MFMAs after the barrier (they cover the read)
+        __syncthreads();
+        read_frag<T>(fr[fi ^ 1], nxt, 0, wm0, wn0, lane);
+      }
+      mma_frag<T>(fr[fi], acc);
+      if (VST_BF_SCHED) sched_group<T>(g == 0, g == G - 1);
+    }
   };
-  for (int kt = 0; kt < nk; kt += 2) {
+  int kt = 0;
+  for (; kt + 1 < nk; kt += 2) {
     step(kt, std::integral_constant<int, 0>());
-    if (kt + 1 < nk) step(kt + 1, std::integral_constant<int, 1>());
+    step(kt + 1, std::integral_constant<int, 1>());
   }
+  if (kt < nk) step(kt, std::integral_constant<int, 0>());
 }
 
 template <int MI, int NI>
@@ -235,13 +278,12 @@ __device__ __forceinline__ int remap_mtile(int bx, int nx) {
   return (bx & 7) * (nx >> 3) + (bx >> 3);
 }
 
-// XCD-aware tile order for a 1-D grid of Mt*Nt tiles.  Consecutive workgroup ids land on
-// consecutive XCDs, so XCD x (= L % 8) gets the contiguous tile range [x*T/8, (x+1)*T/8) in
+// XCD-aware tile order for a 1-D grid of Mt*Nt tiles (xcd_tile, common.h).  Consecutive workgroup
+// ids land on consecutive XCDs, so XCD x (= L % 8) gets a contiguous ~T/8 tile range in
 // (m-major, n-minor) order: the N-tiles that share an A row block run together on one XCD and the
 // XCD's resident working set is (CUs per XCD / Nt) M-tiles of activations, which stays in its L2.
 __device__ __forceinline__ void tile_of(int L, int Mt, int Nt, int& mt, int& nt) {
-  const int T = Mt * Nt;
-  const int t = (T & 7) ? L : (L & 7) * (T >> 3) + (L >> 3);
+  const int t = xcd_tile(L, Mt * Nt);
   mt = t / Nt;
   nt = t - mt * Nt;
 }
@@ -351,15 +393,21 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_k(
       for (int p = 0; p < NP; ++p) rbv[set][j][p] = *reinterpret_cast<const u32x4_t*>(wrow[j] + p * wps + kb);
     }
   };
-  auto adv = [&]() __attribute__((always_inline)) {
+  // go = false (the last two stages): the cursor stays on the final stage.  KSL: branch-free
+  // (scalar selects), so the stage body stays one basic block for the scheduler.
+  auto adv = [&](bool go) __attribute__((always_inline)) {
     if (KSL) {
-      if (++ts == S) {
-        ts = 0;
-        if (++tr == Rk) { tr = 0; ksb += T::BK; }
-      }
+      const int ts1 = ts + 1;
+      const bool w1 = ts1 == S;
+      const int tr1 = tr + (w1 ? 1 : 0);
+      const bool w2 = w1 && tr1 == Rk;
+      ts = go ? (w1 ? 0 : ts1) : ts;
+      tr = go ? (w2 ? 0 : tr1) : tr;
+      ksb = go ? ksb + (w2 ? T::BK : 0) : ksb;
       tap_rows(tr, ts);
       return;
     }
+    if (!go) return;
     kcur += T::BK;
     kc += T::BK;
     if (kc >= C) {
@@ -416,8 +464,7 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_wgrad_bf_k(
   const int Mt = (Mw + T::BM - 1) / T::BM, Nt = (Cyp + T::BN - 1) / T::BN, Zt = (P + chunk - 1) / chunk;
   int mx, ny, zz;
   {
-    const int L = blockIdx.x, Tt = Mt * Nt * Zt;
-    const int tt = (Tt & 7) ? L : (L & 7) * (Tt >> 3) + (L >> 3);
+    const int tt = xcd_tile(blockIdx.x, Mt * Nt * Zt);
     zz = tt / (Mt * Nt);
     const int rem = tt - zz * Mt * Nt;
     ny = rem / Mt;
@@ -477,7 +524,8 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_wgrad_bf_k(
       for (int p = 0; p < NP; ++p) rbv[set][j][p] = *reinterpret_cast<const u32x4_t*>(q + p * ps);
     }
   };
-  auto adv = [&]() __attribute__((always_inline)) {
+  auto adv = [&](bool go) __attribute__((always_inline)) {
+    if (!go) return;
     kp += T::BK;
     pwo += T::BK;
     poff += T::BK;

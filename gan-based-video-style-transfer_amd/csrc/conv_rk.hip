@@ -551,8 +551,7 @@ __global__ __launch_bounds__((Tile<BM, BN, WM, WN, BK, MATH>::NT), 2) void conv_
   const int Mt = (Mw + BM - 1) / BM, Nt = (Cyp + BN - 1) / BN, Zt = (P + chunk - 1) / chunk;
   int mx, ny, zz;
   {
-    const int L = blockIdx.x, Tt = Mt * Nt * Zt;
-    const int tt = (Tt & 7) ? L : (L & 7) * (Tt >> 3) + (L >> 3);
+    const int tt = xcd_tile(blockIdx.x, Mt * Nt * Zt);
     zz = tt / (Mt * Nt);
     const int rem = tt - zz * Mt * Nt;
     ny = rem / Mt;

@@ -136,3 +136,109 @@ class FC2Loader:
         for t in out:  # allocated on the copy stream, consumed on this one
             t.record_stream(cur)
         return out
+
+
+# --------------------------------------------------------------- StarGAN FC2 7-tuple (C4)
+class _AttrDict(dict):
+    """munch.Munch stand-in (attribute access to a dict; munch is not installed)."""
+
+    def __getattr__(self, k):
+        try:
+            return self[k]
+        except KeyError as e:
+            raise AttributeError(k) from e
+
+
+class StarGANDatasetFC2(torch.utils.data.Dataset):
+    """methods/GAN-based/StarGAN/sg2_core/data_loader.py:217-293 DatasetFC2: for every source image
+    and style pair (src, ref) in {(0, 0)} + {(0, i), (i, 0), (i, i)} for styles i = 1..num_dom-1, the
+    7-tuple (src_img, src_img2, src_lbl, ref_img, ref_lbl, mask, flow): the source frame in style
+    src_lbl (style_dir), its second frame (temp_dir, '<name>_2.jpg'), the reference frame in style
+    ref_lbl, and mask / flow from the FC2 .npy block (channels 6:7 / 7:9, moved to CHW).  Paths are
+    joined by string concatenation as the reference does (directories end with '/').  The list is
+    shuffled once with random.seed(1234) (:291-292); base_len: the per-style image count the
+    reference asserts (22208 for FC2; None skips the check)."""
+
+    def __init__(self, data_dir, style_dir, temp_dir, transform=None, num_dom=4, base_len=22208):
+        from .sintel_eval import sintel_transform
+        self.data_dir, self.style_dir, self.temp_dir = data_dir, style_dir, temp_dir
+        self.transform = transform or sintel_transform
+        self.num_dom, self.base_len = num_dom, base_len
+        self.dataset, self.styles = [], []
+        self.preprocess()
+        self.num_images = len(self.dataset)
+
+    def preprocess(self):
+        style_list = sorted(os.listdir(self.style_dir))[:self.num_dom]
+        for sty in style_list:
+            n = len(os.listdir(self.style_dir + sty))
+            if self.base_len is not None:
+                assert self.base_len == n, (self.base_len, n)
+            self.styles.append(sty)
+        for img in sorted(os.listdir(self.style_dir + style_list[0])):
+            file = "/" + img
+            self.dataset.append([file, 0, 0])
+            for i in range(len(style_list) - 1):
+                self.dataset.append([file, 0, i + 1])
+                self.dataset.append([file, i + 1, 0])
+                self.dataset.append([file, i + 1, i + 1])
+        random.seed(1234)
+        random.shuffle(self.dataset)
+
+    def __getitem__(self, index):
+        from PIL import Image
+        file, src_lbl, ref_lbl = self.dataset[index]
+        src_img = self.transform(Image.open(self.style_dir + self.styles[src_lbl] + file))
+        src_img2 = self.transform(Image.open(self.temp_dir + self.styles[src_lbl] + file[:-4] + "_2.jpg"))
+        ref_img = self.transform(Image.open(self.style_dir + self.styles[ref_lbl] + file))
+        np_data = np.load(self.data_dir + file[:-4] + ".npy", allow_pickle=False)[0]
+        mask = torch.from_numpy(np.ascontiguousarray(np.moveaxis(np_data[:, :, 6:7], 2, 0)))
+        flow = torch.from_numpy(np.ascontiguousarray(np.moveaxis(np_data[:, :, 7:9], 2, 0)))
+        return (src_img, src_img2, torch.tensor(src_lbl, dtype=torch.long), ref_img,
+                torch.tensor(ref_lbl, dtype=torch.long), mask, flow)
+
+    def __len__(self):
+        return self.num_images
+
+
+def get_loaderFC2(data_dir, style_dir, temp_dir, batch_size=4, num_workers=0, num_dom=2, mode="train",
+                  base_len=22208):
+    """sg2_core/data_loader.py:295-317: ToTensor + Normalize(0.5) transform, 97 % / 3 % random split,
+    shuffling DataLoaders; returns (train_loader, eval_loader)."""
+    full = StarGANDatasetFC2(data_dir, style_dir, temp_dir, None, num_dom, base_len)
+    train_size = int(0.97 * len(full))
+    train_ds, eval_ds = torch.utils.data.random_split(full, [train_size, len(full) - train_size])
+    mk = lambda ds: torch.utils.data.DataLoader(ds, batch_size=batch_size, shuffle=True,  # noqa: E731
+                                                num_workers=num_workers)
+    return mk(train_ds), mk(eval_ds)
+
+
+class FC2Fetcher:
+    """sg2_core/data_loader.py:321-348: endless iterator over an FC2 loader; each item is the 7-tuple
+    plus latent codes z_trg, z_trg2 ~ N(0, 1) [B, latent_dim], all on the device, as an attribute dict
+    (x_src, x2_src, y_src, x_ref, y_ref, mask, flow, z_trg, z_trg2)."""
+
+    def __init__(self, loader, loader_ref=None, latent_dim=16, mode='', device=None):
+        self.loader, self.latent_dim, self.mode = loader, latent_dim, mode
+        self.device = device or torch.device('cuda' if torch.cuda.is_available() else 'cpu')
+        self.iter = None
+
+    def _fetch_inputs_fc2(self):
+        try:
+            if self.iter is None:
+                raise StopIteration
+            return next(self.iter)
+        except StopIteration:
+            self.iter = iter(self.loader)
+            return next(self.iter)
+
+    def __iter__(self):
+        return self
+
+    def __next__(self):
+        src_img, src_img2, src_lbl, ref_img, ref_lbl, mask, flow = self._fetch_inputs_fc2()
+        z_trg = torch.randn(src_img.size(0), self.latent_dim)
+        z_trg2 = torch.randn(src_img.size(0), self.latent_dim)
+        inputs = dict(x_src=src_img, x2_src=src_img2, y_src=src_lbl, x_ref=ref_img, y_ref=ref_lbl,
+                      mask=mask, flow=flow, z_trg=z_trg, z_trg2=z_trg2)
+        return _AttrDict({k: v.to(self.device) for k, v in inputs.items()})

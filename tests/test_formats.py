@@ -93,3 +93,47 @@ def test_fc2_unpack_bit_exact(tmp_path):
     assert torch.equal(got, formats_ref.u8_image(lv[0].numpy()))
     with pytest.raises(RuntimeError):
         ops.u8_image_to_nhwc4(lv)
+
+
+def test_stargan_fc2_seven_tuple(tmp_path):
+    """StarGAN's FC2 7-tuple loader (sg2_core/data_loader.py:217-348): dataset order (style pairs,
+    random.seed(1234) shuffle), the item tuple (frames through ToTensor + Normalize(0.5), labels,
+    mask / flow from the .npy block in CHW), the 97/3 split and the fetcher's attribute dict."""
+    import random
+
+    import numpy as np
+    from PIL import Image
+
+    from gbvst import fc2
+    rng = np.random.default_rng(3)
+    data, sty, tmp = tmp_path / "npy", tmp_path / "style", tmp_path / "temp"
+    H, W, names, styles = 8, 12, ["a.jpg", "b.jpg", "c.jpg"], ["s0", "s1", "s2"]
+    os.makedirs(data)
+    for n in names:
+        np.save(data / (n[:-4] + ".npy"), rng.random((1, H, W, 9)).astype(np.float32))
+        for s in styles:
+            for d, suffix in ((sty, ""), (tmp, "_2")):
+                os.makedirs(d / s, exist_ok=True)
+                Image.fromarray(rng.integers(0, 256, (H, W, 3), dtype=np.uint8)).save(d / s / (n[:-4] + suffix + ".jpg"))
+    ds = fc2.StarGANDatasetFC2(str(data) + "/", str(sty) + "/", str(tmp) + "/", num_dom=3, base_len=3)
+    expect = []
+    for n in names:
+        expect.append(["/" + n, 0, 0])
+        for i in range(2):
+            expect += [["/" + n, 0, i + 1], ["/" + n, i + 1, 0], ["/" + n, i + 1, i + 1]]
+    random.seed(1234)
+    random.shuffle(expect)
+    assert ds.dataset == expect and len(ds) == 21
+    src, src2, sl, ref, rl, mask, flow = ds[0]
+    f, s_l, r_l = expect[0]
+    raw = np.load(data / (f[1:-4] + ".npy"))[0]
+    assert src.shape == (3, H, W) and src2.shape == (3, H, W) and ref.shape == (3, H, W)
+    assert int(sl) == s_l and int(rl) == r_l
+    assert np.array_equal(mask.numpy(), np.moveaxis(raw[:, :, 6:7], 2, 0))
+    assert np.array_equal(flow.numpy(), np.moveaxis(raw[:, :, 7:9], 2, 0))
+    img = np.asarray(Image.open(str(sty) + "/" + styles[s_l] + f).convert("RGB"))
+    assert torch.equal(src, (torch.from_numpy(img.copy()).permute(2, 0, 1).float() / 255 - 0.5) / 0.5)
+    tr, ev = fc2.get_loaderFC2(str(data) + "/", str(sty) + "/", str(tmp) + "/", batch_size=2, num_dom=3, base_len=3)
+    assert len(tr.dataset) == int(0.97 * 21) and len(ev.dataset) == 21 - int(0.97 * 21)
+    batch = next(fc2.FC2Fetcher(tr, latent_dim=16, device=torch.device("cpu")))
+    assert batch.x_src.shape == (2, 3, H, W) and batch.z_trg.shape == (2, 16) and batch.flow.shape == (2, 2, H, W)

@@ -6,7 +6,9 @@
     C3 frame size 1x3x436x1024: generator forward, flow-warp temporal loss, VGG-19 slices, Grams and
     the composed content / style loss terms.
 Tolerances: north_star's 1e-3 relative on losses / stylised frames; later steps within max(1e-3,
-3x the deviation an fp64 run of the same algorithm shows from the fp32 reference)."""
+3x the deviation the reference's own result shows under an fp64 run of the same algorithm or a 1e-6
+relative weight perturbation — Adam's early steps are ~lr*sign(g), so rounding-level gradient
+differences move near-zero parameters by 2*lr)."""
 import numpy as np
 import pytest
 import torch
@@ -23,14 +25,19 @@ def gb():
     return gbvst
 
 
-def _oracle(g, dtype):
+def _oracle(g, dtype, perturb=0.0):
+    """The C3 oracle run of the fixture; perturb: scale every G/D weight by (1 + perturb * N(0,1)) —
+    a change of the size any other fp32 summation order makes to the forward."""
     from oracle import c3_ref, cpu_ref, prng, style_ref
     m = c3_ref.RefCycleGANConVGG(ngf=8, ndf=8)
     style_ref.load_np(m.vgg, style_ref.vgg_weights(m.vgg, 530))
     m.vgg.to(dtype)
     for name, seed in SEEDS.items():
         net = m.nets()[name]
-        cpu_ref.load_np_state(net, prng.init_state_dict(cpu_ref.state_shapes(net), base_seed=seed))
+        sd = prng.init_state_dict(cpu_ref.state_shapes(net), base_seed=seed)
+        if perturb:
+            sd = {k: (v * (1 + perturb * prng.normal(seed + 17, v.shape))).astype(np.float32) for k, v in sd.items()}
+        cpu_ref.load_np_state(net, sd)
         net.to(dtype)
     m.opt_G = torch.optim.Adam(list(m.G_A.parameters()) + list(m.G_B.parameters()), lr=2e-4, betas=(0.5, 0.999))
     m.opt_D = torch.optim.Adam(list(m.D_A.parameters()) + list(m.D_B.parameters()), lr=2e-4, betas=(0.5, 0.999))
@@ -66,7 +73,8 @@ def test_c3_step_vs_reference_golden(gb, golden, train_math):
     assert names == m.loss_names
     ref = g["losses"]
     l64, p64 = _oracle(g, torch.float64)
-    band = (np.abs(l64 - ref) / np.abs(ref)).max(axis=1)
+    lp, pp = _oracle(g, torch.float32, perturb=1e-6)
+    band = np.maximum(np.abs(l64 - ref), np.abs(lp - ref)).__truediv__(np.abs(ref)).max(axis=1)
     data = tuple(torch.from_numpy(g[k]) for k in ("real_A", "real_A2", "real_B"))
     data = data + (None, torch.from_numpy(g["mask"]), torch.from_numpy(g["flow"]))
     for s in range(ref.shape[0]):
@@ -78,8 +86,10 @@ def test_c3_step_vs_reference_golden(gb, golden, train_math):
         assert rel.max() <= tol, (s, dict(zip(names, rel)), band[s])
     with torch.no_grad():
         out = m.forward_eval(torch.from_numpy(g["probe"])).double().cpu().numpy()
-    dev64 = np.abs(p64 - g["probe_out"]).max()
-    assert np.abs(out - g["probe_out"]).max() <= max(1e-3, 3 * dev64)
+    # after two Adam steps (~lr * sign(g) each) the reference's own output moves this much under an
+    # fp64 run or a 1e-6 weight perturbation; the HIP run must stay within 3x that band
+    dev = max(np.abs(p64 - g["probe_out"]).max(), np.abs(pp - g["probe_out"]).max())
+    assert np.abs(out - g["probe_out"]).max() <= max(1e-3, 3 * dev), (np.abs(out - g["probe_out"]).max(), dev)
 
 
 @pytest.mark.timeout(600)

@@ -127,7 +127,9 @@ def conv_roofline(name, probe, math):
         note = ("stride-1 data gradient as a forward conv over the rotated taps (66x66 padded frame)"
                 if name == "resblock_dgrad" else "ResnetBlock conv forward")
     else:
-        kernel = "vst_conv2d_wgrad (channel-major copies + conv_wgrad_rk_k + split-K sum/store), %s" % m
+        kernel = ("vst_conv2d_wgrad: nhwc_to_cp_pad_k + nhwc_to_cp_planes_k copies + conv_wgrad_bf_k "
+                  "(split-K slabs) + wgrad_reduce_store_k, %s" % m if m != "fp32" else
+                  "vst_conv2d_wgrad: channel-major copies + conv_wgrad_rk_k + wgrad_reduce_store_k, fp32")
         key = {"math": m, "N": N}
         note = "whole weight-gradient op: its 4-5 launches are timed together"
     return {"kernel": kernel, "what": note + " — ResnetBlock 3x3 reflect 256->256 @64x64, N=%d" % N,
@@ -479,8 +481,11 @@ def main():
     }
     if rank == 0 and not args.no_extras:
         rl = {k: conv_roofline(k, p, args.math) for k, p in probes.items()}
-        dom = max(rl, key=lambda k: rl[k]["ms_per_step"] if rl[k] else -1)
-        out["roofline"] = rl[dom]
+        # the dominant kernel of the step is conv_fprop_bf_k<256x128> (its forward AND stride-1
+        # data-gradient launches: ~22 ms of the ~72 ms step, profiles/r02_*); its roofline line is
+        # the forward launch (one kernel, whole CU rounds, no tail); the dgrad / wgrad ops (with their
+        # tail / copy / reduce launches) are in roofline_convs
+        out["roofline"] = rl["resblock_fprop"] or next(v for v in rl.values() if v)
         out["roofline_convs"] = rl
         out["inference"] = inference_fps(device)
     if rank == 0 and world == 1 and not args.no_extras:

@@ -26,7 +26,7 @@
 //                  addend fused in the epilogue
 //   conv_wgrad_k : dw = x_gather^T * dy       m = (r, s, ci), n = out channel, k = pixel;
 //                  split-K over blockIdx.z into an fp32 slab, summed in a fixed split order
-//                  (deterministic) by wgrad_sum_k and written to [Co][Ci][R][S] by wgrad_store_k.
+//                  (deterministic) and written to [Co][Ci][R][S] by wgrad_reduce_store_k.
 #include "common.h"
 
 namespace vst {
@@ -554,37 +554,46 @@ __global__ __launch_bounds__((Tile<BM, BN, WM, WN>::NT), 2) void conv_wgrad_k(
 }
 
 // slab[0][m][n] = sum_z slab[z][m][n] (fixed order), float4 over n: coalesced and fully parallel.
-__global__ void wgrad_sum_k(float* __restrict__ slab, long n4, int nsplit) {
-  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n4) return;
-  float4* s = reinterpret_cast<float4*>(slab);
-  float4 a = s[i];
-  for (int z = 1; z < nsplit; ++z) add4(a, s[i + (long)z * n4]);
-  s[i] = a;
-}
-
-// dw[co*so + ci*si + rs] (+)= sum_z S_z[rs*Cx + ci][co] via a 64x64 LDS transpose tile whose rows
-// are 64 consecutive (ci, rs) of dw's own order (reads coalesced along co, writes contiguous along
-// ci*RS + rs for the dense [Co][Ci][R][S] layout).  nsplit > 1 folds the split-K slabs (stride zs)
-// in the load, in wgrad_sum_k's order (z = 0, 1, 2, ...), so the sums are bit-identical.
-__global__ void wgrad_store_k(const float* __restrict__ S, float* __restrict__ dw, int Cx, int Cyp, int RS,
-                              int Co, int Ci, long so, long si, int accumulate, int nsplit, long zs) {
+// The split-K reduction and the store in one pass: a 64 (ci, rs) x 64 co tile per block, each thread
+// summing 4 float4 column quads over the nsplit slabs (all slab loads of a quad issued back to back,
+// z = 0, 1, 2, ...: a fixed order, so deterministic), then an LDS transpose and the [Co][Ci][R][S]
+// store (+= across the step's passes).  One launch instead of a slab-sized sum pass + a store pass.
+__global__ __launch_bounds__(256) void wgrad_reduce_store_k(const float* __restrict__ S, float* __restrict__ dw,
+                                                            int Cx, int Cyp, int RS, int Co, int Ci, long so,
+                                                            long si, int accumulate, int nsplit, long zs) {
   __shared__ float tile[64][65];
   const int m0 = blockIdx.x * 64, c0 = blockIdx.y * 64;
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int t = threadIdx.x, c4 = (t & 15) * 4, r0 = t >> 4;
   const int Md = Ci * RS;
-  for (int r = ty; r < 64; r += 4) {
-    const int md = m0 + r, c = c0 + tx;
-    float v = 0.f;
-    if (md < Md && c < Cyp) {
-      const int ci = md / RS, rs = md - ci * RS;
-      const float* src = S + (long)(rs * Cx + ci) * Cyp + c;
-      v = src[0];
-      for (int z = 1; z < nsplit; ++z) v += src[(long)z * zs];
-    }
-    tile[r][tx] = v;
+  float4 acc[4];
+  const float* src[4];
+  bool ok[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int md = m0 + r0 + 16 * i;
+    ok[i] = md < Md && c0 + c4 < Cyp;
+    const int mm = ok[i] ? md : 0;
+    const int ci = mm / RS, rs = mm - ci * RS;
+    src[i] = S + (long)(rs * Cx + ci) * Cyp + (ok[i] ? c0 + c4 : 0);
+    acc[i] = ok[i] ? *reinterpret_cast<const float4*>(src[i]) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  for (int z = 1; z < nsplit; ++z) {
+    float4 v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = *reinterpret_cast<const float4*>(src[i] + (ok[i] ? (long)z * zs : 0));
+#pragma unroll
+    for (int i = 0; i < 4; ++i) add4(acc[i], v[i]);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = r0 + 16 * i;
+    tile[r][c4] = acc[i].x;
+    tile[r][c4 + 1] = acc[i].y;
+    tile[r][c4 + 2] = acc[i].z;
+    tile[r][c4 + 3] = acc[i].w;
   }
   __syncthreads();
+  const int tx = t & 63, ty = t >> 6;
   for (int r = ty; r < 64; r += 4) {
     const int c = c0 + r, md = m0 + tx;
     if (c >= Co || md >= Md) continue;
@@ -939,15 +948,9 @@ extern "C" int vst_conv2d_wgrad(const float* x, const float* dy, float* dw, floa
 #undef VST_WG
   int rc = check_launch("conv2d_wgrad");
   if (rc) return rc;
-  // split-K slabs: one streaming sum pass first (a fold inside the store serialises its loads)
-  const bool fold = p.nsplit <= 1;
-  if (p.nsplit > 1 && !fold) {
-    const long n4 = (long)p.Mw * Cyp / 4;
-    hipLaunchKernelGGL(wgrad_sum_k, dim3(ceil_div(n4, 256)), dim3(256), 0, s, ws, n4, p.nsplit);
-  }
-  hipLaunchKernelGGL(wgrad_store_k, dim3(ceil_div(Ci * R * S, 64), ceil_div(Co, 64)), dim3(256), 0, s, ws,
-                     dw, Cx, Cyp, R * S, Co, Ci, so, si, accumulate, fold ? p.nsplit : 1,
-                     (long)p.Mw * Cyp);
+  // split-K slabs: summed in slab order and stored transposed in one pass
+  hipLaunchKernelGGL(wgrad_reduce_store_k, dim3(ceil_div(Ci * R * S, 64), ceil_div(Co, 64)), dim3(256), 0, s,
+                     ws, dw, Cx, Cyp, R * S, Co, Ci, so, si, accumulate, p.nsplit, (long)p.Mw * Cyp);
   return check_launch("conv2d_wgrad_reduce");
 }
 

@@ -43,6 +43,9 @@
 #ifndef VST_BF_SCHED
 #define VST_BF_SCHED 1
 #endif
+#ifndef VST_BF_PRIO
+#define VST_BF_PRIO 0
+#endif
 
 namespace vst {
 namespace bf {
@@ -226,6 +229,9 @@ __device__ __forceinline__ void main_loop(char* smem, int nk, f32x16 (&acc)[T::M
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int wm0 = (wave / T::WAVES_N) * T::WM, wn0 = (wave % T::WAVES_N) * T::WN;
   if (nk <= 0) return;
+  // second-dispatched half of the waves: static priority 1 (it otherwise loses every issue
+  // arbitration to its older partner on the SIMD; MI355X_MICROARCH.md, two waves per SIMD, item 4)
+  if (VST_BF_PRIO && wave >= T::NW / 2) __builtin_amdgcn_s_setprio(1);
   load_all(0);
   store_stage<T>(smem, ra[0], rbv[0], rb, kq);
   adv(nk > 1);
@@ -624,7 +630,9 @@ __global__ void split3_k(const float* __restrict__ w, __bf16* __restrict__ out, 
 //   0: 128x128, 8 waves of 64x32, BK 32      1: 128x64, 4 waves of 64x32, BK 32 (2 blocks / CU)
 //   2: 128x128, 4 waves of 64x64, BK 32      3: 64x128, 4 waves of 32x64, BK 32
 //   4: 128x128, 8 waves of 64x32, BK 64      5: 128x64, 4 waves of 64x32, BK 64
-//   6: 64x64, 4 waves of 32x32, BK 32
+//   6: 64x64, 4 waves of 32x32, BK 32      7: 256x128, 8 waves of 64x64, BK 32
+//   8: 64x64, 4 waves of 32x32, BK 32 (x6) / 64 (x3)
+//   9: 128x128, 4 waves of 64x64, BK 16 (x6: two blocks / CU)
 #define VST_BF_DISPATCH(kind, np, L)                                   \
   switch (kind) {                                                      \
     case 1: L(128, 64, 64, 32, 32, np) break;                          \
@@ -635,11 +643,12 @@ __global__ void split3_k(const float* __restrict__ w, __bf16* __restrict__ out, 
     case 6: L(64, 64, 32, 32, 32, np) break;                           \
     case 7: L(256, 128, 64, 64, 32, np) break;                         \
     case 8: L(64, 64, 32, 32, (np == 3 ? 32 : 64), np) break;          \
+    case 9: L(128, 128, 64, 64, 16, np) break;                         \
     default: L(128, 128, 64, 32, 32, np) break;                        \
   }
 
 int bf_pick(long M, int Nc, int override_kind) {
-  if (override_kind >= 0 && override_kind <= 8) return override_kind;
+  if (override_kind >= 0 && override_kind <= 9) return override_kind;
   if (Nc <= 64) return M / 128 >= 256 ? 1 : 6;
   const long n128 = (Nc + 127) / 128;
   if ((M / 128) * n128 >= 200) return 0;
@@ -659,6 +668,7 @@ static void bf_geom(int kind, int np, int* bm, int* bn, int* slots) {
     case 6: BM = 64; BN = 64; break;
     case 7: BM = 256; break;
     case 8: BM = 64; BN = 64; BK = np == 3 ? 32 : 64; break;
+    case 9: BK = 16; break;
     default: break;
   }
   const int stage = np * (BM + BN) * BK * 2;

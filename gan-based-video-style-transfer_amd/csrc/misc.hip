@@ -35,14 +35,10 @@ __global__ void nhwc_to_nchw_k(const float* __restrict__ x, float* __restrict__ 
   y[i] = x[(n * HW + p) * Cs + c];
 }
 
-// w[O][I][R][S] -> KC: out[r][s][i][o] (Ip x Op per tap) or CK: out[r][s][o][i] (Op x Ip per tap)
-__global__ void weight_pack_k(const float* __restrict__ w, float* __restrict__ out, int O, int I,
-                              int R, int S, int Op, int Ip, int mode, long total,
-                              __bf16* __restrict__ split = nullptr) {
-  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= total) return;
-  const int RS = R * S;
-  int o, i, rs;
+// Element idx of a pack of the logical weight w[O][I][R][S] -> its (o, i, tap) coordinates.
+// KC: out[r][s][i][o] (Ip x Op per tap), CK: out[r][s][o][i] (Op x Ip per tap), OK: out[o][r][s][i],
+// IK / IKF: out[i][r][s][o] (IKF: taps rotated 180 deg).
+__device__ __forceinline__ void pack_coords(long idx, int RS, int Op, int Ip, int mode, int& o, int& i, int& rs) {
   if (mode == VST_PACK_KC) {  // idx = (rs*Ip + i)*Op + o
     o = idx % Op;
     const long q = idx / Op;
@@ -58,23 +54,72 @@ __global__ void weight_pack_k(const float* __restrict__ w, float* __restrict__ o
     const long q = idx / Ip;
     rs = q % RS;
     o = q / RS;
-  } else {  // VST_PACK_IK / VST_PACK_IKF: idx = (i*RS + rs)*Op + o (IKF: taps rotated 180 deg)
+  } else {  // VST_PACK_IK / VST_PACK_IKF: idx = (i*RS + rs)*Op + o
     o = idx % Op;
     const long q = idx / Op;
     rs = q % RS;
     i = q / RS;
     if (mode == VST_PACK_IKF) rs = RS - 1 - rs;
   }
+}
+
+// The three bf16 planes hi, mid, lo of v (vst_weight_split's conversions).
+__device__ __forceinline__ void store_split(__bf16* __restrict__ split, long total, long idx, float v) {
+  const __bf16 h = (__bf16)v;
+  const float r = v - (float)h;
+  const __bf16 m = (__bf16)r;
+  split[idx] = h;
+  split[total + idx] = m;
+  split[2 * total + idx] = (__bf16)(r - (float)m);
+}
+
+// Batched packing: every pack of a network in one launch (vst_weight_pack_batch).  Job j covers
+// blocks [block0, next block0); its logical weight element (o, i, r, s) is read at
+// w[o*so + i*si + tr[r]*sr + ts[s]*ss] (tap maps: the transposed-conv phase packs pick taps;
+// tr[0] < 0 / ts[0] < 0 = identity, any R / S).
+struct PackJob {
+  const float* w;
+  float* out;
+  __bf16* split;
+  int O, I, R, S, Op, Ip, mode, pad_;
+  long total, block0;
+  long so, si, sr, ss;
+  int tr[8], ts[8];
+};
+static_assert(sizeof(PackJob) == 168, "PackJob layout is part of the C ABI (include/vst_hip.h)");
+
+__global__ __launch_bounds__(256) void weight_pack_batch_k(const PackJob* __restrict__ jobs, int nj) {
+  const long b = blockIdx.x;
+  int lo = 0, hi = nj - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (jobs[mid].block0 <= b) lo = mid;
+    else hi = mid - 1;
+  }
+  const PackJob& J = jobs[lo];
+  const long idx = (b - J.block0) * 256 + threadIdx.x;
+  if (idx >= J.total) return;
+  int o, i, rs;
+  pack_coords(idx, J.R * J.S, J.Op, J.Ip, J.mode, o, i, rs);
+  const int r = rs / J.S, s = rs - r * J.S;
+  const int rr = J.tr[0] < 0 ? r : J.tr[r], ss = J.ts[0] < 0 ? s : J.ts[s];  // tr[0] < 0: identity
+  const float v = (o < J.O && i < J.I) ? J.w[o * J.so + i * J.si + rr * J.sr + ss * J.ss] : 0.f;
+  J.out[idx] = v;
+  if (J.split) store_split(J.split, J.total, idx, v);
+}
+
+// w[O][I][R][S] -> one pack (modes as pack_coords), optionally with its split planes
+__global__ void weight_pack_k(const float* __restrict__ w, float* __restrict__ out, int O, int I,
+                              int R, int S, int Op, int Ip, int mode, long total,
+                              __bf16* __restrict__ split = nullptr) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= total) return;
+  const int RS = R * S;
+  int o, i, rs;
+  pack_coords(idx, RS, Op, Ip, mode, o, i, rs);
   const float v = (o < O && i < I) ? w[((long)o * I + i) * RS + rs] : 0.f;
   out[idx] = v;
-  if (split) {  // the three bf16 planes hi, mid, lo of the split-arithmetic kernels (vst_weight_split)
-    const __bf16 h = (__bf16)v;
-    const float r = v - (float)h;
-    const __bf16 m = (__bf16)r;
-    split[idx] = h;
-    split[total + idx] = m;
-    split[2 * total + idx] = (__bf16)(r - (float)m);
-  }
+  if (split) store_split(split, total, idx, v);
 }
 
 __global__ void adam_k(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
@@ -145,6 +190,13 @@ extern "C" int vst_weight_pack_split(const float* w, float* out, void* split, in
   hipLaunchKernelGGL(weight_pack_k, dim3(ceil_div(total, 256)), dim3(256), 0, (hipStream_t)stream, w, out, O, I, R,
                      S, Op, Ip, mode, total, reinterpret_cast<__bf16*>(split));
   return check_launch("weight_pack_split");
+}
+
+extern "C" int vst_weight_pack_batch(const void* jobs, int njobs, long nblocks, void* stream) {
+  VST_REQUIRE(jobs && njobs > 0 && nblocks > 0 && nblocks < (1L << 31), "weight_pack_batch: bad args");
+  hipLaunchKernelGGL(weight_pack_batch_k, dim3((unsigned)nblocks), dim3(256), 0, (hipStream_t)stream,
+                     reinterpret_cast<const PackJob*>(jobs), njobs);
+  return check_launch("weight_pack_batch");
 }
 
 extern "C" int vst_adam_step(float* p, const float* g, float* m, float* v, long n, float lr,

@@ -21,7 +21,7 @@ import torch
 import torch.nn as nn
 
 from . import ops, perceptual
-from .networks import Conv2d, FlatNet, _Marker, _ToNCHW, _ToNHWC
+from .networks import Conv2d, FlatNet, _Marker, _ToNCHW, _ToNHWC, _padded_bias
 from .ops import cpad
 from .optim import FusedAdam
 
@@ -148,12 +148,8 @@ class FastStyleNet(FlatNet):
         P = {}
         for name, m in self.named_modules():
             if isinstance(m, Conv2d):
-                b = m.bias.detach()
-                if b.numel() % 4:
-                    bp = torch.zeros(cpad(b.numel()), device=b.device)
-                    bp[:b.numel()] = b
-                    b = bp
-                P[name] = (ops.weight_pack(m.weight, ops.PACK_FWD), ops.weight_pack(m.weight, ops.PACK_DGRAD), b)
+                P[name] = (ops.weight_pack(m.weight, ops.PACK_FWD), ops.weight_pack(m.weight, ops.PACK_DGRAD),
+                           _padded_bias(m))
         return P
 
     def forward_nhwc(self, x, style_strength=1.0):

@@ -152,6 +152,25 @@ class _Marker(nn.Module):
 ###############################################################################
 # Flat parameter / gradient storage
 ###############################################################################
+# The generator's image-side layers (c0: 3 -> ngf 7x7, and the data gradient of f: ngf -> 3 7x7) carry
+# their 3-channel side padded to 8 channels, so the 7x7 implicit GEMMs run on the split-bf16 kernels
+# (8-channel K chunks; half the K is zeros) instead of the fp32-image [row][k] kernels they otherwise
+# need at 4 channels (~40 TF): VST_C8_EDGES=0 restores those.
+C8_EDGES = os.environ.get("VST_C8_EDGES", "1") != "0"
+
+
+def _pad_channels(x, cs):
+    """NHWC copy of x with its channel stride raised to cs (extra channels zero)."""
+    y = torch.zeros(x.shape[:-1] + (cs,), device=x.device, dtype=x.dtype)
+    ops.copy_channels(x, 0, y, 0, x.shape[-1])
+    return y
+
+
+# Pack every layer of a network in one launch and refresh in place after updates (ops.PackBatch);
+# VST_PACK_BATCH=0: one vst_weight_pack_split launch per pack, rebuilt per weight version.
+PACK_BATCH = os.environ.get("VST_PACK_BATCH", "1") != "0"
+
+
 class FlatNet(nn.Module):
     """Base for HIP-backed networks: every parameter is a view into self.flat_param and its .grad a
     view into self.flat_grad.  Moving the module re-flattens on the new device."""
@@ -191,9 +210,20 @@ class FlatNet(nn.Module):
         return any(p.requires_grad for p in self.parameters())
 
     def packs(self):
+        """The layers' packed weights for the current weight version.  Built once (all packs in one
+        ops.PackBatch launch); after a weight update the same batch re-packs every layer in place."""
         key = self._version_key()
-        if self._packs is None or self._packs[0] != key:
-            self._packs = (key, self._make_packs())
+        if not PACK_BATCH:
+            if self._packs is None or self._packs[0] != key:
+                self._packs = [key, self._make_packs(), None]
+            return self._packs[1]
+        if self._packs is None:
+            with ops.PackBatch() as pb:
+                P = self._make_packs()
+            self._packs = [key, P, pb]
+        elif self._packs[0] != key:
+            self._packs[2].run()
+            self._packs[0] = key
         return self._packs[1]
 
     def _anchor(self):
@@ -288,7 +318,11 @@ def _padded_bias(m):
     if cp == m.bias.numel():
         return m.bias.detach()
     b = torch.zeros(cp, device=m.bias.device)
-    b[:m.bias.numel()] = m.bias.detach()
+    pb = ops.PackBatch._active
+    if pb is not None:
+        pb.copy_into(b, m.bias.detach())  # refreshed with the packs
+    else:
+        b[:m.bias.numel()] = m.bias.detach()
     return b
 
 
@@ -351,6 +385,14 @@ class ResnetGenerator(FlatNet):
     def _make_packs(self):
         c0, d, blocks, u, f = self._layers()
         P = {"c0": _pack_conv(c0), "d0": _pack_conv(d[0]), "d1": _pack_conv(d[1]), "f": _pack_conv(f)}
+        if CONVT_PHASES:
+            # the data gradient of Conv2d(k3, s2, p1) IS ConvTranspose2d(k3, s2, p1, op1) with the
+            # conv weight [Co][Ci] read as the transposed weight [in][out]: four phase convs
+            for i in (0, 1):
+                if d[i].weight.shape[0] % 8 == 0:
+                    P[f"d{i}ph"] = ops.convT3s2_phase_packs(d[i].weight)
+        if C8_EDGES and c0.weight.shape[1] <= 4:
+            P["c08"] = ops.weight_pack(c0.weight, ops.PACK_FWD, Ip=8)
         if TAP_LAST:
             P["ftap"] = ops.weight_pack(f.weight, ops.PACK_CK)
             if c0.weight.shape[1] <= 4:  # image-input first layer: its data gradient as a tap gather
@@ -361,6 +403,8 @@ class ResnetGenerator(FlatNet):
             P[f"b{i}b"] = _pack_conv(b.conv_block[5])
             P["ikf"][f"b{i}a"] = _ikf(b.conv_block[1])
             P["ikf"][f"b{i}b"] = _ikf(b.conv_block[5])
+        if C8_EDGES and DGRAD_AS_FPROP and f.weight.shape[0] <= 4:
+            P["ikf"]["f8"] = ops.weight_pack(f.weight, ops.PACK_IKF, Op=8)
         for i, m in enumerate(u):
             # ConvTranspose2d fwd = transposed kernel with rows (r,s,ci) -> CK pack of Wt[Ci][Co];
             # its dgrad = forward conv with KC pack of Wt seen as [O=Ci][I=Co] -> rows (r,s,co), cols ci
@@ -392,7 +436,15 @@ class _GeneratorFn(torch.autograd.Function):
             s = ops.instnorm_stats(y)
             return y, s, ops.instnorm_act_fwd(y, s, "relu")
 
-        y, s, a = conv_in_relu(x, "c0", ngf, 7, 1, 3, "reflect")
+        if "c08" in P and x.shape[-1] == 4:
+            x8 = _pad_channels(x, 8)
+            _, _, b = P["c0"]
+            y = ops.conv2d_fwd(x8, P["c08"], b, cpad(ngf), 7, 7, 1, 3, "reflect", role=role)
+            s = ops.instnorm_stats(y)
+            a = ops.instnorm_act_fwd(y, s, "relu")
+            sv["x8"] = x8
+        else:
+            y, s, a = conv_in_relu(x, "c0", ngf, 7, 1, 3, "reflect")
         sv["c0"] = (y, s, a)
         y, s, a = conv_in_relu(a, "d0", 2 * ngf, 3, 2, 1, "zero")
         sv["d0"] = (y, s, a)
@@ -467,6 +519,9 @@ class _GeneratorFn(torch.autograd.Function):
                                    addend=addend)
 
         def dgrad_s2(dy, key, cin_p, H, W):
+            ph = P.get(key + "ph")
+            if ph is not None and H == 2 * dy.shape[1] and W == 2 * dy.shape[2]:
+                return ops.convT3s2_fwd(dy, ph, None, cin_p, role="bwd")
             _, ck, _ = P[key]
             return ops.conv2d_tfwd(dy, ck, None, H, W, cin_p, 3, 3, 2, 1)
 
@@ -481,7 +536,11 @@ class _GeneratorFn(torch.autograd.Function):
         else:
             wgrad(f, a, g, 7, 1, 3, "reflect", db=True)
         done(f)
-        ga = dgrad_reflect(g, "f", a.shape[-1], 7, 3, a.shape[1], a.shape[2])
+        if "f8" in P["ikf"] and g.shape[-1] == 4:
+            ga = ops.conv2d_dgrad_s1(_pad_channels(g, 8), P["ikf"]["f8"], a.shape[1], a.shape[2], a.shape[-1], 7,
+                                     3, "reflect")
+        else:
+            ga = dgrad_reflect(g, "f", a.shape[-1], 7, 3, a.shape[1], a.shape[2])
         # up-sampling convT layers
         for i in (1, 0):
             a_in, y, s, an = sv[f"u{i}"]
@@ -521,7 +580,7 @@ class _GeneratorFn(torch.autograd.Function):
         x = sv["x"]
         y, s, _ = sv["c0"]
         dy = in_bwd(ga, y, s, "relu", c0)
-        wgrad(c0, x, dy, 7, 1, 3, "reflect")
+        wgrad(c0, sv.get("x8", x), dy, 7, 1, 3, "reflect")
         done(c0)
         gx = None
         if ctx.needs_input_grad[0]:

@@ -67,14 +67,81 @@ def nhwc_to_nchw(x, c):
     return y
 
 
-def weight_pack(w, mode, transposed=False):
+def _pack_shape(mode, O, I_, R, S, Op=None, Ip=None):
+    Op, Ip = Op or cpad(O), Ip or cpad(I_)
+    return {PACK_KC: (R, S, Ip, Op), PACK_CK: (R, S, Op, Ip), PACK_OK: (Op, R, S, Ip),
+            PACK_IK: (Ip, R, S, Op), PACK_IKF: (Ip, R, S, Op)}[mode]
+
+
+class PackBatch:
+    """A network's weight packs as ONE launch (vst_weight_pack_batch).  Inside ``with PackBatch()``
+    every weight_pack / convT3s2_phase_packs call allocates its outputs and records a job instead of
+    launching; leaving the block packs them all.  ``run()`` re-packs every recorded job in place
+    from the (updated) weights — after an optimizer step the pack set is refreshed by one kernel
+    instead of one launch per pack.  The job sources are the live parameter tensors (views into the
+    network's flat buffer), so the outputs stay valid objects across refreshes."""
+    _active = None
+    REC = 168  # sizeof(PackJob), include/vst_hip.h
+
+    def __init__(self):
+        self.jobs, self.blocks, self.copies, self._dev = [], 0, [], None
+
+    def __enter__(self):
+        self._prev, PackBatch._active = PackBatch._active, self
+        return self
+
+    def __exit__(self, *exc):
+        PackBatch._active = self._prev
+        if exc[0] is None and self.jobs:
+            self.run()
+        return False
+
+    def add(self, w, mode, O, I_, R, S, strides, tr=None, ts=None, Op=None, Ip=None):
+        import struct
+        Op, Ip = Op or cpad(O), Ip or cpad(I_)
+        shape = _pack_shape(mode, O, I_, R, S, Op, Ip)
+        out = torch.empty(shape, device=w.device, dtype=torch.float32)
+        split = torch.empty((3,) + shape, device=w.device, dtype=torch.bfloat16)
+        out.vst_split = split
+        total = out.numel()
+        tr = list(tr) if tr is not None else [-1]  # -1: identity tap map (any R / S)
+        ts = list(ts) if ts is not None else [-1]
+        if len(tr) > 8 or len(ts) > 8:
+            raise ValueError("PackBatch: explicit tap maps need R, S <= 8")
+        rec = struct.pack("<3Q8i2q4q8i8i", w.data_ptr(), out.data_ptr(), split.data_ptr(), O, I_, R, S,
+                          Op, Ip, mode, 0, total, self.blocks, *strides,
+                          *(tr + [0] * (8 - len(tr))), *(ts + [0] * (8 - len(ts))))
+        self.jobs.append((rec, w, out, split))
+        self.blocks += (total + 255) // 256
+        self._dev = None
+        return out
+
+    def copy_into(self, dst, src):
+        """dst[:n] = src on every run (padded bias vectors)."""
+        self.copies.append((dst, src))
+        dst[:src.numel()].copy_(src)
+
+    def run(self):
+        if self._dev is None:
+            buf = b"".join(j[0] for j in self.jobs)
+            self._dev = torch.frombuffer(bytearray(buf), dtype=torch.uint8).to(self.jobs[0][1].device)
+        _call("vst_weight_pack_batch", _p(self._dev), len(self.jobs), self.blocks, _stream())
+        for dst, src in self.copies:
+            dst[:src.numel()].copy_(src)
+
+
+def weight_pack(w, mode, transposed=False, Op=None, Ip=None):
     """Pack a PyTorch conv weight for the GEMM kernels (see vst_weight_pack).  For a
-    ConvTranspose2d weight [Ci][Co][R][S] pass transposed=True: dims are then (O=Ci, I=Co)."""
+    ConvTranspose2d weight [Ci][Co][R][S] pass transposed=True: dims are then (O=Ci, I=Co).
+    Op / Ip: padded channel counts (default cpad; 8 lets a 3-channel side use the split-bf16
+    kernels, whose K chunks are 8 channels deep)."""
     _dev_check(w)
     O, I_, R, S = w.shape
-    Op, Ip = cpad(O), cpad(I_)
-    shape = {PACK_KC: (R, S, Ip, Op), PACK_CK: (R, S, Op, Ip), PACK_OK: (Op, R, S, Ip),
-             PACK_IK: (Ip, R, S, Op), PACK_IKF: (Ip, R, S, Op)}[mode]
+    Op, Ip = Op or cpad(O), Ip or cpad(I_)
+    pb = PackBatch._active
+    if pb is not None:
+        return pb.add(w, mode, O, I_, R, S, (I_ * R * S, R * S, S, 1), Op=Op, Ip=Ip)
+    shape = _pack_shape(mode, O, I_, R, S, Op, Ip)
     out = torch.empty(shape, device=w.device, dtype=torch.float32)
     # the split-arithmetic conv paths read the pack as three bf16 planes (written in the same pass)
     split = torch.empty((3,) + shape, device=w.device, dtype=torch.bfloat16)
@@ -211,6 +278,7 @@ def debug_set_tiles(fprop=-1, tconv=-1, wgrad=-1):
 PLAN_RK, PLAN_SKINNY = -1, -2
 TILE_NAMES = {0: "128x128 (8 waves of 64x32)", 1: "128x64", 2: "128x128 (4 waves of 64x64)", 3: "64x128",
               4: "128x128 BK64", 5: "128x64 BK64", 6: "64x64", 7: "256x128 (8 waves of 64x64)", 8: "64x64 BK64",
+              9: "128x128 BK16 (4 waves of 64x64, 2 blocks/CU at x6)",
               PLAN_RK: "fp32 [row][k] kernel", PLAN_SKINNY: "VALU skinny kernel"}
 
 
@@ -799,6 +867,12 @@ def convT3s2_phase_packs(wt):
     """Phase weight packs of a ConvTranspose2d(k=3, stride=2, padding=1, output_padding=1) weight
     wt [Ci][Co][3][3]: output parity a (rows) / b (cols) uses taps k=1 (even) or k=(2, 0) at input
     offsets (0, +1) (odd).  Returns the VST_PACK_OK packs of the 1x1, 1x2, 2x1, 2x2 phase convs."""
+    pb = PackBatch._active
+    if pb is not None:  # packed straight from wt (transposed view + tap maps), no copies
+        Ci, Co = wt.shape[0], wt.shape[1]
+        st = (9, Co * 9, 3, 1)  # logical [o = co][i = ci][a][b] of wt[ci][co][kh][kw]
+        return [pb.add(wt, PACK_OK, Co, Ci, 1 + a, 1 + b, st, [2, 0] if a else [1], [2, 0] if b else [1])
+                for a, b in ((0, 0), (0, 1), (1, 0), (1, 1))]
     wc = wt.detach().permute(1, 0, 2, 3)  # [Co][Ci][kh][kw]
     odd = torch.tensor([2, 0], device=wt.device)
     ev = torch.tensor([1], device=wt.device)

@@ -84,6 +84,17 @@ int vst_weight_split(const float* w, void* out, long n, void* stream);
 /* vst_weight_pack + vst_weight_split of the pack in one pass (split: 3 * R*S*Op*Ip bf16). */
 int vst_weight_pack_split(const float* w, float* out, void* split, int O, int I, int R, int S, int Op, int Ip,
                           int mode, void* stream);
+/* Many packs in one launch (a network's whole pack set after each optimizer step).  `jobs` is a
+ * DEVICE array of njobs 168-byte records, little-endian, natural alignment:
+ *   {const float* w; float* out; void* split (3 bf16 planes or NULL);
+ *    int O, I, R, S, Op, Ip, mode, pad; long total (= R*S*Op*Ip), block0 (first 256-thread block);
+ *    long so, si, sr, ss; int tr[8], ts[8];}
+ * sorted by block0 (job 0 at block 0, nblocks = the last job's block0 + its blocks).  Element
+ * (o, i, r, s) of job j's logical weight is read at w[o*so + i*si + tr[r]*sr + ts[s]*ss] (tap maps
+ * need R, S <= 8; tr[0] = -1 / ts[0] = -1 means the identity map, any R / S),
+ * so a tap subset / transposed view (ConvTranspose phase packs) packs without a copy.  Replaces one
+ * vst_weight_pack_split launch per pack (networks.py re-packs every layer after every Adam step). */
+int vst_weight_pack_batch(const void* jobs, int njobs, long nblocks, void* stream);
 
 /* ---- convolution (implicit GEMM on MFMA) -------------------------------------------------- */
 /* `math` argument of vst_conv2d_fwd / _tfwd / _wgrad: the GEMM arithmetic of that call.

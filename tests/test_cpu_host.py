@@ -163,3 +163,16 @@ def test_conv_planner_picks_production_kernels():
         assert out[0][0] != 7
     finally:
         ops.debug_set_tiles(-1, -1, -1)
+
+
+def test_pack_batch_records_match_the_abi_layout():
+    """ops.PackBatch job records: 168 bytes each, the field order of include/vst_hip.h's
+    vst_weight_pack_batch record (and misc.hip's static_assert on sizeof(PackJob))."""
+    import re
+    import struct
+    from gbvst import ops
+    assert struct.calcsize("<3Q8i2q4q8i8i") == ops.PackBatch.REC == 168
+    hdr = open(os.path.join(REPO, "include", "vst_hip.h")).read()
+    assert "168-byte records" in hdr and "int vst_weight_pack_batch(const void* jobs" in hdr
+    src = open(os.path.join(REPO, "gan-based-video-style-transfer_amd", "csrc", "misc.hip")).read()
+    assert re.search(r"static_assert\(sizeof\(PackJob\) == 168", src)

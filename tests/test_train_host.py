@@ -1,0 +1,77 @@
+"""train.py host logic on CPU: the loss-log line format (util/visualizer.py:215-221), the epoch loop's
+schedule — update_learning_rate per epoch, print / save_latest / save_epoch frequencies — against
+methods/GAN-based/CycleGANCon/train.py:57-130, with a stand-in model (no GPU work)."""
+import os
+from collections import OrderedDict
+
+import gbvst.train as T
+from gbvst.options import default_opt
+
+
+class _FakeModel:
+    model_names = ["G_A"]
+
+    def __init__(self):
+        self.calls = []
+        self.step = 0
+
+    def setup(self, opt):
+        self.calls.append("setup")
+
+    def update_learning_rate(self):
+        self.calls.append("lr")
+
+    def set_input_nhwc(self, *a):
+        self.calls.append("in5")
+
+    def set_input_fc2(self, data):
+        self.calls.append("in6")
+
+    def optimize_parameters(self, hg=None, hd=None):
+        self.step += 1
+        self.calls.append("opt")
+
+    def get_current_losses(self):
+        return OrderedDict([("D_A", 0.25), ("G_A", 1.0 / 3.0), ("cycle_A", 2.0)])
+
+    def save_networks(self, which):
+        self.calls.append("save:%s" % which)
+
+
+def test_loss_line_format():
+    line = T.Visualizer.format_losses(3, 40, OrderedDict([("D_A", 0.25), ("G_A", 1 / 3)]), 0.0123, 0.5)
+    assert line == "(epoch: 3, iters: 40, time: 0.012, data: 0.500) D_A: 0.250 G_A: 0.333 "
+
+
+def test_epoch_loop_schedule(tmp_path):
+    opt = default_opt(True, checkpoints_dir=str(tmp_path), name="exp", n_epochs=2, n_epochs_decay=1,
+                      batch_size=2, print_freq=4, save_latest_freq=6, save_epoch_freq=2)
+    data = [(0, 1, 2, 3, 4)] * 3  # 3 batches of 2 = 6 images per epoch
+    m = _FakeModel()
+    _, total = T.train(opt, data, model=m, log=lambda *_: None)
+    assert total == 18 and m.step == 9
+    assert m.calls[0] == "setup" and m.calls.count("lr") == 3
+    # save_latest every 6 images (totals 6, 12, 18), save_epoch at epoch 2 ('latest' + '2')
+    saves = [c for c in m.calls if c.startswith("save")]
+    assert saves == ["save:latest", "save:latest", "save:latest", "save:2", "save:latest"]
+    log = open(os.path.join(str(tmp_path), "exp", "loss_log.txt")).read().splitlines()
+    assert log[0].startswith("================ Training Loss (")
+    # print every 4 images: totals 4, 8, 12, 16 -> 4 lines; epoch_iter restarts per epoch
+    body = log[1:]
+    assert len(body) == 4
+    assert body[0].startswith("(epoch: 1, iters: 4, time: ")
+    assert body[1].startswith("(epoch: 2, iters: 2, time: ")
+    assert body[0].endswith("D_A: 0.250 G_A: 0.333 cycle_A: 2.000 ")
+
+
+def test_reference_tuple_input(tmp_path):
+    opt = default_opt(True, checkpoints_dir=str(tmp_path), name="e2", n_epochs=1, n_epochs_decay=0,
+                      batch_size=1, print_freq=100, save_latest_freq=100, save_epoch_freq=5)
+    m = _FakeModel()
+    T.train(opt, [(0, 1, 2, 3, 4, 5)], model=m, log=lambda *_: None)
+    assert "in6" in m.calls and "in5" not in m.calls
+
+
+def test_entry_flags():
+    syn, rest = T._add_entry_flags(["--synthetic", "8", "--name", "x", "--synthetic=4"])
+    assert syn == 4 and rest == ["--name", "x"]

@@ -13,8 +13,11 @@ import gbvst  # noqa: E402
 from gbvst import ops  # noqa: E402
 
 gbvst._lib.load()
+if os.environ.get("KB_TILE"):  # force the forward / dgrad tile kind (vst_debug_set_tiles)
+    ops.debug_set_tiles(int(os.environ["KB_TILE"]), -1, -1)
 dev = torch.device("cuda")
-out = {"lib": os.environ.get("VST_LIB_VARIANT", "default"), "math": ops.get_conv_math()}
+out = {"lib": os.environ.get("VST_LIB_VARIANT", "default"), "math": ops.get_conv_math(),
+       "tile": os.environ.get("KB_TILE", "auto")}
 for B in [int(b) for b in os.environ.get("KB_B", "8,12").split(",")]:
     H, C = 64, 256
     x = torch.randn(B, H, H, C, device=dev)

@@ -6,7 +6,7 @@ usage: pmc_resblock.py <out_dir_of_pmc_runs> <profiles/tag> [reps]
 Expected layout (tools/profile_counters.sh): <dir>/<op>_fetch, <op>_write, <op>_sq1, <op>_sq2, <op>_kt.
 HBM bytes per call: FETCH_SIZE x 2 (the gfx950 wide-read correction, MI355X_MICROARCH.md HBM
 section) + WRITE_SIZE, summed over every dispatch the op launches (dgrad: the 256x128 main + 64x64
-tail launches; wgrad: the channel-major / bf16-plane copies, the GEMM, the split-K sum and store).
+tail launches; wgrad: the channel-major / bf16-plane copies, the GEMM, the split-K reduce + store).
 """
 import csv
 import glob
@@ -17,7 +17,7 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 OPS = {"fprop": ("conv_fprop_bf_k",), "dgrad": ("conv_fprop_bf_k",),
-       "wgrad": ("nhwc_to_cp", "conv_wgrad_bf_k", "wgrad_sum_k", "wgrad_store_k")}
+       "wgrad": ("nhwc_to_cp", "conv_wgrad_bf_k", "wgrad_reduce_store_k")}
 MAIN = {"fprop": "conv_fprop_bf_k", "dgrad": "conv_fprop_bf_k", "wgrad": "conv_wgrad_bf_k"}
 
 

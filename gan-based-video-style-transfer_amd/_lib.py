@@ -42,11 +42,14 @@ SIGNATURES = {
     "vst_conv2d_fwd": (I, [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, I, P]),
     "vst_weight_split": (I, [P, P, L, P]),
     "vst_weight_pack_batch": (I, [P, I, L, P]),
+    "vst_conv2d_fwd_in": (I, [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, I, P, P, P]),
+    "vst_instnorm_finalize": (I, [P, P, I, I, I, I, F, P]),
     "vst_conv2d_tfwd": (I, [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, F, I, P]),
     "vst_conv2d_wgrad_ws_bytes": (SZ, [I, I, I, I, I, I, I, I, I, I]),
     "vst_conv2d_wgrad": (I, [P, P, P, P, SZ, I, I, I, I, I, I, I, I, I, I, I, I, I, I, L, L, I, I, P]),
     "vst_debug_set_tiles": (None, [I, I, I]),
     "vst_conv_plan_fwd": (I, [I, I, I, I, I, I, I, I, I, I, I, P, P, P]),
+    "vst_conv_plan_wgrad": (I, [I, I, I, I, I, I, I, I, I, I, I, P, P, P]),
     "vst_reflect_fold": (I, [P, P, P, I, I, I, I, I, P]),
     "vst_channel_sum_ws_bytes": (SZ, [L, I]),
     "vst_channel_sum": (I, [P, P, P, L, I, I, I, P]),

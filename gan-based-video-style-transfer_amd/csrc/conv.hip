@@ -577,7 +577,21 @@ __global__ __launch_bounds__(256) void wgrad_reduce_store_k(const float* __restr
     src[i] = S + (long)(rs * Cx + ci) * Cyp + (ok[i] ? c0 + c4 : 0);
     acc[i] = ok[i] ? *reinterpret_cast<const float4*>(src[i]) : make_float4(0.f, 0.f, 0.f, 0.f);
   }
-  for (int z = 1; z < nsplit; ++z) {
+  // four slabs' loads in flight per round trip (the adds stay in slab order)
+  int z = 1;
+  for (; z + 3 < nsplit; z += 4) {
+    float4 v[4][4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        v[u][i] = *reinterpret_cast<const float4*>(src[i] + (ok[i] ? (long)(z + u) * zs : 0));
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) add4(acc[i], v[u][i]);
+  }
+  for (; z < nsplit; ++z) {
     float4 v[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) v[i] = *reinterpret_cast<const float4*>(src[i] + (ok[i] ? (long)z * zs : 0));
@@ -602,6 +616,29 @@ __global__ __launch_bounds__(256) void wgrad_reduce_store_k(const float* __restr
     const float v = tile[tx][r];
     *d = accumulate ? *d + v : v;
   }
+}
+
+// First level of the split-K reduction for small outputs with many slabs (image-size layers: a
+// handful of 64x64 output tiles over 100+ pixel chunks): slab group q = slabs [qG, qG+G) summed in
+// order into out[q] (4 slabs' loads in flight per round trip), in parallel over (element, group).
+__global__ __launch_bounds__(256) void slab_group_sum_k(const float* __restrict__ slab, float* __restrict__ out,
+                                                        long n4, int nsplit, int G) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n4) return;
+  const int q = blockIdx.y, z0 = q * G, z1 = min(nsplit, z0 + G);
+  const float4* s4 = reinterpret_cast<const float4*>(slab) + i;
+  float4 a = s4[(long)z0 * n4];
+  int z = z0 + 1;
+  for (; z + 3 < z1; z += 4) {
+    const float4 v0 = s4[(long)z * n4], v1 = s4[(long)(z + 1) * n4], v2 = s4[(long)(z + 2) * n4],
+                 v3 = s4[(long)(z + 3) * n4];
+    add4(a, v0);
+    add4(a, v1);
+    add4(a, v2);
+    add4(a, v3);
+  }
+  for (; z < z1; ++z) add4(a, s4[(long)z * n4]);
+  reinterpret_cast<float4*>(out)[(long)q * n4 + i] = a;
 }
 
 // ------------------------------------------------------------------------------ reflect-pad fold
@@ -811,7 +848,9 @@ extern "C" int vst_conv_plan_fwd(int N, int H, int W, int Cx, int Cop, int R, in
 
 static int conv_fwd_impl(const float* x, const float* wp, const void* wsplit, const float* bias, float* y,
                          int N, int H, int W, int Cx, int Cop, int R, int S, int stride, int padh, int padw,
-                         int pad_mode, int act, float slope, int math, hipStream_t s) {
+                         int pad_mode, int act, float slope, int math, hipStream_t s, double* part = nullptr,
+                         int* nsplit = nullptr) {
+  if (nsplit) *nsplit = 0;
   VST_REQUIRE(x && wp && y, "conv2d_fwd: null pointer");
   VST_REQUIRE(math >= VST_MATH_F32 && math <= VST_MATH_BF16X6, "conv2d_fwd: bad math %d", math);
   VST_REQUIRE(N > 0 && H > 0 && W > 0 && R > 0 && S > 0 && stride > 0 && padh >= 0 && padw >= 0,
@@ -826,9 +865,15 @@ static int conv_fwd_impl(const float* x, const float* wp, const void* wsplit, co
     return skinny_out_launch(0, x, wp, bias, nullptr, y, N, H, W, Cx, Ho, Wo, R, S, stride, padh, refl,
                              act, slope, s);
   }
-  if (math != VST_MATH_F32 && wsplit && Cx % 8 == 0)
-    return bf_fprop_launch(x, wsplit, (long)Cop * R * S * Cx, bias, y, N, H, W, Cx, Ho, Wo, Cop, R, S,
-                           stride, padh, padw, refl, act, slope, math, g_tile_override[0], s);
+  if (math != VST_MATH_F32 && wsplit && Cx % 8 == 0) {
+    // InstanceNorm partials from the epilogue: 32-pixel groups, so the image size must divide
+    const bool stats = part && nsplit && (Ho * Wo) % 32 == 0;
+    const int rc = bf_fprop_launch(x, wsplit, (long)Cop * R * S * Cx, bias, y, N, H, W, Cx, Ho, Wo, Cop, R, S,
+                                   stride, padh, padw, refl, act, slope, math, g_tile_override[0], s,
+                                   stats ? part : nullptr);
+    if (stats && rc == 0) *nsplit = Ho * Wo / 32;
+    return rc;
+  }
   rk_fprop_launch(x, wp, bias, y, N, H, W, Cx, Ho, Wo, Cop, R, S, stride, padh, padw, refl, act, slope,
                   g_tile_override[0], math, s);
   return check_launch("conv2d_fwd");
@@ -840,6 +885,15 @@ extern "C" int vst_conv2d_fwd(const float* x, const float* wp, const void* wspli
                               int pad_mode, int act, float slope, int math, void* stream) {
   return conv_fwd_impl(x, wp, wsplit, bias, y, N, H, W, Cx, Cop, R, S, stride, pad, pad, pad_mode, act, slope,
                        math, (hipStream_t)stream);
+}
+
+extern "C" int vst_conv2d_fwd_in(const float* x, const float* wp, const void* wsplit, const float* bias,
+                                 float* y, int N, int H, int W, int Cx, int Cop, int R, int S, int stride,
+                                 int pad, int pad_mode, int act, float slope, int math, double* part,
+                                 int* nsplit, void* stream) {
+  VST_REQUIRE(part && nsplit, "conv2d_fwd_in: null partials");
+  return conv_fwd_impl(x, wp, wsplit, bias, y, N, H, W, Cx, Cop, R, S, stride, pad, pad, pad_mode, act, slope,
+                       math, (hipStream_t)stream, part, nsplit);
 }
 
 extern "C" int vst_conv2d_fwd_hw(const float* x, const float* wp, const void* wsplit, const float* bias,
@@ -884,8 +938,29 @@ extern "C" int vst_conv2d_tfwd(const float* in, const float* wp, const float* bi
   return check_launch("conv2d_tfwd");
 }
 
+// Two-level split-K reduction (slab_group_sum_k first) when the fused reduce + store kernel would
+// run on few blocks with a long serial slab chain per element.
+static constexpr int WG_GROUP = 16;
+static bool wgrad_two_level(const WgradPlan& p, int Cyp, int Ci, int RS, int Co) {
+  return p.nsplit > 2 * WG_GROUP && (long)ceil_div(Ci * RS, 64) * ceil_div(Co, 64) < 128;
+}
+
 static size_t wgrad_ws_floats(const WgradPlan& p, int Cyp) {
-  return (size_t)p.nsplit * p.Mw * Cyp + p.xt_floats + p.dyt_floats;
+  // after the GEMM the operand copies are dead: the two-level reduction's group sums reuse them
+  const size_t l2 = (size_t)ceil_div(p.nsplit, WG_GROUP) * p.Mw * Cyp;
+  const size_t ops = p.xt_floats + p.dyt_floats;
+  return (size_t)p.nsplit * p.Mw * Cyp + (ops > l2 ? ops : l2);
+}
+
+extern "C" int vst_conv_plan_wgrad(int N, int H, int W, int Cx, int Ho, int Wo, int Cyp, int R, int S,
+                                   int stride, int math, int* path, int* kind, int* nsplit) {
+  VST_REQUIRE(path && kind && nsplit && N > 0 && H > 0 && W > 0 && Ho > 0 && Wo > 0 && R > 0 && S > 0,
+              "conv_plan_wgrad: bad args");
+  const WgradPlan p = plan_wgrad(N, H, W, Ho, Wo, Cx, Cyp, R, S, stride, math);
+  *path = p.bfk ? VST_WPLAN_BF : p.trans ? VST_WPLAN_RK : Cyp == 4 ? VST_WPLAN_SKINNY : VST_WPLAN_GENERIC;
+  *kind = (int)p.tile;
+  *nsplit = p.nsplit;
+  return VST_OK;
 }
 
 extern "C" size_t vst_conv2d_wgrad_ws_bytes(int N, int H, int W, int Cx, int Ho, int Wo, int Cyp,
@@ -948,9 +1023,20 @@ extern "C" int vst_conv2d_wgrad(const float* x, const float* dy, float* dw, floa
 #undef VST_WG
   int rc = check_launch("conv2d_wgrad");
   if (rc) return rc;
-  // split-K slabs: summed in slab order and stored transposed in one pass
+  // split-K slabs: summed in slab order and stored transposed in one pass (small outputs over many
+  // slabs: groups of WG_GROUP slabs summed in parallel first, into the dead operand-copy region)
+  const long slab = (long)p.Mw * Cyp;
+  const float* red = ws;
+  int nred = p.nsplit;
+  if (wgrad_two_level(p, Cyp, Ci, R * S, Co)) {
+    float* l2 = ws + (long)p.nsplit * slab;
+    nred = ceil_div(p.nsplit, WG_GROUP);
+    hipLaunchKernelGGL(slab_group_sum_k, dim3(ceil_div(slab / 4, 256), nred), dim3(256), 0, s, ws, l2, slab / 4,
+                       p.nsplit, WG_GROUP);
+    red = l2;
+  }
   hipLaunchKernelGGL(wgrad_reduce_store_k, dim3(ceil_div(Ci * R * S, 64), ceil_div(Co, 64)), dim3(256), 0, s,
-                     ws, dw, Cx, Cyp, R * S, Co, Ci, so, si, accumulate, p.nsplit, (long)p.Mw * Cyp);
+                     red, dw, Cx, Cyp, R * S, Co, Ci, so, si, accumulate, nred, slab);
   return check_launch("conv2d_wgrad_reduce");
 }
 

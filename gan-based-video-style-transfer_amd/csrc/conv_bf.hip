@@ -318,7 +318,7 @@ template <class T, bool KSL, int REFL>
 __global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_k(
     const float* __restrict__ x, const __bf16* __restrict__ ws, long wps, const float* __restrict__ bias,
     float* __restrict__ y, int H, int W, int C, int Ho, int Wo, int Cop, int S, int st, int padh,
-    int padw, int reflect, int act, float slope, int M, int Ktot, int m_base) {
+    int padw, int reflect, int act, float slope, int M, int Ktot, int m_base, double* __restrict__ part) {
   __shared__ __attribute__((aligned(16))) char smem[2 * T::STAGE];
   constexpr int A_LD = T::A_LD, B_LD = T::B_LD, RPP = T::RPP, NP = T::NP;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -435,12 +435,30 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_k(
 #pragma unroll
     for (int j = 0; j < T::NI; ++j) {
       const int n = n0 + wn0 + 32 * j + (lane & 31);
-      if (n >= Cop) continue;
-      const float bv = bias ? bias[n] : 0.f;
+      const bool nok = n < Cop;
+      const float bv = (bias && nok) ? bias[n] : 0.f;
+      double s1 = 0.0, s2 = 0.0;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int mm = m0 + wm0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        if (mm < M) y[(long)mm * Cop + n] = apply_act(acc[i][j][r] + bv, act, slope);
+        const float v = apply_act(acc[i][j][r] + bv, act, slope);
+        if (nok && mm < M) y[(long)mm * Cop + n] = v;
+        s1 += v;
+        s2 += (double)v * v;
+      }
+      if (part) {
+        // InstanceNorm statistics partials of this 32-row group (vst_conv2d_fwd_in): lanes l and
+        // l ^ 32 hold the group's two row halves of column n; fixed order, fp64.  The launcher
+        // guarantees Ho*Wo % 32 == 0, so a group never straddles an image or M.
+        s1 += __shfl_xor(s1, 32);
+        s2 += __shfl_xor(s2, 32);
+        const int g0 = m0 + wm0 + 32 * i;
+        if (lane < 32 && nok && g0 < M) {
+          const int hw = Ho * Wo, img = g0 / hw, z = (g0 - img * hw) >> 5;
+          double* d = part + (((long)img * (hw >> 5) + z) * Cop + n) * 2;
+          d[0] = s1;
+          d[1] = s2;
+        }
       }
     }
 }
@@ -743,7 +761,7 @@ void bf_plan(long M, int Cop, int math, int kind, int* kind_out, int* m_split_ou
 
 int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* bias, float* y, int N,
                     int H, int W, int C, int Ho, int Wo, int Cop, int R, int S, int st, int padh, int padw,
-                    int reflect, int act, float slope, int math, int kind, hipStream_t s) {
+                    int reflect, int act, float slope, int math, int kind, hipStream_t s, double* part) {
   const int M = N * Ho * Wo, K = R * S * C;
   const __bf16* ws = reinterpret_cast<const __bf16*>(wsplit);
   int kd, m_split, tail_kind;
@@ -754,17 +772,17 @@ int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* b
     const dim3 grid(ceil_div(Mend - mb, BM_) * ceil_div(Cop, BN_));                                 \
     if (VST_BF_KSLICE && C % BK_ == 0 && reflect)                                                   \
       hipLaunchKernelGGL((bf::conv_fprop_bf_k<T, true, 1>), grid, dim3(T::NT), 0, s, x, ws, wps, bias, y, \
-                         H, W, C, Ho, Wo, Cop, S, st, padh, padw, reflect, act, slope, Mend, K, mb); \
+                         H, W, C, Ho, Wo, Cop, S, st, padh, padw, reflect, act, slope, Mend, K, mb, part); \
     else if (VST_BF_KSLICE && C % BK_ == 0)                                                         \
       hipLaunchKernelGGL((bf::conv_fprop_bf_k<T, true, 0>), grid, dim3(T::NT), 0, s, x, ws, wps, bias, y, \
-                         H, W, C, Ho, Wo, Cop, S, st, padh, padw, reflect, act, slope, Mend, K, mb); \
+                         H, W, C, Ho, Wo, Cop, S, st, padh, padw, reflect, act, slope, Mend, K, mb, part); \
     else                                                                                            \
       hipLaunchKernelGGL((bf::conv_fprop_bf_k<T, false, 2>), grid, dim3(T::NT), 0, s, x, ws, wps, bias, y, \
-                         H, W, C, Ho, Wo, Cop, S, st, padh, padw, reflect, act, slope, Mend, K, mb); \
+                         H, W, C, Ho, Wo, Cop, S, st, padh, padw, reflect, act, slope, Mend, K, mb, part); \
   }
-  for (int part = 0; part < (m_split ? 2 : 1); ++part) {
-    const int mb = part ? m_split : 0, Mend = (m_split && !part) ? m_split : M;
-    const int kp = part ? tail_kind : kd;
+  for (int ph = 0; ph < (m_split ? 2 : 1); ++ph) {
+    const int mb = ph ? m_split : 0, Mend = (m_split && !ph) ? m_split : M;
+    const int kp = ph ? tail_kind : kd;
     if (math == VST_MATH_BF16X6) {
       VST_BF_DISPATCH(kp, 3, VST_BF)
     } else {

@@ -555,6 +555,14 @@ extern "C" int vst_instnorm_stats(const float* x, float* stats, float* ws, int N
   return check_launch("instnorm_stats");
 }
 
+extern "C" int vst_instnorm_finalize(const double* part, float* stats, int N, int HW, int C, int nsplit,
+                                     float eps, void* stream) {
+  VST_REQUIRE(part && stats && N > 0 && HW > 0 && C > 0 && nsplit > 0, "instnorm_finalize: bad args");
+  hipLaunchKernelGGL(in_finalize_k, dim3(ceil_div(C, 64), N), dim3(256), 0, (hipStream_t)stream, part, stats, N,
+                     HW, C, nsplit, eps);
+  return check_launch("instnorm_finalize");
+}
+
 extern "C" int vst_instnorm_act_fwd(const float* x, const float* stats, const float* residual,
                                     float* y, int N, int HW, int C, int act, float slope,
                                     void* stream) {

@@ -432,15 +432,13 @@ class _GeneratorFn(torch.autograd.Function):
 
         def conv_in_relu(inp, key, cout, R, st, pad, mode):
             kc, _, b = P[key]
-            y = ops.conv2d_fwd(inp, kc, b, cpad(cout), R, R, st, pad, mode, role=role)
-            s = ops.instnorm_stats(y)
+            y, s = ops.conv2d_fwd_in(inp, kc, b, cpad(cout), R, R, st, pad, mode, role=role)
             return y, s, ops.instnorm_act_fwd(y, s, "relu")
 
         if "c08" in P and x.shape[-1] == 4:
             x8 = _pad_channels(x, 8)
             _, _, b = P["c0"]
-            y = ops.conv2d_fwd(x8, P["c08"], b, cpad(ngf), 7, 7, 1, 3, "reflect", role=role)
-            s = ops.instnorm_stats(y)
+            y, s = ops.conv2d_fwd_in(x8, P["c08"], b, cpad(ngf), 7, 7, 1, 3, "reflect", role=role)
             a = ops.instnorm_act_fwd(y, s, "relu")
             sv["x8"] = x8
         else:
@@ -454,8 +452,7 @@ class _GeneratorFn(torch.autograd.Function):
         for i in range(len(blocks)):
             t, s1, uu = conv_in_relu(h, f"b{i}a", 4 * ngf, 3, 1, 1, "reflect")
             kc, _, b = P[f"b{i}b"]
-            v = ops.conv2d_fwd(uu, kc, b, 4 * ngf, 3, 3, 1, 1, "reflect", role=role)
-            s2 = ops.instnorm_stats(v)
+            v, s2 = ops.conv2d_fwd_in(uu, kc, b, 4 * ngf, 3, 3, 1, 1, "reflect", role=role)
             hn = ops.instnorm_act_fwd(v, s2, "none", residual=h)
             sv[f"b{i}"] = (h, t, s1, uu, v, s2)
             h = hn
@@ -651,8 +648,7 @@ class _DiscriminatorFn(torch.autograd.Function):
             kc, _, b = P[i]
             last = i == L - 1
             if has_in:
-                y = ops.conv2d_fwd(a, kc, b, cpad(cout), 4, 4, st, 1, "zero", role=role)
-                s = ops.instnorm_stats(y)
+                y, s = ops.conv2d_fwd_in(a, kc, b, cpad(cout), 4, 4, st, 1, "zero", role=role)
                 an = ops.instnorm_act_fwd(y, s, "lrelu", SLOPE)
                 saved.append((a, y, s, an))
             else:

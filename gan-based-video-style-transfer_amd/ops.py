@@ -204,6 +204,32 @@ def conv2d_fwd(x, wp, bias, cop, R, S, stride, pad, pad_mode="zero", act="none",
     return y
 
 
+def conv2d_fwd_in(x, wp, bias, cop, R, S, stride, pad, pad_mode="zero", role="fwd"):
+    """A conv that feeds an InstanceNorm: (y, stats).  The split-bf16 kernels emit the statistics
+    partials from their epilogue (vst_conv2d_fwd_in) and one small fold finalizes them; other paths
+    (fp32 policy, 4-channel inputs, image sizes not a multiple of 32 pixels) fall back to
+    instnorm_stats(y).  Same stats layout as instnorm_stats."""
+    import ctypes
+    _dev_check(x, wp, bias)
+    N, H, W, Cx = x.shape
+    Ho = (H + 2 * pad - R) // stride + 1
+    Wo = (W + 2 * pad - S) // stride + 1
+    y = torch.empty((N, Ho, Wo, cop), device=x.device)
+    hw = Ho * Wo
+    part = torch.empty((N * max(1, hw // 32) * cop * 2,), device=x.device, dtype=torch.float64)
+    nsplit = ctypes.c_int(0)
+    h = _probe_begin("fwd", (N, H, W, Cx, cop, R, stride, pad, pad_mode)) if _probes else None
+    _call("vst_conv2d_fwd_in", _p(x), _p(wp), _p(getattr(wp, "vst_split", None)), _p(bias), _p(y), N, H, W, Cx,
+          cop, R, S, stride, pad, PAD[pad_mode], ACT["none"], 0.0, _math(role), _p(part),
+          ctypes.addressof(nsplit), _stream())
+    _probe_end(h)
+    if nsplit.value == 0:
+        return y, instnorm_stats(y)
+    stats = torch.empty((N, cop, 2), device=x.device)
+    _call("vst_instnorm_finalize", _p(part), _p(stats), N, hw, cop, nsplit.value, IN_EPS, _stream())
+    return y, stats
+
+
 def conv2d_tfwd(x, wp, bias, Ho, Wo, cx, R, S, stride, pad, act="none", slope=0.0,
                 pad_mode="zero", addend=None, role="bwd"):
     """Transposed conv / data gradient (vst_conv2d_tfwd).  pad_mode='reflect' (stride 1) is the
@@ -280,6 +306,21 @@ TILE_NAMES = {0: "128x128 (8 waves of 64x32)", 1: "128x64", 2: "128x128 (4 waves
               4: "128x128 BK64", 5: "128x64 BK64", 6: "64x64", 7: "256x128 (8 waves of 64x64)", 8: "64x64 BK64",
               9: "128x128 BK16 (4 waves of 64x64, 2 blocks/CU at x6)",
               PLAN_RK: "fp32 [row][k] kernel", PLAN_SKINNY: "VALU skinny kernel"}
+
+
+WPLAN_NAMES = {0: "conv_wgrad_k (NHWC operands)", 1: "copies + conv_wgrad_rk_k", 2: "copies + conv_wgrad_bf_k",
+               3: "skinny VALU"}
+
+
+def conv_plan_wgrad(N, H, W, Cx, Ho, Wo, Cyp, R, S, stride, math):
+    """Host-only query (vst_conv_plan_wgrad): (path, tile kind, nsplit) of vst_conv2d_wgrad."""
+    import ctypes
+    from ._lib import MATH_MODES
+    m = MATH_MODES[math] if math in MATH_MODES else _math(math)
+    path, kind, ns = ctypes.c_int(0), ctypes.c_int(0), ctypes.c_int(0)
+    _call("vst_conv_plan_wgrad", N, H, W, Cx, Ho, Wo, Cyp, R, S, stride, m, ctypes.addressof(path),
+          ctypes.addressof(kind), ctypes.addressof(ns))
+    return path.value, kind.value, ns.value
 
 
 def conv_plan_fwd(N, H, W, Cx, Cop, R, S, stride, pad_h, pad_w, math, with_tail=False):

@@ -116,6 +116,14 @@ enum { VST_MATH_F32 = 0, VST_MATH_BF16X3 = 1, VST_MATH_BF16X6 = 2 };
 int vst_conv2d_fwd(const float* x, const float* wp, const void* wsplit, const float* bias, float* y,
                    int N, int H, int W, int Cx, int Cop, int R, int S, int stride, int pad,
                    int pad_mode, int act, float slope, int math, void* stream);
+/* vst_conv2d_fwd plus the InstanceNorm statistics partials of its output, from the GEMM epilogue
+ * (the conv that feeds an InstanceNorm): when the split-bf16 kernels run the conv and Ho*Wo % 32 == 0,
+ * part (fp64, N * (Ho*Wo/32) * Cop * 2) receives {sum y, sum y^2} per (image, 32-pixel group,
+ * channel) and *nsplit = Ho*Wo/32; otherwise *nsplit = 0 and the caller runs vst_instnorm_stats.
+ * Replaces the statistics pass's full read of y (networks.py InstanceNorm after each conv). */
+int vst_conv2d_fwd_in(const float* x, const float* wp, const void* wsplit, const float* bias, float* y, int N,
+                      int H, int W, int Cx, int Cop, int R, int S, int stride, int pad, int pad_mode, int act,
+                      float slope, int math, double* part, int* nsplit, void* stream);
 /* Transposed convolution / conv data-gradient (gather form, split by output parity class):
  *   out[n][h][w][cx] = sum_{r,s,cy : h = ho*stride - pad + r, w = wo*stride - pad + s}
  *                        in[n][ho][wo][cy] * w[cy][cx][r][s]        (+ bias[cx], act)
@@ -159,6 +167,13 @@ void vst_debug_set_tiles(int fprop, int tconv, int wgrad);
 enum { VST_PLAN_RK = -1, VST_PLAN_SKINNY = -2 };
 int vst_conv_plan_fwd(int N, int H, int W, int Cx, int Cop, int R, int S, int stride, int pad_h,
                       int pad_w, int math, int* kind, int* m_split, int* tail_kind);
+/* Host-only planning query for vst_conv2d_wgrad: *path = VST_WPLAN_BF (channel-major copies + the
+ * split-bf16 kernel conv_wgrad_bf_k), _RK (copies + conv_wgrad_rk_k), _GENERIC (conv_wgrad_k on the
+ * NHWC operands) or _SKINNY (<= 4 output channels, VALU); *kind = its tile kind; *nsplit = split-K
+ * slabs (reduced by slab_group_sum_k + wgrad_reduce_store_k). */
+enum { VST_WPLAN_GENERIC = 0, VST_WPLAN_RK = 1, VST_WPLAN_BF = 2, VST_WPLAN_SKINNY = 3 };
+int vst_conv_plan_wgrad(int N, int H, int W, int Cx, int Ho, int Wo, int Cyp, int R, int S, int stride,
+                        int math, int* path, int* kind, int* nsplit);
 /* db[c] (+)= sum over NHW pixels of x[p][c] for c < Cl (channel stride Cs); bias gradient of a layer
  * whose output gradient is x.  ws: vst_channel_sum_ws_bytes bytes; fixed-order (deterministic). */
 size_t vst_channel_sum_ws_bytes(long NHW, int Cs);
@@ -175,6 +190,10 @@ int vst_reflect_fold(const float* dxp, const float* addend, float* dx, int N, in
 size_t vst_instnorm_ws_bytes(int N, int HW, int C);
 int vst_instnorm_stats(const float* x, float* stats, float* ws, int N, int HW, int C, float eps,
                        void* stream);
+/* stats[n][c] = {mean, 1/sqrt(var + eps)} from fp64 partials part[n][z][c][2] = {sum, sum of squares}
+ * over z < nsplit groups (vst_conv2d_fwd_in's epilogue partials); fixed-order fold. */
+int vst_instnorm_finalize(const double* part, float* stats, int N, int HW, int C, int nsplit, float eps,
+                          void* stream);
 /* y = act((x - mean) * rstd) (+ residual).  residual may be NULL. */
 int vst_instnorm_act_fwd(const float* x, const float* stats, const float* residual, float* y,
                          int N, int HW, int C, int act, float slope, void* stream);

@@ -408,3 +408,29 @@ def test_production_resnet_conv(ops, conv_math, forced):
         _close(dw.cpu(), wr.grad, tol=tol, what="wgrad")
     finally:
         ops.debug_set_tiles(-1, -1, -1)
+
+
+@pytest.mark.parametrize("case", [
+    # N, H, W, Cx, Cop, R, stride, pad, mode      (fused path / fallback noted)
+    (2, 64, 64, 256, 256, 3, 1, 1, "reflect"),   # 256x128 tiles, K-slice order: fused
+    (12, 64, 64, 256, 256, 3, 1, 1, "reflect"),  # x6 whole rounds + tail launch: fused in both
+    (2, 40, 48, 8, 64, 7, 1, 3, "reflect"),      # 8-channel image edge (tap-major K): fused
+    (2, 64, 64, 64, 128, 3, 2, 1, "zero"),       # stride 2: fused
+    (2, 33, 33, 128, 256, 4, 1, 1, "zero"),      # 32x32 output = 1024 px: fused
+    (2, 34, 34, 64, 128, 4, 1, 1, "zero"),       # 33x33 output (not a multiple of 32 px): fallback
+])
+def test_conv_fwd_in_stats(ops, case, conv_math):
+    """vst_conv2d_fwd_in: the conv output equals vst_conv2d_fwd's, and the InstanceNorm statistics
+    folded from its epilogue partials equal vst_instnorm_stats of that output (fp64 partial sums in
+    another order: mean and rstd to 1e-6 relative)."""
+    N, H, W, Cx, Cop, R, st, pad, mode = case
+    x = _g(11, (N, H, W, Cx)).to(DEV)
+    w = _g(12, (Cop, Cx, R, R), 0.05).to(DEV)
+    b = _g(13, (Cop,), 0.1).to(DEV)
+    kc = ops.weight_pack(w, ops.PACK_FWD)
+    y_ref = ops.conv2d_fwd(x, kc, b, Cop, R, R, st, pad, mode)
+    y, s = ops.conv2d_fwd_in(x, kc, b, Cop, R, R, st, pad, mode)
+    assert torch.equal(y, y_ref)
+    s_ref = ops.instnorm_stats(y_ref)
+    rel = ((s - s_ref).abs() / s_ref.abs().clamp_min(1e-6)).max().item()
+    assert rel < 1e-6, rel

@@ -1,5 +1,6 @@
 """Developer: launch one conv family on the ResnetBlock shape (B=4, 64x64x256, 3x3 reflect) a few
-times (batch KB_B, default 8) — the target of rocprofv3 --pmc passes.  usage: kbench.py fprop|dgrad|tconv|wgrad [reps]"""
+times (batch KB_B, default 8) — the target of rocprofv3 --pmc passes.  usage: kbench.py fprop|dgrad|tconv|wgrad|warp [reps]
+warp: vst_warp_fwd on bench.py's warp_roofline shape (N=32, C=64, 436x1024, random flow)."""
 import os
 import sys
 
@@ -13,6 +14,16 @@ gbvst._lib.load()
 which = sys.argv[1]
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
 dev = torch.device("cuda")
+if which == "warp":
+    N, C, H, W = 32, 64, 436, 1024
+    xw = torch.randn(N, H, W, C, device=dev)
+    flow = torch.randn(N, 2, H, W, device=dev) * 3.0
+    out = torch.empty_like(xw)
+    for _ in range(reps):
+        ops.lib().vst_warp_fwd(xw.data_ptr(), flow.data_ptr(), out.data_ptr(), N, H, W, C, 0,
+                               torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    sys.exit(0)
 B, H, C = int(os.environ.get("KB_B", "8")), 64, 256  # 8 = the batched G_A calls of the train step
 x = torch.randn(B, H, H, C, device=dev)
 w = torch.randn(C, C, 3, 3, device=dev) * 0.02

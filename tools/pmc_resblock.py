@@ -17,8 +17,11 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 OPS = {"fprop": ("conv_fprop_bf_k",), "dgrad": ("conv_fprop_bf_k",),
-       "wgrad": ("nhwc_to_cp", "conv_wgrad_bf_k", "wgrad_reduce_store_k")}
-MAIN = {"fprop": "conv_fprop_bf_k", "dgrad": "conv_fprop_bf_k", "wgrad": "conv_wgrad_bf_k"}
+       "wgrad": ("nhwc_to_cp", "conv_wgrad_bf_k", "wgrad_reduce_store_k", "slab_group_sum_k"),
+       "warp": ("warp_fwd_k",)}
+# the op's main GEMM dispatch (SQ metrics and its timing; the dgrad's 64x64 tail launch is excluded)
+MAIN = {"fprop": "Tile<256, 128", "dgrad": "Tile<256, 128", "wgrad": "conv_wgrad_bf_k", "warp": "warp_fwd_k"}
+WARP_BYTES = 32 * 436 * 1024 * (8.0 * 64 + 8.0)  # bench.py warp_roofline: N*H*W*(4C gather + 8 flow + 4C write)
 
 
 def counters(d, subs):
@@ -54,11 +57,11 @@ def main():
         if not fetch or not write:
             continue
         fb, wb = 2 * sum(fetch) * 1024 / reps, sum(write) * 1024 / reps
-        alg = 4.0 * B * 64 * 64 * 256 * 2 + 256 * 2304 * 3 * 2
+        alg = WARP_BYTES if op == "warp" else 4.0 * B * 64 * 64 * 256 * 2 + 256 * 2304 * 3 * 2
         t = kernel_times(os.path.join(d, op + "_kt"), MAIN[op])
-        name = "resblock_" + op
-        key = {"math": "bf16x6", "N": B}
-        if op != "wgrad":
+        name = "warp" if op == "warp" else "resblock_" + op
+        key = {"N": 32, "C": 64, "H": 436, "W": 1024} if op == "warp" else {"math": "bf16x6", "N": B}
+        if op in ("fprop", "dgrad"):
             import gbvst
             from gbvst import ops
             gbvst._lib.load()
@@ -80,11 +83,21 @@ def main():
             w = sum(sq["SQ_WAVE_CYCLES"])
             lines.append("   wait_any/wave_cycles %.3f  wait_inst_any/wave_cycles %.3f  active_inst_any/wave_cycles %.3f" % (
                 sum(sq["SQ_WAIT_ANY"]) / w, sum(sq.get("SQ_WAIT_INST_ANY", [0])) / w, sum(sq.get("SQ_ACTIVE_INST_ANY", [0])) / w))
-        if "SQ_VALU_MFMA_BUSY_CYCLES" in sq and t:
+        if t:
+            res[name]["achieved_GBps_main_kernel"] = round(alg / (sum(t) / len(t) * 1e-6) / 1e9, 1) if op == "warp" else None
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in sq and t and op != "warp":
             busy = sum(sq["SQ_VALU_MFMA_BUSY_CYCLES"]) / len(sq["SQ_VALU_MFMA_BUSY_CYCLES"])
             dur = sum(t) / len(t) * 1e-6
             lines.append("   MFMA busy fraction (busy cycles / (1024 SIMDs x 2.4 GHz x avg duration)): %.3f" % (busy / (1024 * 2.4e9 * dur)))
-            res[name]["mfma_busy_frac"] = round(busy / (1024 * 2.4e9 * dur), 4)
+            res[name]["mfma_busy_frac_nominal_clock"] = round(busy / (1024 * 2.4e9 * dur), 4)
+            if "SQ_WAVE_CYCLES" in sq and "SQ_WAVES" in sq:
+                # SQ_WAVE_CYCLES counts quad-cycles (MI355X_MICROARCH.md); a wave lives ~the whole
+                # kernel (one block per CU, one round), so this is MFMA busy vs cycles at the real clock
+                life = 4.0 * sum(sq["SQ_WAVE_CYCLES"]) / sum(sq["SQ_WAVES"])
+                clk = life / dur
+                lines.append("   MFMA busy vs wave-lifetime cycles: %.3f (effective clock %.2f GHz)" % (busy / (1024 * life), clk / 1e9))
+                res[name]["mfma_busy_frac_actual_clock"] = round(busy / (1024 * life), 4)
+                res[name]["effective_clock_GHz"] = round(clk / 1e9, 3)
     json.dump(res, open(tag + "_conv_pmc.json", "w"), indent=1)
     open(tag + "_conv_sq.txt", "w").write("\n".join(lines) + "\n")
     print("\n".join(lines))

@@ -105,6 +105,7 @@ SIGNATURES = {
     "vst_tap_wgrad_scatter": (I, [P, P, I, I, I, I, I, P]),
     "vst_tapgather": (I, [P, P, I, I, I, I, I, I, I, P]),
     "vst_interleave_phases": (I, [P, P, P, P, P, I, I, I, I, P]),
+    "vst_interleave_phases_full": (I, [P, P, P, P, P, I, I, I, I, P]),
     "vst_raft_prep_nhwc": (I, [P, I, P, I, I, I, I, I, I, I, P]),
     "vst_loss_masked_l1": (I, [P, P, P, P, P, L, I, I, F, P]),
     "vst_loss_masked_l1_bwd": (I, [P, P, P, P, P, L, I, I, F, P]),

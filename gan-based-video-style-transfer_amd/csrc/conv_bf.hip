@@ -46,6 +46,9 @@
 #ifndef VST_BF_PRIO
 #define VST_BF_PRIO 0
 #endif
+#ifndef VST_BF_STORE_LATE
+#define VST_BF_STORE_LATE 0
+#endif
 
 namespace vst {
 namespace bf {
@@ -92,8 +95,17 @@ __device__ __forceinline__ uint32_t pack2(float a, float b) {
 }
 
 // Split 8 fp32 values into NP bf16 planes (uint4 = 8 bf16 each).
+#ifndef VST_BF_FAKESPLIT
+#define VST_BF_FAKESPLIT 0  // developer timing experiment only: hi plane replicated (WRONG results)
+#endif
 template <int NP>
 __device__ __forceinline__ void split8(const float4& a, const float4& b, uint4 (&o)[NP]) {
+  if (VST_BF_FAKESPLIT) {
+    const uint4 h = make_uint4(pack2(a.x, a.y), pack2(a.z, a.w), pack2(b.x, b.y), pack2(b.z, b.w));
+#pragma unroll
+    for (int p = 0; p < NP; ++p) o[p] = h;
+    return;
+  }
   float r[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
 #pragma unroll
   for (int p = 0; p < NP; ++p) {
@@ -250,9 +262,10 @@ __device__ __forceinline__ void main_loop(char* smem, int nk, f32x16 (&acc)[T::M
       if (g == 0) {
         adv(kt + 2 < nk);
         load_all(P);
-        store_stage<T>(nxt, ra[P ^ 1], rbv[P ^ 1], rb, kq);
+        if (!VST_BF_STORE_LATE) store_stage<T>(nxt, ra[P ^ 1], rbv[P ^ 1], rb, kq);
       }
       if (g == G - 1) {
+        if (VST_BF_STORE_LATE) store_stage<T>(nxt, ra[P ^ 1], rbv[P ^ 1], rb, kq);
         __builtin_amdgcn_sched_barrier(0);  // keep this group's MFMAs after the barrier (they cover the read)
         __syncthreads();
         read_frag<T>(fr[fi ^ 1], nxt, 0, wm0, wn0, lane);

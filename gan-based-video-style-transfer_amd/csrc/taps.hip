@@ -175,7 +175,7 @@ __global__ void tapgather_k(const float4* __restrict__ z, float4* __restrict__ y
 // y[n][2i+a][2j+b][c] = P_ab[n][i+a][j+b][c], P_ab of size (H+a) x (W+b).
 __global__ void interleave_phases_k(const float4* __restrict__ p00, const float4* __restrict__ p01,
                                     const float4* __restrict__ p10, const float4* __restrict__ p11,
-                                    float4* __restrict__ y, int H, int W, int C4, long total) {
+                                    float4* __restrict__ y, int H, int W, int C4, long total, int full) {
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= total) return;
   const int c4 = idx % C4;
@@ -186,7 +186,7 @@ __global__ void interleave_phases_k(const float4* __restrict__ p00, const float4
   const long n = q / (2 * H);
   const int a = Y & 1, b = X & 1, i = Y >> 1, j = X >> 1;
   const float4* src = a ? (b ? p11 : p10) : (b ? p01 : p00);
-  const int Wp = W + b, Hp = H + a;
+  const int Wp = W + (full ? 1 : b), Hp = H + (full ? 1 : a);  // full: every phase is (H+1) x (W+1)
   y[idx] = src[((n * Hp + i + a) * (long)Wp + j + b) * C4 + c4];
 }
 
@@ -333,6 +333,18 @@ extern "C" int vst_interleave_phases(const float* p00, const float* p01, const f
   hipLaunchKernelGGL(interleave_phases_k, dim3(ceil_div(total, 256)), dim3(256), 0, (hipStream_t)stream,
                      reinterpret_cast<const float4*>(p00), reinterpret_cast<const float4*>(p01),
                      reinterpret_cast<const float4*>(p10), reinterpret_cast<const float4*>(p11),
-                     reinterpret_cast<float4*>(y), H, W, C / 4, total);
+                     reinterpret_cast<float4*>(y), H, W, C / 4, total, 0);
   return check_launch("interleave_phases");
+}
+
+extern "C" int vst_interleave_phases_full(const float* p00, const float* p01, const float* p10, const float* p11,
+                                          float* y, int N, int H, int W, int C, void* stream) {
+  VST_REQUIRE(p00 && p01 && p10 && p11 && y && N > 0 && H > 0 && W > 0 && C % 4 == 0,
+              "interleave_phases_full: bad args");
+  const long total = (long)N * 4 * H * W * (C / 4);
+  hipLaunchKernelGGL(interleave_phases_k, dim3(ceil_div(total, 256)), dim3(256), 0, (hipStream_t)stream,
+                     reinterpret_cast<const float4*>(p00), reinterpret_cast<const float4*>(p01),
+                     reinterpret_cast<const float4*>(p10), reinterpret_cast<const float4*>(p11),
+                     reinterpret_cast<float4*>(y), H, W, C / 4, total, 1);
+  return check_launch("interleave_phases_full");
 }

@@ -626,6 +626,9 @@ class NLayerDiscriminator(FlatNet):
         # stride-1 layers with >= 8 output channels: data gradient as a forward conv (IKF pack)
         self._ikf = [(_ikf(m) if (st == 1 and cout % 8 == 0) else None)
                      for m, (cout, st, _) in zip(self._convs(), self.spec)]
+        # stride-2 layers: the data gradient as four 2x2 phase convs (ops.conv4s2_dgrad)
+        self._ph = [(ops.conv4s2_dgrad_phase_packs(m.weight) if (CONVT_PHASES and st == 2 and cout % 8 == 0)
+                     else None) for m, (cout, st, _) in zip(self._convs(), self.spec)]
         return packs
 
     def forward_nhwc(self, x):
@@ -689,9 +692,11 @@ class _DiscriminatorFn(torch.autograd.Function):
                 if final:
                     net._grad_done(m)
             if i > 0 or ctx.needs_input_grad[0]:
-                ikf = net._ikf[i]
+                ikf, ph = net._ikf[i], net._ph[i]
                 if ikf is not None:
                     g = ops.conv2d_dgrad_s1(dy, ikf, a_in.shape[1], a_in.shape[2], a_in.shape[-1], 4, 1)
+                elif ph is not None and a_in.shape[1] == 2 * dy.shape[1] and a_in.shape[2] == 2 * dy.shape[2]:
+                    g = ops.conv4s2_dgrad(dy, ph, a_in.shape[-1])
                 else:
                     _, ck, _ = P[i]
                     g = ops.conv2d_tfwd(dy, ck, None, a_in.shape[1], a_in.shape[2], a_in.shape[-1], 4, 4,

@@ -924,6 +924,36 @@ def convT3s2_phase_packs(wt):
     return packs
 
 
+def conv4s2_dgrad_phase_packs(w):
+    """Phase packs of the data gradient of Conv2d(k=4, stride 2, padding 1) with weight w [Co][Ci][4][4]:
+    output parity a (rows) / b (cols) = a 2x2 conv over dy (padding 1) with taps (3, 1) (even) or
+    (2, 0) (odd) of w read as [out = ci][in = co] (VST_PACK_OK packs, PackBatch tap maps)."""
+    Co, Ci = w.shape[0], w.shape[1]
+    maps = ([3, 1], [2, 0])
+    pb = PackBatch._active
+    if pb is not None:
+        st = (16, Ci * 16, 4, 1)  # logical [o = ci][i = co][r][s] of w[co][ci][kh][kw]
+        return [pb.add(w, PACK_OK, Ci, Co, 2, 2, st, maps[a], maps[b]) for a, b in ((0, 0), (0, 1), (1, 0), (1, 1))]
+    wc = w.detach().permute(1, 0, 2, 3)
+    packs = []
+    for a, b in ((0, 0), (0, 1), (1, 0), (1, 1)):
+        ra, cb = torch.tensor(maps[a], device=w.device), torch.tensor(maps[b], device=w.device)
+        packs.append(weight_pack(wc.index_select(2, ra).index_select(3, cb).contiguous(), PACK_OK))
+    return packs
+
+
+def conv4s2_dgrad(dy, packs, cop, role="bwd"):
+    """Data gradient of Conv2d(k=4, s=2, p=1) onto a (2*Hd) x (2*Wd) input via four 2x2 phase convs
+    (padding 1, outputs (Hd+1) x (Wd+1)) + vst_interleave_phases_full."""
+    _dev_check(dy)
+    N, Hd, Wd, _ = dy.shape
+    outs = [conv2d_fwd(dy, wp, None, cop, 2, 2, 1, 1, "zero", role=role) for wp in packs]
+    y = torch.empty((N, 2 * Hd, 2 * Wd, cop), device=dy.device)
+    _call("vst_interleave_phases_full", _p(outs[0]), _p(outs[1]), _p(outs[2]), _p(outs[3]), _p(y), N, Hd, Wd,
+          cop, _stream())
+    return y
+
+
 def convT3s2_fwd(x, packs, bias, cop, act="none", role="fwd"):
     """ConvTranspose2d(k=3, s=2, p=1, op=1) forward on NHWC x via four phase convs + interleave."""
     _dev_check(x, bias)

@@ -358,6 +358,11 @@ int vst_tapgather(const float* z, float* y, int N, int H, int W, int R, int S, i
  * weight; this interleaves them: y[n][2i+a][2j+b][c] = P_ab[n][i+a][j+b][c] (P_ab is (H+a) x (W+b)). */
 int vst_interleave_phases(const float* p00, const float* p01, const float* p10, const float* p11, float* y, int N,
                           int H, int W, int C, void* stream);
+/* The same interleave for the data gradient of Conv2d(k=4, stride 2, padding 1) (PatchGAN
+ * networks.py:556-578): per output parity two taps per dim (even: w3 at dy[i-1], w1 at dy[i]; odd: w2 at dy[i], w0 at dy[i+1]), i.e. four 2x2 phase convs
+ * with padding 1 whose outputs are all (H+1) x (W+1): y[n][2i+a][2j+b][c] = P_ab[n][i+a][j+b][c]. */
+int vst_interleave_phases_full(const float* p00, const float* p01, const float* p10, const float* p11, float* y,
+                               int N, int H, int W, int C, void* stream);
 
 /* ---- RAFT inference (SURVEY §8 A19 + §8f rank 3) ------------------------------------------ */
 /* Forward conv with separate row / column zero padding (SepConvGRU's (1,5) / (5,1) kernels with

@@ -434,3 +434,32 @@ def test_conv_fwd_in_stats(ops, case, conv_math):
     s_ref = ops.instnorm_stats(y_ref)
     rel = ((s - s_ref).abs() / s_ref.abs().clamp_min(1e-6)).max().item()
     assert rel < 1e-6, rel
+
+
+@pytest.mark.parametrize("ci,co,h,w", [(64, 128, 16, 20), (128, 256, 8, 8), (4, 64, 32, 32)])
+@pytest.mark.parametrize("batched", [False, True], ids=["single", "packbatch"])
+def test_conv4s2_dgrad_phases(ops, conv_math, ci, co, h, w, batched):
+    """Data gradient of the PatchGAN Conv2d(k4, s2, p1) as four 2x2 phase convs + interleave vs
+    torch's conv_transpose2d (= the conv's input gradient); packs built singly and through a
+    PackBatch (tap maps read straight from the weight)."""
+    dy = _g(91, (2, co, h, w))
+    wd = _g(92, (co, ci, 4, 4), 0.05)
+    ref = F.conv_transpose2d(dy, wd, None, stride=2, padding=1)
+    if batched:
+        with ops.PackBatch():
+            packs = ops.conv4s2_dgrad_phase_packs(wd.to(DEV))
+    else:
+        packs = ops.conv4s2_dgrad_phase_packs(wd.to(DEV))
+    g = ops.conv4s2_dgrad(_nhwc(dy, ops), packs, ops.cpad(ci))
+    _close(_nchw(g, ci, ops), ref, tol=CONV_TOL[conv_math], what="conv4s2 dgrad phases")
+
+
+def test_convT3s2_phase_packs_batched_equal_single(ops):
+    """ConvTranspose phase packs recorded in a PackBatch (transposed view + tap maps, no copies)
+    equal the copy-based single packs bit for bit, planes included."""
+    wt = _g(98, (64, 32, 3, 3), 0.05).to(DEV)
+    single = ops.convT3s2_phase_packs(wt)
+    with ops.PackBatch():
+        batched = ops.convT3s2_phase_packs(wt)
+    for s_, b_ in zip(single, batched):
+        assert torch.equal(s_, b_) and torch.equal(s_.vst_split, b_.vst_split)

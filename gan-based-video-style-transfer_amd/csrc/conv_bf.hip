@@ -46,6 +46,12 @@
 #ifndef VST_BF_PRIO
 #define VST_BF_PRIO 0
 #endif
+#ifndef VST_BF_TAIL_FORCE
+#define VST_BF_TAIL_FORCE -1
+#endif
+#ifndef VST_WG_SELECT
+#define VST_WG_SELECT 1
+#endif
 #ifndef VST_BF_STORE_LATE
 #define VST_BF_STORE_LATE 0
 #endif
@@ -489,7 +495,9 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_k(
 // registers for every K-step (the x shifted copy once per tap) and sat at ~0.33 of the x6 ceiling.
 // The split-K chunk index comes from an XCD-aware 1-D grid (every tile of one chunk on one XCD, so
 // its x / dy rows stay in that XCD's L2); partial tiles land in slab[z][m][Cyp].
-template <class T>
+// W1 (Wo >= BK): a K-step crosses at most one output-row end, so the pixel cursor advances with
+// selects only and the two-stage loop body stays one basic block (as the forward's KSL cursor).
+template <class T, bool W1>
 __global__ __launch_bounds__(T::NT, T::MINB) void conv_wgrad_bf_k(
     const float* __restrict__ xt, const __bf16* __restrict__ dyp, long dps, float* __restrict__ slab, int H,
     int W, int Cx, int Ho, int Wo, int Cyp, int S, int pad, int st, int Mw, int P, int chunk, long ldx,
@@ -561,7 +569,20 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_wgrad_bf_k(
       for (int p = 0; p < NP; ++p) rbv[set][j][p] = *reinterpret_cast<const u32x4_t*>(q + p * ps);
     }
   };
+  const long row_step = (long)st * Wp - Wo, img_step = (long)(Hp - st * Ho) * Wp;
   auto adv = [&](bool go) __attribute__((always_inline)) {
+    if (W1 && VST_WG_SELECT) {
+      const int pw1 = pwo + T::BK;
+      const bool e1 = pw1 >= Wo;
+      const int ph1 = pho + (e1 ? 1 : 0);
+      const bool e2 = ph1 == Ho;
+      const long po1 = poff + T::BK + (e1 ? row_step : 0) + (e2 ? img_step : 0);
+      kp = go ? kp + T::BK : kp;
+      pwo = go ? (e1 ? pw1 - Wo : pw1) : pwo;
+      pho = go ? (e2 ? 0 : ph1) : pho;
+      poff = go ? po1 : poff;
+      return;
+    }
     if (!go) return;
     kp += T::BK;
     pwo += T::BK;
@@ -745,6 +766,7 @@ void bf_plan(long M, int Cop, int math, int kind, int* kind_out, int* m_split_ou
         const double cost = (double)(ms / 256 * nt) / VST_NUM_CUS + rounds * (bm * bn) / (256.0 * 128.0) / eff[c];
         if (cost < best - 1e-9) { best = cost; bk = cand[c]; }
       }
+      if (VST_BF_TAIL_FORCE >= 0) bk = VST_BF_TAIL_FORCE;  // developer A/B of the tail tile
       kd = 7;
       if (bk >= 0) {
         m_split = (int)ms;
@@ -824,9 +846,13 @@ void bf_wgrad_launch(const float* xt, const void* dyp, float* slab, int N, int H
 #define VST_BW(BM_, BN_, WM_, WN_, BK_, NP_)                                                          \
   {                                                                                                 \
     using T = bf::Tile<BM_, BN_, WM_, WN_, BK_, NP_>;                                              \
-    hipLaunchKernelGGL((bf::conv_wgrad_bf_k<T>),                                                    \
-                       dim3(ceil_div(Mw, BM_) * ceil_div(Cyp, BN_) * nsplit), dim3(T::NT), 0, s, xt, d, \
-                       dps, slab, H, W, Cx, Ho, Wo, Cyp, S, pad, st, Mw, P, chunk, ldx, ldy);       \
+    const dim3 grid(ceil_div(Mw, BM_) * ceil_div(Cyp, BN_) * nsplit);                              \
+    if (Wo >= BK_)                                                                                  \
+      hipLaunchKernelGGL((bf::conv_wgrad_bf_k<T, true>), grid, dim3(T::NT), 0, s, xt, d, dps, slab, H, W, \
+                         Cx, Ho, Wo, Cyp, S, pad, st, Mw, P, chunk, ldx, ldy);                      \
+    else                                                                                            \
+      hipLaunchKernelGGL((bf::conv_wgrad_bf_k<T, false>), grid, dim3(T::NT), 0, s, xt, d, dps, slab, H, W, \
+                         Cx, Ho, Wo, Cyp, S, pad, st, Mw, P, chunk, ldx, ldy);                      \
   }
   if (math == VST_MATH_BF16X6) {
     VST_BF_DISPATCH(kind, 3, VST_BW)

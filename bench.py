@@ -104,6 +104,17 @@ def _pmc_traffic(name, key):
     return rec.get("hbm_bytes_per_launch")
 
 
+def _mfma(m):
+    """The MFMA instruction the split-bf16 GEMMs of arithmetic m issue in this build (vst_build_info)."""
+    from gbvst import ops
+    if m == "fp32":
+        return "v_mfma_f32_32x32x2_f32"
+    info = ops.lib().vst_build_info().decode()
+    tag = "x6_mfma=" if m == "bf16x6" else "x3_mfma="
+    shape = info.split(tag)[1].split()[0] if tag in info else "32x32x16"
+    return "v_mfma_f32_%s_bf16" % shape
+
+
 def conv_roofline(name, probe, math):
     """Roofline entry of one probed conv: algorithmic FLOPs (2*M*N*K of the conv it computes) per
     launch / the average duration of its launches inside the timed steps (HIP events on the launch
@@ -122,15 +133,17 @@ def conv_roofline(name, probe, math):
     achieved = flop / (ms * 1e-3) / 1e12
     if op == "fwd":
         kind, ms_ = ops.conv_plan_fwd(N, H, W, Cx, Cop, R, R, st, pad, pad, m)
-        kernel = "conv_fprop_bf_k<%s, %s>%s" % (ops.TILE_NAMES.get(kind, kind), m, " + 64x64 tail" if ms_ else "")
-        key = {"math": m, "tile": kind, "m_split": ms_, "N": N}
+        kernel = "conv_fprop_bf_k<%s, %s, %s>%s" % (ops.TILE_NAMES.get(kind, kind), m, _mfma(m),
+                                                    " + tail launch" if ms_ else "")
+        key = {"math": m, "tile": kind, "m_split": ms_, "N": N, "mfma": _mfma(m)}
         note = ("stride-1 data gradient as a forward conv over the rotated taps (66x66 padded frame)"
                 if name == "resblock_dgrad" else "ResnetBlock conv forward")
     else:
         kernel = ("vst_conv2d_wgrad: nhwc_to_cp_pad_k + nhwc_to_cp_planes_k copies + conv_wgrad_bf_k "
                   "(split-K slabs) + wgrad_reduce_store_k, %s" % m if m != "fp32" else
                   "vst_conv2d_wgrad: channel-major copies + conv_wgrad_rk_k + wgrad_reduce_store_k, fp32")
-        key = {"math": m, "N": N}
+        key = {"math": m, "N": N, "mfma": _mfma(m)}
+        kernel += " [%s]" % _mfma(m)
         note = "whole weight-gradient op: its 4-5 launches are timed together"
     return {"kernel": kernel, "what": note + " — ResnetBlock 3x3 reflect 256->256 @64x64, N=%d" % N,
             "bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": "TFLOP/s",

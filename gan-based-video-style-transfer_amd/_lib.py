@@ -36,6 +36,7 @@ SZ = ctypes.c_size_t
 SIGNATURES = {
     "vst_last_error": (ctypes.c_char_p, []),
     "vst_version": (I, []),
+    "vst_build_info": (ctypes.c_char_p, []),
     "vst_nchw_to_nhwc": (I, [P, P, I, I, I, I, I, P]),
     "vst_nhwc_to_nchw": (I, [P, P, I, I, I, I, I, P]),
     "vst_weight_pack": (I, [P, P, I, I, I, I, I, I, I, P]),

@@ -52,6 +52,12 @@
 #ifndef VST_M16_STORE
 #define VST_M16_STORE 0  // M16 loop: stage store in group B (0) or group A (1)
 #endif
+#ifndef VST_M16_RDLO
+#define VST_M16_RDLO 0  // M16 loop: lo plane read in group B (0) or with hi in group A (1)
+#endif
+#ifndef VST_M16_SCHED
+#define VST_M16_SCHED 0  // M16 loop: sched_group_barrier filler pattern (0: compiler order)
+#endif
 #ifndef VST_BF_TAIL_FORCE
 #define VST_BF_TAIL_FORCE -1
 #endif
@@ -395,24 +401,26 @@ __device__ __forceinline__ void main_loop16(char* smem, int nk, f32x4v (&acc)[T:
     constexpr int P = decltype(par)::value;
     const char* cur = smem + P * T::STAGE;
     char* nxt = smem + (P ^ 1) * T::STAGE;
+    constexpr bool SA = VST_M16_STORE == 1, RA = VST_M16_RDLO == 1;
     read_plane16<T>(hi, cur, 0, wm0, wn0, lane);
+    if (RA) read_plane16<T>(lo, cur, 2, wm0, wn0, lane);
     adv(kt + 2 < nk);
     load_all(P);
-    if (VST_M16_STORE == 1) store_stage<T>(nxt, ra[P ^ 1], rbv[P ^ 1], rb, kq);
+    if (SA) store_stage<T>(nxt, ra[P ^ 1], rbv[P ^ 1], rb, kq);
     mma16<T>(mid, mid, acc);
-    if (VST_BF_SCHED) sched16<NM, NR, NV, VST_M16_STORE == 1 ? 4 : 0, VST_M16_STORE == 1 ? NW : 0>();
-    read_plane16<T>(lo, cur, 2, wm0, wn0, lane);
-    if (VST_M16_STORE == 0) store_stage<T>(nxt, ra[P ^ 1], rbv[P ^ 1], rb, kq);
+    if (VST_M16_SCHED) sched16<NM, RA ? 2 * NR : NR, NV, SA ? 4 : 0, SA ? NW : 0>();
+    if (!RA) read_plane16<T>(lo, cur, 2, wm0, wn0, lane);
+    if (!SA) store_stage<T>(nxt, ra[P ^ 1], rbv[P ^ 1], rb, kq);
     mma16<T>(mid, hi, acc);
     mma16<T>(hi, mid, acc);
-    if (VST_BF_SCHED) sched16<2 * NM, NR, 0, VST_M16_STORE == 0 ? 2 : 0, VST_M16_STORE == 0 ? NW : 0>();
+    if (VST_M16_SCHED) sched16<2 * NM, RA ? 0 : NR, 0, SA ? 0 : 2, SA ? 0 : NW>();
     __builtin_amdgcn_sched_barrier(0);
     __syncthreads();
     read_plane16<T>(mid, nxt, 1, wm0, wn0, lane);
     mma16<T>(hi, hi, acc);
     mma16<T>(lo, hi, acc);
     mma16<T>(hi, lo, acc);
-    if (VST_BF_SCHED) sched16<3 * NM, NR, 0, 0, 0>();
+    if (VST_M16_SCHED) sched16<3 * NM, NR, 0, 0, 0>();
   };
   int kt = 0;
   for (; kt + 1 < nk; kt += 2) {
@@ -1073,6 +1081,21 @@ void bf_wgrad_geom(int kind, int math, int* bm, int* bn, int* bk, int* slots) {
 }  // namespace vst
 
 using namespace vst;
+
+extern "C" const char* vst_build_info(void) {
+#define VST_STR2(x) #x
+#define VST_STR(x) VST_STR2(x)
+#if VST_BF_MF16
+#define VST_X6_MFMA "16x16x32"
+#else
+#define VST_X6_MFMA "32x32x16"
+#endif
+  return "x6_mfma=" VST_X6_MFMA " x3_mfma=32x32x16 kslice=" VST_STR(VST_BF_KSLICE) " x6_256=" VST_STR(VST_BF_X6_256)
+         " m16_store=" VST_STR(VST_M16_STORE) " m16_sched=" VST_STR(VST_M16_SCHED);
+#undef VST_X6_MFMA
+#undef VST_STR
+#undef VST_STR2
+}
 
 extern "C" int vst_weight_split(const float* w, void* out, long n, void* stream) {
   VST_REQUIRE(w && out && n > 0, "weight_split: bad args");

@@ -64,6 +64,9 @@ enum { VST_PACK_KC = 0,   /* [R][S][Ci][Co]  (rows k=(r,s,ci), cols co) */
 
 const char* vst_last_error(void);
 int vst_version(void);
+/* Build configuration of the conv kernels, e.g. "x6_mfma=16x16x32 x3_mfma=32x32x16 kslice=1 x6_256=1":
+ * which MFMA instruction the split-bf16 GEMMs issue (recorded with every roofline / PMC record). */
+const char* vst_build_info(void);
 
 /* ---- layout ------------------------------------------------------------------------------ */
 /* NCHW (C logical channels) <-> NHWC with channel stride Cs >= C (pad channels written 0). */

@@ -61,6 +61,11 @@ def main():
         t = kernel_times(os.path.join(d, op + "_kt"), MAIN[op])
         name = "warp" if op == "warp" else "resblock_" + op
         key = {"N": 32, "C": 64, "H": 436, "W": 1024} if op == "warp" else {"math": "bf16x6", "N": B}
+        if op != "warp":  # the MFMA instruction of this build (bench.py matches records on it)
+            import gbvst
+            gbvst._lib.load()
+            info = gbvst._lib.load().vst_build_info().decode()
+            key["mfma"] = "v_mfma_f32_%s_bf16" % info.split("x6_mfma=")[1].split()[0]
         if op in ("fprop", "dgrad"):
             import gbvst
             from gbvst import ops

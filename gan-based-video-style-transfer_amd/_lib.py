@@ -58,6 +58,10 @@ SIGNATURES = {
     "vst_instnorm_stats": (I, [P, P, P, I, I, I, F, P]),
     "vst_instnorm_act_fwd": (I, [P, P, P, P, I, I, I, I, F, P]),
     "vst_instnorm_act_bwd": (I, [P, P, P, P, P, P, I, I, I, I, F, I, P]),
+    "vst_instnorm_act_bwd_planes": (I, [P, P, P, P, P, P, I, I, I, I, F, I, P, L, P]),
+    "vst_conv2d_wgrad_pre": (I, [P, P, P, P, P, SZ, I, I, I, I, I, I, I, I, I, I, I, I, I, I, L, L, I, I, P]),
+    "vst_cp_ld": (L, [L]),
+    "vst_reflect_fold_instnorm_bwd": (I, [P, P, P, P, P, P, P, P, I, I, I, I, I, I, F, I, P, L, P]),
     "vst_act_bwd": (I, [P, P, P, L, I, F, P]),
     "vst_warp_fwd": (I, [P, P, P, I, I, I, I, I, P]),
     "vst_warp_bwd_input": (I, [P, P, P, I, I, I, I, I, P]),

@@ -132,6 +132,107 @@ __global__ __launch_bounds__(NRED) void in_partial_k(const float* __restrict__ x
   }
 }
 
+// The reflect fold of a stride-1 data gradient computed over the padded frame (vst_reflect_fold:
+// g[n][h][w] = addend + sum of dxp over the padded positions that mirror onto (h, w)), fused with
+// the backward partials of the InstanceNorm(+act) below it (in_partial_k<1> over g): g is written
+// once and reduced while in registers, so the IN backward's separate read of g (and of its launch)
+// is gone.  Same block geometry / partial layout / summation order as in_partial_k<1>.
+__global__ __launch_bounds__(NRED) void fold_in_partial_k(const float* __restrict__ dxp,
+                                                          const float* __restrict__ addend,
+                                                          float* __restrict__ gout, const float* __restrict__ x,
+                                                          const float* __restrict__ stats,
+                                                          double* __restrict__ part, int H, int W, int C,
+                                                          int pad, int LP, int PG, int SP, int nsplit, int act,
+                                                          float slope) {
+  constexpr int NV = 3;
+  __shared__ double red[NV * 4][NRED];
+  const int t = threadIdx.x, c4 = t % LP, pg = t / LP;
+  const int n = blockIdx.y, z = blockIdx.x;
+  const int HW = H * W, Hp = H + 2 * pad, Wp = W + 2 * pad;
+  const int p0 = z * SP, p1 = min(HW, p0 + SP);
+  double acc[NV][4];
+#pragma unroll
+  for (int v = 0; v < NV; ++v)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[v][j] = 0.0;
+  float mean[4], rstd[4];
+  {
+    const float4 s0 = reinterpret_cast<const float4*>(stats)[((long)n * C + 4 * c4) / 2];
+    const float4 s1 = reinterpret_cast<const float4*>(stats)[((long)n * C + 4 * c4) / 2 + 1];
+    mean[0] = s0.x; rstd[0] = s0.y; mean[1] = s0.z; rstd[1] = s0.w;
+    mean[2] = s1.x; rstd[2] = s1.y; mean[3] = s1.z; rstd[3] = s1.w;
+  }
+  const float4* src = reinterpret_cast<const float4*>(dxp) + (long)n * Hp * Wp * LP + c4;
+  const float4* xb = reinterpret_cast<const float4*>(x) + (long)n * HW * LP + c4;
+  const float4* ab = addend ? reinterpret_cast<const float4*>(addend) + (long)n * HW * LP + c4 : nullptr;
+  float4* gb = reinterpret_cast<float4*>(gout) + (long)n * HW * LP + c4;
+  auto fold = [&](int p) {
+    const int h = p / W, w = p - (p / W) * W;
+    int hs[3], wsx[3], nh = 0, nw = 0;
+    hs[nh++] = h + pad;
+    if (h >= 1 && h <= pad) hs[nh++] = pad - h;
+    if (h >= H - 1 - pad && h <= H - 2) hs[nh++] = 2 * H - 2 - h + pad;
+    wsx[nw++] = w + pad;
+    if (w >= 1 && w <= pad) wsx[nw++] = pad - w;
+    if (w >= W - 1 - pad && w <= W - 2) wsx[nw++] = 2 * W - 2 - w + pad;
+    float4 g = ab ? ab[(long)p * LP] : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int a = 0; a < nh; ++a)
+      for (int b = 0; b < nw; ++b) add_f4(g, src[((long)hs[a] * Wp + wsx[b]) * LP]);
+    gb[(long)p * LP] = g;
+    return g;
+  };
+  auto accum = [&](const float4 v, const float4 gv) {
+    const float xv[4] = {v.x, v.y, v.z, v.w}, gg[4] = {gv.x, gv.y, gv.z, gv.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float xh = (xv[j] - mean[j]) * rstd[j];
+      float d = 1.f;
+      if (act == VST_ACT_RELU) d = xh > 0.f ? 1.f : 0.f;
+      else if (act == VST_ACT_LRELU) d = xh > 0.f ? 1.f : slope;
+      const float g = gg[j] * d;
+      acc[0][j] += g;
+      acc[1][j] += (double)g * xh;
+      acc[2][j] += xh;
+    }
+  };
+  constexpr int UR = 2;
+  if (pg < PG) {
+    int p = p0 + pg;
+    for (; p + (UR - 1) * PG < p1; p += UR * PG) {
+      float4 v[UR], gv[UR];
+#pragma unroll
+      for (int k = 0; k < UR; ++k) {
+        v[k] = xb[(long)(p + k * PG) * LP];
+        gv[k] = fold(p + k * PG);
+      }
+#pragma unroll
+      for (int k = 0; k < UR; ++k) accum(v[k], gv[k]);
+    }
+    for (; p < p1; p += PG) accum(xb[(long)p * LP], fold(p));
+  }
+#pragma unroll
+  for (int v = 0; v < NV; ++v)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) red[v * 4 + j][t] = acc[v][j];
+  __syncthreads();
+  if (pg == 0) {
+    double out[NV][4];
+#pragma unroll
+    for (int v = 0; v < NV; ++v)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        double sum = 0.0;
+        for (int q = 0; q < PG; ++q) sum += red[v * 4 + j][q * LP + c4];
+        out[v][j] = sum;
+      }
+    double* dst = part + (((long)n * nsplit + z) * C + 4 * c4) * NV;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int v = 0; v < NV; ++v) dst[j * NV + v] = out[v][j];
+  }
+}
+
 // Fold the per-slice partials of one (n, 64-channel group): 4 waves stride the slices (coalesced
 // over c), then combine through LDS in a fixed order.  out[v] = sum_z part[n][z][c][v].
 template <int NV>
@@ -259,6 +360,78 @@ __global__ void in_bwd_apply_k(const float4* __restrict__ gy, const float4* __re
   o.z = in_bwd1(g.z, v.z, s1.x, s1.y, make_float2(k23.x, k23.y), act, slope);
   o.w = in_bwd1(g.w, v.w, s1.z, s1.w, make_float2(k23.z, k23.w), act, slope);
   dx[i] = o;
+}
+
+// in_bwd_apply_k fused with the weight gradient's B-operand image: dx = the IN(+act) input gradient
+// written NHWC (the data gradient's A operand) AND as three bf16 planes [3][C][ldp] (hi, mid, lo;
+// the RNE split of vst_weight_split / nhwc_to_cp_planes_k) through a 64-pixel x 64-channel LDS
+// transpose tile — the conv below the IN consumes dx both ways, so the plane copy's extra read of dx
+// is gone.  grid (ceil(P / 64), ceil(C / 64)), 256 threads.
+__device__ __forceinline__ uint32_t bf16_pack2(float a, float b) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  typedef __bf16 b2 __attribute__((ext_vector_type(2)));
+  const f2 v = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, b2));
+}
+
+__global__ __launch_bounds__(256) void in_bwd_apply_planes_k(const float* __restrict__ gy, const float* __restrict__ x,
+                                                              const float* __restrict__ stats,
+                                                              const float2* __restrict__ coef, float* __restrict__ dx,
+                                                              __bf16* __restrict__ planes, long P, int HW, int C,
+                                                              long ldp, int act, float slope) {
+  __shared__ float tile[64][65];
+  const long p0 = (long)blockIdx.x * 64;
+  const int c0 = blockIdx.y * 64;
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int idx = t + 256 * it, pr = idx >> 4, c4 = (idx & 15) * 4;
+    float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+    const long q = p0 + pr;
+    if (q < P && c0 + c4 < C) {
+      const long nc = (q / HW) * C + c0 + c4;
+      const float4 s0 = reinterpret_cast<const float4*>(stats)[nc / 2];
+      const float4 s1 = reinterpret_cast<const float4*>(stats)[nc / 2 + 1];
+      const float4 k01 = reinterpret_cast<const float4*>(coef)[nc / 2];
+      const float4 k23 = reinterpret_cast<const float4*>(coef)[nc / 2 + 1];
+      const float4 g = *reinterpret_cast<const float4*>(gy + q * C + c0 + c4);
+      const float4 v = *reinterpret_cast<const float4*>(x + q * C + c0 + c4);
+      o.x = in_bwd1(g.x, v.x, s0.x, s0.y, make_float2(k01.x, k01.y), act, slope);
+      o.y = in_bwd1(g.y, v.y, s0.z, s0.w, make_float2(k01.z, k01.w), act, slope);
+      o.z = in_bwd1(g.z, v.z, s1.x, s1.y, make_float2(k23.x, k23.y), act, slope);
+      o.w = in_bwd1(g.w, v.w, s1.z, s1.w, make_float2(k23.z, k23.w), act, slope);
+      *reinterpret_cast<float4*>(dx + q * C + c0 + c4) = o;
+    }
+    tile[pr][c4] = o.x;
+    tile[pr][c4 + 1] = o.y;
+    tile[pr][c4 + 2] = o.z;
+    tile[pr][c4 + 3] = o.w;
+  }
+  __syncthreads();
+  const long plane = (long)C * ldp;
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int idx = t + 256 * it, cr = idx >> 4, p4 = (idx & 15) * 4;
+    if (c0 + cr >= C || p0 + p4 >= P) continue;
+    float r[4] = {tile[p4][cr], tile[p4 + 1][cr], tile[p4 + 2][cr], tile[p4 + 3][cr]};
+    __bf16* dst = planes + (long)(c0 + cr) * ldp + p0 + p4;
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) {
+      const uint32_t q0 = bf16_pack2(r[0], r[1]), q1 = bf16_pack2(r[2], r[3]);
+      if (p0 + p4 + 3 < P) {
+        *reinterpret_cast<uint2*>(dst + pl * plane) = make_uint2(q0, q1);
+      } else {
+        const uint16_t h[4] = {(uint16_t)q0, (uint16_t)(q0 >> 16), (uint16_t)q1, (uint16_t)(q1 >> 16)};
+        for (int e = 0; e < 4 && p0 + p4 + e < P; ++e) reinterpret_cast<uint16_t*>(dst + pl * plane)[e] = h[e];
+      }
+      if (pl < 2) {
+        r[0] -= __uint_as_float(q0 << 16);
+        r[1] -= __uint_as_float(q0 & 0xffff0000u);
+        r[2] -= __uint_as_float(q1 << 16);
+        r[3] -= __uint_as_float(q1 & 0xffff0000u);
+      }
+    }
+  }
 }
 
 __global__ void act_bwd_k(const float* __restrict__ gy, const float* __restrict__ y,
@@ -574,23 +747,69 @@ extern "C" int vst_instnorm_act_fwd(const float* x, const float* stats, const fl
   return check_launch("instnorm_act_fwd");
 }
 
+extern "C" int vst_instnorm_act_bwd_planes(const float* gy, const float* x, const float* stats, float* dx,
+                                           float* db, float* ws, int N, int HW, int C, int act, float slope,
+                                           int accumulate_db, void* planes, long ldp, void* stream);
+
 extern "C" int vst_instnorm_act_bwd(const float* gy, const float* x, const float* stats, float* dx,
                                     float* db, float* ws, int N, int HW, int C, int act, float slope,
                                     int accumulate_db, void* stream) {
+  return vst_instnorm_act_bwd_planes(gy, x, stats, dx, db, ws, N, HW, C, act, slope, accumulate_db, nullptr,
+                                     0, stream);
+}
+
+// IN backward after its partials are in ws: finalize, bias gradient, apply (+ planes).
+static int in_bwd_tail(const float* gy, const float* x, const float* stats, float* dx, float* db, float* ws,
+                       int N, int HW, int C, int act, float slope, int accumulate_db, void* planes, long ldp,
+                       const RedGeom& g, hipStream_t s);
+
+extern "C" int vst_instnorm_act_bwd_planes(const float* gy, const float* x, const float* stats, float* dx,
+                                           float* db, float* ws, int N, int HW, int C, int act, float slope,
+                                           int accumulate_db, void* planes, long ldp, void* stream) {
   RedGeom g;
   VST_REQUIRE(gy && x && stats && dx && ws && red_geom(N, HW, C, g), "instnorm_act_bwd: bad args");
+  VST_REQUIRE(!planes || ldp >= (long)N * HW, "instnorm_act_bwd: plane stride %ld < N*HW", ldp);
   hipStream_t s = (hipStream_t)stream;
+  double* part = reinterpret_cast<double*>(ws);
+  hipLaunchKernelGGL(in_partial_k<1>, dim3(g.nsplit, N), dim3(NRED), 0, s, x, gy, stats, part, HW, C,
+                     g.LP, g.PG, g.SP, g.nsplit, act, slope);
+  return in_bwd_tail(gy, x, stats, dx, db, ws, N, HW, C, act, slope, accumulate_db, planes, ldp, g, s);
+}
+
+extern "C" int vst_reflect_fold_instnorm_bwd(const float* dxp, const float* addend, float* gout, const float* x,
+                                             const float* stats, float* dx, float* db, float* ws, int N, int H,
+                                             int W, int C, int pad, int act, float slope, int accumulate_db,
+                                             void* planes, long ldp, void* stream) {
+  RedGeom g;
+  const int HW = H * W;
+  VST_REQUIRE(dxp && gout && x && stats && dx && ws && pad >= 0 && pad < H && pad < W && red_geom(N, HW, C, g),
+              "reflect_fold_instnorm_bwd: bad args");
+  VST_REQUIRE(!planes || ldp >= (long)N * HW, "reflect_fold_instnorm_bwd: plane stride %ld < N*HW", ldp);
+  hipStream_t s = (hipStream_t)stream;
+  double* part = reinterpret_cast<double*>(ws);
+  hipLaunchKernelGGL(fold_in_partial_k, dim3(g.nsplit, N), dim3(NRED), 0, s, dxp, addend, gout, x, stats, part,
+                     H, W, C, pad, g.LP, g.PG, g.SP, g.nsplit, act, slope);
+  return in_bwd_tail(gout, x, stats, dx, db, ws, N, HW, C, act, slope, accumulate_db, planes, ldp, g, s);
+}
+
+static int in_bwd_tail(const float* gy, const float* x, const float* stats, float* dx, float* db, float* ws,
+                       int N, int HW, int C, int act, float slope, int accumulate_db, void* planes, long ldp,
+                       const RedGeom& g, hipStream_t s) {
   double* part = reinterpret_cast<double*>(ws);
   float2* coef = reinterpret_cast<float2*>(reinterpret_cast<char*>(ws) +
                                            (size_t)N * g.nsplit * C * 3 * sizeof(double));
-  hipLaunchKernelGGL(in_partial_k<1>, dim3(g.nsplit, N), dim3(NRED), 0, s, x, gy, stats, part, HW, C,
-                     g.LP, g.PG, g.SP, g.nsplit, act, slope);
   double* dbn = reinterpret_cast<double*>(reinterpret_cast<char*>(coef) + (size_t)N * C * sizeof(float2));
   hipLaunchKernelGGL(in_bwd_finalize_k, dim3(ceil_div(C, 64), N), dim3(256), 0, s, part, stats, coef, dbn,
                      N, HW, C, g.nsplit);
   if (db)
     hipLaunchKernelGGL(in_bias_grad_k, dim3(ceil_div(C, 256)), dim3(256), 0, s, dbn, db, N, C,
                        accumulate_db);
+  if (planes) {
+    const long P = (long)N * HW;
+    hipLaunchKernelGGL(in_bwd_apply_planes_k, dim3(ceil_div(P, 64), ceil_div(C, 64)), dim3(256), 0, s, gy, x, stats,
+                       coef, dx, reinterpret_cast<__bf16*>(planes), P, HW, C, ldp, act, slope);
+    return check_launch("instnorm_act_bwd_planes");
+  }
   const long total4 = (long)N * HW * C / 4;
   hipLaunchKernelGGL(in_bwd_apply_k, dim3(ceil_div(total4, 256)), dim3(256), 0, s,
                      reinterpret_cast<const float4*>(gy), reinterpret_cast<const float4*>(x), stats,

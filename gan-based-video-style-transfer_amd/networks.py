@@ -418,6 +418,34 @@ class ResnetGenerator(FlatNet):
         return _GeneratorFn.apply(x, self._anchor(), self)
 
 
+# The IN backward writes the weight gradient's dy operand image itself (bf16 planes,
+# ops.instnorm_act_bwd(planes=True)) when that weight gradient runs on the x6 split-bf16 kernel;
+# VST_IN_PLANES=0 keeps the separate plane copy inside vst_conv2d_wgrad.
+IN_PLANES = os.environ.get("VST_IN_PLANES", "1") != "0"
+# The reflect fold of a stride-1 data gradient and the IN backward partials of the layer below it as
+# one pass (ops.conv2d_dgrad_s1_in, VST_FOLD_IN=1).  Off by default: the fused pass is bit-identical
+# but its per-thread fp64 reduction chains run on the fold's (nsplit x N)-block geometry, slower
+# than the elementwise fold + separate partials (C2 step A/B: 65.43 vs 65.24 ms; planes-only 64.80).
+FOLD_IN = os.environ.get("VST_FOLD_IN", "0") == "1"
+_WPLAN_BF = 2  # ops.WPLAN_NAMES: copies + conv_wgrad_bf_k
+
+
+@functools.lru_cache(maxsize=256)
+def _wgrad_on_bf(N, H, W, Cx, Ho, Wo, Cyp, R, st, policy):
+    return ops.conv_plan_wgrad(N, H, W, Cx, Ho, Wo, Cyp, R, R, st, "bwd")[0] == _WPLAN_BF
+
+
+def _in_bwd_for_wgrad(g, y, s, act, slope, db, x_in, R, st, want):
+    """instnorm_act_bwd -> (dy, dy_planes or None); planes only when the wgrad of the conv below
+    (input x_in, kernel R, stride st) takes the x6 split-bf16 path."""
+    if want and IN_PLANES:
+        N, H, W, Cx = x_in.shape
+        _, Ho, Wo, Cyp = y.shape
+        if _wgrad_on_bf(N, H, W, Cx, Ho, Wo, Cyp, R, st, ops.get_conv_math()):
+            return ops.instnorm_act_bwd(g, y, s, act, slope, db=db, planes=True)
+    return ops.instnorm_act_bwd(g, y, s, act, slope, db=db), None
+
+
 class _GeneratorFn(torch.autograd.Function):
     """Whole-generator forward/backward on libvst_hip kernels."""
 
@@ -493,19 +521,22 @@ class _GeneratorFn(torch.autograd.Function):
             if final:
                 net._grad_done(mod)
 
-        def wgrad(mod, inp, dy, R, st, pad, mode, db=False):
+        def wgrad(mod, inp, dy, R, st, pad, mode, db=False, dy_planes=None):
             if not train_w:
                 return
             w = mod.weight
             co, ci = w.shape[0], w.shape[1]
             ops.conv2d_wgrad(inp, dy, w.grad, mod.bias.grad if (db and mod.bias is not None) else None,
-                             R, R, st, pad, mode, co, ci, ci * R * R, R * R, accumulate=True)
+                             R, R, st, pad, mode, co, ci, ci * R * R, R * R, accumulate=True, dy_planes=dy_planes)
 
-        def in_bwd(g, y, s, act, mod):
+        def in_bwd(g, y, s, act, mod, x_in=None, R=3, st=1):
             # IN(+act) backward; the bias gradient of the conv feeding the IN comes out of the
-            # same reduction (sum of dy per channel)
+            # same reduction (sum of dy per channel).  x_in given: also the dy planes of that
+            # conv's x6 weight gradient (None when it runs elsewhere) -> (dy, planes)
             db = mod.bias.grad if (train_w and mod.bias is not None) else None
-            return ops.instnorm_act_bwd(g, y, s, act, db=db)
+            if x_in is None:
+                return ops.instnorm_act_bwd(g, y, s, act, db=db)
+            return _in_bwd_for_wgrad(g, y, s, act, 0.0, db, x_in, R, st, train_w)
 
         def dgrad_reflect(dy, key, cin_p, R, p, H, W, addend=None):
             ikf = P["ikf"].get(key)
@@ -551,33 +582,69 @@ class _GeneratorFn(torch.autograd.Function):
             done(m)
             kc, _, _ = P[f"u{i}"]
             ga = ops.conv2d_fwd(dy, kc, None, a_in.shape[-1], 3, 3, 2, 1, "zero", role="bwd")
-        # residual blocks
+        def dgrad_reflect_in(dy, key, H, W, y_in, s_in, act, mod, x_w, R_w, st_w, addend=None):
+            """dgrad_reflect (3x3, pad 1) + the IN(+act) backward of the layer below it (y_in, s_in;
+            mod = the conv feeding that IN; x_w / R_w / st_w = that conv's weight-gradient input
+            and geometry) -> (g, dy_in, dy_in planes or None).  The fold and the IN backward
+            partials are one pass (ops.conv2d_dgrad_s1_in) when the data gradient runs as a forward
+            conv; otherwise the two steps run separately."""
+            ikf = P["ikf"].get(key)
+            cin_p = y_in.shape[-1]
+            if FOLD_IN and ikf is not None and dy.shape[-1] % 8 == 0 and ikf.shape[0] == cin_p:
+                db = mod.bias.grad if (train_w and mod.bias is not None) else None
+                N = x_w.shape[0]
+                want = (train_w and IN_PLANES and
+                        _wgrad_on_bf(N, x_w.shape[1], x_w.shape[2], x_w.shape[3], y_in.shape[1], y_in.shape[2],
+                                     cin_p, R_w, st_w, ops.get_conv_math()))
+                r = ops.conv2d_dgrad_s1_in(dy, ikf, H, W, cin_p, 3, 1, y_in, s_in, act, 0.0, addend=addend,
+                                           db=db, planes=want)
+                return r if want else (r[0], r[1], None)
+            g = dgrad_reflect(dy, key, cin_p, 3, 1, H, W, addend=addend)
+            dyi, pl = in_bwd(g, y_in, s_in, act, mod, x_w, R_w, st_w)
+            return g, dyi, pl
+
+        # residual blocks: block i's data gradients each carry the IN backward of the layer below
+        # (IN 1 of block i; IN 2 of block i - 1, or the IN of d1 after block 0)
         gh = ga
-        for i in reversed(range(len(blocks))):
+        nb = len(blocks)
+        pre_d1 = None
+        if nb:
+            dv, dvp = in_bwd(gh, sv[f"b{nb - 1}"][4], sv[f"b{nb - 1}"][5], "none", blocks[-1].conv_block[5],
+                             sv[f"b{nb - 1}"][3])
+        for i in reversed(range(nb)):
             h, t, s1, uu, v, s2 = sv[f"b{i}"]
             blk = blocks[i].conv_block
-            dv = in_bwd(gh, v, s2, "none", blk[5])
-            wgrad(blk[5], uu, dv, 3, 1, 1, "reflect")
+            wgrad(blk[5], uu, dv, 3, 1, 1, "reflect", dy_planes=dvp)
             done(blk[5])
-            du = dgrad_reflect(dv, f"b{i}b", uu.shape[-1], 3, 1, uu.shape[1], uu.shape[2])
-            dt = in_bwd(du, t, s1, "relu", blk[1])
-            wgrad(blk[1], h, dt, 3, 1, 1, "reflect")
+            _, dt, dtp = dgrad_reflect_in(dv, f"b{i}b", uu.shape[1], uu.shape[2], t, s1, "relu", blk[1], h, 3, 1)
+            wgrad(blk[1], h, dt, 3, 1, 1, "reflect", dy_planes=dtp)
             done(blk[1])
-            gh = dgrad_reflect(dt, f"b{i}a", h.shape[-1], 3, 1, h.shape[1], h.shape[2], addend=gh)
+            if i > 0:
+                _, _, _, uup, vp, s2p = sv[f"b{i - 1}"]
+                gh, dv, dvp = dgrad_reflect_in(dt, f"b{i}a", h.shape[1], h.shape[2], vp, s2p, "none",
+                                               blocks[i - 1].conv_block[5], uup, 3, 1, addend=gh)
+            else:
+                y1, s1d, _ = sv["d1"]
+                gh, dy1, dyp1 = dgrad_reflect_in(dt, f"b{i}a", h.shape[1], h.shape[2], y1, s1d, "relu", d[1],
+                                                 sv["d0"][2], 3, 2, addend=gh)
+                pre_d1 = (dy1, dyp1)
         ga = gh
         # down-sampling convs
         for key, mod, prev in (("d1", d[1], "d0"), ("d0", d[0], "c0")):
             y, s, _ = sv[key]
             a_in = sv[prev][2]
-            dy = in_bwd(ga, y, s, "relu", mod)
-            wgrad(mod, a_in, dy, 3, 2, 1, "zero")
+            if key == "d1" and pre_d1 is not None:
+                dy, dyp = pre_d1
+            else:
+                dy, dyp = in_bwd(ga, y, s, "relu", mod, a_in, 3, 2)
+            wgrad(mod, a_in, dy, 3, 2, 1, "zero", dy_planes=dyp)
             done(mod)
             ga = dgrad_s2(dy, key, a_in.shape[-1], a_in.shape[1], a_in.shape[2])
         # first conv
         x = sv["x"]
         y, s, _ = sv["c0"]
-        dy = in_bwd(ga, y, s, "relu", c0)
-        wgrad(c0, sv.get("x8", x), dy, 7, 1, 3, "reflect")
+        dy, dyp = in_bwd(ga, y, s, "relu", c0, sv.get("x8", x), 7, 1)
+        wgrad(c0, sv.get("x8", x), dy, 7, 1, 3, "reflect", dy_planes=dyp)
         done(c0)
         gx = None
         if ctx.needs_input_grad[0]:
@@ -677,9 +744,10 @@ class _DiscriminatorFn(torch.autograd.Function):
             a_in, y, s, an = saved[i]
             m = convs[i]
             cout, st, has_in = net.spec[i]
+            dyp = None
             if has_in:
                 db = m.bias.grad if (ctx.train_w and m.bias is not None) else None
-                dy = ops.instnorm_act_bwd(g, y, s, "lrelu", SLOPE, db=db)
+                dy, dyp = _in_bwd_for_wgrad(g, y, s, "lrelu", SLOPE, db, a_in, 4, st, ctx.train_w)
             elif i != L - 1:
                 dy = ops.act_bwd(g, an, "lrelu", SLOPE)
             else:
@@ -688,7 +756,7 @@ class _DiscriminatorFn(torch.autograd.Function):
                 co, ci = m.weight.shape[0], m.weight.shape[1]
                 ops.conv2d_wgrad(a_in, dy, m.weight.grad,
                                  m.bias.grad if (m.bias is not None and not has_in) else None,
-                                 4, 4, st, 1, "zero", co, ci, ci * 16, 16, accumulate=True)
+                                 4, 4, st, 1, "zero", co, ci, ci * 16, 16, accumulate=True, dy_planes=dyp)
                 if final:
                     net._grad_done(m)
             if i > 0 or ctx.needs_input_grad[0]:

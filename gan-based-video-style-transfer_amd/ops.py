@@ -243,16 +243,17 @@ def conv2d_tfwd(x, wp, bias, Ho, Wo, cx, R, S, stride, pad, act="none", slope=0.
 
 
 def conv2d_wgrad(x, dy, dw, db, R, S, stride, pad, pad_mode, co, ci, so, si, accumulate=True,
-                 role="bwd"):
+                 role="bwd", dy_planes=None):
     """dw (+)= weight gradient written with strides (so, si) — see vst_conv2d_wgrad; db (if not
-    None) (+)= per-channel sum of dy (the bias gradient)."""
+    None) (+)= per-channel sum of dy (the bias gradient).  dy_planes: dy's bf16 plane image made by
+    instnorm_act_bwd(..., planes=True) (vst_conv2d_wgrad_pre; used on the x6 split-bf16 path)."""
     _dev_check(x, dy)
     N, H, W, Cx = x.shape
     _, Ho, Wo, Cyp = dy.shape
     nbytes = lib().vst_conv2d_wgrad_ws_bytes(N, H, W, Cx, Ho, Wo, Cyp, R, S, stride)
     ws = torch.empty((nbytes + 3) // 4, device=x.device)
     h = _probe_begin("wgrad", (N, H, W, Cx, Cyp, R, stride, pad, pad_mode)) if _probes else None
-    _call("vst_conv2d_wgrad", _p(x), _p(dy), _p(dw), _p(ws), nbytes, N, H, W, Cx, Ho, Wo,
+    _call("vst_conv2d_wgrad_pre", _p(x), _p(dy), _p(dy_planes), _p(dw), _p(ws), nbytes, N, H, W, Cx, Ho, Wo,
           Cyp, R, S, stride, pad, PAD[pad_mode], co, ci, so, si, 1 if accumulate else 0, _math(role),
           _stream())
     _probe_end(h)
@@ -363,6 +364,29 @@ def conv2d_dgrad_s1(dy, ikf, H, W, cx, R, pad, pad_mode="zero", addend=None, rol
     return dx
 
 
+def conv2d_dgrad_s1_in(dy, ikf, H, W, cx, R, pad, y_in, stats, act="relu", slope=0.0, addend=None, db=None,
+                       accumulate_db=True, planes=False, role="bwd"):
+    """conv2d_dgrad_s1 (reflect) whose fold also runs the InstanceNorm(+act) backward of the layer
+    below (vst_reflect_fold_instnorm_bwd): returns (g, dy_in[, dy_in_planes]) where g = the folded
+    data gradient (+ addend) and dy_in = instnorm_act_bwd(g, y_in, stats, act)."""
+    _dev_check(dy, ikf, addend, y_in, stats)
+    dxp = conv2d_fwd(dy, ikf, None, cx, R, R, 1, R - 1, "zero", role=role)
+    N = dy.shape[0]
+    C = y_in.shape[-1]
+    if cx != C:
+        raise ValueError("conv2d_dgrad_s1_in: data-gradient channels %d != IN channels %d" % (cx, C))
+    g = torch.empty((N, H, W, C), device=dy.device)
+    dyi = torch.empty_like(g)
+    ws = _in_ws(N, H * W, C, dy.device)
+    pl, ldp = None, 0
+    if planes:
+        ldp = lib().vst_cp_ld(N * H * W)
+        pl = torch.empty((3, C, ldp), device=dy.device, dtype=torch.bfloat16)
+    _call("vst_reflect_fold_instnorm_bwd", _p(dxp), _p(addend), _p(g), _p(y_in), _p(stats), _p(dyi), _p(db), _p(ws),
+          N, H, W, C, pad, ACT[act], float(slope), 1 if accumulate_db else 0, _p(pl), ldp, _stream())
+    return (g, dyi, pl) if planes else (g, dyi)
+
+
 def reflect_fold(dxp, p, addend=None):
     _dev_check(dxp, addend)
     N, Hp, Wp, C = dxp.shape
@@ -396,15 +420,21 @@ def instnorm_act_fwd(y, stats, act="relu", slope=0.0, residual=None):
     return a
 
 
-def instnorm_act_bwd(ga, y, stats, act="relu", slope=0.0, db=None, accumulate_db=True):
-    """dy = backward of act(IN(y)); db (if given) (+)= sum of dy per channel (conv-bias grad)."""
+def instnorm_act_bwd(ga, y, stats, act="relu", slope=0.0, db=None, accumulate_db=True, planes=False):
+    """dy = backward of act(IN(y)); db (if given) (+)= sum of dy per channel (conv-bias grad).
+    planes=True: returns (dy, dy_planes) — the apply pass also writes dy's three bf16 planes
+    [3][C][vst_cp_ld(N*H*W)], the x6 weight gradient's operand image (conv2d_wgrad(dy_planes=...))."""
     _dev_check(ga, y, stats)
     N, H, W, C = y.shape
     dy = torch.empty_like(y)
     ws = _in_ws(N, H * W, C, y.device)
-    _call("vst_instnorm_act_bwd", _p(ga), _p(y), _p(stats), _p(dy), _p(db), _p(ws), N, H * W, C,
-          ACT[act], float(slope), 1 if accumulate_db else 0, _stream())
-    return dy
+    pl, ldp = None, 0
+    if planes:
+        ldp = lib().vst_cp_ld(N * H * W)
+        pl = torch.empty((3, C, ldp), device=y.device, dtype=torch.bfloat16)
+    _call("vst_instnorm_act_bwd_planes", _p(ga), _p(y), _p(stats), _p(dy), _p(db), _p(ws), N, H * W, C,
+          ACT[act], float(slope), 1 if accumulate_db else 0, _p(pl), ldp, _stream())
+    return (dy, pl) if planes else dy
 
 
 def act_bwd(gy, y, act, slope=0.0):

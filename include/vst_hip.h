@@ -155,6 +155,16 @@ int vst_conv2d_wgrad(const float* x, const float* dy, float* dw, float* ws, size
                      int H, int W, int Cx, int Ho, int Wo, int Cyp, int R, int S, int stride,
                      int pad, int pad_mode, int Co, int Ci, long so, long si, int accumulate,
                      int math, void* stream);
+/* vst_conv2d_wgrad with the dy operand image made by the producer of dy: dy_planes (or NULL) =
+ * the three bf16 planes [3][Cyp][vst_cp_ld(N*Ho*Wo)] of dy that vst_instnorm_act_bwd_planes writes.
+ * Used only when vst_conv_plan_wgrad reports VST_WPLAN_BF (the x6 split-bf16 kernel); on other
+ * paths dy_planes is ignored and dy is read as in vst_conv2d_wgrad. */
+int vst_conv2d_wgrad_pre(const float* x, const float* dy, const void* dy_planes, float* dw, float* ws,
+                         size_t ws_bytes, int N, int H, int W, int Cx, int Ho, int Wo, int Cyp, int R, int S,
+                         int stride, int pad, int pad_mode, int Co, int Ci, long so, long si, int accumulate,
+                         int math, void* stream);
+/* Plane stride (elements) of the channel-major operand images over P pixels. */
+long vst_cp_ld(long P);
 /* Debug/benchmark only: force the GEMM tile of fprop / tconv / wgrad (-1 = automatic) for calls
  * made from the CALLING host thread (thread-local; other threads keep automatic selection).
  * fprop/tconv: 0 = 128x128 (8 waves), 1 = 64x128, 2 = 128x64, 3 = 64x64, 4 = 128x128 64-deep K,
@@ -207,6 +217,21 @@ int vst_instnorm_act_fwd(const float* x, const float* stats, const float* residu
 int vst_instnorm_act_bwd(const float* gy, const float* x, const float* stats, float* dx, float* db,
                          float* ws, int N, int HW, int C, int act, float slope, int accumulate_db,
                          void* stream);
+/* The reflect fold of a stride-1 data gradient over the padded frame (vst_reflect_fold: gout = addend
+ * (or 0) + the mirrored sums of dxp [N][H+2p][W+2p][C]) fused with the InstanceNorm(+act) backward
+ * below it: gout is written and, in the same pass, reduced into the IN backward partials, then
+ * dx = IN(+act) input gradient of gout (db, planes as vst_instnorm_act_bwd_planes).  ws:
+ * vst_instnorm_ws_bytes(N, H*W, C). */
+int vst_reflect_fold_instnorm_bwd(const float* dxp, const float* addend, float* gout, const float* x,
+                                  const float* stats, float* dx, float* db, float* ws, int N, int H, int W,
+                                  int C, int pad, int act, float slope, int accumulate_db, void* planes, long ldp,
+                                  void* stream);
+/* vst_instnorm_act_bwd whose apply pass also writes dx as the three bf16 planes [3][C][ldp] (hi, mid,
+ * lo; ldp >= N*HW, vst_cp_ld(N*HW)) the x6 weight gradient of the conv below consumes
+ * (vst_conv2d_wgrad_pre).  planes == NULL: identical to vst_instnorm_act_bwd. */
+int vst_instnorm_act_bwd_planes(const float* gy, const float* x, const float* stats, float* dx, float* db,
+                                float* ws, int N, int HW, int C, int act, float slope, int accumulate_db,
+                                void* planes, long ldp, void* stream);
 /* Elementwise activation backward in place-safe form: dx = gy * act'(y) given the OUTPUT y. */
 int vst_act_bwd(const float* gy, const float* y, float* dx, long n, int act, float slope, void* stream);
 

@@ -463,3 +463,76 @@ def test_convT3s2_phase_packs_batched_equal_single(ops):
         batched = ops.convT3s2_phase_packs(wt)
     for s_, b_ in zip(single, batched):
         assert torch.equal(s_, b_) and torch.equal(s_.vst_split, b_.vst_split)
+
+
+# ----------------------------------------------------- fused IN-backward producers (round 2)
+def _split3(x):
+    hi = x.to(torch.bfloat16)
+    r = x - hi.float()
+    mid = r.to(torch.bfloat16)
+    lo = (r - mid.float()).to(torch.bfloat16)
+    return hi, mid, lo
+
+
+@pytest.mark.parametrize("N,H,C,act", [(2, 16, 64, "relu"), (3, 12, 128, "none"), (2, 10, 64, "lrelu")])
+def test_instnorm_bwd_planes_exact(ops, N, H, C, act):
+    """instnorm_act_bwd(planes=True): dy bit-identical to the plain apply pass, and the planes are
+    exactly the RNE three-way bf16 split of dy, channel-major [3][C][vst_cp_ld(P)]."""
+    y = _g(1, (N, H, H, C)).to(DEV)
+    ga = _g(2, (N, H, H, C)).to(DEV)
+    st = ops.instnorm_stats(y)
+    dy0 = ops.instnorm_act_bwd(ga, y, st, act, 0.2)
+    dy1, pl = ops.instnorm_act_bwd(ga, y, st, act, 0.2, planes=True)
+    assert torch.equal(dy0, dy1)
+    P = N * H * H
+    assert pl.shape[2] == ops.lib().vst_cp_ld(P)
+    ref = _split3(dy0.reshape(P, C).t())
+    for k in range(3):
+        assert torch.equal(pl[k, :, :P], ref[k]), k
+
+
+@pytest.mark.parametrize("st", [1, 2])
+def test_wgrad_with_premade_planes_exact(ops, st):
+    """vst_conv2d_wgrad_pre with the IN backward's planes == vst_conv2d_wgrad (x6, bit-identical)."""
+    prev = ops.set_conv_math("bf16x6")
+    try:
+        N, H, Ci, Co = 2, 32, 64, 128
+        x = _g(3, (N, H, H, Ci)).to(DEV)
+        Ho = H // st
+        y = _g(4, (N, Ho, Ho, Co)).to(DEV)
+        ga = _g(5, (N, Ho, Ho, Co)).to(DEV)
+        s = ops.instnorm_stats(y)
+        dy, pl = ops.instnorm_act_bwd(ga, y, s, "relu", planes=True)
+        path, _, _ = ops.conv_plan_wgrad(N, H, H, Ci, Ho, Ho, Co, 3, 3, st, "bf16x6")
+        assert path == 2
+        mode, pad = ("reflect", 1) if st == 1 else ("zero", 1)
+        dw0 = torch.zeros(Co, Ci, 3, 3, device=DEV)
+        dw1 = torch.zeros(Co, Ci, 3, 3, device=DEV)
+        ops.conv2d_wgrad(x, dy, dw0, None, 3, 3, st, pad, mode, Co, Ci, Ci * 9, 9)
+        ops.conv2d_wgrad(x, dy, dw1, None, 3, 3, st, pad, mode, Co, Ci, Ci * 9, 9, dy_planes=pl)
+        assert torch.equal(dw0, dw1)
+    finally:
+        ops.set_conv_math(prev)
+
+
+@pytest.mark.parametrize("act,addend", [("relu", False), ("none", True)])
+def test_dgrad_fold_instnorm_bwd_exact(ops, act, addend):
+    """conv2d_dgrad_s1_in (fold + IN-backward partials in one pass) == conv2d_dgrad_s1 (reflect) then
+    instnorm_act_bwd: folded gradient, IN input gradient, bias gradient and planes bit-identical."""
+    N, H, C = 2, 16, 64
+    dy = _g(6, (N, H, H, C)).to(DEV)
+    w = _g(7, (C, C, 3, 3), 0.05).to(DEV)
+    ikf = ops.weight_pack(w, ops.PACK_IKF)
+    y_in = _g(8, (N, H, H, C)).to(DEV)
+    s_in = ops.instnorm_stats(y_in)
+    add = _g(9, (N, H, H, C)).to(DEV) if addend else None
+    g0 = ops.conv2d_dgrad_s1(dy, ikf, H, H, C, 3, 1, "reflect", addend=add)
+    db0 = torch.zeros(C, device=DEV)
+    d0, p0 = ops.instnorm_act_bwd(g0, y_in, s_in, act, db=db0, planes=True)
+    db1 = torch.zeros(C, device=DEV)
+    g1, d1, p1 = ops.conv2d_dgrad_s1_in(dy, ikf, H, H, C, 3, 1, y_in, s_in, act, addend=add, db=db1, planes=True)
+    assert torch.equal(g0, g1)
+    assert torch.equal(d0, d1)
+    assert torch.equal(db0, db1)
+    P = N * H * H  # the planes' row padding past P is never written (nor read)
+    assert torch.equal(p0[:, :, :P], p1[:, :, :P])

@@ -1,13 +1,11 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
-O=gpurun_out/ab5; mkdir -p $O
-V=gan-based-video-style-transfer_amd/_build/variants
-for v in st1 st1s0 st1r1 s0 st1r1s0 st1 st1s0 st1r1 s0 st1r1s0; do
-  if [ $v = default ]; then L=""; else L=$V/lib_$v.so; fi
-  VST_LIB_VARIANT=$L timeout -k 10 120 python tools/kbench_time.py >> $O/kb.log 2>&1 || { echo kb fail; tail $O/kb.log; exit 1; }
+O=gpurun_out/ab6; mkdir -p $O
+timeout -k 10 400 python -u -m pytest tests/test_gpu_ops.py tests/test_gpu_models.py tests/test_gpu_c3.py tests/test_gpu_train.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 || { echo pytest fail; grep -E "FAIL|Error|assert" $O/pytest.log | head -30; tail -5 $O/pytest.log; exit 1; }
+tail -2 $O/pytest.log
+for v in "1 1" "0 0" "1 1" "0 0" "1 0" "0 1"; do
+  set -- $v
+  VST_IN_PLANES=$1 VST_FOLD_IN=$2 timeout -k 10 200 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-extras > $O/bench_$1$2.json 2>/dev/null || { echo bench fail; exit 1; }
+  python -c "import json,sys; d=json.loads(open('$O/bench_$1$2.json').read().strip().splitlines()[-1]); print('planes=$1 fold=$2', d['value'], d['ms_per_step'])"
 done
-grep -v amdgpu.ids $O/kb.log | python3 -c "
-import sys, json
-for l in sys.stdin:
-    d = json.loads(l); print(d['lib'][-12:], ' '.join('%s=%s' % (k[:-3], v) for k, v in d.items() if k.endswith('_us')))"

@@ -59,7 +59,8 @@ SIGNATURES = {
     "vst_instnorm_act_fwd": (I, [P, P, P, P, I, I, I, I, F, P]),
     "vst_instnorm_act_bwd": (I, [P, P, P, P, P, P, I, I, I, I, F, I, P]),
     "vst_instnorm_act_bwd_planes": (I, [P, P, P, P, P, P, I, I, I, I, F, I, P, L, P]),
-    "vst_conv2d_wgrad_pre": (I, [P, P, P, P, P, SZ, I, I, I, I, I, I, I, I, I, I, I, I, I, I, L, L, I, I, P]),
+    "vst_conv2d_wgrad_pre": (I, [P, P, P, P, P, P, SZ, I, I, I, I, I, I, I, I, I, I, I, I, I, I, L, L, I, I, P]),
+    "vst_instnorm_act_fwd_cp": (I, [P, P, P, P, P, I, I, I, I, I, F, I, I, I, P]),
     "vst_cp_ld": (L, [L]),
     "vst_reflect_fold_instnorm_bwd": (I, [P, P, P, P, P, P, P, P, I, I, I, I, I, I, F, I, P, L, P]),
     "vst_act_bwd": (I, [P, P, P, L, I, F, P]),

@@ -976,23 +976,23 @@ extern "C" size_t vst_conv2d_wgrad_ws_bytes(int N, int H, int W, int Cx, int Ho,
 
 extern "C" long vst_cp_ld(long P) { return rk_cp_ld(P); }
 
-extern "C" int vst_conv2d_wgrad_pre(const float* x, const float* dy, const void* dy_planes, float* dw, float* ws,
-                                    size_t ws_bytes, int N, int H, int W, int Cx, int Ho, int Wo, int Cyp, int R,
-                                    int S, int stride, int pad, int pad_mode, int Co, int Ci, long so, long si,
-                                    int accumulate, int math, void* stream);
+extern "C" int vst_conv2d_wgrad_pre(const float* x, const float* x_t, const float* dy, const void* dy_planes,
+                                    float* dw, float* ws, size_t ws_bytes, int N, int H, int W, int Cx, int Ho, int Wo,
+                                    int Cyp, int R, int S, int stride, int pad, int pad_mode, int Co, int Ci, long so,
+                                    long si, int accumulate, int math, void* stream);
 
 extern "C" int vst_conv2d_wgrad(const float* x, const float* dy, float* dw, float* ws,
                                 size_t ws_bytes, int N, int H, int W, int Cx, int Ho, int Wo,
                                 int Cyp, int R, int S, int stride, int pad, int pad_mode, int Co,
                                 int Ci, long so, long si, int accumulate, int math, void* stream) {
-  return vst_conv2d_wgrad_pre(x, dy, nullptr, dw, ws, ws_bytes, N, H, W, Cx, Ho, Wo, Cyp, R, S, stride, pad,
+  return vst_conv2d_wgrad_pre(x, nullptr, dy, nullptr, dw, ws, ws_bytes, N, H, W, Cx, Ho, Wo, Cyp, R, S, stride, pad,
                               pad_mode, Co, Ci, so, si, accumulate, math, stream);
 }
 
-extern "C" int vst_conv2d_wgrad_pre(const float* x, const float* dy, const void* dy_planes, float* dw, float* ws,
-                                    size_t ws_bytes, int N, int H, int W, int Cx, int Ho, int Wo, int Cyp, int R,
-                                    int S, int stride, int pad, int pad_mode, int Co, int Ci, long so, long si,
-                                    int accumulate, int math, void* stream) {
+extern "C" int vst_conv2d_wgrad_pre(const float* x, const float* x_t, const float* dy, const void* dy_planes,
+                                    float* dw, float* ws, size_t ws_bytes, int N, int H, int W, int Cx, int Ho, int Wo,
+                                    int Cyp, int R, int S, int stride, int pad, int pad_mode, int Co, int Ci, long so,
+                                    long si, int accumulate, int math, void* stream) {
   VST_REQUIRE(x && dy && dw && ws, "conv2d_wgrad: null pointer");
   VST_REQUIRE(math >= VST_MATH_F32 && math <= VST_MATH_BF16X6, "conv2d_wgrad: bad math %d", math);
   VST_REQUIRE(Cx % 4 == 0 && Cyp % 4 == 0, "conv2d_wgrad: channel strides must be multiples of 4");
@@ -1017,9 +1017,9 @@ extern "C" int vst_conv2d_wgrad_pre(const float* x, const float* dy, const void*
     float* xt = ws + (size_t)p.nsplit * p.Mw * Cyp;
     float* dyt = xt + p.xt_floats;
     if (p.bfk) {
-      rk_nhwc_to_cp_pad(x, xt, N, H, W, Cx, pad, refl, stride == 2, 0, s);
+      if (!x_t) rk_nhwc_to_cp_pad(x, xt, N, H, W, Cx, pad, refl, stride == 2, 0, s);  // else: vst_instnorm_act_fwd_cp
       if (!dy_planes) bf_nhwc_to_planes(dy, dyt, P, Cyp, 3, s);  // else: made by vst_instnorm_act_bwd_planes
-      bf_wgrad_launch(xt, dy_planes ? dy_planes : dyt, ws, N, H, W, Cx, Ho, Wo, Cyp, S, pad, stride, p.Mw, p.chunk,
+      bf_wgrad_launch(x_t ? x_t : xt, dy_planes ? dy_planes : dyt, ws, N, H, W, Cx, Ho, Wo, Cyp, S, pad, stride, p.Mw, p.chunk,
                       p.nsplit, (int)p.tile, math, s);
     } else {
       const int pack = math == VST_MATH_BF16X3;  // the x3 kernel stages pre-split (hi, lo) words

@@ -331,6 +331,76 @@ __global__ void in_apply_k(const float4* __restrict__ x, const float* __restrict
   y[i] = v;
 }
 
+// in_apply_k fused with the weight gradient's A-operand image of the conv that consumes the result:
+// a = act(IN(y)) (+ residual) written NHWC (the next conv's input) AND as the padded channel-major
+// copy [C][N][H+2p][W+2p] (reflect or zero border; phase: stride-2 column-phase rows) that
+// nhwc_to_cp_pad_k would make from a in the backward pass — the backward's read of a and its
+// launch are gone.  Walks padded pixels in 64 x 64 LDS tiles (as nhwc_to_cp_pad_k); the interior
+// positions also store a.  grid (ceil(N (H+2p)(W+2p) / 64), ceil(C / 64)), 256 threads.
+__global__ __launch_bounds__(256) void in_apply_cp_pad_k(const float* __restrict__ x, const float* __restrict__ stats,
+                                                          const float* __restrict__ res, float* __restrict__ a,
+                                                          float* __restrict__ xt, int N, int H, int W, int C,
+                                                          int pad, int reflect, int phase, long ld, int act,
+                                                          float slope) {
+  __shared__ float tile[64][65];
+  const int Hp = H + 2 * pad, Wp = W + 2 * pad;
+  const long P = (long)N * Hp * Wp;
+  const long p0 = (long)blockIdx.x * 64;
+  const int c0 = blockIdx.y * 64;
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int idx = t + 256 * it, pr = idx >> 4, c4 = (idx & 15) * 4;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    const long q = p0 + pr;
+    if (q < P && c0 + c4 < C) {
+      const int n = (int)(q / ((long)Hp * Wp));
+      const int rem = (int)(q - (long)n * Hp * Wp);
+      int h = rem / Wp - pad, w = rem % Wp;
+      if (phase) {
+        const int wh = Wp >> 1;
+        w = w < wh ? 2 * w : 2 * (w - wh) + 1;
+      }
+      w -= pad;
+      const bool inner = (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+      bool ok = inner;
+      if (reflect) {
+        h = reflect_idx(h, H);
+        w = reflect_idx(w, W);
+        ok = true;
+      }
+      if (ok) {
+        const long e = (((long)n * H + h) * W + w) * C + c0 + c4;
+        const float4 s0 = reinterpret_cast<const float4*>(stats)[((long)n * C + c0 + c4) / 2];
+        const float4 s1 = reinterpret_cast<const float4*>(stats)[((long)n * C + c0 + c4) / 2 + 1];
+        v = *reinterpret_cast<const float4*>(x + e);
+        v.x = apply_act((v.x - s0.x) * s0.y, act, slope);
+        v.y = apply_act((v.y - s0.z) * s0.w, act, slope);
+        v.z = apply_act((v.z - s1.x) * s1.y, act, slope);
+        v.w = apply_act((v.w - s1.z) * s1.w, act, slope);
+        if (res) add_f4(v, *reinterpret_cast<const float4*>(res + e));
+        if (inner) *reinterpret_cast<float4*>(a + e) = v;
+      }
+    }
+    tile[pr][c4] = v.x;
+    tile[pr][c4 + 1] = v.y;
+    tile[pr][c4 + 2] = v.z;
+    tile[pr][c4 + 3] = v.w;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int idx = t + 256 * it, cr = idx >> 4, p4 = (idx & 15) * 4;
+    if (c0 + cr >= C || p0 + p4 >= P) continue;
+    float* dst = xt + (long)(c0 + cr) * ld + p0 + p4;
+    if (p0 + p4 + 3 < P && (ld & 3) == 0) {
+      *reinterpret_cast<float4*>(dst) = make_float4(tile[p4][cr], tile[p4 + 1][cr], tile[p4 + 2][cr], tile[p4 + 3][cr]);
+    } else {
+      for (int e = 0; e < 4 && p0 + p4 + e < P; ++e) dst[e] = tile[p4 + e][cr];
+    }
+  }
+}
+
 __device__ __forceinline__ float in_bwd1(float gy, float x, float mean, float rstd, float2 k, int act,
                                          float slope) {
   const float xh = (x - mean) * rstd;
@@ -750,6 +820,20 @@ extern "C" int vst_instnorm_act_fwd(const float* x, const float* stats, const fl
 extern "C" int vst_instnorm_act_bwd_planes(const float* gy, const float* x, const float* stats, float* dx,
                                            float* db, float* ws, int N, int HW, int C, int act, float slope,
                                            int accumulate_db, void* planes, long ldp, void* stream);
+
+extern "C" int vst_instnorm_act_fwd_cp(const float* x, const float* stats, const float* residual, float* y,
+                                       float* xt, int N, int H, int W, int C, int act, float slope, int pad,
+                                       int pad_mode, int stride, void* stream) {
+  VST_REQUIRE(x && stats && y && xt && C % 4 == 0 && pad >= 0 && (stride == 1 || stride == 2),
+              "instnorm_act_fwd_cp: bad args");
+  VST_REQUIRE(pad_mode == VST_PAD_ZERO || (pad < H && pad < W), "instnorm_act_fwd_cp: reflect pad >= size");
+  VST_REQUIRE(stride == 1 || (W + 2 * pad) % 2 == 0, "instnorm_act_fwd_cp: stride 2 needs W + 2 pad even");
+  const long P = (long)N * (H + 2 * pad) * (W + 2 * pad);
+  hipLaunchKernelGGL(in_apply_cp_pad_k, dim3(ceil_div(P, 64), ceil_div(C, 64)), dim3(256), 0, (hipStream_t)stream,
+                     x, stats, residual, y, xt, N, H, W, C, pad, pad_mode == VST_PAD_REFLECT, stride == 2,
+                     rk_cp_ld(P), act, slope);
+  return check_launch("instnorm_act_fwd_cp");
+}
 
 extern "C" int vst_instnorm_act_bwd(const float* gy, const float* x, const float* stats, float* dx,
                                     float* db, float* ws, int N, int HW, int C, int act, float slope,

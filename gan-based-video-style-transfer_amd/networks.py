@@ -422,6 +422,10 @@ class ResnetGenerator(FlatNet):
 # ops.instnorm_act_bwd(planes=True)) when that weight gradient runs on the x6 split-bf16 kernel;
 # VST_IN_PLANES=0 keeps the separate plane copy inside vst_conv2d_wgrad.
 IN_PLANES = os.environ.get("VST_IN_PLANES", "1") != "0"
+# The forward IN apply writes the padded channel-major image of its output that the x6 weight
+# gradient of the consuming conv reads (ops.instnorm_act_fwd(cp=...)); VST_IN_XT=0 makes that copy
+# inside vst_conv2d_wgrad instead.
+IN_XT = os.environ.get("VST_IN_XT", "1") != "0"
 # The reflect fold of a stride-1 data gradient and the IN backward partials of the layer below it as
 # one pass (ops.conv2d_dgrad_s1_in, VST_FOLD_IN=1).  Off by default: the fused pass is bit-identical
 # but its per-thread fp64 reduction chains run on the fold's (nsplit x N)-block geometry, slower
@@ -454,34 +458,57 @@ class _GeneratorFn(torch.autograd.Function):
         P = net.packs()
         c0, d, blocks, u, f = net._layers()
         ngf = net.ngf
-        sv = {"x": x}
+        sv = {"x": x, "xt": {}}  # xt: id(activation) -> its wgrad A-operand image (or None)
         N, H, W, _ = x.shape
         role = "fwd" if any(ctx.needs_input_grad[:2]) else "infer"
 
-        def conv_in_relu(inp, key, cout, R, st, pad, mode):
+        train_w = role == "fwd" and anchor.requires_grad
+
+        def cp_for(y, cout, st, mode):
+            """(pad, mode, stride) of the 3x3 conv consuming act(IN(y)) (cout outputs) when its x6
+            weight gradient will read the padded channel-major image the IN apply can write."""
+            if not (train_w and IN_XT):
+                return None
+            N_, H_, W_, C_ = y.shape
+            Ho_, Wo_ = (H_ + 2 - 3) // st + 1, (W_ + 2 - 3) // st + 1
+            return (1, mode, st) if _wgrad_on_bf(N_, H_, W_, C_, Ho_, Wo_, cpad(cout), 3, st,
+                                                 ops.get_conv_math()) else None
+
+        def in_act(y, s, act, cp, residual=None):
+            if cp is None:
+                return ops.instnorm_act_fwd(y, s, act, residual=residual), None
+            return ops.instnorm_act_fwd(y, s, act, residual=residual, cp=cp)
+
+        def conv_in_relu(inp, key, cout, R, st, pad, mode, nxt=None):
+            """conv + IN + ReLU; nxt = (cout, stride, pad mode) of the 3x3 conv consuming the output"""
             kc, _, b = P[key]
             y, s = ops.conv2d_fwd_in(inp, kc, b, cpad(cout), R, R, st, pad, mode, role=role)
-            return y, s, ops.instnorm_act_fwd(y, s, "relu")
+            a, at = in_act(y, s, "relu", cp_for(y, *nxt) if nxt else None)
+            sv["xt"][id(a)] = at
+            return y, s, a
 
         if "c08" in P and x.shape[-1] == 4:
             x8 = _pad_channels(x, 8)
             _, _, b = P["c0"]
             y, s = ops.conv2d_fwd_in(x8, P["c08"], b, cpad(ngf), 7, 7, 1, 3, "reflect", role=role)
-            a = ops.instnorm_act_fwd(y, s, "relu")
+            a, at = in_act(y, s, "relu", cp_for(y, 2 * ngf, 2, "zero"))
+            sv["xt"][id(a)] = at
             sv["x8"] = x8
         else:
-            y, s, a = conv_in_relu(x, "c0", ngf, 7, 1, 3, "reflect")
+            y, s, a = conv_in_relu(x, "c0", ngf, 7, 1, 3, "reflect", nxt=(2 * ngf, 2, "zero"))
         sv["c0"] = (y, s, a)
-        y, s, a = conv_in_relu(a, "d0", 2 * ngf, 3, 2, 1, "zero")
+        y, s, a = conv_in_relu(a, "d0", 2 * ngf, 3, 2, 1, "zero", nxt=(4 * ngf, 2, "zero"))
         sv["d0"] = (y, s, a)
-        y, s, a = conv_in_relu(a, "d1", 4 * ngf, 3, 2, 1, "zero")
+        nb = len(blocks)
+        y, s, a = conv_in_relu(a, "d1", 4 * ngf, 3, 2, 1, "zero", nxt=(4 * ngf, 1, "reflect") if nb else None)
         sv["d1"] = (y, s, a)
         h = a
-        for i in range(len(blocks)):
-            t, s1, uu = conv_in_relu(h, f"b{i}a", 4 * ngf, 3, 1, 1, "reflect")
+        for i in range(nb):
+            t, s1, uu = conv_in_relu(h, f"b{i}a", 4 * ngf, 3, 1, 1, "reflect", nxt=(4 * ngf, 1, "reflect"))
             kc, _, b = P[f"b{i}b"]
             v, s2 = ops.conv2d_fwd_in(uu, kc, b, 4 * ngf, 3, 3, 1, 1, "reflect", role=role)
-            hn = ops.instnorm_act_fwd(v, s2, "none", residual=h)
+            hn, hnt = in_act(v, s2, "none", cp_for(v, 4 * ngf, 1, "reflect") if i + 1 < nb else None, residual=h)
+            sv["xt"][id(hn)] = hnt
             sv[f"b{i}"] = (h, t, s1, uu, v, s2)
             h = hn
         a = h
@@ -521,13 +548,16 @@ class _GeneratorFn(torch.autograd.Function):
             if final:
                 net._grad_done(mod)
 
+        xts = sv["xt"]
+
         def wgrad(mod, inp, dy, R, st, pad, mode, db=False, dy_planes=None):
             if not train_w:
                 return
             w = mod.weight
             co, ci = w.shape[0], w.shape[1]
             ops.conv2d_wgrad(inp, dy, w.grad, mod.bias.grad if (db and mod.bias is not None) else None,
-                             R, R, st, pad, mode, co, ci, ci * R * R, R * R, accumulate=True, dy_planes=dy_planes)
+                             R, R, st, pad, mode, co, ci, ci * R * R, R * R, accumulate=True, dy_planes=dy_planes,
+                             x_t=xts.get(id(inp)))
 
         def in_bwd(g, y, s, act, mod, x_in=None, R=3, st=1):
             # IN(+act) backward; the bias gradient of the conv feeding the IN comes out of the

@@ -243,17 +243,18 @@ def conv2d_tfwd(x, wp, bias, Ho, Wo, cx, R, S, stride, pad, act="none", slope=0.
 
 
 def conv2d_wgrad(x, dy, dw, db, R, S, stride, pad, pad_mode, co, ci, so, si, accumulate=True,
-                 role="bwd", dy_planes=None):
+                 role="bwd", dy_planes=None, x_t=None):
     """dw (+)= weight gradient written with strides (so, si) — see vst_conv2d_wgrad; db (if not
     None) (+)= per-channel sum of dy (the bias gradient).  dy_planes: dy's bf16 plane image made by
-    instnorm_act_bwd(..., planes=True) (vst_conv2d_wgrad_pre; used on the x6 split-bf16 path)."""
+    instnorm_act_bwd(..., planes=True), x_t: x's padded channel-major image made by
+    instnorm_act_fwd(..., cp=...) (vst_conv2d_wgrad_pre; both used on the x6 split-bf16 path)."""
     _dev_check(x, dy)
     N, H, W, Cx = x.shape
     _, Ho, Wo, Cyp = dy.shape
     nbytes = lib().vst_conv2d_wgrad_ws_bytes(N, H, W, Cx, Ho, Wo, Cyp, R, S, stride)
     ws = torch.empty((nbytes + 3) // 4, device=x.device)
     h = _probe_begin("wgrad", (N, H, W, Cx, Cyp, R, stride, pad, pad_mode)) if _probes else None
-    _call("vst_conv2d_wgrad_pre", _p(x), _p(dy), _p(dy_planes), _p(dw), _p(ws), nbytes, N, H, W, Cx, Ho, Wo,
+    _call("vst_conv2d_wgrad_pre", _p(x), _p(x_t), _p(dy), _p(dy_planes), _p(dw), _p(ws), nbytes, N, H, W, Cx, Ho, Wo,
           Cyp, R, S, stride, pad, PAD[pad_mode], co, ci, so, si, 1 if accumulate else 0, _math(role),
           _stream())
     _probe_end(h)
@@ -411,10 +412,19 @@ def instnorm_stats(y):
     return stats
 
 
-def instnorm_act_fwd(y, stats, act="relu", slope=0.0, residual=None):
+def instnorm_act_fwd(y, stats, act="relu", slope=0.0, residual=None, cp=None):
+    """a = act(IN(y)) (+ residual).  cp = (pad, pad_mode, stride) of the conv that consumes a:
+    returns (a, a_t) where a_t is a's padded channel-major image for that conv's x6 weight gradient
+    (vst_instnorm_act_fwd_cp; conv2d_wgrad(x_t=a_t))."""
     _dev_check(y, stats, residual)
     N, H, W, C = y.shape
     a = torch.empty_like(y)
+    if cp is not None:
+        pad, mode, st = cp
+        at = torch.empty((C, lib().vst_cp_ld(N * (H + 2 * pad) * (W + 2 * pad))), device=y.device)
+        _call("vst_instnorm_act_fwd_cp", _p(y), _p(stats), _p(residual), _p(a), _p(at), N, H, W, C, ACT[act],
+              float(slope), pad, PAD[mode], st, _stream())
+        return a, at
     _call("vst_instnorm_act_fwd", _p(y), _p(stats), _p(residual), _p(a), N, H * W, C, ACT[act],
           float(slope), _stream())
     return a

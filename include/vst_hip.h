@@ -155,14 +155,21 @@ int vst_conv2d_wgrad(const float* x, const float* dy, float* dw, float* ws, size
                      int H, int W, int Cx, int Ho, int Wo, int Cyp, int R, int S, int stride,
                      int pad, int pad_mode, int Co, int Ci, long so, long si, int accumulate,
                      int math, void* stream);
-/* vst_conv2d_wgrad with the dy operand image made by the producer of dy: dy_planes (or NULL) =
- * the three bf16 planes [3][Cyp][vst_cp_ld(N*Ho*Wo)] of dy that vst_instnorm_act_bwd_planes writes.
- * Used only when vst_conv_plan_wgrad reports VST_WPLAN_BF (the x6 split-bf16 kernel); on other
- * paths dy_planes is ignored and dy is read as in vst_conv2d_wgrad. */
-int vst_conv2d_wgrad_pre(const float* x, const float* dy, const void* dy_planes, float* dw, float* ws,
-                         size_t ws_bytes, int N, int H, int W, int Cx, int Ho, int Wo, int Cyp, int R, int S,
-                         int stride, int pad, int pad_mode, int Co, int Ci, long so, long si, int accumulate,
+/* vst_conv2d_wgrad with operand images made by the producers of x and dy: x_t (or NULL) = the
+ * padded channel-major image of x that vst_instnorm_act_fwd_cp writes (same pad / mode / stride);
+ * dy_planes (or NULL) = the three bf16 planes [3][Cyp][vst_cp_ld(N*Ho*Wo)] of dy that
+ * vst_instnorm_act_bwd_planes writes.  Used only when vst_conv_plan_wgrad reports VST_WPLAN_BF (the
+ * x6 split-bf16 kernel); on other paths both are ignored and x / dy are read as in vst_conv2d_wgrad. */
+int vst_conv2d_wgrad_pre(const float* x, const float* x_t, const float* dy, const void* dy_planes, float* dw,
+                         float* ws, size_t ws_bytes, int N, int H, int W, int Cx, int Ho, int Wo, int Cyp, int R,
+                         int S, int stride, int pad, int pad_mode, int Co, int Ci, long so, long si, int accumulate,
                          int math, void* stream);
+/* vst_instnorm_act_fwd that also writes x_t = the padded channel-major image [C][vst_cp_ld(N (H+2 pad)
+ * (W+2 pad))] of its output (reflect / zero border by pad_mode; stride 2: column-phase rows) — the
+ * A operand vst_conv2d_wgrad_pre takes for the conv that consumes y (its pad, pad_mode, stride). */
+int vst_instnorm_act_fwd_cp(const float* x, const float* stats, const float* residual, float* y, float* x_t,
+                            int N, int H, int W, int C, int act, float slope, int pad, int pad_mode, int stride,
+                            void* stream);
 /* Plane stride (elements) of the channel-major operand images over P pixels. */
 long vst_cp_ld(long P);
 /* Debug/benchmark only: force the GEMM tile of fprop / tconv / wgrad (-1 = automatic) for calls

@@ -536,3 +536,29 @@ def test_dgrad_fold_instnorm_bwd_exact(ops, act, addend):
     assert torch.equal(db0, db1)
     P = N * H * H  # the planes' row padding past P is never written (nor read)
     assert torch.equal(p0[:, :, :P], p1[:, :, :P])
+
+
+@pytest.mark.parametrize("st,mode,res", [(1, "reflect", False), (1, "reflect", True), (2, "zero", False)])
+def test_instnorm_fwd_cp_and_wgrad_exact(ops, st, mode, res):
+    """instnorm_act_fwd(cp=...): a bit-identical to the plain apply, and the x6 weight gradient from
+    its padded channel-major image (x_t) bit-identical to the one that makes the copy itself."""
+    prev = ops.set_conv_math("bf16x6")
+    try:
+        N, H, C, Co = 2, 32, 64, 128
+        y = _g(11, (N, H, H, C)).to(DEV)
+        s = ops.instnorm_stats(y)
+        r = _g(12, (N, H, H, C)).to(DEV) if res else None
+        act = "none" if res else "relu"
+        a0 = ops.instnorm_act_fwd(y, s, act, residual=r)
+        a1, at = ops.instnorm_act_fwd(y, s, act, residual=r, cp=(1, mode, st))
+        assert torch.equal(a0, a1)
+        Ho = H // st
+        assert ops.conv_plan_wgrad(N, H, H, C, Ho, Ho, Co, 3, 3, st, "bf16x6")[0] == 2
+        dy = _g(13, (N, Ho, Ho, Co)).to(DEV)
+        dw0 = torch.zeros(Co, C, 3, 3, device=DEV)
+        dw1 = torch.zeros(Co, C, 3, 3, device=DEV)
+        ops.conv2d_wgrad(a0, dy, dw0, None, 3, 3, st, 1, mode, Co, C, C * 9, 9)
+        ops.conv2d_wgrad(a0, dy, dw1, None, 3, 3, st, 1, mode, Co, C, C * 9, 9, x_t=at)
+        assert torch.equal(dw0, dw1)
+    finally:
+        ops.set_conv_math(prev)

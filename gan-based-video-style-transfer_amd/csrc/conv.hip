@@ -849,7 +849,7 @@ extern "C" int vst_conv_plan_fwd(int N, int H, int W, int Cx, int Cop, int R, in
 static int conv_fwd_impl(const float* x, const float* wp, const void* wsplit, const float* bias, float* y,
                          int N, int H, int W, int Cx, int Cop, int R, int S, int stride, int padh, int padw,
                          int pad_mode, int act, float slope, int math, hipStream_t s, double* part = nullptr,
-                         int* nsplit = nullptr) {
+                         int* nsplit = nullptr, float* tws = nullptr, size_t tws_bytes = 0) {
   if (nsplit) *nsplit = 0;
   VST_REQUIRE(x && wp && y, "conv2d_fwd: null pointer");
   VST_REQUIRE(math >= VST_MATH_F32 && math <= VST_MATH_BF16X6, "conv2d_fwd: bad math %d", math);
@@ -870,7 +870,7 @@ static int conv_fwd_impl(const float* x, const float* wp, const void* wsplit, co
     const bool stats = part && nsplit && (Ho * Wo) % 32 == 0;
     const int rc = bf_fprop_launch(x, wsplit, (long)Cop * R * S * Cx, bias, y, N, H, W, Cx, Ho, Wo, Cop, R, S,
                                    stride, padh, padw, refl, act, slope, math, g_tile_override[0], s,
-                                   stats ? part : nullptr);
+                                   stats ? part : nullptr, tws, tws_bytes / sizeof(float));
     if (stats && rc == 0) *nsplit = Ho * Wo / 32;
     return rc;
   }
@@ -894,6 +894,36 @@ extern "C" int vst_conv2d_fwd_in(const float* x, const float* wp, const void* ws
   VST_REQUIRE(part && nsplit, "conv2d_fwd_in: null partials");
   return conv_fwd_impl(x, wp, wsplit, bias, y, N, H, W, Cx, Cop, R, S, stride, pad, pad, pad_mode, act, slope,
                        math, (hipStream_t)stream, part, nsplit);
+}
+
+extern "C" size_t vst_conv2d_fwd_ws_bytes(int N, int H, int W, int Cx, int Cop, int R, int S, int stride, int pad,
+                                          int math) {
+  if (N <= 0 || H <= 0 || W <= 0 || R <= 0 || S <= 0 || stride <= 0 || Cx % 8 || Cop == 4) return 0;
+  const int Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - S) / stride + 1;
+  if (Ho <= 0 || Wo <= 0 || g_tile_override[0] >= 0) return 0;
+  return bf_fprop_ws_floats((long)N * Ho * Wo, Cop, Cx, R, S, math) * sizeof(float);
+}
+
+extern "C" int vst_conv2d_fwd_ws(const float* x, const float* wp, const void* wsplit, const float* bias, float* y,
+                                 int N, int H, int W, int Cx, int Cop, int R, int S, int stride, int pad, int pad_mode,
+                                 int act, float slope, int math, double* part, int* nsplit, float* ws,
+                                 size_t ws_bytes, void* stream) {
+  return conv_fwd_impl(x, wp, wsplit, bias, y, N, H, W, Cx, Cop, R, S, stride, pad, pad, pad_mode, act, slope,
+                       math, (hipStream_t)stream, part, nsplit, ws, ws_bytes);
+}
+
+extern "C" int vst_conv_plan_fwd_tail(int N, int H, int W, int Cx, int Cop, int R, int S, int stride, int pad,
+                                      int math, int* ksplit) {
+  VST_REQUIRE(ksplit, "conv_plan_fwd_tail: null");
+  *ksplit = 0;
+  const size_t b = vst_conv2d_fwd_ws_bytes(N, H, W, Cx, Cop, R, S, stride, pad, math);
+  if (b) {
+    const int Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - S) / stride + 1;
+    int kd, m_split, tk;
+    bf_plan((long)N * Ho * Wo, Cop, math, -1, &kd, &m_split, &tk);
+    *ksplit = bf_tail_ks((long)N * Ho * Wo, Cop, m_split, (R * S * Cx + 31) / 32);
+  }
+  return VST_OK;
 }
 
 extern "C" int vst_conv2d_fwd_hw(const float* x, const float* wp, const void* wsplit, const float* bias,

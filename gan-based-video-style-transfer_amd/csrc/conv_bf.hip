@@ -58,6 +58,9 @@
 #ifndef VST_M16_SCHED
 #define VST_M16_SCHED 0  // M16 loop: sched_group_barrier filler pattern (0: compiler order)
 #endif
+#ifndef VST_BF_SPLITK
+#define VST_BF_SPLITK 1  // split-K wave-quantisation tails (when the caller passes a workspace)
+#endif
 #ifndef VST_BF_TAIL_FORCE
 #define VST_BF_TAIL_FORCE -1
 #endif
@@ -483,16 +486,23 @@ __device__ __attribute__((aligned(256))) float g_zero_page[64];
 // order with a per-thread cursor.
 // REFL: 0 = zero padding, 1 = reflect padding (compile-time, branch-free tap map), 2 = runtime
 // `reflect` (the rarely used tap-major variants).
-template <class T, bool KSL, int REFL>
+// SPLIT (KSL only): split-K over the K-steps — block L = z * tiles + tile runs K-steps
+// [z * spk, z * spk + spk) and stores its raw partial tile to slab[z][m - m_base][Cop]
+// (fprop_splitk_reduce_k sums the splits in order and applies bias / act / IN partials).
+template <class T, bool KSL, int REFL, bool SPLIT = false>
 __global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_k(
     const float* __restrict__ x, const __bf16* __restrict__ ws, long wps, const float* __restrict__ bias,
     float* __restrict__ y, int H, int W, int C, int Ho, int Wo, int Cop, int S, int st, int padh,
-    int padw, int reflect, int act, float slope, int M, int Ktot, int m_base, double* __restrict__ part) {
+    int padw, int reflect, int act, float slope, int M, int Ktot, int m_base, double* __restrict__ part,
+    int spk = 0, float* __restrict__ slab = nullptr) {
+  static_assert(!SPLIT || KSL, "split-K needs the channel-slice-major K walk");
   __shared__ __attribute__((aligned(16))) char smem[2 * T::STAGE];
   constexpr int A_LD = T::A_LD, B_LD = T::B_LD, RPP = T::RPP, NP = T::NP;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   int mt_, nt_;
-  tile_of(blockIdx.x, (M - m_base + T::BM - 1) / T::BM, (Cop + T::BN - 1) / T::BN, mt_, nt_);
+  const int Mt_ = (M - m_base + T::BM - 1) / T::BM, Nt_ = (Cop + T::BN - 1) / T::BN;
+  const int zs = SPLIT ? blockIdx.x / (Mt_ * Nt_) : 0;
+  tile_of(SPLIT ? blockIdx.x - zs * Mt_ * Nt_ : blockIdx.x, Mt_, Nt_, mt_, nt_);
   const int m0 = m_base + mt_ * T::BM, n0 = nt_ * T::BN;
   const int kq = t % T::KC, rb = t / T::KC;
   const float* zp = g_zero_page;
@@ -541,8 +551,18 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_k(
   int tr = 0, ts = 0, ksb = 0;                 // KSL
   int kcur = kq8, kc = kq8 % C, kr = 0, ks = 0;  // tap-major
   const int Rk = KSL ? Ktot / (S * C) : 0;
+  const int nk_all = (Ktot + T::BK - 1) / T::BK;
+  int k0 = 0, nk = nk_all;
+  if (SPLIT) {  // K-steps [k0, k0 + nk): slice k0 / (R S), tap k0 % (R S)
+    k0 = zs * spk;
+    nk = min(spk, nk_all - k0);
+    const int taps = Rk * S, tap = k0 % taps;
+    tr = tap / S;
+    ts = tap - tr * S;
+    ksb = (k0 / taps) * T::BK;
+  }
   if (KSL) {
-    tap_rows(0, 0);
+    tap_rows(tr, ts);
   } else {
     const int rs = kq8 / C;
     kr = rs / S;
@@ -598,7 +618,22 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_k(
   if constexpr (T::M16) {
     f32x4v acc[T::MI16][T::NI16];
     zero_acc4(acc);
-    main_loop16<T>(smem, (Ktot + T::BK - 1) / T::BK, acc, ra, rbv, rb, kq, load_all, adv);
+    main_loop16<T>(smem, nk, acc, ra, rbv, rb, kq, load_all, adv);
+    if constexpr (SPLIT) {
+      float* sl = slab + (long)zs * (M - m_base) * Cop;
+#pragma unroll
+      for (int i = 0; i < T::MI16; ++i)
+#pragma unroll
+        for (int j = 0; j < T::NI16; ++j) {
+          const int n = n0 + wn0 + 16 * j + (lane & 15);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int mm = m0 + wm0 + 16 * i + 4 * (lane >> 4) + r;
+            if (n < Cop && mm < M) sl[(long)(mm - m_base) * Cop + n] = acc[i][j][r];
+          }
+        }
+      return;
+    }
     // 16x16 blocks: lane holds column lane & 15, rows 4 (lane >> 4) + r.  IN partials per 32-row
     // group (block pair 2g, 2g+1): per-lane fixed-order fp64 sums, then over the four lanes of a
     // column (xor 16, xor 32).
@@ -638,7 +673,22 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_k(
   }
   f32x16 acc[T::MI][T::NI];
   zero_acc(acc);
-  main_loop<T>(smem, (Ktot + T::BK - 1) / T::BK, acc, ra, rbv, rb, kq, load_all, adv);
+  main_loop<T>(smem, nk, acc, ra, rbv, rb, kq, load_all, adv);
+  if constexpr (SPLIT) {
+    float* sl = slab + (long)zs * (M - m_base) * Cop;
+#pragma unroll
+    for (int i = 0; i < T::MI; ++i)
+#pragma unroll
+      for (int j = 0; j < T::NI; ++j) {
+        const int n = n0 + wn0 + 32 * j + (lane & 31);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int mm = m0 + wm0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          if (n < Cop && mm < M) sl[(long)(mm - m_base) * Cop + n] = acc[i][j][r];
+        }
+      }
+    return;
+  }
 
 #pragma unroll
   for (int i = 0; i < T::MI; ++i)
@@ -823,6 +873,57 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_wgrad_bf_k(
     }
 }
 
+// Split-K tail: y[m][n] = act(sum_z slab[z][m - m_base][n] + bias[n]) (splits summed in order) and,
+// with part, the InstanceNorm partials {sum y, sum y^2} of each 32-row group in the layout of the
+// GEMM epilogue's.  A block owns one 32-row group x 64 channels: thread (row pair r, r + 16; 4
+// channels) issues all its 2 x ks float4 slab loads together, then the 16 row-threads' fp64 sums
+// fold through LDS in a fixed order.  grid (ceil((M - m_base) / 32), ceil(Cop / 64)), 256 threads;
+// Cop % 4 == 0.
+__global__ __launch_bounds__(256) void fprop_splitk_reduce_k(const float* __restrict__ slab, int ks, int m_base, int M,
+                                                             int Cop, const float* __restrict__ bias, int act,
+                                                             float slope, float* __restrict__ y,
+                                                             double* __restrict__ part, int hw) {
+  __shared__ double red[2][16][65];
+  const int t = threadIdx.x, c4 = (t & 15) * 4, sub = t >> 4;
+  const int n = blockIdx.y * 64 + c4;
+  const long rows = M - m_base, zst = rows * Cop;
+  const int r0 = blockIdx.x * 32;
+  double s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
+  if (n < Cop) {
+    const float4 bv = bias ? *reinterpret_cast<const float4*>(bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const long r = r0 + sub + 16 * h;
+      if (r >= rows) break;
+      float4 v = bv;
+      for (int z = 0; z < ks; ++z) add_f4(v, *reinterpret_cast<const float4*>(slab + z * zst + r * Cop + n));
+      const float o[4] = {apply_act(v.x, act, slope), apply_act(v.y, act, slope), apply_act(v.z, act, slope),
+                          apply_act(v.w, act, slope)};
+      *reinterpret_cast<float4*>(y + (m_base + r) * Cop + n) = make_float4(o[0], o[1], o[2], o[3]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        s1[e] += o[e];
+        s2[e] += (double)o[e] * o[e];
+      }
+    }
+  }
+  if (!part) return;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    red[0][sub][c4 + e] = s1[e];
+    red[1][sub][c4 + e] = s2[e];
+  }
+  __syncthreads();
+  if (t < 128) {
+    const int v = t >> 6, c = t & 63, nn = blockIdx.y * 64 + c;
+    if (nn >= Cop) return;
+    double acc = 0.0;
+    for (int q = 0; q < 16; ++q) acc += red[v][q][c];
+    const int g0 = m_base + r0, img = g0 / hw, zg = (g0 - img * hw) >> 5;
+    part[(((long)img * (hw >> 5) + zg) * Cop + nn) * 2 + v] = acc;
+  }
+}
+
 // NHWC [P][Cs] fp32 -> NP bf16 planes [NP][Cs][ld] (hi, (mid,) lo of each value, the same RNE
 // conversions as split8 / split3_k) through a 64x64 LDS transpose tile: the weight gradient's
 // pre-split B operand.
@@ -1003,13 +1104,53 @@ void bf_plan(long M, int Cop, int math, int kind, int* kind_out, int* m_split_ou
   *tail_out = m_split ? tail_kind : -1;
 }
 
+// Split-K count for the wave-quantisation tail of a whole-round x6 plan (the rows past m_split as
+// 256x128 tiles, K split ks ways, + fprop_splitk_reduce_k), 0 = none; cost model in microseconds:
+// rounds x (K-steps x 2.25 + 4) for the GEMM (the 256x128 x6 tile runs ~2.25 us per 32-deep K-step
+// per round) + the reduction's slab traffic at 4 TB/s + a launch.  N=8 ResnetBlock data gradient
+// (2080 tail rows): 14 splits of 6 K-steps; N=12 forward (16384 rows): 2 splits.
+int bf_tail_ks(long M, int Cop, int m_split, int nk) {
+  const long rest = M - m_split;
+  if (m_split <= 0 || rest <= 0) return 0;
+  const long Tt = ((rest + 255) / 256) * ((Cop + 127) / 128);
+  double best = 1e30;
+  int bk = 0;
+  for (int ks = 2; ks <= 16; ++ks) {
+    const int steps = (nk + ks - 1) / ks;
+    if ((long)(ks - 1) * steps >= nk) continue;  // a split would be empty
+    const long rounds = (Tt * ks + VST_NUM_CUS - 1) / VST_NUM_CUS;
+    const double us = rounds * (steps * 2.25 + 4.0) + (double)(ks + 1) * rest * Cop * 4.0 / 4.0e6 + 3.0;
+    if (us < best) {
+      best = us;
+      bk = ks;
+    }
+  }
+  return bk;
+}
+
+size_t bf_fprop_ws_floats(long M, int Cop, int C, int R, int S, int math) {
+  if (math != VST_MATH_BF16X6 || !VST_BF_KSLICE || C % 32 || !VST_BF_SPLITK) return 0;
+  int kd, m_split, tail_kind;
+  bf_plan(M, Cop, math, -1, &kd, &m_split, &tail_kind);
+  if (kd != 7 || !m_split) return 0;
+  const int ks = bf_tail_ks(M, Cop, m_split, (R * S * C + 31) / 32);
+  return ks ? (size_t)ks * (M - m_split) * Cop : 0;
+}
+
 int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* bias, float* y, int N,
                     int H, int W, int C, int Ho, int Wo, int Cop, int R, int S, int st, int padh, int padw,
-                    int reflect, int act, float slope, int math, int kind, hipStream_t s, double* part) {
+                    int reflect, int act, float slope, int math, int kind, hipStream_t s, double* part,
+                    float* tws, size_t tws_floats) {
   const int M = N * Ho * Wo, K = R * S * C;
   const __bf16* ws = reinterpret_cast<const __bf16*>(wsplit);
   int kd, m_split, tail_kind;
   bf_plan(M, Cop, math, kind, &kd, &m_split, &tail_kind);
+  int ks = 0;
+  if (tws && kind < 0 && kd == 7 && m_split && math == VST_MATH_BF16X6 && VST_BF_KSLICE && C % 32 == 0 &&
+      VST_BF_SPLITK) {
+    ks = bf_tail_ks(M, Cop, m_split, (K + 31) / 32);
+    if ((size_t)ks * (M - m_split) * Cop > tws_floats) ks = 0;
+  }
 #define VST_BF(BM_, BN_, WM_, WN_, BK_, NP_)                                                       \
   {                                                                                                 \
     using T = bf::Tile<BM_, BN_, WM_, WN_, BK_, NP_>;                                              \
@@ -1027,6 +1168,20 @@ int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* b
   for (int ph = 0; ph < (m_split ? 2 : 1); ++ph) {
     const int mb = ph ? m_split : 0, Mend = (m_split && !ph) ? m_split : M;
     const int kp = ph ? tail_kind : kd;
+    if (ph == 1 && ks) {
+      using T = bf::Tile<256, 128, 64, 64, 32, 3>;
+      const int nk = (K + T::BK - 1) / T::BK, spk = (nk + ks - 1) / ks;
+      const dim3 grid(ceil_div(M - mb, 256) * ceil_div(Cop, 128) * ks);
+      if (reflect)
+        hipLaunchKernelGGL((bf::conv_fprop_bf_k<T, true, 1, true>), grid, dim3(T::NT), 0, s, x, ws, wps, bias, y, H,
+                           W, C, Ho, Wo, Cop, S, st, padh, padw, reflect, act, slope, M, K, mb, part, spk, tws);
+      else
+        hipLaunchKernelGGL((bf::conv_fprop_bf_k<T, true, 0, true>), grid, dim3(T::NT), 0, s, x, ws, wps, bias, y, H,
+                           W, C, Ho, Wo, Cop, S, st, padh, padw, reflect, act, slope, M, K, mb, part, spk, tws);
+      hipLaunchKernelGGL(bf::fprop_splitk_reduce_k, dim3(ceil_div(M - mb, 32), ceil_div(Cop, 64)), dim3(256), 0, s,
+                         tws, ks, mb, M, Cop, bias, act, slope, y, part, Ho * Wo);
+      continue;
+    }
     if (math == VST_MATH_BF16X6) {
       VST_BF_DISPATCH(kp, 3, VST_BF)
     } else {

@@ -189,6 +189,24 @@ def _probe_end(h):
         p.events.append(ev)
 
 
+# Split-K tails of x6 forward grids (vst_conv2d_fwd_ws); VST_FWD_SPLITK=0 keeps the small-tile tails.
+FWD_SPLITK = os.environ.get("VST_FWD_SPLITK", "1") != "0"
+_fws_cache = {}
+
+
+def _fwd_ws(N, H, W, Cx, cop, R, S, stride, pad, m, device):
+    """Workspace tensor of vst_conv2d_fwd_ws for this shape (None when the launch needs none)."""
+    if not FWD_SPLITK:
+        return None, 0
+    key = (N, H, W, Cx, cop, R, S, stride, pad, m)
+    nb = _fws_cache.get(key)
+    if nb is None:
+        nb = _fws_cache[key] = int(lib().vst_conv2d_fwd_ws_bytes(N, H, W, Cx, cop, R, S, stride, pad, m))
+    if nb == 0:
+        return None, 0
+    return torch.empty((nb + 3) // 4, device=device), nb
+
+
 def conv2d_fwd(x, wp, bias, cop, R, S, stride, pad, pad_mode="zero", act="none", slope=0.0,
                out=None, role="fwd"):
     _dev_check(x, wp, bias)
@@ -196,10 +214,16 @@ def conv2d_fwd(x, wp, bias, cop, R, S, stride, pad, pad_mode="zero", act="none",
     Ho = (H + 2 * pad - R) // stride + 1
     Wo = (W + 2 * pad - S) // stride + 1
     y = out if out is not None else torch.empty((N, Ho, Wo, cop), device=x.device)
+    m = _math(role)
+    ws, nb = _fwd_ws(N, H, W, Cx, cop, R, S, stride, pad, m, x.device) if S == R else (None, 0)
     h = _probe_begin("fwd", (N, H, W, Cx, cop, R, stride, pad, pad_mode)) if _probes else None
-    _call("vst_conv2d_fwd", _p(x), _p(wp), _p(getattr(wp, "vst_split", None)), _p(bias), _p(y), N, H,
-          W, Cx, cop, R, S, stride, pad,
-          PAD[pad_mode], ACT[act], float(slope), _math(role), _stream())
+    if ws is not None:
+        _call("vst_conv2d_fwd_ws", _p(x), _p(wp), _p(getattr(wp, "vst_split", None)), _p(bias), _p(y), N, H, W, Cx,
+              cop, R, S, stride, pad, PAD[pad_mode], ACT[act], float(slope), m, None, None, _p(ws), nb, _stream())
+    else:
+        _call("vst_conv2d_fwd", _p(x), _p(wp), _p(getattr(wp, "vst_split", None)), _p(bias), _p(y), N, H,
+              W, Cx, cop, R, S, stride, pad,
+              PAD[pad_mode], ACT[act], float(slope), m, _stream())
     _probe_end(h)
     return y
 
@@ -218,10 +242,12 @@ def conv2d_fwd_in(x, wp, bias, cop, R, S, stride, pad, pad_mode="zero", role="fw
     hw = Ho * Wo
     part = torch.empty((N * max(1, hw // 32) * cop * 2,), device=x.device, dtype=torch.float64)
     nsplit = ctypes.c_int(0)
+    m = _math(role)
+    ws, nb = _fwd_ws(N, H, W, Cx, cop, R, S, stride, pad, m, x.device) if S == R else (None, 0)
     h = _probe_begin("fwd", (N, H, W, Cx, cop, R, stride, pad, pad_mode)) if _probes else None
-    _call("vst_conv2d_fwd_in", _p(x), _p(wp), _p(getattr(wp, "vst_split", None)), _p(bias), _p(y), N, H, W, Cx,
-          cop, R, S, stride, pad, PAD[pad_mode], ACT["none"], 0.0, _math(role), _p(part),
-          ctypes.addressof(nsplit), _stream())
+    _call("vst_conv2d_fwd_ws", _p(x), _p(wp), _p(getattr(wp, "vst_split", None)), _p(bias), _p(y), N, H, W, Cx,
+          cop, R, S, stride, pad, PAD[pad_mode], ACT["none"], 0.0, m, _p(part),
+          ctypes.addressof(nsplit), _p(ws), nb, _stream())
     _probe_end(h)
     if nsplit.value == 0:
         return y, instnorm_stats(y)
@@ -323,6 +349,16 @@ def conv_plan_wgrad(N, H, W, Cx, Ho, Wo, Cyp, R, S, stride, math):
     _call("vst_conv_plan_wgrad", N, H, W, Cx, Ho, Wo, Cyp, R, S, stride, m, ctypes.addressof(path),
           ctypes.addressof(kind), ctypes.addressof(ns))
     return path.value, kind.value, ns.value
+
+
+def conv_plan_fwd_tail(N, H, W, Cx, Cop, R, S, stride, pad, math):
+    """Host-only: split-K count of the x6 tail launch vst_conv2d_fwd_ws runs for this shape (0: none)."""
+    import ctypes
+    from ._lib import MATH_MODES
+    m = MATH_MODES[math] if math in MATH_MODES else _math(math)
+    ks = ctypes.c_int(0)
+    _call("vst_conv_plan_fwd_tail", N, H, W, Cx, Cop, R, S, stride, pad, m, ctypes.addressof(ks))
+    return ks.value
 
 
 def conv_plan_fwd(N, H, W, Cx, Cop, R, S, stride, pad_h, pad_w, math, with_tail=False):

@@ -119,6 +119,21 @@ enum { VST_MATH_F32 = 0, VST_MATH_BF16X3 = 1, VST_MATH_BF16X6 = 2 };
 int vst_conv2d_fwd(const float* x, const float* wp, const void* wsplit, const float* bias, float* y,
                    int N, int H, int W, int Cx, int Cop, int R, int S, int stride, int pad,
                    int pad_mode, int act, float slope, int math, void* stream);
+/* Workspace of vst_conv2d_fwd_ws for this shape and arithmetic (0: the launch needs none).  Under
+ * bf16x6 a grid that is not a whole number of 256x128-tile rounds runs its whole rounds as one
+ * launch and the remaining pixel rows as a split-K launch (ks K ranges of the same 256x128 tiles)
+ * whose partial tiles go to the workspace and are summed in split order by a reduction that applies
+ * bias / act / the IN partials — instead of a launch of smaller tiles that leaves CUs idle. */
+size_t vst_conv2d_fwd_ws_bytes(int N, int H, int W, int Cx, int Cop, int R, int S, int stride, int pad,
+                               int math);
+/* vst_conv2d_fwd (part == NULL) / vst_conv2d_fwd_in (part, nsplit) with a caller workspace ws of
+ * ws_bytes >= vst_conv2d_fwd_ws_bytes (ws may be NULL when that is 0). */
+int vst_conv2d_fwd_ws(const float* x, const float* wp, const void* wsplit, const float* bias, float* y, int N,
+                      int H, int W, int Cx, int Cop, int R, int S, int stride, int pad, int pad_mode, int act,
+                      float slope, int math, double* part, int* nsplit, float* ws, size_t ws_bytes, void* stream);
+/* Host-only: the split-K count of that tail launch (0 = none) for this shape and arithmetic. */
+int vst_conv_plan_fwd_tail(int N, int H, int W, int Cx, int Cop, int R, int S, int stride, int pad, int math,
+                           int* ksplit);
 /* vst_conv2d_fwd plus the InstanceNorm statistics partials of its output, from the GEMM epilogue
  * (the conv that feeds an InstanceNorm): when the split-bf16 kernels run the conv and Ho*Wo % 32 == 0,
  * part (fp64, N * (Ho*Wo/32) * Cop * 2) receives {sum y, sum y^2} per (image, 32-pixel group,

@@ -562,3 +562,36 @@ def test_instnorm_fwd_cp_and_wgrad_exact(ops, st, mode, res):
         assert torch.equal(dw0, dw1)
     finally:
         ops.set_conv_math(prev)
+
+
+@pytest.mark.parametrize("N,pad", [(8, 2), (12, 1), (12, 2)], ids=["n8_dgrad_frame", "n12_fwd", "n12_dgrad_frame"])
+def test_splitk_tail_vs_small_tiles_and_torch(ops, N, pad):
+    """The x6 split-K wave-quantisation tail (vst_conv2d_fwd_ws: whole rounds of 256x128 tiles, then
+    the remaining rows as ks K-range splits of the same tiles + an in-order reduction with bias and
+    the IN partials) against the small-tile tail (no workspace) and torch fp32 on the CPU.  Shapes:
+    the ResnetBlock conv as the batched train step runs it (N=12 forward; the 66x66-frame data
+    gradient, pad 2, at N=8 / 12)."""
+    prev = ops.set_conv_math("bf16x6")
+    try:
+        C, H = 256, 64
+        assert ops.conv_plan_fwd_tail(N, H, H, C, C, 3, 3, 1, pad, "bf16x6") >= 2
+        x = _g(21, (N, C, H, H))
+        w = _g(22, (C, C, 3, 3), 0.03)
+        b = _g(23, (C,), 0.1)
+        kc = ops.weight_pack(w.to(DEV), ops.PACK_FWD)
+        xn = _nhwc(x, ops)
+        y, s = ops.conv2d_fwd_in(xn, kc, b.to(DEV), C, 3, 3, 1, pad, "zero")
+        ops.FWD_SPLITK = False
+        try:
+            y0, s0 = ops.conv2d_fwd_in(xn, kc, b.to(DEV), C, 3, 3, 1, pad, "zero")
+        finally:
+            ops.FWD_SPLITK = True
+        _close(y, y0, tol=2e-6, what="split-K vs small tiles")
+        # stats [N][C][{mean, rstd}]: mean error in units of the channel's std, rstd relative
+        dm = ((s[..., 0] - s0[..., 0]).abs() * s0[..., 1]).max().item()
+        dr = ((s[..., 1] - s0[..., 1]).abs() / s0[..., 1]).max().item()
+        assert dm < 1e-5 and dr < 1e-5, (dm, dr)
+        yr = F.conv2d(x, w, b, padding=pad)
+        _close(_nchw(y, C, ops), yr, tol=CONV_TOL["bf16x6"], what="split-K vs torch fp32")
+    finally:
+        ops.set_conv_math(prev)

@@ -88,7 +88,7 @@ def DOMINANT_KEYS(B):
             "resblock_wgrad": ("wgrad", (N, 64, 64, 256, 256, 3, 1, 1, "reflect"))}
 
 
-PMC_FILE = os.path.join(HERE, "profiles", "r02_conv_pmc.json")
+PMC_FILE = os.path.join(HERE, "profiles", "r02b_conv_pmc.json")
 
 
 def _pmc_traffic(name, key):
@@ -133,9 +133,10 @@ def conv_roofline(name, probe, math):
     achieved = flop / (ms * 1e-3) / 1e12
     if op == "fwd":
         kind, ms_ = ops.conv_plan_fwd(N, H, W, Cx, Cop, R, R, st, pad, pad, m)
-        kernel = "conv_fprop_bf_k<%s, %s, %s>%s" % (ops.TILE_NAMES.get(kind, kind), m, _mfma(m),
-                                                    " + tail launch" if ms_ else "")
-        key = {"math": m, "tile": kind, "m_split": ms_, "N": N, "mfma": _mfma(m)}
+        ks = ops.conv_plan_fwd_tail(N, H, W, Cx, Cop, R, R, st, pad, m) if (ms_ and ops.FWD_SPLITK) else 0
+        tail = (" + split-K tail (%d splits) + reduction" % ks) if ks else (" + small-tile tail launch" if ms_ else "")
+        kernel = "conv_fprop_bf_k<%s, %s, %s>%s" % (ops.TILE_NAMES.get(kind, kind), m, _mfma(m), tail)
+        key = {"math": m, "tile": kind, "m_split": ms_, "N": N, "mfma": _mfma(m), "ksplit": ks}
         note = ("stride-1 data gradient as a forward conv over the rotated taps (66x66 padded frame)"
                 if name == "resblock_dgrad" else "ResnetBlock conv forward")
     else:

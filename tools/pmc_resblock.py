@@ -16,11 +16,12 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-OPS = {"fprop": ("conv_fprop_bf_k",), "dgrad": ("conv_fprop_bf_k",),
+OPS = {"fprop": ("conv_fprop_bf_k",), "dgrad": ("conv_fprop_bf_k", "fprop_splitk_reduce_k"),
        "wgrad": ("nhwc_to_cp", "conv_wgrad_bf_k", "wgrad_reduce_store_k", "slab_group_sum_k"),
        "warp": ("warp_fwd_k",)}
 # the op's main GEMM dispatch (SQ metrics and its timing; the dgrad's 64x64 tail launch is excluded)
-MAIN = {"fprop": "Tile<256, 128", "dgrad": "Tile<256, 128", "wgrad": "conv_wgrad_bf_k", "warp": "warp_fwd_k"}
+MAIN = {"fprop": "3>, true, 1, false>", "dgrad": "3>, true, 0, false>", "wgrad": "conv_wgrad_bf_k",
+        "warp": "warp_fwd_k"}
 WARP_BYTES = 32 * 436 * 1024 * (8.0 * 64 + 8.0)  # bench.py warp_roofline: N*H*W*(4C gather + 8 flow + 4C write)
 
 
@@ -72,7 +73,8 @@ def main():
             gbvst._lib.load()
             pad = 1 if op == "fprop" else 2
             kind, ms = ops.conv_plan_fwd(B, 64, 64, 256, 256, 3, 3, 1, pad, pad, "bf16x6")
-            key.update(tile=kind, m_split=ms)
+            ks = ops.conv_plan_fwd_tail(B, 64, 64, 256, 256, 3, 3, 1, pad, "bf16x6") if (ms and ops.FWD_SPLITK) else 0
+            key.update(tile=kind, m_split=ms, ksplit=ks)
         res[name] = {"key": key, "dispatches_per_call": len(fetch) / reps, "fetch_bytes": fb, "write_bytes": wb,
                      "hbm_bytes_per_launch": fb + wb, "algorithmic_bytes": alg,
                      "main_kernel_avg_us": round(sum(t) / len(t), 2) if t else None,

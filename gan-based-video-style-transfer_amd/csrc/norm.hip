@@ -168,6 +168,12 @@ __global__ __launch_bounds__(NRED) void fold_in_partial_k(const float* __restric
   float4* gb = reinterpret_cast<float4*>(gout) + (long)n * HW * LP + c4;
   auto fold = [&](int p) {
     const int h = p / W, w = p - (p / W) * W;
+    float4 g = ab ? ab[(long)p * LP] : make_float4(0.f, 0.f, 0.f, 0.f);
+    if (h > pad && h < H - 1 - pad && w > pad && w < W - 1 - pad) {  // interior: one source
+      add_f4(g, src[((long)(h + pad) * Wp + w + pad) * LP]);
+      gb[(long)p * LP] = g;
+      return g;
+    }
     int hs[3], wsx[3], nh = 0, nw = 0;
     hs[nh++] = h + pad;
     if (h >= 1 && h <= pad) hs[nh++] = pad - h;
@@ -175,7 +181,6 @@ __global__ __launch_bounds__(NRED) void fold_in_partial_k(const float* __restric
     wsx[nw++] = w + pad;
     if (w >= 1 && w <= pad) wsx[nw++] = pad - w;
     if (w >= W - 1 - pad && w <= W - 2) wsx[nw++] = 2 * W - 2 - w + pad;
-    float4 g = ab ? ab[(long)p * LP] : make_float4(0.f, 0.f, 0.f, 0.f);
     for (int a = 0; a < nh; ++a)
       for (int b = 0; b < nw; ++b) add_f4(g, src[((long)hs[a] * Wp + wsx[b]) * LP]);
     gb[(long)p * LP] = g;
@@ -195,7 +200,7 @@ __global__ __launch_bounds__(NRED) void fold_in_partial_k(const float* __restric
       acc[2][j] += xh;
     }
   };
-  constexpr int UR = 2;
+  constexpr int UR = 4;
   if (pg < PG) {
     int p = p0 + pg;
     for (; p + (UR - 1) * PG < p1; p += UR * PG) {

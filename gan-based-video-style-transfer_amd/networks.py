@@ -398,9 +398,13 @@ class ResnetGenerator(FlatNet):
             if c0.weight.shape[1] <= 4:  # image-input first layer: its data gradient as a tap gather
                 P["c0kc"] = ops.weight_pack(c0.weight, ops.PACK_KC)
         P["ikf"] = {}
+        # the ResnetBlock data gradients run as forward convs over the IKF packs when the channel
+        # count suits the split-bf16 kernel (dgrad_reflect): their IK packs are then never read
+        ik_blocks = not (DGRAD_AS_FPROP and cpad(4 * self.ngf) % 8 == 0)
         for i, b in enumerate(blocks):
-            P[f"b{i}a"] = _pack_conv(b.conv_block[1])
-            P[f"b{i}b"] = _pack_conv(b.conv_block[5])
+            for key, m in ((f"b{i}a", b.conv_block[1]), (f"b{i}b", b.conv_block[5])):
+                P[key] = _pack_conv(m) if ik_blocks else (ops.weight_pack(m.weight, ops.PACK_FWD), None,
+                                                           _padded_bias(m))
             P["ikf"][f"b{i}a"] = _ikf(b.conv_block[1])
             P["ikf"][f"b{i}b"] = _ikf(b.conv_block[5])
         if C8_EDGES and DGRAD_AS_FPROP and f.weight.shape[0] <= 4:

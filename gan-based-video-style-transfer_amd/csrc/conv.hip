@@ -737,6 +737,9 @@ static int pick_splits(int tiles, int slots, int max_ns, int min_ns = 1) {
 #ifndef VST_WG_BIG
 #define VST_WG_BIG 5  // rk tile kind of the wide (Cyp > 64, Mw >= 1024) weight gradients
 #endif
+#ifndef VST_WG_BIGM
+#define VST_WG_BIGM 512  // x6 wgrads with Cyp > 64 and Mw >= this run on 256x128 tiles (A/B: 1024 -> 512, -0.15 ms/step)
+#endif
 #ifndef VST_WG_BF
 #define VST_WG_BF 1   // x6 weight gradients on the split-bf16 kernel (conv_wgrad_bf_k)
 #endif
@@ -760,7 +763,7 @@ static WgradPlan plan_wgrad(int N, int H, int W, int Ho, int Wo, int Cx, int Cyp
     // x6: the split-bf16 weight-gradient kernel (conv_bf.hip), 256x128 tiles for the wide layers
     p.trans = p.bfk = true;
     p.pad = s1 ? pd2 / 2 : -1;
-    const int kind = Cyp > 64 ? (p.Mw >= 1024 ? 7 : 3) : (p.Mw >= 1024 ? 1 : 8);
+    const int kind = Cyp > 64 ? (p.Mw >= VST_WG_BIGM ? 7 : 3) : (p.Mw >= 1024 ? 1 : 8);
     p.tile = (TileKind)kind;
     int bm, bn, bk, slots;
     bf_wgrad_geom(kind, math, &bm, &bn, &bk, &slots);

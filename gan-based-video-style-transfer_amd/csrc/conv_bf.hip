@@ -890,7 +890,8 @@ __global__ __launch_bounds__(256) void fprop_splitk_reduce_k(const float* __rest
   const int r0 = blockIdx.x * 32;
   double s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
   if (n < Cop) {
-    const float4 bv = bias ? *reinterpret_cast<const float4*>(bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+    // scalar loads: a bias may be a view at any 4-byte offset of a network's flat parameter buffer
+    const float4 bv = bias ? make_float4(bias[n], bias[n + 1], bias[n + 2], bias[n + 3]) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const long r = r0 + sub + 16 * h;

@@ -558,18 +558,23 @@ __global__ __launch_bounds__((Tile<BM, BN, WM, WN>::NT), 2) void conv_wgrad_k(
 // summing 4 float4 column quads over the nsplit slabs (all slab loads of a quad issued back to back,
 // z = 0, 1, 2, ...: a fixed order, so deterministic), then an LDS transpose and the [Co][Ci][R][S]
 // store (+= across the step's passes).  One launch instead of a slab-sized sum pass + a store pass.
+// Split-K slabs S[z][(rs, ci)][Cyp] summed in slab order and stored transposed into dw[co][ci][rs]
+// (strides so / si).  A block owns 32 (rs, ci) rows x 64 channels: 2 rows per thread with 8 slabs'
+// loads per round trip (16 float4 in flight per thread, ~1100 waves for a ResnetBlock weight), then a
+// 32 x 64 LDS transpose for the [co]-major store.  grid (ceil(Ci*RS / 32), ceil(Cyp / 64)).
 __global__ __launch_bounds__(256) void wgrad_reduce_store_k(const float* __restrict__ S, float* __restrict__ dw,
                                                             int Cx, int Cyp, int RS, int Co, int Ci, long so,
                                                             long si, int accumulate, int nsplit, long zs) {
-  __shared__ float tile[64][65];
-  const int m0 = blockIdx.x * 64, c0 = blockIdx.y * 64;
+  __shared__ float tile[32][65];
+  const int m0 = blockIdx.x * 32, c0 = blockIdx.y * 64;
   const int t = threadIdx.x, c4 = (t & 15) * 4, r0 = t >> 4;
   const int Md = Ci * RS;
-  float4 acc[4];
-  const float* src[4];
-  bool ok[4];
+  constexpr int NR = 2, UZ = 8;
+  float4 acc[NR];
+  const float* src[NR];
+  bool ok[NR];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < NR; ++i) {
     const int md = m0 + r0 + 16 * i;
     ok[i] = md < Md && c0 + c4 < Cyp;
     const int mm = ok[i] ? md : 0;
@@ -577,29 +582,28 @@ __global__ __launch_bounds__(256) void wgrad_reduce_store_k(const float* __restr
     src[i] = S + (long)(rs * Cx + ci) * Cyp + (ok[i] ? c0 + c4 : 0);
     acc[i] = ok[i] ? *reinterpret_cast<const float4*>(src[i]) : make_float4(0.f, 0.f, 0.f, 0.f);
   }
-  // four slabs' loads in flight per round trip (the adds stay in slab order)
   int z = 1;
-  for (; z + 3 < nsplit; z += 4) {
-    float4 v[4][4];
+  for (; z + UZ - 1 < nsplit; z += UZ) {
+    float4 v[UZ][NR];
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+    for (int u = 0; u < UZ; ++u)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < NR; ++i)
         v[u][i] = *reinterpret_cast<const float4*>(src[i] + (ok[i] ? (long)(z + u) * zs : 0));
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+    for (int u = 0; u < UZ; ++u)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) add4(acc[i], v[u][i]);
+      for (int i = 0; i < NR; ++i) add4(acc[i], v[u][i]);
   }
   for (; z < nsplit; ++z) {
-    float4 v[4];
+    float4 v[NR];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] = *reinterpret_cast<const float4*>(src[i] + (ok[i] ? (long)z * zs : 0));
+    for (int i = 0; i < NR; ++i) v[i] = *reinterpret_cast<const float4*>(src[i] + (ok[i] ? (long)z * zs : 0));
 #pragma unroll
-    for (int i = 0; i < 4; ++i) add4(acc[i], v[i]);
+    for (int i = 0; i < NR; ++i) add4(acc[i], v[i]);
   }
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < NR; ++i) {
     const int r = r0 + 16 * i;
     tile[r][c4] = acc[i].x;
     tile[r][c4 + 1] = acc[i].y;
@@ -607,8 +611,8 @@ __global__ __launch_bounds__(256) void wgrad_reduce_store_k(const float* __restr
     tile[r][c4 + 3] = acc[i].w;
   }
   __syncthreads();
-  const int tx = t & 63, ty = t >> 6;
-  for (int r = ty; r < 64; r += 4) {
+  const int tx = t & 31, ty = t >> 5;
+  for (int r = ty; r < 64; r += 8) {
     const int c = c0 + r, md = m0 + tx;
     if (c >= Co || md >= Md) continue;
     const int ci = md / RS, rs = md - ci * RS;
@@ -1083,7 +1087,7 @@ extern "C" int vst_conv2d_wgrad_pre(const float* x, const float* x_t, const floa
                        p.nsplit, WG_GROUP);
     red = l2;
   }
-  hipLaunchKernelGGL(wgrad_reduce_store_k, dim3(ceil_div(Ci * R * S, 64), ceil_div(Co, 64)), dim3(256), 0, s,
+  hipLaunchKernelGGL(wgrad_reduce_store_k, dim3(ceil_div(Ci * R * S, 32), ceil_div(Co, 64)), dim3(256), 0, s,
                      red, dw, Cx, Cyp, R * S, Co, Ci, so, si, accumulate, nred, slab);
   return check_launch("conv2d_wgrad_reduce");
 }

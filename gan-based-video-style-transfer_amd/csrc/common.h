@@ -100,6 +100,7 @@ int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* b
                     double* part = nullptr, float* tws = nullptr, size_t tws_floats = 0);
 size_t bf_fprop_ws_floats(long M, int Cop, int C, int R, int S, int math);
 int bf_tail_ks(long M, int Cop, int m_split, int nk);
+void bf_split_plan(long M, int Cop, int C, int R, int S, int math, int kind, int* m_first, int* ks_out);
 void bf_plan(long M, int Cop, int math, int kind, int* kind_out, int* m_split_out, int* tail_out);
 // split-arithmetic weight gradient (conv_bf.hip): dy as pre-split bf16 planes, x as the padded fp32 copy
 void bf_nhwc_to_planes(const float* x, void* y, long P, int Cs, int np, hipStream_t s);

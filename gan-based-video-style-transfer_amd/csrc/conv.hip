@@ -926,9 +926,8 @@ extern "C" int vst_conv_plan_fwd_tail(int N, int H, int W, int Cx, int Cop, int 
   const size_t b = vst_conv2d_fwd_ws_bytes(N, H, W, Cx, Cop, R, S, stride, pad, math);
   if (b) {
     const int Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - S) / stride + 1;
-    int kd, m_split, tk;
-    bf_plan((long)N * Ho * Wo, Cop, math, -1, &kd, &m_split, &tk);
-    *ksplit = bf_tail_ks((long)N * Ho * Wo, Cop, m_split, (R * S * Cx + 31) / 32);
+    int mf;
+    bf_split_plan((long)N * Ho * Wo, Cop, Cx, R, S, math, -1, &mf, ksplit);
   }
   return VST_OK;
 }

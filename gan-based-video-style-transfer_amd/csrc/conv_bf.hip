@@ -61,6 +61,9 @@
 #ifndef VST_BF_SPLITK
 #define VST_BF_SPLITK 1  // split-K wave-quantisation tails (when the caller passes a workspace)
 #endif
+#ifndef VST_BF_FULLSPLIT_MAX
+#define VST_BF_FULLSPLIT_MAX 128  // x6 forwards of at most this many 256x128 tiles run whole as split-K
+#endif
 #ifndef VST_BF_TAIL_FORCE
 #define VST_BF_TAIL_FORCE -1
 #endif
@@ -1129,13 +1132,53 @@ int bf_tail_ks(long M, int Cop, int m_split, int nk) {
   return bk;
 }
 
-size_t bf_fprop_ws_floats(long M, int Cop, int C, int R, int S, int math) {
-  if (math != VST_MATH_BF16X6 || !VST_BF_KSLICE || C % 32 || !VST_BF_SPLITK) return 0;
+// Split-K plan of an x6 forward with a workspace: (first split row, splits), splits = 0 for none.
+//   * tail: a whole-round 256x128 plan with a partial last round -> that round as splits (bf_tail_ks);
+//   * full: a grid of at most VST_BF_FULLSPLIT_MAX 256x128 tiles (the PatchGAN layers, half-batch
+//     passes) -> the whole conv as ks K-range splits of 256x128 tiles filling the CUs, instead of
+//     small tiles that cannot fill them either; same cost model.
+void bf_split_plan(long M, int Cop, int C, int R, int S, int math, int kind, int* m_first, int* ks_out) {
+  *m_first = 0;
+  *ks_out = 0;
+  if (math != VST_MATH_BF16X6 || !VST_BF_KSLICE || C % 32 || !VST_BF_SPLITK || kind >= 0) return;
+  const int nk = (R * S * C + 31) / 32;
   int kd, m_split, tail_kind;
   bf_plan(M, Cop, math, -1, &kd, &m_split, &tail_kind);
-  if (kd != 7 || !m_split) return 0;
-  const int ks = bf_tail_ks(M, Cop, m_split, (R * S * C + 31) / 32);
-  return ks ? (size_t)ks * (M - m_split) * Cop : 0;
+  if (kd == 7 && m_split) {
+    *m_first = m_split;
+    *ks_out = bf_tail_ks(M, Cop, m_split, nk);
+    return;
+  }
+  const long b256 = ((M + 255) / 256) * ((Cop + 127) / 128);
+  if (kd == 7 || b256 > VST_BF_FULLSPLIT_MAX) return;
+  // the small-tile plan it would replace: rounds x K-steps x the tile's per-round K-step time (x6,
+  // 16x16x32; measured on the ResnetBlock / PatchGAN shapes: 256x128 2.25 us, 128x128 1.5 us,
+  // 64x128 at two per CU 1.8 us; the 64-wide tiles assumed 1.2 us)
+  int bm, bn, sl;
+  bf_geom(kd, 3, &bm, &bn, &sl);
+  const long blocks = ((M + bm - 1) / bm) * ((Cop + bn - 1) / bn);
+  const long rounds_small = (blocks + (long)sl * VST_NUM_CUS - 1) / ((long)sl * VST_NUM_CUS);
+  const double t_small = (kd == 0 || kd == 2 || kd == 4 || kd == 9) ? 1.5 : (kd == 3 ? 1.8 : 1.2);
+  const double small_us = rounds_small * nk * t_small + 3.0;
+  double best = 0.85 * small_us;
+  int bk = 0;
+  for (int ks = 2; ks <= 32; ++ks) {
+    const int steps = (nk + ks - 1) / ks;
+    if (steps < 4 || (long)(ks - 1) * steps >= nk) continue;
+    const long rounds = (b256 * ks + VST_NUM_CUS - 1) / VST_NUM_CUS;
+    const double us = rounds * (steps * 2.25 + 4.0) + (double)(ks + 1) * M * Cop * 4.0 / 4.0e6 + 3.0;
+    if (us < best) {
+      best = us;
+      bk = ks;
+    }
+  }
+  *ks_out = bk;
+}
+
+size_t bf_fprop_ws_floats(long M, int Cop, int C, int R, int S, int math) {
+  int mf, ks;
+  bf_split_plan(M, Cop, C, R, S, math, -1, &mf, &ks);
+  return ks ? (size_t)ks * (M - mf) * Cop : 0;
 }
 
 int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* bias, float* y, int N,
@@ -1146,11 +1189,14 @@ int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* b
   const __bf16* ws = reinterpret_cast<const __bf16*>(wsplit);
   int kd, m_split, tail_kind;
   bf_plan(M, Cop, math, kind, &kd, &m_split, &tail_kind);
-  int ks = 0;
-  if (tws && kind < 0 && kd == 7 && m_split && math == VST_MATH_BF16X6 && VST_BF_KSLICE && C % 32 == 0 &&
-      VST_BF_SPLITK) {
-    ks = bf_tail_ks(M, Cop, m_split, (K + 31) / 32);
-    if ((size_t)ks * (M - m_split) * Cop > tws_floats) ks = 0;
+  int ks = 0, m_first = 0;
+  if (tws) {
+    bf_split_plan(M, Cop, C, R, S, math, kind, &m_first, &ks);
+    if ((size_t)ks * (M - m_first) * Cop > tws_floats) ks = 0;
+    if (ks && !m_first) {  // the whole conv as split-K 256x128 tiles: the split launch alone
+      m_split = 0;
+      kd = -1;
+    }
   }
 #define VST_BF(BM_, BN_, WM_, WN_, BK_, NP_)                                                       \
   {                                                                                                 \
@@ -1166,7 +1212,7 @@ int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* b
       hipLaunchKernelGGL((bf::conv_fprop_bf_k<T, false, 2>), grid, dim3(T::NT), 0, s, x, ws, wps, bias, y, \
                          H, W, C, Ho, Wo, Cop, S, st, padh, padw, reflect, act, slope, Mend, K, mb, part); \
   }
-  for (int ph = 0; ph < (m_split ? 2 : 1); ++ph) {
+  for (int ph = (ks && !m_first) ? 1 : 0; ph < ((m_split || (ks && !m_first)) ? 2 : 1); ++ph) {
     const int mb = ph ? m_split : 0, Mend = (m_split && !ph) ? m_split : M;
     const int kp = ph ? tail_kind : kd;
     if (ph == 1 && ks) {

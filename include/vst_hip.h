@@ -131,7 +131,9 @@ size_t vst_conv2d_fwd_ws_bytes(int N, int H, int W, int Cx, int Cop, int R, int 
 int vst_conv2d_fwd_ws(const float* x, const float* wp, const void* wsplit, const float* bias, float* y, int N,
                       int H, int W, int Cx, int Cop, int R, int S, int stride, int pad, int pad_mode, int act,
                       float slope, int math, double* part, int* nsplit, float* ws, size_t ws_bytes, void* stream);
-/* Host-only: the split-K count of that tail launch (0 = none) for this shape and arithmetic. */
+/* Host-only: the split-K count (0 = none) vst_conv2d_fwd_ws uses for this shape and arithmetic: of
+ * the tail launch, or — for grids of at most 128 256x128 tiles (PatchGAN layers, half batches) — of
+ * the whole conv, run as one split-K launch + the reduction. */
 int vst_conv_plan_fwd_tail(int N, int H, int W, int Cx, int Cop, int R, int S, int stride, int pad, int math,
                            int* ksplit);
 /* vst_conv2d_fwd plus the InstanceNorm statistics partials of its output, from the GEMM epilogue

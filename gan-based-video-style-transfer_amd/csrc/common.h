@@ -103,7 +103,8 @@ int bf_tail_ks(long M, int Cop, int m_split, int nk);
 void bf_split_plan(long M, int Cop, int C, int R, int S, int math, int kind, int* m_first, int* ks_out);
 void bf_plan(long M, int Cop, int math, int kind, int* kind_out, int* m_split_out, int* tail_out);
 // split-arithmetic weight gradient (conv_bf.hip): dy as pre-split bf16 planes, x as the padded fp32 copy
-void bf_nhwc_to_planes(const float* x, void* y, long P, int Cs, int np, hipStream_t s);
+void bf_nhwc_to_planes(const float* x, void* y, long P, int Cs, int np, hipStream_t s, int row_in = 0,
+                       int row_out = 0);
 void bf_wgrad_launch(const float* xt, const void* dyp, float* slab, int N, int H, int W, int Cx, int Ho,
                      int Wo, int Cyp, int S, int pad, int st, int Mw, int chunk, int nsplit, int kind, int math,
                      hipStream_t s);
@@ -112,7 +113,7 @@ void bf_wgrad_geom(int kind, int math, int* bm, int* bn, int* bk, int* slots);
 void rk_tile_geom(int kind, int math, int* bm, int* bn, int* bk, int* slots);
 void rk_nhwc_to_cp(const float* x, float* y, long P, int Cs, int pack, hipStream_t s);
 void rk_nhwc_to_cp_pad(const float* x, float* y, int N, int H, int W, int Cs, int pad, int reflect,
-                       int phase, int pack, hipStream_t s);
+                       int phase, int pack, hipStream_t s, int extra = 0);
 void rk_wgrad_launch(const float* xt, const float* dyt, float* slab, int N, int H, int W, int Cx,
                      int Ho, int Wo, int Cyp, int S, int pad, int st, int Mw, int chunk,
                      int nsplit, int kind, int math, hipStream_t s);

@@ -712,6 +712,7 @@ struct WgradPlan {
   bool bfk;          // trans, on the split-bf16 kernel (conv_wgrad_bf_k; x6, Wo % 8 == 0): dy as
                      // pre-split bf16 planes, `tile` is then a conv_bf tile kind
   int pad;           // trans: the border the padded x copy carries (derived from H -> Ho)
+  int wpad;          // bfk, stride 1, Wo % 8 != 0: output columns padded to a multiple of 8 (zero dy)
   long xt_floats;    // workspace floats after the slabs: xt [Cx][N*Hp*Wp] then dyt [Cyp][P]
   long dyt_floats;
 };
@@ -741,6 +742,9 @@ static int pick_splits(int tiles, int slots, int max_ns, int min_ns = 1) {
 #ifndef VST_WG_BIG
 #define VST_WG_BIG 5  // rk tile kind of the wide (Cyp > 64, Mw >= 1024) weight gradients
 #endif
+#ifndef VST_WG_PADW
+#define VST_WG_PADW 1  // stride-1 x6 wgrads with Wo % 8 != 0 on the split-bf16 kernel via Wo-padded rows
+#endif
 #ifndef VST_WG_BIGM
 #define VST_WG_BIGM 512  // x6 wgrads with Cyp > 64 and Mw >= this run on 256x128 tiles (A/B: 1024 -> 512, -0.15 ms/step)
 #endif
@@ -755,6 +759,7 @@ static WgradPlan plan_wgrad(int N, int H, int W, int Ho, int Wo, int Cx, int Cyp
   p.trans = false;
   p.bfk = false;
   p.pad = 0;
+  p.wpad = 0;
   p.xt_floats = p.dyt_floats = 0;
   const int P = N * Ho * Wo;
   const int ov = g_tile_override[2];
@@ -763,22 +768,27 @@ static WgradPlan plan_wgrad(int N, int H, int W, int Ho, int Wo, int Cx, int Cyp
   // stride 2: the pad is not recoverable from the shapes; the padded copy is sized for pad <= R - 1
   // (checked at the call) and its rows are column-phase split, which needs W + 2 pad even
   const bool s2 = stride == 2 && W % 2 == 0;
-  if (Cyp > 4 && (s1 || s2) && Wo % 8 == 0 && ov < 0 && math == VST_MATH_BF16X6 && VST_WG_BF) {
+  // stride 1 with Wo % 8 != 0 (PatchGAN's 31-wide layer): the output rows padded to a multiple of
+  // 8 columns with zero dy (and zero x columns past the border), so 8-pixel chunks stay in one row
+  const int wpad = (s1 && Wo % 8 && Wo >= 8 && VST_WG_PADW) ? (8 - Wo % 8) : 0;
+  if (Cyp > 4 && (s1 || s2) && (Wo + wpad) % 8 == 0 && ov < 0 && math == VST_MATH_BF16X6 && VST_WG_BF) {
     // x6: the split-bf16 weight-gradient kernel (conv_bf.hip), 256x128 tiles for the wide layers
     p.trans = p.bfk = true;
     p.pad = s1 ? pd2 / 2 : -1;
+    p.wpad = wpad;
     const int kind = Cyp > 64 ? (p.Mw >= VST_WG_BIGM ? 7 : 3) : (p.Mw >= 1024 ? 1 : 8);
     p.tile = (TileKind)kind;
     int bm, bn, bk, slots;
     bf_wgrad_geom(kind, math, &bm, &bn, &bk, &slots);
     const int tiles = ceil_div(p.Mw, bm) * ceil_div(Cyp, bn);
-    const int ns = pick_splits(tiles, slots, ceil_div(P, 8 * bk) < 256 ? ceil_div(P, 8 * bk) : 256,
-                               ceil_div(P, WGRAD_CHUNK_MAX));
-    p.chunk = ceil_div(ceil_div(P, ns), bk) * bk;
-    p.nsplit = ceil_div(P, p.chunk);
+    const int Pw = N * Ho * (Wo + wpad);
+    const int ns = pick_splits(tiles, slots, ceil_div(Pw, 8 * bk) < 256 ? ceil_div(Pw, 8 * bk) : 256,
+                               ceil_div(Pw, WGRAD_CHUNK_MAX));
+    p.chunk = ceil_div(ceil_div(Pw, ns), bk) * bk;
+    p.nsplit = ceil_div(Pw, p.chunk);
     const int pmax = s1 ? p.pad : (R > S ? R : S) - 1;
-    p.xt_floats = rk_cp_ld((long)N * (H + 2 * pmax) * (W + 2 * pmax)) * Cx;  // padded fp32 image
-    p.dyt_floats = (rk_cp_ld(P) * Cyp * 3 + 1) / 2;                           // 3 bf16 planes
+    p.xt_floats = rk_cp_ld((long)N * (H + 2 * pmax) * (W + 2 * pmax + wpad)) * Cx;  // padded fp32 image
+    p.dyt_floats = (rk_cp_ld(Pw) * Cyp * 3 + 1) / 2;                                // 3 bf16 planes
     return p;
   }
   if (Cyp > 4 && (s1 || s2) && Wo % 4 == 0 && ov < 8) {
@@ -993,7 +1003,8 @@ extern "C" int vst_conv_plan_wgrad(int N, int H, int W, int Cx, int Ho, int Wo, 
   VST_REQUIRE(path && kind && nsplit && N > 0 && H > 0 && W > 0 && Ho > 0 && Wo > 0 && R > 0 && S > 0,
               "conv_plan_wgrad: bad args");
   const WgradPlan p = plan_wgrad(N, H, W, Ho, Wo, Cx, Cyp, R, S, stride, math);
-  *path = p.bfk ? VST_WPLAN_BF : p.trans ? VST_WPLAN_RK : Cyp == 4 ? VST_WPLAN_SKINNY : VST_WPLAN_GENERIC;
+  *path = p.bfk ? (p.wpad ? VST_WPLAN_BF_PADW : VST_WPLAN_BF) : p.trans ? VST_WPLAN_RK
+                                                                     : Cyp == 4 ? VST_WPLAN_SKINNY : VST_WPLAN_GENERIC;
   *kind = (int)p.tile;
   *nsplit = p.nsplit;
   return VST_OK;
@@ -1053,10 +1064,16 @@ extern "C" int vst_conv2d_wgrad_pre(const float* x, const float* x_t, const floa
     float* xt = ws + (size_t)p.nsplit * p.Mw * Cyp;
     float* dyt = xt + p.xt_floats;
     if (p.bfk) {
-      if (!x_t) rk_nhwc_to_cp_pad(x, xt, N, H, W, Cx, pad, refl, stride == 2, 0, s);  // else: vst_instnorm_act_fwd_cp
-      if (!dy_planes) bf_nhwc_to_planes(dy, dyt, P, Cyp, 3, s);  // else: made by vst_instnorm_act_bwd_planes
-      bf_wgrad_launch(x_t ? x_t : xt, dy_planes ? dy_planes : dyt, ws, N, H, W, Cx, Ho, Wo, Cyp, S, pad, stride, p.Mw, p.chunk,
-                      p.nsplit, (int)p.tile, math, s);
+      if (p.wpad) {  // Wo-padded rows: the producer-made images do not have this layout
+        x_t = nullptr;
+        dy_planes = nullptr;
+      }
+      const int Wo8 = Wo + p.wpad;
+      if (!x_t) rk_nhwc_to_cp_pad(x, xt, N, H, W, Cx, pad, refl, stride == 2, 0, s, p.wpad);  // else: vst_instnorm_act_fwd_cp
+      if (!dy_planes)  // else: made by vst_instnorm_act_bwd_planes
+        bf_nhwc_to_planes(dy, dyt, (long)N * Ho * Wo8, Cyp, 3, s, p.wpad ? Wo : 0, p.wpad ? Wo8 : 0);
+      bf_wgrad_launch(x_t ? x_t : xt, dy_planes ? dy_planes : dyt, ws, N, H, W + p.wpad, Cx, Ho, Wo8, Cyp, S, pad,
+                      stride, p.Mw, p.chunk, p.nsplit, (int)p.tile, math, s);
     } else {
       const int pack = math == VST_MATH_BF16X3;  // the x3 kernel stages pre-split (hi, lo) words
       rk_nhwc_to_cp_pad(x, xt, N, H, W, Cx, pad, refl, stride == 2, pack, s);

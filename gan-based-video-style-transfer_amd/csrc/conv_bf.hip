@@ -931,9 +931,11 @@ __global__ __launch_bounds__(256) void fprop_splitk_reduce_k(const float* __rest
 // NHWC [P][Cs] fp32 -> NP bf16 planes [NP][Cs][ld] (hi, (mid,) lo of each value, the same RNE
 // conversions as split8 / split3_k) through a 64x64 LDS transpose tile: the weight gradient's
 // pre-split B operand.
+// rin / rout (> 0): the plane pixels are rows of rout words holding rin source pixels each, then
+// zeros (the Wo-padded weight gradient); P counts plane pixels.
 template <int NP>
 __global__ __launch_bounds__(256) void nhwc_to_cp_planes_k(const float* __restrict__ x, __bf16* __restrict__ y,
-                                                           long P, int Cs, long ld) {
+                                                           long P, int Cs, long ld, int rin, int rout) {
   __shared__ float tile[64][65];
   const long p0 = (long)blockIdx.x * 64;
   const int c0 = blockIdx.y * 64;
@@ -942,7 +944,15 @@ __global__ __launch_bounds__(256) void nhwc_to_cp_planes_k(const float* __restri
   for (int it = 0; it < 4; ++it) {
     const int idx = t + 256 * it, pr = idx >> 4, c4 = (idx & 15) * 4;
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (p0 + pr < P && c0 + c4 < Cs) v = *reinterpret_cast<const float4*>(x + (p0 + pr) * Cs + c0 + c4);
+    long q = p0 + pr;
+    bool ok = q < P && c0 + c4 < Cs;
+    if (rout > 0) {
+      const long row = q / rout;
+      const int col = (int)(q - row * rout);
+      ok = ok && col < rin;
+      q = row * rin + col;
+    }
+    if (ok) v = *reinterpret_cast<const float4*>(x + q * Cs + c0 + c4);
     tile[pr][c4] = v.x;
     tile[pr][c4 + 1] = v.y;
     tile[pr][c4 + 2] = v.z;
@@ -1240,11 +1250,13 @@ int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* b
 }
 
 
-void bf_nhwc_to_planes(const float* x, void* y, long P, int Cs, int np, hipStream_t s) {
+void bf_nhwc_to_planes(const float* x, void* y, long P, int Cs, int np, hipStream_t s, int row_in, int row_out) {
   const dim3 g((unsigned)((P + 63) / 64), ceil_div(Cs, 64));
   __bf16* yb = reinterpret_cast<__bf16*>(y);
-  if (np == 3) hipLaunchKernelGGL(bf::nhwc_to_cp_planes_k<3>, g, dim3(256), 0, s, x, yb, P, Cs, rk_cp_ld(P));
-  else hipLaunchKernelGGL(bf::nhwc_to_cp_planes_k<2>, g, dim3(256), 0, s, x, yb, P, Cs, rk_cp_ld(P));
+  if (np == 3)
+    hipLaunchKernelGGL(bf::nhwc_to_cp_planes_k<3>, g, dim3(256), 0, s, x, yb, P, Cs, rk_cp_ld(P), row_in, row_out);
+  else
+    hipLaunchKernelGGL(bf::nhwc_to_cp_planes_k<2>, g, dim3(256), 0, s, x, yb, P, Cs, rk_cp_ld(P), row_in, row_out);
 }
 
 void bf_wgrad_launch(const float* xt, const void* dyp, float* slab, int N, int H, int W, int Cx, int Ho,

@@ -733,9 +733,9 @@ __global__ __launch_bounds__(256) void nhwc_to_cp_k(const float* __restrict__ x,
 template <bool PACK>
 __global__ __launch_bounds__(256) void nhwc_to_cp_pad_k(const float* __restrict__ x, float* __restrict__ y,
                                                         int N, int H, int W, int Cs, int pad, int reflect,
-                                                        int phase, long ld) {
+                                                        int phase, long ld, int extra) {
   __shared__ float tile[64][65];
-  const int Hp = H + 2 * pad, Wp = W + 2 * pad;
+  const int Hp = H + 2 * pad, Wp = W + 2 * pad + extra;  // extra: zero columns right of the border
   const long P = (long)N * Hp * Wp;
   const long p0 = (long)blockIdx.x * 64;
   const int c0 = blockIdx.y * 64;
@@ -754,7 +754,7 @@ __global__ __launch_bounds__(256) void nhwc_to_cp_pad_k(const float* __restrict_
         w = w < wh ? 2 * w : 2 * (w - wh) + 1;
       }
       w -= pad;
-      bool ok = true;
+      bool ok = w < W + pad;  // the extra columns stay zero
       if (reflect) {
         h = reflect_idx(h, H);
         w = reflect_idx(w, W);
@@ -791,15 +791,15 @@ __global__ __launch_bounds__(256) void nhwc_to_cp_pad_k(const float* __restrict_
 long rk_cp_ld(long P) { return (P + 63) / 64 * 64 + 64; }
 
 void rk_nhwc_to_cp_pad(const float* x, float* y, int N, int H, int W, int Cs, int pad, int reflect,
-                       int phase, int pack, hipStream_t s) {
-  const long P = (long)N * (H + 2 * pad) * (W + 2 * pad);
+                       int phase, int pack, hipStream_t s, int extra) {
+  const long P = (long)N * (H + 2 * pad) * (W + 2 * pad + extra);
   const dim3 g((unsigned)((P + 63) / 64), ceil_div(Cs, 64));
   if (pack)
     hipLaunchKernelGGL(rk::nhwc_to_cp_pad_k<true>, g, dim3(256), 0, s, x, y, N, H, W, Cs, pad, reflect,
-                       phase, rk_cp_ld(P));
+                       phase, rk_cp_ld(P), extra);
   else
     hipLaunchKernelGGL(rk::nhwc_to_cp_pad_k<false>, g, dim3(256), 0, s, x, y, N, H, W, Cs, pad, reflect,
-                       phase, rk_cp_ld(P));
+                       phase, rk_cp_ld(P), extra);
 }
 
 void rk_nhwc_to_cp(const float* x, float* y, long P, int Cs, int pack, hipStream_t s) {

@@ -337,7 +337,7 @@ TILE_NAMES = {0: "128x128 (8 waves of 64x32)", 1: "128x64", 2: "128x128 (4 waves
 
 
 WPLAN_NAMES = {0: "conv_wgrad_k (NHWC operands)", 1: "copies + conv_wgrad_rk_k", 2: "copies + conv_wgrad_bf_k",
-               3: "skinny VALU"}
+               3: "skinny VALU", 4: "Wo-padded copies + conv_wgrad_bf_k"}
 
 
 def conv_plan_wgrad(N, H, W, Cx, Ho, Wo, Cyp, R, S, stride, math):

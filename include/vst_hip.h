@@ -208,7 +208,7 @@ int vst_conv_plan_fwd(int N, int H, int W, int Cx, int Cop, int R, int S, int st
  * split-bf16 kernel conv_wgrad_bf_k), _RK (copies + conv_wgrad_rk_k), _GENERIC (conv_wgrad_k on the
  * NHWC operands) or _SKINNY (<= 4 output channels, VALU); *kind = its tile kind; *nsplit = split-K
  * slabs (reduced by slab_group_sum_k + wgrad_reduce_store_k). */
-enum { VST_WPLAN_GENERIC = 0, VST_WPLAN_RK = 1, VST_WPLAN_BF = 2, VST_WPLAN_SKINNY = 3 };
+enum { VST_WPLAN_GENERIC = 0, VST_WPLAN_RK = 1, VST_WPLAN_BF = 2, VST_WPLAN_SKINNY = 3, VST_WPLAN_BF_PADW = 4 };
 int vst_conv_plan_wgrad(int N, int H, int W, int Cx, int Ho, int Wo, int Cyp, int R, int S, int stride,
                         int math, int* path, int* kind, int* nsplit);
 /* db[c] (+)= sum over NHW pixels of x[p][c] for c < Cl (channel stride Cs); bias gradient of a layer

@@ -595,3 +595,26 @@ def test_splitk_tail_vs_small_tiles_and_torch(ops, N, pad):
         _close(_nchw(y, C, ops), yr, tol=CONV_TOL["bf16x6"], what="split-K vs torch fp32")
     finally:
         ops.set_conv_math(prev)
+
+
+@pytest.mark.parametrize("N,H,Ci,Co,k,pad,mode", [(2, 32, 64, 128, 4, 1, "zero"), (2, 30, 64, 96, 3, 1, "reflect"),
+                                                  (3, 21, 32, 72, 3, 1, "zero")])
+def test_wgrad_wo_padded_rows(ops, N, H, Ci, Co, k, pad, mode):
+    """x6 weight gradients of stride-1 convs whose output width is not a multiple of 8 (PatchGAN's
+    31-wide layer) on the split-bf16 kernel via Wo-padded rows (VST_WPLAN_BF_PADW) vs torch fp32."""
+    prev = ops.set_conv_math("bf16x6")
+    try:
+        Ho = H + 2 * pad - k + 1
+        assert Ho % 8
+        assert ops.conv_plan_wgrad(N, H, H, Ci, Ho, Ho, Co, k, k, 1, "bf16x6")[0] == 4
+        x = _g(31, (N, Ci, H, H))
+        gy = _g(32, (N, Co, Ho, Ho))
+        w = _g(33, (Co, Ci, k, k), 0.05).requires_grad_(True)
+        xp = F.pad(x, (pad,) * 4, mode="reflect") if mode == "reflect" else F.pad(x, (pad,) * 4)
+        F.conv2d(xp, w).backward(gy)
+        dw = torch.zeros(Co, Ci, k, k, device=DEV)
+        ops.conv2d_wgrad(_nhwc(x, ops), _nhwc(gy, ops), dw, None, k, k, 1, pad, mode, Co, Ci, Ci * k * k, k * k,
+                         accumulate=False)
+        _close(dw.cpu(), w.grad, tol=CONV_TOL["bf16x6"], what="Wo-padded wgrad")
+    finally:
+        ops.set_conv_math(prev)

@@ -941,6 +941,18 @@ def loss_masked_l1_bwd(a, b, mask, gout, scale, cl):
 
 
 # ----------------------------------------------------------------------- tap-GEMM convolutions
+# VST_TAP_CHUNK_MB > 0 runs the tap GEMMs' R*R*4-wide intermediates (411 MB for 8 images at 256^2,
+# 7x7) in chunks of images sized for the 256 MB Infinity Cache, each chunk overwriting one buffer.
+# Off by default: the C2 step A/B measured 63.15-63.27 ms with 128 MB chunks, 64.12 with 64 MB,
+# 62.85-62.87 in one pass (the smaller GEMM launches lose more than the cache hits save).
+TAP_CHUNK_BYTES = int(float(os.environ.get("VST_TAP_CHUNK_MB", "0")) * (1 << 20))
+
+
+def _tap_chunks(N, per_image_bytes):
+    n = N if TAP_CHUNK_BYTES <= 0 else max(1, min(N, TAP_CHUNK_BYTES // max(1, per_image_bytes)))
+    return [(i, min(N, i + n)) for i in range(0, N, n)]
+
+
 def tap_conv_fwd(x, ck, bias, R, pad, pad_mode="zero", act="none", slope=0.0, role="fwd"):
     """'same' conv with <= 4 output channels on the MFMA kernel (see vst_tapsum_fwd): ck is the
     VST_PACK_CK pack [R][S][4][Ci] of the weight, bias padded to 4 (or None); returns NHWC4."""
@@ -948,10 +960,13 @@ def tap_conv_fwd(x, ck, bias, R, pad, pad_mode="zero", act="none", slope=0.0, ro
     N, H, W, Cx = x.shape
     if ck.shape != (R, R, 4, Cx):
         raise ValueError("tap_conv_fwd: CK pack shape %s does not match R=%d, Cx=%d" % (tuple(ck.shape), R, Cx))
-    z = conv2d_fwd(x, ck, None, R * R * 4, 1, 1, 1, 0, "zero", role=role)
     y = torch.empty((N, H, W, 4), device=x.device)
-    _call("vst_tapsum_fwd", _p(z), R * R * 4, _p(bias), _p(y), N, H, W, R, R, pad, PAD[pad_mode], ACT[act],
-          float(slope), _stream())
+    chunks = _tap_chunks(N, H * W * R * R * 16)
+    zbuf = torch.empty((chunks[0][1], H, W, R * R * 4), device=x.device)
+    for a, b in chunks:
+        z = conv2d_fwd(x[a:b], ck, None, R * R * 4, 1, 1, 1, 0, "zero", role=role, out=zbuf[:b - a])
+        _call("vst_tapsum_fwd", _p(z), R * R * 4, _p(bias), _p(y[a:b]), b - a, H, W, R, R, pad, PAD[pad_mode],
+              ACT[act], float(slope), _stream())
     return y
 
 
@@ -960,10 +975,13 @@ def tap_conv_wgrad(x, dy, dw, R, pad, pad_mode="zero", accumulate=True, role="bw
     _dev_check(x, dy, dw)
     N, H, W, Cx = x.shape
     Co, Ci = dw.shape[0], dw.shape[1]
-    d = torch.empty((N, H, W, R * R * 4), device=x.device)
-    _call("vst_tapfold", _p(dy), _p(d), N, H, W, R, R, pad, PAD[pad_mode], _stream())
+    chunks = _tap_chunks(N, H * W * R * R * 16)
+    dbuf = torch.empty((chunks[0][1], H, W, R * R * 4), device=x.device)
     t = torch.empty((R * R * 4, Ci), device=x.device)
-    conv2d_wgrad(x, d, t, None, 1, 1, 1, 0, "zero", R * R * 4, Ci, Ci, 1, accumulate=False, role=role)
+    for a, b in chunks:
+        d = dbuf[:b - a]
+        _call("vst_tapfold", _p(dy[a:b]), _p(d), b - a, H, W, R, R, pad, PAD[pad_mode], _stream())
+        conv2d_wgrad(x[a:b], d, t, None, 1, 1, 1, 0, "zero", R * R * 4, Ci, Ci, 1, accumulate=a > 0, role=role)
     _call("vst_tap_wgrad_scatter", _p(t), _p(dw), Co, Ci, R, R, 1 if accumulate else 0, _stream())
 
 
@@ -974,9 +992,12 @@ def tap_conv_dgrad(dy, kc, R, pad, pad_mode="zero", role="bwd"):
     N, H, W, Cy = dy.shape
     if kc.shape != (R, R, 4, Cy):
         raise ValueError("tap_conv_dgrad: KC pack shape %s does not match R=%d, Cy=%d" % (tuple(kc.shape), R, Cy))
-    z = conv2d_fwd(dy, kc, None, R * R * 4, 1, 1, 1, 0, "zero", role=role)
     y = torch.empty((N, H, W, 4), device=dy.device)
-    _call("vst_tapgather", _p(z), _p(y), N, H, W, R, R, pad, PAD[pad_mode], _stream())
+    chunks = _tap_chunks(N, H * W * R * R * 16)
+    zbuf = torch.empty((chunks[0][1], H, W, R * R * 4), device=dy.device)
+    for a, b in chunks:
+        z = conv2d_fwd(dy[a:b], kc, None, R * R * 4, 1, 1, 1, 0, "zero", role=role, out=zbuf[:b - a])
+        _call("vst_tapgather", _p(z), _p(y[a:b]), b - a, H, W, R, R, pad, PAD[pad_mode], _stream())
     return y
 
 

@@ -618,3 +618,28 @@ def test_wgrad_wo_padded_rows(ops, N, H, Ci, Co, k, pad, mode):
         _close(dw.cpu(), w.grad, tol=CONV_TOL["bf16x6"], what="Wo-padded wgrad")
     finally:
         ops.set_conv_math(prev)
+
+
+def test_tap_conv_image_chunks(ops):
+    """The tap-GEMM convs run in image chunks sized for the Infinity Cache (ops.TAP_CHUNK_BYTES):
+    forward and data gradient bit-identical to one pass over the batch, weight gradient within the
+    split-K summation-order tolerance."""
+    N, H, Ci = 5, 24, 64
+    x = _g(41, (N, H, H, Ci)).to(DEV)
+    w = _g(42, (3, Ci, 7, 7), 0.05).to(DEV)
+    dy4 = _g(43, (N, H, H, 4)).to(DEV)
+    ck = ops.weight_pack(w, ops.PACK_CK)
+    prev = ops.TAP_CHUNK_BYTES
+    try:
+        ops.TAP_CHUNK_BYTES = 0
+        y0 = ops.tap_conv_fwd(x, ck, None, 7, 3, "reflect")
+        dw0 = torch.zeros(3, Ci, 7, 7, device=DEV)
+        ops.tap_conv_wgrad(x, dy4, dw0, 7, 3, "reflect", accumulate=False)
+        ops.TAP_CHUNK_BYTES = 2 * H * H * 49 * 16  # two images per chunk: 3 chunks
+        y1 = ops.tap_conv_fwd(x, ck, None, 7, 3, "reflect")
+        dw1 = torch.zeros(3, Ci, 7, 7, device=DEV)
+        ops.tap_conv_wgrad(x, dy4, dw1, 7, 3, "reflect", accumulate=False)
+    finally:
+        ops.TAP_CHUNK_BYTES = prev
+    assert torch.equal(y0, y1)
+    _close(dw1, dw0, tol=2e-6, what="chunked tap wgrad")

@@ -307,15 +307,6 @@ __global__ void in_bwd_finalize_k(const double* __restrict__ part, const float* 
   dbn[idx] = rstd * ((a[0] - HW * mg) - mgx * a[2]);
 }
 
-// db[c] (+)= sum_n dbn[n][c] in a fixed order (conv-bias gradient)
-__global__ void in_bias_grad_k(const double* __restrict__ dbn, float* __restrict__ db, int N, int C,
-                               int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s = 0.0;
-  for (int n = 0; n < N; ++n) s += dbn[(long)n * C + c];
-  db[c] = accumulate ? db[c] + (float)s : (float)s;
-}
 
 __global__ void in_apply_k(const float4* __restrict__ x, const float* __restrict__ stats,
                            const float4* __restrict__ res, float4* __restrict__ y, long total4,
@@ -415,10 +406,23 @@ __device__ __forceinline__ float in_bwd1(float gy, float x, float mean, float rs
   return rstd * (gy * d - k.x - xh * k.y);
 }
 
+// db[c] (+)= sum_n dbn[n][c] in a fixed order (the conv-bias gradient), by the first blocks of the
+// apply pass that follows in_bwd_finalize_k (replaces a launch of its own)
+__device__ __forceinline__ void in_bias_grad_blocks(const double* __restrict__ dbn, float* __restrict__ db, int N,
+                                                    int C, int accumulate, int c) {
+  if (c >= C) return;
+  double s = 0.0;
+  for (int n = 0; n < N; ++n) s += dbn[(long)n * C + c];
+  db[c] = accumulate ? db[c] + (float)s : (float)s;
+}
+
 __global__ void in_bwd_apply_k(const float4* __restrict__ gy, const float4* __restrict__ x,
                                const float* __restrict__ stats, const float2* __restrict__ coef,
                                float4* __restrict__ dx, long total4, int HW, int C4, int act,
-                               float slope) {
+                               float slope, const double* __restrict__ dbn, float* __restrict__ db, int N,
+                               int accumulate_db) {
+  if (db && blockIdx.x * blockDim.x < 4 * C4)
+    in_bias_grad_blocks(dbn, db, N, 4 * C4, accumulate_db, blockIdx.x * blockDim.x + threadIdx.x);
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total4) return;
   const int c4 = i % C4;
@@ -453,11 +457,14 @@ __global__ __launch_bounds__(256) void in_bwd_apply_planes_k(const float* __rest
                                                               const float* __restrict__ stats,
                                                               const float2* __restrict__ coef, float* __restrict__ dx,
                                                               __bf16* __restrict__ planes, long P, int HW, int C,
-                                                              long ldp, int act, float slope) {
+                                                              long ldp, int act, float slope,
+                                                              const double* __restrict__ dbn, float* __restrict__ db,
+                                                              int N, int accumulate_db) {
   __shared__ float tile[64][65];
   const long p0 = (long)blockIdx.x * 64;
   const int c0 = blockIdx.y * 64;
   const int t = threadIdx.x;
+  if (db && blockIdx.x == 0 && t < 64) in_bias_grad_blocks(dbn, db, N, C, accumulate_db, c0 + t);
 #pragma unroll
   for (int it = 0; it < 4; ++it) {
     const int idx = t + 256 * it, pr = idx >> 4, c4 = (idx & 15) * 4;
@@ -890,19 +897,20 @@ static int in_bwd_tail(const float* gy, const float* x, const float* stats, floa
   double* dbn = reinterpret_cast<double*>(reinterpret_cast<char*>(coef) + (size_t)N * C * sizeof(float2));
   hipLaunchKernelGGL(in_bwd_finalize_k, dim3(ceil_div(C, 64), N), dim3(256), 0, s, part, stats, coef, dbn,
                      N, HW, C, g.nsplit);
-  if (db)
-    hipLaunchKernelGGL(in_bias_grad_k, dim3(ceil_div(C, 256)), dim3(256), 0, s, dbn, db, N, C,
-                       accumulate_db);
+  // the bias gradient (sum over n of dbn) is taken by the apply pass's first blocks
   if (planes) {
     const long P = (long)N * HW;
     hipLaunchKernelGGL(in_bwd_apply_planes_k, dim3(ceil_div(P, 64), ceil_div(C, 64)), dim3(256), 0, s, gy, x, stats,
-                       coef, dx, reinterpret_cast<__bf16*>(planes), P, HW, C, ldp, act, slope);
+                       coef, dx, reinterpret_cast<__bf16*>(planes), P, HW, C, ldp, act, slope, dbn, db, N,
+                       accumulate_db);
     return check_launch("instnorm_act_bwd_planes");
   }
   const long total4 = (long)N * HW * C / 4;
+  VST_REQUIRE(!db || total4 >= C, "instnorm_act_bwd: fewer elements than channels");
   hipLaunchKernelGGL(in_bwd_apply_k, dim3(ceil_div(total4, 256)), dim3(256), 0, s,
                      reinterpret_cast<const float4*>(gy), reinterpret_cast<const float4*>(x), stats,
-                     coef, reinterpret_cast<float4*>(dx), total4, HW, C / 4, act, slope);
+                     coef, reinterpret_cast<float4*>(dx), total4, HW, C / 4, act, slope, dbn, db, N,
+                     accumulate_db);
   return check_launch("instnorm_act_bwd");
 }
 

@@ -95,6 +95,59 @@ __global__ void tapfold_k(const float4* __restrict__ g, float4* __restrict__ d, 
   d[i] = acc;
 }
 
+// tapfold_k writing D straight as the x6 weight gradient's B operand: three bf16 planes
+// [3][R*S*4][ldp] (hi, mid, lo; RNE splits as vst_weight_split), channel-major over the P pixels, so
+// the fp32 D (N*H*W*R*S*16 bytes) and its plane copy are never materialised.  grid (ceil(P / 256),
+// R*S): a thread owns one pixel q and one tap (r, s), i.e. the 4 channels (r, s, 0..3).
+__device__ __forceinline__ uint32_t tap_bf16x2(float a, float b) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  typedef __bf16 b2 __attribute__((ext_vector_type(2)));
+  const f2 v = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, b2));
+}
+
+__global__ __launch_bounds__(256) void tapfold_planes_k(const float4* __restrict__ g, uint16_t* __restrict__ planes,
+                                                        int H, int W, int R, int S, int pad, int reflect, long P,
+                                                        long ldp) {
+  const long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= P) return;
+  const int rs = blockIdx.y;
+  const int qw = q % W;
+  const long t = q / W;
+  const int qh = t % H;
+  const long n = t / H;
+  const int r = rs / S, s = rs - r * S;
+  int ph[3], pw[3];
+  const int mh = preimages(qh, r, pad, H, reflect, ph);
+  const int mw = preimages(qw, s, pad, W, reflect, pw);
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int a = 0; a < mh; ++a)
+    for (int b = 0; b < mw; ++b) {
+      const float4 v = g[(n * H + ph[a]) * (long)W + pw[b]];
+      acc.x += v.x;
+      acc.y += v.y;
+      acc.z += v.z;
+      acc.w += v.w;
+    }
+  float v[4] = {acc.x, acc.y, acc.z, acc.w};
+  const long plane = (long)R * S * 4 * ldp;
+  uint16_t* dst = planes + (long)rs * 4 * ldp + q;
+#pragma unroll
+  for (int pl = 0; pl < 3; ++pl) {
+    const uint32_t q0 = tap_bf16x2(v[0], v[1]), q1 = tap_bf16x2(v[2], v[3]);
+    dst[pl * plane] = (uint16_t)q0;
+    dst[pl * plane + ldp] = (uint16_t)(q0 >> 16);
+    dst[pl * plane + 2 * ldp] = (uint16_t)q1;
+    dst[pl * plane + 3 * ldp] = (uint16_t)(q1 >> 16);
+    if (pl < 2) {
+      v[0] -= __uint_as_float(q0 << 16);
+      v[1] -= __uint_as_float(q0 & 0xffff0000u);
+      v[2] -= __uint_as_float(q1 << 16);
+      v[3] -= __uint_as_float(q1 & 0xffff0000u);
+    }
+  }
+}
+
 // Row-segment form of tapsum: a 64-lane block owns 64 consecutive output pixels of one row; for
 // each filter row r it stages the S taps of that row for the 64 + S - 1 source pixels in LDS
 // (each pixel's S float4 are contiguous in Z), then every lane sums its S taps from LDS.  Every Z
@@ -294,6 +347,17 @@ extern "C" int vst_tapfold(const float* g, float* d, int N, int H, int W, int R,
                      reinterpret_cast<const float4*>(g), reinterpret_cast<float4*>(d), H, W, R, S, pad,
                      pad_mode == VST_PAD_REFLECT, total);
   return check_launch("tapfold");
+}
+
+extern "C" int vst_tapfold_planes(const float* g, void* planes, long ldp, int N, int H, int W, int R, int S, int pad,
+                                  int pad_mode, void* stream) {
+  const long P = (long)N * H * W;
+  VST_REQUIRE(g && planes && N > 0 && H > 0 && W > 0 && R > 0 && S > 0 && pad >= 0 && ldp >= P,
+              "tapfold_planes: bad args");
+  hipLaunchKernelGGL(tapfold_planes_k, dim3(ceil_div(P, 256), R * S), dim3(256), 0, (hipStream_t)stream,
+                     reinterpret_cast<const float4*>(g), reinterpret_cast<uint16_t*>(planes), H, W, R, S, pad,
+                     pad_mode == VST_PAD_REFLECT, P, ldp);
+  return check_launch("tapfold_planes");
 }
 
 extern "C" int vst_tap_wgrad_scatter(const float* t, float* dw, int Co, int Ci, int R, int S, int accumulate,

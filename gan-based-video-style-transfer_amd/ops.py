@@ -946,6 +946,9 @@ def loss_masked_l1_bwd(a, b, mask, gout, scale, cl):
 # Off by default: the C2 step A/B measured 63.15-63.27 ms with 128 MB chunks, 64.12 with 64 MB,
 # 62.85-62.87 in one pass (the smaller GEMM launches lose more than the cache hits save).
 TAP_CHUNK_BYTES = int(float(os.environ.get("VST_TAP_CHUNK_MB", "0")) * (1 << 20))
+# tap_conv_wgrad: the folded dy written as the x6 wgrad's bf16 planes (vst_tapfold_planes);
+# VST_TAP_PLANES=0 writes the fp32 D and lets the wgrad copy it into planes.
+TAP_PLANES = os.environ.get("VST_TAP_PLANES", "1") != "0"
 
 
 def _tap_chunks(N, per_image_bytes):
@@ -975,6 +978,20 @@ def tap_conv_wgrad(x, dy, dw, R, pad, pad_mode="zero", accumulate=True, role="bw
     _dev_check(x, dy, dw)
     N, H, W, Cx = x.shape
     Co, Ci = dw.shape[0], dw.shape[1]
+    K = R * R * 4
+    if TAP_PLANES and TAP_CHUNK_BYTES <= 0 and conv_plan_wgrad(N, H, W, Cx, H, W, K, 1, 1, 1, role)[0] == 2:
+        # D straight as the x6 wgrad's bf16 planes (vst_tapfold_planes): no fp32 D, no plane copy
+        P = N * H * W
+        ldp = lib().vst_cp_ld(P)
+        pl = torch.empty((3, K, ldp), device=x.device, dtype=torch.bfloat16)
+        _call("vst_tapfold_planes", _p(dy), _p(pl), ldp, N, H, W, R, R, pad, PAD[pad_mode], _stream())
+        t = torch.empty((K, Ci), device=x.device)
+        nbytes = lib().vst_conv2d_wgrad_ws_bytes(N, H, W, Cx, H, W, K, 1, 1, 1)
+        ws = torch.empty((nbytes + 3) // 4, device=x.device)
+        _call("vst_conv2d_wgrad_pre", _p(x), None, _p(pl), _p(pl), _p(t), _p(ws), nbytes, N, H, W, Cx, H, W, K, 1, 1, 1,
+              0, PAD["zero"], K, Ci, Ci, 1, 0, _math(role), _stream())
+        _call("vst_tap_wgrad_scatter", _p(t), _p(dw), Co, Ci, R, R, 1 if accumulate else 0, _stream())
+        return
     chunks = _tap_chunks(N, H * W * R * R * 16)
     dbuf = torch.empty((chunks[0][1], H, W, R * R * 4), device=x.device)
     t = torch.empty((R * R * 4, Ci), device=x.device)

@@ -397,6 +397,10 @@ int vst_tapsum_fwd(const float* z, int zcs, const float* bias, float* y, int N, 
  * (g NHWC4); then vst_conv2d_wgrad(x, d) as a 1x1 wgrad gives t[(r*S+s)*4 + co][ci], and
  * vst_tap_wgrad_scatter writes dw[co][ci][r][s] (+)= t (co < Co <= 4). */
 int vst_tapfold(const float* g, float* d, int N, int H, int W, int R, int S, int pad, int pad_mode, void* stream);
+/* vst_tapfold writing D as the three bf16 planes [3][R*S*4][ldp] (ldp >= N*H*W, vst_cp_ld) the x6
+ * weight gradient takes as its dy image (vst_conv2d_wgrad_pre): no fp32 D, no plane copy. */
+int vst_tapfold_planes(const float* g, void* planes, long ldp, int N, int H, int W, int R, int S, int pad,
+                       int pad_mode, void* stream);
 int vst_tap_wgrad_scatter(const float* t, float* dw, int Co, int Ci, int R, int S, int accumulate, void* stream);
 /* Data gradient of a 'same' conv with <= 4 INPUT channels (the generators' first layer, c7s1-64 on
  * the image): z = vst_conv2d_fwd(dy, VST_PACK_KC pack seen as a 1x1 conv with R*S*4 outputs), then

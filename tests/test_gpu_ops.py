@@ -643,3 +643,25 @@ def test_tap_conv_image_chunks(ops):
         ops.TAP_CHUNK_BYTES = prev
     assert torch.equal(y0, y1)
     _close(dw1, dw0, tol=2e-6, what="chunked tap wgrad")
+
+
+@pytest.mark.parametrize("mode", ["reflect", "zero"])
+def test_tapfold_planes_exact(ops, mode):
+    """tap_conv_wgrad with the folded dy written as bf16 planes (vst_tapfold_planes) == the fp32 D +
+    plane-copy path, bit for bit (same sums, same RNE splits), under bf16x6."""
+    prev_m = ops.set_conv_math("bf16x6")
+    prev = ops.TAP_PLANES
+    try:
+        N, H, Ci = 3, 20, 64
+        x = _g(61, (N, H, H, Ci)).to(DEV)
+        dy4 = _g(62, (N, H, H, 4)).to(DEV)
+        out = []
+        for flag in (False, True):
+            ops.TAP_PLANES = flag
+            dw = _g(63, (3, Ci, 7, 7)).to(DEV)
+            ops.tap_conv_wgrad(x, dy4, dw, 7, 3, mode, accumulate=True)
+            out.append(dw)
+        assert torch.equal(out[0], out[1])
+    finally:
+        ops.TAP_PLANES = prev
+        ops.set_conv_math(prev_m)

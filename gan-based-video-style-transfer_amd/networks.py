@@ -525,7 +525,13 @@ class _GeneratorFn(torch.autograd.Function):
             else:
                 y = ops.conv2d_tfwd(a, ck, b, 2 * Hi, 2 * Wi, cpad(cout), 3, 3, 2, 1, role=role)
             s = ops.instnorm_stats(y)
-            an = ops.instnorm_act_fwd(y, s, "relu")
+            cp = None
+            if i == 1 and "ftap" in P and train_w and IN_XT:  # the tap wgrad's (1x1, pad 0) x image
+                N_, H_, W_, C_ = y.shape
+                if _wgrad_on_bf(N_, H_, W_, C_, H_, W_, 4 * 49, 1, 1, ops.get_conv_math()):
+                    cp = (0, "zero", 1)
+            an, at = in_act(y, s, "relu", cp)
+            sv["xt"][id(an)] = at
             sv[f"u{i}"] = (a, y, s, an)
             a = an
         kc, _, b = P["f"]
@@ -592,7 +598,7 @@ class _GeneratorFn(torch.autograd.Function):
         g = ops.act_bwd(gout, out, "tanh")
         if "ftap" in P:
             if train_w:
-                ops.tap_conv_wgrad(a, g, f.weight.grad, 7, 3, "reflect", accumulate=True)
+                ops.tap_conv_wgrad(a, g, f.weight.grad, 7, 3, "reflect", accumulate=True, x_t=xts.get(id(a)))
                 if f.bias is not None:
                     ops.channel_sum(g, f.bias.grad, f.weight.shape[0], accumulate=True)
         else:

@@ -973,8 +973,9 @@ def tap_conv_fwd(x, ck, bias, R, pad, pad_mode="zero", act="none", slope=0.0, ro
     return y
 
 
-def tap_conv_wgrad(x, dy, dw, R, pad, pad_mode="zero", accumulate=True, role="bwd"):
-    """dw [Co<=4][Ci][R][R] (+)= weight gradient of tap_conv_fwd given dy NHWC4 (pre-activation)."""
+def tap_conv_wgrad(x, dy, dw, R, pad, pad_mode="zero", accumulate=True, role="bwd", x_t=None):
+    """dw [Co<=4][Ci][R][R] (+)= weight gradient of tap_conv_fwd given dy NHWC4 (pre-activation).
+    x_t: x's unpadded channel-major image (instnorm_act_fwd(cp=(0, "zero", 1))) for the x6 path."""
     _dev_check(x, dy, dw)
     N, H, W, Cx = x.shape
     Co, Ci = dw.shape[0], dw.shape[1]
@@ -988,7 +989,7 @@ def tap_conv_wgrad(x, dy, dw, R, pad, pad_mode="zero", accumulate=True, role="bw
         t = torch.empty((K, Ci), device=x.device)
         nbytes = lib().vst_conv2d_wgrad_ws_bytes(N, H, W, Cx, H, W, K, 1, 1, 1)
         ws = torch.empty((nbytes + 3) // 4, device=x.device)
-        _call("vst_conv2d_wgrad_pre", _p(x), None, _p(pl), _p(pl), _p(t), _p(ws), nbytes, N, H, W, Cx, H, W, K, 1, 1, 1,
+        _call("vst_conv2d_wgrad_pre", _p(x), _p(x_t), _p(pl), _p(pl), _p(t), _p(ws), nbytes, N, H, W, Cx, H, W, K, 1, 1, 1,
               0, PAD["zero"], K, Ci, Ci, 1, 0, _math(role), _stream())
         _call("vst_tap_wgrad_scatter", _p(t), _p(dw), Co, Ci, R, R, 1 if accumulate else 0, _stream())
         return

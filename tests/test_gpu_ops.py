@@ -665,3 +665,22 @@ def test_tapfold_planes_exact(ops, mode):
     finally:
         ops.TAP_PLANES = prev
         ops.set_conv_math(prev_m)
+
+
+def test_tap_wgrad_with_forward_x_image(ops):
+    """tap_conv_wgrad reading x's channel-major image written by the forward IN apply
+    (instnorm_act_fwd(cp=(0, 'zero', 1))) == making that copy itself (bit-identical)."""
+    prev_m = ops.set_conv_math("bf16x6")
+    try:
+        N, H, Ci = 2, 24, 64
+        y = _g(71, (N, H, H, Ci)).to(DEV)
+        s = ops.instnorm_stats(y)
+        a, at = ops.instnorm_act_fwd(y, s, "relu", cp=(0, "zero", 1))
+        dy4 = _g(72, (N, H, H, 4)).to(DEV)
+        dw0 = torch.zeros(3, Ci, 7, 7, device=DEV)
+        dw1 = torch.zeros(3, Ci, 7, 7, device=DEV)
+        ops.tap_conv_wgrad(a, dy4, dw0, 7, 3, "reflect")
+        ops.tap_conv_wgrad(a, dy4, dw1, 7, 3, "reflect", x_t=at)
+        assert torch.equal(dw0, dw1)
+    finally:
+        ops.set_conv_math(prev_m)

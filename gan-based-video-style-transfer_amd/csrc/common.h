@@ -86,7 +86,7 @@ inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
 int skinny_out_launch(int mode, const float* in, const float* wp, const float* bias,
                       const float* addend, float* out, int N, int Hi, int Wi, int Cin, int Ho,
                       int Wo, int R, int S, int st, int pad, int reflect, int act, float slope,
-                      hipStream_t s);
+                      hipStream_t s, int co_real = 4);
 // [row][k]-LDS implicit-GEMM fprop / transposed conv (conv_rk.hip); kind = tile override or -1
 // (padh, padw: zero/reflect padding rows / columns — the forward kernels take them separately)
 void rk_fprop_launch(const float* x, const float* wp, const float* bias, float* y, int N, int H, int W,

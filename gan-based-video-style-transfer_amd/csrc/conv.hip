@@ -866,7 +866,7 @@ extern "C" int vst_conv_plan_fwd(int N, int H, int W, int Cx, int Cop, int R, in
 static int conv_fwd_impl(const float* x, const float* wp, const void* wsplit, const float* bias, float* y,
                          int N, int H, int W, int Cx, int Cop, int R, int S, int stride, int padh, int padw,
                          int pad_mode, int act, float slope, int math, hipStream_t s, double* part = nullptr,
-                         int* nsplit = nullptr, float* tws = nullptr, size_t tws_bytes = 0) {
+                         int* nsplit = nullptr, float* tws = nullptr, size_t tws_bytes = 0, int co_real = 4) {
   if (nsplit) *nsplit = 0;
   VST_REQUIRE(x && wp && y, "conv2d_fwd: null pointer");
   VST_REQUIRE(math >= VST_MATH_F32 && math <= VST_MATH_BF16X6, "conv2d_fwd: bad math %d", math);
@@ -880,7 +880,7 @@ static int conv_fwd_impl(const float* x, const float* wp, const void* wsplit, co
   if (Cop == 4) {  // image-channel outputs / PatchGAN head: VALU path (skinny.hip)
     VST_REQUIRE(padh == padw, "conv2d_fwd: the 4-channel-output path needs equal row/column padding");
     return skinny_out_launch(0, x, wp, bias, nullptr, y, N, H, W, Cx, Ho, Wo, R, S, stride, padh, refl,
-                             act, slope, s);
+                             act, slope, s, co_real);
   }
   if (math != VST_MATH_F32 && wsplit && Cx % 8 == 0) {
     // InstanceNorm partials from the epilogue: 32-pixel groups, so the image size must divide
@@ -902,6 +902,14 @@ extern "C" int vst_conv2d_fwd(const float* x, const float* wp, const void* wspli
                               int pad_mode, int act, float slope, int math, void* stream) {
   return conv_fwd_impl(x, wp, wsplit, bias, y, N, H, W, Cx, Cop, R, S, stride, pad, pad, pad_mode, act, slope,
                        math, (hipStream_t)stream);
+}
+
+extern "C" int vst_conv2d_fwd_co(const float* x, const float* wp, const void* wsplit, const float* bias, float* y,
+                                 int N, int H, int W, int Cx, int Cop, int R, int S, int stride, int pad, int pad_mode,
+                                 int act, float slope, int math, int co_real, void* stream) {
+  VST_REQUIRE(co_real >= 1 && co_real <= Cop, "conv2d_fwd_co: bad real channel count %d", co_real);
+  return conv_fwd_impl(x, wp, wsplit, bias, y, N, H, W, Cx, Cop, R, S, stride, pad, pad, pad_mode, act, slope,
+                       math, (hipStream_t)stream, nullptr, nullptr, nullptr, 0, co_real);
 }
 
 extern "C" int vst_conv2d_fwd_in(const float* x, const float* wp, const void* wsplit, const float* bias,

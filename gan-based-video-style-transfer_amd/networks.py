@@ -435,6 +435,9 @@ IN_XT = os.environ.get("VST_IN_XT", "1") != "0"
 # but its per-thread fp64 reduction chains run on the fold's (nsplit x N)-block geometry, slower
 # than the elementwise fold + separate partials (C2 step A/B: 65.43 vs 65.24 ms; planes-only 64.80).
 FOLD_IN = os.environ.get("VST_FOLD_IN", "0") == "1"
+# The discriminator head (1 real output channel of 4) runs the one-channel skinny forward
+# (ops.conv2d_fwd(co_real=1)); VST_D_CO1=0 keeps the 4-channel sums.
+D_CO1 = os.environ.get("VST_D_CO1", "1") != "0"
 _WPLAN_BF = 2  # ops.WPLAN_NAMES: copies + conv_wgrad_bf_k
 
 
@@ -764,7 +767,7 @@ class _DiscriminatorFn(torch.autograd.Function):
             else:
                 act = "none" if last else "lrelu"
                 an = ops.conv2d_fwd(a, kc, b, cpad(cout), 4, 4, st, 1, "zero", act=act, slope=SLOPE,
-                                     role=role)
+                                     role=role, co_real=cout if D_CO1 else None)
                 saved.append((a, None, None, an))
             a = an
         ctx.saved, ctx.net, ctx.P = saved, net, P

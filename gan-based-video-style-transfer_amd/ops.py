@@ -208,8 +208,17 @@ def _fwd_ws(N, H, W, Cx, cop, R, S, stride, pad, m, device):
 
 
 def conv2d_fwd(x, wp, bias, cop, R, S, stride, pad, pad_mode="zero", act="none", slope=0.0,
-               out=None, role="fwd"):
+               out=None, role="fwd", co_real=None):
+    """co_real: the real output channels when cop pads them (vst_conv2d_fwd_co)."""
     _dev_check(x, wp, bias)
+    if co_real is not None and co_real < cop:
+        N, H, W, Cx = x.shape
+        Ho = (H + 2 * pad - R) // stride + 1
+        Wo = (W + 2 * pad - S) // stride + 1
+        y = out if out is not None else torch.empty((N, Ho, Wo, cop), device=x.device)
+        _call("vst_conv2d_fwd_co", _p(x), _p(wp), _p(getattr(wp, "vst_split", None)), _p(bias), _p(y), N, H, W, Cx,
+              cop, R, S, stride, pad, PAD[pad_mode], ACT[act], float(slope), _math(role), int(co_real), _stream())
+        return y
     N, H, W, Cx = x.shape
     Ho = (H + 2 * pad - R) // stride + 1
     Wo = (W + 2 * pad - S) // stride + 1

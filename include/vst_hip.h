@@ -136,6 +136,12 @@ int vst_conv2d_fwd_ws(const float* x, const float* wp, const void* wsplit, const
  * the whole conv, run as one split-K launch + the reduction. */
 int vst_conv_plan_fwd_tail(int N, int H, int W, int Cx, int Cop, int R, int S, int stride, int pad, int math,
                            int* ksplit);
+/* vst_conv2d_fwd for a weight whose output channels co_real..Cop-1 are padding (zero weight rows,
+ * zero bias): the 4-output-channel path (Cop == 4) then computes only the real ones (PatchGAN head:
+ * co_real = 1); the padded channels come out as act(0), as from vst_conv2d_fwd. */
+int vst_conv2d_fwd_co(const float* x, const float* wp, const void* wsplit, const float* bias, float* y, int N, int H,
+                      int W, int Cx, int Cop, int R, int S, int stride, int pad, int pad_mode, int act, float slope,
+                      int math, int co_real, void* stream);
 /* vst_conv2d_fwd plus the InstanceNorm statistics partials of its output, from the GEMM epilogue
  * (the conv that feeds an InstanceNorm): when the split-bf16 kernels run the conv and Ho*Wo % 32 == 0,
  * part (fp64, N * (Ho*Wo/32) * Cop * 2) receives {sum y, sum y^2} per (image, 32-pixel group,

@@ -684,3 +684,30 @@ def test_tap_wgrad_with_forward_x_image(ops):
         assert torch.equal(dw0, dw1)
     finally:
         ops.set_conv_math(prev_m)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(2, 512, 31, 31, 1, "zero", "none"), (1, 64, 9, 7, 2, "zero", "lrelu"),
+                                   (1, 36, 12, 10, 1, "reflect", "tanh")])
+def test_conv_fwd_one_real_channel(ops, shape):
+    """vst_conv2d_fwd_co with co_real = 1 (the PatchGAN head: one real channel padded to 4): the
+    padded channels equal the 4-channel path's exactly, the real one agrees with it to fp32 rounding
+    (the compiler contracts the one-channel sum into a different FMA chain) and matches torch."""
+    N, Ci, H, W, st, mode, act = shape
+    k, pad = 4, 1
+    x = _g(61, (N, Ci, H, W))
+    w = _g(62, (1, Ci, k, k), 0.05)
+    b = _g(63, (1,), 0.1)
+    kc = ops.weight_pack(w.to(DEV), ops.PACK_FWD)
+    bp = torch.zeros(ops.cpad(1), device=DEV)
+    bp[:1] = b.to(DEV)
+    xn = _nhwc(x, ops)
+    y4 = ops.conv2d_fwd(xn, kc, bp, ops.cpad(1), k, k, st, pad, mode, act=act, slope=0.2)
+    y1 = ops.conv2d_fwd(xn, kc, bp, ops.cpad(1), k, k, st, pad, mode, act=act, slope=0.2, co_real=1)
+    assert torch.equal(y1[..., 1:], y4[..., 1:])
+    d = (y1[..., 0] - y4[..., 0]).abs().max().item()
+    assert d <= 1e-6 * (y4[..., 0].abs().max().item() + 1e-12) * Ci ** 0.5, d
+    xp = F.pad(x, (pad,) * 4, mode="reflect") if mode == "reflect" else x
+    yr = F.conv2d(xp, w, b, stride=st, padding=0 if mode == "reflect" else pad)
+    yr = {"none": yr, "lrelu": F.leaky_relu(yr, 0.2), "tanh": torch.tanh(yr)}[act]
+    _close(_nchw(y1, 1, ops), yr, tol=1e-4, what="co_real=1 fwd")

@@ -863,6 +863,13 @@ extern "C" int vst_conv_plan_fwd(int N, int H, int W, int Cx, int Cop, int R, in
   return VST_OK;
 }
 
+// 4-channel inputs (images) on the split-bf16 kernels (conv_fprop_bf_k<.., false, 3>) rather than
+// the fp32 [row][k] kernels; VST_BF_C4=0 restores the latter.
+static const bool g_bf_c4 = [] {
+  const char* e = getenv("VST_BF_C4");
+  return !(e && e[0] == '0');
+}();
+
 static int conv_fwd_impl(const float* x, const float* wp, const void* wsplit, const float* bias, float* y,
                          int N, int H, int W, int Cx, int Cop, int R, int S, int stride, int padh, int padw,
                          int pad_mode, int act, float slope, int math, hipStream_t s, double* part = nullptr,
@@ -882,7 +889,7 @@ static int conv_fwd_impl(const float* x, const float* wp, const void* wsplit, co
     return skinny_out_launch(0, x, wp, bias, nullptr, y, N, H, W, Cx, Ho, Wo, R, S, stride, padh, refl,
                              act, slope, s, co_real);
   }
-  if (math != VST_MATH_F32 && wsplit && Cx % 8 == 0) {
+  if (math != VST_MATH_F32 && wsplit && (Cx % 8 == 0 || (Cx == 4 && g_bf_c4))) {
     // InstanceNorm partials from the epilogue: 32-pixel groups, so the image size must divide
     const bool stats = part && nsplit && (Ho * Wo) % 32 == 0;
     const int rc = bf_fprop_launch(x, wsplit, (long)Cop * R * S * Cx, bias, y, N, H, W, Cx, Ho, Wo, Cop, R, S,

@@ -488,7 +488,10 @@ __device__ __attribute__((aligned(256))) float g_zero_page[64];
 // Without KSL (C not a multiple of BK: the image-input layers) the K-steps walk k = (r, s, ci) in
 // order with a per-thread cursor.
 // REFL: 0 = zero padding, 1 = reflect padding (compile-time, branch-free tap map), 2 = runtime
-// `reflect` (the rarely used tap-major variants).
+// `reflect` (the rarely used tap-major variants), 3 = as 2 for a 4-channel input (the image layers:
+// 3 channels + 1 zero): a thread's 8-deep K chunk then spans two taps, the second one's rows have
+// their own offsets (aoff2), and a K that ends half-way through a chunk (R*S odd) reads zeros for the
+// missing tap.  K = R*S*4 instead of R*S*8 with the input padded to 8 channels: half the MFMA work.
 // SPLIT (KSL only): split-K over the K-steps — block L = z * tiles + tile runs K-steps
 // [z * spk, z * spk + spk) and stores its raw partial tile to slab[z][m - m_base][Cop]
 // (fprop_splitk_reduce_k sums the splits in order and applies bias / act / IN partials).
@@ -512,7 +515,8 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_k(
 
   // A rows (output pixels m0 + rb + RPP*j): tap-independent geometry.  Rows past M gather row 0's
   // pixels instead: their outputs are never stored, so no mask is needed for them.
-  int hb[A_LD], wb[A_LD], pb[A_LD], aoff[A_LD];
+  constexpr bool C4 = REFL == 3;
+  int hb[A_LD], wb[A_LD], pb[A_LD], aoff[A_LD], aoff2[C4 ? A_LD : 1];
 #pragma unroll
   for (int j = 0; j < A_LD; ++j) {
     const int m = m0 + rb + RPP * j;
@@ -524,20 +528,28 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_k(
     pb[j] = n * H * W * C;
   }
   // element offset of row j's pixel under tap (kr, ks), -1 where the tap reads zero padding
-  const bool refl = REFL == 2 ? reflect != 0 : REFL == 1;
+  const bool refl = REFL >= 2 ? reflect != 0 : REFL == 1;
   const int WC = W * C;
-  auto tap_rows = [&](int kr, int ks) __attribute__((always_inline)) {
+  auto tap_rows_to = [&](int* dst, int kr, int ks) __attribute__((always_inline)) {
 #pragma unroll
     for (int j = 0; j < A_LD; ++j) {
       int hi = hb[j] + kr, wi = wb[j] + ks;
       if (refl) {
         hi = reflect_idx(hi, H);
         wi = reflect_idx(wi, W);
-        aoff[j] = pb[j] + __mul24(hi, WC) + __mul24(wi, C);
+        dst[j] = pb[j] + __mul24(hi, WC) + __mul24(wi, C);
       } else {
         const bool ok = (unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W;
-        aoff[j] = ok ? pb[j] + __mul24(hi, WC) + __mul24(wi, C) : -1;
+        dst[j] = ok ? pb[j] + __mul24(hi, WC) + __mul24(wi, C) : -1;
       }
+    }
+  };
+  // C4: the chunk's second tap is the one after (kr, ks) (past the last tap it is never read)
+  auto tap_rows = [&](int kr, int ks) __attribute__((always_inline)) {
+    tap_rows_to(aoff, kr, ks);
+    if constexpr (C4) {
+      const bool wrap = ks + 1 == S;
+      tap_rows_to(aoff2, wrap ? kr + 1 : kr, wrap ? 0 : ks + 1);
     }
   };
   // B rows (output channels n0 + rb + RPP*j); channels past Cop read row Cop-1 (never stored)
@@ -579,6 +591,30 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_k(
     const bool kin = KSL || kcur < Ktot;  // the K tail reads zeros (A) against row 0 (B)
     const int ka = KSL ? ksb + kq8 : kc;
     const int kb = KSL ? (tr * S + ts) * C + ksb + kq8 : (kin ? kcur : 0);
+    if constexpr (C4) {
+      // chunk = taps kcur/4 and kcur/4 + 1; the second is missing when kcur + 4 == Ktot.  Weight rows
+      // are 4*R*S bf16 long (8-byte aligned for odd R*S): two 8-byte loads per plane.
+      const bool kin2 = kcur + 4 < Ktot;
+#pragma unroll
+      for (int j = 0; j < A_LD; ++j) {
+        const float* p0 = (kin && aoff[j] >= 0) ? x + aoff[j] : zp;
+        const float* p1 = (kin2 && aoff2[j] >= 0) ? x + aoff2[j] : zp;
+        ra[set][j][0] = *reinterpret_cast<const float4*>(p0);
+        ra[set][j][1] = *reinterpret_cast<const float4*>(p1);
+      }
+      const __bf16* zb = reinterpret_cast<const __bf16*>(zp);
+#pragma unroll
+      for (int j = 0; j < B_LD; ++j) {
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+          const __bf16* q = wrow[j] + p * wps + kb;
+          const uint2 lo = *reinterpret_cast<const uint2*>(q);
+          const uint2 hi = *reinterpret_cast<const uint2*>(kin2 ? q + 4 : zb);
+          rbv[set][j][p] = u32x4_t{lo.x, lo.y, hi.x, hi.y};
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < A_LD; ++j) {
       const float* p = (kin && aoff[j] >= 0) ? x + aoff[j] + ka : zp;
@@ -1212,7 +1248,10 @@ int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* b
   {                                                                                                 \
     using T = bf::Tile<BM_, BN_, WM_, WN_, BK_, NP_>;                                              \
     const dim3 grid(ceil_div(Mend - mb, BM_) * ceil_div(Cop, BN_));                                 \
-    if (VST_BF_KSLICE && C % BK_ == 0 && reflect)                                                   \
+    if (C == 4)                                                                                     \
+      hipLaunchKernelGGL((bf::conv_fprop_bf_k<T, false, 3>), grid, dim3(T::NT), 0, s, x, ws, wps, bias, y, \
+                         H, W, C, Ho, Wo, Cop, S, st, padh, padw, reflect, act, slope, Mend, K, mb, part); \
+    else if (VST_BF_KSLICE && C % BK_ == 0 && reflect)                                              \
       hipLaunchKernelGGL((bf::conv_fprop_bf_k<T, true, 1>), grid, dim3(T::NT), 0, s, x, ws, wps, bias, y, \
                          H, W, C, Ho, Wo, Cop, S, st, padh, padw, reflect, act, slope, Mend, K, mb, part); \
     else if (VST_BF_KSLICE && C % BK_ == 0)                                                         \

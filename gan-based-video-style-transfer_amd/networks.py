@@ -157,6 +157,11 @@ class _Marker(nn.Module):
 # (8-channel K chunks; half the K is zeros) instead of the fp32-image [row][k] kernels they otherwise
 # need at 4 channels (~40 TF): VST_C8_EDGES=0 restores those.
 C8_EDGES = os.environ.get("VST_C8_EDGES", "1") != "0"
+# The generator's first conv runs on the 4-channel image itself (conv_fprop_bf_k's 4-channel variant,
+# K = 49*4 instead of 49*8); the 8-channel copy is still made for its weight gradient.  Likewise the
+# data gradient of the last conv (a forward conv over its 4-channel output gradient).  VST_C4_FWD=0
+# runs both on 8-channel copies.
+C4_FWD = os.environ.get("VST_C4_FWD", "1") != "0" and os.environ.get("VST_BF_C4", "1") != "0"
 
 
 def _pad_channels(x, cs):
@@ -407,7 +412,9 @@ class ResnetGenerator(FlatNet):
                                                            _padded_bias(m))
             P["ikf"][f"b{i}a"] = _ikf(b.conv_block[1])
             P["ikf"][f"b{i}b"] = _ikf(b.conv_block[5])
-        if C8_EDGES and DGRAD_AS_FPROP and f.weight.shape[0] <= 4:
+        if C4_FWD and DGRAD_AS_FPROP and f.weight.shape[0] <= 4:
+            P["ikf"]["f4"] = ops.weight_pack(f.weight, ops.PACK_IKF)
+        elif C8_EDGES and DGRAD_AS_FPROP and f.weight.shape[0] <= 4:
             P["ikf"]["f8"] = ops.weight_pack(f.weight, ops.PACK_IKF, Op=8)
         for i, m in enumerate(u):
             # ConvTranspose2d fwd = transposed kernel with rows (r,s,ci) -> CK pack of Wt[Ci][Co];
@@ -497,7 +504,10 @@ class _GeneratorFn(torch.autograd.Function):
         if "c08" in P and x.shape[-1] == 4:
             x8 = _pad_channels(x, 8)
             _, _, b = P["c0"]
-            y, s = ops.conv2d_fwd_in(x8, P["c08"], b, cpad(ngf), 7, 7, 1, 3, "reflect", role=role)
+            if C4_FWD:
+                y, s = ops.conv2d_fwd_in(x, P["c0"][0], b, cpad(ngf), 7, 7, 1, 3, "reflect", role=role)
+            else:
+                y, s = ops.conv2d_fwd_in(x8, P["c08"], b, cpad(ngf), 7, 7, 1, 3, "reflect", role=role)
             a, at = in_act(y, s, "relu", cp_for(y, 2 * ngf, 2, "zero"))
             sv["xt"][id(a)] = at
             sv["x8"] = x8
@@ -607,7 +617,9 @@ class _GeneratorFn(torch.autograd.Function):
         else:
             wgrad(f, a, g, 7, 1, 3, "reflect", db=True)
         done(f)
-        if "f8" in P["ikf"] and g.shape[-1] == 4:
+        if "f4" in P["ikf"] and g.shape[-1] == 4:
+            ga = ops.conv2d_dgrad_s1(g, P["ikf"]["f4"], a.shape[1], a.shape[2], a.shape[-1], 7, 3, "reflect")
+        elif "f8" in P["ikf"] and g.shape[-1] == 4:
             ga = ops.conv2d_dgrad_s1(_pad_channels(g, 8), P["ikf"]["f8"], a.shape[1], a.shape[2], a.shape[-1], 7,
                                      3, "reflect")
         else:

@@ -282,6 +282,9 @@ def test_adam_matches_torch(ops):
     ("c7_reflect", 2, 16, 14, 12, 16, 7, 3, "reflect"),
     ("D4_s1_zero", 2, 32, 9, 11, 64, 4, 1, "zero"),
     ("k3_zero", 2, 24, 8, 8, 40, 3, 1, "zero"),
+    # 3 output channels: the forward conv over a 4-channel dy (the generator's last layer)
+    ("out3_c7_reflect", 2, 16, 14, 12, 3, 7, 3, "reflect"),
+    ("out3_k3_zero", 1, 8, 9, 7, 3, 3, 1, "zero"),
 ], ids=lambda c: c[0])
 def test_dgrad_as_fprop(ops, case, conv_math):
     """Stride-1 data gradient computed by the forward-conv kernel over the rotated-tap (IKF) pack,
@@ -711,3 +714,33 @@ def test_conv_fwd_one_real_channel(ops, shape):
     yr = F.conv2d(xp, w, b, stride=st, padding=0 if mode == "reflect" else pad)
     yr = {"none": yr, "lrelu": F.leaky_relu(yr, 0.2), "tanh": torch.tanh(yr)}[act]
     _close(_nchw(y1, 1, ops), yr, tol=1e-4, what="co_real=1 fwd")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(2, 3, 8, 8, 64, 7, 1, 3, "reflect"), (1, 3, 4, 5, 16, 7, 1, 3, "reflect"),
+                                   (3, 3, 16, 12, 64, 4, 2, 1, "zero"), (2, 1, 9, 7, 24, 3, 1, 1, "zero"),
+                                   (1, 4, 33, 17, 32, 5, 1, 2, "reflect")])
+def test_conv_fwd_four_channel_input(ops, shape):
+    """4-channel inputs on the split-bf16 forward (conv_fprop_bf_k<.., false, 3>): K chunks spanning
+    two taps, an odd tap count (the last chunk's missing tap reads zeros), reflect at the smallest
+    legal frame; output and the epilogue's InstanceNorm statistics vs torch."""
+    N, Ci, H, W, Co, k, st, pad, mode = shape
+    x = _g(71, (N, Ci, H, W))
+    w = _g(72, (Co, Ci, k, k), 0.1)
+    b = _g(73, (Co,), 0.1)
+    kc = ops.weight_pack(w.to(DEV), ops.PACK_FWD)
+    bp = torch.zeros(ops.cpad(Co), device=DEV)
+    bp[:Co] = b.to(DEV)
+    xn = _nhwc(x, ops)
+    assert xn.shape[-1] == 4
+    xp = F.pad(x, (pad,) * 4, mode="reflect") if mode == "reflect" else x
+    yr = F.conv2d(xp, w, b, stride=st, padding=0 if mode == "reflect" else pad)
+    y = ops.conv2d_fwd(xn, kc, bp, ops.cpad(Co), k, k, st, pad, mode)
+    _close(_nchw(y, Co, ops), yr, tol=CONV_TOL["bf16x6"], what="c4 fwd")
+    y2, s = ops.conv2d_fwd_in(xn, kc, bp, ops.cpad(Co), k, k, st, pad, mode)
+    assert torch.equal(y2, y)
+    st_ = s.view(N, ops.cpad(Co), 2)[:, :Co].cpu()
+    mean = yr.mean(dim=(2, 3))
+    rstd = 1.0 / torch.sqrt(yr.var(dim=(2, 3), unbiased=False) + 1e-5)
+    assert ((st_[..., 0] - mean).abs() * rstd).max().item() < 1e-5
+    assert ((st_[..., 1] - rstd).abs() / rstd).max().item() < 1e-4

@@ -839,6 +839,13 @@ static WgradPlan plan_wgrad(int N, int H, int W, int Ho, int Wo, int Cx, int Cyp
 
 using namespace vst;
 
+// 4-channel inputs (images) on the split-bf16 kernels (conv_fprop_bf_k<.., false, 3>) rather than
+// the fp32 [row][k] kernels; VST_BF_C4=0 restores the latter.
+static const bool g_bf_c4 = [] {
+  const char* e = getenv("VST_BF_C4");
+  return !(e && e[0] == '0');
+}();
+
 extern "C" void vst_debug_set_tiles(int fprop, int tconv, int wgrad) {
   g_tile_override[0] = fprop;
   g_tile_override[1] = tconv;
@@ -855,20 +862,13 @@ extern "C" int vst_conv_plan_fwd(int N, int H, int W, int Cx, int Cop, int R, in
   *tail_kind = -1;
   if (Cop == 4) {
     *kind = VST_PLAN_SKINNY;
-  } else if (math != VST_MATH_F32 && Cx % 8 == 0) {
+  } else if (math != VST_MATH_F32 && (Cx % 8 == 0 || (Cx == 4 && g_bf_c4))) {
     bf_plan((long)N * Ho * Wo, Cop, math, g_tile_override[0], kind, m_split, tail_kind);
   } else {
     *kind = VST_PLAN_RK;
   }
   return VST_OK;
 }
-
-// 4-channel inputs (images) on the split-bf16 kernels (conv_fprop_bf_k<.., false, 3>) rather than
-// the fp32 [row][k] kernels; VST_BF_C4=0 restores the latter.
-static const bool g_bf_c4 = [] {
-  const char* e = getenv("VST_BF_C4");
-  return !(e && e[0] == '0');
-}();
 
 static int conv_fwd_impl(const float* x, const float* wp, const void* wsplit, const float* bias, float* y,
                          int N, int H, int W, int Cx, int Cop, int R, int S, int stride, int padh, int padw,

@@ -151,6 +151,9 @@ def test_conv_planner_picks_production_kernels():
     assert kind == 0 and ms == 2 * 256 // 2 * 128 and 0 < ms < 8 * 66 * 66
     assert ops.conv_plan_fwd(8, 64, 64, 256, 256, 3, 3, 1, 1, 1, "fp32") == (ops.PLAN_RK, 0)
     assert ops.conv_plan_fwd(2, 32, 32, 64, 4, 7, 7, 1, 3, 3, "bf16x6")[0] == ops.PLAN_SKINNY
+    # the generator's first conv: a 4-channel image on the split-bf16 kernels (not the fp32 rk path)
+    assert ops.conv_plan_fwd(8, 256, 256, 4, 64, 7, 7, 1, 3, 3, "bf16x6")[0] not in (ops.PLAN_RK, ops.PLAN_SKINNY)
+    assert ops.conv_plan_fwd(8, 256, 256, 4, 64, 7, 7, 1, 3, 3, "fp32")[0] == ops.PLAN_RK
     ops.debug_set_tiles(7, -1, -1)
     try:
         assert ops.conv_plan_fwd(2, 12, 10, 32, 32, 3, 3, 1, 1, 1, "bf16x3") == (7, 0)

@@ -502,7 +502,8 @@ class _GeneratorFn(torch.autograd.Function):
             return y, s, a
 
         if "c08" in P and x.shape[-1] == 4:
-            x8 = _pad_channels(x, 8)
+            # the 8-channel copy feeds the forward only without C4_FWD, else just c0's weight gradient
+            x8 = _pad_channels(x, 8) if (train_w or not C4_FWD) else None
             _, _, b = P["c0"]
             if C4_FWD:
                 y, s = ops.conv2d_fwd_in(x, P["c0"][0], b, cpad(ngf), 7, 7, 1, 3, "reflect", role=role)
@@ -510,7 +511,8 @@ class _GeneratorFn(torch.autograd.Function):
                 y, s = ops.conv2d_fwd_in(x8, P["c08"], b, cpad(ngf), 7, 7, 1, 3, "reflect", role=role)
             a, at = in_act(y, s, "relu", cp_for(y, 2 * ngf, 2, "zero"))
             sv["xt"][id(a)] = at
-            sv["x8"] = x8
+            if x8 is not None:
+                sv["x8"] = x8
         else:
             y, s, a = conv_in_relu(x, "c0", ngf, 7, 1, 3, "reflect", nxt=(2 * ngf, 2, "zero"))
         sv["c0"] = (y, s, a)

@@ -130,7 +130,33 @@ SIGNATURES = {
     "vst_raft_coords_update": (I, [P, P, I, I, I, I, P]),
     "vst_raft_upsample": (I, [P, P, I, P, I, I, I, P]),
     "vst_u8_image_to_nhwc4": (I, [P, P, L, P]),
+    # SURVEY §8b spelling (abi.hip)
+    "vst_conv_desc_out_hw": (I, [P, P, P]),
+    "vst_workspace_size": (SZ, [P, I]),
+    "vst_conv2d_fwd_desc": (I, [P, P, P, P, P, P, P, P, P, SZ, P]),
+    "vst_conv2d_dgrad_desc": (I, [P, P, P, P, P, P, SZ, P]),
+    "vst_conv2d_wgrad_desc": (I, [P, P, P, P, I, I, I, P, SZ, P]),
+    "vst_adam_multi_tensor": (I, [P, P, P, P, P, I, F, F, F, F, I, P]),
+    "vst_gram_ws_bytes": (SZ, [I, I]),
+    "vst_gram": (I, [P, P, I, I, I, P, SZ, I, P]),
+    "vst_corr_volume_ws_bytes": (SZ, [I, I, I, I]),
+    "vst_corr_volume": (I, [P, P, P, I, I, I, I, I, P, I, P, SZ, I, P]),
+    "vst_warp_bilinear_fwd": (I, [P, P, P, I, I, I, I, I, I, P]),
+    "vst_warp_bilinear_bwd_input": (I, [P, P, P, I, I, I, I, I, I, P]),
+    "vst_masked_sqdiff_mean_fwd": (I, [P, P, P, P, P, P, I, I, I, I, I, F, P]),
+    "vst_masked_sqdiff_mean_bwd": (I, [P, P, P, P, P, P, P, I, I, I, I, I, F, P]),
+    "vst_l1_mean_fwd": (I, [P, P, P, P, L, I, I, F, P]),
+    "vst_l1_mean_bwd": (I, [P, P, P, P, L, I, I, F, P]),
+    "vst_mse_const_fwd": (I, [P, F, P, P, L, I, I, F, P]),
+    "vst_mse_const_bwd": (I, [P, F, P, P, L, I, I, F, P]),
 }
+
+
+class VstConvDesc(ctypes.Structure):
+    """include/vst_hip.h vst_conv_desc."""
+    _fields_ = [(n, ctypes.c_int) for n in ("N", "H", "W", "C", "K", "R", "S", "stride", "pad", "pad_mode",
+                                             "dilation", "transposed", "output_padding", "layout", "dtype",
+                                             "epilogue")] + [("slope", ctypes.c_float), ("math", ctypes.c_int)]
 
 
 # Per-file compiler flags.  conv_bf.hip: no SLP vectorisation — it pairs the operand split's fp32
@@ -147,6 +173,8 @@ def build(force=False, verbose=False, out=None, defines=()):
     """Compile every HIP source into _build/libvst_hip.so for gfx950 (cross-compiles without a GPU).
     out/defines: developer variant builds (tools/build_variant.py)."""
     lib_path = out or os.path.join(BUILD, "libvst_hip.so")
+    if out is None and any(d.split("=")[0] == "VST_DEV_VARIANT" for d in defines):
+        raise ValueError("VST_DEV_VARIANT builds go to a variant path (tools/build_variant.py), never the product library")
     objdir = os.path.join(os.path.dirname(lib_path), "obj_" + os.path.basename(lib_path)[:-3])
     os.makedirs(objdir, exist_ok=True)
     srcs = sources()

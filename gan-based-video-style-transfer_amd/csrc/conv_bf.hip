@@ -139,6 +139,12 @@ __device__ __forceinline__ uint32_t pack2(float a, float b) {
 #ifndef VST_BF_FAKESPLIT
 #define VST_BF_FAKESPLIT 0  // developer timing experiment only: hi plane replicated (WRONG results)
 #endif
+// The two timing modes above compute WRONG results: only a developer variant build (tools/
+// build_variant.py, which defines VST_DEV_VARIANT and writes _build/variants/, never the product
+// library) may turn them on.
+#if (VST_BF_FAKESPLIT || VST_BF_FAKE16) && !defined(VST_DEV_VARIANT)
+#error "VST_BF_FAKESPLIT / VST_BF_FAKE16 are developer-only timing modes (wrong results): build them with tools/build_variant.py"
+#endif
 template <int NP>
 __device__ __forceinline__ void split8(const float4& a, const float4& b, uint4 (&o)[NP]) {
   if (VST_BF_FAKESPLIT) {

@@ -53,10 +53,13 @@ class GradExchange:
     """Callable grad hook for CycleGANModel.optimize_parameters(grad_hook_G=..., grad_hook_D=...)
     (the join); ``attach(nets)`` additionally launches buckets during backward."""
 
-    def __init__(self, world_size=None, group=None, bucket_bytes=BUCKET_BYTES):
+    def __init__(self, world_size=None, group=None, bucket_bytes=BUCKET_BYTES, force=False):
+        """force: run the bucketed collectives even at world 1 (they are identities there), so the
+        single-GPU test exercises the RCCL async_op / wait stream ordering on hardware."""
         self.world = world_size or dist.get_world_size(group)
         self.group = group
         self.bucket_bytes = bucket_bytes
+        self.force = force
         self._states = {}
 
     def _state(self, net):
@@ -69,7 +72,7 @@ class GradExchange:
     def attach(self, nets):
         """Hook each network's backward: buckets are all-reduced as soon as the phase's last
         backward pass has written them."""
-        if self.world == 1:
+        if self.world == 1 and not self.force:
             return self
         for net in nets:
             st = self._state(net)
@@ -90,7 +93,7 @@ class GradExchange:
 
     def __call__(self, nets):
         """Join: launch the remaining buckets, wait for all, average."""
-        if self.world == 1:
+        if self.world == 1 and not self.force:
             for n in nets:
                 _reset(n)
             return

@@ -94,6 +94,31 @@ def _set_input(model, data):
         model.set_input_fc2(data)
 
 
+def _optimize(model, grad_hook):
+    """optimize_parameters with the DP exchange on EVERY optimizer phase the model has: G and D, plus
+    MoGAN's motion-net phase (grad_hook_M, MoGAN/models/cycle_gan_model.py:315-352) — a phase without
+    the exchange would let that phase's replicas diverge across ranks."""
+    import inspect
+    if grad_hook is None:
+        return model.optimize_parameters()
+    params = inspect.signature(model.optimize_parameters).parameters
+    if "grad_hook_M" in params:
+        return model.optimize_parameters(grad_hook, grad_hook, grad_hook_M=grad_hook)
+    extra = [p for p in params if p.startswith("grad_hook") and p not in ("grad_hook_G", "grad_hook_D")]
+    if extra:
+        raise NotImplementedError("data-parallel training of %s: optimizer phases %s have no gradient "
+                                  "exchange" % (type(model).__name__, extra))
+    return model.optimize_parameters(grad_hook, grad_hook)
+
+
+def shard_indices(n, world, rank):
+    """DistributedSampler (drop_last=True, no shuffle) shard: rank r takes items r, r+world, ... of the
+    first world*floor(n/world) items, so every rank holds the same count and runs the same number of
+    batches (a rank with one more batch would block forever in its gradient all-reduce)."""
+    usable = (n // world) * world
+    return list(range(rank, usable, world))
+
+
 def train(opt, dataset, model=None, world=1, rank=0, grad_hook=None, log=print):
     """train.py:48-130.  ``dataset``: an iterable of batches with ``len()`` = images per epoch (per rank).
     Returns (model, total_iters)."""
@@ -120,7 +145,7 @@ def train(opt, dataset, model=None, world=1, rank=0, grad_hook=None, log=print):
             total_iters += opt.batch_size
             epoch_iter += opt.batch_size
             _set_input(model, data)
-            model.optimize_parameters(grad_hook, grad_hook)
+            _optimize(model, grad_hook)
             if total_iters % opt.print_freq == 0:
                 losses = model.get_current_losses()  # one host sync, as the reference's float(loss)
                 t_comp = (time.time() - iter_start_time) / opt.batch_size
@@ -174,8 +199,8 @@ def main(argv=None):
         dataset = SyntheticFC2(synthetic, opt.batch_size, opt.crop_size, device, seed=rank)
     else:
         full = DatasetFC2(opt.image_dir, opt.style_dir)
-        if world > 1:  # rank r reads images r, r+world, ... (DistributedSampler without shuffle)
-            full.dataset = full.dataset[rank::world]
+        if world > 1:  # rank r reads images r, r+world, ... of an equal-size shard (DistributedSampler)
+            full.dataset = [full.dataset[i] for i in shard_indices(len(full.dataset), world, rank)]
             full.num_images = len(full.dataset)
         dataset = FC2Loader(full, batch_size=opt.batch_size, shuffle=not opt.serial_batches,
                             max_dataset_size=opt.max_dataset_size, device=device, seed=rank, drop_last=world > 1)

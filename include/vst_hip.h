@@ -483,6 +483,87 @@ int vst_fc2_unpack(const float* raw, float* img1, float* img2, float* mask, floa
  * NHWC4 float32 (channel 3 zero). */
 int vst_u8_image_to_nhwc4(const unsigned char* x, float* y, long npix, void* stream);
 
+/* ---- SURVEY §8b spelling of the ABI (abi.hip: host wrappers over the entry points above) ----- *
+ * The contract in SURVEY §8b names a conv descriptor, a workspace query and a few entry points the
+ * shape-argument API above spells differently.  These wrappers give a binder written from §8b the
+ * names it expects; each forwards to the kernels above (no extra launch except where stated).
+ *   §8b name                         forwards to
+ *   vst_conv2d_fwd/dgrad/wgrad(desc) vst_conv2d_fwd_ws / vst_conv2d_tfwd / vst_conv2d_wgrad (the
+ *                                    `_desc` suffix: the shape-argument names are taken above)
+ *   vst_workspace_size               vst_conv2d_fwd_ws_bytes / vst_conv2d_wgrad_ws_bytes
+ *   vst_warp_bilinear_fwd/bwd_input  vst_warp_fwd / vst_warp_masked_fwd (validity mask flag)
+ *   vst_masked_sqdiff_mean_fwd/bwd   vst_loss_temporal(_bwd)   (fused warp + masked squared diff)
+ *   vst_l1_mean_fwd/bwd              vst_loss_l1(_bwd)
+ *   vst_mse_const_fwd/bwd            vst_loss_mse_const(_bwd)
+ *   vst_gram                         per-image 1x1 vst_conv2d_wgrad + vst_axpby (1/HW)
+ *   vst_corr_volume                  vst_channel_normalize + vst_weight_split + 1x1 vst_conv2d_fwd per
+ *                                    image, then vst_corr_pyramid (vst_corr_pyramid / _lookup above)
+ *   vst_adam_multi_tensor            vst_adam_step per tensor
+ *   vst_instnorm_act_fwd/bwd         (already the §8b names) */
+enum { VST_LAYOUT_NHWC = 0 };
+enum { VST_DTYPE_F32 = 0 };
+enum { VST_OP_FWD = 0, VST_OP_DGRAD = 1, VST_OP_WGRAD = 2 };
+typedef struct vst_conv_desc {
+  int N, H, W;            /* input batch and spatial size (a transposed conv: its input) */
+  int C, K;               /* input / output channel strides (multiples of 4; padding channels zero) */
+  int R, S, stride, pad;  /* filter taps, stride, symmetric padding */
+  int pad_mode;           /* VST_PAD_ZERO | VST_PAD_REFLECT (reflect: direct convs) */
+  int dilation;           /* 1 (0 is read as 1) */
+  int transposed;         /* ConvTranspose2d (weight [Ci][Co][R][S]) */
+  int output_padding;     /* transposed only */
+  int layout;             /* VST_LAYOUT_NHWC */
+  int dtype;              /* VST_DTYPE_F32 */
+  int epilogue;           /* VST_ACT_* applied after the bias (forward only) */
+  float slope;            /* LeakyReLU slope */
+  int math;               /* VST_MATH_* */
+} vst_conv_desc;
+/* Output spatial size of the descriptor's forward op. */
+int vst_conv_desc_out_hw(const vst_conv_desc* d, int* Ho, int* Wo);
+/* Bytes of caller workspace op (VST_OP_*) needs for this descriptor (0: none; also 0 for a bad desc). */
+size_t vst_workspace_size(const vst_conv_desc* d, int op);
+/* Forward: y = act(conv(x) + bias).  wp: VST_PACK_OK pack (+ wsplit planes) of a Conv2d weight, or
+ * the VST_PACK_IK pack of a ConvTranspose2d weight.  in_part / in_nsplit: optional InstanceNorm
+ * partials (vst_conv2d_fwd_in; direct convs). */
+int vst_conv2d_fwd_desc(const vst_conv_desc* d, const float* x, const float* wp, const void* wsplit,
+                        const float* bias, float* y, double* in_part, int* in_nsplit, float* ws, size_t ws_bytes,
+                        void* stream);
+/* Data gradient: dx from dy.  Conv2d: wp = VST_PACK_IK pack (reflect padding folded in-kernel);
+ * ConvTranspose2d: wp = the VST_PACK_OK pack of its weight seen as a Conv2d weight [Ci][Co] (+ planes). */
+int vst_conv2d_dgrad_desc(const vst_conv_desc* d, const float* dy, const float* wp, const void* wsplit, float* dx,
+                          float* ws, size_t ws_bytes, void* stream);
+/* Weight gradient into dw (PyTorch layout of the weight, Co x Ci logical output / input channels of
+ * the layer; accumulate != 0 adds).  ws: vst_workspace_size(d, VST_OP_WGRAD) bytes. */
+int vst_conv2d_wgrad_desc(const vst_conv_desc* d, const float* x, const float* dy, float* dw, int Co, int Ci,
+                          int accumulate, float* ws, size_t ws_bytes, void* stream);
+int vst_adam_multi_tensor(float* const* p, const float* const* g, float* const* m, float* const* v, const long* n,
+                          int ntensors, float lr, float beta1, float beta2, float eps, int step, void* stream);
+/* G[b] = F_b^T F_b / HW for NHWC features f [B][HW][C] (fast_style_transfer.py:813-817). */
+size_t vst_gram_ws_bytes(int HW, int C);
+int vst_gram(const float* f, float* G, int B, int HW, int C, float* ws, size_t ws_bytes, int math, void* stream);
+/* CorrBlock volume + pyramid (corr.py:12-60) from NHWC fmaps [B][H][W][Dp] (D logical channels);
+ * sqrt_d: device array of D floats = sqrt(D); pyr: vst_corr_pyramid_floats(B*H*W, H, W, vst_cp_ld(H*W),
+ * levels) floats. */
+size_t vst_corr_volume_ws_bytes(int B, int H, int W, int Dp);
+int vst_corr_volume(const float* f1, const float* f2, float* pyr, int B, int H, int W, int Dp, int D,
+                    const float* sqrt_d, int levels, float* ws, size_t ws_bytes, int math, void* stream);
+int vst_warp_bilinear_fwd(const float* x, const float* flow, float* out, int N, int H, int W, int Cs,
+                          int align_corners, int validity_mask, void* stream);
+int vst_warp_bilinear_bwd_input(const float* gout, const float* flow, float* gx, int N, int H, int W, int Cs,
+                                int align_corners, int validity_mask, void* stream);
+int vst_masked_sqdiff_mean_fwd(const float* a, const float* b, const float* flow, const float* mask, float* loss,
+                               float* part, int N, int H, int W, int Cs, int Cl, float lambda, void* stream);
+int vst_masked_sqdiff_mean_bwd(const float* a, const float* b, const float* flow, const float* mask,
+                               const float* gout, float* ga, float* gb, int N, int H, int W, int Cs, int Cl,
+                               float lambda, void* stream);
+int vst_l1_mean_fwd(const float* a, const float* b, float* loss, float* part, long npix, int Cs, int Cl, float scale,
+                    void* stream);
+int vst_l1_mean_bwd(const float* a, const float* b, const float* gout, float* grad, long npix, int Cs, int Cl,
+                    float scale, void* stream);
+int vst_mse_const_fwd(const float* a, float target, float* loss, float* part, long npix, int Cs, int Cl, float scale,
+                      void* stream);
+int vst_mse_const_bwd(const float* a, float target, const float* gout, float* grad, long npix, int Cs, int Cl,
+                      float scale, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -198,3 +198,48 @@ def test_wgrad_planner_routes_generator_layers_to_bf16_kernel():
         path, kind, ns = ops.conv_plan_wgrad(*sh, "bf16x6")
         assert path == BF, (name, path)
     assert ops.conv_plan_wgrad(*shapes["res"], "bf16x6")[1:] == (7, 14)
+
+
+def test_wrong_result_modes_refused_in_product_build():
+    """VERDICT r2 hygiene: the developer timing modes of conv_bf.hip that compute wrong results
+    (VST_BF_FAKESPLIT, VST_BF_FAKE16) stop the preprocessor unless the variant builder's
+    VST_DEV_VARIANT is defined; the product builder refuses that define."""
+    import subprocess
+    import pytest
+    from gbvst import _lib
+    src = os.path.join(_lib.CSRC, "conv_bf.hip")
+    for mode in ("VST_BF_FAKESPLIT=1", "VST_BF_FAKE16=1"):
+        r = subprocess.run([_lib.HIPCC, "-E", "--offload-arch=gfx950", "--cuda-host-only", "-D" + mode, src,
+                            "-o", os.devnull], stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+        assert r.returncode != 0 and b"developer-only" in r.stdout, (mode, r.stdout[-400:])
+    r = subprocess.run([_lib.HIPCC, "-E", "--offload-arch=gfx950", "--cuda-host-only", "-DVST_BF_FAKESPLIT=1",
+                        "-DVST_DEV_VARIANT=1", src, "-o", os.devnull], stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+    assert r.returncode == 0, r.stdout[-400:]
+    with pytest.raises(ValueError):
+        _lib.build(defines=["VST_DEV_VARIANT=1"])
+
+
+def test_conv_desc_host_validation():
+    """§8b descriptor entry points validate on the host before any launch (no GPU needed)."""
+    import ctypes
+    import gbvst
+    lib = gbvst._lib.load()
+    d = gbvst._lib.VstConvDesc()
+    for k, v in dict(N=2, H=64, W=64, C=256, K=256, R=3, S=3, stride=1, pad=1, pad_mode=1, dilation=1,
+                     math=2).items():
+        setattr(d, k, v)
+    ho, wo = ctypes.c_int(), ctypes.c_int()
+    assert lib.vst_conv_desc_out_hw(ctypes.byref(d), ctypes.byref(ho), ctypes.byref(wo)) == 0
+    assert (ho.value, wo.value) == (64, 64)
+    assert lib.vst_workspace_size(ctypes.byref(d), 2) == lib.vst_conv2d_wgrad_ws_bytes(2, 64, 64, 256, 64, 64, 256,
+                                                                                      3, 3, 1)
+    d.transposed, d.pad_mode, d.stride, d.output_padding, d.H, d.W = 1, 0, 2, 1, 32, 32
+    assert lib.vst_conv_desc_out_hw(ctypes.byref(d), ctypes.byref(ho), ctypes.byref(wo)) == 0
+    assert (ho.value, wo.value) == (64, 64)
+    for field, bad in (("dilation", 2), ("layout", 1), ("dtype", 3), ("C", 6), ("output_padding", 2)):
+        old = getattr(d, field)
+        setattr(d, field, bad)
+        assert lib.vst_conv_desc_out_hw(ctypes.byref(d), ctypes.byref(ho), ctypes.byref(wo)) == 1, field
+        assert lib.vst_workspace_size(ctypes.byref(d), 0) == 0
+        setattr(d, field, old)
+    assert lib.vst_conv_desc_out_hw(None, ctypes.byref(ho), ctypes.byref(wo)) == 1

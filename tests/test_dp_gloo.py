@@ -283,3 +283,61 @@ def test_generator_reports_layers_in_reverse_flat_order():
     for m in reversed(D._convs()):
         D._grad_done(m)
     assert offs == sorted(offs, reverse=True) and offs[-1] == 0
+
+
+class _CountModel:
+    """Stand-in model whose optimizer step is one all-reduce (the gradient exchange's collective)."""
+    model_names = []
+
+    def __init__(self):
+        self.steps = 0
+
+    def setup(self, opt):
+        pass
+
+    def update_learning_rate(self):
+        pass
+
+    def set_input_nhwc(self, *a):
+        pass
+
+    def optimize_parameters(self, hg=None, hd=None):
+        t = torch.ones(1)
+        dist.all_reduce(t)
+        self.steps += 1
+
+
+def _shard_worker(rank, world, port, q, n):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=__import__("datetime").timedelta(seconds=60))
+    import gbvst.train as T
+    from gbvst.options import default_opt
+    idx = T.shard_indices(n, world, rank)
+    bs = 2
+    batches = [tuple(idx[i:i + bs]) + (0, 0, 0) for i in range(0, len(idx) - bs + 1, bs)]  # drop_last
+    opt = default_opt(True, checkpoints_dir="/tmp/vst_shard_%d" % port, name="s", n_epochs=2, n_epochs_decay=0,
+                      batch_size=bs, print_freq=10 ** 6, save_latest_freq=10 ** 6, save_epoch_freq=10 ** 6)
+    m = _CountModel()
+    T.train(opt, batches, model=m, world=world, rank=rank, grad_hook=None, log=lambda *_: None)
+    q.put((rank, m.steps))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_train_shard_non_divisible_gloo_world3():
+    """train.py DP shard with a dataset size world does not divide (22 items, world 3, batch 2): every
+    rank runs the same number of steps, so no rank waits in a collective the others never join."""
+    world, n = 3, 22
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_shard_worker, args=(r, world, port, q, n)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in range(world)])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [s for _, s in res] == [6, 6, 6], res   # 7 items -> 3 batches per epoch x 2 epochs

@@ -117,3 +117,68 @@ def test_dp_world2_overlap_equals_single_process():
             off += n
         # buckets went out during that network's last backward pass (before the join)
         assert len(res[0][2][name]) > 0, (name, res[0][2][name])
+
+
+def _nccl_worker(port, q):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    try:
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+        import gbvst
+        from gbvst import dp
+        gbvst._lib.load()
+        m = _setup()
+        nets = [m.netG_A, m.netG_B, m.netD_A, m.netD_B]
+        # force: the world-1 short-circuit is bypassed, so every bucket goes through RCCL
+        # all_reduce(async_op=True) launched from inside backward and the join's work.wait()
+        ex = dp.GradExchange(1, bucket_bytes=64 << 10, force=True).attach(nets)
+        grads = {}
+        m.optimize_parameters(_grads_hook(grads, ex), _grads_hook(grads, ex))
+        torch.cuda.synchronize()
+        logs = {name: list(ex._state(getattr(m, "net" + name)).last_log) for name in ("G_A", "G_B", "D_A", "D_B")}
+        out = {name: grads[id(getattr(m, "net" + name))].numpy() for name in ("G_A", "G_B", "D_A", "D_B")}
+        w = {name: getattr(m, "net" + name).flat_param.detach().cpu().numpy() for name in ("G_A", "D_A")}
+        q.put((out, logs, w, dist.get_backend(), None))
+        dist.destroy_process_group()
+    except Exception:  # report, do not hang the parent
+        import traceback
+        q.put((None, None, None, None, traceback.format_exc()))
+
+
+@pytest.mark.timeout(600)
+def test_dp_nccl_world1_forced_buckets():
+    """The RCCL path on hardware: a one-rank `nccl` (= RCCL) process group with the bucketed exchange
+    forced on.  Buckets are all_reduce(async_op=True) calls enqueued from inside the HIP backward
+    passes; the join makes the compute stream wait on them before Adam.  A one-rank sum is the
+    identity, so the step must equal the run without any exchange up to the warp backward's atomic
+    summation order — any stream-ordering fault (Adam reading a bucket before RCCL wrote it back, or
+    the join's scaling racing the collective) shows as a gradient or weight far outside that."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_nccl_worker, args=(_free_port(), q))
+    p.start()
+    out, logs, w, backend, err = q.get(timeout=400)
+    p.join(timeout=120)
+    assert err is None, err
+    assert p.exitcode == 0
+    assert backend == "nccl"
+    import gbvst
+    gbvst._lib.load()
+    m = _setup()
+    grads = {}
+    m.optimize_parameters(_grads_hook(grads), _grads_hook(grads))
+    torch.cuda.synchronize()
+    for name in ("G_A", "G_B", "D_A", "D_B"):
+        net = getattr(m, "net" + name)
+        ref = grads[id(net)].numpy().astype(np.float64)
+        rel = np.linalg.norm(out[name] - ref) / np.linalg.norm(ref)
+        assert rel < 1e-5, (name, rel)
+        assert len(logs[name]) > 0, (name, logs[name])   # launched during backward, not at the join
+    lr = 2e-4
+    for name in ("G_A", "D_A"):
+        d = np.abs(w[name] - getattr(m, "net" + name).flat_param.detach().cpu().numpy())
+        # Adam's first update is ~lr*sign(g): rounding-level gradient noise can flip a near-zero one
+        assert d.max() <= 2.5 * lr and d.mean() < 1e-3 * lr, (name, d.max(), d.mean())

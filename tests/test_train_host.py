@@ -75,3 +75,41 @@ def test_reference_tuple_input(tmp_path):
 def test_entry_flags():
     syn, rest = T._add_entry_flags(["--synthetic", "8", "--name", "x", "--synthetic=4"])
     assert syn == 4 and rest == ["--name", "x"]
+
+
+def test_dp_shard_equal_counts():
+    """with len % world != 0, every rank must still hold the same item count (DistributedSampler
+    drop_last semantics), or the ranks with an extra batch block in the gradient all-reduce."""
+    for n in (22208, 22, 7, 3):
+        for world in (2, 3, 8):
+            shards = [T.shard_indices(n, world, r) for r in range(world)]
+            assert len({len(s) for s in shards}) == 1
+            flat = sorted(i for s in shards for i in s)
+            assert flat == list(range((n // world) * world))
+
+
+class _MoFake(_FakeModel):
+    def optimize_parameters(self, grad_hook_G=None, grad_hook_D=None, grad_hook_M=None):
+        self.calls.append(("opt", grad_hook_G, grad_hook_D, grad_hook_M))
+
+
+class _ExtraPhase(_FakeModel):
+    def optimize_parameters(self, grad_hook_G=None, grad_hook_D=None, grad_hook_X=None):
+        pass
+
+
+def test_dp_hook_reaches_every_phase():
+    """MoGAN's motion-net phase (grad_hook_M) gets the DP exchange too; a model with an
+    optimizer phase the loop does not know is refused instead of silently diverging."""
+    import pytest
+    hook = object()
+    m = _MoFake()
+    T._optimize(m, hook)
+    assert m.calls[-1] == ("opt", hook, hook, hook)
+    T._optimize(m, None)
+    assert m.calls[-1] == ("opt", None, None, None)
+    with pytest.raises(NotImplementedError):
+        T._optimize(_ExtraPhase(), hook)
+    f = _FakeModel()
+    T._optimize(f, hook)
+    assert f.step == 1

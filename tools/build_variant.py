@@ -9,4 +9,4 @@ import gbvst  # noqa: E402
 name, defs = sys.argv[1], sys.argv[2:]
 out = os.path.join(gbvst._lib.BUILD, "variants", "lib_%s.so" % name)
 os.makedirs(os.path.dirname(out), exist_ok=True)
-print(gbvst._lib.build(force=True, out=out, defines=defs))
+print(gbvst._lib.build(force=True, out=out, defines=list(defs) + ["VST_DEV_VARIANT=1"]))

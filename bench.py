@@ -202,7 +202,8 @@ def sintel_inference_fps(device, reps=5):
     with torch.no_grad():
         ms = _time_on_stream(lambda: G(x), reps, warm=2)
     return {"metric": "generator-only inference fps 1024x436", "batch": 1, "value": round(1000.0 / ms, 2),
-            "unit": "frames/s", "tflops": round(675.14 / ms, 2)}
+            "unit": "frames/s", "tflops": round(675.14 / ms, 2),
+            "roofline": _mfma_roofline(675.14 / ms, "whole generator forward at 1x3x436x1024: 675.14 GFLOP/frame")}
 
 
 def johnson_train_fps(device, B=4, S=256, steps=5):
@@ -223,7 +224,7 @@ def johnson_train_fps(device, B=4, S=256, steps=5):
             "value": round(B / dt, 2), "unit": "frames/s", "ms_per_step": round(dt * 1e3, 3)}
 
 
-def stargan_train_fps(device, B=4, S=256, c_dim=4, cycles=1):
+def stargan_train_fps(device, B=4, S=256, c_dim=4, cycles=2):
     """StarGAN C4: solver.py's training iteration at SxS, c_dim 4, n_critic 5, B_local
     images per rank; one timed cycle = 5 D iterations (each with the WGAN-GP double backward) + 1 G
     step.  Reported as per-D-iteration images/s (BASELINE.md's C4 line).  Random-init weights."""
@@ -233,7 +234,7 @@ def stargan_train_fps(device, B=4, S=256, c_dim=4, cycles=1):
     x = (torch.rand(B, 3, S, S, generator=g) * 2 - 1).to(device)
     lo = torch.randint(0, c_dim, (B,), generator=g)
     lt = torch.randint(0, c_dim, (B,), generator=g)
-    for _ in range(5):
+    for _ in range(10):
         sol.train_step(x, lo, lt)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -267,7 +268,7 @@ def raft_inference(device, B=1, H=436, W=1024, iters=20, reps=3):
             "pairs_per_s": round(B / dt, 2), "tflops": round(fl / dt / 1e12, 2)}
 
 
-def mogan_train_fps(device, B=4, S=256, pairs=2):
+def mogan_train_fps(device, B=4, S=256, pairs=2, H=None, W=None):
     """MoGAN C5-style step: CycleGAN ngf=ndf=64 generators / discriminators, motion nets,
     8 RAFT flows (20 iterations; one batched call) per optimize_parameters, E-step / M-step alternating; B frame pairs
     of SxS, random-init weights.  Reported per optimize_parameters call (E and M averaged)."""
@@ -276,7 +277,8 @@ def mogan_train_fps(device, B=4, S=256, pairs=2):
     opt = default_opt(True, model="mogan", pool_size=50, gpu_ids=[device.index or 0])
     m = mogan_model.MoGANModel(opt)
     g = torch.Generator(device="cpu").manual_seed(3)
-    imgs = [(torch.rand(B, 3, S, S, generator=g) * 2 - 1) for _ in range(4)]
+    H, W = H or S, W or S
+    imgs = [(torch.rand(B, 3, H, W, generator=g) * 2 - 1) for _ in range(4)]
     m.set_input_fc2(imgs)
     for _ in range(2):
         m.optimize_parameters()
@@ -286,7 +288,7 @@ def mogan_train_fps(device, B=4, S=256, pairs=2):
         m.optimize_parameters()
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / (2 * pairs)
-    return {"metric": "MoGAN optimize_parameters frames/s %dx%d (8 RAFT flows x 20 iterations per step)" % (S, S),
+    return {"metric": "MoGAN optimize_parameters frames/s %dx%d (8 RAFT flows x 20 iterations per step)" % (W, H),
             "batch": B, "value": round(B / dt, 2), "unit": "frames/s", "ms_per_step": round(dt * 1e3, 3)}
 
 
@@ -313,26 +315,129 @@ def c3_train_fps(device, B=1, H=436, W=1024, steps=4):
     return {"metric": "C3 train step frames/s %dx%d (CycleGANCon + flow-warp + VGG-19 content/Gram loss)" % (W, H),
             "batch": B, "value": round(B / dt, 3), "unit": "frames/s", "ms_per_step": round(dt * 1e3, 2),
             "tflops_conv_G_D": round(TRAIN_TFLOP_PER_FRAME_C3 / dt, 2),
+            "roofline": _mfma_roofline(TRAIN_TFLOP_PER_FRAME_C3 / dt, "G/D conv FLOPs of the step (14.831 TFLOP/frame, "
+                                       "SURVEY §8d) over the whole step time; the VGG-19 work is not counted"),
+            "loss_weights": {"lambda_content": m.opt.lambda_content, "lambda_style": m.opt.lambda_style},
             "losses": {k: round(v, 4) for k, v in m.get_current_losses().items()}}
 
 
-def inference_fps(device, B=16, reps=10):
+def _g_inference_model(device):
     from gbvst import networks
-    G = networks.define_G(3, 3, 64, "resnet_9blocks", "instance", False, "normal", 0.02,
-                          [device.index or 0])
+    return networks.define_G(3, 3, 64, "resnet_9blocks", "instance", False, "normal", 0.02, [device.index or 0])
+
+
+def _mfma_roofline(tflops, what):
+    """Whole-workload MFMA roofline of an fp32-equivalent (bf16x6) conv path: algorithmic conv
+    TFLOP/s vs the x6 ceiling (dense bf16 peak / 6 products per fp32 MAC)."""
+    peak = BF16_MFMA_PEAK_TFLOPS / 6.0
+    return {"bound": "mfma", "achieved": round(tflops, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
+            "frac": round(tflops / peak, 4), "what": what, "traffic": None}
+
+
+def inference_fps(device, B=16, reps=10, G=None):
+    """Generator-only inference (forward_eval, CycleGAN/models/cycle_gan_model.py:164-171) at 256x256:
+    batch B throughput, plus B=1 per-frame with a device sync after every frame (the reference's DT
+    metric, CycleGAN/sintel_eval.py:210-214, which itself has no sync)."""
+    G = G or _g_inference_model(device)
     x = torch.randn(B, 3, 256, 256, device=device)
+    x1 = x[:1].contiguous()
     with torch.no_grad():
         for _ in range(2):
             G(x)
+            G(x1)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(reps):
             G(x)
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / reps
+        t1 = []
+        for _ in range(3 * reps):
+            a = time.perf_counter()
+            G(x1)
+            torch.cuda.synchronize()
+            t1.append(time.perf_counter() - a)
     fps = B / dt
+    dt1 = sorted(t1)[len(t1) // 2]
+    tf = fps * G_GFLOP_PER_FRAME / 1e3
     return {"metric": "generator-only inference fps 256x256", "batch": B, "value": round(fps, 2),
-            "unit": "frames/s", "tflops": round(fps * G_GFLOP_PER_FRAME / 1e3, 2)}
+            "unit": "frames/s", "tflops": round(tf, 2),
+            "roofline": _mfma_roofline(tf, "whole generator forward, B=%d: 99.10 GFLOP/frame" % B),
+            "batch1": {"value": round(1.0 / dt1, 2), "unit": "frames/s", "ms_per_frame": round(dt1 * 1e3, 3),
+                       "timing": "median of %d single-frame calls, device sync after each" % (3 * reps),
+                       "roofline": _mfma_roofline(G_GFLOP_PER_FRAME / dt1 / 1e3, "B=1 forward")}}
+
+
+def inference_cpu_baseline(device, G=None):
+    """§8(d) CPU leg of generator inference: oracle/cpu_ref.RefResnetGenerator (stock PyTorch NCHW
+    fp32, the reference arithmetic) holding the GPU generator's weights, timed on the host cores at
+    256x256 B=1 and B=16 and 436x1024 B=1; parity = max |GPU - CPU| of the same frames."""
+    from oracle import cpu_ref
+    threads = host_cpus()
+    torch.set_num_threads(threads)
+    G = G or _g_inference_model(device)
+    R = cpu_ref.RefResnetGenerator(3, 3, 64, 9)
+    R.load_state_dict({k: v.detach().cpu() for k, v in G.state_dict().items()})
+    g = torch.Generator().manual_seed(77)
+    out, err = {}, 0.0
+    for name, (B, H, W, reps) in {"256x256_b1": (1, 256, 256, 3), "256x256_b16": (16, 256, 256, 1),
+                                  "436x1024_b1": (1, 436, 1024, 1)}.items():
+        x = torch.rand(B, 3, H, W, generator=g) * 2 - 1
+        with torch.no_grad():
+            y = R(x)                      # warm-up (and the parity frame)
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                R(x)
+            dt = (time.perf_counter() - t0) / reps
+            yg = G(x.to(device)).cpu()
+        err = max(err, (yg - y).abs().max().item())
+        out[name] = {"value": round(B / dt, 3), "unit": "frames/s", "s_per_call": round(dt, 3)}
+    return {"kind": "port", "cores": threads, "sample": "oracle/cpu_ref.RefResnetGenerator forward, torch threads=%d "
+            "(%s); 1 warm-up + timed calls per size" % (threads, cpu_model()), "sizes": out,
+            "parity": {"what": "max |G_gpu(x) - G_cpu(x)| over the timed frames (outputs in [-1, 1])",
+                       "max_abs": err, "bound": 1e-3, "pass": err <= 1e-3}}
+
+
+def c1_faststyle(device, reps=10):
+    """Config C1: the Johnson FastStyleNet (methods/learning-based/network.py:263-298) single 256x256
+    frame forward — on the GPU (HIP) and, as the configuration itself is stated, on PyTorch-CPU (the
+    oracle style_ref.RefFastStyleNet on the host cores), same counter-PRNG weights; parity of the
+    stylised image."""
+    from gbvst import faststyle
+    from oracle import prng, style_ref
+    threads = host_cpus()
+    torch.set_num_threads(threads)
+    ref = style_ref.RefFastStyleNet(3)
+    sd = style_ref.fsn_weights(ref, 5100)
+    style_ref.load_np(ref, sd)
+    net = faststyle.FastStyleNet(3, 1)
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    net = net.to(device)
+    x = torch.from_numpy(prng.uniform_f32(5101, (1, 3, 256, 256)))
+    xd = x.to(device)
+    with torch.no_grad():
+        for _ in range(3):
+            net(xd)
+        torch.cuda.synchronize()
+        t = []
+        for _ in range(reps):
+            a = time.perf_counter()
+            y = net(xd)[1]
+            torch.cuda.synchronize()
+            t.append(time.perf_counter() - a)
+        yr = ref(x)[1]
+        t0 = time.perf_counter()
+        for _ in range(3):
+            ref(x)
+        dtc = (time.perf_counter() - t0) / 3
+    dtg = sorted(t)[len(t) // 2]
+    err = (y.cpu() - yr).abs().max().item() / (yr.abs().max().item())
+    return {"metric": "C1: FastStyleNet 256x256 single-frame forward", "value": round(1.0 / dtg, 2), "unit": "frames/s",
+            "ms_per_frame": round(dtg * 1e3, 3), "cpu_baseline": {"value": round(1.0 / dtc, 3), "unit": "frames/s",
+                                                                  "cores": threads, "kind": "port",
+                                                                  "sample": "oracle/style_ref.RefFastStyleNet, 3 timed "
+                                                                            "forwards after 1 warm-up"},
+            "parity": {"max_rel": err, "bound": 1e-3, "pass": err <= 1e-3}}
 
 
 def host_cpus():
@@ -390,13 +495,19 @@ def cpu_baseline_and_parity(init_sd, batch_cpu, hip_losses0, steps=2):
 
 
 def time_steps(model, steps, hook_g, hook_d, world, device):
+    return time_fn(lambda: model.optimize_parameters(hook_g, hook_d), steps, world, device)
+
+
+def time_fn(step, steps, world, device):
+    """Wall time of exactly `steps` calls of step(), barrier + device sync on both sides, max over
+    ranks."""
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
-        model.optimize_parameters(hook_g, hook_d)
+        step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -416,12 +527,91 @@ MATH_LABEL = {"bf16x6": "fp32 (bf16x6 split products: fp32-equivalent, fp32 accu
               "bf16x3": "bf16x3 split products (~2^-16 relative) in every conv"}
 
 
+def _isolated(fn, *a, **kw):
+    """Run one extra from a clean allocator state (its own warm-up is inside fn), so its value does
+    not depend on which extras ran before it."""
+    import gc
+    gc.collect()
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    t0 = time.perf_counter()
+    r = fn(*a, **kw)
+    torch.cuda.synchronize()
+    r["wall_s"] = round(time.perf_counter() - t0, 2)
+    return r
+
+
+def _line(metric, value, unit, world, args, ms, config, math):
+    return {"metric": metric, "value": round(value, 3), "unit": unit, "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "fp32" if math in ("bf16x6", "fp32") else math,
+            "math": {"policy": math, "conv": MATH_LABEL[math]}, "data": "synthetic (random-init weights)",
+            "config": config}
+
+
+def workload_c4(args, world, rank, local, device):
+    """Config C4: StarGAN (methods/GAN-based/StarGAN/solver.py:241-411) at 256x256, c_dim 4, n_critic 5,
+    B_local images per rank, data parallel: every D iteration (with the WGAN-GP double backward) and
+    every 5th G step exchange their gradients with RCCL all_reduce (dp.GradExchange on the solver's
+    grad_hook).  value = images of all ranks per D iteration / s."""
+    from gbvst import dp, stargan
+    B = args.batch
+    sol = stargan.StarGANSolver(image_size=args.size, c_dim=4, n_critic=5, device=device)
+    if world > 1:
+        dp.broadcast_params([sol.G, sol.D])
+        sol.grad_hook = dp.GradExchange(world).attach([sol.G, sol.D])
+    g = torch.Generator(device="cpu").manual_seed(11 + rank)
+    x = (torch.rand(B, 3, args.size, args.size, generator=g) * 2 - 1).to(device)
+    lo, lt = torch.randint(0, 4, (B,), generator=g), torch.randint(0, 4, (B,), generator=g)
+    for _ in range(max(5, args.warmup)):
+        sol.train_step(x, lo, lt)
+    el = time_fn(lambda: sol.train_step(x, lo, lt), args.steps, world, device)
+    cfg = {"workload": "C4: StarGAN solver iteration (D step + WGAN-GP every iteration, G step every 5th), "
+                       "%dx%d, c_dim 4, conv_dim 64, 6+6 repeats, B_local=%d" % (args.size, args.size, B),
+           "global_batch": B * world, "height": args.size, "width": args.size, "parallelism": "dp%d" % world,
+           "dp_exchange": "RCCL all_reduce of the D (every iteration) and G (every 5th) flat gradients" if world > 1
+           else None}
+    return _line("images/sec: StarGAN train per D iteration (n_critic 5) 256x256", B * world * args.steps / el,
+                 "images/s", world, args, el / args.steps * 1e3, cfg, args.math)
+
+
+def workload_c5(args, world, rank, local, device):
+    """Config C5: Mocycle-GAN (methods/GAN-based/MoGAN/models/cycle_gan_model.py:297-331) at 1024x436,
+    B_local frame pairs per rank, 8 RAFT flows x 20 iterations per optimize_parameters, E-step / M-step
+    alternating, data parallel with the G, D (E-step) and M (M-step) gradients exchanged with RCCL
+    from inside backward (grad_hook_G / _D / _M).  value = frames of all ranks / s."""
+    from gbvst import dp, mogan_model
+    from gbvst.options import default_opt
+    B, H, W = args.batch, 436, 1024
+    m = mogan_model.MoGANModel(default_opt(True, model="mogan", pool_size=args.pool, gpu_ids=[local]))
+    nets = [getattr(m, "net" + n) for n in ("G_A", "G_B", "D_A", "D_B", "M_A", "M_B")]
+    ex = None
+    if world > 1:
+        dp.broadcast_params(nets)
+        ex = dp.GradExchange(world).attach(nets)
+    g = torch.Generator(device="cpu").manual_seed(3 + rank)
+    m.set_input_fc2([(torch.rand(B, 3, H, W, generator=g) * 2 - 1) for _ in range(4)])
+    for _ in range(max(2, args.warmup + args.warmup % 2)):   # even: the timed steps start at an E-step
+        m.optimize_parameters(ex, ex, ex)
+    el = time_fn(lambda: m.optimize_parameters(ex, ex, ex), args.steps, world, device)
+    cfg = {"workload": "C5: MoGAN optimize_parameters (E/M alternating, 8 RAFT flows x 20 iterations), "
+                       "ngf=ndf=64, %dx%d, B_local=%d, pool_size=%d" % (W, H, B, args.pool),
+           "global_batch": B * world, "height": H, "width": W, "parallelism": "dp%d" % world,
+           "dp_exchange": "RCCL all_reduce of G/D (E-step) and M (M-step) buckets launched during backward"
+           if world > 1 else None}
+    return _line("frames/sec: MoGAN train step (RAFT flow) 1024x436", B * world * args.steps / el, "frames/s", world,
+                 args, el / args.steps * 1e3, cfg, args.math)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=4, help="frame pairs per GPU (C2: 4)")
+    ap.add_argument("--workload", choices=["c2", "c4", "c5"], default="c2",
+                    help="c2 (default, the BASELINE metric): CycleGANCon step; c4: StarGAN DP; c5: MoGAN DP")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="per-GPU batch (c2: 4 frame pairs, c4: 4 images, c5: 1 frame pair)")
     ap.add_argument("--size", type=int, default=256)
     ap.add_argument("--pool", type=int, default=50)
     ap.add_argument("--math", default=os.environ.get("VST_CONV_MATH", "bf16x6"),
@@ -429,6 +619,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
     args = ap.parse_args()
+    if args.batch is None:
+        args.batch = {"c2": 4, "c4": 4, "c5": 1}[args.workload]
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -447,6 +639,14 @@ def main():
 
     ops.set_conv_math(args.math)
     torch.manual_seed(0)
+    if args.workload != "c2":
+        out = {"c4": workload_c4, "c5": workload_c5}[args.workload](args, world, rank, local, device)
+        if rank == 0:
+            print(json.dumps(out), flush=True)
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
     opt = default_opt(True, gpu_ids=[local], pool_size=args.pool)
     model = CycleGANModel(opt)
     nets = {"G_A": model.netG_A, "G_B": model.netG_B, "D_A": model.netD_A, "D_B": model.netD_B}
@@ -491,35 +691,42 @@ def main():
                    "global_batch": B * world, "height": S, "width": S, "parallelism": "dp%d" % world,
                    "dp_exchange": "RCCL all_reduce of 8 MiB flat-gradient buckets launched during backward" if world > 1 else None},
         "algorithmic_tflops": round(value * TRAIN_TFLOP_PER_FRAME, 2),
+        "step_roofline": _mfma_roofline(value / world * TRAIN_TFLOP_PER_FRAME,
+                                        "whole train step per GPU: 2.1753 TFLOP/frame of conv work (SURVEY §8d)"),
         "final_losses": {k: round(v, 5) for k, v in losses.items()},
     }
     if rank == 0 and not args.no_extras:
         rl = {k: conv_roofline(k, p, args.math) for k, p in probes.items()}
         # the dominant kernel of the step is conv_fprop_bf_k<256x128> (its forward AND stride-1
-        # data-gradient launches: ~22 ms of the ~72 ms step, profiles/r02_*); its roofline line is
-        # the forward launch (one kernel, whole CU rounds, no tail); the dgrad / wgrad ops (with their
-        # tail / copy / reduce launches) are in roofline_convs
+        # data-gradient launches); its roofline line is the forward launch (one kernel, whole CU
+        # rounds, no tail); the dgrad / wgrad ops (with their tail / copy / reduce launches) are in
+        # roofline_convs
         out["roofline"] = rl["resblock_fprop"] or next(v for v in rl.values() if v)
         out["roofline_convs"] = rl
-        out["inference"] = inference_fps(device)
     if rank == 0 and world == 1 and not args.no_extras:
+        G_inf = _g_inference_model(device)
+        out["inference"] = _isolated(inference_fps, device, G=G_inf)
         # the same step under the round-1 "mixed" policy, separately labelled (not the headline)
         prev = ops.set_conv_math("mixed")
         model.optimize_parameters()
         el = time_steps(model, args.steps, None, None, 1, device)
         out["mixed_policy"] = {"value": round(B * args.steps / el, 3), "unit": "frames/s",
                                "ms_per_step": round(el / args.steps * 1e3, 3), "dtype": "mixed",
-                               "math": MATH_LABEL["mixed"], "inference": inference_fps(device)}
+                               "math": MATH_LABEL["mixed"], "inference": _isolated(inference_fps, device, G=G_inf)}
         ops.set_conv_math(prev)
-        out["extras"] = {"c3_train": c3_train_fps(device),
-                         "sintel_inference": sintel_inference_fps(device),
-                         "warp_roofline": warp_roofline(device),
-                         "raft_corr": corr_volume(device),
-                         "johnson_train": johnson_train_fps(device),
-                         "stargan_train": stargan_train_fps(device),
-                         "raft_sintel": raft_inference(device),
-                         "raft_mogan": raft_inference(device, B=4, H=256, W=256),
-                         "mogan_train": mogan_train_fps(device)}
+        out["extras"] = {"c3_train": _isolated(c3_train_fps, device),
+                         "sintel_inference": _isolated(sintel_inference_fps, device),
+                         "warp_roofline": _isolated(warp_roofline, device),
+                         "raft_corr": _isolated(corr_volume, device),
+                         "c1_faststyle": _isolated(c1_faststyle, device),
+                         "johnson_train": _isolated(johnson_train_fps, device),
+                         "stargan_train": _isolated(stargan_train_fps, device),
+                         "raft_sintel": _isolated(raft_inference, device),
+                         "raft_mogan": _isolated(raft_inference, device, B=4, H=256, W=256),
+                         "mogan_train_c5": _isolated(mogan_train_fps, device, B=1, H=436, W=1024),
+                         "mogan_train": _isolated(mogan_train_fps, device)}
+        if not args.no_cpu_baseline:
+            out["inference"]["cpu_baseline"] = inference_cpu_baseline(device, G=G_inf)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"], out["parity"] = cpu_baseline_and_parity(init_sd, batch_cpu, losses0)
     if rank == 0:

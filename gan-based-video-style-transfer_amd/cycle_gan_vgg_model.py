@@ -30,9 +30,14 @@ class CycleGANVGGModel(CycleGANModel):
     def modify_commandline_options(parser, is_train=True):
         parser = CycleGANModel.modify_commandline_options(parser, is_train)
         if is_train:
-            parser.add_argument('--lambda_content', type=float, default=1.0, help='VGG-19 relu4_1 content weight')
-            parser.add_argument('--lambda_style', type=float, default=0.01,
-                                help='VGG-19 Gram style weight (seeded VGG: the Gram MSE is O(100))')
+            # defaults calibrated for the torchvision-initialised VGG-19 (kaiming fan_out, the net's own
+            # seeded init; pretrained weights are not available offline) on [-1, 1] frames: its Gram
+            # MSE sums to ~2e-3 and the relu4_1 content MSE to ~4e-3, so these weights make both terms
+            # O(0.1-1) beside the cycle losses (~4) at any frame size (the Grams are 1/(h*w)
+            # normalised).  The reduced-size golden (tests/golden/c3_small.npz) was composed with
+            # lambda_content 1, lambda_style 0.01 on a fan_in-initialised VGG whose Grams are ~1e4x larger.
+            parser.add_argument('--lambda_content', type=float, default=100.0, help='VGG-19 relu4_1 content weight')
+            parser.add_argument('--lambda_style', type=float, default=500.0, help='VGG-19 Gram style weight')
             parser.add_argument('--vgg_seed', type=int, default=0, help='seed of the (non-pretrained) VGG-19')
         return parser
 

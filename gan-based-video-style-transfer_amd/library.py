@@ -72,29 +72,38 @@ def _(x, weight, bias, stride, padding, pad_mode):
 
 @torch.library.custom_op("vst::conv2d_backward", mutates_args=())
 def conv2d_backward(grad: Tensor, x: Tensor, weight: Tensor, stride: int, padding: int,
-                    pad_mode: str) -> Tuple[Tensor, Tensor, Tensor]:
-    """(dx, dweight, dbias) of vst::conv2d.  dx: the transposed conv (reflect: stride 1, mirrored
-    contributions gathered in-kernel); dweight: the split-K weight-gradient GEMM; dbias: the
-    per-channel sum of grad."""
+                    pad_mode: str, need_input: bool = True, need_weight: bool = True) -> Tuple[Tensor, Tensor, Tensor]:
+    """(dx, dweight, dbias) of vst::conv2d.  dx: the transposed conv (reflect, stride 1: mirrored
+    contributions gathered in-kernel; reflect, stride > 1: the transposed conv onto the padded frame,
+    then the reflect fold); dweight: the split-K weight-gradient GEMM; dbias: the per-channel sum of
+    grad.  need_input / need_weight = False skip that GEMM (its output is returned as zeros)."""
     _check_pad(pad_mode)
     ops._dev_check(grad, x, weight)
     N, Ci, H, W = x.shape
     Co, _, R, S = weight.shape
-    if pad_mode == "reflect" and stride != 1:
-        raise NotImplementedError("vst::conv2d_backward: reflect padding needs stride 1")
     gy = _nhwc(grad)
-    xn = _nhwc(x)
-    ik = ops.weight_pack(weight.detach().contiguous(), ops.PACK_DGRAD)
-    dxn = ops.conv2d_tfwd(gy, ik, None, H, W, ops.cpad(Ci), R, S, stride, padding, pad_mode=pad_mode)
+    if need_input:
+        ik = ops.weight_pack(weight.detach().contiguous(), ops.PACK_DGRAD)
+        if pad_mode == "reflect" and stride != 1:
+            dxp = ops.conv2d_tfwd(gy, ik, None, H + 2 * padding, W + 2 * padding, ops.cpad(Ci), R, S, stride, 0)
+            dx = ops.nhwc_to_nchw(ops.reflect_fold(dxp, padding), Ci)
+        else:
+            dxn = ops.conv2d_tfwd(gy, ik, None, H, W, ops.cpad(Ci), R, S, stride, padding, pad_mode=pad_mode)
+            dx = ops.nhwc_to_nchw(dxn, Ci)
+    else:
+        dx = torch.zeros_like(x)
     dw = torch.zeros_like(weight)
     db = torch.zeros(Co, device=x.device)
-    ops.conv2d_wgrad(xn, gy, dw, db, R, S, stride, padding, pad_mode, Co, Ci, Ci * R * S, R * S,
-                     accumulate=False)
-    return ops.nhwc_to_nchw(dxn, Ci), dw, db
+    if need_weight:
+        ops.conv2d_wgrad(_nhwc(x), gy, dw, db, R, S, stride, padding, pad_mode, Co, Ci, Ci * R * S, R * S,
+                         accumulate=False)
+    else:
+        ops.channel_sum(gy, db, Co, accumulate=False)
+    return dx, dw, db
 
 
 @conv2d_backward.register_fake
-def _(grad, x, weight, stride, padding, pad_mode):
+def _(grad, x, weight, stride, padding, pad_mode, need_input=True, need_weight=True):
     return torch.empty_like(x), torch.empty_like(weight), weight.new_empty((weight.shape[0],))
 
 
@@ -107,8 +116,10 @@ def _conv2d_setup(ctx, inputs, output):
 def _conv2d_bwd(ctx, grad):
     x, weight = ctx.saved_tensors
     stride, padding, pad_mode, has_bias = ctx.conf
-    dx, dw, db = torch.ops.vst.conv2d_backward(grad.contiguous(), x, weight, stride, padding, pad_mode)
-    return dx, dw, (db if has_bias else None), None, None, None
+    need_x, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+    dx, dw, db = torch.ops.vst.conv2d_backward(grad.contiguous(), x, weight, stride, padding, pad_mode,
+                                               need_x, need_w)
+    return (dx if need_x else None), (dw if need_w else None), (db if has_bias else None), None, None, None
 
 
 conv2d.register_autograd(_conv2d_bwd, setup_context=_conv2d_setup)

@@ -396,7 +396,8 @@ class ResnetGenerator(FlatNet):
             for i in (0, 1):
                 if d[i].weight.shape[0] % 8 == 0:
                     P[f"d{i}ph"] = ops.convT3s2_phase_packs(d[i].weight)
-        if C8_EDGES and c0.weight.shape[1] <= 4:
+        if C8_EDGES and not C4_FWD and c0.weight.shape[1] <= 4:
+            # the 8-channel forward pack is read only when the image conv runs on 8-channel copies
             P["c08"] = ops.weight_pack(c0.weight, ops.PACK_FWD, Ip=8)
         if TAP_LAST:
             P["ftap"] = ops.weight_pack(f.weight, ops.PACK_CK)
@@ -501,7 +502,7 @@ class _GeneratorFn(torch.autograd.Function):
             sv["xt"][id(a)] = at
             return y, s, a
 
-        if "c08" in P and x.shape[-1] == 4:
+        if C8_EDGES and x.shape[-1] == 4 and (C4_FWD or "c08" in P):
             # the 8-channel copy feeds the forward only without C4_FWD, else just c0's weight gradient
             x8 = _pad_channels(x, 8) if (train_w or not C4_FWD) else None
             _, _, b = P["c0"]

@@ -81,7 +81,9 @@ class RefMoGAN:
             setattr(self, "warp_" + other, warp)
             setattr(self, "mask_" + d, mask)
 
-    def optimize_parameters(self):
+    def optimize_parameters(self, grad_hook_G=None, grad_hook_D=None, grad_hook_M=None):
+        """grad_hook_*(nets): called between each phase's backward and its Adam step (the tests read
+        the gradients there, as the HIP model's DP hooks do)."""
         self.forward_train()
         if self.e_step:
             self._req([self.D_A, self.D_B], False)
@@ -99,11 +101,15 @@ class RefMoGAN:
             loss = (self.loss_G_A + self.loss_G_B + self.loss_cycle_A + self.loss_cycle_B + self.loss_idt_A
                     + self.loss_idt_B + self.loss_MC_A + self.loss_MC_B + self.loss_MT_A + self.loss_MT_B)
             loss.backward()
+            if grad_hook_G is not None:
+                grad_hook_G([self.G_A, self.G_B])
             self.opt_G.step()
             self._req([self.D_A, self.D_B], True)
             self.opt_D.zero_grad()
             self.loss_D_A = cpu_ref.RefCycleGANCon._backward_D(self.D_A, self.real_B, self.fake_B)
             self.loss_D_B = cpu_ref.RefCycleGANCon._backward_D(self.D_B, self.real_A, self.fake_A)
+            if grad_hook_D is not None:
+                grad_hook_D([self.D_A, self.D_B])
             self.opt_D.step()
             self._req([self.M_A, self.M_B], True)
             self._req([self.G_A, self.G_B], False)
@@ -114,6 +120,8 @@ class RefMoGAN:
             self.loss_AM_A = torch.abs(self.bf_M_A - self.bf_fake_B).mean() * self.lAM
             self.loss_AM_B = torch.abs(self.bf_M_B - self.bf_fake_A).mean() * self.lAM
             (self.loss_AM_A + self.loss_AM_B).backward()
+            if grad_hook_M is not None:
+                grad_hook_M([self.M_A, self.M_B])
             self.opt_M.step()
             self._req([self.M_A, self.M_B], False)
             self._req([self.G_A, self.G_B], True)

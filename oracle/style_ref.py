@@ -236,12 +236,22 @@ def np_state(net):
 
 
 # ------------------------------------------------------------------- fixture weights (PRNG)
-def vgg_weights(net, base):
+def vgg_weights(net, base, init="fan_in"):
+    """Counter-PRNG VGG state_dict.  init "fan_in": N(0, 2/fan_in) weights, N(0, 0.05) biases (the
+    golden fixtures); "fan_out": torchvision's VGG init, kaiming_normal_(fan_out, relu) weights and
+    zero biases — the scale the HIP model's own seeded Vgg16/Vgg19 use (perceptual.py)."""
     sd = {}
     for k, v in net.state_dict().items():
-        fan_in = int(np.prod(v.shape[1:])) if v.dim() > 1 else 1
-        std = (2.0 / fan_in) ** 0.5 if k.endswith("weight") else 0.05
-        sd[k] = _prng().normal(_prng().seed_for(k, base), tuple(v.shape), std=std)
+        if init == "fan_out":
+            fan = int(v.shape[0] * np.prod(v.shape[2:])) if v.dim() > 1 else 1
+            std = (2.0 / fan) ** 0.5
+        else:
+            fan = int(np.prod(v.shape[1:])) if v.dim() > 1 else 1
+            std = (2.0 / fan) ** 0.5 if k.endswith("weight") else 0.05
+        if init == "fan_out" and not k.endswith("weight"):
+            sd[k] = np.zeros(tuple(v.shape), np.float32)
+        else:
+            sd[k] = _prng().normal(_prng().seed_for(k, base), tuple(v.shape), std=std)
     return sd
 
 

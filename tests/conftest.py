@@ -56,3 +56,9 @@ def train_math(request):
 @pytest.fixture(params=OP_MATHS + ["mixed"])
 def infer_math(request):
     yield from _math_fixture(request)
+
+
+@pytest.fixture(params=["bf16x6", "mixed"])
+def prod_math(request):
+    """The policies bench.py measures (bf16x6 headline, mixed labelled): the full-size parity tests."""
+    yield from _math_fixture(request)

@@ -53,11 +53,18 @@ def _oracle(g, dtype, perturb=0.0):
     return np.array(out), probe
 
 
+def c3_lambdas():
+    from oracle import c3_ref
+    return c3_ref.LAMBDA_C, c3_ref.LAMBDA_S
+
+
 def _hip_model(gb, ngf, ndf, pool=0):
     from gbvst.cycle_gan_vgg_model import CycleGANVGGModel
     from gbvst.options import default_opt
     from oracle import cpu_ref, prng, style_ref
-    m = CycleGANVGGModel(default_opt(True, model="cycle_gan_vgg", ngf=ngf, ndf=ndf, pool_size=pool, gpu_ids=[0]))
+    # the golden's composition weights (oracle/c3_ref.LAMBDA_*), not the model's calibrated defaults
+    m = CycleGANVGGModel(default_opt(True, model="cycle_gan_vgg", ngf=ngf, ndf=ndf, pool_size=pool, gpu_ids=[0],
+                                     lambda_content=c3_lambdas()[0], lambda_style=c3_lambdas()[1]))
     m.netVGG.load_state_dict({k: torch.from_numpy(v) for k, v in style_ref.vgg_weights(m.netVGG, 530).items()})
     for name, seed in SEEDS.items():
         net = getattr(m, "net" + name)

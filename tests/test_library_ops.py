@@ -67,6 +67,7 @@ CONV_CASES = [  # (N, Ci, Co, H, k, stride, pad, pad_mode, bias)
     (2, 3, 64, 20, 7, 1, 3, "reflect", True),      # c7s1-64
     (2, 64, 128, 16, 4, 2, 1, "zero", True),       # PatchGAN s2
     (1, 32, 8, 12, 3, 1, 1, "zero", False),
+    (2, 16, 32, 16, 3, 2, 1, "reflect", True),     # strided reflect: padded-frame dgrad + fold
 ]
 
 
@@ -86,8 +87,6 @@ def test_conv2d_vs_torch(case, gpu_fp32_math):
     assert y.shape == yr.shape
     assert _rel(y, yr) < 2e-5
     gy = torch.randn(y.shape, generator=g).cuda()
-    if mode == "reflect" and st != 1:
-        return
     y.backward(gy)
     yr.backward(gy)
     assert _rel(x.grad, xr.grad) < 2e-5
@@ -182,3 +181,26 @@ def test_warp_fbcheck_temporal_gram_adam():
     opt.step()
     torch.ops.vst.adam_(p, gr, m, v, 2e-4, 0.5, 0.999, 1e-8, 1)
     assert _rel(p, pt.detach()) < 1e-6
+
+
+@pytest.mark.gpu
+def test_conv2d_backward_skips_unneeded_gemms(gpu_fp32_math):
+    """a frozen weight gets no weight-gradient GEMM (and no dw), an input without
+    requires_grad no data-gradient conv; the remaining gradients are unchanged."""
+    from unittest import mock
+    from gbvst import ops
+    g = torch.Generator().manual_seed(9)
+    x = torch.randn(2, 16, 12, 12, generator=g).cuda()
+    w = (torch.randn(32, 16, 3, 3, generator=g) * 0.05).cuda()
+    b = (torch.randn(32, generator=g) * 0.1).cuda()
+    xr, wr, br = x.clone().requires_grad_(True), w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    F.conv2d(F.pad(xr, (1,) * 4, mode="reflect"), wr, br).sum().backward()
+    xg = x.clone().requires_grad_(True)
+    bg = b.clone().requires_grad_(True)
+    with mock.patch.object(ops, "conv2d_wgrad", side_effect=AssertionError("wgrad ran")):
+        torch.ops.vst.conv2d(xg, w, bg, 1, 1, "reflect").sum().backward()
+    assert _rel(xg.grad, xr.grad) < 2e-5 and _rel(bg.grad, br.grad) < 1e-5
+    wg = w.clone().requires_grad_(True)
+    with mock.patch.object(ops, "conv2d_tfwd", side_effect=AssertionError("dgrad ran")):
+        torch.ops.vst.conv2d(x, wg, None, 1, 1, "reflect").sum().backward()
+    assert _rel(wg.grad, wr.grad) < 2e-5

@@ -135,8 +135,11 @@ extern "C" int vst_gram(const float* f, float* G, int B, int HW, int C, float* w
   return vst_axpby(G, G, (long)B * C * C, 1.0f / (float)HW, 0.0f, stream);
 }
 
+// level-0 plane stride of the pyramid: H*W rounded up to a multiple of 4 (raft_corr.CorrBlock's cpad)
+static long corr_ld0(long HW) { return (HW + 3) / 4 * 4; }
+
 extern "C" size_t vst_corr_volume_ws_bytes(int B, int H, int W, int Dp) {
-  const long HW = (long)H * W, ld0 = vst_cp_ld(HW);
+  const long HW = (long)H * W, ld0 = corr_ld0(HW);
   (void)B;
   // fmap1 / sqrt(D) (one image), fmap2 rows padded to ld0, its three bf16 planes
   return (size_t)(HW * Dp + ld0 * Dp) * sizeof(float) + (size_t)3 * ld0 * Dp * 2;
@@ -149,7 +152,7 @@ extern "C" int vst_corr_volume(const float* f1, const float* f2, float* pyr, int
               "corr_volume: bad arguments");
   VST_REQUIRE(ws_bytes >= vst_corr_volume_ws_bytes(B, H, W, Dp), "corr_volume: workspace too small");
   hipStream_t s = (hipStream_t)stream;
-  const long HW = (long)H * W, ld0 = vst_cp_ld(HW);
+  const long HW = (long)H * W, ld0 = corr_ld0(HW);
   float* f1s = ws;
   float* wp = ws + HW * Dp;
   void* planes = wp + ld0 * Dp;

@@ -58,6 +58,15 @@
 #ifndef VST_M16_SCHED
 #define VST_M16_SCHED 0  // M16 loop: sched_group_barrier filler pattern (0: compiler order)
 #endif
+#ifndef VST_M16_LOADFIRST
+#define VST_M16_LOADFIRST 0  // M16 loop: scheduling fence after group A (its global loads issue before group B's stores)
+#endif
+#ifndef VST_M16_PRIO
+#define VST_M16_PRIO 0  // M16 loop: s_setprio 1 for the second-dispatched half of the waves
+#endif
+#ifndef VST_M16_LOADEARLY
+#define VST_M16_LOADEARLY 0  // M16 loop: the next stages' loads first in the step, fenced
+#endif
 #ifndef VST_BF_SPLITK
 #define VST_BF_SPLITK 1  // split-K wave-quantisation tails (when the caller passes a workspace)
 #endif
@@ -72,6 +81,9 @@
 #endif
 #ifndef VST_BF_STORE_LATE
 #define VST_BF_STORE_LATE 0
+#endif
+#ifndef VST_BF_LDS_EPI
+#define VST_BF_LDS_EPI 0  // M16 forward epilogue: tile staged through LDS, stored as whole float4 rows
 #endif
 
 namespace vst {
@@ -402,6 +414,7 @@ __device__ __forceinline__ void main_loop16(char* smem, int nk, f32x4v (&acc)[T:
   if (nk <= 0) return;
   constexpr int NM = T::MI16 * T::NI16, NR = T::MI16 + T::NI16;
   constexpr int NV = T::A_LD * 2 + T::B_LD * T::NP, NW = T::A_LD * T::NP + T::B_LD * T::NP;
+  if (VST_M16_PRIO && wave >= T::NW / 2) __builtin_amdgcn_s_setprio(1);
   load_all(0);
   store_stage<T>(smem, ra[0], rbv[0], rb, kq);
   adv(nk > 1);
@@ -414,13 +427,21 @@ __device__ __forceinline__ void main_loop16(char* smem, int nk, f32x4v (&acc)[T:
     const char* cur = smem + P * T::STAGE;
     char* nxt = smem + (P ^ 1) * T::STAGE;
     constexpr bool SA = VST_M16_STORE == 1, RA = VST_M16_RDLO == 1;
+    if (VST_M16_LOADEARLY) {
+      adv(kt + 2 < nk);
+      load_all(P);
+      __builtin_amdgcn_sched_barrier(0);
+    }
     read_plane16<T>(hi, cur, 0, wm0, wn0, lane);
     if (RA) read_plane16<T>(lo, cur, 2, wm0, wn0, lane);
-    adv(kt + 2 < nk);
-    load_all(P);
+    if (!VST_M16_LOADEARLY) {
+      adv(kt + 2 < nk);
+      load_all(P);
+    }
     if (SA) store_stage<T>(nxt, ra[P ^ 1], rbv[P ^ 1], rb, kq);
     mma16<T>(mid, mid, acc);
     if (VST_M16_SCHED) sched16<NM, RA ? 2 * NR : NR, NV, SA ? 4 : 0, SA ? NW : 0>();
+    if (VST_M16_LOADFIRST) __builtin_amdgcn_sched_barrier(0);
     if (!RA) read_plane16<T>(lo, cur, 2, wm0, wn0, lane);
     if (!SA) store_stage<T>(nxt, ra[P ^ 1], rbv[P ^ 1], rb, kq);
     mma16<T>(mid, hi, acc);
@@ -682,6 +703,12 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_k(
     // 16x16 blocks: lane holds column lane & 15, rows 4 (lane >> 4) + r.  IN partials per 32-row
     // group (block pair 2g, 2g+1): per-lane fixed-order fp64 sums, then over the four lanes of a
     // column (xor 16, xor 32).
+    // LDS_EPI: the activated tile goes to LDS (row stride BN + 16 floats: the two rows of a 32-lane
+    // write group land 16 banks apart) and leaves as whole float4 rows (coalesced stores).
+    constexpr bool LEPI = VST_BF_LDS_EPI && T::BM * (T::BN + 16) * 4 <= 2 * T::STAGE;
+    constexpr int LDE = T::BN + 16;
+    float* ept = reinterpret_cast<float*>(smem);
+    if (LEPI) __syncthreads();  // every wave is done reading the last stage
 #pragma unroll
     for (int g = 0; g < T::MI16 / 2; ++g)
 #pragma unroll
@@ -696,7 +723,10 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_k(
           for (int r = 0; r < 4; ++r) {
             const int mm = m0 + wm0 + 16 * (2 * g + h) + 4 * (lane >> 4) + r;
             const float v = apply_act(acc[2 * g + h][j][r] + bv, act, slope);
-            if (nok && mm < M) y[(long)mm * Cop + n] = v;
+            if (LEPI)
+              ept[(mm - m0) * LDE + (n - n0)] = v;
+            else if (nok && mm < M)
+              y[(long)mm * Cop + n] = v;
             s1 += v;
             s2 += (double)v * v;
           }
@@ -714,6 +744,17 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_k(
           }
         }
       }
+    if (LEPI) {
+      __syncthreads();
+      constexpr int C4 = T::BN / 4;
+#pragma unroll 4
+      for (int idx = t; idx < T::BM * C4; idx += T::NT) {
+        const int row = idx / C4, c = 4 * (idx - row * C4);
+        const int mm = m0 + row, n = n0 + c;
+        if (mm < M && n < Cop)
+          *reinterpret_cast<float4*>(y + (long)mm * Cop + n) = *reinterpret_cast<const float4*>(ept + row * LDE + c);
+      }
+    }
     return;
   }
   f32x16 acc[T::MI][T::NI];

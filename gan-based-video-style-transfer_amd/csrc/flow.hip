@@ -81,34 +81,55 @@ __device__ __forceinline__ bool warp_valid(const Bilin& b, int H, int W) {
   return !(m < 0.9999f) && m > 0.f;
 }
 
-// out (NHWC, Cs channels, processed 4 at a time) = warp(x, flow) (MASKED: * fs_lib validity mask)
-template <int MASKED>
-__global__ void warp_fwd_k(const float* __restrict__ x, const float* __restrict__ flow,
-                           float* __restrict__ out, int N, int H, int W, int C4, int align) {
-  const long total = (long)N * H * W * C4;
-  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= total) return;
-  const int c4 = i % C4;
-  const long pix = i / C4;
-  const int w = pix % W, h = (pix / W) % H, n = pix / ((long)W * H);
-  const long fo = (long)n * 2 * H * W + (long)h * W + w;
-  const Bilin b = bilin(h, w, flow[fo], flow[fo + (long)H * W], H, W, align);
+// out (NHWC, Cs channels, processed 4 at a time) = warp(x, flow) (MASKED: * fs_lib validity mask).
+// Grid (ceil(W*C4 / 256), H, N): image and row come from the block index and the thread's pixel and
+// channel chunk from a 32-bit split of its row offset (CT = C4 at compile time for the common widths,
+// 0 = runtime), so no thread pays 64-bit divisions; a row's threads read its flow values once per
+// pixel (broadcast within the pixel's C4 lanes) and gather each corner as C4 contiguous float4s.
+template <int MASKED, int CT>
+__global__ __launch_bounds__(256) void warp_fwd_k(const float* __restrict__ x, const float* __restrict__ flow,
+                                                  float* __restrict__ out, int N, int H, int W, int C4_, int align) {
+  const int C4 = CT ? CT : C4_;
+  const int local = blockIdx.x * 256 + threadIdx.x;
+  if (local >= W * C4) return;
+  const int h = blockIdx.y, n = blockIdx.z;
+  const int w = CT == 1 ? local : local / C4, c4 = CT == 1 ? 0 : local - w * C4;
+  const long plane = (long)H * W;
+  const long fo = (long)n * 2 * plane + (long)h * W + w;
+  const Bilin b = bilin(h, w, flow[fo], flow[fo + plane], H, W, align);
+  float4* op = reinterpret_cast<float4*>(out) + ((long)n * plane + (long)h * W) * C4 + local;
   if (MASKED && !warp_valid(b, H, W)) {
-    reinterpret_cast<float4*>(out)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    *op = make_float4(0.f, 0.f, 0.f, 0.f);
     return;
   }
-  const float4* xs = reinterpret_cast<const float4*>(x) + (long)n * H * W * C4 + c4;
+  const float4* xs = reinterpret_cast<const float4*>(x) + (long)n * plane * C4 + c4;
   float4 v_nw = make_float4(0, 0, 0, 0), v_ne = v_nw, v_sw = v_nw, v_se = v_nw;
-  if (inb(b.y0, b.x0, H, W)) v_nw = xs[((long)b.y0 * W + b.x0) * C4];
-  if (inb(b.y0, b.x0 + 1, H, W)) v_ne = xs[((long)b.y0 * W + b.x0 + 1) * C4];
-  if (inb(b.y0 + 1, b.x0, H, W)) v_sw = xs[((long)(b.y0 + 1) * W + b.x0) * C4];
-  if (inb(b.y0 + 1, b.x0 + 1, H, W)) v_se = xs[((long)(b.y0 + 1) * W + b.x0 + 1) * C4];
+  const int r0 = b.y0 * W, r1 = r0 + W;
+  if (inb(b.y0, b.x0, H, W)) v_nw = xs[(long)(r0 + b.x0) * C4];
+  if (inb(b.y0, b.x0 + 1, H, W)) v_ne = xs[(long)(r0 + b.x0 + 1) * C4];
+  if (inb(b.y0 + 1, b.x0, H, W)) v_sw = xs[(long)(r1 + b.x0) * C4];
+  if (inb(b.y0 + 1, b.x0 + 1, H, W)) v_se = xs[(long)(r1 + b.x0 + 1) * C4];
   float4 o;
   o.x = bilerp(v_nw.x, v_ne.x, v_sw.x, v_se.x, b.nw, b.ne, b.sw, b.se);
   o.y = bilerp(v_nw.y, v_ne.y, v_sw.y, v_se.y, b.nw, b.ne, b.sw, b.se);
   o.z = bilerp(v_nw.z, v_ne.z, v_sw.z, v_se.z, b.nw, b.ne, b.sw, b.se);
   o.w = bilerp(v_nw.w, v_ne.w, v_sw.w, v_se.w, b.nw, b.ne, b.sw, b.se);
-  reinterpret_cast<float4*>(out)[i] = o;
+  *op = o;
+}
+
+template <int MASKED>
+static int warp_fwd_launch(const float* x, const float* flow, float* out, int N, int H, int W, int Cs, int align,
+                           hipStream_t s) {
+  VST_REQUIRE(H <= 65535 && N <= 65535 && (long)W * (Cs / 4) < (1L << 31), "warp_fwd: grid too large");
+  const int C4 = Cs / 4;
+  const dim3 grid(ceil_div((long)W * C4, 256), H, N);
+#define VST_WARP(CT) hipLaunchKernelGGL((warp_fwd_k<MASKED, CT>), grid, dim3(256), 0, s, x, flow, out, N, H, W, C4, align)
+  if (C4 == 1) VST_WARP(1);
+  else if (C4 == 16) VST_WARP(16);
+  else if (C4 == 32) VST_WARP(32);
+  else VST_WARP(0);
+#undef VST_WARP
+  return VST_OK;
 }
 
 template <int MASKED>
@@ -233,18 +254,14 @@ using namespace vst;
 extern "C" int vst_warp_fwd(const float* x, const float* flow, float* out, int N, int H, int W,
                             int Cs, int align_corners, void* stream) {
   VST_REQUIRE(x && flow && out && Cs % 4 == 0 && N > 0 && H > 0 && W > 0, "warp_fwd: bad args");
-  const long total = (long)N * H * W * (Cs / 4);
-  hipLaunchKernelGGL(warp_fwd_k<0>, dim3(ceil_div(total, 256)), dim3(256), 0, (hipStream_t)stream, x,
-                     flow, out, N, H, W, Cs / 4, align_corners);
+  if (int e = warp_fwd_launch<0>(x, flow, out, N, H, W, Cs, align_corners, (hipStream_t)stream)) return e;
   return check_launch("warp_fwd");
 }
 
 extern "C" int vst_warp_masked_fwd(const float* x, const float* flow, float* out, int N, int H, int W,
                                    int Cs, int align_corners, void* stream) {
   VST_REQUIRE(x && flow && out && Cs % 4 == 0 && N > 0 && H > 0 && W > 0, "warp_masked_fwd: bad args");
-  const long total = (long)N * H * W * (Cs / 4);
-  hipLaunchKernelGGL(warp_fwd_k<1>, dim3(ceil_div(total, 256)), dim3(256), 0, (hipStream_t)stream, x,
-                     flow, out, N, H, W, Cs / 4, align_corners);
+  if (int e = warp_fwd_launch<1>(x, flow, out, N, H, W, Cs, align_corners, (hipStream_t)stream)) return e;
   return check_launch("warp_masked_fwd");
 }
 

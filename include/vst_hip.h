@@ -541,8 +541,8 @@ int vst_adam_multi_tensor(float* const* p, const float* const* g, float* const* 
 size_t vst_gram_ws_bytes(int HW, int C);
 int vst_gram(const float* f, float* G, int B, int HW, int C, float* ws, size_t ws_bytes, int math, void* stream);
 /* CorrBlock volume + pyramid (corr.py:12-60) from NHWC fmaps [B][H][W][Dp] (D logical channels);
- * sqrt_d: device array of D floats = sqrt(D); pyr: vst_corr_pyramid_floats(B*H*W, H, W, vst_cp_ld(H*W),
- * levels) floats. */
+ * sqrt_d: device array of D floats = sqrt(D); pyr: vst_corr_pyramid_floats(B*H*W, H, W, ld0, levels) floats
+ * with the level-0 plane stride ld0 = H*W rounded up to a multiple of 4. */
 size_t vst_corr_volume_ws_bytes(int B, int H, int W, int Dp);
 int vst_corr_volume(const float* f1, const float* f2, float* pyr, int B, int H, int W, int Dp, int D,
                     const float* sqrt_d, int levels, float* ws, size_t ws_bytes, int math, void* stream);

@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out/${TAG:-r03a}
 mkdir -p $OUT
 PYT="python -u -m pytest -x -v --timeout 900 --timeout-method thread"
-timeout -k 10 900 $PYT -m gpu tests/test_gpu_abi.py tests/test_gpu_dp.py tests/test_library_ops.py tests/test_gpu_fullsize.py > $OUT/pytest_new.log 2>&1 || { echo "new tests failed"; tail -40 $OUT/pytest_new.log; exit 1; }
+timeout -k 10 900 ${PYT/ -x/} -m gpu tests/test_gpu_abi.py tests/test_gpu_dp.py tests/test_library_ops.py tests/test_gpu_fullsize.py > $OUT/pytest_new.log 2>&1 || { echo "new tests failed"; tail -40 $OUT/pytest_new.log; exit 1; }
 tail -3 $OUT/pytest_new.log
 if [ -n "$FULL" ]; then
   timeout -k 10 900 $PYT -m gpu tests > $OUT/pytest.log 2>&1 || { echo "pytest failed"; tail -30 $OUT/pytest.log; exit 1; }

@@ -44,4 +44,34 @@ for B in [int(b) for b in os.environ.get("KB_B", "8,12").split(",")]:
         us = sorted(ts)[2]
         out["%s_N%d_us" % (name, B)] = round(us, 1)
         out["%s_N%d_TF" % (name, B)] = round(flop / us / 1e6, 1)
+if os.environ.get("KB_EXTRA", "1") != "0":
+    # the image-side 7x7 forward (generator c0: 3(+1) -> 64 channels, reflect 3) at N=8, 256x256, and
+    # the warp kernel at bench.py's roofline shape
+    def _t(fn, reps=10):
+        for _ in range(3):
+            fn()
+        ts = []
+        for _ in range(3):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(reps):
+                fn()
+            e1.record()
+            e1.synchronize()
+            ts.append(e0.elapsed_time(e1) / reps * 1e3)
+        return round(sorted(ts)[1], 1)
+    x4 = torch.randn(8, 256, 256, 4, device=dev)
+    x4[..., 3] = 0
+    w0 = torch.randn(64, 3, 7, 7, device=dev) * 0.05
+    k0 = ops.weight_pack(w0, ops.PACK_FWD)
+    b0 = torch.zeros(64, device=dev)
+    out["c0fwd_N8_us"] = _t(lambda: ops.conv2d_fwd_in(x4, k0, b0, 64, 7, 7, 1, 3, "reflect"))
+    xw = torch.randn(32, 436, 1024, 64, device=dev)
+    fl = torch.randn(32, 2, 436, 1024, device=dev) * 3.0
+    ow = torch.empty_like(xw)
+    us = _t(lambda: ops.lib().vst_warp_fwd(xw.data_ptr(), fl.data_ptr(), ow.data_ptr(), 32, 436, 1024, 64, 0,
+                                            torch.cuda.current_stream().cuda_stream), reps=5)
+    out["warp_us"] = us
+    out["warp_TBs"] = round(32 * 436 * 1024 * (8.0 * 64 + 8.0) / us / 1e6, 3)
+    del xw, fl, ow
 print(json.dumps(out), flush=True)

@@ -84,7 +84,7 @@ def _time_on_stream(fn, reps, warm=3):
 def DOMINANT_KEYS(B):
     N = 2 * B
     return {"resblock_fprop": ("fwd", (N, 64, 64, 256, 256, 3, 1, 1, "reflect")),
-            "resblock_dgrad": ("fwd", (N, 64, 64, 256, 256, 3, 1, 2, "zero")),
+            "resblock_dgrad": ("dgrad", (N, 64, 64, 256, 256, 3, 1, 1, "reflect")),
             "resblock_wgrad": ("wgrad", (N, 64, 64, 256, 256, 3, 1, 1, "reflect"))}
 
 
@@ -139,6 +139,11 @@ def conv_roofline(name, probe, math):
         key = {"math": m, "tile": kind, "m_split": ms_, "N": N, "mfma": _mfma(m), "ksplit": ks}
         note = ("stride-1 data gradient as a forward conv over the rotated taps (66x66 padded frame)"
                 if name == "resblock_dgrad" else "ResnetBlock conv forward")
+    elif op == "dgrad":
+        kernel = ("vst_conv2d_dgrad_refl: conv_fprop_bf_k interior (zero pad 1, %s) + border rows as "
+                  "split-K conv_fprop_bf_k<REFL=4> + dgrad_border_add_k [%s]" % (m, _mfma(m)))
+        key = {"math": m, "N": N, "mfma": _mfma(m), "op": "dgrad_refl"}
+        note = "stride-1 reflect data gradient: interior conv + border GEMM (no padded frame, no fold)"
     else:
         kernel = ("vst_conv2d_wgrad: nhwc_to_cp_pad_k + nhwc_to_cp_planes_k copies + conv_wgrad_bf_k "
                   "(split-K slabs) + wgrad_reduce_store_k, %s" % m if m != "fp32" else

@@ -130,6 +130,8 @@ SIGNATURES = {
     "vst_raft_coords_update": (I, [P, P, I, I, I, I, P]),
     "vst_raft_upsample": (I, [P, P, I, P, I, I, I, P]),
     "vst_u8_image_to_nhwc4": (I, [P, P, L, P]),
+    "vst_conv2d_dgrad_refl_ws_bytes": (SZ, [I, I, I, I, I, I]),
+    "vst_conv2d_dgrad_refl": (I, [P, P, P, P, P, SZ, I, I, I, I, I, I, P]),
     # SURVEY §8b spelling (abi.hip)
     "vst_conv_desc_out_hw": (I, [P, P, P]),
     "vst_workspace_size": (SZ, [P, I]),

@@ -97,7 +97,7 @@ long rk_cp_ld(long P);
 int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* bias, float* y, int N,
                     int H, int W, int C, int Ho, int Wo, int Cop, int R, int S, int st, int padh, int padw,
                     int reflect, int act, float slope, int math, int kind, hipStream_t s,
-                    double* part = nullptr, float* tws = nullptr, size_t tws_floats = 0);
+                    double* part = nullptr, float* tws = nullptr, size_t tws_floats = 0, const float* addend = nullptr);
 size_t bf_fprop_ws_floats(long M, int Cop, int C, int R, int S, int math);
 int bf_tail_ks(long M, int Cop, int m_split, int nk);
 void bf_split_plan(long M, int Cop, int C, int R, int S, int math, int kind, int* m_first, int* ks_out);

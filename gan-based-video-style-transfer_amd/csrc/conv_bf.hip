@@ -496,6 +496,92 @@ __device__ __forceinline__ void tile_of(int L, int Mt, int Nt, int& mt, int& nt)
   nt = t - mt * Nt;
 }
 
+// ---------------------------------------------------------- reflect-pad-1 data gradient border
+// The data gradient of ReflectionPad2d(1) + 3x3 conv (stride 1) on an H x W map is
+//   dx(j) = sum over padded positions q with r(q) = j of dxp(q),   r(-1) = 1, r(H) = H - 2,
+// dxp = the full correlation of dy with the rotated taps (a 3x3 conv of dy with zero padding 2).
+// The interior term dxp(j), j in H x W, is the zero-pad-1 forward conv over dy (one exact grid: for
+// N = 8 at 64 x 64 the 256x128 tiles make one whole CU round).  The 2(H+W)+4 padded border
+// positions q add into the rows / columns 1 and H-2 / W-2: this map orders them per image as
+//   rows [0, S):   single targets — top (q = (-1, w)), bottom (q = (H, w)) for w not in {1, W-2},
+//                  then left (q = (h, -1)), right (q = (h, W)) for h not in {1, H-2};
+//   rows [S, S4):  padding to a multiple of 4 (no position);
+//   rows S4 + 4g + {0, 1, 2}: the three positions of corner target g (g: (1,1), (1,W-2), (H-2,1),
+//                  (H-2,W-2)), + 4g + 3 none — a 4-row group sits in one lane's accumulator rows.
+// S = 2 (W - 2) + 2 (H - 2), S4 = S rounded up to a multiple of 4, rows per image S4 + 16.
+// (qh, qw) = the padded position (-100 for none: every tap gathers zeros), (th, tw) its target.
+__host__ __device__ __forceinline__ int dgrad_border_rows(int H, int W) {
+  return ((2 * (W - 2) + 2 * (H - 2) + 3) / 4) * 4 + 16;
+}
+
+__host__ __device__ __forceinline__ void dgrad_border_pos(int b, int H, int W, int& qh, int& qw, int& th, int& tw) {
+  const int sw = W - 2, sh = H - 2, S = 2 * sw + 2 * sh, S4 = (S + 3) / 4 * 4;
+  qh = qw = th = tw = -100;
+  if (b < 2 * sw) {  // top / bottom
+    const int k = b < sw ? b : b - sw;
+    tw = k == 0 ? 0 : (k == sw - 1 ? W - 1 : k + 1);
+    qw = tw;
+    qh = b < sw ? -1 : H;
+    th = b < sw ? 1 : H - 2;
+    return;
+  }
+  if (b < S) {  // left / right
+    const int b2 = b - 2 * sw, k = b2 < sh ? b2 : b2 - sh;
+    th = k == 0 ? 0 : (k == sh - 1 ? H - 1 : k + 1);
+    qh = th;
+    qw = b2 < sh ? -1 : W;
+    tw = b2 < sh ? 1 : W - 2;
+    return;
+  }
+  if (b < S4) return;
+  const int g = (b - S4) >> 2, r = (b - S4) & 3;
+  if (r == 3) return;
+  const int top = g < 2, left = (g & 1) == 0;
+  th = top ? 1 : H - 2;
+  tw = left ? 1 : W - 2;
+  const int ph = top ? -1 : H, pw = left ? -1 : W;  // the out-of-frame row / column
+  if (r == 0) { qh = ph; qw = tw; }
+  else if (r == 1) { qh = ph; qw = pw; }
+  else { qh = th; qw = pw; }
+}
+
+// dx[n][th][tw][c] += the border rows' GEMM result (split slabs summed in order); a corner target's
+// three rows are summed in row order by one thread.  grid (ceil(N*NB / 16), ceil(C / 64)): thread
+// (one of 16 rows, 4-channel group); every dx element has exactly one writer.  The slab loads of a
+// row are issued together (up to 16 splits in flight per thread).
+__global__ __launch_bounds__(256) void dgrad_border_add_k(const float* __restrict__ slab, int ks, int Mb, int C,
+                                                          float* __restrict__ dx, int H, int W, int NB) {
+  const int t = threadIdx.x;
+  const int c = blockIdx.y * 64 + (t & 15) * 4;
+  const int m = blockIdx.x * 16 + (t >> 4);
+  if (m >= Mb || c >= C) return;
+  const int n = m / NB, b = m - n * NB;
+  int qh, qw, th, tw;
+  dgrad_border_pos(b, H, W, qh, qw, th, tw);
+  if (th < 0) return;
+  const int S4 = NB - 16;
+  if (b >= S4 && ((b - S4) & 3) != 0) return;
+  const int nr = b >= S4 ? 3 : 1;
+  const long zst = (long)Mb * C;
+  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int r = 0; r < nr; ++r) {
+    const float* base = slab + (long)(m + r) * C + c;
+    float4 u[16];
+#pragma unroll
+    for (int z = 0; z < 16; ++z)
+      if (z < ks) u[z] = *reinterpret_cast<const float4*>(base + z * zst);
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int z = 0; z < 16; ++z)
+      if (z < ks) add_f4(acc, u[z]);
+    add_f4(v, acc);
+  }
+  float4* d = reinterpret_cast<float4*>(dx + (((long)n * H + th) * W + tw) * C + c);
+  float4 o = *d;
+  add_f4(o, v);
+  *d = o;
+}
+
 // ------------------------------------------------------------------------------------------ fprop
 // Target of every masked A gather (zero-padding taps, the K tail): loads from it return zeros, so
 // the stage writer needs no per-row select.  Never written.
@@ -527,8 +613,9 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_k(
     const float* __restrict__ x, const __bf16* __restrict__ ws, long wps, const float* __restrict__ bias,
     float* __restrict__ y, int H, int W, int C, int Ho, int Wo, int Cop, int S, int st, int padh,
     int padw, int reflect, int act, float slope, int M, int Ktot, int m_base, double* __restrict__ part,
-    int spk = 0, float* __restrict__ slab = nullptr) {
+    int spk = 0, float* __restrict__ slab = nullptr, const float* __restrict__ addend = nullptr) {
   static_assert(!SPLIT || KSL, "split-K needs the channel-slice-major K walk");
+  static_assert(REFL != 4 || (SPLIT && KSL), "border rows run as split-K slabs");
   __shared__ __attribute__((aligned(16))) char smem[2 * T::STAGE];
   constexpr int A_LD = T::A_LD, B_LD = T::B_LD, RPP = T::RPP, NP = T::NP;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -548,6 +635,16 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_k(
   for (int j = 0; j < A_LD; ++j) {
     const int m = m0 + rb + RPP * j;
     const int mm = m < M ? m : 0;
+    if constexpr (REFL == 4) {
+      // border rows of a reflect-pad-1 data gradient (dgrad_border_pos): Wo = rows per image
+      const int n = mm / Wo;
+      int qh, qw, th, tw;
+      dgrad_border_pos(mm - n * Wo, H, W, qh, qw, th, tw);
+      hb[j] = qh - padh;
+      wb[j] = qw - padw;
+      pb[j] = n * H * W * C;
+      continue;
+    }
     const int hw = Ho * Wo;
     const int n = mm / hw, rem = mm - n * hw, ho = rem / Wo, wo = rem - ho * Wo;
     hb[j] = ho * st - padh;
@@ -705,7 +802,10 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_k(
     // column (xor 16, xor 32).
     // LDS_EPI: the activated tile goes to LDS (row stride BN + 16 floats: the two rows of a 32-lane
     // write group land 16 banks apart) and leaves as whole float4 rows (coalesced stores).
-    constexpr bool LEPI = VST_BF_LDS_EPI && T::BM * (T::BN + 16) * 4 <= 2 * T::STAGE;
+    // (an addend — the residual gradient of a data gradient — is always added on this path: its float4
+    // loads ride with the row stores instead of 4-byte reads per accumulator element)
+    constexpr bool LFIT = T::BM * (T::BN + 16) * 4 <= 2 * T::STAGE;
+    const bool LEPI = LFIT && (VST_BF_LDS_EPI || addend != nullptr);
     constexpr int LDE = T::BN + 16;
     float* ept = reinterpret_cast<float*>(smem);
     if (LEPI) __syncthreads();  // every wave is done reading the last stage
@@ -722,7 +822,8 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_k(
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int mm = m0 + wm0 + 16 * (2 * g + h) + 4 * (lane >> 4) + r;
-            const float v = apply_act(acc[2 * g + h][j][r] + bv, act, slope);
+            const float ad = (!LEPI && addend && nok && mm < M) ? addend[(long)mm * Cop + n] : 0.f;
+            const float v = apply_act(acc[2 * g + h][j][r] + bv, act, slope) + ad;
             if (LEPI)
               ept[(mm - m0) * LDE + (n - n0)] = v;
             else if (nok && mm < M)
@@ -751,8 +852,11 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_k(
       for (int idx = t; idx < T::BM * C4; idx += T::NT) {
         const int row = idx / C4, c = 4 * (idx - row * C4);
         const int mm = m0 + row, n = n0 + c;
-        if (mm < M && n < Cop)
-          *reinterpret_cast<float4*>(y + (long)mm * Cop + n) = *reinterpret_cast<const float4*>(ept + row * LDE + c);
+        if (mm < M && n < Cop) {
+          float4 v = *reinterpret_cast<const float4*>(ept + row * LDE + c);
+          if (addend) add_f4(v, *reinterpret_cast<const float4*>(addend + (long)mm * Cop + n));
+          *reinterpret_cast<float4*>(y + (long)mm * Cop + n) = v;
+        }
       }
     }
     return;
@@ -787,7 +891,8 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_k(
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int mm = m0 + wm0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        const float v = apply_act(acc[i][j][r] + bv, act, slope);
+        const float ad = (addend && nok && mm < M) ? addend[(long)mm * Cop + n] : 0.f;
+        const float v = apply_act(acc[i][j][r] + bv, act, slope) + ad;
         if (nok && mm < M) y[(long)mm * Cop + n] = v;
         s1 += v;
         s2 += (double)v * v;
@@ -968,7 +1073,8 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_wgrad_bf_k(
 __global__ __launch_bounds__(256) void fprop_splitk_reduce_k(const float* __restrict__ slab, int ks, int m_base, int M,
                                                              int Cop, const float* __restrict__ bias, int act,
                                                              float slope, float* __restrict__ y,
-                                                             double* __restrict__ part, int hw) {
+                                                             double* __restrict__ part, int hw,
+                                                             const float* __restrict__ addend = nullptr) {
   __shared__ double red[2][16][65];
   const int t = threadIdx.x, c4 = (t & 15) * 4, sub = t >> 4;
   const int n = blockIdx.y * 64 + c4;
@@ -984,8 +1090,15 @@ __global__ __launch_bounds__(256) void fprop_splitk_reduce_k(const float* __rest
       if (r >= rows) break;
       float4 v = bv;
       for (int z = 0; z < ks; ++z) add_f4(v, *reinterpret_cast<const float4*>(slab + z * zst + r * Cop + n));
-      const float o[4] = {apply_act(v.x, act, slope), apply_act(v.y, act, slope), apply_act(v.z, act, slope),
-                          apply_act(v.w, act, slope)};
+      float o[4] = {apply_act(v.x, act, slope), apply_act(v.y, act, slope), apply_act(v.z, act, slope),
+                    apply_act(v.w, act, slope)};
+      if (addend) {  // added after the activation (the addend of a data gradient: the residual gradient)
+        const float4 a = *reinterpret_cast<const float4*>(addend + (m_base + r) * Cop + n);
+        o[0] += a.x;
+        o[1] += a.y;
+        o[2] += a.z;
+        o[3] += a.w;
+      }
       *reinterpret_cast<float4*>(y + (m_base + r) * Cop + n) = make_float4(o[0], o[1], o[2], o[3]);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -1277,7 +1390,7 @@ size_t bf_fprop_ws_floats(long M, int Cop, int C, int R, int S, int math) {
 int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* bias, float* y, int N,
                     int H, int W, int C, int Ho, int Wo, int Cop, int R, int S, int st, int padh, int padw,
                     int reflect, int act, float slope, int math, int kind, hipStream_t s, double* part,
-                    float* tws, size_t tws_floats) {
+                    float* tws, size_t tws_floats, const float* addend) {
   const int M = N * Ho * Wo, K = R * S * C;
   const __bf16* ws = reinterpret_cast<const __bf16*>(wsplit);
   int kd, m_split, tail_kind;
@@ -1297,16 +1410,20 @@ int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* b
     const dim3 grid(ceil_div(Mend - mb, BM_) * ceil_div(Cop, BN_));                                 \
     if (C == 4)                                                                                     \
       hipLaunchKernelGGL((bf::conv_fprop_bf_k<T, false, 3>), grid, dim3(T::NT), 0, s, x, ws, wps, bias, y, \
-                         H, W, C, Ho, Wo, Cop, S, st, padh, padw, reflect, act, slope, Mend, K, mb, part); \
+                         H, W, C, Ho, Wo, Cop, S, st, padh, padw, reflect, act, slope, Mend, K, mb, part, 0,      \
+                         nullptr, addend);                                                          \
     else if (VST_BF_KSLICE && C % BK_ == 0 && reflect)                                              \
       hipLaunchKernelGGL((bf::conv_fprop_bf_k<T, true, 1>), grid, dim3(T::NT), 0, s, x, ws, wps, bias, y, \
-                         H, W, C, Ho, Wo, Cop, S, st, padh, padw, reflect, act, slope, Mend, K, mb, part); \
+                         H, W, C, Ho, Wo, Cop, S, st, padh, padw, reflect, act, slope, Mend, K, mb, part, 0,      \
+                         nullptr, addend);                                                          \
     else if (VST_BF_KSLICE && C % BK_ == 0)                                                         \
       hipLaunchKernelGGL((bf::conv_fprop_bf_k<T, true, 0>), grid, dim3(T::NT), 0, s, x, ws, wps, bias, y, \
-                         H, W, C, Ho, Wo, Cop, S, st, padh, padw, reflect, act, slope, Mend, K, mb, part); \
+                         H, W, C, Ho, Wo, Cop, S, st, padh, padw, reflect, act, slope, Mend, K, mb, part, 0,      \
+                         nullptr, addend);                                                          \
     else                                                                                            \
       hipLaunchKernelGGL((bf::conv_fprop_bf_k<T, false, 2>), grid, dim3(T::NT), 0, s, x, ws, wps, bias, y, \
-                         H, W, C, Ho, Wo, Cop, S, st, padh, padw, reflect, act, slope, Mend, K, mb, part); \
+                         H, W, C, Ho, Wo, Cop, S, st, padh, padw, reflect, act, slope, Mend, K, mb, part, 0,      \
+                         nullptr, addend);                                                          \
   }
   for (int ph = (ks && !m_first) ? 1 : 0; ph < ((m_split || (ks && !m_first)) ? 2 : 1); ++ph) {
     const int mb = ph ? m_split : 0, Mend = (m_split && !ph) ? m_split : M;
@@ -1317,12 +1434,14 @@ int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* b
       const dim3 grid(ceil_div(M - mb, 256) * ceil_div(Cop, 128) * ks);
       if (reflect)
         hipLaunchKernelGGL((bf::conv_fprop_bf_k<T, true, 1, true>), grid, dim3(T::NT), 0, s, x, ws, wps, bias, y, H,
-                           W, C, Ho, Wo, Cop, S, st, padh, padw, reflect, act, slope, M, K, mb, part, spk, tws);
+                           W, C, Ho, Wo, Cop, S, st, padh, padw, reflect, act, slope, M, K, mb, part, spk, tws,
+                           nullptr);
       else
         hipLaunchKernelGGL((bf::conv_fprop_bf_k<T, true, 0, true>), grid, dim3(T::NT), 0, s, x, ws, wps, bias, y, H,
-                           W, C, Ho, Wo, Cop, S, st, padh, padw, reflect, act, slope, M, K, mb, part, spk, tws);
+                           W, C, Ho, Wo, Cop, S, st, padh, padw, reflect, act, slope, M, K, mb, part, spk, tws,
+                           nullptr);
       hipLaunchKernelGGL(bf::fprop_splitk_reduce_k, dim3(ceil_div(M - mb, 32), ceil_div(Cop, 64)), dim3(256), 0, s,
-                         tws, ks, mb, M, Cop, bias, act, slope, y, part, Ho * Wo);
+                         tws, ks, mb, M, Cop, bias, act, slope, y, part, Ho * Wo, addend);
       continue;
     }
     if (math == VST_MATH_BF16X6) {
@@ -1335,6 +1454,68 @@ int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* b
   return check_launch("conv2d_fwd(bf16 split)");
 }
 
+
+// Border GEMM of the reflect-pad-1 data gradient (dgrad_border_pos rows): K-split count and slab
+// floats.  The rows (2(H+W)+8..+16 per image) are few, so the 256x128 (x6) / 128x128 (x3) tiles run
+// as ks K-range splits filling the CUs; the slabs are summed by dgrad_border_add_k.
+static void bf_border_plan(int N, int H, int W, int Cy, int Cx, int math, int* ks_out, long* mb_out) {
+  const int NB = bf::dgrad_border_rows(H, W);
+  const long Mb = (long)N * NB;
+  const int bm = math == VST_MATH_BF16X6 ? 256 : 128;
+  const long tiles = ((Mb + bm - 1) / bm) * ((Cx + 127) / 128);
+  const int nk = (9 * Cy + 31) / 32;
+  int ks = (int)(VST_NUM_CUS / (tiles > 0 ? tiles : 1));
+  ks = ks < 1 ? 1 : (ks > 16 ? 16 : ks);
+  while (ks > 1 && (ks - 1) * ((nk + ks - 1) / ks) >= nk) --ks;  // no empty split
+  *ks_out = ks;
+  *mb_out = Mb;
+}
+
+bool bf_dgrad_refl1_ok(int N, int H, int W, int Cy, int Cx, int math) {
+  return math != VST_MATH_F32 && VST_BF_KSLICE && Cy % 32 == 0 && Cx % 4 == 0 && H >= 4 && W >= 4 && N > 0;
+}
+
+size_t bf_dgrad_refl1_ws_floats(int N, int H, int W, int Cy, int Cx, int math) {
+  int ks;
+  long Mb;
+  bf_border_plan(N, H, W, Cy, Cx, math, &ks, &Mb);
+  return bf_fprop_ws_floats((long)N * H * W, Cx, Cy, 3, 3, math) + (size_t)ks * Mb * Cx;
+}
+
+// dx = data gradient of ReflectionPad2d(1) + 3x3 conv (stride 1) from dy (+ addend), wsplit = the
+// VST_PACK_IKF planes of the conv weight: the interior as the zero-pad-1 forward conv (addend in its
+// epilogue), then the border GEMM (split-K slabs) and dgrad_border_add_k.  Replaces the conv over the
+// (H+2) x (W+2) zero-padded frame + reflect fold.
+int bf_dgrad_refl1_launch(const float* dy, const void* wsplit, long wps, const float* addend, float* dx, int N, int H,
+                          int W, int Cy, int Cx, int math, hipStream_t s, float* ws, size_t ws_floats) {
+  int ks;
+  long Mb;
+  bf_border_plan(N, H, W, Cy, Cx, math, &ks, &Mb);
+  const size_t main_ws = bf_fprop_ws_floats((long)N * H * W, Cx, Cy, 3, 3, math);
+  VST_REQUIRE(ws_floats >= main_ws + (size_t)ks * Mb * Cx, "dgrad_refl: workspace too small");
+  if (int e = bf_fprop_launch(dy, wsplit, wps, nullptr, dx, N, H, W, Cy, H, W, Cx, 3, 3, 1, 1, 1, 0, VST_ACT_NONE, 0.f,
+                              math, -1, s, nullptr, main_ws ? ws : nullptr, main_ws, addend))
+    return e;
+  float* slab = ws + main_ws;
+  const __bf16* wb = reinterpret_cast<const __bf16*>(wsplit);
+  const int NB = bf::dgrad_border_rows(H, W), K = 9 * Cy;
+  if (math == VST_MATH_BF16X6) {
+    using T = bf::Tile<256, 128, 64, 64, 32, 3>;
+    const int nk = (K + T::BK - 1) / T::BK, spk = (nk + ks - 1) / ks;
+    const dim3 grid(ceil_div(Mb, 256) * ceil_div(Cx, 128) * ks);
+    hipLaunchKernelGGL((bf::conv_fprop_bf_k<T, true, 4, true>), grid, dim3(T::NT), 0, s, dy, wb, wps, nullptr, dx, H,
+                       W, Cy, H, NB, Cx, 3, 1, 1, 1, 0, VST_ACT_NONE, 0.f, (int)Mb, K, 0, nullptr, spk, slab, nullptr);
+  } else {
+    using T = bf::Tile<128, 128, 64, 32, 32, 2>;
+    const int nk = (K + T::BK - 1) / T::BK, spk = (nk + ks - 1) / ks;
+    const dim3 grid(ceil_div(Mb, 128) * ceil_div(Cx, 128) * ks);
+    hipLaunchKernelGGL((bf::conv_fprop_bf_k<T, true, 4, true>), grid, dim3(T::NT), 0, s, dy, wb, wps, nullptr, dx, H,
+                       W, Cy, H, NB, Cx, 3, 1, 1, 1, 0, VST_ACT_NONE, 0.f, (int)Mb, K, 0, nullptr, spk, slab, nullptr);
+  }
+  hipLaunchKernelGGL(bf::dgrad_border_add_k, dim3(ceil_div(Mb, 16), ceil_div(Cx, 64)), dim3(256), 0, s, slab, ks,
+                     (int)Mb, Cx, dx, H, W, NB);
+  return check_launch("conv2d_dgrad_refl");
+}
 
 void bf_nhwc_to_planes(const float* x, void* y, long P, int Cs, int np, hipStream_t s, int row_in, int row_out) {
   const dim3 g((unsigned)((P + 63) / 64), ceil_div(Cs, 64));
@@ -1402,4 +1583,20 @@ extern "C" int vst_weight_split(const float* w, void* out, long n, void* stream)
   hipLaunchKernelGGL(bf::split3_k, dim3(ceil_div(n, 256)), dim3(256), 0, (hipStream_t)stream, w,
                      reinterpret_cast<__bf16*>(out), n);
   return check_launch("weight_split");
+}
+
+extern "C" size_t vst_conv2d_dgrad_refl_ws_bytes(int N, int H, int W, int Cy, int Cx, int math) {
+  if (!bf_dgrad_refl1_ok(N, H, W, Cy, Cx, math)) return 0;
+  return bf_dgrad_refl1_ws_floats(N, H, W, Cy, Cx, math) * sizeof(float);
+}
+
+extern "C" int vst_conv2d_dgrad_refl(const float* dy, const void* wsplit, const float* addend, float* dx, float* ws,
+                                     size_t ws_bytes, int N, int H, int W, int Cy, int Cx, int math, void* stream) {
+  VST_REQUIRE(dy && wsplit && dx && ws, "conv2d_dgrad_refl: null pointer");
+  if (!bf_dgrad_refl1_ok(N, H, W, Cy, Cx, math)) {
+    ::vst::set_error("conv2d_dgrad_refl: needs split-bf16 math, Cy %% 32 == 0, Cx %% 4 == 0, H, W >= 4");
+    return VST_EUNSUPPORTED;
+  }
+  return bf_dgrad_refl1_launch(dy, wsplit, (long)Cx * 9 * Cy, addend, dx, N, H, W, Cy, Cx, math, (hipStream_t)stream,
+                               ws, ws_bytes / sizeof(float));
 }

@@ -393,12 +393,32 @@ def channel_sum(x, db, cl, accumulate=True):
     _call("vst_channel_sum", _p(x), _p(db), _p(ws), nhw, cs, cl, 1 if accumulate else 0, _stream())
 
 
+# ReflectionPad2d(1) + 3x3 data gradients as the interior conv + border GEMM (vst_conv2d_dgrad_refl)
+# instead of the conv over the zero-padded frame + reflect fold; VST_DGRAD_BORDER=0 keeps the fold.
+DGRAD_BORDER = os.environ.get("VST_DGRAD_BORDER", "1") != "0"
+
+
 def conv2d_dgrad_s1(dy, ikf, H, W, cx, R, pad, pad_mode="zero", addend=None, role="bwd"):
     """Data gradient of a stride-1 conv as a FORWARD conv (the split-bf16 MFMA fprop kernel with
-    pre-split weights).  Reflect padding: dx_full = conv(dy, rot180(W)^T, zero pad R-1) over the
-    padded input frame [H+2p][W+2p], then the reflect fold (+ addend).  Zero padding p <= R-1:
-    dx = conv(dy, rot180(W)^T, zero pad R-1-p) directly (+ addend).  ikf: VST_PACK_IKF pack."""
+    pre-split weights).  Reflect padding, 3x3 / pad 1: the interior dx = conv(dy, rot180(W)^T, zero
+    pad 1) (+ addend in its epilogue) plus the padded border positions' GEMM added into rows / columns
+    1 and H-2 / W-2 (vst_conv2d_dgrad_refl).  Other reflect cases: dx_full = conv(dy, rot180(W)^T,
+    zero pad R-1) over the padded input frame [H+2p][W+2p], then the reflect fold (+ addend).  Zero
+    padding p <= R-1: dx = conv(dy, rot180(W)^T, zero pad R-1-p) directly (+ addend).  ikf:
+    VST_PACK_IKF pack."""
     _dev_check(dy, ikf, addend)
+    if pad_mode == "reflect" and DGRAD_BORDER and R == 3 and pad == 1 and getattr(ikf, "vst_split", None) is not None:
+        N, Hy, Wy, Cy = dy.shape
+        m = _math(role)
+        nb = int(lib().vst_conv2d_dgrad_refl_ws_bytes(N, H, W, Cy, cx, m)) if (Hy, Wy) == (H, W) else 0
+        if nb:
+            dx = torch.empty((N, H, W, cx), device=dy.device)
+            ws = torch.empty((nb + 3) // 4, device=dy.device)
+            h = _probe_begin("dgrad", (N, H, W, Cy, cx, R, 1, pad, pad_mode)) if _probes else None
+            _call("vst_conv2d_dgrad_refl", _p(dy), _p(ikf.vst_split), _p(addend), _p(dx), _p(ws), nb, N, H, W, Cy, cx,
+                  m, _stream())
+            _probe_end(h)
+            return dx
     if pad_mode == "reflect":
         dxp = conv2d_fwd(dy, ikf, None, cx, R, R, 1, R - 1, "zero", role=role)
         return reflect_fold(dxp, pad, addend)

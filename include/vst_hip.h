@@ -178,6 +178,16 @@ int vst_conv2d_wgrad(const float* x, const float* dy, float* dw, float* ws, size
                      int H, int W, int Cx, int Ho, int Wo, int Cyp, int R, int S, int stride,
                      int pad, int pad_mode, int Co, int Ci, long so, long si, int accumulate,
                      int math, void* stream);
+/* Data gradient of ReflectionPad2d(1) + 3x3 conv, stride 1 (the ResnetBlock convs, networks.py:404-426):
+ * dx[N][H][W][Cx] (+= addend, or NULL) from dy[N][H][W][Cy], wsplit = the bf16 planes of the
+ * VST_PACK_IKF pack of the conv weight.  The interior term runs as the zero-pad-1 forward conv of dy
+ * (addend in its epilogue); the 2(H+W)+4 positions of the padded border, whose contributions the
+ * reflection folds into rows / columns 1 and H-2 / W-2, run as one small split-K GEMM whose slabs are
+ * added there (no (H+2) x (W+2) frame, no fold pass).  Needs math BF16X3/X6, Cy % 32 == 0,
+ * Cx % 4 == 0, H, W >= 4 (else VST_EUNSUPPORTED; ws_bytes query returns 0).  ws: ws_bytes bytes. */
+size_t vst_conv2d_dgrad_refl_ws_bytes(int N, int H, int W, int Cy, int Cx, int math);
+int vst_conv2d_dgrad_refl(const float* dy, const void* wsplit, const float* addend, float* dx, float* ws,
+                          size_t ws_bytes, int N, int H, int W, int Cy, int Cx, int math, void* stream);
 /* vst_conv2d_wgrad with operand images made by the producers of x and dy: x_t (or NULL) = the
  * padded channel-major image of x that vst_instnorm_act_fwd_cp writes (same pad / mode / stride);
  * dy_planes (or NULL) = the three bf16 planes [3][Cyp][vst_cp_ld(N*Ho*Wo)] of dy that

@@ -529,7 +529,11 @@ def test_dgrad_fold_instnorm_bwd_exact(ops, act, addend):
     y_in = _g(8, (N, H, H, C)).to(DEV)
     s_in = ops.instnorm_stats(y_in)
     add = _g(9, (N, H, H, C)).to(DEV) if addend else None
-    g0 = ops.conv2d_dgrad_s1(dy, ikf, H, H, C, 3, 1, "reflect", addend=add)
+    prev, ops.DGRAD_BORDER = ops.DGRAD_BORDER, False   # the padded-frame + fold route it fuses
+    try:
+        g0 = ops.conv2d_dgrad_s1(dy, ikf, H, H, C, 3, 1, "reflect", addend=add)
+    finally:
+        ops.DGRAD_BORDER = prev
     db0 = torch.zeros(C, device=DEV)
     d0, p0 = ops.instnorm_act_bwd(g0, y_in, s_in, act, db=db0, planes=True)
     db1 = torch.zeros(C, device=DEV)
@@ -744,3 +748,41 @@ def test_conv_fwd_four_channel_input(ops, shape):
     rstd = 1.0 / torch.sqrt(yr.var(dim=(2, 3), unbiased=False) + 1e-5)
     assert ((st_[..., 0] - mean).abs() * rstd).max().item() < 1e-5
     assert ((st_[..., 1] - rstd).abs() / rstd).max().item() < 1e-4
+
+
+@pytest.mark.parametrize("case", [
+    # name, N, C_in(=dx), C_out(=dy), H, W
+    ("small", 2, 32, 32, 16, 16),
+    ("odd_HW_sum", 3, 64, 64, 13, 20),   # H + W odd: padded border rows
+    ("minimal", 1, 32, 64, 4, 4),
+    ("cx_not_128", 2, 36, 32, 9, 7),
+    ("prod_N8", 8, 256, 256, 64, 64),    # the batched G_A calls: the interior is one whole CU round
+    ("prod_N12", 12, 256, 256, 64, 64),  # interior with the split-K tail (addend in the reduction)
+], ids=lambda c: c[0])
+def test_dgrad_reflect_border(ops, conv_math, case):
+    """ReflectionPad2d(1) + 3x3 data gradient as the interior zero-pad-1 conv (+ addend in its
+    epilogue) + the padded-border GEMM added into rows / columns 1 and H-2 / W-2
+    (vst_conv2d_dgrad_refl), against torch autograd and against the padded-frame + fold path."""
+    name, N, Ci, Co, H, W = case
+    x = _g(111, (N, Ci, H, W)).requires_grad_(True)
+    w = _g(112, (Co, Ci, 3, 3), 0.05)
+    y = F.conv2d(F.pad(x, (1,) * 4, mode="reflect"), w)
+    gy = _g(113, tuple(y.shape))
+    y.backward(gy)
+    ikf = ops.weight_pack(w.to(DEV), ops.PACK_IKF)
+    add = _g(114, (N, Ci, H, W))
+    gyn, addn = _nhwc(gy, ops), _nhwc(add, ops)
+    cx = ops.cpad(Ci)
+    m = ops._math("bwd")
+    used = int(ops.lib().vst_conv2d_dgrad_refl_ws_bytes(N, H, W, Co, cx, m)) > 0
+    assert used == (conv_math != "fp32")
+    dx = ops.conv2d_dgrad_s1(gyn, ikf, H, W, cx, 3, 1, "reflect", addend=addn)
+    _close(_nchw(dx, Ci, ops) - add, x.grad, tol=CONV_TOL[conv_math], what=name)
+    prev, ops.DGRAD_BORDER = ops.DGRAD_BORDER, False
+    try:
+        dx_fold = ops.conv2d_dgrad_s1(gyn, ikf, H, W, cx, 3, 1, "reflect", addend=addn)
+    finally:
+        ops.DGRAD_BORDER = prev
+    _close(dx, dx_fold, tol=CONV_TOL[conv_math], what=name + " vs fold path")
+    if cx > Ci:
+        assert float(dx[..., Ci:].abs().max()) == 0.0

@@ -154,7 +154,13 @@ __device__ __forceinline__ uint32_t pack2(float a, float b) {
 // The two timing modes above compute WRONG results: only a developer variant build (tools/
 // build_variant.py, which defines VST_DEV_VARIANT and writes _build/variants/, never the product
 // library) may turn them on.
-#if (VST_BF_FAKESPLIT || VST_BF_FAKE16) && !defined(VST_DEV_VARIANT)
+#ifndef VST_BF_FAKE_ZA
+#define VST_BF_FAKE_ZA 0  // developer timing experiment only: every A gather reads the zero page (WRONG results)
+#endif
+#ifndef VST_BF_FAKE_ZB
+#define VST_BF_FAKE_ZB 0  // developer timing experiment only: every B load reads the zero page (WRONG results)
+#endif
+#if (VST_BF_FAKESPLIT || VST_BF_FAKE16 || VST_BF_FAKE_ZA || VST_BF_FAKE_ZB) && !defined(VST_DEV_VARIANT)
 #error "VST_BF_FAKESPLIT / VST_BF_FAKE16 are developer-only timing modes (wrong results): build them with tools/build_variant.py"
 #endif
 template <int NP>
@@ -741,14 +747,22 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_k(
     }
 #pragma unroll
     for (int j = 0; j < A_LD; ++j) {
-      const float* p = (kin && aoff[j] >= 0) ? x + aoff[j] + ka : zp;
+      // FAKE_ZA 1: every A gather from the zero page; 2: all but the first tap of each channel slice
+      // (only the L2-miss-prone loads stay real); 3: only the first tap's loads from the zero page
+      const bool tap0 = KSL && tr == 0 && ts == 0;
+      // 4: every row reads the first pixel's channel slice (real, changing values, one cache line)
+      const bool fake = VST_BF_FAKE_ZA == 1 || (VST_BF_FAKE_ZA == 2 && !tap0) || (VST_BF_FAKE_ZA == 3 && tap0);
+      const float* p = (kin && aoff[j] >= 0 && !fake) ? x + (VST_BF_FAKE_ZA == 4 ? 0 : aoff[j]) + ka : zp;
       ra[set][j][0] = *reinterpret_cast<const float4*>(p);
       ra[set][j][1] = *reinterpret_cast<const float4*>(p + 4);
     }
 #pragma unroll
     for (int j = 0; j < B_LD; ++j) {
 #pragma unroll
-      for (int p = 0; p < NP; ++p) rbv[set][j][p] = *reinterpret_cast<const u32x4_t*>(wrow[j] + p * wps + kb);
+      for (int p = 0; p < NP; ++p)
+        rbv[set][j][p] = *reinterpret_cast<const u32x4_t*>(
+            VST_BF_FAKE_ZB == 1 ? reinterpret_cast<const __bf16*>(zp)
+                                : (VST_BF_FAKE_ZB == 2 ? ws : wrow[j]) + p * wps + kb);  // 2: weight row 0 for every row
     }
   };
   // go = false (the last two stages): the cursor stays on the final stage.  KSL: branch-free

@@ -238,15 +238,18 @@ __global__ __launch_bounds__(NRED) void fold_in_partial_k(const float* __restric
   }
 }
 
-// Fold the per-slice partials of one (n, 64-channel group): 4 waves stride the slices (coalesced
-// over c), then combine through LDS in a fixed order.  out[v] = sum_z part[n][z][c][v].
-template <int NV>
+// Fold the per-slice partials of one (n, CPB-channel group): G = 256 / CPB thread groups stride the
+// slices (coalesced over c), then combine through LDS in a fixed order.  out[v] = sum_z
+// part[n][z][c][v].  CPB = 16 for the IN finalizes (4x the blocks of CPB = 64: these small kernels are
+// latency-bound, their slice chains 4x shorter).
+template <int NV, int CPB = 64>
 __device__ __forceinline__ bool fold_slices(const double* __restrict__ part, int n, int C, int nsplit,
                                             double (&out)[NV]) {
-  __shared__ double red[NV][4][64];
-  const int cl = threadIdx.x & 63, q = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
-  // 4 independent accumulator chains per thread (slices q, q+4, q+8, q+12, then +16 ...) so the
+  constexpr int G = 256 / CPB;
+  __shared__ double red[NV][G][CPB];
+  const int cl = threadIdx.x % CPB, q = threadIdx.x / CPB;
+  const int c = blockIdx.x * CPB + cl;
+  // 4 independent accumulator chains per thread (slices q, q+G, q+2G, q+3G, then +4G ...) so the
   // loads overlap instead of serialising on the fp64 add chain; combined in a fixed order.
   double acc[NV], acc4[4][NV];
 #pragma unroll
@@ -257,13 +260,13 @@ __device__ __forceinline__ bool fold_slices(const double* __restrict__ part, int
     const long zs = (long)C * NV;
     const double* base = part + (((long)n * nsplit) * C + c) * NV;
     int z = q;
-    for (; z + 12 < nsplit; z += 16) {
+    for (; z + 3 * G < nsplit; z += 4 * G) {
 #pragma unroll
       for (int u = 0; u < 4; ++u)
 #pragma unroll
-        for (int v = 0; v < NV; ++v) acc4[u][v] += base[(long)(z + 4 * u) * zs + v];
+        for (int v = 0; v < NV; ++v) acc4[u][v] += base[(long)(z + G * u) * zs + v];
     }
-    for (; z < nsplit; z += 4)
+    for (; z < nsplit; z += G)
 #pragma unroll
       for (int v = 0; v < NV; ++v) acc4[0][v] += base[(long)z * zs + v];
   }
@@ -274,17 +277,22 @@ __device__ __forceinline__ bool fold_slices(const double* __restrict__ part, int
   __syncthreads();
   if (q != 0 || c >= C) return false;
 #pragma unroll
-  for (int v = 0; v < NV; ++v) out[v] = red[v][0][cl] + red[v][1][cl] + red[v][2][cl] + red[v][3][cl];
+  for (int v = 0; v < NV; ++v) {
+    double o = 0.0;
+#pragma unroll
+    for (int g = 0; g < G; ++g) o += red[v][g][cl];
+    out[v] = o;
+  }
   return true;
 }
 
-// grid (C/64, N), 256 threads
+// grid (C/16, N), 256 threads
 __global__ void in_finalize_k(const double* __restrict__ part, float* __restrict__ stats, int N,
                               int HW, int C, int nsplit, float eps) {
   double sq[2];
   const int n = blockIdx.y;
-  if (!fold_slices<2>(part, n, C, nsplit, sq)) return;
-  const int idx = n * C + blockIdx.x * 64 + (threadIdx.x & 63);
+  if (!fold_slices<2, 16>(part, n, C, nsplit, sq)) return;
+  const int idx = n * C + blockIdx.x * 16 + (threadIdx.x & 15);
   const double mean = sq[0] / HW;
   double var = sq[1] / HW - mean * mean;
   if (var < 0) var = 0;
@@ -299,8 +307,8 @@ __global__ void in_bwd_finalize_k(const double* __restrict__ part, const float* 
                                   int C, int nsplit) {
   double a[3];
   const int n = blockIdx.y;
-  if (!fold_slices<3>(part, n, C, nsplit, a)) return;
-  const int idx = n * C + blockIdx.x * 64 + (threadIdx.x & 63);
+  if (!fold_slices<3, 16>(part, n, C, nsplit, a)) return;
+  const int idx = n * C + blockIdx.x * 16 + (threadIdx.x & 15);
   const double mg = a[0] / HW, mgx = a[1] / HW;
   coef[idx] = make_float2((float)mg, (float)mgx);
   const double rstd = stats[2 * idx + 1];
@@ -805,7 +813,7 @@ extern "C" int vst_instnorm_stats(const float* x, float* stats, float* ws, int N
   double* part = reinterpret_cast<double*>(ws);
   hipLaunchKernelGGL(in_partial_k<0>, dim3(g.nsplit, N), dim3(NRED), 0, s, x, (const float*)nullptr,
                      (const float*)nullptr, part, HW, C, g.LP, g.PG, g.SP, g.nsplit, 0, 0.f);
-  hipLaunchKernelGGL(in_finalize_k, dim3(ceil_div(C, 64), N), dim3(256), 0, s, part, stats, N, HW, C,
+  hipLaunchKernelGGL(in_finalize_k, dim3(ceil_div(C, 16), N), dim3(256), 0, s, part, stats, N, HW, C,
                      g.nsplit, eps);
   return check_launch("instnorm_stats");
 }
@@ -813,7 +821,7 @@ extern "C" int vst_instnorm_stats(const float* x, float* stats, float* ws, int N
 extern "C" int vst_instnorm_finalize(const double* part, float* stats, int N, int HW, int C, int nsplit,
                                      float eps, void* stream) {
   VST_REQUIRE(part && stats && N > 0 && HW > 0 && C > 0 && nsplit > 0, "instnorm_finalize: bad args");
-  hipLaunchKernelGGL(in_finalize_k, dim3(ceil_div(C, 64), N), dim3(256), 0, (hipStream_t)stream, part, stats, N,
+  hipLaunchKernelGGL(in_finalize_k, dim3(ceil_div(C, 16), N), dim3(256), 0, (hipStream_t)stream, part, stats, N,
                      HW, C, nsplit, eps);
   return check_launch("instnorm_finalize");
 }
@@ -895,7 +903,7 @@ static int in_bwd_tail(const float* gy, const float* x, const float* stats, floa
   float2* coef = reinterpret_cast<float2*>(reinterpret_cast<char*>(ws) +
                                            (size_t)N * g.nsplit * C * 3 * sizeof(double));
   double* dbn = reinterpret_cast<double*>(reinterpret_cast<char*>(coef) + (size_t)N * C * sizeof(float2));
-  hipLaunchKernelGGL(in_bwd_finalize_k, dim3(ceil_div(C, 64), N), dim3(256), 0, s, part, stats, coef, dbn,
+  hipLaunchKernelGGL(in_bwd_finalize_k, dim3(ceil_div(C, 16), N), dim3(256), 0, s, part, stats, coef, dbn,
                      N, HW, C, g.nsplit);
   // the bias gradient (sum over n of dbn) is taken by the apply pass's first blocks
   if (planes) {

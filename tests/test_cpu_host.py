@@ -208,7 +208,7 @@ def test_wrong_result_modes_refused_in_product_build():
     import pytest
     from gbvst import _lib
     src = os.path.join(_lib.CSRC, "conv_bf.hip")
-    for mode in ("VST_BF_FAKESPLIT=1", "VST_BF_FAKE16=1"):
+    for mode in ("VST_BF_FAKESPLIT=1", "VST_BF_FAKE16=1", "VST_BF_FAKE_ZA=1", "VST_BF_FAKE_ZB=1"):
         r = subprocess.run([_lib.HIPCC, "-E", "--offload-arch=gfx950", "--cuda-host-only", "-D" + mode, src,
                             "-o", os.devnull], stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
         assert r.returncode != 0 and b"developer-only" in r.stdout, (mode, r.stdout[-400:])

@@ -98,6 +98,11 @@ int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* b
                     int H, int W, int C, int Ho, int Wo, int Cop, int R, int S, int st, int padh, int padw,
                     int reflect, int act, float slope, int math, int kind, hipStream_t s,
                     double* part = nullptr, float* tws = nullptr, size_t tws_floats = 0, const float* addend = nullptr);
+// direct patch-staged 4-channel-input convs (conv_c4.hip)
+bool c4_direct_ok(int C, int Cop, int R, int S, int st, int Ho, int Wo, int math);
+int c4_direct_launch(const float* x, const void* wsplit, long wps, const float* bias, float* y, int N, int H, int W,
+                     int Ho, int Wo, int R, int S, int pad, int reflect, int act, float slope, int math, double* part,
+                     hipStream_t s);
 size_t bf_fprop_ws_floats(long M, int Cop, int C, int R, int S, int math);
 int bf_tail_ks(long M, int Cop, int m_split, int nk);
 void bf_split_plan(long M, int Cop, int C, int R, int S, int math, int kind, int* m_first, int* ks_out);

@@ -862,6 +862,9 @@ extern "C" int vst_conv_plan_fwd(int N, int H, int W, int Cx, int Cop, int R, in
   *tail_kind = -1;
   if (Cop == 4) {
     *kind = VST_PLAN_SKINNY;
+  } else if (Cx == 4 && g_bf_c4 && g_tile_override[0] < 0 && padh == padw &&
+             c4_direct_ok(Cx, Cop, R, S, stride, Ho, Wo, math)) {
+    *kind = VST_PLAN_C4_DIRECT;
   } else if (math != VST_MATH_F32 && (Cx % 8 == 0 || (Cx == 4 && g_bf_c4))) {
     bf_plan((long)N * Ho * Wo, Cop, math, g_tile_override[0], kind, m_split, tail_kind);
   } else {

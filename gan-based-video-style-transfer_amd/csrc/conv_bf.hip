@@ -1406,6 +1406,9 @@ int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* b
                     int reflect, int act, float slope, int math, int kind, hipStream_t s, double* part,
                     float* tws, size_t tws_floats, const float* addend) {
   const int M = N * Ho * Wo, K = R * S * C;
+  // 4-channel inputs with 64 outputs (the generator's 7x7 image convs): the direct patch-staged kernel
+  if (kind < 0 && padh == padw && !addend && c4_direct_ok(C, Cop, R, S, st, Ho, Wo, math))
+    return c4_direct_launch(x, wsplit, wps, bias, y, N, H, W, Ho, Wo, R, S, padh, reflect, act, slope, math, part, s);
   const __bf16* ws = reinterpret_cast<const __bf16*>(wsplit);
   int kd, m_split, tail_kind;
   bf_plan(M, Cop, math, kind, &kd, &m_split, &tail_kind);

@@ -1,0 +1,374 @@
+// Direct (patch-staged) split-bf16 MFMA convolution of a 4-channel NHWC input: the generator's image
+// convs — ReflectionPad2d(3) + Conv2d(3 -> 64, 7x7) (reference networks.py:340-343, the first layer)
+// and the data gradient of its last layer (ReflectionPad2d(3) + Conv2d(64 -> 3, 7x7), networks.py:
+// 365-366, run as a forward conv over the 4-channel output gradient with the rotated taps).
+//
+// The implicit-GEMM kernel (conv_fprop_bf_k<.., REFL = 3>) gathers every 8-deep K chunk of every
+// output row from global memory and splits it into bf16 planes in registers: for a 7x7 filter each
+// input value is gathered and split 49 times, and K = 196 is only 7 K-steps, so the per-tile pipeline
+// fill and epilogue dominate (153-164 us per N = 8 call at 256^2, ~4x its MFMA time).  Here a block
+// owns one output-row segment (<= 256 pixels): it stages the R input rows the segment reads (with the
+// reflect / zero border applied) ONCE as pre-split bf16 planes in LDS, keeps all 64 x R x 8 x 4 weight
+// planes resident in LDS for the whole (persistent) launch, and builds every A fragment straight from
+// the patch: an MFMA K-step is one kernel row r — 8 taps (S padded to 8 with zero weights) x 4
+// channels, the two taps of a lane's 8-deep chunk being adjacent pixels of the patch row (16
+// contiguous bytes per plane).  No barrier inside the K loop; the next segment's patch is loaded into
+// registers while the current one computes.
+//
+// Products: the x6 / x3 sums of conv_fprop_bf_k (same terms, same per-K-step order); accumulation
+// fp32.  Epilogue: bias, activation, optional InstanceNorm statistics partials per 32-pixel group in
+// the layout of vst_conv2d_fwd_in ([img][HW/32][Cop][2] fp64).
+#include "common.h"
+
+#include <type_traits>
+
+namespace vst {
+namespace c4 {
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
+
+constexpr int NT = 512;          // 8 waves
+constexpr int SEG = 256;         // output pixels per segment: 8 waves x 32 rows
+constexpr int MAXR = 8;          // kernel rows (and taps per row, S padded to 8)
+constexpr int COP = 64;          // output channels (one 64-wide GEMM column tile)
+constexpr int PW = SEG + 8;      // patch row width in pixels (segment + 7 taps, rounded)
+constexpr int PATCH_PLANE = MAXR * PW * 8;          // bytes per plane: [R][PW][4] bf16
+constexpr int W_PLANE = MAXR * 4 * COP * 16;        // bytes per plane: [R][kq][64][8] bf16
+constexpr int LDS_BYTES = 3 * (PATCH_PLANE + W_PLANE);
+static_assert(LDS_BYTES <= 160 * 1024, "LDS");
+constexpr int PF = 5;            // patch float4s prefetched per thread (R * (L + 7) <= PF * NT)
+static_assert(MAXR * PW <= PF * NT, "patch prefetch coverage");
+
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+  const f32x2_t v = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
+}
+
+// one output-row segment: image n, output row ho, columns [wo0, wo0 + L)
+struct Seg {
+  int n, ho, wo0, L;
+};
+
+__device__ __forceinline__ Seg seg_of(int t, int Ho, int Wo, int nseg) {
+  Seg s;
+  const int row = t / nseg, q = t - row * nseg;
+  s.n = row / Ho;
+  s.ho = row - s.n * Ho;
+  s.wo0 = q * SEG;
+  s.L = q == nseg - 1 ? Wo - s.wo0 : SEG;
+  return s;
+}
+
+// y[n][ho][wo][co] = act(bias[co] + sum_{r,s,c} xpad[n][ho + r][wo + s][c] * w[co][r][s][c]),
+// xpad = x with a `pad` border (reflect or zero); stride 1, 4 input channels, Cop = 64.
+// ws: split weight planes [NP][64][R*S*4] (plane stride wps), the VST_PACK_OK layout of the
+// implicit-GEMM kernels.  grid = min(tiles, CUs), persistent over the segments t = blockIdx.x + k*grid.
+template <int NP, int R, int ACT>
+__global__ __launch_bounds__(NT, 1) void conv_c4_direct_k(const float* __restrict__ x, const __bf16* __restrict__ ws,
+                                                           long wps, const float* __restrict__ bias,
+                                                           float* __restrict__ y, int H, int W, int Ho, int Wo,
+                                                           int S, int pad, int reflect, float slope,
+                                                           int nseg, int T, int nimg, double* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+  char* patch = smem;                      // [NP][R][PW][4] bf16
+  char* wl = smem + 3 * PATCH_PLANE;       // [NP][R][kq 4][64][8] bf16
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int K = R * S * 4;
+
+  // weights -> LDS once: 16-B chunk (r, kq, co) = taps s = 2kq, 2kq + 1 (zero past S) x 4 channels.
+  // Branch-free buffer loads (a tap past S gets an out-of-range offset and reads zero), all in flight
+  // together: one round trip per block instead of one per chunk.
+  {
+    constexpr int NCH = NP * R * 4 * COP, PER = (NCH + NT - 1) / NT;
+    const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<__bf16*>(ws), 0, (int)((NP - 1) * wps * 2 + (long)COP * K * 2), 0x00020000);
+    u32x2v lo[PER], hi[PER];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int e = t + u * NT;
+      const int p = e / (R * 4 * COP), rem = e - p * R * 4 * COP;
+      const int r = rem / (4 * COP), kq = (rem / COP) & 3, co = rem % COP;
+      const int base = (int)((p * wps + (long)co * K + r * S * 4) * 2);  // bytes
+      const bool in = e < NCH;
+      lo[u] = __builtin_amdgcn_raw_buffer_load_b64(wrs, in && 2 * kq < S ? base + 2 * kq * 8 : 0x7ffffff0, 0, 0);
+      hi[u] = __builtin_amdgcn_raw_buffer_load_b64(wrs, in && 2 * kq + 1 < S ? base + (2 * kq + 1) * 8 : 0x7ffffff0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int e = t + u * NT;
+      if (e >= NCH) continue;
+      const int p = e / (R * 4 * COP), rem = e - p * R * 4 * COP;
+      const int r = rem / (4 * COP), kq = (rem / COP) & 3, co = rem % COP;
+      *reinterpret_cast<uint4*>(wl + p * W_PLANE + ((r * 4 + kq) * COP + co) * 16) =
+          make_uint4(lo[u][0], lo[u][1], hi[u][0], hi[u][1]);
+    }
+  }
+
+  // patch element e = (r, c): input row ho - pad + r, column wo0 - pad + c of image n
+  float4 pf[PF];
+  // Buffer loads through a descriptor over x: an element outside the frame (zero padding, the rows
+  // past R) gets an offset past the descriptor's range and reads as zero — no branch around any load
+  // (loads under branches make the wait-count pass drain vmcnt(0) at their use, behind the previous
+  // segment's output stores).
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(x), 0, nimg * H * W * 16, 0x00020000);
+  auto prefetch = [&](const Seg& g) __attribute__((always_inline)) {
+    const int cols = g.L + 7;
+#pragma unroll
+    for (int i = 0; i < PF; ++i) {
+      const int e = t + i * NT;
+      const int r = e / cols, c = e - r * cols;
+      int hi = g.ho - pad + r, wi = g.wo0 - pad + c;
+      bool ok;
+      if (reflect) {
+        hi = reflect_idx(hi, H);
+        wi = reflect_idx(wi, W);
+        ok = (unsigned)wi < (unsigned)W;  // columns past the last tap's reach may leave the frame
+      } else {
+        ok = (unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W;
+      }
+      ok = ok && r < R;
+      const int off = ok ? ((g.n * H + hi) * W + wi) * 16 : (int)0x7ffffff0;
+      pf[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
+    }
+  };
+  auto store_patch = [&](const Seg& g) __attribute__((always_inline)) {
+    const int cols = g.L + 7;
+#pragma unroll
+    for (int i = 0; i < PF; ++i) {
+      const int e = t + i * NT;
+      const int r = e / cols, c = e - r * cols;
+      // no branch (see prefetch): elements past the R rows land in row MAXR - 1, which no K-step reads
+      static_assert(R < MAXR, "a spare patch row");
+      float a[4] = {pf[i].x, pf[i].y, pf[i].z, pf[i].w};
+      char* dst = patch + ((r < R ? r : MAXR - 1) * PW + c) * 8;
+#pragma unroll
+      for (int p = 0; p < NP; ++p) {
+        const uint32_t q0 = pack2(a[0], a[1]), q1 = pack2(a[2], a[3]);
+        *reinterpret_cast<uint2*>(dst + p * PATCH_PLANE) = make_uint2(q0, q1);
+        if (p + 1 < NP) {
+          a[0] -= __uint_as_float(q0 << 16);
+          a[1] -= __uint_as_float(q0 & 0xffff0000u);
+          a[2] -= __uint_as_float(q1 << 16);
+          a[3] -= __uint_as_float(q1 & 0xffff0000u);
+        }
+      }
+    }
+  };
+
+  // this lane's bias values (channels 16 j + 4 (lane >> 4) + q), loaded once before any prefetch so
+  // the epilogue never waits behind the patch loads; scalar loads: a bias view may sit at any 4-byte
+  // offset of a flat parameter buffer
+  float4 bvs[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c0 = 16 * j + 4 * (lane >> 4);
+    bvs[j] = bias ? make_float4(bias[c0], bias[c0 + 1], bias[c0 + 2], bias[c0 + 3]) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  const int kq = lane >> 4;
+  const int sub = wave;  // this wave's 32-pixel sub-tile of every segment (SEG = 8 waves x 32)
+  const int HWo = Ho * Wo;
+  f32x4v acc[2][4];
+
+  // the fragments of kernel row r: A = the weight planes (4 blocks of 16 channels), B = the patch
+  // pixels (2 blocks of 16).  D^T = W . X^T: a lane's accumulator holds 4 consecutive channels of one
+  // pixel (pixel 16 i + (lane & 15), channels 16 j + 4 (lane >> 4) + q) and leaves as one float4.
+  struct Fr {
+    bf16x8_t w[NP][4], x[NP][2];
+  };
+  auto load_fr = [&](Fr& f, int r) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      // pixel (segment-local) 32 sub + 16 i + (lane & 15); taps 2 kq, 2 kq + 1 -> patch columns
+      const int pc = 32 * sub + 16 * i + (lane & 15) + 2 * kq;
+      const char* src = patch + (r * PW + pc) * 8;
+#pragma unroll
+      for (int p = 0; p < NP; ++p) {
+        const uint2 lo = *reinterpret_cast<const uint2*>(src + p * PATCH_PLANE);
+        const uint2 hi = *reinterpret_cast<const uint2*>(src + p * PATCH_PLANE + 8);
+        f.x[p][i] = __builtin_bit_cast(bf16x8_t, make_uint4(lo.x, lo.y, hi.x, hi.y));
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int p = 0; p < NP; ++p)
+        f.w[p][j] = *reinterpret_cast<const bf16x8_t*>(wl + p * W_PLANE + ((r * 4 + kq) * COP + 16 * j + (lane & 15)) * 16);
+  };
+  auto compute = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
+    Fr fr[2];  // double-buffered: row r + 1's LDS reads run under row r's MFMAs
+    load_fr(fr[0], 0);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const Fr& f = fr[r & 1];
+      if (r + 1 < R) load_fr(fr[(r + 1) & 1], r + 1);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          // (x-plane, w-plane) products in conv_fprop_bf_k's per-K-step order
+#define VST_C4MF(pa, pb) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.w[pb][j], f.x[pa][i], acc[i][j], 0, 0, 0)
+          if constexpr (NP == 3) {
+            VST_C4MF(1, 1); VST_C4MF(1, 0); VST_C4MF(0, 1); VST_C4MF(0, 0); VST_C4MF(2, 0); VST_C4MF(0, 2);
+          } else {
+            VST_C4MF(1, 0); VST_C4MF(0, 1); VST_C4MF(0, 0);
+          }
+#undef VST_C4MF
+        }
+      __builtin_amdgcn_sched_barrier(0);  // at most two fragment sets live
+    }
+  };
+  // bias, activation, the output float4s and the InstanceNorm partials of segment `cs`.  Stores go
+  // through buffer descriptors whose range check drops the pixels past the segment (and every partial
+  // of a launch without them, or of a sub-tile past the segment): no branch around any store.
+  // live = false (the first pass, before any segment was computed): every store is dropped.
+  auto epilogue = [&](const Seg& cs, bool live) __attribute__((always_inline)) {
+    const float* yseg = y + (((long)cs.n * Ho + cs.ho) * Wo + cs.wo0) * COP;
+    const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(yseg), 0, live ? cs.L * COP * (int)sizeof(float) : 0, 0x00020000);
+    const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
+        part ? part + (long)cs.n * (HWo >> 5) * COP * 2 : nullptr, 0,
+        part && live ? (HWo >> 5) * COP * 2 * (int)sizeof(double) : 0, 0x00020000);
+    const int pskip = 32 * sub < cs.L ? 0 : (1 << 30);  // a sub-tile past the segment: no partials
+    const int z = (cs.ho * Wo + cs.wo0 + 32 * sub) >> 5;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c0 = 16 * j + 4 * kq;
+      const float4 bv = bvs[j];
+      float v[2][4];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int px = 32 * sub + 16 * i + (lane & 15);  // segment-local pixel
+        v[i][0] = apply_act(acc[i][j][0] + bv.x, ACT, slope);
+        v[i][1] = apply_act(acc[i][j][1] + bv.y, ACT, slope);
+        v[i][2] = apply_act(acc[i][j][2] + bv.z, ACT, slope);
+        v[i][3] = apply_act(acc[i][j][3] + bv.w, ACT, slope);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, f32x4v{v[i][0], v[i][1], v[i][2], v[i][3]}),
+                                               yrs, (px * COP + c0) * (int)sizeof(float), 0, 0);
+      }
+      // InstanceNorm partials of the sub-tile's 32 pixels (one group: a launch with partials has
+      // Wo % 32 == 0): d = {sum v, sum v^2} of channel c0 + q over this lane's two pixels, then a
+      // butterfly reduce-scatter over the row's 16 lanes (xor 8, 4, 2 halve the 8 values, xor 1
+      // completes the last): lane l ends with index 4 b3 + 2 b2 + b1 (b = bits of l), i.e. channel
+      // c0 + 2 b3 + b2, value b1 (sum / sum of squares)
+      double d[8];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        d[2 * q] = (double)v[0][q] + (double)v[1][q];
+        d[2 * q + 1] = (double)v[0][q] * v[0][q] + (double)v[1][q] * v[1][q];
+      }
+      // (written out: a loop over (m, n) that the compiler leaves rolled indexes d[] at run time)
+      auto half = [&](auto M, auto Nn) __attribute__((always_inline)) {
+        constexpr int m = decltype(M)::value, n = decltype(Nn)::value;
+        const bool up = (lane & m) != 0;
+#pragma unroll
+        for (int u = 0; u < n / 2; ++u) {
+          const double send = up ? d[u] : d[u + n / 2];
+          const double keep = up ? d[u + n / 2] : d[u];
+          d[u] = keep + __shfl_xor(send, m);
+        }
+      };
+      half(std::integral_constant<int, 8>(), std::integral_constant<int, 8>());
+      half(std::integral_constant<int, 4>(), std::integral_constant<int, 4>());
+      half(std::integral_constant<int, 2>(), std::integral_constant<int, 2>());
+      d[0] += __shfl_xor(d[0], 1);
+      // lanes l and l ^ 1 hold the same value: both store it (no lane branch)
+      const int co = c0 + 2 * ((lane >> 3) & 1) + ((lane >> 2) & 1);
+      const int off = ((z * COP + co) * 2 + ((lane >> 1) & 1)) * (int)sizeof(double) + pskip;
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2v, d[0]), prs, off, 0, 0);
+    }
+  };
+
+  // Pipeline per segment: [barrier] patch(cur) -> LDS [barrier] prefetch(next) loads, epilogue(prev)
+  // stores, MFMAs(cur).  The next patch's loads and the previous segment's output stores are both
+  // issued before the MFMAs, so the waits at the next patch write find them done.
+  int tile = blockIdx.x;
+  Seg g = seg_of(tile, Ho, Wo, nseg);
+  prefetch(g);
+  Seg prev = g;
+  bool have_prev = false;
+  // a dropped epilogue behind the first loads: the loop is entered with the same loads-then-stores
+  // queue as its back edge, so the waits at the patch write stay counted (a merge with an entry state
+  // without the stores makes the last one vmcnt(0))
+  __builtin_amdgcn_sched_barrier(0);
+  epilogue(prev, false);
+  for (;;) {
+    __syncthreads();  // every wave is done reading the previous patch (and the weights are in)
+    store_patch(g);   // past the last segment: a re-load of the last one, never read
+    __syncthreads();
+    const Seg cur = g;
+    const int nxt = tile + gridDim.x;
+    // the loads first: the epilogue's store data registers are then never a load's destination (a
+    // register an in-flight store still reads is only reusable after vmcnt(0)).  No branch around the
+    // loads or the stores either, so every wait for a load stays a counted one.
+    g = seg_of(nxt < T ? nxt : (tile < T ? tile : T - 1), Ho, Wo, nseg);  // past the end: a re-load
+    prefetch(g);
+    __builtin_amdgcn_sched_barrier(0);  // keep the loads ahead of the stores
+    epilogue(prev, have_prev);
+    if (tile >= T) break;
+    if (32 * sub < cur.L) compute();  // no VMEM inside: a branch here costs no wait
+    prev = cur;
+    have_prev = true;
+    tile = nxt;
+  }
+}
+
+}  // namespace c4
+
+// Routing: does the direct kernel take this forward conv?  4 input channels, 64 outputs, stride 1,
+// 7 x S (S <= 8) filters, split-bf16 math, and rows that split into whole 256-pixel segments (or one
+// shorter one): a short last segment would cost a whole segment's time.  Its InstanceNorm partials
+// are per 32-pixel row piece, so an image whose H*W is a multiple of 32 (the callers then ask for
+// partials) must also have Wo % 32 == 0: a conv is routed the same way with and without partials.
+static const bool g_c4_direct = [] {
+  const char* e = getenv("VST_C4_DIRECT");
+  return !(e && e[0] == '0');
+}();
+
+bool c4_direct_ok(int C, int Cop, int R, int S, int st, int Ho, int Wo, int math) {
+  return g_c4_direct && C == 4 && Cop == c4::COP && st == 1 && R == 7 && S >= 1 && S <= c4::MAXR &&
+         (math == VST_MATH_BF16X6 || math == VST_MATH_BF16X3) && (Wo <= c4::SEG || Wo % c4::SEG == 0) &&
+         (Wo % 32 == 0 || ((long)Ho * Wo) % 32 != 0);
+}
+
+int c4_direct_launch(const float* x, const void* wsplit, long wps, const float* bias, float* y, int N, int H, int W,
+                     int Ho, int Wo, int R, int S, int pad, int reflect, int act, float slope, int math, double* part,
+                     hipStream_t s) {
+  const int nseg = (Wo + c4::SEG - 1) / c4::SEG;
+  VST_REQUIRE(R == 7 && S <= c4::MAXR, "conv_c4_direct: 7 x S (S <= 8) filters only");
+  VST_REQUIRE((long)N * Ho * nseg < (1L << 31), "conv_c4_direct: too many segments");
+  VST_REQUIRE((long)N * H * W * 16 < 0x7ffffff0L, "conv_c4_direct: input over 2 GB (32-bit buffer offsets)");
+  const int T = N * Ho * nseg;
+  const int grid = T < VST_NUM_CUS ? T : VST_NUM_CUS;
+  const __bf16* ws = reinterpret_cast<const __bf16*>(wsplit);
+  // the activation is a template argument: a runtime one makes every epilogue element evaluate all
+  // of them (tanh included) and select
+#define VST_C4D(NP_, ACT_)                                                                                         \
+  hipLaunchKernelGGL((c4::conv_c4_direct_k<NP_, 7, ACT_>), dim3(grid), dim3(c4::NT), 0, s, x, ws, wps, bias, y, H, W, \
+                     Ho, Wo, S, pad, reflect, slope, nseg, T, N, part)
+#define VST_C4D_ACT(NP_)                                \
+  switch (act) {                                        \
+    case VST_ACT_RELU: VST_C4D(NP_, VST_ACT_RELU); break;   \
+    case VST_ACT_LRELU: VST_C4D(NP_, VST_ACT_LRELU); break; \
+    case VST_ACT_TANH: VST_C4D(NP_, VST_ACT_TANH); break;   \
+    default: VST_C4D(NP_, VST_ACT_NONE); break;             \
+  }
+  if (math == VST_MATH_BF16X6) {
+    VST_C4D_ACT(3)
+  } else {
+    VST_C4D_ACT(2)
+  }
+#undef VST_C4D_ACT
+#undef VST_C4D
+  return check_launch("conv2d_fwd(4-channel direct)");
+}
+
+}  // namespace vst

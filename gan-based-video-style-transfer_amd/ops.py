@@ -338,11 +338,12 @@ def debug_set_tiles(fprop=-1, tconv=-1, wgrad=-1):
     lib().vst_debug_set_tiles(int(fprop), int(tconv), int(wgrad))
 
 
-PLAN_RK, PLAN_SKINNY = -1, -2
+PLAN_RK, PLAN_SKINNY, PLAN_C4_DIRECT = -1, -2, -3
 TILE_NAMES = {0: "128x128 (8 waves of 64x32)", 1: "128x64", 2: "128x128 (4 waves of 64x64)", 3: "64x128",
               4: "128x128 BK64", 5: "128x64 BK64", 6: "64x64", 7: "256x128 (8 waves of 64x64)", 8: "64x64 BK64",
               9: "128x128 BK16 (4 waves of 64x64, 2 blocks/CU at x6)",
-              PLAN_RK: "fp32 [row][k] kernel", PLAN_SKINNY: "VALU skinny kernel"}
+              PLAN_RK: "fp32 [row][k] kernel", PLAN_SKINNY: "VALU skinny kernel",
+              PLAN_C4_DIRECT: "4-channel patch-staged direct kernel"}
 
 
 WPLAN_NAMES = {0: "conv_wgrad_k (NHWC operands)", 1: "copies + conv_wgrad_rk_k", 2: "copies + conv_wgrad_bf_k",

@@ -214,10 +214,11 @@ long vst_cp_ld(long P);
 void vst_debug_set_tiles(int fprop, int tconv, int wgrad);
 /* Host-only planning query (no launch, no device needed): the kernel vst_conv2d_fwd would run for
  * this shape and `math` on this thread.  *kind = split-arithmetic tile kind (0..8, see
- * vst_debug_set_tiles; 7 = 256x128), VST_PLAN_RK (fp32 [row][k] kernel) or VST_PLAN_SKINNY
- * (<= 4 output channels, VALU); *m_split = first output-pixel row of the wave-quantisation tail
+ * vst_debug_set_tiles; 7 = 256x128), VST_PLAN_RK (fp32 [row][k] kernel), VST_PLAN_SKINNY
+ * (<= 4 output channels, VALU) or VST_PLAN_C4_DIRECT (4 input channels, 64 outputs, stride 1,
+ * R, S <= 8: the patch-staged direct kernel, conv_c4.hip); *m_split = first output-pixel row of the wave-quantisation tail
  * launch, 0 when the grid runs as one launch; *tail_kind = that tail launch's tile kind (-1: none). */
-enum { VST_PLAN_RK = -1, VST_PLAN_SKINNY = -2 };
+enum { VST_PLAN_RK = -1, VST_PLAN_SKINNY = -2, VST_PLAN_C4_DIRECT = -3 };
 int vst_conv_plan_fwd(int N, int H, int W, int Cx, int Cop, int R, int S, int stride, int pad_h,
                       int pad_w, int math, int* kind, int* m_split, int* tail_kind);
 /* Host-only planning query for vst_conv2d_wgrad: *path = VST_WPLAN_BF (channel-major copies + the

@@ -154,6 +154,23 @@ def test_conv_planner_picks_production_kernels():
     # the generator's first conv: a 4-channel image on the split-bf16 kernels (not the fp32 rk path)
     assert ops.conv_plan_fwd(8, 256, 256, 4, 64, 7, 7, 1, 3, 3, "bf16x6")[0] not in (ops.PLAN_RK, ops.PLAN_SKINNY)
     assert ops.conv_plan_fwd(8, 256, 256, 4, 64, 7, 7, 1, 3, 3, "fp32")[0] == ops.PLAN_RK
+    # 4 channels -> 64 at stride 1 (the generator's c0 at 256^2 and at Sintel width, a zero-pad-6 frame,
+    # a short row): the patch-staged direct kernel; not where a row would end in a short extra
+    # segment (the last layer's 262-wide data-gradient frame), nor where its InstanceNorm partials could
+    # not follow the 32-pixel groups (H*W % 32 == 0 but Wo % 32 != 0), nor under a forced tile
+    for shp in [(8, 256, 256, 3), (1, 436, 1024, 3), (8, 250, 250, 6), (2, 20, 18, 3)]:
+        N_, H_, W_, p_ = shp
+        for m_ in ("bf16x6", "bf16x3"):
+            assert ops.conv_plan_fwd(N_, H_, W_, 4, 64, 7, 7, 1, p_, p_, m_)[0] == ops.PLAN_C4_DIRECT, (shp, m_)
+    assert ops.conv_plan_fwd(2, 8, 8, 4, 64, 7, 7, 1, 3, 3, "bf16x6")[0] != ops.PLAN_C4_DIRECT
+    assert ops.conv_plan_fwd(8, 256, 256, 4, 64, 7, 7, 1, 6, 6, "bf16x6")[0] != ops.PLAN_C4_DIRECT
+    assert ops.conv_plan_fwd(2, 32, 32, 4, 64, 4, 4, 2, 1, 1, "bf16x6")[0] != ops.PLAN_C4_DIRECT
+    assert ops.conv_plan_fwd(2, 32, 32, 4, 32, 7, 7, 1, 3, 3, "bf16x6")[0] != ops.PLAN_C4_DIRECT
+    ops.debug_set_tiles(1, -1, -1)
+    try:
+        assert ops.conv_plan_fwd(8, 256, 256, 4, 64, 7, 7, 1, 3, 3, "bf16x6")[0] == 1
+    finally:
+        ops.debug_set_tiles(-1, -1, -1)
     ops.debug_set_tiles(7, -1, -1)
     try:
         assert ops.conv_plan_fwd(2, 12, 10, 32, 32, 3, 3, 1, 1, 1, "bf16x3") == (7, 0)

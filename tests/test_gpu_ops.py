@@ -786,3 +786,50 @@ def test_dgrad_reflect_border(ops, conv_math, case):
     _close(dx, dx_fold, tol=CONV_TOL[conv_math], what=name + " vs fold path")
     if cx > Ci:
         assert float(dx[..., Ci:].abs().max()) == 0.0
+
+
+@pytest.mark.parametrize("shape", [
+    # N, H, W, pad, mode, act
+    (2, 256, 256, 3, "reflect", "none"),   # the generator's c0 at 256^2: one 256-pixel segment per row
+    (1, 436, 1024, 3, "reflect", "none"),  # Sintel width: 4 segments per row
+    (2, 250, 250, 6, "zero", "none"),      # zero padding 6 (a data-gradient-style frame), 256-wide rows
+    (1, 20, 512, 3, "reflect", "relu"),    # two 256-pixel segments per row
+    (3, 20, 18, 3, "reflect", "lrelu"),    # a partial 32-row sub-tile
+    (2, 64, 64, 3, "reflect", "tanh"),
+], ids=lambda s: "x".join(str(v) for v in s))
+def test_conv_c4_direct(ops, shape, conv_math):
+    """The patch-staged direct kernel for 4-channel inputs with 64 outputs (conv_c4.hip; the generator's
+    7x7 image convs): output vs torch fp32, vs the implicit-GEMM 4-channel route (forced tile), and —
+    where Wo % 32 == 0 — the epilogue's InstanceNorm statistics vs torch."""
+    if conv_math == "fp32":
+        pytest.skip("the direct kernel is a split-bf16 kernel (fp32 runs the [row][k] path)")
+    N, H, W, pad, mode, act = shape
+    Ci, Co, k = 3, 64, 7
+    x = _g(81, (N, Ci, H, W))
+    w = _g(82, (Co, Ci, k, k), 0.05)
+    b = _g(83, (Co,), 0.1)
+    kc = ops.weight_pack(w.to(DEV), ops.PACK_FWD)
+    bp = b.to(DEV).contiguous()
+    xn = _nhwc(x, ops)
+    assert ops.conv_plan_fwd(N, H, W, 4, Co, k, k, 1, pad, pad, conv_math)[0] == ops.PLAN_C4_DIRECT
+    xp = F.pad(x, (pad,) * 4, mode="reflect") if mode == "reflect" else x
+    yr = F.conv2d(xp, w, b, padding=0 if mode == "reflect" else pad)
+    yr = {"none": yr, "relu": F.relu(yr), "lrelu": F.leaky_relu(yr, 0.2), "tanh": torch.tanh(yr)}[act]
+    y = ops.conv2d_fwd(xn, kc, bp, Co, k, k, 1, pad, mode, act=act, slope=0.2)
+    tol = CONV_TOL[conv_math]
+    _close(_nchw(y, Co, ops), yr, tol=tol, what="c4 direct vs torch")
+    ops.debug_set_tiles(1, -1, -1)  # the implicit-GEMM 4-channel route (128x64 tiles)
+    try:
+        y_ig = ops.conv2d_fwd(xn, kc, bp, Co, k, k, 1, pad, mode, act=act, slope=0.2)
+    finally:
+        ops.debug_set_tiles(-1, -1, -1)
+    _close(y, y_ig, tol=tol, what="c4 direct vs implicit GEMM")
+    Ho, Wo = y.shape[1], y.shape[2]
+    if act == "none" and (Ho * Wo) % 32 == 0:
+        y2, s = ops.conv2d_fwd_in(xn, kc, bp, Co, k, k, 1, pad, mode)
+        assert torch.equal(y2, y)
+        st_ = s.view(N, Co, 2).cpu()
+        mean = yr.mean(dim=(2, 3))
+        rstd = 1.0 / torch.sqrt(yr.var(dim=(2, 3), unbiased=False) + 1e-5)
+        assert ((st_[..., 0] - mean).abs() * rstd).max().item() < 1e-5
+        assert ((st_[..., 1] - rstd).abs() / rstd).max().item() < 1e-4

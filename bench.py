@@ -143,7 +143,8 @@ def conv_roofline(name, probe, math):
         kernel = ("vst_conv2d_dgrad_refl: conv_fprop_bf_k interior (zero pad 1, %s) + border rows as "
                   "split-K conv_fprop_bf_k<REFL=4> + dgrad_border_add_k [%s]" % (m, _mfma(m)))
         key = {"math": m, "N": N, "mfma": _mfma(m), "op": "dgrad_refl"}
-        note = "stride-1 reflect data gradient: interior conv + border GEMM (no padded frame, no fold)"
+        note = ("stride-1 reflect data gradient: interior conv + border GEMM (no padded frame, no fold; the "
+                "border slabs are added by the IN-backward partial pass that follows)")
     else:
         kernel = ("vst_conv2d_wgrad: nhwc_to_cp_pad_k + nhwc_to_cp_planes_k copies + conv_wgrad_bf_k "
                   "(split-K slabs) + wgrad_reduce_store_k, %s" % m if m != "fp32" else
@@ -162,20 +163,36 @@ def conv_roofline(name, probe, math):
 
 def warp_roofline(device, N=32, C=64, H=436, W=1024, reps=10):
     """vst_warp_fwd (utils/flowtools.py warp) on the SURVEY §8d large synthetic: HBM-bound; algorithmic
-    bytes = N*H*W*(4C gather-once + 8 flow + 4C write)."""
+    bytes = N*H*W*(4C gather-once + 8 flow + 4C write).  The flow is §8d's generator at the Sintel size
+    (bicubic upsample of an N(0, 4^2) 9x9 grid, x4 as for C3: smooth, up to ~+-40 px); the same kernel on
+    an i.i.d. N(0, 3^2) px per-pixel flow (no neighbour locality: every corner a separate cache line
+    set) is reported as the worst case."""
+    import torch.nn.functional as F
     from gbvst import ops
     x = torch.randn(N, H, W, C, device=device)
-    flow = torch.randn(N, 2, H, W, device=device) * 3.0
+    g = torch.Generator(device="cpu").manual_seed(4321)
+    coarse = torch.randn(N, 2, 9, 9, generator=g) * 4.0
+    flow = (F.interpolate(coarse, size=(H, W), mode="bicubic", align_corners=True) * 4.0).to(device).contiguous()
     out = torch.empty_like(x)
-    fn = lambda: ops.lib().vst_warp_fwd(x.data_ptr(), flow.data_ptr(), out.data_ptr(), N, H, W, C, 0,  # noqa: E731
-                                        torch.cuda.current_stream().cuda_stream)
-    ms = _time_on_stream(fn, reps)
     nbytes = N * H * W * (8.0 * C + 8.0)
-    gbs = nbytes / (ms * 1e-3) / 1e9
-    del x, out
+
+    def timed(fl):
+        fn = lambda: ops.lib().vst_warp_fwd(x.data_ptr(), fl.data_ptr(), out.data_ptr(), N, H, W, C, 0,  # noqa: E731
+                                            torch.cuda.current_stream().cuda_stream)
+        ms = _time_on_stream(fn, reps)
+        return ms, nbytes / (ms * 1e-3) / 1e9
+
+    ms, gbs = timed(flow)
+    del flow
+    iid = torch.randn(N, 2, H, W, device=device) * 3.0
+    ms_iid, gbs_iid = timed(iid)
+    del x, out, iid
     return {"kernel": "warp_fwd_k (N=%d, C=%d, %dx%d)" % (N, C, H, W), "bound": "hbm",
             "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
-            "avg_launch_ms": round(ms, 4), "bytes_per_launch": nbytes}
+            "avg_launch_ms": round(ms, 4), "bytes_per_launch": nbytes,
+            "flow": "SURVEY 8d smooth synthetic (bicubic 9x9 N(0,4^2) grid, x4)",
+            "iid_flow_worst_case": {"flow": "i.i.d. N(0, 3^2) px per pixel", "achieved": round(gbs_iid, 1),
+                                    "frac": round(gbs_iid / HBM_PEAK_GBS, 4), "avg_launch_ms": round(ms_iid, 4)}}
 
 
 def corr_volume(device, B=1, D=256, H=55, W=128, reps=5):

@@ -132,6 +132,10 @@ SIGNATURES = {
     "vst_u8_image_to_nhwc4": (I, [P, P, L, P]),
     "vst_conv2d_dgrad_refl_ws_bytes": (SZ, [I, I, I, I, I, I]),
     "vst_conv2d_dgrad_refl": (I, [P, P, P, P, P, SZ, I, I, I, I, I, I, P]),
+    "vst_conv2d_dgrad_refl_in_ws_bytes": (SZ, [I, I, I, I, I, I]),
+    "vst_conv2d_dgrad_refl_in": (I, [P, P, P, P, P, P, P, P, P, SZ, I, I, I, I, I, I, F, I, P, L, I, P]),
+    "vst_conv2d_dgrad_refl_slabs": (I, [P, P, P, P, P, SZ, I, I, I, I, I, I, P]),
+    "vst_instnorm_act_bwd_refl_border": (I, [P, P, P, P, P, P, P, I, I, I, I, I, I, F, I, P, L, I, P]),
     # SURVEY §8b spelling (abi.hip)
     "vst_conv_desc_out_hw": (I, [P, P, P]),
     "vst_workspace_size": (SZ, [P, I]),

@@ -50,6 +50,26 @@ __device__ __forceinline__ int reflect_idx(int i, int n) {
   return i >= n ? 2 * n - 2 - i : i;
 }
 
+// The border rows of a ReflectionPad2d(1) + 3x3 data gradient (conv_bf.hip dgrad_border_pos: per
+// image NB = dgrad_border_rows rows of padded positions) that add into pixel (h, w): 0 for a pixel no
+// padded position mirrors onto, 1 for the single-target rows / columns, 3 for the four corner targets
+// (1 | H-2, 1 | W-2).  *b0 = the first such row.
+__host__ __device__ __forceinline__ int dgrad_border_rows_of(int h, int w, int H, int W, int* b0) {
+  const int sw = W - 2, sh = H - 2, S4 = ((2 * sw + 2 * sh + 3) / 4) * 4;
+  const bool rh = h == 1 || h == H - 2, rw = w == 1 || w == W - 2;
+  if (rh && rw) {
+    *b0 = S4 + 4 * ((h == 1 ? 0 : 2) + (w == 1 ? 0 : 1));
+    return 3;
+  }
+  const int kw = w == 0 ? 0 : (w == W - 1 ? sw - 1 : w - 1);
+  const int kh = h == 0 ? 0 : (h == H - 1 ? sh - 1 : h - 1);
+  if (h == 1) { *b0 = kw; return 1; }
+  if (h == H - 2) { *b0 = sw + kw; return 1; }
+  if (w == 1) { *b0 = 2 * sw + kh; return 1; }
+  if (w == W - 2) { *b0 = 2 * sw + sh + kh; return 1; }
+  return 0;
+}
+
 __device__ __forceinline__ float apply_act(float v, int act, float slope) {
   if (act == VST_ACT_RELU) return v > 0.f ? v : 0.f;
   if (act == VST_ACT_LRELU) return v > 0.f ? v : v * slope;
@@ -103,6 +123,14 @@ bool c4_direct_ok(int C, int Cop, int R, int S, int st, int Ho, int Wo, int math
 int c4_direct_launch(const float* x, const void* wsplit, long wps, const float* bias, float* y, int N, int H, int W,
                      int Ho, int Wo, int R, int S, int pad, int reflect, int act, float slope, int math, double* part,
                      hipStream_t s);
+// ReflectionPad2d(1) + 3x3 data gradient: interior GEMM + border-GEMM slabs (+ their add unless the
+// caller takes them: add_border = false)
+bool bf_dgrad_refl1_ok(int N, int H, int W, int Cy, int Cx, int math);
+size_t bf_dgrad_refl1_ws_floats(int N, int H, int W, int Cy, int Cx, int math);
+size_t bf_dgrad_refl1_slabs(int N, int H, int W, int Cy, int Cx, int math, int* ks, int* nb);
+int bf_dgrad_refl1_launch(const float* dy, const void* wsplit, long wps, const float* addend, float* dx, int N, int H,
+                          int W, int Cy, int Cx, int math, hipStream_t s, float* ws, size_t ws_floats, bool add_border,
+                          const float** slab_out, int* ks_out, int* nb_out);
 size_t bf_fprop_ws_floats(long M, int Cop, int C, int R, int S, int math);
 int bf_tail_ks(long M, int Cop, int m_split, int nk);
 void bf_split_plan(long M, int Cop, int C, int R, int S, int math, int kind, int* m_first, int* ks_out);

@@ -1492,6 +1492,14 @@ bool bf_dgrad_refl1_ok(int N, int H, int W, int Cy, int Cx, int math) {
   return math != VST_MATH_F32 && VST_BF_KSLICE && Cy % 32 == 0 && Cx % 4 == 0 && H >= 4 && W >= 4 && N > 0;
 }
 
+// where the border GEMM's slabs sit in the dgrad workspace (floats) and their split count / rows per image
+size_t bf_dgrad_refl1_slabs(int N, int H, int W, int Cy, int Cx, int math, int* ks, int* nb) {
+  long Mb;
+  bf_border_plan(N, H, W, Cy, Cx, math, ks, &Mb);
+  *nb = bf::dgrad_border_rows(H, W);
+  return bf_fprop_ws_floats((long)N * H * W, Cx, Cy, 3, 3, math);
+}
+
 size_t bf_dgrad_refl1_ws_floats(int N, int H, int W, int Cy, int Cx, int math) {
   int ks;
   long Mb;
@@ -1502,9 +1510,12 @@ size_t bf_dgrad_refl1_ws_floats(int N, int H, int W, int Cy, int Cx, int math) {
 // dx = data gradient of ReflectionPad2d(1) + 3x3 conv (stride 1) from dy (+ addend), wsplit = the
 // VST_PACK_IKF planes of the conv weight: the interior as the zero-pad-1 forward conv (addend in its
 // epilogue), then the border GEMM (split-K slabs) and dgrad_border_add_k.  Replaces the conv over the
-// (H+2) x (W+2) zero-padded frame + reflect fold.
+// (H+2) x (W+2) zero-padded frame + reflect fold.  add_border = false: the slabs are left for the
+// caller (vst_conv2d_dgrad_refl_in adds them in its InstanceNorm-backward partial pass); *slab_out,
+// *ks_out, *nb_out describe them.
 int bf_dgrad_refl1_launch(const float* dy, const void* wsplit, long wps, const float* addend, float* dx, int N, int H,
-                          int W, int Cy, int Cx, int math, hipStream_t s, float* ws, size_t ws_floats) {
+                          int W, int Cy, int Cx, int math, hipStream_t s, float* ws, size_t ws_floats, bool add_border,
+                          const float** slab_out, int* ks_out, int* nb_out) {
   int ks;
   long Mb;
   bf_border_plan(N, H, W, Cy, Cx, math, &ks, &Mb);
@@ -1529,8 +1540,12 @@ int bf_dgrad_refl1_launch(const float* dy, const void* wsplit, long wps, const f
     hipLaunchKernelGGL((bf::conv_fprop_bf_k<T, true, 4, true>), grid, dim3(T::NT), 0, s, dy, wb, wps, nullptr, dx, H,
                        W, Cy, H, NB, Cx, 3, 1, 1, 1, 0, VST_ACT_NONE, 0.f, (int)Mb, K, 0, nullptr, spk, slab, nullptr);
   }
-  hipLaunchKernelGGL(bf::dgrad_border_add_k, dim3(ceil_div(Mb, 16), ceil_div(Cx, 64)), dim3(256), 0, s, slab, ks,
-                     (int)Mb, Cx, dx, H, W, NB);
+  if (slab_out) *slab_out = slab;
+  if (ks_out) *ks_out = ks;
+  if (nb_out) *nb_out = NB;
+  if (add_border)
+    hipLaunchKernelGGL(bf::dgrad_border_add_k, dim3(ceil_div(Mb, 16), ceil_div(Cx, 64)), dim3(256), 0, s, slab, ks,
+                       (int)Mb, Cx, dx, H, W, NB);
   return check_launch("conv2d_dgrad_refl");
 }
 
@@ -1615,5 +1630,5 @@ extern "C" int vst_conv2d_dgrad_refl(const float* dy, const void* wsplit, const 
     return VST_EUNSUPPORTED;
   }
   return bf_dgrad_refl1_launch(dy, wsplit, (long)Cx * 9 * Cy, addend, dx, N, H, W, Cy, Cx, math, (hipStream_t)stream,
-                               ws, ws_bytes / sizeof(float));
+                               ws, ws_bytes / sizeof(float), true, nullptr, nullptr, nullptr);
 }

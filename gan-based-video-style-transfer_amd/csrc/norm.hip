@@ -238,6 +238,114 @@ __global__ __launch_bounds__(NRED) void fold_in_partial_k(const float* __restric
   }
 }
 
+// The border add of a ReflectionPad2d(1) + 3x3 data gradient (conv_bf.hip: the interior conv left g
+// without the padded border positions, whose GEMM left ks split-K slabs [ks][N*NB][C]) fused with the
+// backward partials of the InstanceNorm(+act) below it: the pixels a padded position mirrors onto
+// (rows / columns 1 and H-2 / W-2: ~6 % at 64 x 64) get the slab sums added (split order, then row
+// order: dgrad_border_add_k's arithmetic) and written back; every pixel's g is then reduced while in
+// registers.  Replaces dgrad_border_add_k + in_partial_k<1>: one read of g and two launches fewer.
+// Same block geometry / partial layout / summation order as in_partial_k<1>.
+__global__ __launch_bounds__(NRED) void border_in_partial_k(float* __restrict__ g, const float* __restrict__ slab,
+                                                            int ks, int Mb, int NB, const float* __restrict__ x,
+                                                            const float* __restrict__ stats, double* __restrict__ part,
+                                                            int H, int W, int C, int LP, int PG, int SP, int nsplit,
+                                                            int act, float slope) {
+  constexpr int NV = 3;
+  __shared__ double red[NV * 4][NRED];
+  const int t = threadIdx.x, c4 = t % LP, pg = t / LP;
+  const int n = blockIdx.y, z = blockIdx.x;
+  const int HW = H * W;
+  const int p0 = z * SP, p1 = min(HW, p0 + SP);
+  double acc[NV][4];
+#pragma unroll
+  for (int v = 0; v < NV; ++v)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[v][j] = 0.0;
+  float mean[4], rstd[4];
+  {
+    const float4 s0 = reinterpret_cast<const float4*>(stats)[((long)n * C + 4 * c4) / 2];
+    const float4 s1 = reinterpret_cast<const float4*>(stats)[((long)n * C + 4 * c4) / 2 + 1];
+    mean[0] = s0.x; rstd[0] = s0.y; mean[1] = s0.z; rstd[1] = s0.w;
+    mean[2] = s1.x; rstd[2] = s1.y; mean[3] = s1.z; rstd[3] = s1.w;
+  }
+  const float4* xb = reinterpret_cast<const float4*>(x) + (long)n * HW * LP + c4;
+  float4* gb = reinterpret_cast<float4*>(g) + (long)n * HW * LP + c4;
+  const long zst = (long)Mb * C;
+  // g of pixel p: + its border rows' slab sums where a padded position mirrors onto it (written back)
+  auto border = [&](int p, float4 gv) {
+    int b0;
+    const int nr = dgrad_border_rows_of(p / W, p - (p / W) * W, H, W, &b0);
+    if (nr == 0) return gv;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int r = 0; r < nr; ++r) {
+      // a row's (<= 16) split slabs loaded together, then summed in split order
+      const float* base = slab + ((long)n * NB + b0 + r) * C + 4 * c4;
+      float4 u[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q)
+        if (q < ks) u[q] = *reinterpret_cast<const float4*>(base + q * zst);
+      float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int q = 0; q < 16; ++q)
+        if (q < ks) add_f4(a, u[q]);
+      add_f4(v, a);
+    }
+    add_f4(gv, v);
+    gb[(long)p * LP] = gv;
+    return gv;
+  };
+  auto accum = [&](const float4 v, const float4 gv) {
+    const float xv[4] = {v.x, v.y, v.z, v.w}, gg[4] = {gv.x, gv.y, gv.z, gv.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float xh = (xv[j] - mean[j]) * rstd[j];
+      float d = 1.f;
+      if (act == VST_ACT_RELU) d = xh > 0.f ? 1.f : 0.f;
+      else if (act == VST_ACT_LRELU) d = xh > 0.f ? 1.f : slope;
+      const float gm = gg[j] * d;
+      acc[0][j] += gm;
+      acc[1][j] += (double)gm * xh;
+      acc[2][j] += xh;
+    }
+  };
+  constexpr int UR = IN_UNROLL;
+  if (pg < PG) {
+    int p = p0 + pg;
+    for (; p + (UR - 1) * PG < p1; p += UR * PG) {
+      float4 v[UR], gv[UR];
+#pragma unroll
+      for (int k = 0; k < UR; ++k) {
+        v[k] = xb[(long)(p + k * PG) * LP];
+        gv[k] = gb[(long)(p + k * PG) * LP];
+      }
+#pragma unroll
+      for (int k = 0; k < UR; ++k) accum(v[k], border(p + k * PG, gv[k]));
+    }
+    for (; p < p1; p += PG) accum(xb[(long)p * LP], border(p, gb[(long)p * LP]));
+  }
+#pragma unroll
+  for (int v = 0; v < NV; ++v)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) red[v * 4 + j][t] = acc[v][j];
+  __syncthreads();
+  if (pg == 0) {
+    double out[NV][4];
+#pragma unroll
+    for (int v = 0; v < NV; ++v)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        double sum = 0.0;
+        for (int q = 0; q < PG; ++q) sum += red[v * 4 + j][q * LP + c4];
+        out[v][j] = sum;
+      }
+    double* dst = part + (((long)n * nsplit + z) * C + 4 * c4) * NV;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int v = 0; v < NV; ++v) dst[j * NV + v] = out[v][j];
+  }
+}
+
 // Fold the per-slice partials of one (n, CPB-channel group): G = 256 / CPB thread groups stride the
 // slices (coalesced over c), then combine through LDS in a fixed order.  out[v] = sum_z
 // part[n][z][c][v].  CPB = 16 for the IN finalizes (4x the blocks of CPB = 64: these small kernels are
@@ -894,6 +1002,64 @@ extern "C" int vst_reflect_fold_instnorm_bwd(const float* dxp, const float* adde
   hipLaunchKernelGGL(fold_in_partial_k, dim3(g.nsplit, N), dim3(NRED), 0, s, dxp, addend, gout, x, stats, part,
                      H, W, C, pad, g.LP, g.PG, g.SP, g.nsplit, act, slope);
   return in_bwd_tail(gout, x, stats, dx, db, ws, N, HW, C, act, slope, accumulate_db, planes, ldp, g, s);
+}
+
+// ReflectionPad2d(1) + 3x3 conv data gradient (vst_conv2d_dgrad_refl) and the InstanceNorm(+act)
+// backward of the layer below it: the interior GEMM (+ addend) writes g, the border GEMM leaves its
+// slabs (vst_conv2d_dgrad_refl_slabs, in the dgrad workspace), then border_in_partial_k adds them into
+// g while taking the IN partials, the finalize and the apply (+ dy planes) follow
+// (vst_instnorm_act_bwd_refl_border).  vst_conv2d_dgrad_refl_in = both, one workspace: the IN
+// partials / coefficients, then the dgrad's.
+static size_t in_ws_bytes_al(int N, int HW, int C) { return (vst_instnorm_ws_bytes(N, HW, C) + 255) / 256 * 256; }
+
+extern "C" int vst_conv2d_dgrad_refl_slabs(const float* dy, const void* wsplit, const float* addend, float* gout,
+                                           float* ws, size_t ws_bytes, int N, int H, int W, int Cy, int Cx, int math,
+                                           void* stream) {
+  VST_REQUIRE(dy && wsplit && gout && ws, "conv2d_dgrad_refl_slabs: null pointer");
+  VST_REQUIRE(bf_dgrad_refl1_ok(N, H, W, Cy, Cx, math),
+              "conv2d_dgrad_refl_slabs: needs split-bf16 math, Cy %% 32 == 0, Cx %% 4 == 0, H, W >= 4");
+  return bf_dgrad_refl1_launch(dy, wsplit, (long)Cx * 9 * Cy, addend, gout, N, H, W, Cy, Cx, math, (hipStream_t)stream,
+                               ws, ws_bytes / sizeof(float), false, nullptr, nullptr, nullptr);
+}
+
+extern "C" int vst_instnorm_act_bwd_refl_border(float* gout, const float* x, const float* stats, float* dx, float* db,
+                                                float* in_ws, const float* dgrad_ws, int N, int H, int W, int Cy,
+                                                int Cx, int act, float slope, int accumulate_db, void* planes,
+                                                long ldp, int math, void* stream) {
+  RedGeom g;
+  const int HW = H * W;
+  VST_REQUIRE(gout && x && stats && dx && in_ws && dgrad_ws, "instnorm_act_bwd_refl_border: null pointer");
+  VST_REQUIRE(bf_dgrad_refl1_ok(N, H, W, Cy, Cx, math) && red_geom(N, HW, Cx, g),
+              "instnorm_act_bwd_refl_border: unsupported shape / arithmetic");
+  VST_REQUIRE(!planes || ldp >= (long)N * HW, "instnorm_act_bwd_refl_border: plane stride %ld < N*HW", ldp);
+  int ks, NB;
+  const size_t off = bf_dgrad_refl1_slabs(N, H, W, Cy, Cx, math, &ks, &NB);
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(border_in_partial_k, dim3(g.nsplit, N), dim3(NRED), 0, s, gout, dgrad_ws + off, ks, N * NB, NB, x,
+                     stats, reinterpret_cast<double*>(in_ws), H, W, Cx, g.LP, g.PG, g.SP, g.nsplit, act, slope);
+  return in_bwd_tail(gout, x, stats, dx, db, in_ws, N, HW, Cx, act, slope, accumulate_db, planes, ldp, g, s);
+}
+
+extern "C" size_t vst_conv2d_dgrad_refl_in_ws_bytes(int N, int H, int W, int Cy, int Cx, int math) {
+  RedGeom g;
+  if (!bf_dgrad_refl1_ok(N, H, W, Cy, Cx, math) || !red_geom(N, H * W, Cx, g)) return 0;
+  return in_ws_bytes_al(N, H * W, Cx) + bf_dgrad_refl1_ws_floats(N, H, W, Cy, Cx, math) * sizeof(float);
+}
+
+extern "C" int vst_conv2d_dgrad_refl_in(const float* dy, const void* wsplit, const float* addend, float* gout,
+                                        const float* x, const float* stats, float* dx, float* db, float* ws,
+                                        size_t ws_bytes, int N, int H, int W, int Cy, int Cx, int act, float slope,
+                                        int accumulate_db, void* planes, long ldp, int math, void* stream) {
+  VST_REQUIRE(ws && ws_bytes >= vst_conv2d_dgrad_refl_in_ws_bytes(N, H, W, Cy, Cx, math) &&
+                  vst_conv2d_dgrad_refl_in_ws_bytes(N, H, W, Cy, Cx, math) > 0,
+              "conv2d_dgrad_refl_in: unsupported shape or workspace too small (%zu bytes)", ws_bytes);
+  const size_t inb = in_ws_bytes_al(N, H * W, Cx);
+  float* dws = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + inb);
+  if (int e = vst_conv2d_dgrad_refl_slabs(dy, wsplit, addend, gout, dws, ws_bytes - inb, N, H, W, Cy, Cx, math,
+                                          stream))
+    return e;
+  return vst_instnorm_act_bwd_refl_border(gout, x, stats, dx, db, ws, dws, N, H, W, Cy, Cx, act, slope,
+                                          accumulate_db, planes, ldp, math, stream);
 }
 
 static int in_bwd_tail(const float* gy, const float* x, const float* stats, float* dx, float* db, float* ws,

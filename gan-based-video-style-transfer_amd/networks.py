@@ -443,6 +443,12 @@ IN_XT = os.environ.get("VST_IN_XT", "1") != "0"
 # but its per-thread fp64 reduction chains run on the fold's (nsplit x N)-block geometry, slower
 # than the elementwise fold + separate partials (C2 step A/B: 65.43 vs 65.24 ms; planes-only 64.80).
 FOLD_IN = os.environ.get("VST_FOLD_IN", "0") == "1"
+# The ReflectionPad2d(1) data gradient's border add taken by the IN backward partial pass of the layer
+# below (ops.conv2d_dgrad_refl_in: one read of g and one launch fewer per ResnetBlock data gradient,
+# results bit-identical).  Opt-in (VST_DGRAD_IN=1): slower in the step (C2 A/B, same box: 65.6 vs
+# 64.75 ms) — the per-pixel border test and the target pixels' slab loads stall the partial pass's
+# load stream more than the separate border pass costs.
+DGRAD_IN = os.environ.get("VST_DGRAD_IN", "0") == "1"
 # The discriminator head (1 real output channel of 4) runs the one-channel skinny forward
 # (ops.conv2d_fwd(co_real=1)); VST_D_CO1=0 keeps the 4-channel sums.
 D_CO1 = os.environ.get("VST_D_CO1", "1") != "0"
@@ -643,11 +649,22 @@ class _GeneratorFn(torch.autograd.Function):
         def dgrad_reflect_in(dy, key, H, W, y_in, s_in, act, mod, x_w, R_w, st_w, addend=None):
             """dgrad_reflect (3x3, pad 1) + the IN(+act) backward of the layer below it (y_in, s_in;
             mod = the conv feeding that IN; x_w / R_w / st_w = that conv's weight-gradient input
-            and geometry) -> (g, dy_in, dy_in planes or None).  The fold and the IN backward
-            partials are one pass (ops.conv2d_dgrad_s1_in) when the data gradient runs as a forward
-            conv; otherwise the two steps run separately."""
+            and geometry) -> (g, dy_in, dy_in planes or None).  On the border route the border add
+            rides in the IN backward partial pass (ops.conv2d_dgrad_refl_in); with VST_FOLD_IN=1 the
+            fold and the partials are one pass (ops.conv2d_dgrad_s1_in); otherwise the two steps run
+            separately."""
             ikf = P["ikf"].get(key)
             cin_p = y_in.shape[-1]
+            if DGRAD_IN and not FOLD_IN and ikf is not None and dy.shape[-1] % 8 == 0:
+                db = mod.bias.grad if (train_w and mod.bias is not None) else None
+                N = x_w.shape[0]
+                want = (train_w and IN_PLANES and
+                        _wgrad_on_bf(N, x_w.shape[1], x_w.shape[2], x_w.shape[3], y_in.shape[1], y_in.shape[2],
+                                     cin_p, R_w, st_w, ops.get_conv_math()))
+                r = ops.conv2d_dgrad_refl_in(dy, ikf, H, W, cin_p, y_in, s_in, act, 0.0, addend=addend, db=db,
+                                             planes=want)
+                if r is not None:
+                    return r if want else (r[0], r[1], None)
             if FOLD_IN and ikf is not None and dy.shape[-1] % 8 == 0 and ikf.shape[0] == cin_p:
                 db = mod.bias.grad if (train_w and mod.bias is not None) else None
                 N = x_w.shape[0]

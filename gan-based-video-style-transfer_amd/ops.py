@@ -454,6 +454,41 @@ def conv2d_dgrad_s1_in(dy, ikf, H, W, cx, R, pad, y_in, stats, act="relu", slope
     return (g, dyi, pl) if planes else (g, dyi)
 
 
+def conv2d_dgrad_refl_in(dy, ikf, H, W, cx, y_in, stats, act="relu", slope=0.0, addend=None, db=None,
+                         accumulate_db=True, planes=False, role="bwd"):
+    """ReflectionPad2d(1) + 3x3 data gradient (conv2d_dgrad_s1's interior conv + border GEMM) fused with
+    the InstanceNorm(+act) backward of the layer below it (vst_conv2d_dgrad_refl_in): returns (g, dy_in[,
+    dy_in_planes]) — g = the data gradient (+ addend), dy_in = instnorm_act_bwd(g, y_in, stats, act) —
+    or None when the fused route does not support the shape / arithmetic."""
+    _dev_check(dy, ikf, addend, y_in, stats)
+    if not DGRAD_BORDER or getattr(ikf, "vst_split", None) is None:
+        return None
+    N, Hy, Wy, Cy = dy.shape
+    C = y_in.shape[-1]
+    if (Hy, Wy) != (H, W) or cx != C:
+        return None
+    m = _math(role)
+    nbd = int(lib().vst_conv2d_dgrad_refl_ws_bytes(N, H, W, Cy, C, m))
+    if not nbd or not int(lib().vst_conv2d_dgrad_refl_in_ws_bytes(N, H, W, Cy, C, m)):
+        return None
+    g = torch.empty((N, H, W, C), device=dy.device)
+    dyi = torch.empty_like(g)
+    dws = torch.empty((nbd + 3) // 4, device=dy.device)
+    iws = _in_ws(N, H * W, C, dy.device)
+    pl, ldp = None, 0
+    if planes:
+        ldp = lib().vst_cp_ld(N * H * W)
+        pl = torch.empty((3, C, ldp), device=dy.device, dtype=torch.bfloat16)
+    # two calls (vst_conv2d_dgrad_refl_in's halves) so the data gradient alone carries the launch probe
+    h = _probe_begin("dgrad", (N, H, W, Cy, C, 3, 1, 1, "reflect")) if _probes else None
+    _call("vst_conv2d_dgrad_refl_slabs", _p(dy), _p(ikf.vst_split), _p(addend), _p(g), _p(dws), nbd, N, H, W, Cy, C, m,
+          _stream())
+    _probe_end(h)
+    _call("vst_instnorm_act_bwd_refl_border", _p(g), _p(y_in), _p(stats), _p(dyi), _p(db), _p(iws), _p(dws), N, H, W,
+          Cy, C, ACT[act], float(slope), 1 if accumulate_db else 0, _p(pl), ldp, m, _stream())
+    return (g, dyi, pl) if planes else (g, dyi)
+
+
 def reflect_fold(dxp, p, addend=None):
     _dev_check(dxp, addend)
     N, Hp, Wp, C = dxp.shape

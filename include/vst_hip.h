@@ -267,6 +267,26 @@ int vst_reflect_fold_instnorm_bwd(const float* dxp, const float* addend, float* 
                                   const float* stats, float* dx, float* db, float* ws, int N, int H, int W,
                                   int C, int pad, int act, float slope, int accumulate_db, void* planes, long ldp,
                                   void* stream);
+/* vst_conv2d_dgrad_refl fused with the InstanceNorm(+act) backward of the layer below it (the
+ * ResnetBlock data gradients, networks.py:404-426, each followed by the IN backward of the block's
+ * previous layer): gout = the data gradient (+ addend), x / stats = that IN's input and statistics,
+ * dx = its input gradient (db, planes as vst_instnorm_act_bwd_planes).  The border GEMM's slabs are
+ * added into gout by the same pass that takes the IN partials (one read of gout instead of a border
+ * pass + a partial pass).  gout and dx equal vst_conv2d_dgrad_refl + vst_instnorm_act_bwd_planes bit for
+ * bit.  Same support as vst_conv2d_dgrad_refl (ws_bytes query 0 = unsupported).  In two calls (the
+ * data gradient can then be timed on its own): vst_conv2d_dgrad_refl_slabs (gout without the border,
+ * slabs left in its ws: vst_conv2d_dgrad_refl_ws_bytes) and vst_instnorm_act_bwd_refl_border (in_ws:
+ * vst_instnorm_ws_bytes(N, H*W, Cx); dgrad_ws: that same dgrad workspace). */
+size_t vst_conv2d_dgrad_refl_in_ws_bytes(int N, int H, int W, int Cy, int Cx, int math);
+int vst_conv2d_dgrad_refl_in(const float* dy, const void* wsplit, const float* addend, float* gout, const float* x,
+                             const float* stats, float* dx, float* db, float* ws, size_t ws_bytes, int N, int H,
+                             int W, int Cy, int Cx, int act, float slope, int accumulate_db, void* planes, long ldp,
+                             int math, void* stream);
+int vst_conv2d_dgrad_refl_slabs(const float* dy, const void* wsplit, const float* addend, float* gout, float* ws,
+                                size_t ws_bytes, int N, int H, int W, int Cy, int Cx, int math, void* stream);
+int vst_instnorm_act_bwd_refl_border(float* gout, const float* x, const float* stats, float* dx, float* db,
+                                     float* in_ws, const float* dgrad_ws, int N, int H, int W, int Cy, int Cx, int act,
+                                     float slope, int accumulate_db, void* planes, long ldp, int math, void* stream);
 /* vst_instnorm_act_bwd whose apply pass also writes dx as the three bf16 planes [3][C][ldp] (hi, mid,
  * lo; ldp >= N*HW, vst_cp_ld(N*HW)) the x6 weight gradient of the conv below consumes
  * (vst_conv2d_wgrad_pre).  planes == NULL: identical to vst_instnorm_act_bwd. */

@@ -833,3 +833,51 @@ def test_conv_c4_direct(ops, shape, conv_math):
         rstd = 1.0 / torch.sqrt(yr.var(dim=(2, 3), unbiased=False) + 1e-5)
         assert ((st_[..., 0] - mean).abs() * rstd).max().item() < 1e-5
         assert ((st_[..., 1] - rstd).abs() / rstd).max().item() < 1e-4
+
+
+@pytest.mark.parametrize("case", [
+    # name, N, C_in (= dx = IN channels), C_out (= dy), H, W, act, addend
+    ("small_relu", 2, 32, 32, 16, 16, "relu", True),
+    ("odd_HW_none", 3, 64, 64, 13, 20, "none", False),
+    ("minimal", 1, 32, 64, 4, 4, "relu", True),
+    ("prod_N8", 8, 256, 256, 64, 64, "relu", False),   # the batched G_A calls
+    ("prod_N12", 12, 256, 256, 64, 64, "none", True),  # interior with the split-K tail
+], ids=lambda c: c[0])
+def test_dgrad_refl_in_fused(ops, case):
+    """vst_conv2d_dgrad_refl_in (the border add taken by the IN backward partial pass) vs the separate
+    passes it replaces (vst_conv2d_dgrad_refl + vst_instnorm_act_bwd_planes): g, the IN input gradient,
+    its bf16 planes and the conv-bias gradient all bit-identical; and vs torch autograd."""
+    name, N, Ci, Co, H, W, act, with_add = case
+    prev = ops.set_conv_math("bf16x6")
+    try:
+        w = _g(121, (Co, Ci, 3, 3), 0.05)
+        ikf = ops.weight_pack(w.to(DEV), ops.PACK_IKF)
+        dy = _nhwc(_g(122, (N, Co, H, W)), ops)
+        add = _nhwc(_g(123, (N, Ci, H, W)), ops) if with_add else None
+        y_in = _nhwc(_g(124, (N, Ci, H, W)), ops)
+        s = ops.instnorm_stats(y_in)
+        db0 = torch.zeros(Ci, device=DEV)
+        db1 = torch.zeros(Ci, device=DEV)
+        r = ops.conv2d_dgrad_refl_in(dy, ikf, H, W, Ci, y_in, s, act, addend=add, db=db1, planes=True)
+        assert r is not None
+        g1, dx1, pl1 = r
+        g0 = ops.conv2d_dgrad_s1(dy, ikf, H, W, Ci, 3, 1, "reflect", addend=add)
+        dx0, pl0 = ops.instnorm_act_bwd(g0, y_in, s, act, db=db0, planes=True)
+        assert torch.equal(g1, g0), name
+        assert torch.equal(dx1, dx0), name
+        P = N * H * W  # the plane rows are padded to vst_cp_ld(P): compare the written part
+        assert torch.equal(pl1[:, :, :P], pl0[:, :, :P]), name
+        assert torch.equal(db1, db0), name
+        # vs torch: g = reflect-pad conv data gradient (+ addend); dx = IN(+act) backward of g
+        x = _g(125, (N, Ci, H, W)).requires_grad_(True)
+        yy = F.conv2d(F.pad(x, (1,) * 4, mode="reflect"), w)
+        yy.backward(_nchw(dy, Co, ops))
+        gref = x.grad + (_nchw(add, Ci, ops) if with_add else 0)
+        _close(_nchw(g1, Ci, ops), gref, tol=CONV_TOL["bf16x6"], what=name + " g")
+        yt = _nchw(y_in, Ci, ops).requires_grad_(True)
+        a = F.instance_norm(yt, eps=1e-5)
+        a = F.relu(a) if act == "relu" else a
+        a.backward(_nchw(g1, Ci, ops))
+        _close(_nchw(dx1, Ci, ops), yt.grad, tol=1e-4, what=name + " IN bwd")
+    finally:
+        ops.set_conv_math(prev)

@@ -1,6 +1,7 @@
 """Developer: launch one conv family on the ResnetBlock shape (B=4, 64x64x256, 3x3 reflect) a few
-times (batch KB_B, default 8) — the target of rocprofv3 --pmc passes.  usage: kbench.py fprop|dgrad|tconv|wgrad|warp [reps]
-warp: vst_warp_fwd on bench.py's warp_roofline shape (N=32, C=64, 436x1024, random flow)."""
+times (batch KB_B, default 8) — the target of rocprofv3 --pmc passes.  usage: kbench.py fprop|dgrad|tconv|wgrad|warp|c0 [reps]
+warp: vst_warp_fwd on bench.py's warp_roofline shape (N=32, C=64, 436x1024, its smooth flow; KB_FLOW=iid:
+the i.i.d. worst case).  c0: the generator's first conv (conv_c4_direct_k) at N=KB_B, 256x256."""
 import os
 import sys
 
@@ -15,13 +16,29 @@ which = sys.argv[1]
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
 dev = torch.device("cuda")
 if which == "warp":
+    import torch.nn.functional as F
     N, C, H, W = 32, 64, 436, 1024
     xw = torch.randn(N, H, W, C, device=dev)
-    flow = torch.randn(N, 2, H, W, device=dev) * 3.0
+    if os.environ.get("KB_FLOW", "smooth") == "iid":
+        flow = torch.randn(N, 2, H, W, device=dev) * 3.0
+    else:  # bench.py warp_roofline's SURVEY 8d smooth flow (bicubic 9x9 N(0, 4^2) grid, x4)
+        g = torch.Generator(device="cpu").manual_seed(4321)
+        coarse = torch.randn(N, 2, 9, 9, generator=g) * 4.0
+        flow = (F.interpolate(coarse, size=(H, W), mode="bicubic", align_corners=True) * 4.0).to(dev).contiguous()
     out = torch.empty_like(xw)
     for _ in range(reps):
         ops.lib().vst_warp_fwd(xw.data_ptr(), flow.data_ptr(), out.data_ptr(), N, H, W, C, 0,
                                torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    sys.exit(0)
+if which == "c0":  # the generator's first conv (4-channel image -> 64, 7x7 reflect 3) with IN partials
+    B = int(os.environ.get("KB_B", "8"))
+    x4 = torch.rand(B, 256, 256, 4, device=dev) * 2 - 1
+    x4[..., 3] = 0
+    k0 = ops.weight_pack(torch.randn(64, 3, 7, 7, device=dev) * 0.05, ops.PACK_FWD)
+    b0 = torch.zeros(64, device=dev)
+    for _ in range(reps):
+        ops.conv2d_fwd_in(x4, k0, b0, 64, 7, 7, 1, 3, "reflect")
     torch.cuda.synchronize()
     sys.exit(0)
 B, H, C = int(os.environ.get("KB_B", "8")), 64, 256  # 8 = the batched G_A calls of the train step

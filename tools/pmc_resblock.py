@@ -16,12 +16,12 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-OPS = {"fprop": ("conv_fprop_bf_k",), "dgrad": ("conv_fprop_bf_k", "fprop_splitk_reduce_k"),
+OPS = {"fprop": ("conv_fprop_bf_k",), "dgrad": ("conv_fprop_bf_k", "fprop_splitk_reduce_k", "dgrad_border_add_k"),
        "wgrad": ("nhwc_to_cp", "conv_wgrad_bf_k", "wgrad_reduce_store_k", "slab_group_sum_k"),
-       "warp": ("warp_fwd_k",)}
+       "warp": ("warp_fwd_k",), "c0": ("conv_c4_direct_k", "in_finalize_k")}
 # the op's main GEMM dispatch (SQ metrics and its timing; the dgrad's 64x64 tail launch is excluded)
 MAIN = {"fprop": "3>, true, 1, false>", "dgrad": "3>, true, 0, false>", "wgrad": "conv_wgrad_bf_k",
-        "warp": "warp_fwd_k"}
+        "warp": "warp_fwd_k", "c0": "conv_c4_direct_k"}
 WARP_BYTES = 32 * 436 * 1024 * (8.0 * 64 + 8.0)  # bench.py warp_roofline: N*H*W*(4C gather + 8 flow + 4C write)
 
 
@@ -58,9 +58,14 @@ def main():
         if not fetch or not write:
             continue
         fb, wb = 2 * sum(fetch) * 1024 / reps, sum(write) * 1024 / reps
-        alg = WARP_BYTES if op == "warp" else 4.0 * B * 64 * 64 * 256 * 2 + 256 * 2304 * 3 * 2
+        if op == "warp":
+            alg = WARP_BYTES
+        elif op == "c0":  # the 4-channel image read once + the 64-channel output written once + weight planes
+            alg = 4.0 * B * 256 * 256 * (4 + 64) + 64 * 196 * 3 * 2
+        else:
+            alg = 4.0 * B * 64 * 64 * 256 * 2 + 256 * 2304 * 3 * 2
         t = kernel_times(os.path.join(d, op + "_kt"), MAIN[op])
-        name = "warp" if op == "warp" else "resblock_" + op
+        name = op if op in ("warp", "c0") else "resblock_" + op
         key = {"N": 32, "C": 64, "H": 436, "W": 1024} if op == "warp" else {"math": "bf16x6", "N": B}
         if op != "warp":  # the MFMA instruction of this build (bench.py matches records on it)
             import gbvst
@@ -71,10 +76,12 @@ def main():
             import gbvst
             from gbvst import ops
             gbvst._lib.load()
-            pad = 1 if op == "fprop" else 2
-            kind, ms = ops.conv_plan_fwd(B, 64, 64, 256, 256, 3, 3, 1, pad, pad, "bf16x6")
-            ks = ops.conv_plan_fwd_tail(B, 64, 64, 256, 256, 3, 3, 1, pad, "bf16x6") if (ms and ops.FWD_SPLITK) else 0
+            # the reflect-pad-1 data gradient: the interior as the zero-pad-1 conv (+ the border GEMM)
+            kind, ms = ops.conv_plan_fwd(B, 64, 64, 256, 256, 3, 3, 1, 1, 1, "bf16x6")
+            ks = ops.conv_plan_fwd_tail(B, 64, 64, 256, 256, 3, 3, 1, 1, "bf16x6") if (ms and ops.FWD_SPLITK) else 0
             key.update(tile=kind, m_split=ms, ksplit=ks)
+            if op == "dgrad":
+                key["op"] = "dgrad_refl"  # bench.py's dgrad key
         res[name] = {"key": key, "dispatches_per_call": len(fetch) / reps, "fetch_bytes": fb, "write_bytes": wb,
                      "hbm_bytes_per_launch": fb + wb, "algorithmic_bytes": alg,
                      "main_kernel_avg_us": round(sum(t) / len(t), 2) if t else None,

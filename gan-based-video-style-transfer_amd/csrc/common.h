@@ -117,7 +117,8 @@ long rk_cp_ld(long P);
 int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* bias, float* y, int N,
                     int H, int W, int C, int Ho, int Wo, int Cop, int R, int S, int st, int padh, int padw,
                     int reflect, int act, float slope, int math, int kind, hipStream_t s,
-                    double* part = nullptr, float* tws = nullptr, size_t tws_floats = 0, const float* addend = nullptr);
+                    double* part = nullptr, float* tws = nullptr, size_t tws_floats = 0, const float* addend = nullptr,
+                    int oph = 0);
 // direct patch-staged 4-channel-input convs (conv_c4.hip)
 bool c4_direct_ok(int C, int Cop, int R, int S, int st, int Ho, int Wo, int math);
 int c4_direct_launch(const float* x, const void* wsplit, long wps, const float* bias, float* y, int N, int H, int W,

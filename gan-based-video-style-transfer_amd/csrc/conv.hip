@@ -967,6 +967,26 @@ extern "C" int vst_conv2d_fwd_hw(const float* x, const float* wp, const void* ws
                        slope, math, (hipStream_t)stream);
 }
 
+// One phase (a, b) of a stride-2 ConvTranspose2d(k3, p1, op1) stored straight into the interleaved
+// 2H x 2W output y (the phase conv of conv2d_fwd_hw(x, wp, R = 1 + a, S = 1 + b, pad a / b), whose pixel
+// (ph, pw) is y's (2(ph-a)+a, 2(pw-b)+b)): the four phases replace four phase images + the
+// vst_interleave_phases pass.  Split-bf16 arithmetic only (VST_EUNSUPPORTED otherwise: use the
+// phase images + interleave).
+extern "C" int vst_conv2d_fwd_phase(const float* x, const void* wsplit, const float* bias, float* y, int N, int H,
+                                    int W, int Cx, int Cop, int a, int b, int act, float slope, int math,
+                                    void* stream) {
+  VST_REQUIRE(x && wsplit && y && (a == 0 || a == 1) && (b == 0 || b == 1), "conv2d_fwd_phase: bad args");
+  VST_REQUIRE(N > 0 && H > 0 && W > 0 && Cx % 8 == 0 && Cop % 4 == 0 && Cop != 4, "conv2d_fwd_phase: bad shape");
+  if (math == VST_MATH_F32) {
+    ::vst::set_error("conv2d_fwd_phase: split-bf16 arithmetic only");
+    return VST_EUNSUPPORTED;
+  }
+  const int R = 1 + a, S = 1 + b;
+  return bf_fprop_launch(x, wsplit, (long)Cop * R * S * Cx, bias, y, N, H, W, Cx, H + a, W + b, Cop, R, S, 1, a, b, 0,
+                         act, slope, math, g_tile_override[0], (hipStream_t)stream, nullptr, nullptr, 0, nullptr,
+                         1 + 2 * a + b);
+}
+
 extern "C" int vst_conv2d_tfwd(const float* in, const float* wp, const float* bias,
                                const float* addend, float* out, int N, int Hi, int Wi, int Cy,
                                int Ho, int Wo, int Cx, int R, int S, int stride, int pad,

@@ -588,6 +588,19 @@ __global__ __launch_bounds__(256) void dgrad_border_add_k(const float* __restric
   *d = o;
 }
 
+// ------------------------------------------------------------------------ ConvTranspose phases
+// Stride-2 ConvTranspose2d(k3, p1, op1) as four phase convs (vst_interleave_phases): phase (a, b) =
+// oph - 1 = 2a + b is an (H+a) x (W+b) conv whose pixel (ph, pw) is output pixel (2(ph-a)+a,
+// 2(pw-b)+b) of the 2H x 2W result, its first row (a = 1) / column (b = 1) unused.  With oph > 0 the
+// forward kernel stores each row there directly: -1 = the unused row / column (not stored).
+__device__ __forceinline__ int phase_row(int mm, int oph, int Ho, int Wo) {
+  const int a = (oph - 1) >> 1, b = (oph - 1) & 1;
+  const int hw = Ho * Wo, n = mm / hw, rem = mm - n * hw, ph = rem / Wo, pw = rem - ph * Wo;
+  if ((a && ph == 0) || (b && pw == 0)) return -1;
+  const int H = Ho - a, W = Wo - b;
+  return (n * 2 * H + 2 * (ph - a) + a) * 2 * W + 2 * (pw - b) + b;
+}
+
 // ------------------------------------------------------------------------------------------ fprop
 // Target of every masked A gather (zero-padding taps, the K tail): loads from it return zeros, so
 // the stage writer needs no per-row select.  Never written.
@@ -619,7 +632,7 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_k(
     const float* __restrict__ x, const __bf16* __restrict__ ws, long wps, const float* __restrict__ bias,
     float* __restrict__ y, int H, int W, int C, int Ho, int Wo, int Cop, int S, int st, int padh,
     int padw, int reflect, int act, float slope, int M, int Ktot, int m_base, double* __restrict__ part,
-    int spk = 0, float* __restrict__ slab = nullptr, const float* __restrict__ addend = nullptr) {
+    int spk = 0, float* __restrict__ slab = nullptr, const float* __restrict__ addend = nullptr, int oph = 0) {
   static_assert(!SPLIT || KSL, "split-K needs the channel-slice-major K walk");
   static_assert(REFL != 4 || (SPLIT && KSL), "border rows run as split-K slabs");
   __shared__ __attribute__((aligned(16))) char smem[2 * T::STAGE];
@@ -819,7 +832,7 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_k(
     // (an addend — the residual gradient of a data gradient — is always added on this path: its float4
     // loads ride with the row stores instead of 4-byte reads per accumulator element)
     constexpr bool LFIT = T::BM * (T::BN + 16) * 4 <= 2 * T::STAGE;
-    const bool LEPI = LFIT && (VST_BF_LDS_EPI || addend != nullptr);
+    const bool LEPI = LFIT && (VST_BF_LDS_EPI || addend != nullptr || oph != 0);
     constexpr int LDE = T::BN + 16;
     float* ept = reinterpret_cast<float*>(smem);
     if (LEPI) __syncthreads();  // every wave is done reading the last stage
@@ -840,8 +853,8 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_k(
             const float v = apply_act(acc[2 * g + h][j][r] + bv, act, slope) + ad;
             if (LEPI)
               ept[(mm - m0) * LDE + (n - n0)] = v;
-            else if (nok && mm < M)
-              y[(long)mm * Cop + n] = v;
+            else if (nok && mm < M && (!oph || phase_row(mm, oph, Ho, Wo) >= 0))
+              y[(long)(oph ? phase_row(mm, oph, Ho, Wo) : mm) * Cop + n] = v;
             s1 += v;
             s2 += (double)v * v;
           }
@@ -866,10 +879,11 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_k(
       for (int idx = t; idx < T::BM * C4; idx += T::NT) {
         const int row = idx / C4, c = 4 * (idx - row * C4);
         const int mm = m0 + row, n = n0 + c;
-        if (mm < M && n < Cop) {
+        const int orow = oph ? phase_row(mm, oph, Ho, Wo) : mm;
+        if (mm < M && n < Cop && orow >= 0) {
           float4 v = *reinterpret_cast<const float4*>(ept + row * LDE + c);
           if (addend) add_f4(v, *reinterpret_cast<const float4*>(addend + (long)mm * Cop + n));
-          *reinterpret_cast<float4*>(y + (long)mm * Cop + n) = v;
+          *reinterpret_cast<float4*>(y + (long)orow * Cop + n) = v;
         }
       }
     }
@@ -907,7 +921,8 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_k(
         const int mm = m0 + wm0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
         const float ad = (addend && nok && mm < M) ? addend[(long)mm * Cop + n] : 0.f;
         const float v = apply_act(acc[i][j][r] + bv, act, slope) + ad;
-        if (nok && mm < M) y[(long)mm * Cop + n] = v;
+        if (nok && mm < M && (!oph || phase_row(mm, oph, Ho, Wo) >= 0))
+          y[(long)(oph ? phase_row(mm, oph, Ho, Wo) : mm) * Cop + n] = v;
         s1 += v;
         s2 += (double)v * v;
       }
@@ -1404,10 +1419,11 @@ size_t bf_fprop_ws_floats(long M, int Cop, int C, int R, int S, int math) {
 int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* bias, float* y, int N,
                     int H, int W, int C, int Ho, int Wo, int Cop, int R, int S, int st, int padh, int padw,
                     int reflect, int act, float slope, int math, int kind, hipStream_t s, double* part,
-                    float* tws, size_t tws_floats, const float* addend) {
+                    float* tws, size_t tws_floats, const float* addend, int oph) {
+  if (oph) tws = nullptr;  // phase stores: no split-K slabs (their reduce stores unmapped)
   const int M = N * Ho * Wo, K = R * S * C;
   // 4-channel inputs with 64 outputs (the generator's 7x7 image convs): the direct patch-staged kernel
-  if (kind < 0 && padh == padw && !addend && c4_direct_ok(C, Cop, R, S, st, Ho, Wo, math))
+  if (kind < 0 && padh == padw && !addend && !oph && c4_direct_ok(C, Cop, R, S, st, Ho, Wo, math))
     return c4_direct_launch(x, wsplit, wps, bias, y, N, H, W, Ho, Wo, R, S, padh, reflect, act, slope, math, part, s);
   const __bf16* ws = reinterpret_cast<const __bf16*>(wsplit);
   int kd, m_split, tail_kind;
@@ -1428,19 +1444,19 @@ int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* b
     if (C == 4)                                                                                     \
       hipLaunchKernelGGL((bf::conv_fprop_bf_k<T, false, 3>), grid, dim3(T::NT), 0, s, x, ws, wps, bias, y, \
                          H, W, C, Ho, Wo, Cop, S, st, padh, padw, reflect, act, slope, Mend, K, mb, part, 0,      \
-                         nullptr, addend);                                                          \
+                         nullptr, addend, oph);                                                          \
     else if (VST_BF_KSLICE && C % BK_ == 0 && reflect)                                              \
       hipLaunchKernelGGL((bf::conv_fprop_bf_k<T, true, 1>), grid, dim3(T::NT), 0, s, x, ws, wps, bias, y, \
                          H, W, C, Ho, Wo, Cop, S, st, padh, padw, reflect, act, slope, Mend, K, mb, part, 0,      \
-                         nullptr, addend);                                                          \
+                         nullptr, addend, oph);                                                          \
     else if (VST_BF_KSLICE && C % BK_ == 0)                                                         \
       hipLaunchKernelGGL((bf::conv_fprop_bf_k<T, true, 0>), grid, dim3(T::NT), 0, s, x, ws, wps, bias, y, \
                          H, W, C, Ho, Wo, Cop, S, st, padh, padw, reflect, act, slope, Mend, K, mb, part, 0,      \
-                         nullptr, addend);                                                          \
+                         nullptr, addend, oph);                                                          \
     else                                                                                            \
       hipLaunchKernelGGL((bf::conv_fprop_bf_k<T, false, 2>), grid, dim3(T::NT), 0, s, x, ws, wps, bias, y, \
                          H, W, C, Ho, Wo, Cop, S, st, padh, padw, reflect, act, slope, Mend, K, mb, part, 0,      \
-                         nullptr, addend);                                                          \
+                         nullptr, addend, oph);                                                          \
   }
   for (int ph = (ks && !m_first) ? 1 : 0; ph < ((m_split || (ks && !m_first)) ? 2 : 1); ++ph) {
     const int mb = ph ? m_split : 0, Mend = (m_split && !ph) ? m_split : M;

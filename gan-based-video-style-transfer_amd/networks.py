@@ -162,6 +162,9 @@ C8_EDGES = os.environ.get("VST_C8_EDGES", "1") != "0"
 # data gradient of the last conv (a forward conv over its 4-channel output gradient).  VST_C4_FWD=0
 # runs both on 8-channel copies.
 C4_FWD = os.environ.get("VST_C4_FWD", "1") != "0" and os.environ.get("VST_BF_C4", "1") != "0"
+# ... and the first conv's weight gradient reads the 4-channel image too (the split-bf16 wgrad takes any
+# channel count: K rows 49*4 instead of 49*8, and no 8-channel copy at all); VST_C4_WGRAD=0 keeps the copy.
+C4_WGRAD = C4_FWD and os.environ.get("VST_C4_WGRAD", "1") != "0"
 
 
 def _pad_channels(x, cs):
@@ -510,7 +513,7 @@ class _GeneratorFn(torch.autograd.Function):
 
         if C8_EDGES and x.shape[-1] == 4 and (C4_FWD or "c08" in P):
             # the 8-channel copy feeds the forward only without C4_FWD, else just c0's weight gradient
-            x8 = _pad_channels(x, 8) if (train_w or not C4_FWD) else None
+            x8 = _pad_channels(x, 8) if ((train_w and not C4_WGRAD) or not C4_FWD) else None
             _, _, b = P["c0"]
             if C4_FWD:
                 y, s = ops.conv2d_fwd_in(x, P["c0"][0], b, cpad(ngf), 7, 7, 1, 3, "reflect", role=role)

@@ -1134,10 +1134,24 @@ def conv4s2_dgrad(dy, packs, cop, role="bwd"):
     return y
 
 
+# ConvTranspose2d phase convs storing straight into the interleaved output (vst_conv2d_fwd_phase)
+# instead of four phase images + vst_interleave_phases; VST_CONVT_DIRECT=0 keeps the latter.
+CONVT_DIRECT = os.environ.get("VST_CONVT_DIRECT", "1") != "0"
+
+
 def convT3s2_fwd(x, packs, bias, cop, act="none", role="fwd"):
-    """ConvTranspose2d(k=3, s=2, p=1, op=1) forward on NHWC x via four phase convs + interleave."""
+    """ConvTranspose2d(k=3, s=2, p=1, op=1) forward on NHWC x via four phase convs, stored straight into
+    the interleaved output (split-bf16 math) or as phase images + interleave."""
     _dev_check(x, bias)
-    N, H, W, _ = x.shape
+    N, H, W, Cx = x.shape
+    m = _math(role)
+    if CONVT_DIRECT and m != _lib.MATH_MODES["fp32"] and Cx % 8 == 0 and cop != 4 and \
+            all(getattr(wp, "vst_split", None) is not None for wp in packs):
+        y = torch.empty((N, 2 * H, 2 * W, cop), device=x.device)
+        for (a, b), wp in zip(((0, 0), (0, 1), (1, 0), (1, 1)), packs):
+            _call("vst_conv2d_fwd_phase", _p(x), _p(wp.vst_split), _p(bias), _p(y), N, H, W, Cx, cop, a, b, ACT[act],
+                  0.0, m, _stream())
+        return y
     outs = []
     for (a, b), wp in zip(((0, 0), (0, 1), (1, 0), (1, 1)), packs):
         outs.append(conv2d_fwd_hw(x, wp, bias, cop, 1 + a, 1 + b, 1, a, b, act=act, role=role))

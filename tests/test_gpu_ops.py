@@ -358,16 +358,26 @@ def test_tap_conv_dgrad(ops, conv_math, ci, co, k, mode):
     assert float(dx[..., ci:].abs().max()) == 0.0
 
 
-@pytest.mark.parametrize("ci,co,h,w", [(128, 64, 9, 11), (256, 128, 8, 8), (64, 32, 5, 70)])
+@pytest.mark.parametrize("ci,co,h,w", [(128, 64, 9, 11), (256, 128, 8, 8), (64, 32, 5, 70),
+                                        (256, 128, 64, 64), (128, 64, 128, 128)])  # the generator's u0 / u1
 def test_convT_phases(ops, conv_math, ci, co, h, w):
-    """ConvTranspose2d(k3, s2, p1, op1) forward as four phase convs + interleave vs torch."""
+    """ConvTranspose2d(k3, s2, p1, op1) forward as four phase convs vs torch; the phases stored straight
+    into the interleaved output (vst_conv2d_fwd_phase, split-bf16 math) equal the phase images +
+    interleave route bit for bit (same GEMMs, other store addresses)."""
     x = _g(95, (2, ci, h, w))
     wt = _g(96, (ci, co, 3, 3), 0.05)
     b = _g(97, (co,), 0.1)
     ref = F.conv_transpose2d(x, wt, b, stride=2, padding=1, output_padding=1)
     packs = ops.convT3s2_phase_packs(wt.to(DEV))
-    y = ops.convT3s2_fwd(_nhwc(x, ops), packs, b.to(DEV), co)
+    xn = _nhwc(x, ops)
+    y = ops.convT3s2_fwd(xn, packs, b.to(DEV), co)
     _close(_nchw(y, co, ops), ref, tol=CONV_TOL[conv_math], what="convT phases")
+    prev, ops.CONVT_DIRECT = ops.CONVT_DIRECT, False
+    try:
+        y_il = ops.convT3s2_fwd(xn, packs, b.to(DEV), co)
+    finally:
+        ops.CONVT_DIRECT = prev
+    assert torch.equal(y, y_il)
 
 
 @pytest.mark.parametrize("forced", [False, True], ids=["planned", "t256x128"])

@@ -88,7 +88,7 @@ def DOMINANT_KEYS(B):
             "resblock_wgrad": ("wgrad", (N, 64, 64, 256, 256, 3, 1, 1, "reflect"))}
 
 
-PMC_FILE = os.path.join(HERE, "profiles", "r02b_conv_pmc.json")
+PMC_FILE = os.path.join(HERE, "profiles", "r03c_conv_pmc.json")
 
 
 def _pmc_traffic(name, key):
@@ -143,8 +143,9 @@ def conv_roofline(name, probe, math):
         kernel = ("vst_conv2d_dgrad_refl: conv_fprop_bf_k interior (zero pad 1, %s) + border rows as "
                   "split-K conv_fprop_bf_k<REFL=4> + dgrad_border_add_k [%s]" % (m, _mfma(m)))
         key = {"math": m, "N": N, "mfma": _mfma(m), "op": "dgrad_refl"}
-        note = ("stride-1 reflect data gradient: interior conv + border GEMM (no padded frame, no fold; the "
-                "border slabs are added by the IN-backward partial pass that follows)")
+        note = ("stride-1 reflect data gradient: interior conv + border GEMM (no padded frame, no fold); "
+                "dgrad_border_add_k adds the border slabs (VST_DGRAD_IN=1 moves that add into the "
+                "IN-backward partial pass)")
     else:
         kernel = ("vst_conv2d_wgrad: nhwc_to_cp_pad_k + nhwc_to_cp_planes_k copies + conv_wgrad_bf_k "
                   "(split-K slabs) + wgrad_reduce_store_k, %s" % m if m != "fp32" else
@@ -190,6 +191,7 @@ def warp_roofline(device, N=32, C=64, H=436, W=1024, reps=10):
     return {"kernel": "warp_fwd_k (N=%d, C=%d, %dx%d)" % (N, C, H, W), "bound": "hbm",
             "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
             "avg_launch_ms": round(ms, 4), "bytes_per_launch": nbytes,
+            "traffic": _pmc_traffic("warp", {"N": N, "C": C, "H": H, "W": W}),
             "flow": "SURVEY 8d smooth synthetic (bicubic 9x9 N(0,4^2) grid, x4)",
             "iid_flow_worst_case": {"flow": "i.i.d. N(0, 3^2) px per pixel", "achieved": round(gbs_iid, 1),
                                     "frac": round(gbs_iid / HBM_PEAK_GBS, 4), "avg_launch_ms": round(ms_iid, 4)}}

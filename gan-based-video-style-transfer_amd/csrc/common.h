@@ -70,6 +70,35 @@ __host__ __device__ __forceinline__ int dgrad_border_rows_of(int h, int w, int H
   return 0;
 }
 
+// The border slabs' layout (conv_bf.hip bf_dgrad_refl1_slabs): ks split-K slabs of Mb rows; Ll == 0:
+// the full-K border rows, Lt = NB rows per image (dgrad_border_pos); else the K-restricted segments
+// top [0, Lt), bottom [Lt, 2Lt) (image n, column k: q = (-1 | H, k-1)), left [2Lt, 2Lt+Ll), right
+// [2Lt+Ll, 2Lt+2Ll) (image n, row k: q = (k, -1 | W)).
+struct BorderSlabs {
+  int ks, Mb, Lt, Ll;
+};
+
+// The slab rows that add into pixel (h, w) of image n, in summation order (<= 3; 0: none)
+__host__ __device__ __forceinline__ int dgrad_border_slab_rows(int n, int h, int w, int H, int W, int Lt, int Ll,
+                                                               int* rows) {
+  if (Ll == 0) {
+    int b0;
+    const int nr = dgrad_border_rows_of(h, w, H, W, &b0);
+    for (int r = 0; r < nr; ++r) rows[r] = n * Lt + b0 + r;
+    return nr;
+  }
+  int nr = 0;
+  if (h == 1 || h == H - 2) {
+    const int base = (h == 1 ? 0 : Lt) + n * (W + 2);
+    rows[nr++] = base + w + 1;                  // q = (-1 | H, w)
+    if (w == 1) rows[nr++] = base;              // q = (-1 | H, -1)
+    if (w == W - 2) rows[nr++] = base + W + 1;  // q = (-1 | H, W)
+  }
+  if (w == 1) rows[nr++] = 2 * Lt + n * H + h;           // q = (h, -1)
+  if (w == W - 2) rows[nr++] = 2 * Lt + Ll + n * H + h;  // q = (h, W)
+  return nr;
+}
+
 __device__ __forceinline__ float apply_act(float v, int act, float slope) {
   if (act == VST_ACT_RELU) return v > 0.f ? v : 0.f;
   if (act == VST_ACT_LRELU) return v > 0.f ? v : v * slope;
@@ -128,10 +157,9 @@ int c4_direct_launch(const float* x, const void* wsplit, long wps, const float* 
 // caller takes them: add_border = false)
 bool bf_dgrad_refl1_ok(int N, int H, int W, int Cy, int Cx, int math);
 size_t bf_dgrad_refl1_ws_floats(int N, int H, int W, int Cy, int Cx, int math);
-size_t bf_dgrad_refl1_slabs(int N, int H, int W, int Cy, int Cx, int math, int* ks, int* nb);
+size_t bf_dgrad_refl1_slabs(int N, int H, int W, int Cy, int Cx, int math, BorderSlabs* b);
 int bf_dgrad_refl1_launch(const float* dy, const void* wsplit, long wps, const float* addend, float* dx, int N, int H,
-                          int W, int Cy, int Cx, int math, hipStream_t s, float* ws, size_t ws_floats, bool add_border,
-                          const float** slab_out, int* ks_out, int* nb_out);
+                          int W, int Cy, int Cx, int math, hipStream_t s, float* ws, size_t ws_floats, bool add_border);
 size_t bf_fprop_ws_floats(long M, int Cop, int C, int R, int S, int math);
 int bf_tail_ks(long M, int Cop, int m_split, int nk);
 void bf_split_plan(long M, int Cop, int C, int R, int S, int math, int kind, int* m_first, int* ks_out);

@@ -588,6 +588,65 @@ __global__ __launch_bounds__(256) void dgrad_border_add_k(const float* __restric
   *d = o;
 }
 
+// The K-restricted border GEMM (conv_fprop_bf_k REFL 5): the padded positions as four segments of
+// rows, each padded to a whole number of M-tiles:
+//   top    [0, Lt):            image n, k in [0, W+2): q = (-1, k-1)  (the two corners included)
+//   bottom [Lt, 2Lt):          q = (H, k-1)
+//   left   [2Lt, 2Lt+Ll):      image n, k in [0, H):   q = (k, -1)
+//   right  [2Lt+Ll, 2Lt+2Ll):  q = (k, W)
+// A top / bottom row reads only dy row 0 / H-1 (taps (2, s) / (0, s)), a left / right row only dy
+// column 0 / W-1 (taps (r, 2) / (r, 0)): K = 3 C instead of 9 C (the other six taps of a border
+// position gather zeros).  Lt = N (W+2), Ll = N H, each rounded up to the tile height bm.
+__host__ __device__ __forceinline__ int border5_seg_rows(int n_img, int len, int bm) {
+  return (n_img * len + bm - 1) / bm * bm;
+}
+
+// dx[n][th][tw][c] += the sum of the REFL-5 slab rows whose position mirrors onto (th, tw): the
+// targets are rows 1 / H-2 (all columns), then columns 1 / W-2 (rows not 1 / H-2), T = 2W + 2H per
+// image; a target sums its (1..3) rows in a fixed order (top / bottom rows by column, then the left
+// / right row), each row's splits in order.  grid (ceil(N*T / 16), ceil(C / 64)), thread = (target,
+// 4-channel group); every dx element has exactly one writer.
+__global__ __launch_bounds__(256) void dgrad_border5_add_k(const float* __restrict__ slab, int ks, int Mb, int C,
+                                                           float* __restrict__ dx, int N, int H, int W, int Lt,
+                                                           int Ll) {
+  const int t = threadIdx.x;
+  const int c = blockIdx.y * 64 + (t & 15) * 4;
+  const int T = 2 * W + 2 * H;
+  const int m = blockIdx.x * 16 + (t >> 4);
+  if (m >= N * T || c >= C) return;
+  const int n = m / T, b = m - n * T;
+  int th, tw;
+  if (b < 2 * W) {
+    th = b < W ? 1 : H - 2;
+    tw = b < W ? b : b - W;
+  } else {
+    const int b2 = b - 2 * W;
+    th = b2 < H ? b2 : b2 - H;
+    tw = b2 < H ? 1 : W - 2;
+    if (th == 1 || th == H - 2) return;  // a row target
+  }
+  int rows[3];
+  const int nr = dgrad_border_slab_rows(n, th, tw, H, W, Lt, Ll, rows);
+  const long zst = (long)Mb * C;
+  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int r = 0; r < nr; ++r) {
+    const float* base = slab + (long)rows[r] * C + c;
+    float4 u[16];
+#pragma unroll
+    for (int z = 0; z < 16; ++z)
+      if (z < ks) u[z] = *reinterpret_cast<const float4*>(base + z * zst);
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int z = 0; z < 16; ++z)
+      if (z < ks) add_f4(acc, u[z]);
+    add_f4(v, acc);
+  }
+  float4* d = reinterpret_cast<float4*>(dx + (((long)n * H + th) * W + tw) * C + c);
+  float4 o = *d;
+  add_f4(o, v);
+  *d = o;
+}
+
 // ------------------------------------------------------------------------ ConvTranspose phases
 // Stride-2 ConvTranspose2d(k3, p1, op1) as four phase convs (vst_interleave_phases): phase (a, b) =
 // oph - 1 = 2a + b is an (H+a) x (W+b) conv whose pixel (ph, pw) is output pixel (2(ph-a)+a,
@@ -634,7 +693,7 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_k(
     int padw, int reflect, int act, float slope, int M, int Ktot, int m_base, double* __restrict__ part,
     int spk = 0, float* __restrict__ slab = nullptr, const float* __restrict__ addend = nullptr, int oph = 0) {
   static_assert(!SPLIT || KSL, "split-K needs the channel-slice-major K walk");
-  static_assert(REFL != 4 || (SPLIT && KSL), "border rows run as split-K slabs");
+  static_assert(REFL < 4 || (SPLIT && KSL), "border rows run as split-K slabs");
   __shared__ __attribute__((aligned(16))) char smem[2 * T::STAGE];
   constexpr int A_LD = T::A_LD, B_LD = T::B_LD, RPP = T::RPP, NP = T::NP;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -649,11 +708,25 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_k(
   // A rows (output pixels m0 + rb + RPP*j): tap-independent geometry.  Rows past M gather row 0's
   // pixels instead: their outputs are never stored, so no mask is needed for them.
   constexpr bool C4 = REFL == 3;
+  // REFL 5 (dgrad_border5 rows: segment `seg` of the block; Ho / Wo = the padded top-bottom / left-right
+  // segment lengths, st = images): K = the 3 taps that reach the frame, Sx of them per tap row
+  const int seg = REFL != 5 ? 0 : (m0 < Ho ? 0 : (m0 < 2 * Ho ? 1 : (m0 < 2 * Ho + Wo ? 2 : 3)));
+  const int Sx = REFL != 5 ? S : (seg < 2 ? 3 : 1);
   int hb[A_LD], wb[A_LD], pb[A_LD], aoff[A_LD], aoff2[C4 ? A_LD : 1];
 #pragma unroll
   for (int j = 0; j < A_LD; ++j) {
     const int m = m0 + rb + RPP * j;
     const int mm = m < M ? m : 0;
+    if constexpr (REFL == 5) {
+      const int L = seg < 2 ? W + 2 : H;
+      const int r = mm - (seg == 0 ? 0 : (seg == 1 ? Ho : (seg == 2 ? 2 * Ho : 2 * Ho + Wo)));
+      const int n = r / L, k = r - n * L;
+      const bool live = (unsigned)r < (unsigned)(st * L);  // the segment's padding rows gather zeros
+      hb[j] = !live ? -1000000 : (seg == 0 ? 0 : (seg == 1 ? H - 1 : k - 1));
+      wb[j] = seg < 2 ? k - 2 : (seg == 2 ? 0 : W - 1);
+      pb[j] = live ? n * H * W * C : 0;
+      continue;
+    }
     if constexpr (REFL == 4) {
       // border rows of a reflect-pad-1 data gradient (dgrad_border_pos): Wo = rows per image
       const int n = mm / Wo;
@@ -700,7 +773,7 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_k(
 #pragma unroll
   for (int j = 0; j < B_LD; ++j) {
     const int n = n0 + rb + RPP * j;
-    wrow[j] = ws + (long)(n < Cop ? n : Cop - 1) * Ktot;
+    wrow[j] = ws + (long)(n < Cop ? n : Cop - 1) * (REFL == 5 ? 3 * Ktot : Ktot);
   }
 
   // K cursor.  KSL: block-uniform (tap r, tap s, slice base) + this thread's chunk 8*kq.
@@ -708,15 +781,15 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_k(
   const int kq8 = 8 * kq;
   int tr = 0, ts = 0, ksb = 0;                 // KSL
   int kcur = kq8, kc = kq8 % C, kr = 0, ks = 0;  // tap-major
-  const int Rk = KSL ? Ktot / (S * C) : 0;
+  const int Rk = KSL ? Ktot / (Sx * C) : 0;
   const int nk_all = (Ktot + T::BK - 1) / T::BK;
   int k0 = 0, nk = nk_all;
   if (SPLIT) {  // K-steps [k0, k0 + nk): slice k0 / (R S), tap k0 % (R S)
     k0 = zs * spk;
     nk = min(spk, nk_all - k0);
-    const int taps = Rk * S, tap = k0 % taps;
-    tr = tap / S;
-    ts = tap - tr * S;
+    const int taps = Rk * Sx, tap = k0 % taps;
+    tr = tap / Sx;
+    ts = tap - tr * Sx;
     ksb = (k0 / taps) * T::BK;
   }
   if (KSL) {
@@ -733,7 +806,9 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_k(
   auto load_all = [&](int set) __attribute__((always_inline)) {
     const bool kin = KSL || kcur < Ktot;  // the K tail reads zeros (A) against row 0 (B)
     const int ka = KSL ? ksb + kq8 : kc;
-    const int kb = KSL ? (tr * S + ts) * C + ksb + kq8 : (kin ? kcur : 0);
+    // REFL 5: tap (2, ts) top, (0, ts) bottom, (tr, 2) left, (tr, 0) right of the 3x3 weight rows
+    const int tap5 = seg == 0 ? 6 + ts : (seg == 1 ? ts : 3 * tr + (seg == 2 ? 2 : 0));
+    const int kb = KSL ? (REFL == 5 ? tap5 : tr * S + ts) * C + ksb + kq8 : (kin ? kcur : 0);
     if constexpr (C4) {
       // chunk = taps kcur/4 and kcur/4 + 1; the second is missing when kcur + 4 == Ktot.  Weight rows
       // are 4*R*S bf16 long (8-byte aligned for odd R*S): two 8-byte loads per plane.
@@ -783,7 +858,7 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_k(
   auto adv = [&](bool go) __attribute__((always_inline)) {
     if (KSL) {
       const int ts1 = ts + 1;
-      const bool w1 = ts1 == S;
+      const bool w1 = ts1 == Sx;
       const int tr1 = tr + (w1 ? 1 : 0);
       const bool w2 = w1 && tr1 == Rk;
       ts = go ? (w1 ? 0 : ts1) : ts;
@@ -1504,34 +1579,65 @@ static void bf_border_plan(int N, int H, int W, int Cy, int Cx, int math, int* k
   *mb_out = Mb;
 }
 
+// The K-restricted border GEMM (REFL 5, 128x128 tiles): segment lengths and K-split count.  ks: at
+// least 4 K-steps per split and at most one CU round (VST_BORDER_KS overrides; VST_BORDER5=0 keeps the
+// full-K border rows of bf_border_plan).
+static const bool g_border5 = [] {
+  const char* e = getenv("VST_BORDER5");
+  return !(e && e[0] == '0');
+}();
+static const int g_border_ks = [] {
+  const char* e = getenv("VST_BORDER_KS");
+  return e ? atoi(e) : 0;
+}();
+static void bf_border5_plan(int N, int H, int W, int Cy, int Cx, int* ks_out, int* lt, int* ll) {
+  *lt = bf::border5_seg_rows(N, W + 2, 128);
+  *ll = bf::border5_seg_rows(N, H, 128);
+  const long tiles = (long)(2 * *lt + 2 * *ll) / 128 * ((Cx + 127) / 128);
+  const int nk = (3 * Cy + 31) / 32;
+  int ks = g_border_ks > 0 ? g_border_ks : (int)(VST_NUM_CUS / (tiles > 0 ? tiles : 1));
+  if (g_border_ks <= 0 && ks > nk / 4) ks = nk / 4;
+  ks = ks < 1 ? 1 : (ks > 16 ? 16 : ks);
+  while (ks > 1 && (ks - 1) * ((nk + ks - 1) / ks) >= nk) --ks;  // no empty split
+  *ks_out = ks;
+}
+
 bool bf_dgrad_refl1_ok(int N, int H, int W, int Cy, int Cx, int math) {
   return math != VST_MATH_F32 && VST_BF_KSLICE && Cy % 32 == 0 && Cx % 4 == 0 && H >= 4 && W >= 4 && N > 0;
 }
 
 // where the border GEMM's slabs sit in the dgrad workspace (floats) and their split count / rows per image
-size_t bf_dgrad_refl1_slabs(int N, int H, int W, int Cy, int Cx, int math, int* ks, int* nb) {
-  long Mb;
-  bf_border_plan(N, H, W, Cy, Cx, math, ks, &Mb);
-  *nb = bf::dgrad_border_rows(H, W);
+size_t bf_dgrad_refl1_slabs(int N, int H, int W, int Cy, int Cx, int math, BorderSlabs* b) {
+  if (g_border5) {
+    bf_border5_plan(N, H, W, Cy, Cx, &b->ks, &b->Lt, &b->Ll);
+    b->Mb = 2 * b->Lt + 2 * b->Ll;
+  } else {
+    long Mb;
+    bf_border_plan(N, H, W, Cy, Cx, math, &b->ks, &Mb);
+    b->Mb = (int)Mb;
+    b->Lt = bf::dgrad_border_rows(H, W);
+    b->Ll = 0;
+  }
   return bf_fprop_ws_floats((long)N * H * W, Cx, Cy, 3, 3, math);
 }
 
 size_t bf_dgrad_refl1_ws_floats(int N, int H, int W, int Cy, int Cx, int math) {
-  int ks;
+  int ks, ks5, lt, ll;
   long Mb;
   bf_border_plan(N, H, W, Cy, Cx, math, &ks, &Mb);
-  return bf_fprop_ws_floats((long)N * H * W, Cx, Cy, 3, 3, math) + (size_t)ks * Mb * Cx;
+  bf_border5_plan(N, H, W, Cy, Cx, &ks5, &lt, &ll);
+  const size_t b4 = (size_t)ks * Mb * Cx, b5 = g_border5 ? (size_t)ks5 * (2 * lt + 2 * ll) * Cx : 0;
+  return bf_fprop_ws_floats((long)N * H * W, Cx, Cy, 3, 3, math) + (b4 > b5 ? b4 : b5);
 }
 
 // dx = data gradient of ReflectionPad2d(1) + 3x3 conv (stride 1) from dy (+ addend), wsplit = the
 // VST_PACK_IKF planes of the conv weight: the interior as the zero-pad-1 forward conv (addend in its
-// epilogue), then the border GEMM (split-K slabs) and dgrad_border_add_k.  Replaces the conv over the
-// (H+2) x (W+2) zero-padded frame + reflect fold.  add_border = false: the slabs are left for the
-// caller (vst_conv2d_dgrad_refl_in adds them in its InstanceNorm-backward partial pass); *slab_out,
-// *ks_out, *nb_out describe them.
+// epilogue), then the border GEMM (split-K slabs) and dgrad_border_add_k (add_border with VST_BORDER5
+// on: the K-restricted border GEMM and dgrad_border5_add_k).  Replaces the conv over the
+// (H+2) x (W+2) zero-padded frame + reflect fold.  add_border = false: the slabs (bf_dgrad_refl1_slabs)
+// are left for the caller (vst_conv2d_dgrad_refl_in adds them in its InstanceNorm-backward partial pass).
 int bf_dgrad_refl1_launch(const float* dy, const void* wsplit, long wps, const float* addend, float* dx, int N, int H,
-                          int W, int Cy, int Cx, int math, hipStream_t s, float* ws, size_t ws_floats, bool add_border,
-                          const float** slab_out, int* ks_out, int* nb_out) {
+                          int W, int Cy, int Cx, int math, hipStream_t s, float* ws, size_t ws_floats, bool add_border) {
   int ks;
   long Mb;
   bf_border_plan(N, H, W, Cy, Cx, math, &ks, &Mb);
@@ -1542,6 +1648,23 @@ int bf_dgrad_refl1_launch(const float* dy, const void* wsplit, long wps, const f
     return e;
   float* slab = ws + main_ws;
   const __bf16* wb = reinterpret_cast<const __bf16*>(wsplit);
+  if (g_border5) {
+    int ks5, lt, ll;
+    bf_border5_plan(N, H, W, Cy, Cx, &ks5, &lt, &ll);
+    const int Mt = 2 * lt + 2 * ll, K = 3 * Cy;
+    VST_REQUIRE(ws_floats >= main_ws + (size_t)ks5 * Mt * Cx, "dgrad_refl: workspace too small");
+#define VST_B5(NP_)                                                                                            {                                                                                                             using T = bf::Tile<128, 128, 64, 32, 32, NP_>;                                                              const int nk = (K + T::BK - 1) / T::BK, spk = (nk + ks5 - 1) / ks5;                                         const dim3 grid(Mt / 128 * ceil_div(Cx, 128) * ks5);                                                        hipLaunchKernelGGL((bf::conv_fprop_bf_k<T, true, 5, true>), grid, dim3(T::NT), 0, s, dy, wb, wps, nullptr,                          dx, H, W, Cy, lt, ll, Cx, 3, N, 1, 1, 0, VST_ACT_NONE, 0.f, Mt, K, 0, nullptr, spk,                           slab, nullptr);                                                                        }
+    if (math == VST_MATH_BF16X6)
+      VST_B5(3)
+    else
+      VST_B5(2)
+#undef VST_B5
+    const int T = 2 * W + 2 * H;
+    if (add_border)
+      hipLaunchKernelGGL(bf::dgrad_border5_add_k, dim3(ceil_div((long)N * T, 16), ceil_div(Cx, 64)), dim3(256), 0, s,
+                       slab, ks5, Mt, Cx, dx, N, H, W, lt, ll);
+    return check_launch("conv2d_dgrad_refl");
+  }
   const int NB = bf::dgrad_border_rows(H, W), K = 9 * Cy;
   if (math == VST_MATH_BF16X6) {
     using T = bf::Tile<256, 128, 64, 64, 32, 3>;
@@ -1556,9 +1679,6 @@ int bf_dgrad_refl1_launch(const float* dy, const void* wsplit, long wps, const f
     hipLaunchKernelGGL((bf::conv_fprop_bf_k<T, true, 4, true>), grid, dim3(T::NT), 0, s, dy, wb, wps, nullptr, dx, H,
                        W, Cy, H, NB, Cx, 3, 1, 1, 1, 0, VST_ACT_NONE, 0.f, (int)Mb, K, 0, nullptr, spk, slab, nullptr);
   }
-  if (slab_out) *slab_out = slab;
-  if (ks_out) *ks_out = ks;
-  if (nb_out) *nb_out = NB;
   if (add_border)
     hipLaunchKernelGGL(bf::dgrad_border_add_k, dim3(ceil_div(Mb, 16), ceil_div(Cx, 64)), dim3(256), 0, s, slab, ks,
                        (int)Mb, Cx, dx, H, W, NB);
@@ -1646,5 +1766,5 @@ extern "C" int vst_conv2d_dgrad_refl(const float* dy, const void* wsplit, const 
     return VST_EUNSUPPORTED;
   }
   return bf_dgrad_refl1_launch(dy, wsplit, (long)Cx * 9 * Cy, addend, dx, N, H, W, Cy, Cx, math, (hipStream_t)stream,
-                               ws, ws_bytes / sizeof(float), true, nullptr, nullptr, nullptr);
+                               ws, ws_bytes / sizeof(float), true);
 }

@@ -239,14 +239,15 @@ __global__ __launch_bounds__(NRED) void fold_in_partial_k(const float* __restric
 }
 
 // The border add of a ReflectionPad2d(1) + 3x3 data gradient (conv_bf.hip: the interior conv left g
-// without the padded border positions, whose GEMM left ks split-K slabs [ks][N*NB][C]) fused with the
+// without the padded border positions, whose GEMM left ks split-K slabs [ks][Mb][C], BorderSlabs) fused with the
 // backward partials of the InstanceNorm(+act) below it: the pixels a padded position mirrors onto
 // (rows / columns 1 and H-2 / W-2: ~6 % at 64 x 64) get the slab sums added (split order, then row
 // order: dgrad_border_add_k's arithmetic) and written back; every pixel's g is then reduced while in
 // registers.  Replaces dgrad_border_add_k + in_partial_k<1>: one read of g and two launches fewer.
 // Same block geometry / partial layout / summation order as in_partial_k<1>.
 __global__ __launch_bounds__(NRED) void border_in_partial_k(float* __restrict__ g, const float* __restrict__ slab,
-                                                            int ks, int Mb, int NB, const float* __restrict__ x,
+                                                            int ks, int Mb, int Lt, int Ll,
+                                                            const float* __restrict__ x,
                                                             const float* __restrict__ stats, double* __restrict__ part,
                                                             int H, int W, int C, int LP, int PG, int SP, int nsplit,
                                                             int act, float slope) {
@@ -273,13 +274,13 @@ __global__ __launch_bounds__(NRED) void border_in_partial_k(float* __restrict__ 
   const long zst = (long)Mb * C;
   // g of pixel p: + its border rows' slab sums where a padded position mirrors onto it (written back)
   auto border = [&](int p, float4 gv) {
-    int b0;
-    const int nr = dgrad_border_rows_of(p / W, p - (p / W) * W, H, W, &b0);
+    int rows[3];
+    const int nr = dgrad_border_slab_rows(n, p / W, p - (p / W) * W, H, W, Lt, Ll, rows);
     if (nr == 0) return gv;
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int r = 0; r < nr; ++r) {
       // a row's (<= 16) split slabs loaded together, then summed in split order
-      const float* base = slab + ((long)n * NB + b0 + r) * C + 4 * c4;
+      const float* base = slab + (long)rows[r] * C + 4 * c4;
       float4 u[16];
 #pragma unroll
       for (int q = 0; q < 16; ++q)
@@ -1019,7 +1020,7 @@ extern "C" int vst_conv2d_dgrad_refl_slabs(const float* dy, const void* wsplit, 
   VST_REQUIRE(bf_dgrad_refl1_ok(N, H, W, Cy, Cx, math),
               "conv2d_dgrad_refl_slabs: needs split-bf16 math, Cy %% 32 == 0, Cx %% 4 == 0, H, W >= 4");
   return bf_dgrad_refl1_launch(dy, wsplit, (long)Cx * 9 * Cy, addend, gout, N, H, W, Cy, Cx, math, (hipStream_t)stream,
-                               ws, ws_bytes / sizeof(float), false, nullptr, nullptr, nullptr);
+                               ws, ws_bytes / sizeof(float), false);
 }
 
 extern "C" int vst_instnorm_act_bwd_refl_border(float* gout, const float* x, const float* stats, float* dx, float* db,
@@ -1032,11 +1033,11 @@ extern "C" int vst_instnorm_act_bwd_refl_border(float* gout, const float* x, con
   VST_REQUIRE(bf_dgrad_refl1_ok(N, H, W, Cy, Cx, math) && red_geom(N, HW, Cx, g),
               "instnorm_act_bwd_refl_border: unsupported shape / arithmetic");
   VST_REQUIRE(!planes || ldp >= (long)N * HW, "instnorm_act_bwd_refl_border: plane stride %ld < N*HW", ldp);
-  int ks, NB;
-  const size_t off = bf_dgrad_refl1_slabs(N, H, W, Cy, Cx, math, &ks, &NB);
+  BorderSlabs b;
+  const size_t off = bf_dgrad_refl1_slabs(N, H, W, Cy, Cx, math, &b);
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(border_in_partial_k, dim3(g.nsplit, N), dim3(NRED), 0, s, gout, dgrad_ws + off, ks, N * NB, NB, x,
-                     stats, reinterpret_cast<double*>(in_ws), H, W, Cx, g.LP, g.PG, g.SP, g.nsplit, act, slope);
+  hipLaunchKernelGGL(border_in_partial_k, dim3(g.nsplit, N), dim3(NRED), 0, s, gout, dgrad_ws + off, b.ks, b.Mb, b.Lt,
+                     b.Ll, x, stats, reinterpret_cast<double*>(in_ws), H, W, Cx, g.LP, g.PG, g.SP, g.nsplit, act, slope);
   return in_bwd_tail(gout, x, stats, dx, db, in_ws, N, HW, Cx, act, slope, accumulate_db, planes, ldp, g, s);
 }
 

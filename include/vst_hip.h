@@ -456,10 +456,6 @@ int vst_interleave_phases(const float* p00, const float* p01, const float* p10, 
  * with padding 1 whose outputs are all (H+1) x (W+1): y[n][2i+a][2j+b][c] = P_ab[n][i+a][j+b][c]. */
 int vst_interleave_phases_full(const float* p00, const float* p01, const float* p10, const float* p11, float* y,
                                int N, int H, int W, int C, void* stream);
-
-/* ---- RAFT inference (SURVEY §8 A19 + §8f rank 3) ------------------------------------------ */
-/* Forward conv with separate row / column zero padding (SepConvGRU's (1,5) / (5,1) kernels with
- * padding (0,2) / (2,0), update.py:36-43); otherwise identical to vst_conv2d_fwd. */
 /* One phase (a, b) in {0,1}^2 of a stride-2 ConvTranspose2d(k3, p1, op1) stored straight into the
  * interleaved output y [N][2H][2W][Cop]: the phase conv vst_conv2d_fwd_hw(x, phase pack, R = 1 + a,
  * S = 1 + b, pad a / b) whose pixel (ph, pw) is y's (2(ph-a)+a, 2(pw-b)+b).  Four calls write every
@@ -467,6 +463,10 @@ int vst_interleave_phases_full(const float* p00, const float* p01, const float* 
  * planes; Cx % 8 == 0; split-bf16 math only (VST_EUNSUPPORTED for VST_MATH_F32). */
 int vst_conv2d_fwd_phase(const float* x, const void* wsplit, const float* bias, float* y, int N, int H, int W,
                          int Cx, int Cop, int a, int b, int act, float slope, int math, void* stream);
+
+/* ---- RAFT inference (SURVEY §8 A19 + §8f rank 3) ------------------------------------------ */
+/* Forward conv with separate row / column zero padding (SepConvGRU's (1,5) / (5,1) kernels with
+ * padding (0,2) / (2,0), update.py:36-43); otherwise identical to vst_conv2d_fwd. */
 int vst_conv2d_fwd_hw(const float* x, const float* wp, const void* wsplit, const float* bias, float* y,
                       int N, int H, int W, int Cx, int Cop, int R, int S, int stride, int pad_h, int pad_w,
                       int act, float slope, int math, void* stream);

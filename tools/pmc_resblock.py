@@ -16,7 +16,7 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-OPS = {"fprop": ("conv_fprop_bf_k",), "dgrad": ("conv_fprop_bf_k", "fprop_splitk_reduce_k", "dgrad_border_add_k"),
+OPS = {"fprop": ("conv_fprop_bf_k",), "dgrad": ("conv_fprop_bf_k", "fprop_splitk_reduce_k", "dgrad_border_add_k", "dgrad_border5_add_k"),
        "wgrad": ("nhwc_to_cp", "conv_wgrad_bf_k", "wgrad_reduce_store_k", "slab_group_sum_k"),
        "warp": ("warp_fwd_k",), "c0": ("conv_c4_direct_k", "in_finalize_k")}
 # the op's main GEMM dispatch (SQ metrics and its timing; the dgrad's 64x64 tail launch is excluded)

@@ -15,7 +15,7 @@ Also reported (same JSON line):
                 3x3 conv forward / stride-1 dgrad / wgrad at N=2B=8 (the batched G_A calls), each
                 timed with HIP events around each of its launches inside the timed steps:
                 algorithmic FLOPs / avg duration vs the ceiling of the arithmetic it runs; traffic =
-                PMC-measured HBM bytes per launch from profiles/r02_conv_pmc.json when that record
+                PMC-measured HBM bytes per launch from the committed record (PMC_FILE) when that record
                 matches the policy / tile / shape, else null.
   mixed_policy  the same step under the round-1 "mixed" policy (x6 forwards, x3 gradients), labelled.
   cpu_baseline  rank 0 only, N=1: the CPU oracle (stock PyTorch, NCHW fp32) with the GPU run's
@@ -88,7 +88,7 @@ def DOMINANT_KEYS(B):
             "resblock_wgrad": ("wgrad", (N, 64, 64, 256, 256, 3, 1, 1, "reflect"))}
 
 
-PMC_FILE = os.path.join(HERE, "profiles", "r03c_conv_pmc.json")
+PMC_FILE = os.path.join(HERE, "profiles", "r03d_conv_pmc.json")
 
 
 def _pmc_traffic(name, key):
@@ -140,8 +140,8 @@ def conv_roofline(name, probe, math):
         note = ("stride-1 data gradient as a forward conv over the rotated taps (66x66 padded frame)"
                 if name == "resblock_dgrad" else "ResnetBlock conv forward")
     elif op == "dgrad":
-        kernel = ("vst_conv2d_dgrad_refl: conv_fprop_bf_k interior (zero pad 1, %s) + border rows as "
-                  "split-K conv_fprop_bf_k<REFL=4> + dgrad_border_add_k [%s]" % (m, _mfma(m)))
+        kernel = ("vst_conv2d_dgrad_refl: conv_fprop_bf_k interior (zero pad 1, %s) + the K-restricted border "
+                  "GEMM (split-K conv_fprop_bf_k<REFL=5>, 128x128) + dgrad_border5_add_k [%s]" % (m, _mfma(m)))
         key = {"math": m, "N": N, "mfma": _mfma(m), "op": "dgrad_refl"}
         note = ("stride-1 reflect data gradient: interior conv + border GEMM (no padded frame, no fold); "
                 "dgrad_border_add_k adds the border slabs (VST_DGRAD_IN=1 moves that add into the "

@@ -143,6 +143,9 @@ void rk_fprop_launch(const float* x, const float* wp, const float* bias, float* 
                      int act, float slope, int kind, int math, hipStream_t s);
 long rk_cp_ld(long P);
 // split-operand bf16 implicit GEMM (conv_bf.hip); wsplit = vst_weight_split planes, stride wps
+bool bf_convT_phases_ok(int C, int Cop, int math);
+int bf_convT_phases_launch(const float* x, const void* const ws[4], const float* bias, float* y, int N, int H, int W,
+                           int C, int Cop, int act, float slope, int math, hipStream_t s);
 int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* bias, float* y, int N,
                     int H, int W, int C, int Ho, int Wo, int Cop, int R, int S, int st, int padh, int padw,
                     int reflect, int act, float slope, int math, int kind, hipStream_t s,

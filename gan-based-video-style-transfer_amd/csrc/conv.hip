@@ -987,6 +987,18 @@ extern "C" int vst_conv2d_fwd_phase(const float* x, const void* wsplit, const fl
                          1 + 2 * a + b);
 }
 
+extern "C" int vst_conv2d_convT_s2(const float* x, const void* ws00, const void* ws01, const void* ws10,
+                                   const void* ws11, const float* bias, float* y, int N, int H, int W, int Cx, int Cop,
+                                   int act, float slope, int math, void* stream) {
+  VST_REQUIRE(x && ws00 && ws01 && ws10 && ws11 && y && N > 0 && H > 0 && W > 0, "conv2d_convT_s2: bad args");
+  if (!bf_convT_phases_ok(Cx, Cop, math)) {
+    ::vst::set_error("conv2d_convT_s2: needs split-bf16 math, Cx %% 32 == 0, Cop %% 4 == 0");
+    return VST_EUNSUPPORTED;
+  }
+  const void* ws[4] = {ws00, ws01, ws10, ws11};
+  return bf_convT_phases_launch(x, ws, bias, y, N, H, W, Cx, Cop, act, slope, math, (hipStream_t)stream);
+}
+
 extern "C" int vst_conv2d_tfwd(const float* in, const float* wp, const float* bias,
                                const float* addend, float* out, int N, int Hi, int Wi, int Cy,
                                int Ho, int Wo, int Cx, int R, int S, int stride, int pad,

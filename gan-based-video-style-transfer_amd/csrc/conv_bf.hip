@@ -686,12 +686,13 @@ __device__ __attribute__((aligned(256))) float g_zero_page[64];
 // SPLIT (KSL only): split-K over the K-steps — block L = z * tiles + tile runs K-steps
 // [z * spk, z * spk + spk) and stores its raw partial tile to slab[z][m - m_base][Cop]
 // (fprop_splitk_reduce_k sums the splits in order and applies bias / act / IN partials).
-template <class T, bool KSL, int REFL, bool SPLIT = false>
-__global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_k(
-    const float* __restrict__ x, const __bf16* __restrict__ ws, long wps, const float* __restrict__ bias,
+// (body of conv_fprop_bf_k and conv_convT_phases_k; bid = the block's index in its tile grid)
+template <class T, bool KSL, int REFL, bool SPLIT>
+__device__ __forceinline__ void conv_fprop_bf_body(
+    int bid, const float* __restrict__ x, const __bf16* __restrict__ ws, long wps, const float* __restrict__ bias,
     float* __restrict__ y, int H, int W, int C, int Ho, int Wo, int Cop, int S, int st, int padh,
     int padw, int reflect, int act, float slope, int M, int Ktot, int m_base, double* __restrict__ part,
-    int spk = 0, float* __restrict__ slab = nullptr, const float* __restrict__ addend = nullptr, int oph = 0) {
+    int spk, float* __restrict__ slab, const float* __restrict__ addend, int oph) {
   static_assert(!SPLIT || KSL, "split-K needs the channel-slice-major K walk");
   static_assert(REFL < 4 || (SPLIT && KSL), "border rows run as split-K slabs");
   __shared__ __attribute__((aligned(16))) char smem[2 * T::STAGE];
@@ -699,8 +700,8 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_k(
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   int mt_, nt_;
   const int Mt_ = (M - m_base + T::BM - 1) / T::BM, Nt_ = (Cop + T::BN - 1) / T::BN;
-  const int zs = SPLIT ? blockIdx.x / (Mt_ * Nt_) : 0;
-  tile_of(SPLIT ? blockIdx.x - zs * Mt_ * Nt_ : blockIdx.x, Mt_, Nt_, mt_, nt_);
+  const int zs = SPLIT ? bid / (Mt_ * Nt_) : 0;
+  tile_of(SPLIT ? bid - zs * Mt_ * Nt_ : bid, Mt_, Nt_, mt_, nt_);
   const int m0 = m_base + mt_ * T::BM, n0 = nt_ * T::BN;
   const int kq = t % T::KC, rb = t / T::KC;
   const float* zp = g_zero_page;
@@ -1016,6 +1017,46 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_k(
         }
       }
     }
+}
+
+template <class T, bool KSL, int REFL, bool SPLIT = false>
+__global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_k(
+    const float* __restrict__ x, const __bf16* __restrict__ ws, long wps, const float* __restrict__ bias,
+    float* __restrict__ y, int H, int W, int C, int Ho, int Wo, int Cop, int S, int st, int padh,
+    int padw, int reflect, int act, float slope, int M, int Ktot, int m_base, double* __restrict__ part,
+    int spk = 0, float* __restrict__ slab = nullptr, const float* __restrict__ addend = nullptr, int oph = 0) {
+  conv_fprop_bf_body<T, KSL, REFL, SPLIT>(blockIdx.x, x, ws, wps, bias, y, H, W, C, Ho, Wo, Cop, S, st, padh, padw,
+                                          reflect, act, slope, M, Ktot, m_base, part, spk, slab, addend, oph);
+}
+
+// All four phases of a stride-2 ConvTranspose2d(k3, p1, op1) forward in ONE launch, each stored
+// straight into the interleaved output (phase_row).  Phase (a, b) is the (1+a) x (1+b) zero-pad (a, b)
+// conv over x whose (H+a) x (W+b) pixels map onto y's (2(ph-a)+a, 2(pw-b)+b).  Separately the phases
+// are four launches of 256-265 tiles each at N=8 (u0: 256 -> 128 at 64x64 on 128x128 tiles): each
+// a CU round plus a few stragglers, with K = 8-32 steps against its prologue / epilogue.  Here the
+// grid is their concatenation, the 4-tap phase first (longest first), each job's range starting on a
+// multiple of 8 so its XCD-aware tile order holds: ~4 rounds for the four.
+struct PhaseJobs {
+  const __bf16* ws[4];  // per job (launch order: phases 11, 01, 10, 00), the pack's bf16 planes
+  int t0[5];            // job j's blocks [t0[j], t0[j] + tiles_j), t0[j] % 8 == 0; t0[4] = grid
+};
+
+template <class T>
+__global__ __launch_bounds__(T::NT, T::MINB) void conv_convT_phases_k(const float* __restrict__ x, PhaseJobs jobs,
+                                                                      const float* __restrict__ bias,
+                                                                      float* __restrict__ y, int N, int H, int W,
+                                                                      int C, int Cop, int act, float slope) {
+  const int bid = blockIdx.x;
+  const int j = bid < jobs.t0[1] ? 0 : (bid < jobs.t0[2] ? 1 : (bid < jobs.t0[3] ? 2 : 3));
+  const int ph = j == 0 ? 3 : (j == 1 ? 1 : (j == 2 ? 2 : 0));
+  const int a = ph >> 1, b = ph & 1;
+  const int t0 = j == 0 ? jobs.t0[0] : (j == 1 ? jobs.t0[1] : (j == 2 ? jobs.t0[2] : jobs.t0[3]));
+  const __bf16* ws = j == 0 ? jobs.ws[0] : (j == 1 ? jobs.ws[1] : (j == 2 ? jobs.ws[2] : jobs.ws[3]));
+  const int Ho = H + a, Wo = W + b, M = N * Ho * Wo, K = (1 + a) * (1 + b) * C;
+  const int tiles = (M + T::BM - 1) / T::BM * ((Cop + T::BN - 1) / T::BN);
+  if (bid - t0 >= tiles) return;  // the job's padding to a multiple of 8 blocks
+  conv_fprop_bf_body<T, true, 0, false>(bid - t0, x, ws, (long)Cop * K, bias, y, H, W, C, Ho, Wo, Cop, 1 + b, 1, a,
+                                        b, 0, act, slope, M, K, 0, nullptr, 0, nullptr, nullptr, 1 + 2 * a + b);
 }
 
 // -------------------------------------------------------------------------- weight gradient
@@ -1683,6 +1724,42 @@ int bf_dgrad_refl1_launch(const float* dy, const void* wsplit, long wps, const f
     hipLaunchKernelGGL(bf::dgrad_border_add_k, dim3(ceil_div(Mb, 16), ceil_div(Cx, 64)), dim3(256), 0, s, slab, ks,
                        (int)Mb, Cx, dx, H, W, NB);
   return check_launch("conv2d_dgrad_refl");
+}
+
+// The four phases of a stride-2 ConvTranspose2d(k3, p1, op1) forward as one conv_convT_phases_k launch
+// (ws[ph], ph = 2a + b: the phase packs' bf16 planes).  128x128 tiles (128x64 for Cop <= 64); C a
+// multiple of the K-slice (32).
+bool bf_convT_phases_ok(int C, int Cop, int math) {
+  return math != VST_MATH_F32 && VST_BF_KSLICE && C % 32 == 0 && Cop % 4 == 0;
+}
+
+int bf_convT_phases_launch(const float* x, const void* const ws[4], const float* bias, float* y, int N, int H, int W,
+                           int C, int Cop, int act, float slope, int math, hipStream_t s) {
+  VST_REQUIRE(bf_convT_phases_ok(C, Cop, math), "convT phases: unsupported shape / arithmetic");
+  const int bm = 128, bn = Cop <= 64 ? 64 : 128;
+  bf::PhaseJobs jobs;
+  int t = 0;
+  for (int j = 0; j < 4; ++j) {
+    const int ph = j == 0 ? 3 : (j == 1 ? 1 : (j == 2 ? 2 : 0)), a = ph >> 1, b = ph & 1;
+    jobs.ws[j] = reinterpret_cast<const __bf16*>(ws[ph]);
+    jobs.t0[j] = t;
+    const long tiles = ((long)N * (H + a) * (W + b) + bm - 1) / bm * ((Cop + bn - 1) / bn);
+    t += (int)((tiles + 7) / 8 * 8);
+  }
+  jobs.t0[4] = t;
+#define VST_CT(BN_, WN_, NP_)                                                                             \
+  {                                                                                                        \
+    using T = bf::Tile<128, BN_, 64, WN_, 32, NP_>;                                                        \
+    hipLaunchKernelGGL(bf::conv_convT_phases_k<T>, dim3(t), dim3(T::NT), 0, s, x, jobs, bias, y, N, H, W, C, Cop, \
+                       act, slope);                                                                        \
+  }
+  if (math == VST_MATH_BF16X6) {
+    if (bn == 64) VST_CT(64, 32, 3) else VST_CT(128, 32, 3)
+  } else {
+    if (bn == 64) VST_CT(64, 32, 2) else VST_CT(128, 32, 2)
+  }
+#undef VST_CT
+  return check_launch("conv2d_convT_s2");
 }
 
 void bf_nhwc_to_planes(const float* x, void* y, long P, int Cs, int np, hipStream_t s, int row_in, int row_out) {

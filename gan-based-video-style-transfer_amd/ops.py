@@ -1137,6 +1137,8 @@ def conv4s2_dgrad(dy, packs, cop, role="bwd"):
 # ConvTranspose2d phase convs storing straight into the interleaved output (vst_conv2d_fwd_phase)
 # instead of four phase images + vst_interleave_phases; VST_CONVT_DIRECT=0 keeps the latter.
 CONVT_DIRECT = os.environ.get("VST_CONVT_DIRECT", "1") != "0"
+# ... and all four in one launch (vst_conv2d_convT_s2) where Cx % 32 == 0; VST_CONVT_GROUPED=0: one per phase.
+CONVT_GROUPED = os.environ.get("VST_CONVT_GROUPED", "1") != "0"
 
 
 def convT3s2_fwd(x, packs, bias, cop, act="none", role="fwd"):
@@ -1148,6 +1150,10 @@ def convT3s2_fwd(x, packs, bias, cop, act="none", role="fwd"):
     if CONVT_DIRECT and m != _lib.MATH_MODES["fp32"] and Cx % 8 == 0 and cop != 4 and \
             all(getattr(wp, "vst_split", None) is not None for wp in packs):
         y = torch.empty((N, 2 * H, 2 * W, cop), device=x.device)
+        if CONVT_GROUPED and Cx % 32 == 0:
+            _call("vst_conv2d_convT_s2", _p(x), *[_p(wp.vst_split) for wp in packs], _p(bias), _p(y), N, H, W, Cx,
+                  cop, ACT[act], 0.0, m, _stream())
+            return y
         for (a, b), wp in zip(((0, 0), (0, 1), (1, 0), (1, 1)), packs):
             _call("vst_conv2d_fwd_phase", _p(x), _p(wp.vst_split), _p(bias), _p(y), N, H, W, Cx, cop, a, b, ACT[act],
                   0.0, m, _stream())

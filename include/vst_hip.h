@@ -463,6 +463,13 @@ int vst_interleave_phases_full(const float* p00, const float* p01, const float* 
  * planes; Cx % 8 == 0; split-bf16 math only (VST_EUNSUPPORTED for VST_MATH_F32). */
 int vst_conv2d_fwd_phase(const float* x, const void* wsplit, const float* bias, float* y, int N, int H, int W,
                          int Cx, int Cop, int a, int b, int act, float slope, int math, void* stream);
+/* All four phases of that ConvTranspose2d forward in ONE launch (the four vst_conv2d_fwd_phase calls'
+ * tiles concatenated, the 2x2 phase first), same output bit for bit.  ws_ab = phase (a, b)'s pack
+ * planes.  Cx % 32 == 0, Cop % 4 == 0, split-bf16 math (else VST_EUNSUPPORTED: use the per-phase
+ * calls).  Replaces CycleGAN networks.py:357-364's ConvTranspose2d forward. */
+int vst_conv2d_convT_s2(const float* x, const void* ws00, const void* ws01, const void* ws10, const void* ws11,
+                        const float* bias, float* y, int N, int H, int W, int Cx, int Cop, int act, float slope,
+                        int math, void* stream);
 
 /* ---- RAFT inference (SURVEY §8 A19 + §8f rank 3) ------------------------------------------ */
 /* Forward conv with separate row / column zero padding (SepConvGRU's (1,5) / (5,1) kernels with

@@ -363,7 +363,9 @@ def test_tap_conv_dgrad(ops, conv_math, ci, co, k, mode):
 def test_convT_phases(ops, conv_math, ci, co, h, w):
     """ConvTranspose2d(k3, s2, p1, op1) forward as four phase convs vs torch; the phases stored straight
     into the interleaved output (vst_conv2d_fwd_phase, split-bf16 math) equal the phase images +
-    interleave route bit for bit (same GEMMs, other store addresses)."""
+    interleave route bit for bit (same GEMMs, other store addresses); all four phases in one launch
+    (vst_conv2d_convT_s2, Cx % 32 == 0) vs torch and vs the per-phase launches (its 128x128 / 128x64
+    tiles walk K as the planned tiles do for the x6 tiles: equal there; within fp32 rounding else)."""
     x = _g(95, (2, ci, h, w))
     wt = _g(96, (ci, co, 3, 3), 0.05)
     b = _g(97, (co,), 0.1)
@@ -372,12 +374,16 @@ def test_convT_phases(ops, conv_math, ci, co, h, w):
     xn = _nhwc(x, ops)
     y = ops.convT3s2_fwd(xn, packs, b.to(DEV), co)
     _close(_nchw(y, co, ops), ref, tol=CONV_TOL[conv_math], what="convT phases")
-    prev, ops.CONVT_DIRECT = ops.CONVT_DIRECT, False
+    prev, prev_g = ops.CONVT_DIRECT, ops.CONVT_GROUPED
     try:
+        ops.CONVT_GROUPED = False
+        y_ph = ops.convT3s2_fwd(xn, packs, b.to(DEV), co)
+        ops.CONVT_DIRECT = False
         y_il = ops.convT3s2_fwd(xn, packs, b.to(DEV), co)
     finally:
-        ops.CONVT_DIRECT = prev
-    assert torch.equal(y, y_il)
+        ops.CONVT_DIRECT, ops.CONVT_GROUPED = prev, prev_g
+    assert torch.equal(y_ph, y_il)
+    _close(y, y_ph, tol=1e-6, what="grouped vs per-phase launches")
 
 
 @pytest.mark.parametrize("forced", [False, True], ids=["planned", "t256x128"])

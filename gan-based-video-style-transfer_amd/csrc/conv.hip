@@ -960,6 +960,14 @@ extern "C" int vst_conv_plan_fwd_tail(int N, int H, int W, int Cx, int Cop, int 
   return VST_OK;
 }
 
+// vst_conv2d_fwd_hw with a padding mode (vst_tapconv_h_fwd's R x 1 reflect conv)
+extern "C" int vst_conv2d_fwd_hwp(const float* x, const float* wp, const void* wsplit, const float* bias, float* y,
+                                  int N, int H, int W, int Cx, int Cop, int R, int S, int stride, int pad_h, int pad_w,
+                                  int pad_mode, int act, float slope, int math, void* stream) {
+  return conv_fwd_impl(x, wp, wsplit, bias, y, N, H, W, Cx, Cop, R, S, stride, pad_h, pad_w, pad_mode, act, slope,
+                       math, (hipStream_t)stream);
+}
+
 extern "C" int vst_conv2d_fwd_hw(const float* x, const float* wp, const void* wsplit, const float* bias,
                                  float* y, int N, int H, int W, int Cx, int Cop, int R, int S, int stride,
                                  int pad_h, int pad_w, int act, float slope, int math, void* stream) {

@@ -38,8 +38,18 @@ __global__ void nhwc_to_nchw_k(const float* __restrict__ x, float* __restrict__ 
 // Element idx of a pack of the logical weight w[O][I][R][S] -> its (o, i, tap) coordinates.
 // KC: out[r][s][i][o] (Ip x Op per tap), CK: out[r][s][o][i] (Op x Ip per tap), OK: out[o][r][s][i],
 // IK / IKF: out[i][r][s][o] (IKF: taps rotated 180 deg).
-__device__ __forceinline__ void pack_coords(long idx, int RS, int Op, int Ip, int mode, int& o, int& i, int& rs) {
-  if (mode == VST_PACK_KC) {  // idx = (rs*Ip + i)*Op + o
+// SOK: out[s][o][r][i] (the OK pack of the R x 1 conv with S*Op outputs (s, o)).
+__device__ __forceinline__ void pack_coords(long idx, int R, int S, int Op, int Ip, int mode, int& o, int& i,
+                                            int& rs) {
+  const int RS = R * S;
+  if (mode == VST_PACK_SOK) {  // idx = ((s*Op + o)*R + r)*Ip + i
+    i = idx % Ip;
+    const long q = idx / Ip;
+    const int r = q % R;
+    const long q2 = q / R;
+    o = q2 % Op;
+    rs = r * S + (int)(q2 / Op);
+  } else if (mode == VST_PACK_KC) {  // idx = (rs*Ip + i)*Op + o
     o = idx % Op;
     const long q = idx / Op;
     i = q % Ip;
@@ -100,7 +110,7 @@ __global__ __launch_bounds__(256) void weight_pack_batch_k(const PackJob* __rest
   const long idx = (b - J.block0) * 256 + threadIdx.x;
   if (idx >= J.total) return;
   int o, i, rs;
-  pack_coords(idx, J.R * J.S, J.Op, J.Ip, J.mode, o, i, rs);
+  pack_coords(idx, J.R, J.S, J.Op, J.Ip, J.mode, o, i, rs);
   const int r = rs / J.S, s = rs - r * J.S;
   const int rr = J.tr[0] < 0 ? r : J.tr[r], ss = J.ts[0] < 0 ? s : J.ts[s];  // tr[0] < 0: identity
   const float v = (o < J.O && i < J.I) ? J.w[o * J.so + i * J.si + rr * J.sr + ss * J.ss] : 0.f;
@@ -116,7 +126,7 @@ __global__ void weight_pack_k(const float* __restrict__ w, float* __restrict__ o
   if (idx >= total) return;
   const int RS = R * S;
   int o, i, rs;
-  pack_coords(idx, RS, Op, Ip, mode, o, i, rs);
+  pack_coords(idx, R, S, Op, Ip, mode, o, i, rs);
   const float v = (o < O && i < I) ? w[((long)o * I + i) * RS + rs] : 0.f;
   out[idx] = v;
   if (split) store_split(split, total, idx, v);
@@ -174,7 +184,7 @@ extern "C" int vst_nhwc_to_nchw(const float* x, float* y, int N, int C, int H, i
 
 extern "C" int vst_weight_pack(const float* w, float* out, int O, int I, int R, int S, int Op,
                                int Ip, int mode, void* stream) {
-  VST_REQUIRE(w && out && O <= Op && I <= Ip && mode >= VST_PACK_KC && mode <= VST_PACK_IKF,
+  VST_REQUIRE(w && out && O <= Op && I <= Ip && mode >= VST_PACK_KC && mode <= VST_PACK_SOK,
               "weight_pack: bad args");
   const long total = (long)R * S * Op * Ip;
   hipLaunchKernelGGL(weight_pack_k, dim3(ceil_div(total, 256)), dim3(256), 0, (hipStream_t)stream, w,
@@ -184,7 +194,7 @@ extern "C" int vst_weight_pack(const float* w, float* out, int O, int I, int R, 
 
 extern "C" int vst_weight_pack_split(const float* w, float* out, void* split, int O, int I, int R, int S, int Op,
                                      int Ip, int mode, void* stream) {
-  VST_REQUIRE(w && out && split && O <= Op && I <= Ip && mode >= VST_PACK_KC && mode <= VST_PACK_IKF,
+  VST_REQUIRE(w && out && split && O <= Op && I <= Ip && mode >= VST_PACK_KC && mode <= VST_PACK_SOK,
               "weight_pack_split: bad args");
   const long total = (long)R * S * Op * Ip;
   hipLaunchKernelGGL(weight_pack_k, dim3(ceil_div(total, 256)), dim3(256), 0, (hipStream_t)stream, w, out, O, I, R,

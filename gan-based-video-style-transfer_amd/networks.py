@@ -310,6 +310,9 @@ DGRAD_AS_FPROP = os.environ.get("VST_DGRAD_FPROP", "1") != "0"
 # The generator's last conv (4 padded output channels) runs as a tap GEMM on the matrix cores
 # (ops.tap_conv_fwd / tap_conv_wgrad) instead of the VALU skinny kernel; VST_TAP_CONV=0 disables.
 TAP_LAST = os.environ.get("VST_TAP_CONV", "1") != "0"
+# ... its forward as the 7x1 conv with (column tap, channel) outputs + a column tap sum (ops.tap_conv_fwd_h:
+# a 28-wide intermediate instead of the 196-wide one); VST_TAP_H=0 keeps the 1x1 conv + full tap sum.
+TAP_H = os.environ.get("VST_TAP_H", "1") != "0"
 # The up-sampling ConvTranspose2d (k3 s2 p1 op1) forward as four sub-pixel phase convs on the
 # split-bf16 forward kernel + an interleave (ops.convT3s2_fwd); VST_CONVT_PHASES=0 disables.
 CONVT_PHASES = os.environ.get("VST_CONVT_PHASES", "1") != "0"
@@ -404,6 +407,8 @@ class ResnetGenerator(FlatNet):
             P["c08"] = ops.weight_pack(c0.weight, ops.PACK_FWD, Ip=8)
         if TAP_LAST:
             P["ftap"] = ops.weight_pack(f.weight, ops.PACK_CK)
+            if TAP_H and f.weight.shape[0] <= 4 and f.weight.shape[2] == f.weight.shape[3]:
+                P["ftaph"] = ops.weight_pack(f.weight, ops.PACK_SOK, Op=4)
             if c0.weight.shape[1] <= 4:  # image-input first layer: its data gradient as a tap gather
                 P["c0kc"] = ops.weight_pack(c0.weight, ops.PACK_KC)
         P["ikf"] = {}
@@ -561,7 +566,8 @@ class _GeneratorFn(torch.autograd.Function):
             a = an
         kc, _, b = P["f"]
         if "ftap" in P:
-            out = ops.tap_conv_fwd(a, P["ftap"], b, 7, 3, "reflect", act="tanh", role=role)
+            out = (ops.tap_conv_fwd_h(a, P["ftaph"], b, 7, 3, "reflect", act="tanh", role=role) if "ftaph" in P else
+                   ops.tap_conv_fwd(a, P["ftap"], b, 7, 3, "reflect", act="tanh", role=role))
         else:
             out = ops.conv2d_fwd(a, kc, b, cpad(net.output_nc), 7, 7, 1, 3, "reflect", act="tanh", role=role)
         sv["f"] = (a, out)

@@ -12,7 +12,7 @@ from . import _lib
 
 ACT = {"none": 0, "relu": 1, "lrelu": 2, "tanh": 3}
 PAD = {"zero": 0, "reflect": 1}
-PACK_KC, PACK_CK, PACK_OK, PACK_IK, PACK_IKF = 0, 1, 2, 3, 4
+PACK_KC, PACK_CK, PACK_OK, PACK_IK, PACK_IKF, PACK_SOK = 0, 1, 2, 3, 4, 5
 # the conv kernels consume: forward conv -> PACK_OK, data-gradient / transposed conv -> PACK_IK
 PACK_FWD, PACK_DGRAD = PACK_OK, PACK_IK
 IN_EPS = 1e-5
@@ -70,7 +70,7 @@ def nhwc_to_nchw(x, c):
 def _pack_shape(mode, O, I_, R, S, Op=None, Ip=None):
     Op, Ip = Op or cpad(O), Ip or cpad(I_)
     return {PACK_KC: (R, S, Ip, Op), PACK_CK: (R, S, Op, Ip), PACK_OK: (Op, R, S, Ip),
-            PACK_IK: (Ip, R, S, Op), PACK_IKF: (Ip, R, S, Op)}[mode]
+            PACK_IK: (Ip, R, S, Op), PACK_IKF: (Ip, R, S, Op), PACK_SOK: (S * Op, R, 1, Ip)}[mode]
 
 
 class PackBatch:
@@ -1035,6 +1035,20 @@ def tap_conv_fwd(x, ck, bias, R, pad, pad_mode="zero", act="none", slope=0.0, ro
         z = conv2d_fwd(x[a:b], ck, None, R * R * 4, 1, 1, 1, 0, "zero", role=role, out=zbuf[:b - a])
         _call("vst_tapsum_fwd", _p(z), R * R * 4, _p(bias), _p(y[a:b]), b - a, H, W, R, R, pad, PAD[pad_mode],
               ACT[act], float(slope), _stream())
+    return y
+
+
+def tap_conv_fwd_h(x, sok, bias, R, pad, pad_mode="zero", act="none", slope=0.0, role="fwd"):
+    """The same conv as tap_conv_fwd with the (r, ci) contraction on the matrix cores and only the column
+    taps summed afterwards (vst_tapconv_h_fwd): sok = the VST_PACK_SOK pack [S*4][R][1][Ci]."""
+    _dev_check(x, sok, bias)
+    N, H, W, Cx = x.shape
+    if sok.shape != (R * 4, R, 1, Cx):
+        raise ValueError("tap_conv_fwd_h: SOK pack shape %s does not match R=%d, Cx=%d" % (tuple(sok.shape), R, Cx))
+    y = torch.empty((N, H, W, 4), device=x.device)
+    z = torch.empty((N, H, W, R * 4), device=x.device)
+    _call("vst_tapconv_h_fwd", _p(x), _p(sok), _p(getattr(sok, "vst_split", None)), _p(bias), _p(z), _p(y), N, H, W,
+          Cx, R, pad, PAD[pad_mode], ACT[act], float(slope), _math(role), _stream())
     return y
 
 

@@ -58,9 +58,11 @@ enum { VST_PACK_KC = 0,   /* [R][S][Ci][Co]  (rows k=(r,s,ci), cols co) */
        VST_PACK_CK = 1,   /* [R][S][Co][Ci]  (rows k=(r,s,co), cols ci) */
        VST_PACK_OK = 2,   /* [Co][R][S][Ci]  conv forward B operand, k=(r,s,ci) contiguous per co */
        VST_PACK_IK = 3,   /* [Ci][R][S][Co]  dgrad / transposed-conv B operand, k=(r,s,co) per ci */
-       VST_PACK_IKF = 4 };/* IK with the taps rotated 180 deg: w[co][ci][R-1-r][S-1-s] — the
+       VST_PACK_IKF = 4,  /* IK with the taps rotated 180 deg: w[co][ci][R-1-r][S-1-s] — the
                            * VST_PACK_OK pack of the conv whose forward is this conv's stride-1
                            * data gradient (dx = conv(dy, IKF, pad R-1-pad), then reflect fold) */
+       VST_PACK_SOK = 5 };/* [S][Co][R][Ci]: the VST_PACK_OK pack of the R x 1 conv with S*Op outputs
+                           * (s, co) — out[(s*Op + co)][r][ci] = w[co][ci][r][s] (vst_tapconv_h_fwd) */
 
 const char* vst_last_error(void);
 int vst_version(void);
@@ -430,6 +432,16 @@ int vst_instnorm_stats_from_running(const float* running_mean, const float* runn
  * networks.py:365-367 (c7s1-3) on the matrix cores. */
 int vst_tapsum_fwd(const float* z, int zcs, const float* bias, float* y, int N, int H, int W, int R, int S,
                    int pad, int pad_mode, int act, float slope, void* stream);
+/* The same conv with the contraction over (r, ci) on the matrix cores and only the column taps
+ * summed afterwards: z[q][(s*4 + co)] = sum_{r,ci} x[src_row(q, r)][ci] w[co][ci][r][s] is the R x 1
+ * conv (row padding `pad`, pad_mode) of x with the VST_PACK_SOK pack (+ wsplit planes; 4*S outputs),
+ * then y[p][co] = act(bias[co] + sum_s z[(h, src(w + s - pad))][s*4 + co]).  z = caller's buffer of
+ * N*H*W*4*S floats.  Replaces vst_conv2d_fwd(1x1, R*S*4 outputs) + vst_tapsum_fwd: z is S*16 bytes
+ * per pixel instead of R*S*16, and the GEMM's K is R*Cx instead of Cx.  'same' convs (2 pad == R-1 ==
+ * S-1), R == S <= 8, Cx % 8 == 0. */
+int vst_tapconv_h_fwd(const float* x, const float* wp, const void* wsplit, const float* bias, float* z, float* y,
+                      int N, int H, int W, int Cx, int R, int pad, int pad_mode, int act, float slope, int math,
+                      void* stream);
 /* Adjoint gather of the weight gradient: d[q][(r*S+s)*4 + co] = sum_{p: src(p,r,s) = q} g[p][co]
  * (g NHWC4); then vst_conv2d_wgrad(x, d) as a 1x1 wgrad gives t[(r*S+s)*4 + co][ci], and
  * vst_tap_wgrad_scatter writes dw[co][ci][r][s] (+)= t (co < Co <= 4). */
@@ -477,6 +489,10 @@ int vst_conv2d_convT_s2(const float* x, const void* ws00, const void* ws01, cons
 int vst_conv2d_fwd_hw(const float* x, const float* wp, const void* wsplit, const float* bias, float* y,
                       int N, int H, int W, int Cx, int Cop, int R, int S, int stride, int pad_h, int pad_w,
                       int act, float slope, int math, void* stream);
+/* vst_conv2d_fwd_hw with a padding mode (VST_PAD_ZERO / VST_PAD_REFLECT). */
+int vst_conv2d_fwd_hwp(const float* x, const float* wp, const void* wsplit, const float* bias, float* y, int N, int H,
+                       int W, int Cx, int Cop, int R, int S, int stride, int pad_h, int pad_w, int pad_mode, int act,
+                       float slope, int math, void* stream);
 /* InputPadder.pad (utils/raft/raft/utils/utils.py:7-20, replicate) + raft.py:89-90 2*(x/255)-1:
  * NCHW [B][3][H][W] -> NHWC4 [B][H+pt+pb][W+pl+pr][4]. */
 int vst_raft_prep(const float* img, float* out, int B, int H, int W, int pad_l, int pad_r, int pad_t,

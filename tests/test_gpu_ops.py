@@ -334,10 +334,36 @@ def test_tap_conv(ops, conv_math, co, ci, k, mode):
     xn = _nhwc(x.detach(), ops)
     yt = ops.tap_conv_fwd(xn, ck, bp, k, pad, mode, act="tanh")
     _close(_nchw(yt, co, ops), y, tol=CONV_TOL[conv_math], what="tap fwd")
+    sok = ops.weight_pack(w.detach().to(DEV), ops.PACK_SOK, Op=4)
+    yh = ops.tap_conv_fwd_h(xn, sok, bp, k, pad, mode, act="tanh")
+    _close(_nchw(yh, co, ops), y, tol=CONV_TOL[conv_math], what="tap fwd (k x 1 conv + column taps)")
     g = ops.act_bwd(_nhwc(gy, ops), yt, "tanh")
     dw = torch.full((co, ci, k, k), 0.25, device=DEV)
     ops.tap_conv_wgrad(xn, g, dw, k, pad, mode, accumulate=True)
     _close(dw.cpu() - 0.25, w.grad, tol=CONV_TOL[conv_math], what="tap wgrad")
+
+
+def test_tap_conv_fwd_h_production(ops, conv_math):
+    """The generator's last layer (64 -> 3, 7x7 reflect, tanh) at 256x256 through vst_tapconv_h_fwd vs torch
+    fp32 and vs the 1x1-conv + full tap-sum route; the SOK pack built by a PackBatch equals the direct one."""
+    N, ci, H, W, co, k = 2, 64, 256, 256, 3, 7
+    x = _g(85, (N, ci, H, W))
+    w = _g(86, (co, ci, k, k), 0.02)
+    b = _g(87, (co,), 0.1)
+    ref = torch.tanh(F.conv2d(F.pad(x, (3,) * 4, mode="reflect"), w, b))
+    wd = w.to(DEV)
+    sok = ops.weight_pack(wd, ops.PACK_SOK, Op=4)
+    with ops.PackBatch():
+        sok_b = ops.weight_pack(wd, ops.PACK_SOK, Op=4)
+    assert torch.equal(sok, sok_b) and torch.equal(sok.vst_split, sok_b.vst_split)
+    bp = torch.zeros(4, device=DEV)
+    bp[:co] = b.to(DEV)
+    xn = _nhwc(x, ops)
+    yh = ops.tap_conv_fwd_h(xn, sok, bp, k, 3, "reflect", act="tanh")
+    _close(_nchw(yh, co, ops), ref, tol=CONV_TOL[conv_math], what="last layer, row conv + column taps")
+    yt = ops.tap_conv_fwd(xn, ops.weight_pack(wd, ops.PACK_CK), bp, k, 3, "reflect", act="tanh")
+    _close(yh, yt, tol=CONV_TOL[conv_math], what="vs 1x1 conv + full tap sum")
+    assert float(yh[..., 3].abs().max()) == float(torch.tanh(torch.zeros(1))[0])
 
 
 @pytest.mark.parametrize("ci,co,k,mode", [(3, 64, 7, "reflect"), (2, 64, 7, "reflect"), (3, 32, 3, "zero")])

@@ -144,7 +144,7 @@ def conv_roofline(name, probe, math):
                   "GEMM (split-K conv_fprop_bf_k<REFL=5>, 128x128) + dgrad_border5_add_k [%s]" % (m, _mfma(m)))
         key = {"math": m, "N": N, "mfma": _mfma(m), "op": "dgrad_refl"}
         note = ("stride-1 reflect data gradient: interior conv + border GEMM (no padded frame, no fold); "
-                "dgrad_border_add_k adds the border slabs (VST_DGRAD_IN=1 moves that add into the "
+                "dgrad_border5_add_k adds the border slabs (VST_DGRAD_IN=1 moves that add into the "
                 "IN-backward partial pass)")
     else:
         kernel = ("vst_conv2d_wgrad: nhwc_to_cp_pad_k + nhwc_to_cp_planes_k copies + conv_wgrad_bf_k "

@@ -298,20 +298,21 @@ __global__ __launch_bounds__(64) void tapgather_row_k(const float4* __restrict__
 
 // dw[co][ci][rs] (+)= t[(rs*4 + co)][ci], co < Co
 // y[p][co] = act(bias[co] + sum_s z[(n, h, src(w + s - pad))][s*4 + co]): the column taps of
-// vst_tapconv_h_fwd (z rows of S float4s).  One thread per pixel, s in order.
+// vst_tapconv_h_fwd (z rows of Wz pixels x S float4s, y rows of Wo pixels).  One thread per pixel,
+// s in order.
 template <int S>
 __global__ __launch_bounds__(256) void tapsum_h_k(const float4* __restrict__ z, const float* __restrict__ bias,
-                                                  float4* __restrict__ y, int W, int pad, int reflect, int act,
-                                                  float slope, long P) {
+                                                  float4* __restrict__ y, int Wz, int Wo, int pad, int reflect,
+                                                  int act, float slope, long P) {
   const long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= P) return;
-  const long row = p / W;
-  const int w = (int)(p - row * W);
-  const float4* zr = z + row * W * S;
+  const long row = p / Wo;
+  const int w = (int)(p - row * Wo);
+  const float4* zr = z + row * Wz * S;
   float4 v[S];
 #pragma unroll
   for (int s = 0; s < S; ++s) {
-    const int ww = src_index(w + s - pad, W, reflect);
+    const int ww = src_index(w + s - pad, Wz, reflect);
     v[s] = ww >= 0 ? zr[(long)ww * S + s] : make_float4(0.f, 0.f, 0.f, 0.f);
   }
   float4 acc = bias ? make_float4(bias[0], bias[1], bias[2], bias[3]) : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -345,23 +346,28 @@ using namespace vst;
 extern "C" int vst_tapconv_h_fwd(const float* x, const float* wp, const void* wsplit, const float* bias, float* z,
                                  float* y, int N, int H, int W, int Cx, int R, int pad, int pad_mode, int act,
                                  float slope, int math, void* stream) {
-  VST_REQUIRE(x && wp && z && y && N > 0 && H > 0 && W > 0 && Cx % 8 == 0 && 2 * pad == R - 1 && pad >= 0,
-              "tapconv_h_fwd: bad args ('same' convs, Cx %% 8 == 0)");
+  VST_REQUIRE(x && wp && z && y && N > 0 && H > 0 && W > 0 && Cx % 8 == 0 && pad >= 0 && pad < R,
+              "tapconv_h_fwd: bad args (Cx %% 8 == 0, 0 <= pad < R)");
   VST_REQUIRE(R == 3 || R == 5 || R == 7, "tapconv_h_fwd: R in {3, 5, 7}");
-  VST_REQUIRE(pad_mode == VST_PAD_ZERO || (pad < H && pad < W), "tapconv_h_fwd: reflect pad >= size");
+  VST_REQUIRE(pad_mode == VST_PAD_ZERO || (2 * pad == R - 1 && pad < H && pad < W),
+              "tapconv_h_fwd: reflect padding needs a 'same' conv with pad < size");
+  const int Ho = H + 2 * pad - R + 1, Wo = W + 2 * pad - R + 1;
   // the R x 1 conv: rows padded by `pad`, the columns by 0 (their taps are summed below)
   if (int e = vst_conv2d_fwd_hwp(x, wp, wsplit, nullptr, z, N, H, W, Cx, 4 * R, R, 1, 1, pad, 0, pad_mode,
                                  VST_ACT_NONE, 0.f, math, stream))
     return e;
-  const long P = (long)N * H * W;
+  const long P = (long)N * Ho * Wo;
   const int refl = pad_mode == VST_PAD_REFLECT;
   hipStream_t st = (hipStream_t)stream;
   const float4* z4 = reinterpret_cast<const float4*>(z);
   float4* y4 = reinterpret_cast<float4*>(y);
   const dim3 g((unsigned)ceil_div(P, 256));
-  if (R == 3) hipLaunchKernelGGL(tapsum_h_k<3>, g, dim3(256), 0, st, z4, bias, y4, W, pad, refl, act, slope, P);
-  else if (R == 5) hipLaunchKernelGGL(tapsum_h_k<5>, g, dim3(256), 0, st, z4, bias, y4, W, pad, refl, act, slope, P);
-  else hipLaunchKernelGGL(tapsum_h_k<7>, g, dim3(256), 0, st, z4, bias, y4, W, pad, refl, act, slope, P);
+  if (R == 3)
+    hipLaunchKernelGGL(tapsum_h_k<3>, g, dim3(256), 0, st, z4, bias, y4, W, Wo, pad, refl, act, slope, P);
+  else if (R == 5)
+    hipLaunchKernelGGL(tapsum_h_k<5>, g, dim3(256), 0, st, z4, bias, y4, W, Wo, pad, refl, act, slope, P);
+  else
+    hipLaunchKernelGGL(tapsum_h_k<7>, g, dim3(256), 0, st, z4, bias, y4, W, Wo, pad, refl, act, slope, P);
   return check_launch("tapconv_h_fwd");
 }
 

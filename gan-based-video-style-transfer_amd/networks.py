@@ -313,6 +313,8 @@ TAP_LAST = os.environ.get("VST_TAP_CONV", "1") != "0"
 # ... its forward as the 7x1 conv with (column tap, channel) outputs + a column tap sum (ops.tap_conv_fwd_h:
 # a 28-wide intermediate instead of the 196-wide one); VST_TAP_H=0 keeps the 1x1 conv + full tap sum.
 TAP_H = os.environ.get("VST_TAP_H", "1") != "0"
+# the image-input first layer's data gradient the same way (ops.tap_conv_dgrad_h); VST_TAP_HD=0: tap gather.
+TAP_HD = os.environ.get("VST_TAP_HD", "1") != "0"
 # The up-sampling ConvTranspose2d (k3 s2 p1 op1) forward as four sub-pixel phase convs on the
 # split-bf16 forward kernel + an interleave (ops.convT3s2_fwd); VST_CONVT_PHASES=0 disables.
 CONVT_PHASES = os.environ.get("VST_CONVT_PHASES", "1") != "0"
@@ -411,6 +413,8 @@ class ResnetGenerator(FlatNet):
                 P["ftaph"] = ops.weight_pack(f.weight, ops.PACK_SOK, Op=4)
             if c0.weight.shape[1] <= 4:  # image-input first layer: its data gradient as a tap gather
                 P["c0kc"] = ops.weight_pack(c0.weight, ops.PACK_KC)
+                if TAP_HD and c0.weight.shape[2] == c0.weight.shape[3]:  # ... or a 7x1 conv + column taps + fold
+                    P["c0sokd"] = ops.dgrad_sok_pack(c0.weight)
         P["ikf"] = {}
         # the ResnetBlock data gradients run as forward convs over the IKF packs when the channel
         # count suits the split-bf16 kernel (dgrad_reflect): their IK packs are then never read
@@ -733,7 +737,8 @@ class _GeneratorFn(torch.autograd.Function):
         gx = None
         if ctx.needs_input_grad[0]:
             if "c0kc" in P and x.shape[-1] == 4:
-                gx = ops.tap_conv_dgrad(dy, P["c0kc"], 7, 3, "reflect")
+                gx = (ops.tap_conv_dgrad_h(dy, P["c0sokd"], 7, 3, "reflect") if "c0sokd" in P else
+                      ops.tap_conv_dgrad(dy, P["c0kc"], 7, 3, "reflect"))
             else:
                 gx = dgrad_reflect(dy, "c0", x.shape[-1], 7, 3, x.shape[1], x.shape[2])
         ctx.sv = None

@@ -1045,8 +1045,9 @@ def tap_conv_fwd_h(x, sok, bias, R, pad, pad_mode="zero", act="none", slope=0.0,
     N, H, W, Cx = x.shape
     if sok.shape != (R * 4, R, 1, Cx):
         raise ValueError("tap_conv_fwd_h: SOK pack shape %s does not match R=%d, Cx=%d" % (tuple(sok.shape), R, Cx))
-    y = torch.empty((N, H, W, 4), device=x.device)
-    z = torch.empty((N, H, W, R * 4), device=x.device)
+    Ho, Wo = H + 2 * pad - R + 1, W + 2 * pad - R + 1
+    y = torch.empty((N, Ho, Wo, 4), device=x.device)
+    z = torch.empty((N, Ho, W, R * 4), device=x.device)
     _call("vst_tapconv_h_fwd", _p(x), _p(sok), _p(getattr(sok, "vst_split", None)), _p(bias), _p(z), _p(y), N, H, W,
           Cx, R, pad, PAD[pad_mode], ACT[act], float(slope), _math(role), _stream())
     return y
@@ -1096,6 +1097,29 @@ def tap_conv_dgrad(dy, kc, R, pad, pad_mode="zero", role="bwd"):
         z = conv2d_fwd(dy[a:b], kc, None, R * R * 4, 1, 1, 1, 0, "zero", role=role, out=zbuf[:b - a])
         _call("vst_tapgather", _p(z), _p(y[a:b]), b - a, H, W, R, R, pad, PAD[pad_mode], _stream())
     return y
+
+
+def dgrad_sok_pack(w):
+    """VST_PACK_SOK pack of the data gradient of a conv with <= 4 input channels, w [Co][Ci][R][S]: the
+    conv dy -> dx over the taps rotated 180 deg, w_d[o = ci][i = co][r][s] = w[co][ci][R-1-r][S-1-s]."""
+    Co, Ci, R, S = w.shape
+    pb = PackBatch._active
+    if pb is not None:  # straight from w: transposed strides + reversed tap maps
+        return pb.add(w, PACK_SOK, Ci, Co, R, S, (R * S, Ci * R * S, S, 1), list(range(R - 1, -1, -1)),
+                      list(range(S - 1, -1, -1)), Op=4)
+    return weight_pack(w.detach().permute(1, 0, 2, 3).flip(2, 3).contiguous(), PACK_SOK, Op=4)
+
+
+def tap_conv_dgrad_h(dy, sokd, R, pad, pad_mode="zero", role="bwd"):
+    """Data gradient (NHWC4) of a 'same' conv with <= 4 input channels via vst_tapconv_h_fwd: the full
+    correlation of dy with the rotated taps (sokd = dgrad_sok_pack(w); zero pad R-1), then the reflect fold
+    (reflect padding) or the interior crop (zero padding)."""
+    _dev_check(dy, sokd)
+    full = tap_conv_fwd_h(dy, sokd, None, R, R - 1, "zero", role=role)
+    if pad_mode == "reflect":
+        return reflect_fold(full, pad) if pad == (R - 1) // 2 else None
+    o = R - 1 - pad
+    return full[:, o:full.shape[1] - o, o:full.shape[2] - o].contiguous()
 
 
 def convT3s2_phase_packs(wt):

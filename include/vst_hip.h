@@ -435,10 +435,12 @@ int vst_tapsum_fwd(const float* z, int zcs, const float* bias, float* y, int N, 
 /* The same conv with the contraction over (r, ci) on the matrix cores and only the column taps
  * summed afterwards: z[q][(s*4 + co)] = sum_{r,ci} x[src_row(q, r)][ci] w[co][ci][r][s] is the R x 1
  * conv (row padding `pad`, pad_mode) of x with the VST_PACK_SOK pack (+ wsplit planes; 4*S outputs),
- * then y[p][co] = act(bias[co] + sum_s z[(h, src(w + s - pad))][s*4 + co]).  z = caller's buffer of
- * N*H*W*4*S floats.  Replaces vst_conv2d_fwd(1x1, R*S*4 outputs) + vst_tapsum_fwd: z is S*16 bytes
- * per pixel instead of R*S*16, and the GEMM's K is R*Cx instead of Cx.  'same' convs (2 pad == R-1 ==
- * S-1), R == S <= 8, Cx % 8 == 0. */
+ * then y[p][co] = act(bias[co] + sum_s z[(h, src(w + s - pad))][s*4 + co]).  Output Ho x Wo =
+ * (H + 2 pad - R + 1) x (W + 2 pad - R + 1); z = caller's buffer of N*Ho*W*4*R floats.  Replaces
+ * vst_conv2d_fwd(1x1, R*S*4 outputs) + vst_tapsum_fwd: z is S*16 bytes per pixel instead of R*S*16,
+ * and the GEMM's K is R*Cx instead of Cx.  R == S in {3, 5, 7}, Cx % 8 == 0; reflect: 'same' convs
+ * (2 pad == R-1); zero: any pad < R (pad R-1 with the rotated-tap pack = the full correlation of a
+ * data gradient, whose reflect fold gives the image-input layer's dx: ops.tap_conv_dgrad_h). */
 int vst_tapconv_h_fwd(const float* x, const float* wp, const void* wsplit, const float* bias, float* z, float* y,
                       int N, int H, int W, int Cx, int R, int pad, int pad_mode, int act, float slope, int math,
                       void* stream);

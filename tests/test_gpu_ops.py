@@ -366,7 +366,8 @@ def test_tap_conv_fwd_h_production(ops, conv_math):
     assert float(yh[..., 3].abs().max()) == float(torch.tanh(torch.zeros(1))[0])
 
 
-@pytest.mark.parametrize("ci,co,k,mode", [(3, 64, 7, "reflect"), (2, 64, 7, "reflect"), (3, 32, 3, "zero")])
+@pytest.mark.parametrize("ci,co,k,mode", [(3, 64, 7, "reflect"), (2, 64, 7, "reflect"), (3, 32, 3, "zero"),
+                                          (3, 64, 7, "zero")])
 def test_tap_conv_dgrad(ops, conv_math, ci, co, k, mode):
     """Data gradient of a 'same' conv with <= 4 input channels (generator first layer) as a 1x1 conv
     over all taps + the adjoint tap gather, against torch autograd."""
@@ -382,6 +383,15 @@ def test_tap_conv_dgrad(ops, conv_math, ci, co, k, mode):
     dx = ops.tap_conv_dgrad(_nhwc(gy, ops), kc, k, pad, mode)
     _close(_nchw(dx, ci, ops), x.grad, tol=CONV_TOL[conv_math], what="tap dgrad")
     assert float(dx[..., ci:].abs().max()) == 0.0
+    # the k x 1 conv + column-tap route over the full-correlation frame (+ reflect fold / interior crop);
+    # the PackBatch-built rotated SOK pack equals the direct one
+    sokd = ops.dgrad_sok_pack(w.to(DEV))
+    with ops.PackBatch():
+        sokd_b = ops.dgrad_sok_pack(w.to(DEV))
+    assert torch.equal(sokd, sokd_b)
+    dxh = ops.tap_conv_dgrad_h(_nhwc(gy, ops), sokd, k, pad, mode)
+    _close(_nchw(dxh, ci, ops), x.grad, tol=CONV_TOL[conv_math], what="tap dgrad (k x 1 conv + column taps)")
+    assert float(dxh[..., ci:].abs().max()) == 0.0
 
 
 @pytest.mark.parametrize("ci,co,h,w", [(128, 64, 9, 11), (256, 128, 8, 8), (64, 32, 5, 70),

@@ -112,6 +112,8 @@ SIGNATURES = {
     "vst_conv2d_fwd_hw": (I, [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, I, P]),
     "vst_conv2d_fwd_hwp": (I, [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, F, I, P]),
     "vst_tapconv_h_fwd": (I, [P, P, P, P, P, P, I, I, I, I, I, I, I, I, F, I, P]),
+    "vst_tapshift_planes": (I, [P, P, L, I, I, I, I, P]),
+    "vst_tap_wgrad_scatter_h": (I, [P, P, I, I, I, I, I, P]),
     "vst_conv2d_fwd_phase": (I, [P, P, P, P, I, I, I, I, I, I, I, I, F, I, P]),
     "vst_conv2d_convT_s2": (I, [P, P, P, P, P, P, P, I, I, I, I, I, I, F, I, P]),
     "vst_raft_prep": (I, [P, P, I, I, I, I, I, I, I, P]),

@@ -327,6 +327,57 @@ __global__ __launch_bounds__(256) void tapsum_h_k(const float4* __restrict__ z, 
                      apply_act(acc.w, act, slope));
 }
 
+// dy of the R x 1 weight-gradient form of a reflect 'same' conv with 4 (padded) outputs
+// (vst_tapshift_planes): over the (H+2) x (W+S+1) output frame of the R x 1 conv with padding
+// pad+1, channel (s, co) of pixel (ho, wo) is g[ho-1][wo-1-s][co] (zero outside), written as the x6
+// wgrad's three bf16 planes [3][S*4][ldp].  grid (ceil(P / 256), S): thread = (frame pixel, column tap).
+__global__ __launch_bounds__(256) void tapshift_planes_k(const float4* __restrict__ g, uint16_t* __restrict__ planes,
+                                                         int H, int W, int S, long P, long ldp) {
+  const long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= P) return;
+  const int s = blockIdx.y;
+  const int Wf = W + S + 1, Hf = H + 2;
+  const int wo = q % Wf;
+  const long t = q / Wf;
+  const int ho = t % Hf;
+  const long n = t / Hf;
+  const int h = ho - 1, w = wo - 1 - s;
+  const float4 a = ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W) ? g[(n * H + h) * (long)W + w]
+                                                                            : make_float4(0.f, 0.f, 0.f, 0.f);
+  float v[4] = {a.x, a.y, a.z, a.w};
+  const long plane = (long)S * 4 * ldp;
+  uint16_t* dst = planes + (long)s * 4 * ldp + q;
+#pragma unroll
+  for (int pl = 0; pl < 3; ++pl) {
+    const uint32_t q0 = tap_bf16x2(v[0], v[1]), q1 = tap_bf16x2(v[2], v[3]);
+    dst[pl * plane] = (uint16_t)q0;
+    dst[pl * plane + ldp] = (uint16_t)(q0 >> 16);
+    dst[pl * plane + 2 * ldp] = (uint16_t)q1;
+    dst[pl * plane + 3 * ldp] = (uint16_t)(q1 >> 16);
+    if (pl < 2) {
+      v[0] -= __uint_as_float(q0 << 16);
+      v[1] -= __uint_as_float(q0 & 0xffff0000u);
+      v[2] -= __uint_as_float(q1 << 16);
+      v[3] -= __uint_as_float(q1 & 0xffff0000u);
+    }
+  }
+}
+
+// dw[co][ci][r][s] (+)= t[((s*4 + co)*Ci + ci)*R + r] (the R x 1 wgrad's [(s, co)][ci][r] result)
+__global__ void tap_wgrad_scatter_h_k(const float* __restrict__ t, float* __restrict__ dw, int Ci, int R, int S,
+                                      int accumulate, long total) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int s = i % S;
+  const long u = i / S;
+  const int r = u % R;
+  const long u2 = u / R;
+  const int ci = u2 % Ci;
+  const int co = u2 / Ci;
+  const float v = t[(((long)s * 4 + co) * Ci + ci) * R + r];
+  dw[i] = accumulate ? dw[i] + v : v;
+}
+
 __global__ void tap_wgrad_scatter_k(const float* __restrict__ t, float* __restrict__ dw, int Co, int Ci, int RS,
                                     int accumulate, long total) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -416,6 +467,23 @@ extern "C" int vst_tapfold_planes(const float* g, void* planes, long ldp, int N,
                      reinterpret_cast<const float4*>(g), reinterpret_cast<uint16_t*>(planes), H, W, R, S, pad,
                      pad_mode == VST_PAD_REFLECT, P, ldp);
   return check_launch("tapfold_planes");
+}
+
+extern "C" int vst_tapshift_planes(const float* g, void* planes, long ldp, int N, int H, int W, int S, void* stream) {
+  const long P = (long)N * (H + 2) * (W + S + 1);
+  VST_REQUIRE(g && planes && N > 0 && H > 0 && W > 0 && S > 0 && S <= 8 && ldp >= P, "tapshift_planes: bad args");
+  hipLaunchKernelGGL(tapshift_planes_k, dim3(ceil_div(P, 256), S), dim3(256), 0, (hipStream_t)stream,
+                     reinterpret_cast<const float4*>(g), reinterpret_cast<uint16_t*>(planes), H, W, S, P, ldp);
+  return check_launch("tapshift_planes");
+}
+
+extern "C" int vst_tap_wgrad_scatter_h(const float* t, float* dw, int Co, int Ci, int R, int S, int accumulate,
+                                       void* stream) {
+  VST_REQUIRE(t && dw && Co > 0 && Co <= 4 && Ci > 0 && R > 0 && S > 0, "tap_wgrad_scatter_h: bad args");
+  const long total = (long)Co * Ci * R * S;
+  hipLaunchKernelGGL(tap_wgrad_scatter_h_k, dim3(ceil_div(total, 256)), dim3(256), 0, (hipStream_t)stream, t, dw, Ci,
+                     R, S, accumulate, total);
+  return check_launch("tap_wgrad_scatter_h");
 }
 
 extern "C" int vst_tap_wgrad_scatter(const float* t, float* dw, int Co, int Ci, int R, int S, int accumulate,

@@ -315,6 +315,8 @@ TAP_LAST = os.environ.get("VST_TAP_CONV", "1") != "0"
 TAP_H = os.environ.get("VST_TAP_H", "1") != "0"
 # the image-input first layer's data gradient the same way (ops.tap_conv_dgrad_h); VST_TAP_HD=0: tap gather.
 TAP_HD = os.environ.get("VST_TAP_HD", "1") != "0"
+# ... and the last layer's weight gradient as the 7x1 conv's (ops.tap_conv_wgrad_h); VST_TAP_HW=0: tap fold.
+TAP_HW = os.environ.get("VST_TAP_HW", "1") != "0"
 # The up-sampling ConvTranspose2d (k3 s2 p1 op1) forward as four sub-pixel phase convs on the
 # split-bf16 forward kernel + an interleave (ops.convT3s2_fwd); VST_CONVT_PHASES=0 disables.
 CONVT_PHASES = os.environ.get("VST_CONVT_PHASES", "1") != "0"
@@ -560,9 +562,15 @@ class _GeneratorFn(torch.autograd.Function):
                 y = ops.conv2d_tfwd(a, ck, b, 2 * Hi, 2 * Wi, cpad(cout), 3, 3, 2, 1, role=role)
             s = ops.instnorm_stats(y)
             cp = None
-            if i == 1 and "ftap" in P and train_w and IN_XT:  # the tap wgrad's (1x1, pad 0) x image
+            if i == 1 and "ftap" in P:
+                # the last layer's weight gradient: the 7x1 conv's (x padded by 4, reflect) or the tap fold's
+                # (1x1, pad 0); decided here so the x image below matches the route the backward takes
+                sv["ftap_h"] = TAP_HW and ops.tap_conv_wgrad_h_ok(y, 7, 3, "reflect")
+            if i == 1 and "ftap" in P and train_w and IN_XT:
                 N_, H_, W_, C_ = y.shape
-                if _wgrad_on_bf(N_, H_, W_, C_, H_, W_, 4 * 49, 1, 1, ops.get_conv_math()):
+                if sv["ftap_h"]:
+                    cp = (4, "reflect", 1)
+                elif _wgrad_on_bf(N_, H_, W_, C_, H_, W_, 4 * 49, 1, 1, ops.get_conv_math()):
                     cp = (0, "zero", 1)
             an, at = in_act(y, s, "relu", cp)
             sv["xt"][id(an)] = at
@@ -633,7 +641,10 @@ class _GeneratorFn(torch.autograd.Function):
         g = ops.act_bwd(gout, out, "tanh")
         if "ftap" in P:
             if train_w:
-                ops.tap_conv_wgrad(a, g, f.weight.grad, 7, 3, "reflect", accumulate=True, x_t=xts.get(id(a)))
+                if sv.get("ftap_h"):
+                    ops.tap_conv_wgrad_h(a, g, f.weight.grad, 7, 3, "reflect", accumulate=True, x_t=xts.get(id(a)))
+                else:
+                    ops.tap_conv_wgrad(a, g, f.weight.grad, 7, 3, "reflect", accumulate=True, x_t=xts.get(id(a)))
                 if f.bias is not None:
                     ops.channel_sum(g, f.bias.grad, f.weight.shape[0], accumulate=True)
         else:

@@ -1083,6 +1083,34 @@ def tap_conv_wgrad(x, dy, dw, R, pad, pad_mode="zero", accumulate=True, role="bw
     _call("vst_tap_wgrad_scatter", _p(t), _p(dw), Co, Ci, R, R, 1 if accumulate else 0, _stream())
 
 
+def tap_conv_wgrad_h_ok(x, R, pad, pad_mode, role="bwd"):
+    """Does tap_conv_wgrad_h take this shape: a reflect 'same' conv whose R x 1 wgrad frame (W+R+1 wide)
+    runs on the x6 split-bf16 kernel without padded rows."""
+    N, H, W, Cx = x.shape
+    return (pad_mode == "reflect" and 2 * pad == R - 1 and pad + 1 < min(H, W) and
+            conv_plan_wgrad(N, H, W, Cx, H + 2, W + R + 1, 4 * R, R, 1, 1, role)[0] == 2)
+
+
+def tap_conv_wgrad_h(x, dy, dw, R, pad, pad_mode="reflect", accumulate=True, role="bwd", x_t=None):
+    """tap_conv_wgrad as the R x 1 conv's weight gradient (vst_tapshift_planes): dy's column-shifted copies
+    as 4R channels over the (H+2) x (W+R+1) frame, x padded by pad+1.  x_t: x's channel-major image padded
+    by pad+1, reflect (instnorm_act_fwd(cp=(pad + 1, "reflect", 1))), or None."""
+    _dev_check(x, dy, dw)
+    N, H, W, Cx = x.shape
+    Co, Ci = dw.shape[0], dw.shape[1]
+    K = 4 * R
+    Ho, Wo = H + 2, W + R + 1
+    ldp = lib().vst_cp_ld(N * Ho * Wo)
+    pl = torch.empty((3, K, ldp), device=x.device, dtype=torch.bfloat16)
+    _call("vst_tapshift_planes", _p(dy), _p(pl), ldp, N, H, W, R, _stream())
+    t = torch.empty((K, Ci, R), device=x.device)
+    nbytes = lib().vst_conv2d_wgrad_ws_bytes(N, H, W, Cx, Ho, Wo, K, R, 1, 1)
+    ws = torch.empty((nbytes + 3) // 4, device=x.device)
+    _call("vst_conv2d_wgrad_pre", _p(x), _p(x_t), _p(pl), _p(pl), _p(t), _p(ws), nbytes, N, H, W, Cx, Ho, Wo, K, R, 1,
+          1, pad + 1, PAD["reflect"], K, Ci, Ci * R, R, 0, _math(role), _stream())
+    _call("vst_tap_wgrad_scatter_h", _p(t), _p(dw), Co, Ci, R, R, 1 if accumulate else 0, _stream())
+
+
 def tap_conv_dgrad(dy, kc, R, pad, pad_mode="zero", role="bwd"):
     """Data gradient (NHWC4) of a 'same' conv with <= 4 input channels: kc = VST_PACK_KC pack
     [R][R][4][Cy] of its weight (see vst_tapgather)."""

@@ -444,6 +444,15 @@ int vst_tapsum_fwd(const float* z, int zcs, const float* bias, float* y, int N, 
 int vst_tapconv_h_fwd(const float* x, const float* wp, const void* wsplit, const float* bias, float* z, float* y,
                       int N, int H, int W, int Cx, int R, int pad, int pad_mode, int act, float slope, int math,
                       void* stream);
+/* The weight gradient of the same reflect 'same' conv as the R x 1 conv's: with padding pad+1 (reflect;
+ * the extra ring multiplies zero dy) its output frame is (H+2) x (W+S+1), and its dy channel (s, co)
+ * at (ho, wo) is g[ho-1][wo-1-s][co] — vst_tapshift_planes writes that as the x6 wgrad's bf16 planes
+ * [3][S*4][ldp] (ldp >= N (H+2) (W+S+1)); vst_conv2d_wgrad_pre(x, x_t padded by pad+1, planes,
+ * Cyp = 4S, R, S = 1, pad + 1, reflect, Co = 4S, so = Ci*R, si = R) gives t[(s*4+co)][ci][r], and
+ * vst_tap_wgrad_scatter_h writes dw[co][ci][r][s] (+)= t.  No R*S-fold of g: 4S channels instead of
+ * 4RS. */
+int vst_tapshift_planes(const float* g, void* planes, long ldp, int N, int H, int W, int S, void* stream);
+int vst_tap_wgrad_scatter_h(const float* t, float* dw, int Co, int Ci, int R, int S, int accumulate, void* stream);
 /* Adjoint gather of the weight gradient: d[q][(r*S+s)*4 + co] = sum_{p: src(p,r,s) = q} g[p][co]
  * (g NHWC4); then vst_conv2d_wgrad(x, d) as a 1x1 wgrad gives t[(r*S+s)*4 + co][ci], and
  * vst_tap_wgrad_scatter writes dw[co][ci][r][s] (+)= t (co < Co <= 4). */

@@ -343,6 +343,38 @@ def test_tap_conv(ops, conv_math, co, ci, k, mode):
     _close(dw.cpu() - 0.25, w.grad, tol=CONV_TOL[conv_math], what="tap wgrad")
 
 
+@pytest.mark.parametrize("N,ci,H,W,k,xt", [(2, 64, 12, 56, 7, False), (2, 64, 12, 56, 7, True), (3, 32, 9, 60, 3, True),
+                                          (2, 64, 256, 256, 7, True)])
+def test_tap_conv_wgrad_h(ops, N, ci, H, W, k, xt):
+    """Weight gradient of a reflect 'same' conv with <= 4 outputs as the k x 1 conv's (vst_tapshift_planes +
+    vst_conv2d_wgrad_pre with pad + 1 + vst_tap_wgrad_scatter_h), x6, against torch autograd and the tap-fold
+    route; x's padded channel-major image made by the wgrad or by the IN apply (cp=(pad + 1, reflect))."""
+    prev = ops.set_conv_math("bf16x6")
+    try:
+        co, pad = 3, (k - 1) // 2
+        x = _g(101, (N, ci, H, W))
+        w = (_g(102, (co, ci, k, k), 0.05)).requires_grad_(True)
+        y = F.conv2d(F.pad(x, (pad,) * 4, mode="reflect"), w)
+        gy = _g(103, tuple(y.shape))
+        y.backward(gy)
+        xn, g = _nhwc(x, ops), _nhwc(gy, ops)
+        assert ops.tap_conv_wgrad_h_ok(xn, k, pad, "reflect")
+        x_t = None
+        if xt:  # the IN apply's image of x itself: a = IN(z) with z chosen so that a == x (identity stats)
+            st = torch.zeros((N, xn.shape[-1], 2), device=DEV)
+            st[..., 1] = 1.0
+            a, x_t = ops.instnorm_act_fwd(xn, st, "none", cp=(pad + 1, "reflect", 1))
+            assert torch.equal(a, xn)
+        dw = torch.full((co, ci, k, k), 0.25, device=DEV)
+        ops.tap_conv_wgrad_h(xn, g, dw, k, pad, "reflect", accumulate=True, x_t=x_t)
+        _close(dw.cpu() - 0.25, w.grad, tol=CONV_TOL["bf16x6"], what="tap wgrad (k x 1 form)")
+        dw0 = torch.zeros((co, ci, k, k), device=DEV)
+        ops.tap_conv_wgrad(xn, g, dw0, k, pad, "reflect", accumulate=False)
+        _close(dw.cpu() - 0.25, dw0.cpu(), tol=CONV_TOL["bf16x6"], what="vs tap fold")
+    finally:
+        ops.set_conv_math(prev)
+
+
 def test_tap_conv_fwd_h_production(ops, conv_math):
     """The generator's last layer (64 -> 3, 7x7 reflect, tanh) at 256x256 through vst_tapconv_h_fwd vs torch
     fp32 and vs the 1x1-conv + full tap-sum route; the SOK pack built by a PackBatch equals the direct one."""

@@ -562,14 +562,16 @@ __global__ __launch_bounds__((Tile<BM, BN, WM, WN>::NT), 2) void conv_wgrad_k(
 // (strides so / si).  A block owns 32 (rs, ci) rows x 64 channels: 2 rows per thread with 8 slabs'
 // loads per round trip (16 float4 in flight per thread, ~1100 waves for a ResnetBlock weight), then a
 // 32 x 64 LDS transpose for the [co]-major store.  grid (ceil(Ci*RS / 32), ceil(Cyp / 64)).
+// NR: rows per thread (block = 16 NR rows x 64 columns)
+template <int NR>
 __global__ __launch_bounds__(256) void wgrad_reduce_store_k(const float* __restrict__ S, float* __restrict__ dw,
                                                             int Cx, int Cyp, int RS, int Co, int Ci, long so,
                                                             long si, int accumulate, int nsplit, long zs) {
-  __shared__ float tile[32][65];
-  const int m0 = blockIdx.x * 32, c0 = blockIdx.y * 64;
+  constexpr int RB = 16 * NR, UZ = 8;
+  __shared__ float tile[RB][65];
+  const int m0 = blockIdx.x * RB, c0 = blockIdx.y * 64;
   const int t = threadIdx.x, c4 = (t & 15) * 4, r0 = t >> 4;
   const int Md = Ci * RS;
-  constexpr int NR = 2, UZ = 8;
   float4 acc[NR];
   const float* src[NR];
   bool ok[NR];
@@ -611,8 +613,8 @@ __global__ __launch_bounds__(256) void wgrad_reduce_store_k(const float* __restr
     tile[r][c4 + 3] = acc[i].w;
   }
   __syncthreads();
-  const int tx = t & 31, ty = t >> 5;
-  for (int r = ty; r < 64; r += 8) {
+  const int tx = t % RB, ty = t / RB;
+  for (int r = ty; r < 64; r += 256 / RB) {
     const int c = c0 + r, md = m0 + tx;
     if (c >= Co || md >= Md) continue;
     const int ci = md / RS, rs = md - ci * RS;
@@ -841,6 +843,13 @@ using namespace vst;
 
 // 4-channel inputs (images) on the split-bf16 kernels (conv_fprop_bf_k<.., false, 3>) rather than
 // the fp32 [row][k] kernels; VST_BF_C4=0 restores the latter.
+// wgrad_reduce_store_k on 16-row blocks (VST_WG_RED16=0: 32-row): twice the blocks for the same slabs,
+// -0.16 ms/step in the same-box A/B (profiles/r03d_wgred_step_ab.jsonl)
+static const bool g_wg_red16 = [] {
+  const char* e = getenv("VST_WG_RED16");
+  return !(e && e[0] == '0');
+}();
+
 static const bool g_bf_c4 = [] {
   const char* e = getenv("VST_BF_C4");
   return !(e && e[0] == '0');
@@ -1161,8 +1170,12 @@ extern "C" int vst_conv2d_wgrad_pre(const float* x, const float* x_t, const floa
                        p.nsplit, WG_GROUP);
     red = l2;
   }
-  hipLaunchKernelGGL(wgrad_reduce_store_k, dim3(ceil_div(Ci * R * S, 32), ceil_div(Co, 64)), dim3(256), 0, s,
-                     red, dw, Cx, Cyp, R * S, Co, Ci, so, si, accumulate, nred, slab);
+  if (g_wg_red16)  // 16-row blocks: twice the blocks (the 2304 x 256 ResnetBlock gradient: 288 -> 576)
+    hipLaunchKernelGGL(wgrad_reduce_store_k<1>, dim3(ceil_div(Ci * R * S, 16), ceil_div(Co, 64)), dim3(256), 0, s,
+                       red, dw, Cx, Cyp, R * S, Co, Ci, so, si, accumulate, nred, slab);
+  else
+    hipLaunchKernelGGL(wgrad_reduce_store_k<2>, dim3(ceil_div(Ci * R * S, 32), ceil_div(Co, 64)), dim3(256), 0, s,
+                       red, dw, Cx, Cyp, R * S, Co, Ci, so, si, accumulate, nred, slab);
   return check_launch("conv2d_wgrad_reduce");
 }
 

@@ -116,6 +116,7 @@ SIGNATURES = {
     "vst_tap_wgrad_scatter_h": (I, [P, P, I, I, I, I, I, P]),
     "vst_conv2d_fwd_phase": (I, [P, P, P, P, I, I, I, I, I, I, I, I, F, I, P]),
     "vst_conv2d_convT_s2": (I, [P, P, P, P, P, P, P, I, I, I, I, I, I, F, I, P]),
+    "vst_conv4s2_dgrad": (I, [P, P, P, P, P, P, I, I, I, I, I, I, P]),
     "vst_raft_prep": (I, [P, P, I, I, I, I, I, I, I, P]),
     "vst_tapsum_fwd": (I, [P, I, P, P, I, I, I, I, I, I, I, I, F, P]),
     "vst_tapfold": (I, [P, P, I, I, I, I, I, I, I, P]),

@@ -145,7 +145,7 @@ long rk_cp_ld(long P);
 // split-operand bf16 implicit GEMM (conv_bf.hip); wsplit = vst_weight_split planes, stride wps
 bool bf_convT_phases_ok(int C, int Cop, int math);
 int bf_convT_phases_launch(const float* x, const void* const ws[4], const float* bias, float* y, int N, int H, int W,
-                           int C, int Cop, int act, float slope, int math, hipStream_t s);
+                           int C, int Cop, int act, float slope, int math, hipStream_t s, int full = 0);
 int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* bias, float* y, int N,
                     int H, int W, int C, int Ho, int Wo, int Cop, int R, int S, int st, int padh, int padw,
                     int reflect, int act, float slope, int math, int kind, hipStream_t s,

@@ -1016,6 +1016,19 @@ extern "C" int vst_conv2d_convT_s2(const float* x, const void* ws00, const void*
   return bf_convT_phases_launch(x, ws, bias, y, N, H, W, Cx, Cop, act, slope, math, (hipStream_t)stream);
 }
 
+extern "C" int vst_conv4s2_dgrad(const float* dy, const void* ws00, const void* ws01, const void* ws10,
+                                 const void* ws11, float* dx, int N, int Hd, int Wd, int Cy, int Cop, int math,
+                                 void* stream) {
+  VST_REQUIRE(dy && ws00 && ws01 && ws10 && ws11 && dx && N > 0 && Hd > 0 && Wd > 0, "conv4s2_dgrad: bad args");
+  if (!bf_convT_phases_ok(Cy, Cop, math)) {
+    ::vst::set_error("conv4s2_dgrad: needs split-bf16 math, Cy %% 32 == 0, Cop %% 4 == 0");
+    return VST_EUNSUPPORTED;
+  }
+  const void* ws[4] = {ws00, ws01, ws10, ws11};
+  return bf_convT_phases_launch(dy, ws, nullptr, dx, N, Hd, Wd, Cy, Cop, VST_ACT_NONE, 0.f, math, (hipStream_t)stream,
+                                1);
+}
+
 extern "C" int vst_conv2d_tfwd(const float* in, const float* wp, const float* bias,
                                const float* addend, float* out, int N, int Hi, int Wi, int Cy,
                                int Ho, int Wo, int Cx, int R, int S, int stride, int pad,

@@ -652,12 +652,17 @@ __global__ __launch_bounds__(256) void dgrad_border5_add_k(const float* __restri
 // oph - 1 = 2a + b is an (H+a) x (W+b) conv whose pixel (ph, pw) is output pixel (2(ph-a)+a,
 // 2(pw-b)+b) of the 2H x 2W result, its first row (a = 1) / column (b = 1) unused.  With oph > 0 the
 // forward kernel stores each row there directly: -1 = the unused row / column (not stored).
+// oph 5..8 (oph - 5 = 2a + b): the data gradient of Conv2d(k4, s2, p1) (vst_conv4s2_dgrad): every
+// phase is an (H+1) x (W+1) conv with the same map, its row H / column W (a = 0, b = 0) or its first
+// row / column (a = 1, b = 1) unused.
 __device__ __forceinline__ int phase_row(int mm, int oph, int Ho, int Wo) {
-  const int a = (oph - 1) >> 1, b = (oph - 1) & 1;
+  const bool full = oph > 4;
+  const int q = full ? oph - 5 : oph - 1, a = q >> 1, b = q & 1;
   const int hw = Ho * Wo, n = mm / hw, rem = mm - n * hw, ph = rem / Wo, pw = rem - ph * Wo;
-  if ((a && ph == 0) || (b && pw == 0)) return -1;
-  const int H = Ho - a, W = Wo - b;
-  return (n * 2 * H + 2 * (ph - a) + a) * 2 * W + 2 * (pw - b) + b;
+  const int H = full ? Ho - 1 : Ho - a, W = full ? Wo - 1 : Wo - b;
+  const int i = ph - a, j = pw - b;
+  if (i < 0 || j < 0 || i >= H || j >= W) return -1;
+  return (n * 2 * H + 2 * i + a) * 2 * W + 2 * j + b;
 }
 
 // ------------------------------------------------------------------------------------------ fprop
@@ -1041,22 +1046,26 @@ struct PhaseJobs {
   int t0[5];            // job j's blocks [t0[j], t0[j] + tiles_j), t0[j] % 8 == 0; t0[4] = grid
 };
 
+// full: the four 2x2 pad-1 phase convs of a Conv2d(k4, s2, p1) data gradient (oph 5..8, (H+1) x (W+1) each)
 template <class T>
 __global__ __launch_bounds__(T::NT, T::MINB) void conv_convT_phases_k(const float* __restrict__ x, PhaseJobs jobs,
                                                                       const float* __restrict__ bias,
                                                                       float* __restrict__ y, int N, int H, int W,
-                                                                      int C, int Cop, int act, float slope) {
+                                                                      int C, int Cop, int act, float slope,
+                                                                      int full) {
   const int bid = blockIdx.x;
   const int j = bid < jobs.t0[1] ? 0 : (bid < jobs.t0[2] ? 1 : (bid < jobs.t0[3] ? 2 : 3));
   const int ph = j == 0 ? 3 : (j == 1 ? 1 : (j == 2 ? 2 : 0));
   const int a = ph >> 1, b = ph & 1;
   const int t0 = j == 0 ? jobs.t0[0] : (j == 1 ? jobs.t0[1] : (j == 2 ? jobs.t0[2] : jobs.t0[3]));
   const __bf16* ws = j == 0 ? jobs.ws[0] : (j == 1 ? jobs.ws[1] : (j == 2 ? jobs.ws[2] : jobs.ws[3]));
-  const int Ho = H + a, Wo = W + b, M = N * Ho * Wo, K = (1 + a) * (1 + b) * C;
+  const int R = full ? 2 : 1 + a, S = full ? 2 : 1 + b, pah = full ? 1 : a, paw = full ? 1 : b;
+  const int Ho = H + (full ? 1 : a), Wo = W + (full ? 1 : b), M = N * Ho * Wo, K = R * S * C;
   const int tiles = (M + T::BM - 1) / T::BM * ((Cop + T::BN - 1) / T::BN);
   if (bid - t0 >= tiles) return;  // the job's padding to a multiple of 8 blocks
-  conv_fprop_bf_body<T, true, 0, false>(bid - t0, x, ws, (long)Cop * K, bias, y, H, W, C, Ho, Wo, Cop, 1 + b, 1, a,
-                                        b, 0, act, slope, M, K, 0, nullptr, 0, nullptr, nullptr, 1 + 2 * a + b);
+  conv_fprop_bf_body<T, true, 0, false>(bid - t0, x, ws, (long)Cop * K, bias, y, H, W, C, Ho, Wo, Cop, S, 1, pah,
+                                        paw, 0, act, slope, M, K, 0, nullptr, 0, nullptr, nullptr,
+                                        (full ? 5 : 1) + 2 * a + b);
 }
 
 // -------------------------------------------------------------------------- weight gradient
@@ -1734,7 +1743,7 @@ bool bf_convT_phases_ok(int C, int Cop, int math) {
 }
 
 int bf_convT_phases_launch(const float* x, const void* const ws[4], const float* bias, float* y, int N, int H, int W,
-                           int C, int Cop, int act, float slope, int math, hipStream_t s) {
+                           int C, int Cop, int act, float slope, int math, hipStream_t s, int full) {
   VST_REQUIRE(bf_convT_phases_ok(C, Cop, math), "convT phases: unsupported shape / arithmetic");
   const int bm = 128, bn = Cop <= 64 ? 64 : 128;
   bf::PhaseJobs jobs;
@@ -1743,7 +1752,8 @@ int bf_convT_phases_launch(const float* x, const void* const ws[4], const float*
     const int ph = j == 0 ? 3 : (j == 1 ? 1 : (j == 2 ? 2 : 0)), a = ph >> 1, b = ph & 1;
     jobs.ws[j] = reinterpret_cast<const __bf16*>(ws[ph]);
     jobs.t0[j] = t;
-    const long tiles = ((long)N * (H + a) * (W + b) + bm - 1) / bm * ((Cop + bn - 1) / bn);
+    const long rows = (long)N * (H + (full ? 1 : a)) * (W + (full ? 1 : b));
+    const long tiles = (rows + bm - 1) / bm * ((Cop + bn - 1) / bn);
     t += (int)((tiles + 7) / 8 * 8);
   }
   jobs.t0[4] = t;
@@ -1751,7 +1761,7 @@ int bf_convT_phases_launch(const float* x, const void* const ws[4], const float*
   {                                                                                                        \
     using T = bf::Tile<128, BN_, 64, WN_, 32, NP_>;                                                        \
     hipLaunchKernelGGL(bf::conv_convT_phases_k<T>, dim3(t), dim3(T::NT), 0, s, x, jobs, bias, y, N, H, W, C, Cop, \
-                       act, slope);                                                                        \
+                       act, slope, full);                                                                  \
   }
   if (math == VST_MATH_BF16X6) {
     if (bn == 64) VST_CT(64, 32, 3) else VST_CT(128, 32, 3)

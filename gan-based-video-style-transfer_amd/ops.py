@@ -1188,11 +1188,23 @@ def conv4s2_dgrad_phase_packs(w):
     return packs
 
 
+# the four phases in one launch stored interleaved (vst_conv4s2_dgrad); VST_C4S2_GROUPED=0: images + interleave
+C4S2_GROUPED = os.environ.get("VST_C4S2_GROUPED", "1") != "0"
+
+
 def conv4s2_dgrad(dy, packs, cop, role="bwd"):
     """Data gradient of Conv2d(k=4, s=2, p=1) onto a (2*Hd) x (2*Wd) input via four 2x2 phase convs
     (padding 1, outputs (Hd+1) x (Wd+1)) + vst_interleave_phases_full."""
     _dev_check(dy)
-    N, Hd, Wd, _ = dy.shape
+    N, Hd, Wd, Cy = dy.shape
+    m = _math(role)
+    if C4S2_GROUPED and m != _lib.MATH_MODES["fp32"] and Cy % 32 == 0 and cop != 4 and \
+            all(getattr(wp, "vst_split", None) is not None for wp in packs):
+        # one launch, stored straight into the interleaved gradient (vst_conv4s2_dgrad)
+        y = torch.empty((N, 2 * Hd, 2 * Wd, cop), device=dy.device)
+        _call("vst_conv4s2_dgrad", _p(dy), *[_p(wp.vst_split) for wp in packs], _p(y), N, Hd, Wd, Cy, cop, m,
+              _stream())
+        return y
     outs = [conv2d_fwd(dy, wp, None, cop, 2, 2, 1, 1, "zero", role=role) for wp in packs]
     y = torch.empty((N, 2 * Hd, 2 * Wd, cop), device=dy.device)
     _call("vst_interleave_phases_full", _p(outs[0]), _p(outs[1]), _p(outs[2]), _p(outs[3]), _p(y), N, Hd, Wd,

@@ -493,6 +493,12 @@ int vst_conv2d_fwd_phase(const float* x, const void* wsplit, const float* bias, 
 int vst_conv2d_convT_s2(const float* x, const void* ws00, const void* ws01, const void* ws10, const void* ws11,
                         const float* bias, float* y, int N, int H, int W, int Cx, int Cop, int act, float slope,
                         int math, void* stream);
+/* Data gradient of Conv2d(k4, s2, p1) (PatchGAN networks.py:556-578) in ONE launch: the four 2x2 pad-1
+ * phase convs of dy [N][Hd][Wd][Cy] (ws_ab = the bf16 planes of conv4s2 phase pack (a, b)) stored straight
+ * into dx [N][2Hd][2Wd][Cop] (dx[2i+a][2j+b] = P_ab[i+a][j+b]); replaces four phase images +
+ * vst_interleave_phases_full.  Cy % 32 == 0, Cop % 4 == 0, split-bf16 math (else VST_EUNSUPPORTED). */
+int vst_conv4s2_dgrad(const float* dy, const void* ws00, const void* ws01, const void* ws10, const void* ws11,
+                      float* dx, int N, int Hd, int Wd, int Cy, int Cop, int math, void* stream);
 
 /* ---- RAFT inference (SURVEY §8 A19 + §8f rank 3) ------------------------------------------ */
 /* Forward conv with separate row / column zero padding (SepConvGRU's (1,5) / (5,1) kernels with

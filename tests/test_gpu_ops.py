@@ -523,7 +523,8 @@ def test_conv_fwd_in_stats(ops, case, conv_math):
     assert rel < 1e-6, rel
 
 
-@pytest.mark.parametrize("ci,co,h,w", [(64, 128, 16, 20), (128, 256, 8, 8), (4, 64, 32, 32)])
+@pytest.mark.parametrize("ci,co,h,w", [(64, 128, 16, 20), (128, 256, 8, 8), (4, 64, 32, 32), (64, 128, 64, 64),
+                                        (128, 256, 32, 32)])  # the last two: D's layers 2 / 3 at 256^2
 @pytest.mark.parametrize("batched", [False, True], ids=["single", "packbatch"])
 def test_conv4s2_dgrad_phases(ops, conv_math, ci, co, h, w, batched):
     """Data gradient of the PatchGAN Conv2d(k4, s2, p1) as four 2x2 phase convs + interleave vs
@@ -539,6 +540,14 @@ def test_conv4s2_dgrad_phases(ops, conv_math, ci, co, h, w, batched):
         packs = ops.conv4s2_dgrad_phase_packs(wd.to(DEV))
     g = ops.conv4s2_dgrad(_nhwc(dy, ops), packs, ops.cpad(ci))
     _close(_nchw(g, ci, ops), ref, tol=CONV_TOL[conv_math], what="conv4s2 dgrad phases")
+    # the one-launch route (vst_conv4s2_dgrad, split-bf16, Cy % 32 == 0) vs four phase images + interleave
+    prev, ops.C4S2_GROUPED = ops.C4S2_GROUPED, False
+    try:
+        g_il = ops.conv4s2_dgrad(_nhwc(dy, ops), packs, ops.cpad(ci))
+    finally:
+        ops.C4S2_GROUPED = prev
+    # (other tiles than the per-phase launches pick: another K-accumulation order, fp32-rounding apart)
+    _close(g, g_il, tol=CONV_TOL[conv_math], what="one launch vs phase images + interleave")
 
 
 def test_convT3s2_phase_packs_batched_equal_single(ops):

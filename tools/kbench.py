@@ -1,5 +1,6 @@
 """Developer: launch one conv family on the ResnetBlock shape (B=4, 64x64x256, 3x3 reflect) a few
-times (batch KB_B, default 8) — the target of rocprofv3 --pmc passes.  usage: kbench.py fprop|dgrad|tconv|wgrad|warp|c0 [reps]
+times (batch KB_B, default 8) — the target of rocprofv3 --pmc passes.  usage: kbench.py fprop|dgrad|tconv|wgrad|wgrad_pre|warp|c0 [reps]
+(wgrad_pre: the weight gradient as the train step runs it, on the IN passes' premade x image / dy planes)
 warp: vst_warp_fwd on bench.py's warp_roofline shape (N=32, C=64, 436x1024, its smooth flow; KB_FLOW=iid:
 the i.i.d. worst case).  c0: the generator's first conv (conv_c4_direct_k) at N=KB_B, 256x256."""
 import os
@@ -48,6 +49,12 @@ kc, ck = ops.weight_pack(w, ops.PACK_FWD), ops.weight_pack(w, ops.PACK_DGRAD)
 ikf = ops.weight_pack(w, ops.PACK_IKF)
 gy = torch.randn(B, H, H, C, device=dev)
 dw = torch.zeros(C, C, 3, 3, device=dev)
+if which == "wgrad_pre":  # the step's form: x's padded image and dy's planes made by their producers
+    st = torch.zeros((B, C, 2), device=dev)
+    st[..., 1] = 1.0
+    _, x_t = ops.instnorm_act_fwd(x, st, "none", cp=(1, "reflect", 1))
+    gy, dy_planes = ops.instnorm_act_bwd(gy, x, st, "none", planes=True)
+    torch.cuda.synchronize()
 for _ in range(reps):
     if which == "fprop":
         ops.conv2d_fwd(x, kc, None, C, 3, 3, 1, 1, "reflect")
@@ -55,6 +62,8 @@ for _ in range(reps):
         ops.conv2d_dgrad_s1(gy, ikf, H, H, C, 3, 1, "reflect")
     elif which == "tconv":
         ops.conv2d_tfwd(gy, ck, None, H, H, C, 3, 3, 1, 1, pad_mode="reflect")
+    elif which == "wgrad_pre":
+        ops.conv2d_wgrad(x, gy, dw, None, 3, 3, 1, 1, "reflect", C, C, C * 9, 9, dy_planes=dy_planes, x_t=x_t)
     else:
         ops.conv2d_wgrad(x, gy, dw, None, 3, 3, 1, 1, "reflect", C, C, C * 9, 9)
 torch.cuda.synchronize()

@@ -627,13 +627,52 @@ def workload_c5(args, world, rank, local, device):
                  args, el / args.steps * 1e3, cfg, args.math)
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(n):
+    """`bench.py --gpus N` run directly: N ranks as child processes of a torchrun on this node (the
+    reference scales with nn.DataParallel over gpu_ids, CycleGAN/models/networks.py:111-116; here it is
+    one process per GPU), each re-running this script with the same arguments.  The parent makes no
+    GPU call; it returns the launcher's exit status."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % n,
+           "--master-addr=127.0.0.1", "--master-port=%d" % free_port(), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # RCCL on this host: dmabuf IPC only
+    return subprocess.call(cmd, env=env)
+
+
+def workload_dpcheck(args, world, rank, local):
+    """The launcher check: every rank joins the process group (gloo: no GPU is touched), all-reduces
+    its rank + 1, and rank 0 prints the group's size and the sum."""
+    if world > 1:
+        dist.init_process_group("gloo")
+        world = dist.get_world_size()
+        assert world == args.gpus, (world, args.gpus)
+    t = torch.tensor([rank + 1.0])
+    if world > 1:
+        dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"metric": "dpcheck", "n_gpus": world, "rank_sum": t.item(),
+                          "expected": world * (world + 1) / 2}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", choices=["c2", "c4", "c5"], default="c2",
-                    help="c2 (default, the BASELINE metric): CycleGANCon step; c4: StarGAN DP; c5: MoGAN DP")
+    ap.add_argument("--workload", choices=["c2", "c4", "c5", "dpcheck"], default="c2",
+                    help="c2 (default, the BASELINE metric): CycleGANCon step; c4: StarGAN DP; c5: MoGAN DP; "
+                         "dpcheck: the launcher's rank check alone (no GPU work)")
     ap.add_argument("--batch", type=int, default=None,
                     help="per-GPU batch (c2: 4 frame pairs, c4: 4 images, c5: 1 frame pair)")
     ap.add_argument("--size", type=int, default=256)
@@ -644,14 +683,24 @@ def main():
     ap.add_argument("--no-extras", action="store_true")
     args = ap.parse_args()
     if args.batch is None:
-        args.batch = {"c2": 4, "c4": 4, "c5": 1}[args.workload]
+        args.batch = {"c2": 4, "c4": 4, "c5": 1, "dpcheck": 1}[args.workload]
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # --gpus N without an outer launcher: start the N ranks here, one process per GPU, before
+        # this process touches the GPU (it never does: it only waits for its children)
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but the launcher started WORLD_SIZE=%d ranks" % (args.gpus, world))
+    if args.workload == "dpcheck":
+        return workload_dpcheck(args, world, rank, local)
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        world = dist.get_world_size()           # n_gpus is the process group's size
+        assert world == args.gpus, (world, args.gpus)
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
 

@@ -101,6 +101,9 @@ def _pmc_traffic(name, key):
         return None
     if not rec or any(rec.get("key", {}).get(k) != v for k, v in key.items()):
         return None
+    from gbvst import _lib
+    if rec.get("source_stamp") != _lib.source_stamp():   # taken on other kernel code or knobs
+        return None
     return rec.get("hbm_bytes_per_launch")
 
 

@@ -23,6 +23,24 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
 _lib = None
+
+
+def source_stamp():
+    """Short hash of the kernel sources (csrc/* + include/vst_hip.h) plus the VST_* environment knobs
+    that change what the kernels do: profiling records carry it, and a record whose stamp differs from
+    the running code's is not used for its numbers."""
+    import hashlib
+    h = hashlib.sha1()
+    for f in sorted(glob.glob(os.path.join(CSRC, "*"))) + [os.path.join(REPO, "include", "vst_hip.h")]:
+        if f.endswith((".hip", ".h")):
+            h.update(os.path.basename(f).encode())
+            h.update(open(f, "rb").read())
+    knobs = sorted((k, v) for k, v in os.environ.items()
+                   if k.startswith("VST_") and k not in ("VST_CONV_MATH", "VST_LIB_VARIANT"))
+    h.update(repr(knobs).encode())
+    return h.hexdigest()[:12]
+
+
 MATH_MODES = {"fp32": 0, "bf16x3": 1, "bf16x6": 2}  # VST_MATH_* (include/vst_hip.h)
 
 P = ctypes.c_void_p

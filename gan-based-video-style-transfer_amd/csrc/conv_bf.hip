@@ -1546,6 +1546,9 @@ int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* b
                     int reflect, int act, float slope, int math, int kind, hipStream_t s, double* part,
                     float* tws, size_t tws_floats, const float* addend, int oph) {
   if (oph) tws = nullptr;  // phase stores: no split-K slabs (their reduce stores unmapped)
+  // the epilogue routes differ on whether an addend enters the IN partials (the per-element store
+  // counts it, the LDS-staged one adds it at the row store): no caller needs both, so refuse it
+  VST_REQUIRE(!(part && addend), "conv fprop: IN partials together with an addend are not supported");
   const int M = N * Ho * Wo, K = R * S * C;
   // 4-channel inputs with 64 outputs (the generator's 7x7 image convs): the direct patch-staged kernel
   if (kind < 0 && padh == padw && !addend && !oph && c4_direct_ok(C, Cop, R, S, st, Ho, Wo, math))

@@ -23,6 +23,18 @@ from . import ops, perceptual
 from .cycle_gan_model import CycleGANModel
 
 CONTENT_LEVEL = 3  # relu4_1
+SEEDED_LAMBDA = (100.0, 500.0)       # (content, style) for the seeded kaiming fan_out VGG-19
+PRETRAINED_LAMBDA = (1.0, 0.01)      # for real (or fan_in-scale) VGG-19 weights
+
+
+def resolve_loss_weights(opt):
+    """Fill unset lambda_content / lambda_style from the VGG weight source (seeded or --vgg_weights)."""
+    d = PRETRAINED_LAMBDA if getattr(opt, 'vgg_weights', '') else SEEDED_LAMBDA
+    if getattr(opt, 'lambda_content', None) is None:
+        opt.lambda_content = d[0]
+    if getattr(opt, 'lambda_style', None) is None:
+        opt.lambda_style = d[1]
+    return opt
 
 
 class CycleGANVGGModel(CycleGANModel):
@@ -36,15 +48,26 @@ class CycleGANVGGModel(CycleGANModel):
             # O(0.1-1) beside the cycle losses (~4) at any frame size (the Grams are 1/(h*w)
             # normalised).  The reduced-size golden (tests/golden/c3_small.npz) was composed with
             # lambda_content 1, lambda_style 0.01 on a fan_in-initialised VGG whose Grams are ~1e4x larger.
-            parser.add_argument('--lambda_content', type=float, default=100.0, help='VGG-19 relu4_1 content weight')
-            parser.add_argument('--lambda_style', type=float, default=500.0, help='VGG-19 Gram style weight')
+            # Real (pretrained) weights have Grams of that larger order too, so --vgg_weights switches
+            # the defaults to 1 / 0.01; explicit values always win.
+            parser.add_argument('--lambda_content', type=float, default=None,
+                                help='VGG-19 relu4_1 content weight (default 100 seeded VGG, 1 with --vgg_weights)')
+            parser.add_argument('--lambda_style', type=float, default=None,
+                                help='VGG-19 Gram style weight (default 500 seeded VGG, 0.01 with --vgg_weights)')
             parser.add_argument('--vgg_seed', type=int, default=0, help='seed of the (non-pretrained) VGG-19')
+            parser.add_argument('--vgg_weights', type=str, default='',
+                                help='torchvision vgg19 state_dict (.pth, loaded weights_only) or its features')
         return parser
 
     def __init__(self, opt):
         super().__init__(opt)
         self.loss_names = self.loss_names + ['G_C', 'G_S']
         self.netVGG = perceptual.Vgg19(seed=getattr(opt, 'vgg_seed', 0)).to(self.device)
+        path = getattr(opt, 'vgg_weights', '')
+        if path:
+            sd = torch.load(path, map_location='cpu', weights_only=True)
+            self.netVGG.load_torchvision_features(sd)
+        resolve_loss_weights(opt)
         mean, std = perceptual._mean_std(self.device)
         self._vgg_mean, self._vgg_std = (mean - 0.5).contiguous(), std
 

@@ -1143,9 +1143,11 @@ def tap_conv_dgrad_h(dy, sokd, R, pad, pad_mode="zero", role="bwd"):
     correlation of dy with the rotated taps (sokd = dgrad_sok_pack(w); zero pad R-1), then the reflect fold
     (reflect padding) or the interior crop (zero padding)."""
     _dev_check(dy, sokd)
+    if pad_mode == "reflect" and pad != (R - 1) // 2:
+        raise NotImplementedError("tap_conv_dgrad_h: reflect padding %d with R=%d (only 'same', (R-1)/2)" % (pad, R))
     full = tap_conv_fwd_h(dy, sokd, None, R, R - 1, "zero", role=role)
     if pad_mode == "reflect":
-        return reflect_fold(full, pad) if pad == (R - 1) // 2 else None
+        return reflect_fold(full, pad)
     o = R - 1 - pad
     return full[:, o:full.shape[1] - o, o:full.shape[2] - o].contiguous()
 

@@ -218,7 +218,8 @@ void vst_debug_set_tiles(int fprop, int tconv, int wgrad);
  * this shape and `math` on this thread.  *kind = split-arithmetic tile kind (0..8, see
  * vst_debug_set_tiles; 7 = 256x128), VST_PLAN_RK (fp32 [row][k] kernel), VST_PLAN_SKINNY
  * (<= 4 output channels, VALU) or VST_PLAN_C4_DIRECT (4 input channels, 64 outputs, stride 1,
- * R, S <= 8: the patch-staged direct kernel, conv_c4.hip); *m_split = first output-pixel row of the wave-quantisation tail
+ * R == 7, S <= 8, split-bf16 math (bf16x6 / bf16x3), Wo <= 256 or a multiple of 256, and Wo a multiple
+ * of 32 unless Ho*Wo is not: the patch-staged direct kernel, conv_c4.hip); *m_split = first output-pixel row of the wave-quantisation tail
  * launch, 0 when the grid runs as one launch; *tail_kind = that tail launch's tile kind (-1: none). */
 enum { VST_PLAN_RK = -1, VST_PLAN_SKINNY = -2, VST_PLAN_C4_DIRECT = -3 };
 int vst_conv_plan_fwd(int N, int H, int W, int Cx, int Cop, int R, int S, int stride, int pad_h,

@@ -113,3 +113,17 @@ def test_dp_hook_reaches_every_phase():
     f = _FakeModel()
     T._optimize(f, hook)
     assert f.step == 1
+
+
+def test_c3_loss_weight_defaults_follow_vgg_source():
+    """C3's VGG loss weights: 100 / 500 for the seeded VGG-19, 1 / 0.01 with --vgg_weights (real VGG
+    Grams are ~1e4x larger), explicit values kept."""
+    from gbvst.cycle_gan_vgg_model import resolve_loss_weights
+    from gbvst.options import parse_options
+    o = resolve_loss_weights(parse_options(["--model", "cycle_gan_vgg"], True))
+    assert (o.lambda_content, o.lambda_style) == (100.0, 500.0)
+    o = resolve_loss_weights(parse_options(["--model", "cycle_gan_vgg", "--vgg_weights", "v.pth"], True))
+    assert (o.lambda_content, o.lambda_style) == (1.0, 0.01)
+    o = resolve_loss_weights(parse_options(["--model", "cycle_gan_vgg", "--vgg_weights", "v.pth",
+                                            "--lambda_style", "3"], True))
+    assert (o.lambda_content, o.lambda_style) == (1.0, 3.0)

@@ -84,7 +84,8 @@ def main():
             key.update(tile=kind, m_split=ms, ksplit=ks)
             if op == "dgrad":
                 key["op"] = "dgrad_refl"  # bench.py's dgrad key
-        res[name] = {"key": key, "dispatches_per_call": len(fetch) / reps, "fetch_bytes": fb, "write_bytes": wb,
+        from gbvst import _lib as _L
+        res[name] = {"key": key, "source_stamp": _L.source_stamp(), "dispatches_per_call": len(fetch) / reps, "fetch_bytes": fb, "write_bytes": wb,
                      "hbm_bytes_per_launch": fb + wb, "algorithmic_bytes": alg,
                      "main_kernel_avg_us": round(sum(t) / len(t), 2) if t else None,
                      "note": "FETCH_SIZE x2 (gfx950 wide-read correction) + WRITE_SIZE, summed over the op's dispatches"}

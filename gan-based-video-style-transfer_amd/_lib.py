@@ -103,6 +103,8 @@ SIGNATURES = {
     # learning-based style path / RAFT correlation (style.hip, norm.hip, flow.hip)
     "vst_warp_masked_fwd": (I, [P, P, P, I, I, I, I, I, P]),
     "vst_warp_masked_bwd_input": (I, [P, P, P, I, I, I, I, I, P]),
+    "vst_warp_bwd_det_ws_bytes": (SZ, [I, I, I]),
+    "vst_warp_bwd_input_det": (I, [P, P, P, P, SZ, I, I, I, I, I, I, I, I, P]),
     "vst_instnorm_affine_fwd": (I, [P, P, P, P, P, F, P, P, I, I, I, I, F, P]),
     "vst_instnorm_affine_ws_bytes": (SZ, [I, I, I]),
     "vst_instnorm_affine_bwd": (I, [P, P, P, P, P, P, F, P, P, P, P, P, P, I, I, I, I, F, I, P]),

@@ -328,6 +328,26 @@ def get_conv_math():
     return _policy_name
 
 
+# Deterministic debug switch: the warp input gradients (warp_bwd_nhwc,
+# warp_masked_bwd_nhwc, the temporal loss's ga) run the atomic-free sort + ordered-gather path
+# (vst_warp_bwd_input_det) instead of the fp32-atomic scatter, so two runs agree bit for bit.
+_deterministic = os.environ.get("VST_DETERMINISTIC", "0") == "1"
+
+
+def set_deterministic(flag):
+    """Select the deterministic warp backward (True) or the atomic scatter (False); returns the previous."""
+    global _deterministic
+    prev, _deterministic = _deterministic, bool(flag)
+    return prev
+
+
+def _warp_bwd_det(gout, flow, gx, align_corners, masked, negate, cl):
+    N, H, W, C = gout.shape
+    ws = torch.empty(lib().vst_warp_bwd_det_ws_bytes(N, H, W), device=gout.device, dtype=torch.uint8)
+    _call("vst_warp_bwd_input_det", _p(gout), _p(flow), _p(gx), _p(ws), ws.numel(), N, H, W, C, cl,
+          int(align_corners), int(masked), int(negate), _stream())
+
+
 def _math(role):
     from ._lib import MATH_MODES
     return MATH_MODES[_POLICIES[_policy_name][role]]
@@ -568,6 +588,9 @@ def warp_bwd_nhwc(gout, flow, align_corners=False):
     _dev_check(gout, flow)
     N, H, W, C = gout.shape
     gx = torch.zeros_like(gout)
+    if _deterministic:
+        _warp_bwd_det(gout, flow, gx, align_corners, False, False, C)
+        return gx
     _call("vst_warp_bwd_input", _p(gout), _p(flow), _p(gx), N, H, W, C, int(align_corners), _stream())
     return gx
 
@@ -596,6 +619,12 @@ def loss_temporal(a, b, flow, mask, lam, cl=3):
 
 def loss_temporal_bwd(a, b, flow, mask, gout, ga, gb, lam, cl=3):
     N, H, W, Cs = a.shape
+    if _deterministic and ga is not None:   # gb first, then ga -= its ordered scatter
+        gbuf = gb if gb is not None else torch.empty_like(a)
+        _call("vst_loss_temporal_bwd", _p(a), _p(b), _p(flow), _p(mask), _p(gout), None, _p(gbuf), N, H, W,
+              Cs, cl, float(lam), _stream())
+        _warp_bwd_det(gbuf, flow, ga, False, False, True, cl)
+        return
     _call("vst_loss_temporal_bwd", _p(a), _p(b), _p(flow), _p(mask), _p(gout), _p(ga), _p(gb), N, H, W,
           Cs, cl, float(lam), _stream())
 
@@ -659,6 +688,9 @@ def warp_masked_bwd_nhwc(gout, flow, align_corners=False):
     _dev_check(gout, flow)
     N, H, W, C = gout.shape
     gx = torch.zeros_like(gout)
+    if _deterministic:
+        _warp_bwd_det(gout, flow, gx, align_corners, True, False, C)
+        return gx
     _call("vst_warp_masked_bwd_input", _p(gout), _p(flow), _p(gx), N, H, W, C, int(align_corners),
           _stream())
     return gx

@@ -308,6 +308,15 @@ int vst_warp_fwd(const float* x, const float* flow, float* out, int N, int H, in
 /* gx[...] += bilinear-transpose scatter of gout (gx must be zero-initialised by the caller). */
 int vst_warp_bwd_input(const float* gout, const float* flow, float* gx, int N, int H, int W, int Cs,
                        int align_corners, void* stream);
+/* Deterministic (atomic-free) warp input gradient — the debug switch of SURVEY §7 item 4, replacing
+ * the atomic scatter of vst_warp_bwd_input / vst_warp_masked_bwd_input (masked = 1: fs_lib.warp's
+ * validity mask) / vst_loss_temporal_bwd's ga (negate = 1, gout = that call's gb): gx[t][c] (c < Cl) +=
+ * sum over the output pixels p and corners k (nw, ne, sw, se) landing on t, in ascending (p, k) order,
+ * of (+-) w_k(p) * gout[p][c] — one fp32 rounding per add, identical from run to run.  ws: caller-owned,
+ * vst_warp_bwd_det_ws_bytes(N, H, W) bytes.  Reference: utils/flowtools.py:18-32 (F.grid_sample). */
+size_t vst_warp_bwd_det_ws_bytes(int N, int H, int W);
+int vst_warp_bwd_input_det(const float* gout, const float* flow, float* gx, void* ws, size_t ws_bytes, int N,
+                           int H, int W, int Cs, int Cl, int align_corners, int masked, int negate, void* stream);
 /* mask[n][0][h][w] in {0,1} from forward/backward flows ff, bf ([N][2][H][W]). */
 int vst_fbcheck(const float* ff, const float* bf, float* mask, int N, int H, int W, void* stream);
 

@@ -67,3 +67,25 @@ def test_train_step_matches_reference(golden):
     with torch.no_grad():
         out = m.G_A(torch.from_numpy(g["probe"]))
     np.testing.assert_allclose(out.numpy(), g["probe_out"], rtol=1e-3, atol=1e-4)
+
+
+def test_ordered_warp_backward_matches_reference(golden):
+    """oracle/flow_ref.warp_bwd_ordered (the deterministic warp backward's checker) against the
+    reference's own grid_sample input gradients: same corner weights, only the summation order of
+    colliding contributions differs (the align_corners=False quirk makes even integer flows sample
+    between pixels, so every case has collisions)."""
+    from oracle import flow_ref
+    g = golden("warp")
+    for case in ("zero", "int", "frac", "oob", "h1", "w1"):
+        gout = np.ascontiguousarray(g[f"{case}_gout"].transpose(0, 2, 3, 1))
+        dx = flow_ref.warp_bwd_ordered(gout, g[f"{case}_flow"]).transpose(0, 3, 1, 2)
+        np.testing.assert_allclose(dx, g[f"{case}_dx"], rtol=0, atol=1e-6)
+    # the masked variant (fs_lib.warp) and align_corners=True against torch autograd on CPU
+    x = torch.from_numpy(prng.uniform_f32(71, (2, 4, 9, 11), -1.0, 1.0)).requires_grad_(True)
+    fl = torch.from_numpy(prng.normal(72, (2, 2, 9, 11), std=2.0).astype(np.float32))
+    go = torch.from_numpy(prng.uniform_f32(73, (2, 4, 9, 11), -1.0, 1.0))
+    for align in (False, True):
+        x.grad = None
+        cpu_ref.warp(x, fl, align_corners=align).backward(go)
+        dx = flow_ref.warp_bwd_ordered(go.permute(0, 2, 3, 1).numpy(), fl.numpy(), align=align)
+        np.testing.assert_allclose(dx.transpose(0, 3, 1, 2), x.grad.numpy(), rtol=0, atol=2e-6)

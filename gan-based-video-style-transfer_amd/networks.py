@@ -174,6 +174,11 @@ def _pad_channels(x, cs):
     return y
 
 
+# No-grad forwards replay captured HIP graphs (FlatNet.graphed_forward); VST_GRAPHS=0 runs them eagerly.
+GRAPHS = os.environ.get("VST_GRAPHS", "1") != "0"
+GRAPH_CACHE = 8  # captured input shapes kept per network
+
+
 # Pack every layer of a network in one launch and refresh in place after updates (ops.PackBatch);
 # VST_PACK_BATCH=0: one vst_weight_pack_split launch per pack, rebuilt per weight version.
 PACK_BATCH = os.environ.get("VST_PACK_BATCH", "1") != "0"
@@ -199,6 +204,7 @@ class FlatNet(nn.Module):
         self.flat_param, self.flat_grad = flat, gflat
         self._wversion = getattr(self, "_wversion", 0) + 1
         self._packs = None
+        self._graphs = {}  # captured forwards read the packs: recaptured after a rebuild
 
     def _apply(self, fn, *args, **kwargs):
         super()._apply(fn, *args, **kwargs)
@@ -224,11 +230,13 @@ class FlatNet(nn.Module):
         if not PACK_BATCH:
             if self._packs is None or self._packs[0] != key:
                 self._packs = [key, self._make_packs(), None]
+                self._graphs = {}
             return self._packs[1]
         if self._packs is None:
             with ops.PackBatch() as pb:
                 P = self._make_packs()
             self._packs = [key, P, pb]
+            self._graphs = {}
         elif self._packs[0] != key:
             self._packs[2].run()
             self._packs[0] = key
@@ -242,10 +250,45 @@ class FlatNet(nn.Module):
         return a if self.weights_trainable() and torch.is_grad_enabled() else a.detach()
 
     def forward(self, x):
-        """Reference-compatible NCHW entry: [N, C, H, W] -> [N, C', H', W']."""
+        """Reference-compatible NCHW entry: [N, C, H, W] -> [N, C', H', W'].  Inference calls (no grad,
+        GPU input) replay a HIP graph captured once per input shape (graphed_forward)."""
+        if GRAPHS and not torch.is_grad_enabled() and x.is_cuda and not torch.cuda.is_current_stream_capturing():
+            return self.graphed_forward(x)
+        return self._forward_eager(x)
+
+    def _forward_eager(self, x):
         cin = self.input_nc
         y = self.forward_nhwc(_ToNHWC.apply(x, cpad(cin)))
         return _ToNCHW.apply(y, self.output_nc)
+
+    def graphed_forward(self, x):
+        """No-grad forward replayed from a HIP graph captured once per (shape, device, conv policy,
+        pack set): the ~100 kernel launches of a generator forward (forward_eval,
+        CycleGAN/models/cycle_gan_model.py:164-171) become one graph launch, so small batches are
+        not bound by host launch latency.  The packs are refreshed in place before each replay
+        (weight updates keep the captured buffers valid).  Returns a fresh output tensor."""
+        P = self.packs()
+        key = (tuple(x.shape), x.device, ops.get_conv_math(), id(P))
+        cache = self._graphs
+        ent = cache.get(key)
+        if ent is None:
+            if len(cache) >= GRAPH_CACHE:
+                cache.clear()
+            xs = x.detach().float().contiguous().clone()
+            side = torch.cuda.Stream(device=x.device)
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):  # warm-up outside capture (allocator, first-touch)
+                self._forward_eager(xs)
+            torch.cuda.current_stream().wait_stream(side)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                out = self._forward_eager(xs)
+            ent = (g, xs, out)
+            cache[key] = ent
+        g, xs, out = ent
+        xs.copy_(x)
+        g.replay()
+        return out.clone()
 
     # ---- gradient readiness for the data-parallel exchange (dp.GradExchange.attach) ----------
     # Every training forward (trainable weights, grad enabled) adds one pending backward pass; the

@@ -1,0 +1,18 @@
+#!/bin/bash
+# Host AddressSanitizer run of the C-ABI's host code: builds the library with
+# -fsanitize=address on the HOST side only (-Xarch_host; GPU ASan is not available on this pool) into
+# _build/variants/libvst_hip_asan.so, then runs the CPU host tests (tests/test_cpu_host.py: symbol
+# export, the conv / wgrad planners, descriptor validation, workspace sizing) plus the ABI argument-
+# validation test against it, with clang's ASan runtime preloaded.  CPU only: run here, never on a GPU box.
+set -o pipefail
+cd "$(dirname "$0")/.." || exit 1
+OUT=gan-based-video-style-transfer_amd/_build/variants/libvst_hip_asan.so
+RT=$(ls /opt/rocm/lib/llvm/lib/clang/*/lib/linux/libclang_rt.asan-x86_64.so | head -1)
+VST_VARIANT_HIPCC_FLAGS="-Xarch_host -fsanitize=address -Xarch_host -fno-omit-frame-pointer" \
+  python3 -c "
+import sys; sys.path.insert(0, '.')
+import gbvst
+print(gbvst._lib.build(out='$OUT', force=True))" || exit 1
+[ "$(nm -D "$OUT" | grep -c __asan_report)" -gt 0 ] || { echo "no ASan instrumentation in $OUT"; exit 1; }
+LD_PRELOAD="$RT" ASAN_OPTIONS=detect_leaks=0:abort_on_error=1 VST_LIB_VARIANT="$PWD/$OUT" \
+  python3 -m pytest -q -p no:cacheprovider tests/test_cpu_host.py tests/test_asan_host.py

@@ -88,13 +88,12 @@ def DOMINANT_KEYS(B):
             "resblock_wgrad": ("wgrad", (N, 64, 64, 256, 256, 3, 1, 1, "reflect"))}
 
 
-PMC_FILE = os.path.join(HERE, "profiles", "r03d_conv_pmc.json")
+PMC_FILE = os.path.join(HERE, "profiles", "r04a_conv_pmc.json")
 
 
-def _pmc_traffic(name, key):
-    """HBM bytes per launch of this kernel from the committed rocprofv3 PMC record (two passes:
-    FETCH_SIZE x2 per the gfx950 wide-read correction, WRITE_SIZE), only if the record was taken
-    on the same policy, tile and shape; else None."""
+def _pmc_record(name, key):
+    """This kernel's entry of the committed rocprofv3 PMC record, only if it was taken on the same
+    policy, tile and shape and on the same kernel sources / knobs (source stamp); else None."""
     try:
         rec = json.load(open(PMC_FILE)).get(name)
     except (OSError, ValueError):
@@ -104,7 +103,32 @@ def _pmc_traffic(name, key):
     from gbvst import _lib
     if rec.get("source_stamp") != _lib.source_stamp():   # taken on other kernel code or knobs
         return None
-    return rec.get("hbm_bytes_per_launch")
+    return rec
+
+
+def _pmc_traffic(name, key):
+    """HBM bytes per launch from the PMC record (FETCH_SIZE x2 per the gfx950 wide-read correction +
+    WRITE_SIZE, separate passes), or None."""
+    rec = _pmc_record(name, key)
+    return rec.get("hbm_bytes_per_launch") if rec else None
+
+
+NOMINAL_CLOCK_GHZ = 2.4   # the clock the dense MFMA peaks are quoted at (MI355X_MICROARCH.md)
+
+
+def _held_clock(entry, name, key):
+    """peak_at_held_clock: the ceiling scaled to the clock the chip held under this kernel (the PMC
+    record's SQ_WAVE_CYCLES-derived effective clock), and the fraction against it — the DVFS share of
+    the gap to the nominal-clock ceiling as a number."""
+    rec = _pmc_record(name, key)
+    clk = rec.get("effective_clock_GHz") if rec else None
+    if not clk:
+        entry.update(held_clock_GHz=None, peak_at_held_clock=None, frac_at_held_clock=None)
+        return entry
+    pk = entry["peak"] * clk / NOMINAL_CLOCK_GHZ
+    entry.update(held_clock_GHz=clk, peak_at_held_clock=round(pk, 1), frac_at_held_clock=round(entry["achieved"] / pk, 4),
+                 mfma_busy_at_held_clock=rec.get("mfma_busy_frac_actual_clock"))
+    return entry
 
 
 def _mfma(m):
@@ -150,19 +174,23 @@ def conv_roofline(name, probe, math):
                 "dgrad_border5_add_k adds the border slabs (VST_DGRAD_IN=1 moves that add into the "
                 "IN-backward partial pass)")
     else:
-        kernel = ("vst_conv2d_wgrad: nhwc_to_cp_pad_k + nhwc_to_cp_planes_k copies + conv_wgrad_bf_k "
-                  "(split-K slabs) + wgrad_reduce_store_k, %s" % m if m != "fp32" else
+        # the step's route (networks.py IN_XT / IN_PLANES): the IN apply writes x's padded channel-major
+        # image and the IN backward dy's bf16 planes, so the op is the GEMM + the split-K reduction
+        kernel = ("vst_conv2d_wgrad on producer-written operands (x image from the IN apply, dy planes from the "
+                  "IN backward): conv_wgrad_bf_k (split-K slabs) + wgrad_reduce_store_k, %s" % m if m != "fp32" else
                   "vst_conv2d_wgrad: channel-major copies + conv_wgrad_rk_k + wgrad_reduce_store_k, fp32")
         key = {"math": m, "N": N, "mfma": _mfma(m)}
         kernel += " [%s]" % _mfma(m)
-        note = "whole weight-gradient op: its 4-5 launches are timed together"
-    return {"kernel": kernel, "what": note + " — ResnetBlock 3x3 reflect 256->256 @64x64, N=%d" % N,
-            "bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
-            "frac": round(achieved / peak, 4),
-            "peak_basis": "dense bf16 MFMA %.0f TFLOP/s / products per fp32-equivalent MAC (%s)" % (BF16_MFMA_PEAK_TFLOPS, m),
-            "traffic": _pmc_traffic(name, key), "avg_launch_ms": round(ms, 4), "flop_per_launch": flop,
-            "launches_timed": len(probe.events), "ms_per_step": round(ms * len(probe.events) / max(1, probe.steps), 3),
-            "fp32_mfma_peak": FP32_MFMA_PEAK_TFLOPS}
+        note = "whole weight-gradient op as the train step runs it (its launches timed together)"
+        name = "resblock_wgrad_pre"   # the PMC record of this route (tools/kbench.py wgrad_pre)
+    entry = {"kernel": kernel, "what": note + " — ResnetBlock 3x3 reflect 256->256 @64x64, N=%d" % N,
+             "bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
+             "frac": round(achieved / peak, 4),
+             "peak_basis": "dense bf16 MFMA %.0f TFLOP/s / products per fp32-equivalent MAC (%s)" % (BF16_MFMA_PEAK_TFLOPS, m),
+             "traffic": _pmc_traffic(name, key), "avg_launch_ms": round(ms, 4), "flop_per_launch": flop,
+             "launches_timed": len(probe.events), "ms_per_step": round(ms * len(probe.events) / max(1, probe.steps), 3),
+             "fp32_mfma_peak": FP32_MFMA_PEAK_TFLOPS}
+    return _held_clock(entry, name, key)
 
 
 def warp_roofline(device, N=32, C=64, H=436, W=1024, reps=10):
@@ -319,6 +347,31 @@ def mogan_train_fps(device, B=4, S=256, pairs=2, H=None, W=None):
             "batch": B, "value": round(B / dt, 2), "unit": "frames/s", "ms_per_step": round(dt * 1e3, 3)}
 
 
+VGG19_TO_RELU5_1 = [(3, 64), (64, 64), "pool", (64, 128), (128, 128), "pool", (128, 256), (256, 256), (256, 256),
+                    (256, 256), "pool", (256, 512), (512, 512), (512, 512), (512, 512), "pool", (512, 512)]
+VGG19_SLICE_ENDS = (0, 2, 4, 8, 12)   # conv index after which relu1_1 .. relu5_1 are taken
+
+
+def vgg19_c3_flops(H, W):
+    """Algorithmic FLOPs of the VGG-19 work in one C3 step (cycle_gan_vgg_model.extra_G_loss, network.py:45-78):
+    3 forwards to relu5_1 (fake_B2 with grad, the real_A2 content target and the real_B style target),
+    1 data-gradient pass (the frozen VGG's backward to fake_B2: every conv's dgrad, conv1_1's included),
+    5 Grams each for fake_B2 and real_B (c^2 hw MACs, fast_style_transfer.py:813-817) and the Gram
+    backward (c^2 hw).  3x3 convs: 9 Cin Cout MACs per output pixel."""
+    h, w, conv, levels = H, W, 0.0, []
+    for i, L in enumerate(VGG19_TO_RELU5_1):
+        if L == "pool":
+            h, w = h // 2, w // 2
+            continue
+        ci, co = L
+        conv += 9.0 * ci * co * h * w
+        n_conv = sum(1 for x in VGG19_TO_RELU5_1[:i + 1] if x != "pool") - 1
+        if n_conv in VGG19_SLICE_ENDS:
+            levels.append(co * co * h * w)
+    gram = sum(levels)
+    return {"conv_fwd_gflop": 2 * conv / 1e9, "total_tflop": (2 * conv * 4 + 2 * gram * 3) / 1e12}
+
+
 def c3_train_fps(device, B=1, H=436, W=1024, steps=4):
     """Config C3: CycleGANCon step + VGG-19 content / Gram loss on fake_B2
     (gbvst.cycle_gan_vgg_model) on synthetic Sintel-size frame pairs 1x3x436x1024 (flow x4), random-init
@@ -339,11 +392,14 @@ def c3_train_fps(device, B=1, H=436, W=1024, steps=4):
         m.optimize_parameters()
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / steps
+    vgg = vgg19_c3_flops(H, W)
     return {"metric": "C3 train step frames/s %dx%d (CycleGANCon + flow-warp + VGG-19 content/Gram loss)" % (W, H),
             "batch": B, "value": round(B / dt, 3), "unit": "frames/s", "ms_per_step": round(dt * 1e3, 2),
             "tflops_conv_G_D": round(TRAIN_TFLOP_PER_FRAME_C3 / dt, 2),
-            "roofline": _mfma_roofline(TRAIN_TFLOP_PER_FRAME_C3 / dt, "G/D conv FLOPs of the step (14.831 TFLOP/frame, "
-                                       "SURVEY §8d) over the whole step time; the VGG-19 work is not counted"),
+            "roofline": _mfma_roofline((TRAIN_TFLOP_PER_FRAME_C3 + vgg["total_tflop"]) / dt,
+                                       "G/D conv FLOPs (14.831 TFLOP/frame, SURVEY §8d) + the VGG-19 conv / Gram FLOPs "
+                                       "(%.3f TFLOP/frame: 3 forwards to relu5_1, 1 data-gradient pass, 10 Grams + "
+                                       "their backward) over the whole step time" % vgg["total_tflop"]),
             "loss_weights": {"lambda_content": m.opt.lambda_content, "lambda_style": m.opt.lambda_style},
             "losses": {k: round(v, 4) for k, v in m.get_current_losses().items()}}
 

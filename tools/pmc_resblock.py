@@ -54,6 +54,12 @@ def main():
     reps = int(sys.argv[3]) if len(sys.argv) > 3 else 5
     B = int(os.environ.get("KB_B", "8"))
     res, lines = {}, []
+    sf = os.path.join(d, "source_stamp.txt")   # written on the GPU box by profile_counters.sh
+    if os.path.exists(sf):
+        stamp = open(sf).read().strip()
+    else:
+        from gbvst import _lib as _L
+        stamp = _L.source_stamp()
     for op, subs in OPS.items():
         fetch = counters(os.path.join(d, op + "_fetch"), subs).get("FETCH_SIZE", [])
         write = counters(os.path.join(d, op + "_write"), subs).get("WRITE_SIZE", [])
@@ -84,8 +90,7 @@ def main():
             key.update(tile=kind, m_split=ms, ksplit=ks)
             if op == "dgrad":
                 key["op"] = "dgrad_refl"  # bench.py's dgrad key
-        from gbvst import _lib as _L
-        res[name] = {"key": key, "source_stamp": _L.source_stamp(), "dispatches_per_call": len(fetch) / reps, "fetch_bytes": fb, "write_bytes": wb,
+        res[name] = {"key": key, "source_stamp": stamp, "dispatches_per_call": len(fetch) / reps, "fetch_bytes": fb, "write_bytes": wb,
                      "hbm_bytes_per_launch": fb + wb, "algorithmic_bytes": alg,
                      "main_kernel_avg_us": round(sum(t) / len(t), 2) if t else None,
                      "note": "FETCH_SIZE x2 (gfx950 wide-read correction) + WRITE_SIZE, summed over the op's dispatches"}

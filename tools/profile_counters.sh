@@ -7,6 +7,8 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 OUT=gpurun_out/${TAG:-pmc}
 mkdir -p $OUT
+# the kernel-source stamp of the code being profiled (tools/pmc_resblock.py stores it in the record)
+python3 -c "import sys; sys.path.insert(0, '.'); from gbvst import _lib; print(_lib.source_stamp())" > $OUT/source_stamp.txt || exit 1
 SQ1="SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES"
 SQ2="SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_SALU"
 for op in ${OPS:-fprop dgrad wgrad warp}; do

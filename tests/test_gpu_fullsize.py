@@ -108,19 +108,36 @@ def bands(golden):
     return {k: float(g[k]) for k in g.files}
 
 
+def _log_deviations(prefix, rows):
+    """VST_PARITY_LOG=<dir>: write every compared quantity's (deviation, tolerance, band) as JSON."""
+    import json
+    import os
+    d = os.environ.get("VST_PARITY_LOG")
+    if not d:
+        return
+    from gbvst import ops
+    os.makedirs(d, exist_ok=True)
+    name = (prefix.strip("|") or "run") + "_" + ops.get_conv_math()
+    json.dump({k: {"dev": v, "tol": t, "band": b} for k, v, t, b in rows},
+              open(os.path.join(d, "fullsize_%s.json" % name), "w"), indent=0, sort_keys=True)
+
+
 def _check(prefix, got, ref, bands, floors, skip=()):
     """Every quantity of ref (an oracle run) against got within max(floor, 3 x band)."""
-    bad = []
+    bad, rows = [], []
     for key, r in ref.items():
         if any(s in key for s in skip):
             continue
         assert key in got, key
         kind = key.split("|", 1)[0]
         floor = floors(key) if callable(floors) else floors[kind]
-        tol = max(floor, 3 * bands.get(prefix + key, 0.0))
+        band = bands.get(prefix + key, 0.0)
+        tol = max(floor, 3 * band)
         dev = deviation(key, got[key], r)
+        rows.append((key, dev, tol, band))
         if not dev <= tol:
             bad.append((key, dev, tol))
+    _log_deviations(prefix, rows)
     assert not bad, bad[:12]
 
 

@@ -128,8 +128,9 @@ def _nccl_worker(port, q):
         torch.cuda.set_device(0)
         dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
         import gbvst
-        from gbvst import dp
+        from gbvst import dp, ops
         gbvst._lib.load()
+        ops.set_deterministic(True)
         m = _setup()
         nets = [m.netG_A, m.netG_B, m.netD_A, m.netD_B]
         # force: the world-1 short-circuit is bypassed, so every bucket goes through RCCL
@@ -153,9 +154,9 @@ def test_dp_nccl_world1_forced_buckets():
     """The RCCL path on hardware: a one-rank `nccl` (= RCCL) process group with the bucketed exchange
     forced on.  Buckets are all_reduce(async_op=True) calls enqueued from inside the HIP backward
     passes; the join makes the compute stream wait on them before Adam.  A one-rank sum is the
-    identity, so the step must equal the run without any exchange up to the warp backward's atomic
-    summation order — any stream-ordering fault (Adam reading a bucket before RCCL wrote it back, or
-    the join's scaling racing the collective) shows as a gradient or weight far outside that."""
+    identity and both runs use the deterministic warp backward, so the step must equal the run without
+    any exchange BIT FOR BIT — any stream-ordering fault (Adam reading a bucket before RCCL wrote it
+    back, or the join's scaling racing the collective) shows as a differing gradient or weight."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     p = ctx.Process(target=_nccl_worker, args=(_free_port(), q))
@@ -166,19 +167,142 @@ def test_dp_nccl_world1_forced_buckets():
     assert p.exitcode == 0
     assert backend == "nccl"
     import gbvst
+    from gbvst import ops
     gbvst._lib.load()
-    m = _setup()
-    grads = {}
-    m.optimize_parameters(_grads_hook(grads), _grads_hook(grads))
-    torch.cuda.synchronize()
+    prev = ops.set_deterministic(True)
+    try:
+        m = _setup()
+        grads = {}
+        m.optimize_parameters(_grads_hook(grads), _grads_hook(grads))
+        torch.cuda.synchronize()
+    finally:
+        ops.set_deterministic(prev)
     for name in ("G_A", "G_B", "D_A", "D_B"):
         net = getattr(m, "net" + name)
-        ref = grads[id(net)].numpy().astype(np.float64)
-        rel = np.linalg.norm(out[name] - ref) / np.linalg.norm(ref)
-        assert rel < 1e-5, (name, rel)
+        ref = grads[id(net)].numpy()
+        assert np.array_equal(out[name], ref), (name, np.abs(out[name] - ref).max())
         assert len(logs[name]) > 0, (name, logs[name])   # launched during backward, not at the join
-    lr = 2e-4
     for name in ("G_A", "D_A"):
-        d = np.abs(w[name] - getattr(m, "net" + name).flat_param.detach().cpu().numpy())
-        # Adam's first update is ~lr*sign(g): rounding-level gradient noise can flip a near-zero one
-        assert d.max() <= 2.5 * lr and d.mean() < 1e-3 * lr, (name, d.max(), d.mean())
+        ref = getattr(m, "net" + name).flat_param.detach().cpu().numpy()
+        assert np.array_equal(w[name], ref), (name, np.abs(w[name] - ref).max())
+
+
+# ------------------------------------------------------------------------------ MoGAN (config C5)
+# The three exchange phases of MoGAN/models/cycle_gan_model.py:315-352 under DP: the E-step's G and D
+# gradients (grad_hook_G / grad_hook_D) and the M-step's motion-net gradients (grad_hook_M), each
+# bucket launched from inside that phase's last backward pass.  Every per-sample piece (G / D / M, RAFT,
+# warp, fb-check) is batch-independent and every loss a batch mean, so two ranks on half batches with
+# averaged gradients equal one process on the whole batch.  Both sides run the deterministic warp
+# backward, so the only difference left is the split-K order of the weight gradients (batch size).
+_MG_NAMES = ("G_A", "G_B", "D_A", "D_B", "M_A", "M_B")
+
+
+def _mogan_setup(B_slice=None):
+    import argparse
+    from gbvst import mogan_model, raft
+    from gbvst.options import default_opt
+    from oracle import cpu_ref, prng, raft_ref
+    r = raft.RAFT(argparse.Namespace(small=False))
+    shapes = {k: tuple(v.shape) for k, v in r.state_dict().items()}
+    r.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in raft_ref.raft_weights(shapes, 1300, 1e-3).items()})
+    opt = default_opt(True, model="mogan", ngf=8, ndf=8, pool_size=0, gpu_ids=[0])
+    m = mogan_model.MoGANModel(opt, raft_model=r.to("cuda").eval(), raft_iters=4)
+    for i, name in enumerate(_MG_NAMES):
+        net = getattr(m, "net" + name)
+        sd = prng.init_state_dict(cpu_ref.state_shapes(net), base_seed=950 + i)
+        net.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    imgs = [torch.from_numpy(prng.uniform_f32(960 + i, (4, 3, 64, 64), -1.0, 1.0)) for i in range(4)]
+    if B_slice is not None:
+        imgs = [t[B_slice] for t in imgs]
+    m.set_input_fc2(imgs)
+    return m
+
+
+def _mogan_run(m, ex=None):
+    """E-step then M-step; returns {phase: {net: flat grad}} captured at each phase's hook."""
+    grads = {"E": {}, "M": {}}
+
+    def hook(phase):
+        def h(nets):
+            if ex is not None:
+                ex(nets)
+            for n in nets:
+                grads[phase][id(n)] = n.flat_grad.detach().cpu().clone()
+        return h
+    m.optimize_parameters(hook("E"), hook("E"), hook("E"))
+    m.optimize_parameters(hook("M"), hook("M"), hook("M"))
+    torch.cuda.synchronize()
+    out = {}
+    for phase, names in (("E", _MG_NAMES[:4]), ("M", _MG_NAMES[4:])):
+        out[phase] = {n: grads[phase][id(getattr(m, "net" + n))].numpy() for n in names}
+    return out
+
+
+def _mogan_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import gbvst
+        from gbvst import dp, ops
+        gbvst._lib.load()
+        torch.cuda.set_device(0)
+        ops.set_deterministic(True)
+        m = _mogan_setup(slice(rank * 2, rank * 2 + 2))
+        nets = [getattr(m, "net" + n) for n in _MG_NAMES]
+        ex = dp.GradExchange(world, bucket_bytes=64 << 10).attach(nets)
+        out = _mogan_run(m, ex)
+        logs = {n: list(ex._state(getattr(m, "net" + n)).last_log) for n in _MG_NAMES}
+        q.put((rank, out, logs, None))
+    except Exception:  # report, do not hang the parent
+        import traceback
+        q.put((rank, None, None, traceback.format_exc()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+def test_mogan_dp_world2_three_phases_equal_single_process():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_mogan_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=500) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=120)
+    for r in res:
+        assert r[3] is None, r[3]
+    for p in procs:
+        assert p.exitcode == 0
+    import gbvst
+    from gbvst import ops
+    gbvst._lib.load()
+    prev = ops.set_deterministic(True)
+    try:
+        m = _mogan_setup()
+        full = _mogan_run(m)
+    finally:
+        ops.set_deterministic(prev)
+    # the E-step gradients (before any update) to 1e-4; the M-step ones after the E-step's Adam update
+    # (its first step is ~lr * sign(g): rounding-level differences in near-zero gradients move a few
+    # weights by ~lr on one side only) to 1e-3
+    for phase, tol in (("E", 1e-4), ("M", 1e-3)):
+        for name, ref in full[phase].items():
+            r0, r1 = res[0][1][phase][name], res[1][1][phase][name]
+            assert np.array_equal(r0, r1), (phase, name)
+            net = getattr(m, "net" + name)
+            off = 0
+            for k, p in net.named_parameters():
+                n = p.numel()
+                in_bias = k.endswith("bias") and k not in ("model.26.bias", "model.0.bias", "model.11.bias")
+                if not in_bias:
+                    a, b = r0[off:off + n].astype(np.float64), ref[off:off + n].astype(np.float64)
+                    rel = np.linalg.norm(a - b) / (np.linalg.norm(b) + 1e-30)
+                    assert rel < tol, (phase, name, k, rel)
+                off += n
+            assert len(res[0][2][name]) > 0, (phase, name)   # buckets launched during backward

@@ -152,6 +152,10 @@ int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* b
                     double* part = nullptr, float* tws = nullptr, size_t tws_floats = 0, const float* addend = nullptr,
                     int oph = 0);
 // direct patch-staged 4-channel-input convs (conv_c4.hip)
+// the 64 -> 4-output 7 x 7 tap conv as one direct kernel (conv_tap64.hip)
+bool tap64_ok(int Cx, int R, int W, int math);
+int tap64_launch(const float* x, const void* wsplit, long wps, const float* bias, float* y, int N, int H, int W,
+                 int pad, int reflect, int act, float slope, int math, hipStream_t s);
 bool c4_direct_ok(int C, int Cop, int R, int S, int st, int Ho, int Wo, int math);
 int c4_direct_launch(const float* x, const void* wsplit, long wps, const float* bias, float* y, int N, int H, int W,
                      int Ho, int Wo, int R, int S, int pad, int reflect, int act, float slope, int math, double* part,

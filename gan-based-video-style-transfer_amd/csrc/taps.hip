@@ -403,6 +403,10 @@ extern "C" int vst_tapconv_h_fwd(const float* x, const float* wp, const void* ws
   VST_REQUIRE(pad_mode == VST_PAD_ZERO || (2 * pad == R - 1 && pad < H && pad < W),
               "tapconv_h_fwd: reflect padding needs a 'same' conv with pad < size");
   const int Ho = H + 2 * pad - R + 1, Wo = W + 2 * pad - R + 1;
+  // 64 channels, 7 x 7, split-bf16: the R x 1 conv and the column taps as one direct kernel (conv_tap64.hip)
+  if (wsplit && tap64_ok(Cx, R, W, math))
+    return tap64_launch(x, wsplit, (long)4 * R * R * Cx, bias, y, N, H, W, pad, pad_mode == VST_PAD_REFLECT, act,
+                        slope, math, (hipStream_t)stream);
   // the R x 1 conv: rows padded by `pad`, the columns by 0 (their taps are summed below)
   if (int e = vst_conv2d_fwd_hwp(x, wp, wsplit, nullptr, z, N, H, W, Cx, 4 * R, R, 1, 1, pad, 0, pad_mode,
                                  VST_ACT_NONE, 0.f, math, stream))

@@ -104,6 +104,18 @@ class CycleGANModel(BaseModel):
             self.optimizer_M = FusedAdam([self.netM_A, self.netM_B], lr=opt.lr, betas=(opt.beta1, 0.999))
             self.optimizers = [self.optimizer_G, self.optimizer_D, self.optimizer_M]
             self.set_requires_grad([self.netM_A, self.netM_B], False)
+        # test conditioning hook (parity tests only): a list of dicts of NCHW flows / masks, one per
+        # forward_train, used instead of the RAFT calls and fb-check masks (FLOW_KEYS + mask_A / mask_B)
+        self.flow_inject = None
+
+    FLOW_KEYS = ("ff_real_A", "bf_real_A", "bf_fake_B", "bf_rec_A", "ff_real_B", "bf_real_B", "bf_fake_A", "bf_rec_B")
+
+    def _injected(self):
+        if not self.flow_inject:
+            return None
+        src = self.flow_inject.pop(0)
+        return {k: (ops.nchw_to_nhwc(v.to(self.device).float().contiguous()) if k in self.FLOW_KEYS
+                    else v.to(self.device).float().contiguous()) for k, v in src.items()}
 
     def initRaftModel(self, opt):
         """:119-126 — the reference loads raft/models/raft-chairs.pth, which is not shipped; the
@@ -188,15 +200,22 @@ class CycleGANModel(BaseModel):
                   self.rec_B2]
         seconds = [self.real_A2, self.real_A, self.fake_B, self.rec_A, self.real_B2, self.real_B, self.fake_A,
                    self.rec_B]
-        fl = self.computeRAFT(torch.cat([t.detach() for t in firsts]), torch.cat([t.detach() for t in seconds]))
-        (self.ff_real_A, self.bf_real_A, self.bf_fake_B, self.bf_rec_A,
-         self.ff_real_B, self.bf_real_B, self.bf_fake_A, self.bf_rec_B) = (fl[k * B:(k + 1) * B] for k in range(8))
+        inj = self._injected()
+        if inj is None:
+            fl = self.computeRAFT(torch.cat([t.detach() for t in firsts]), torch.cat([t.detach() for t in seconds]))
+            (self.ff_real_A, self.bf_real_A, self.bf_fake_B, self.bf_rec_A,
+             self.ff_real_B, self.bf_real_B, self.bf_fake_A, self.bf_rec_B) = (fl[k * B:(k + 1) * B] for k in range(8))
+        else:
+            for k in self.FLOW_KEYS:
+                setattr(self, k, inj[k])
         self.bf_M_A = self.netM_A.forward_nhwc(self.bf_real_A)
         self.warp_B = warp_nhwc(self.fake_B, ops.nhwc_to_nchw(self.bf_M_A.detach(), 2))
-        self.mask_A = ops.fbcheck(ops.nhwc_to_nchw(self.ff_real_A, 2), ops.nhwc_to_nchw(self.bf_real_A, 2))
+        self.mask_A = inj["mask_A"] if inj is not None else ops.fbcheck(ops.nhwc_to_nchw(self.ff_real_A, 2),
+                                                                       ops.nhwc_to_nchw(self.bf_real_A, 2))
         self.bf_M_B = self.netM_B.forward_nhwc(self.bf_real_B)
         self.warp_A = warp_nhwc(self.fake_A, ops.nhwc_to_nchw(self.bf_M_B.detach(), 2))
-        self.mask_B = ops.fbcheck(ops.nhwc_to_nchw(self.ff_real_B, 2), ops.nhwc_to_nchw(self.bf_real_B, 2))
+        self.mask_B = inj["mask_B"] if inj is not None else ops.fbcheck(ops.nhwc_to_nchw(self.ff_real_B, 2),
+                                                                       ops.nhwc_to_nchw(self.bf_real_B, 2))
 
     def forward(self):
         """:198-203 (used by test)."""

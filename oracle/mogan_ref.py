@@ -33,6 +33,10 @@ class RefMoGAN:
             adam([self.M_A, self.M_B])
         self._req([self.M_A, self.M_B], False)
         self.e_step = True
+        # conditioning hooks of the parity tests: every forward_train's 8 RAFT flows + 2 fb-check masks
+        # are appended to `record`; with `inject` (a list of such dicts, consumed in order) they are
+        # taken from there instead of computed (the discrete / RAFT-amplified parts held equal)
+        self.record, self.inject = [], None
 
     def nets(self):
         return {"G_A": self.G_A, "G_B": self.G_B, "D_A": self.D_A, "D_B": self.D_B, "M_A": self.M_A, "M_B": self.M_B}
@@ -62,24 +66,33 @@ class RefMoGAN:
         self.rec_A2 = self.G_B(self.fake_B2)
         self.fake_A2 = self.G_B(self.real_B2)
         self.rec_B2 = self.G_A(self.fake_A2)
+        rec = {}
+        src = self.inject.pop(0) if self.inject else None
         for d, (r, r2, f, f2, rc, rc2, M) in (("A", (self.real_A, self.real_A2, self.fake_B, self.fake_B2, self.rec_A,
                                                      self.rec_A2, self.M_A)),
                                               ("B", (self.real_B, self.real_B2, self.fake_A, self.fake_A2, self.rec_B,
                                                      self.rec_B2, self.M_B))):
-            ff_real = self.raft(r, r2)
-            bf_real = self.raft(r2, r)
-            bf_fake = self.raft(f2, f)
-            bf_rec = self.raft(rc2, rc)
+            other = "B" if d == "A" else "A"
+            names = ("ff_real_" + d, "bf_real_" + d, "bf_fake_" + other, "bf_rec_" + d)
+            if src is not None:
+                ff_real, bf_real, bf_fake, bf_rec = (src[k].clone() for k in names)
+            else:
+                ff_real = self.raft(r, r2)
+                bf_real = self.raft(r2, r)
+                bf_fake = self.raft(f2, f)
+                bf_rec = self.raft(rc2, rc)
             bf_M = M(bf_real)
             warp = cpu_ref.warp(f, bf_M)
-            mask = cpu_ref.fbc_check(ff_real, bf_real)
-            other = "B" if d == "A" else "A"
+            mask = src["mask_" + d].clone() if src is not None else cpu_ref.fbc_check(ff_real, bf_real)
+            rec.update(zip(names, (ff_real, bf_real, bf_fake, bf_rec)))
+            rec["mask_" + d] = mask
             setattr(self, "bf_real_" + d, bf_real)
             setattr(self, "bf_fake_" + other, bf_fake)
             setattr(self, "bf_rec_" + d, bf_rec)
             setattr(self, "bf_M_" + d, bf_M)
             setattr(self, "warp_" + other, warp)
             setattr(self, "mask_" + d, mask)
+        self.record.append({k: v.detach().clone() for k, v in rec.items()})
 
     def optimize_parameters(self, grad_hook_G=None, grad_hook_D=None, grad_hook_M=None):
         """grad_hook_*(nets): called between each phase's backward and its Adam step (the tests read

@@ -69,9 +69,9 @@ def update_block(sd, net, inp, corr, flow, want_mask=True):
     return h, mask, delta
 
 
-def coords_grid(b, h, w):
+def coords_grid(b, h, w, dtype=torch.float32):
     ys, xs = torch.meshgrid(torch.arange(h), torch.arange(w), indexing="ij")
-    return torch.stack([xs, ys], 0).float()[None].repeat(b, 1, 1, 1)
+    return torch.stack([xs, ys], 0).to(dtype)[None].repeat(b, 1, 1, 1)
 
 
 def upsample_flow(flow, mask):
@@ -106,7 +106,7 @@ def raft_forward(sd, image1, image2, iters=12, flow_init=None, test_mode=False, 
     c = encoder(sd, "cnet.", image1, "batch")
     net, inp = torch.tanh(c[:, :128]), torch.relu(c[:, 128:])
     h8, w8 = c.shape[-2:]
-    coords0, coords1 = coords_grid(b, h8, w8), coords_grid(b, h8, w8)
+    coords0, coords1 = coords_grid(b, h8, w8, fmap1.dtype), coords_grid(b, h8, w8, fmap1.dtype)
     if flow_init is not None:
         coords1 = coords1 + flow_init
     preds = []

@@ -212,7 +212,8 @@ class RefCorrBlock:
         self.num_levels, self.radius = num_levels, radius
         b, d, h, w = fmap1.shape
         corr = torch.matmul(fmap1.view(b, d, h * w).transpose(1, 2), fmap2.view(b, d, h * w))
-        corr = (corr / torch.sqrt(torch.tensor(d).float())).reshape(b * h * w, 1, h, w)
+        # the reference's .float() (corr.py:22); dtype-following so the parity tests can run it in fp64
+        corr = (corr / torch.sqrt(torch.tensor(d).to(fmap1.dtype))).reshape(b * h * w, 1, h, w)
         self.pyr = [corr]
         for _ in range(num_levels - 1):
             corr = F.avg_pool2d(corr, 2, stride=2)
@@ -224,11 +225,11 @@ class RefCorrBlock:
         b, h1, w1, _ = coords.shape
         outs = []
         for i in range(self.num_levels):
-            d = torch.linspace(-r, r, 2 * r + 1)
+            d = torch.linspace(-r, r, 2 * r + 1, dtype=coords.dtype)
             delta = torch.stack(torch.meshgrid(d, d, indexing="ij"), axis=-1)
             c = coords.reshape(b * h1 * w1, 1, 1, 2) / 2 ** i + delta.view(1, 2 * r + 1, 2 * r + 1, 2)
             outs.append(bilinear_sampler(self.pyr[i], c).view(b, h1, w1, -1))
-        return torch.cat(outs, dim=-1).permute(0, 3, 1, 2).contiguous().float()
+        return torch.cat(outs, dim=-1).permute(0, 3, 1, 2).contiguous().to(self.pyr[0].dtype)
 
 
 def np_state(net):

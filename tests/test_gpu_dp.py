@@ -211,7 +211,7 @@ def _mogan_setup(B_slice=None):
         net = getattr(m, "net" + name)
         sd = prng.init_state_dict(cpu_ref.state_shapes(net), base_seed=950 + i)
         net.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
-    imgs = [torch.from_numpy(prng.uniform_f32(960 + i, (4, 3, 64, 64), -1.0, 1.0)) for i in range(4)]
+    imgs = [torch.from_numpy(prng.uniform_f32(960 + i, (4, 3, 128, 128), -1.0, 1.0)) for i in range(4)]
     if B_slice is not None:
         imgs = [t[B_slice] for t in imgs]
     m.set_input_fc2(imgs)

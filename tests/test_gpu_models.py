@@ -262,3 +262,26 @@ def test_full_size_train_step_vs_oracle(gb, full_oracle, train_math):
     dev64 = float(band["probe_dev64"])
     err = (out - p32).abs().max().item()
     assert err <= max(1e-3, 3 * dev64), (err, dev64)
+
+
+def test_graphed_inference_matches_eager(gb):
+    """No-grad forwards replay a captured HIP graph (FlatNet.graphed_forward): bit-identical to the
+    eager launches, per input shape, and still after a weight update (packs refreshed in place)."""
+    from gbvst import networks
+    G = networks.define_G(3, 3, 16, "resnet_9blocks", "instance", False, "normal", 0.02, [0])
+    D = networks.define_D(3, 16, "basic", 3, "instance", "normal", 0.02, [0])
+    g = torch.Generator().manual_seed(3)
+    with torch.no_grad():
+        for net, shapes in ((G, [(1, 3, 64, 64), (2, 3, 64, 96)]), (D, [(2, 3, 64, 64)])):
+            for shp in shapes:
+                x = (torch.rand(*shp, generator=g) * 2 - 1).cuda()
+                y = net(x)
+                assert torch.equal(y, net._forward_eager(x)), shp
+                assert torch.equal(net(x), y)           # replay again
+            key = next(iter(net._graphs))
+            net.flat_param.mul_(1.01)                  # a weight update
+            net.bump_version()
+            x = (torch.rand(*shapes[0], generator=g) * 2 - 1).cuda()
+            y = net(x)
+            assert next(iter(net._graphs)) == key      # same captured graph, refreshed packs
+            assert torch.equal(y, net._forward_eager(x))

@@ -398,6 +398,36 @@ def test_tap_conv_fwd_h_production(ops, conv_math):
     assert float(yh[..., 3].abs().max()) == float(torch.tanh(torch.zeros(1))[0])
 
 
+@pytest.mark.parametrize("N,H,W,pad,mode,act", [(2, 12, 64, 3, "reflect", "tanh"), (3, 9, 128, 6, "zero", "none"),
+                                                 (1, 7, 1024, 3, "reflect", "tanh"), (2, 20, 256, 6, "zero", "none"),
+                                                 (1, 5, 512, 3, "reflect", "none")])
+def test_tap64_direct(ops, conv_math, N, H, W, pad, mode, act):
+    """The direct 64 -> 4 7x7 tap kernel (conv_tap64.hip, inside vst_tapconv_h_fwd when W | 1024): the last
+    layer's forward (reflect 3, tanh) and the first layer's full-correlation data-gradient form (zero pad 6,
+    (H+6) x (W+6) output), groups of several rows / one row / rows past the end, vs torch fp32 and vs the
+    1x1-conv + full tap-sum route."""
+    ci, co, k = 64, 3, 7
+    x = _g(111, (N, ci, H, W))
+    w = _g(112, (co, ci, k, k), 0.02)
+    b = _g(113, (co,), 0.1) if act == "tanh" else None
+    xp = F.pad(x, (pad,) * 4, mode="reflect") if mode == "reflect" else F.pad(x, (pad,) * 4)
+    ref = F.conv2d(xp, w, b)
+    ref = torch.tanh(ref) if act == "tanh" else ref
+    wd = w.to(DEV)
+    bp = None
+    if b is not None:
+        bp = torch.zeros(4, device=DEV)
+        bp[:co] = b.to(DEV)
+    xn = _nhwc(x, ops)
+    yh = ops.tap_conv_fwd_h(xn, ops.weight_pack(wd, ops.PACK_SOK, Op=4), bp, k, pad, mode, act=act)
+    assert yh.shape == (N, H + 2 * pad - 6, W + 2 * pad - 6, 4)
+    _close(_nchw(yh, co, ops), ref, tol=CONV_TOL[conv_math], what="tap64 direct vs torch")
+    assert float(yh[..., 3].abs().max()) == 0.0
+    if pad == (k - 1) // 2:   # the tap-sum route takes 'same' convolutions only
+        yt = ops.tap_conv_fwd(xn, ops.weight_pack(wd, ops.PACK_CK), bp, k, pad, mode, act=act)
+        _close(yh, yt, tol=CONV_TOL[conv_math], what="vs 1x1 conv + full tap sum")
+
+
 @pytest.mark.parametrize("ci,co,k,mode", [(3, 64, 7, "reflect"), (2, 64, 7, "reflect"), (3, 32, 3, "zero"),
                                           (3, 64, 7, "zero")])
 def test_tap_conv_dgrad(ops, conv_math, ci, co, k, mode):

@@ -131,9 +131,16 @@ class CycleGANModel(BaseModel):
             B, H, W, _ = img1.shape
             padder = InputPadder((B, 3, H, W))
             if getattr(self.raftModel, "use_graphs", False):
-                return self.raftModel.graphed(img1.detach(), img2.detach(), it, padder.pads, nhwc=True)[1]
-            _, flow_up = self.raftModel(img1.detach(), img2.detach(), iters=it, test_mode=True, pads=padder.pads,
-                                        nhwc=True)
+                flow_up = self.raftModel.graphed(img1.detach(), img2.detach(), it, padder.pads, nhwc=True)[1]
+            else:
+                _, flow_up = self.raftModel(img1.detach(), img2.detach(), iters=it, test_mode=True, pads=padder.pads,
+                                            nhwc=True)
+            l, r, t, b = padder.pads
+            if l or r or t or b:
+                # the reference returns the padded flow_up (:128-134) and then warps / compares it with the
+                # unpadded frames, which fails for frames that are not multiples of 8 (1024x436: 440 rows);
+                # the flow is cut back to the frame here (InputPadder.unpad), as the oracle does
+                flow_up = flow_up[:, t:flow_up.shape[1] - b, l:flow_up.shape[2] - r].contiguous()
         return flow_up
 
     # ------------------------------------------------------------------------------- inputs

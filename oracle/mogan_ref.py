@@ -48,11 +48,15 @@ class RefMoGAN:
                 p.requires_grad_(flag)
 
     def raft(self, a, b):
+        """computeRAFT (:128-134).  The reference returns flow_up at the padded size, which its warp /
+        motion losses cannot take for frames that are not multiples of 8 (1024x436 pads to 440 rows);
+        the flow is cut back to the frame (InputPadder.unpad), the build's defined behaviour there."""
         with torch.no_grad():
             pads = raft_ref.input_pads(a.shape)
             _, up = raft_ref.raft_forward(self.raft_sd, raft_ref.pad_replicate(a, pads),
                                           raft_ref.pad_replicate(b, pads), iters=self.raft_iters, test_mode=True)
-        return up
+        l, r, t, bt = pads
+        return up[..., t:up.shape[-2] - bt, l:up.shape[-1] - r]
 
     def set_input_fc2(self, img1, img2, simg1, simg2):
         self.real_A, self.real_A2, self.real_B, self.real_B2 = img1, img2, simg1, simg2

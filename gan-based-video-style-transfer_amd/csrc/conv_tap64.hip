@@ -69,14 +69,19 @@ __device__ __forceinline__ void split(const float4& a, const float4& b, bf16x8_t
 // x: NHWC [N][H][W][64]; ws: the VST_PACK_SOK pack's NP bf16 planes [28][R][64] (plane stride wps);
 // y: NHWC4 [N][Ho][Wo][4].  Rows of the R x 1 conv are padded by `pad` (reflect or zero), Ho = H + 2 pad
 // - R + 1; the column taps read z column src(p + s - pad) (reflected, or zero outside [0, W)), Wo = W +
-// 2 pad - R + 1.  W divides GQ: a group is RI = GQ / W whole rows; T = N * Ho rows in all.
-template <int NP, int ACT, bool REFL>
+// 2 pad - R + 1.  A group is RI = GQ / W consecutive output rows of one image (gpi groups per image, the
+// last one's rows past Ho computed and dropped).  Wave w owns z column blocks [w CBW, (w+1) CBW) of all
+// RI rows, so output row rho's K-step (r, c) reads input row ho0 + rho + r - pad: the split fragments of
+// input row j = rho + r are shared by the RI rows as r advances (a window of RI rows, one new row split
+// per K-step instead of RI), and the loads / split VALU per MFMA drop RI-fold.
+template <int NP, int ACT, bool REFL, int RI>
 __global__ __launch_bounds__(NT, 1) void tap64_k(const float* __restrict__ x, const __bf16* __restrict__ ws, long wps,
                                                  const float* __restrict__ bias, float* __restrict__ y, int H, int W,
-                                                 int Ho, int Wo, int pad, float slope, int T, int groups, int nimg) {
+                                                 int Ho, int Wo, int pad, float slope, int gpi, int groups, int nimg) {
+  constexpr int CBW = MBW / RI;  // column blocks per wave
+  static_assert(CBW * RI == MBW, "RI divides the wave's M-blocks");
   __shared__ __attribute__((aligned(16))) float zl[GQ * ZS];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int RI = GQ / W;
   const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<float*>(x), 0, nimg * H * W * CI * (int)sizeof(float), 0x00020000);
   const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
@@ -88,102 +93,120 @@ __global__ __launch_bounds__(NT, 1) void tap64_k(const float* __restrict__ x, co
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int n = 16 * j + (lane & 15);
-    boff[j] = n < NZ ? n * R * CI + 8 * kc : -1;
+    boff[j] = n < NZ ? (n * R * CI + 8 * kc) * 2 : -1;  // bytes
   }
-  auto load_b = [&](int k, bf16x8_t (&b)[2][NP]) __attribute__((always_inline)) {
-    const int r = k >> 1, ch = (k & 1) * 32;
+  const int wpsb = (int)(wps * 2);
+  auto load_b = [&](int r, int c, bf16x8_t (&b)[2][NP]) __attribute__((always_inline)) {
+    const int kb = (r * CI + 32 * c) * 2;
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int p = 0; p < NP; ++p) {
-        const int off = boff[j] >= 0 ? (int)((p * wps + boff[j] + r * CI + ch) * 2) : 0x7ffffff0;
+        const int off = boff[j] >= 0 ? p * wpsb + boff[j] + kb : 0x7ffffff0;
         b[j][p] = __builtin_bit_cast(bf16x8_t, __builtin_amdgcn_raw_buffer_load_b128(wrs, off, 0, 0));
       }
   };
+  // this lane's z columns (one per column block) and their byte offsets inside an input row
+  int colb[CBW];
+#pragma unroll
+  for (int cb = 0; cb < CBW; ++cb) colb[cb] = ((16 * (wave * CBW + cb) + (lane & 15)) * CI + 8 * kc) * (int)sizeof(float);
+  const int rowb = W * CI * (int)sizeof(float);
 
   for (int g = blockIdx.x; g < groups; g += gridDim.x) {
-    // this lane's pixel of each of the wave's M-blocks: row t0 + rho, column q
-    int img[MBW], hrow[MBW], col[MBW];
-#pragma unroll
-    for (int m = 0; m < MBW; ++m) {
-      const int qq = 16 * (wave * MBW + m) + (lane & 15);
-      const int rho = qq / W, q = qq - rho * W;
-      const int tr = g * RI + rho;
-      const int n = tr / Ho, ho = tr - n * Ho;
-      img[m] = tr < T ? n : -1;  // a row past the end gathers zeros (its outputs are not stored)
-      hrow[m] = ho - pad;
-      col[m] = q;
-    }
-    auto a_off = [&](int m, int k) __attribute__((always_inline)) {
-      const int r = k >> 1, ch = (k & 1) * 32 + 8 * kc;
-      int h = hrow[m] + r;
-      bool ok = img[m] >= 0;
+    const int n = g / gpi, ho0 = (g - n * gpi) * RI;
+    // byte offset of window row j (input row ho0 + j - pad) of image n, or -1 for a zero-padding row
+    auto row_off = [&](int j) __attribute__((always_inline)) {
+      int h = ho0 + j - pad;
+      bool ok = true;
       if constexpr (REFL) {
         h = reflect_idx(h, H);
       } else {
-        ok = ok && (unsigned)h < (unsigned)H;
+        ok = (unsigned)h < (unsigned)H;
       }
-      return ok ? (((img[m] * H + h) * W + col[m]) * CI + ch) * (int)sizeof(float) : (int)0x7ffffff0;
+      return ok ? (n * H + h) * rowb : -1;
     };
-    float4 a[MBW][2];
+    auto load_raw = [&](int j, int c, float4 (&raw)[CBW][2]) __attribute__((always_inline)) {
+      const int ro = row_off(j);
 #pragma unroll
-    for (int m = 0; m < MBW; ++m) {
-      const int off = a_off(m, 0);
-      a[m][0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
-      a[m][1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off + 16, 0, 0));
-    }
-    bf16x8_t b[2][NP], bn[2][NP];
-    load_b(0, b);
-    f32x4v acc[MBW][2];
+      for (int cb = 0; cb < CBW; ++cb) {
+        const int off = ro >= 0 ? ro + colb[cb] + 128 * c : (int)0x7ffffff0;
+        raw[cb][0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
+        raw[cb][1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off + 16, 0, 0));
+      }
+    };
+    f32x4v acc[RI][CBW][2];
 #pragma unroll
-    for (int m = 0; m < MBW; ++m)
+    for (int rho = 0; rho < RI; ++rho)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) acc[m][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
+      for (int cb = 0; cb < CBW; ++cb)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[rho][cb][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
 #pragma unroll 1
-    for (int k = 0; k < KS; ++k) {
-      const int kn = k + 1 < KS ? k + 1 : k;  // the last step re-loads (never used): no branch
-      load_b(kn, bn);
+    for (int c = 0; c < 2; ++c) {
+      bf16x8_t F[RI + R - 1][CBW][NP];  // window rows j = rho + r (live: RI at a time)
+      {
+        float4 raw[RI][CBW][2];
 #pragma unroll
-      for (int m = 0; m < MBW; ++m) {
-        bf16x8_t ap[NP];
-        split<NP>(a[m][0], a[m][1], ap);
-        const int off = a_off(m, kn);
-        a[m][0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
-        a[m][1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off + 16, 0, 0));
+        for (int j = 0; j < RI; ++j) load_raw(j, c, raw[j]);
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          // (A plane, B plane) terms of the x6 / x3 sums (conv_fprop_bf_k's set)
-#define VST_T64(pa, pb) acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ap[pa], b[j][pb], acc[m][j], 0, 0, 0)
-          if constexpr (NP == 3) {
-            VST_T64(1, 1); VST_T64(1, 0); VST_T64(0, 1); VST_T64(0, 0); VST_T64(2, 0); VST_T64(0, 2);
-          } else {
-            VST_T64(1, 0); VST_T64(0, 1); VST_T64(0, 0);
-          }
+        for (int j = 0; j < RI; ++j)
+#pragma unroll
+          for (int cb = 0; cb < CBW; ++cb) split<NP>(raw[j][cb][0], raw[j][cb][1], F[j][cb]);
+      }
+      bf16x8_t b[2][NP], bn[2][NP];
+      load_b(0, c, b);
+      float4 rn[CBW][2];
+      load_raw(RI, c, rn);
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        if (r + 1 < R) load_b(r + 1, c, bn);
+        if (r >= 1) {
+#pragma unroll
+          for (int cb = 0; cb < CBW; ++cb) split<NP>(rn[cb][0], rn[cb][1], F[r + RI - 1][cb]);
+          if (r + 1 < R) load_raw(r + RI, c, rn);
+        }
+#pragma unroll
+        for (int rho = 0; rho < RI; ++rho)
+#pragma unroll
+          for (int cb = 0; cb < CBW; ++cb)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              const bf16x8_t(&ap)[NP] = F[rho + r][cb];
+              // (A plane, B plane) terms of the x6 / x3 sums (conv_fprop_bf_k's set)
+#define VST_T64(pa, pb) acc[rho][cb][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ap[pa], b[j][pb], acc[rho][cb][j], 0, 0, 0)
+              if constexpr (NP == 3) {
+                VST_T64(1, 1); VST_T64(1, 0); VST_T64(0, 1); VST_T64(0, 0); VST_T64(2, 0); VST_T64(0, 2);
+              } else {
+                VST_T64(1, 0); VST_T64(0, 1); VST_T64(0, 0);
+              }
 #undef VST_T64
+            }
+        if (r + 1 < R) {
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int p = 0; p < NP; ++p) b[j][p] = bn[j][p];
         }
       }
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int p = 0; p < NP; ++p) b[j][p] = bn[j][p];
     }
     // z -> LDS: lane (column 16 j + (lane & 15), rows 4 (lane >> 4) + i) of each accumulator block
 #pragma unroll
-    for (int m = 0; m < MBW; ++m)
+    for (int rho = 0; rho < RI; ++rho)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int cb = 0; cb < CBW; ++cb)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int qq = 16 * (wave * MBW + m) + 4 * (lane >> 4) + i;
-          zl[qq * ZS + 16 * j + (lane & 15)] = acc[m][j][i];
-        }
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int qq = rho * W + 16 * (wave * CBW + cb) + 4 * (lane >> 4) + i;
+            zl[qq * ZS + 16 * j + (lane & 15)] = acc[rho][cb][j][i];
+          }
     __syncthreads();
     // column taps: output pixel (rho, p) of the group, bias then s = 0..6 in order (tapsum_h_k)
-    const int outs = RI * Wo;
+    const int rows = Ho - ho0 < RI ? Ho - ho0 : RI;
+    const int outs = rows * Wo;
     for (int e = t; e < outs; e += NT) {
       const int rho = e / Wo, p = e - rho * Wo;
-      const int tr = g * RI + rho;
-      if (tr >= T) break;
       float4 v = bv;
 #pragma unroll
       for (int s = 0; s < R; ++s) {
@@ -199,7 +222,7 @@ __global__ __launch_bounds__(NT, 1) void tap64_k(const float* __restrict__ x, co
         v.z += zv.z;
         v.w += zv.w;
       }
-      const long o = ((long)tr * Wo + p) * 4;
+      const long o = (((long)n * Ho + ho0 + rho) * Wo + p) * 4;
       *reinterpret_cast<float4*>(y + o) = make_float4(apply_act(v.x, ACT, slope), apply_act(v.y, ACT, slope),
                                                       apply_act(v.z, ACT, slope), apply_act(v.w, ACT, slope));
     }
@@ -215,9 +238,9 @@ static const bool g_tap64 = [] {
 }();
 
 // Does the direct kernel take this tap conv?  64 input channels, 7 x 7, 4 (padded) outputs, x6 / x3
-// math, W a multiple of 16 dividing 1024 (a group is whole rows), reflect 'same' or zero padding.
+// math, W in {256, 512, 1024} (a group is 1024 / W whole rows), reflect 'same' or zero padding.
 bool tap64_ok(int Cx, int R, int W, int math) {
-  return g_tap64 && Cx == tap64::CI && R == tap64::R && W % 16 == 0 && tap64::GQ % W == 0 &&
+  return g_tap64 && Cx == tap64::CI && R == tap64::R && W % 256 == 0 && tap64::GQ % W == 0 &&
          (math == VST_MATH_BF16X6 || math == VST_MATH_BF16X3);
 }
 
@@ -225,22 +248,28 @@ int tap64_launch(const float* x, const void* wsplit, long wps, const float* bias
                  int pad, int reflect, int act, float slope, int math, hipStream_t s) {
   const int Ho = H + 2 * pad - tap64::R + 1, Wo = W + 2 * pad - tap64::R + 1;
   VST_REQUIRE(Ho > 0 && Wo > 0 && (!reflect || (pad < H && pad < W)), "tap64: bad padding");
+  VST_REQUIRE(W % 256 == 0 && tap64::GQ % W == 0, "tap64: W must be 256, 512 or 1024");
   VST_REQUIRE((long)N * H * W * tap64::CI * 4 < 0x7ffffff0L, "tap64: input over 2 GB (32-bit buffer offsets)");
-  const int RI = tap64::GQ / W, T = N * Ho, groups = (T + RI - 1) / RI;
+  const int RI = tap64::GQ / W, gpi = (Ho + RI - 1) / RI, groups = N * gpi;
   const int grid = groups < VST_NUM_CUS ? groups : VST_NUM_CUS;
   const __bf16* ws = reinterpret_cast<const __bf16*>(wsplit);
-#define VST_T64K(NP_, ACT_)                                                                                      \
-  if (reflect)                                                                                                    \
-    hipLaunchKernelGGL((tap64::tap64_k<NP_, ACT_, true>), dim3(grid), dim3(tap64::NT), 0, s, x, ws, wps, bias, y, H, \
-                       W, Ho, Wo, pad, slope, T, groups, N);                                                      \
-  else                                                                                                            \
-    hipLaunchKernelGGL((tap64::tap64_k<NP_, ACT_, false>), dim3(grid), dim3(tap64::NT), 0, s, x, ws, wps, bias, y, H, \
-                       W, Ho, Wo, pad, slope, T, groups, N)
-#define VST_T64K_ACT(NP_)                            \
-  switch (act) {                                     \
-    case VST_ACT_TANH: VST_T64K(NP_, VST_ACT_TANH); break; \
-    case VST_ACT_NONE: VST_T64K(NP_, VST_ACT_NONE); break; \
-    default: return VST_EUNSUPPORTED;                \
+#define VST_T64K_R(NP_, ACT_, REFL_, RI_)                                                                          \
+  hipLaunchKernelGGL((tap64::tap64_k<NP_, ACT_, REFL_, RI_>), dim3(grid), dim3(tap64::NT), 0, s, x, ws, wps, bias, y, \
+                     H, W, Ho, Wo, pad, slope, gpi, groups, N)
+#define VST_T64K(NP_, ACT_)                                  \
+  switch (RI * 2 + (reflect ? 1 : 0)) {                       \
+    case 2: VST_T64K_R(NP_, ACT_, false, 1); break;           \
+    case 3: VST_T64K_R(NP_, ACT_, true, 1); break;            \
+    case 4: VST_T64K_R(NP_, ACT_, false, 2); break;           \
+    case 5: VST_T64K_R(NP_, ACT_, true, 2); break;            \
+    case 8: VST_T64K_R(NP_, ACT_, false, 4); break;           \
+    default: VST_T64K_R(NP_, ACT_, true, 4); break;           \
+  }
+#define VST_T64K_ACT(NP_)                                    \
+  switch (act) {                                             \
+    case VST_ACT_TANH: VST_T64K(NP_, VST_ACT_TANH); break;   \
+    case VST_ACT_NONE: VST_T64K(NP_, VST_ACT_NONE); break;   \
+    default: return VST_EUNSUPPORTED;                        \
   }
   if (math == VST_MATH_BF16X6) {
     VST_T64K_ACT(3)
@@ -249,6 +278,7 @@ int tap64_launch(const float* x, const void* wsplit, long wps, const float* bias
   }
 #undef VST_T64K_ACT
 #undef VST_T64K
+#undef VST_T64K_R
   return check_launch("tapconv64 (direct)");
 }
 

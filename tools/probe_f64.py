@@ -8,7 +8,7 @@ import torch.nn.functional as F
 dev = torch.device("cuda")
 for dt in (torch.float32, torch.float64):
     x = torch.randn(8, 256, 64, 64, device=dev, dtype=dt, requires_grad=True)
-    w = torch.randn(256, 256, 3, 3, device=dev, dtype=dt, requires_grad=True) * 0.02
+    w = (torch.randn(256, 256, 3, 3, device=dev, dtype=dt) * 0.02).requires_grad_(True)
     for _ in range(2):
         y = F.conv2d(F.pad(x, (1,) * 4, mode="reflect"), w)
         y.sum().backward()

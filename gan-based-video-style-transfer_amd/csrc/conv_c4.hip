@@ -22,6 +22,16 @@
 
 #include <type_traits>
 
+#ifndef VST_C4_NOCOMPUTE
+#define VST_C4_NOCOMPUTE 0  // developer timing experiment only: no MFMAs (WRONG results)
+#endif
+#ifndef VST_C4_NOSTORE
+#define VST_C4_NOSTORE 0    // developer timing experiment only: every output / partial store dropped
+#endif
+#if (VST_C4_NOCOMPUTE || VST_C4_NOSTORE) && !defined(VST_DEV_VARIANT)
+#error "VST_C4_NOCOMPUTE / VST_C4_NOSTORE are developer-only timing modes: build them with tools/build_variant.py"
+#endif
+
 namespace vst {
 namespace c4 {
 
@@ -233,10 +243,10 @@ __global__ __launch_bounds__(NT, 1) void conv_c4_direct_k(const float* __restric
   auto epilogue = [&](const Seg& cs, bool live) __attribute__((always_inline)) {
     const float* yseg = y + (((long)cs.n * Ho + cs.ho) * Wo + cs.wo0) * COP;
     const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(yseg), 0, live ? cs.L * COP * (int)sizeof(float) : 0, 0x00020000);
+        const_cast<float*>(yseg), 0, live && !VST_C4_NOSTORE ? cs.L * COP * (int)sizeof(float) : 0, 0x00020000);
     const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
         part ? part + (long)cs.n * (HWo >> 5) * COP * 2 : nullptr, 0,
-        part && live ? (HWo >> 5) * COP * 2 * (int)sizeof(double) : 0, 0x00020000);
+        part && live && !VST_C4_NOSTORE ? (HWo >> 5) * COP * 2 * (int)sizeof(double) : 0, 0x00020000);
     const int pskip = 32 * sub < cs.L ? 0 : (1 << 30);  // a sub-tile past the segment: no partials
     const int z = (cs.ho * Wo + cs.wo0 + 32 * sub) >> 5;
 #pragma unroll
@@ -314,11 +324,282 @@ __global__ __launch_bounds__(NT, 1) void conv_c4_direct_k(const float* __restric
     __builtin_amdgcn_sched_barrier(0);  // keep the loads ahead of the stores
     epilogue(prev, have_prev);
     if (tile >= T) break;
-    if (32 * sub < cur.L) compute();  // no VMEM inside: a branch here costs no wait
+    if (32 * sub < cur.L && !VST_C4_NOCOMPUTE) compute();  // no VMEM inside: a branch here costs no wait
     prev = cur;
     have_prev = true;
     tile = nxt;
   }
+}
+
+// Row-ring form of the same conv (VST_C4_RING, default): a block owns a run of consecutive output rows
+// of one image column segment, so segment ho + 1 reads six of segment ho's seven input rows.  The patch
+// is a ring of MAXR = 8 row slots (padded row pr in slot pr & 7): each segment stages ONE new input row
+// (segment ho + 1's last, into the slot segment ho - 1 freed) while segment ho computes, instead of all
+// seven rows between two barriers — one barrier per segment, 1/7 of the split / ds_write work.  The
+// eight waves run as two groups, one wave of each per SIMD: group 0 computes segment ho then runs its
+// epilogue, group 1 runs segment ho - 1's epilogue then computes segment ho, so one wave's MFMAs overlap
+// the other's epilogue VALU and stores on every SIMD (the lock-step form serialised them: the MFMAs
+// were ~55 of 102 us at N = 8, everything else ~48).  A run that enters a new (image, column segment)
+// restages all seven rows behind a barrier.  Same products, order and epilogue as conv_c4_direct_k.
+template <int NP, int R, int ACT>
+__global__ __launch_bounds__(NT, 1) void conv_c4_ring_k(const float* __restrict__ x, const __bf16* __restrict__ ws,
+                                                         long wps, const float* __restrict__ bias,
+                                                         float* __restrict__ y, int H, int W, int Ho, int Wo,
+                                                         int S, int pad, int reflect, float slope, int nseg, int T,
+                                                         int per, int nimg, double* __restrict__ part) {
+  static_assert(R < MAXR && MAXR == 8, "ring: a free slot, slot = padded row & 7");
+  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+  char* patch = smem;                      // [NP][8 slots][PW][4] bf16
+  char* wl = smem + 3 * PATCH_PLANE;       // [NP][R][kq 4][64][8] bf16
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int K = R * S * 4;
+  const int tb = blockIdx.x * per;
+  const int te = tb + per < T ? tb + per : T;
+
+  {  // weights -> LDS once (as conv_c4_direct_k)
+    constexpr int NCH = NP * R * 4 * COP, PER = (NCH + NT - 1) / NT;
+    const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<__bf16*>(ws), 0, (int)((NP - 1) * wps * 2 + (long)COP * K * 2), 0x00020000);
+    u32x2v lo[PER], hi[PER];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int e = t + u * NT;
+      const int p = e / (R * 4 * COP), rem = e - p * R * 4 * COP;
+      const int r = rem / (4 * COP), kq = (rem / COP) & 3, co = rem % COP;
+      const int base = (int)((p * wps + (long)co * K + r * S * 4) * 2);
+      const bool in = e < NCH;
+      lo[u] = __builtin_amdgcn_raw_buffer_load_b64(wrs, in && 2 * kq < S ? base + 2 * kq * 8 : 0x7ffffff0, 0, 0);
+      hi[u] = __builtin_amdgcn_raw_buffer_load_b64(wrs, in && 2 * kq + 1 < S ? base + (2 * kq + 1) * 8 : 0x7ffffff0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int e = t + u * NT;
+      if (e >= NCH) continue;
+      const int p = e / (R * 4 * COP), rem = e - p * R * 4 * COP;
+      const int r = rem / (4 * COP), kq = (rem / COP) & 3, co = rem % COP;
+      *reinterpret_cast<uint4*>(wl + p * W_PLANE + ((r * 4 + kq) * COP + co) * 16) =
+          make_uint4(lo[u][0], lo[u][1], hi[u][0], hi[u][1]);
+    }
+  }
+
+  // segment s -> image n, column segment q, output row ho (ho fastest: a block's run walks rows)
+  auto segof = [&](int s) __attribute__((always_inline)) {
+    Seg g;
+    g.ho = s % Ho;
+    const int rest = s / Ho, q = rest % nseg;
+    g.n = rest / nseg;
+    g.wo0 = q * SEG;
+    g.L = q == nseg - 1 ? Wo - g.wo0 : SEG;
+    return g;
+  };
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(x), 0, nimg * H * W * 16, 0x00020000);
+  // byte offset of patch element (padded row pr, column c) of segment g; out of the frame (zero padding)
+  // or past the columns the segment reads: an offset past the descriptor's range (reads zero)
+  auto xoff = [&](const Seg& g, int pr, int c) __attribute__((always_inline)) {
+    int hi = pr - pad, wi = g.wo0 - pad + c;
+    bool ok;
+    if (reflect) {
+      hi = reflect_idx(hi, H);
+      wi = reflect_idx(wi, W);
+      ok = (unsigned)wi < (unsigned)W;
+    } else {
+      ok = (unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W;
+    }
+    ok = ok && c < g.L + 7;
+    return ok ? ((g.n * H + hi) * W + wi) * 16 : (int)0x7ffffff0;
+  };
+  // split one float4 (4 channels of a patch pixel) into the NP planes of slot pr & 7, column c
+  auto put = [&](int pr, int c, const float4& v) __attribute__((always_inline)) {
+    char* dst = patch + ((pr & 7) * PW + c) * 8;
+    float a[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const uint32_t q0 = pack2(a[0], a[1]), q1 = pack2(a[2], a[3]);
+      *reinterpret_cast<uint2*>(dst + p * PATCH_PLANE) = make_uint2(q0, q1);
+      if (p + 1 < NP) {
+        a[0] -= __uint_as_float(q0 << 16);
+        a[1] -= __uint_as_float(q0 & 0xffff0000u);
+        a[2] -= __uint_as_float(q1 << 16);
+        a[3] -= __uint_as_float(q1 & 0xffff0000u);
+      }
+    }
+  };
+  // all R rows of segment g (elements past them land in the free slot g.ho + R)
+  auto full_stage = [&](const Seg& g) __attribute__((always_inline)) {
+    constexpr int FP = (R * (SEG + 7) + NT - 1) / NT;
+    const int cols = g.L + 7;
+    float4 pf[FP];
+#pragma unroll
+    for (int i = 0; i < FP; ++i) {
+      const int e = t + i * NT, r = e / cols, c = e - r * cols;
+      pf[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                             xrs, r < R ? xoff(g, g.ho + r, c) : (int)0x7ffffff0, 0, 0));
+    }
+#pragma unroll
+    for (int i = 0; i < FP; ++i) {
+      const int e = t + i * NT, r = e / cols, c = e - r * cols;
+      put(g.ho + (r < R ? r : R), c < PW ? c : PW - 1, pf[i]);
+    }
+  };
+  // one padded row of segment g's columns: thread t = column t (threads past the row write column
+  // PW - 1 with zeros, a column no fragment reads)
+  auto load_row = [&](const Seg& g, int pr) __attribute__((always_inline)) {
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xrs, xoff(g, pr, t), 0, 0));
+  };
+  auto put_row = [&](int pr, const float4& v) __attribute__((always_inline)) { put(pr, t < PW ? t : PW - 1, v); };
+
+  float4 bvs[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c0 = 16 * j + 4 * (lane >> 4);
+    bvs[j] = bias ? make_float4(bias[c0], bias[c0 + 1], bias[c0 + 2], bias[c0 + 3]) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  const int kq = lane >> 4;
+  const int sub = wave;      // this wave's 32-pixel sub-tile of every segment
+  // one wave of each group per SIMD; an SGPR value, so `grp` branches are scalar (two exclusive paths,
+  // each with its own counted waits) rather than exec-masked sequences of both
+  const int grp = __builtin_amdgcn_readfirstlane(wave >> 2);
+  const int HWo = Ho * Wo;
+  f32x4v acc[2][4];
+
+  struct Fr {
+    bf16x8_t w[NP][4], x[NP][2];
+  };
+  auto load_fr = [&](Fr& f, int ho, int r) __attribute__((always_inline)) {
+    const char* rowp = patch + ((ho + r) & 7) * PW * 8;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int pc = 32 * sub + 16 * i + (lane & 15) + 2 * kq;
+      const char* src = rowp + pc * 8;
+#pragma unroll
+      for (int p = 0; p < NP; ++p) {
+        const uint2 lo = *reinterpret_cast<const uint2*>(src + p * PATCH_PLANE);
+        const uint2 hi = *reinterpret_cast<const uint2*>(src + p * PATCH_PLANE + 8);
+        f.x[p][i] = __builtin_bit_cast(bf16x8_t, make_uint4(lo.x, lo.y, hi.x, hi.y));
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int p = 0; p < NP; ++p)
+        f.w[p][j] = *reinterpret_cast<const bf16x8_t*>(wl + p * W_PLANE + ((r * 4 + kq) * COP + 16 * j + (lane & 15)) * 16);
+  };
+  auto compute = [&](int ho) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
+    Fr fr[2];
+    load_fr(fr[0], ho, 0);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const Fr& f = fr[r & 1];
+      if (r + 1 < R) load_fr(fr[(r + 1) & 1], ho, r + 1);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+#define VST_C4MF(pa, pb) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.w[pb][j], f.x[pa][i], acc[i][j], 0, 0, 0)
+          if constexpr (NP == 3) {
+            VST_C4MF(1, 1); VST_C4MF(1, 0); VST_C4MF(0, 1); VST_C4MF(0, 0); VST_C4MF(2, 0); VST_C4MF(0, 2);
+          } else {
+            VST_C4MF(1, 0); VST_C4MF(0, 1); VST_C4MF(0, 0);
+          }
+#undef VST_C4MF
+        }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  auto epilogue = [&](const Seg& cs, bool live) __attribute__((always_inline)) {
+    const float* yseg = y + (((long)cs.n * Ho + cs.ho) * Wo + cs.wo0) * COP;
+    const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(yseg), 0, live && !VST_C4_NOSTORE ? cs.L * COP * (int)sizeof(float) : 0, 0x00020000);
+    const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
+        part ? part + (long)cs.n * (HWo >> 5) * COP * 2 : nullptr, 0,
+        part && live && !VST_C4_NOSTORE ? (HWo >> 5) * COP * 2 * (int)sizeof(double) : 0, 0x00020000);
+    const int pskip = 32 * sub < cs.L ? 0 : (1 << 30);
+    const int z = (cs.ho * Wo + cs.wo0 + 32 * sub) >> 5;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c0 = 16 * j + 4 * kq;
+      const float4 bv = bvs[j];
+      float v[2][4];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int px = 32 * sub + 16 * i + (lane & 15);
+        v[i][0] = apply_act(acc[i][j][0] + bv.x, ACT, slope);
+        v[i][1] = apply_act(acc[i][j][1] + bv.y, ACT, slope);
+        v[i][2] = apply_act(acc[i][j][2] + bv.z, ACT, slope);
+        v[i][3] = apply_act(acc[i][j][3] + bv.w, ACT, slope);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, f32x4v{v[i][0], v[i][1], v[i][2], v[i][3]}),
+                                               yrs, (px * COP + c0) * (int)sizeof(float), 0, 0);
+      }
+      double d[8];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        d[2 * q] = (double)v[0][q] + (double)v[1][q];
+        d[2 * q + 1] = (double)v[0][q] * v[0][q] + (double)v[1][q] * v[1][q];
+      }
+      auto half = [&](auto M, auto Nn) __attribute__((always_inline)) {
+        constexpr int m = decltype(M)::value, n = decltype(Nn)::value;
+        const bool up = (lane & m) != 0;
+#pragma unroll
+        for (int u = 0; u < n / 2; ++u) {
+          const double send = up ? d[u] : d[u + n / 2];
+          const double keep = up ? d[u + n / 2] : d[u];
+          d[u] = keep + __shfl_xor(send, m);
+        }
+      };
+      half(std::integral_constant<int, 8>(), std::integral_constant<int, 8>());
+      half(std::integral_constant<int, 4>(), std::integral_constant<int, 4>());
+      half(std::integral_constant<int, 2>(), std::integral_constant<int, 2>());
+      d[0] += __shfl_xor(d[0], 1);
+      const int co = c0 + 2 * ((lane >> 3) & 1) + ((lane >> 2) & 1);
+      const int off = ((z * COP + co) * 2 + ((lane >> 1) & 1)) * (int)sizeof(double) + pskip;
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2v, d[0]), prs, off, 0, 0);
+    }
+  };
+
+  if (tb >= T) return;  // block-uniform, before any barrier
+  Seg g = segof(tb);
+  full_stage(g);
+  float4 prow = load_row(g, g.ho + R);  // segment tb + 1's last row
+  // every path into the loop head carries the prefetch load followed by one epilogue's 12 stores (here
+  // dropped ones), so the wait before put_row stays vmcnt(12) instead of draining the stores
+  __builtin_amdgcn_sched_barrier(0);
+  epilogue(g, false);
+  __syncthreads();
+  Seg prev = g;
+  bool have_prev = false;
+  for (int s = tb; s < te; ++s) {
+    const Seg cur = g;
+    // the prefetched row into its slot ((cur.ho + R) & 7 = (cur.ho - 1) & 7: segment s - 1's first row,
+    // free since the last barrier); junk when segment s + 1 starts a new run (restaged below)
+    put_row(cur.ho + R, prow);
+    prow = load_row(cur, cur.ho + R + 1);  // segment s + 2's last row
+    if (grp == 0) {
+      if (32 * sub < cur.L && !VST_C4_NOCOMPUTE) compute(cur.ho);
+      epilogue(cur, true);
+    } else {
+      epilogue(prev, have_prev);
+      if (32 * sub < cur.L && !VST_C4_NOCOMPUTE) compute(cur.ho);
+    }
+    prev = cur;
+    have_prev = true;
+    __syncthreads();  // segment s read, row cur.ho + R + ... written
+    if (s + 1 < te) {
+      g = segof(s + 1);
+      if (g.ho == 0) {  // a new image / column segment: all R rows (block-uniform)
+        full_stage(g);
+        prow = load_row(g, g.ho + R);
+        __builtin_amdgcn_sched_barrier(0);
+        epilogue(g, false);
+        __syncthreads();
+      }
+    }
+  }
+  if (grp == 1) epilogue(prev, have_prev);
 }
 
 }  // namespace c4
@@ -330,6 +611,10 @@ __global__ __launch_bounds__(NT, 1) void conv_c4_direct_k(const float* __restric
 // partials) must also have Wo % 32 == 0: a conv is routed the same way with and without partials.
 static const bool g_c4_direct = [] {
   const char* e = getenv("VST_C4_DIRECT");
+  return !(e && e[0] == '0');
+}();
+static const bool g_c4_ring = [] {
+  const char* e = getenv("VST_C4_RING");
   return !(e && e[0] == '0');
 }();
 
@@ -348,12 +633,17 @@ int c4_direct_launch(const float* x, const void* wsplit, long wps, const float* 
   VST_REQUIRE((long)N * H * W * 16 < 0x7ffffff0L, "conv_c4_direct: input over 2 GB (32-bit buffer offsets)");
   const int T = N * Ho * nseg;
   const int grid = T < VST_NUM_CUS ? T : VST_NUM_CUS;
+  const int per = (T + VST_NUM_CUS - 1) / VST_NUM_CUS, rgrid = (T + per - 1) / per;
   const __bf16* ws = reinterpret_cast<const __bf16*>(wsplit);
   // the activation is a template argument: a runtime one makes every epilogue element evaluate all
   // of them (tanh included) and select
-#define VST_C4D(NP_, ACT_)                                                                                         \
-  hipLaunchKernelGGL((c4::conv_c4_direct_k<NP_, 7, ACT_>), dim3(grid), dim3(c4::NT), 0, s, x, ws, wps, bias, y, H, W, \
-                     Ho, Wo, S, pad, reflect, slope, nseg, T, N, part)
+#define VST_C4D(NP_, ACT_)                                                                                      \
+  if (g_c4_ring)                                                                                                \
+    hipLaunchKernelGGL((c4::conv_c4_ring_k<NP_, 7, ACT_>), dim3(rgrid), dim3(c4::NT), 0, s, x, ws, wps, bias, y, H,  \
+                       W, Ho, Wo, S, pad, reflect, slope, nseg, T, per, N, part);                                \
+  else                                                                                                          \
+    hipLaunchKernelGGL((c4::conv_c4_direct_k<NP_, 7, ACT_>), dim3(grid), dim3(c4::NT), 0, s, x, ws, wps, bias, y, H, \
+                       W, Ho, Wo, S, pad, reflect, slope, nseg, T, N, part)
 #define VST_C4D_ACT(NP_)                                \
   switch (act) {                                        \
     case VST_ACT_RELU: VST_C4D(NP_, VST_ACT_RELU); break;   \

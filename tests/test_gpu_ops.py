@@ -919,6 +919,9 @@ def test_dgrad_reflect_border(ops, conv_math, case):
     (1, 20, 512, 3, "reflect", "relu"),    # two 256-pixel segments per row
     (3, 20, 18, 3, "reflect", "lrelu"),    # a partial 32-row sub-tile
     (2, 64, 64, 3, "reflect", "tanh"),
+    # row-ring runs (conv_c4_ring_k: a block owns per = ceil(T / CUs) consecutive row segments):
+    (3, 175, 256, 3, "reflect", "none"),   # per 3, runs crossing image boundaries (a restage mid-run)
+    (12, 256, 256, 3, "reflect", "none"),  # per 12: the train step's N=12 c0
 ], ids=lambda s: "x".join(str(v) for v in s))
 def test_conv_c4_direct(ops, shape, conv_math):
     """The patch-staged direct kernel for 4-channel inputs with 64 outputs (conv_c4.hip; the generator's

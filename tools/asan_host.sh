@@ -1,12 +1,12 @@
 #!/bin/bash
 # Host AddressSanitizer run of the C-ABI's host code: builds the library with
 # -fsanitize=address on the HOST side only (-Xarch_host; GPU ASan is not available on this pool) into
-# _build/variants/libvst_hip_asan.so, then runs the CPU host tests (tests/test_cpu_host.py: symbol
+# _build/asan/libvst_hip_asan.so, then runs the CPU host tests (tests/test_cpu_host.py: symbol
 # export, the conv / wgrad planners, descriptor validation, workspace sizing) plus the ABI argument-
 # validation test against it, with clang's ASan runtime preloaded.  CPU only: run here, never on a GPU box.
 set -o pipefail
 cd "$(dirname "$0")/.." || exit 1
-OUT=gan-based-video-style-transfer_amd/_build/variants/libvst_hip_asan.so
+OUT=gan-based-video-style-transfer_amd/_build/asan/libvst_hip_asan.so
 RT=$(ls /opt/rocm/lib/llvm/lib/clang/*/lib/linux/libclang_rt.asan-x86_64.so | head -1)
 VST_VARIANT_HIPCC_FLAGS="-Xarch_host -fsanitize=address -Xarch_host -fno-omit-frame-pointer" \
   python3 -c "

@@ -150,7 +150,9 @@ int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* b
                     int H, int W, int C, int Ho, int Wo, int Cop, int R, int S, int st, int padh, int padw,
                     int reflect, int act, float slope, int math, int kind, hipStream_t s,
                     double* part = nullptr, float* tws = nullptr, size_t tws_floats = 0, const float* addend = nullptr,
-                    int oph = 0);
+                    int oph = 0, const float* nst = nullptr);
+// can the forward over relu(IN(x)) (nst = x's statistics) normalise in its A staging for this shape?
+bool bf_fprop_nrm_ok(int N, int H, int W, int C, int Cop, int R, int S, int st, int pad, int reflect, int math);
 // direct patch-staged 4-channel-input convs (conv_c4.hip)
 // the 64 -> 4-output 7 x 7 tap conv as one direct kernel (conv_tap64.hip)
 bool tap64_ok(int Cx, int R, int W, int math);

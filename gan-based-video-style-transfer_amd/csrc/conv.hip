@@ -956,6 +956,36 @@ extern "C" int vst_conv2d_fwd_ws(const float* x, const float* wp, const void* ws
                        math, (hipStream_t)stream, part, nsplit, ws, ws_bytes);
 }
 
+// A forward conv over relu(IN(x)): x = the raw output of the previous conv, nst = its InstanceNorm
+// statistics [N][Cx][2] (mean, rstd; vst_instnorm_finalize / _stats), normalised in the A staging
+// (conv_fprop_bf_nrm_k) — no normalised activation is written.  vst_conv2d_fwd_nrm_ok says whether a
+// shape takes it (x6, Cx % 32 == 0, reflect padding, stride 1, Ho*Wo % 256 == 0, a 256x128 or split-K
+// plan); the workspace is vst_conv2d_fwd_ws_bytes's.
+extern "C" int vst_conv2d_fwd_nrm_ok(int N, int H, int W, int Cx, int Cop, int R, int S, int stride, int pad,
+                                     int pad_mode, int math) {
+  return bf_fprop_nrm_ok(N, H, W, Cx, Cop, R, S, stride, pad, pad_mode == VST_PAD_REFLECT, math) &&
+         g_tile_override[0] < 0;
+}
+
+extern "C" int vst_conv2d_fwd_nrm_ws(const float* x, const float* nst, const void* wsplit, const float* bias, float* y,
+                                     int N, int H, int W, int Cx, int Cop, int R, int S, int stride, int pad,
+                                     int pad_mode, int act, float slope, int math, double* part, int* nsplit, float* ws,
+                                     size_t ws_bytes, void* stream) {
+  if (nsplit) *nsplit = 0;
+  VST_REQUIRE(x && nst && wsplit && y, "conv2d_fwd_nrm: null pointer");
+  VST_REQUIRE(vst_conv2d_fwd_nrm_ok(N, H, W, Cx, Cop, R, S, stride, pad, pad_mode, math),
+              "conv2d_fwd_nrm: unsupported shape / arithmetic (vst_conv2d_fwd_nrm_ok)");
+  VST_REQUIRE(ws_bytes >= vst_conv2d_fwd_ws_bytes(N, H, W, Cx, Cop, R, S, stride, pad, math),
+              "conv2d_fwd_nrm: workspace too small");
+  const int Ho = H + 2 * pad - R + 1, Wo = W + 2 * pad - S + 1;
+  const bool stats = part && nsplit;
+  const int rc = bf_fprop_launch(x, wsplit, (long)Cop * R * S * Cx, bias, y, N, H, W, Cx, Ho, Wo, Cop, R, S, 1, pad,
+                                 pad, 1, act, slope, math, -1, (hipStream_t)stream, stats ? part : nullptr, ws,
+                                 ws_bytes / sizeof(float), nullptr, 0, nst);
+  if (stats && rc == 0) *nsplit = Ho * Wo / 32;
+  return rc;
+}
+
 extern "C" int vst_conv_plan_fwd_tail(int N, int H, int W, int Cx, int Cop, int R, int S, int stride, int pad,
                                       int math, int* ksplit) {
   VST_REQUIRE(ksplit, "conv_plan_fwd_tail: null");

@@ -310,10 +310,10 @@ __device__ __forceinline__ void sched_group(bool first, bool after_barrier) {
 // (vmcnt(0)) before each stage's stores.  load_all(set) loads the cursor's stage into register
 // set `set`; adv(go) moves the cursor one stage on when go.  An odd stage count runs its last stage after
 // the two-stage loop.
-template <class T, class LoadAll, class Adv>
+template <class T, class LoadAll, class Adv, class Prep>
 __device__ __forceinline__ void main_loop(char* smem, int nk, f32x16 (&acc)[T::MI][T::NI],
                                           float4 (&ra)[2][T::A_LD][2], u32x4_t (&rbv)[2][T::B_LD][T::NP],
-                                          int rb, int kq, LoadAll load_all, Adv adv) {
+                                          int rb, int kq, LoadAll load_all, Adv adv, Prep prep) {
   constexpr int G = T::BK / 16;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int wm0 = (wave / T::WAVES_N) * T::WM, wn0 = (wave % T::WAVES_N) * T::WN;
@@ -322,6 +322,7 @@ __device__ __forceinline__ void main_loop(char* smem, int nk, f32x16 (&acc)[T::M
   // arbitration to its older partner on the SIMD; MI355X_MICROARCH.md, two waves per SIMD, item 4)
   if (VST_BF_PRIO && wave >= T::NW / 2) __builtin_amdgcn_s_setprio(1);
   load_all(0);
+  prep(0);
   store_stage<T>(smem, ra[0], rbv[0], rb, kq);
   adv(nk > 1);
   load_all(1);
@@ -339,10 +340,16 @@ __device__ __forceinline__ void main_loop(char* smem, int nk, f32x16 (&acc)[T::M
       if (g == 0) {
         adv(kt + 2 < nk);
         load_all(P);
-        if (!VST_BF_STORE_LATE) store_stage<T>(nxt, ra[P ^ 1], rbv[P ^ 1], rb, kq);
+        if (!VST_BF_STORE_LATE) {
+          prep(P ^ 1);
+          store_stage<T>(nxt, ra[P ^ 1], rbv[P ^ 1], rb, kq);
+        }
       }
       if (g == G - 1) {
-        if (VST_BF_STORE_LATE) store_stage<T>(nxt, ra[P ^ 1], rbv[P ^ 1], rb, kq);
+        if (VST_BF_STORE_LATE) {
+          prep(P ^ 1);
+          store_stage<T>(nxt, ra[P ^ 1], rbv[P ^ 1], rb, kq);
+        }
         __builtin_amdgcn_sched_barrier(0);  // keep this group's MFMAs after the barrier (they cover the read)
         __syncthreads();
         read_frag<T>(fr[fi ^ 1], nxt, 0, wm0, wn0, lane);
@@ -411,10 +418,10 @@ __device__ __forceinline__ void sched16() {
 //   C: barrier; (hi, hi), (lo, hi), (hi, lo)   read mid of stage kt + 1 (the freed mid set)
 // Every product term of the x6 sum is the 32x32x16 loop's; only the summation order of the six
 // terms into the fp32 accumulator differs (mid*mid first).
-template <class T, class LoadAll, class Adv>
+template <class T, class LoadAll, class Adv, class Prep>
 __device__ __forceinline__ void main_loop16(char* smem, int nk, f32x4v (&acc)[T::MI16][T::NI16],
                                             float4 (&ra)[2][T::A_LD][2], u32x4_t (&rbv)[2][T::B_LD][T::NP],
-                                            int rb, int kq, LoadAll load_all, Adv adv) {
+                                            int rb, int kq, LoadAll load_all, Adv adv, Prep prep) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int wm0 = (wave / T::WAVES_N) * T::WM, wn0 = (wave % T::WAVES_N) * T::WN;
   if (nk <= 0) return;
@@ -422,6 +429,7 @@ __device__ __forceinline__ void main_loop16(char* smem, int nk, f32x4v (&acc)[T:
   constexpr int NV = T::A_LD * 2 + T::B_LD * T::NP, NW = T::A_LD * T::NP + T::B_LD * T::NP;
   if (VST_M16_PRIO && wave >= T::NW / 2) __builtin_amdgcn_s_setprio(1);
   load_all(0);
+  prep(0);
   store_stage<T>(smem, ra[0], rbv[0], rb, kq);
   adv(nk > 1);
   load_all(1);
@@ -444,12 +452,18 @@ __device__ __forceinline__ void main_loop16(char* smem, int nk, f32x4v (&acc)[T:
       adv(kt + 2 < nk);
       load_all(P);
     }
-    if (SA) store_stage<T>(nxt, ra[P ^ 1], rbv[P ^ 1], rb, kq);
+    if (SA) {
+      prep(P ^ 1);
+      store_stage<T>(nxt, ra[P ^ 1], rbv[P ^ 1], rb, kq);
+    }
     mma16<T>(mid, mid, acc);
     if (VST_M16_SCHED) sched16<NM, RA ? 2 * NR : NR, NV, SA ? 4 : 0, SA ? NW : 0>();
     if (VST_M16_LOADFIRST) __builtin_amdgcn_sched_barrier(0);
     if (!RA) read_plane16<T>(lo, cur, 2, wm0, wn0, lane);
-    if (!SA) store_stage<T>(nxt, ra[P ^ 1], rbv[P ^ 1], rb, kq);
+    if (!SA) {
+      prep(P ^ 1);
+      store_stage<T>(nxt, ra[P ^ 1], rbv[P ^ 1], rb, kq);
+    }
     mma16<T>(mid, hi, acc);
     mma16<T>(hi, mid, acc);
     if (VST_M16_SCHED) sched16<2 * NM, RA ? 0 : NR, 0, SA ? 0 : 2, SA ? 0 : NW>();
@@ -692,13 +706,21 @@ __device__ __attribute__((aligned(256))) float g_zero_page[64];
 // [z * spk, z * spk + spk) and stores its raw partial tile to slab[z][m - m_base][Cop]
 // (fprop_splitk_reduce_k sums the splits in order and applies bias / act / IN partials).
 // (body of conv_fprop_bf_k and conv_convT_phases_k; bid = the block's index in its tile grid)
-template <class T, bool KSL, int REFL, bool SPLIT>
+// NRM (KSL, REFL 1 only): x is the raw output of the previous conv and every gathered A value enters as
+// relu((v - mean) * rstd) with the InstanceNorm statistics nst [N][C][2] (mean, rstd) — the IN + ReLU
+// apply of in_apply_k (same expression, same rounding) done in the A staging instead of a pass that
+// writes the normalised activation.  Reflect padding only (a zero-padding tap must stay zero), and
+// every tile's rows in one image (Ho*Wo a multiple of BM): the 8 channels' statistics of a K-step are
+// four float4 loads beside the A gathers.
+template <class T, bool KSL, int REFL, bool SPLIT, bool NRM = false>
 __device__ __forceinline__ void conv_fprop_bf_body(
     int bid, const float* __restrict__ x, const __bf16* __restrict__ ws, long wps, const float* __restrict__ bias,
     float* __restrict__ y, int H, int W, int C, int Ho, int Wo, int Cop, int S, int st, int padh,
     int padw, int reflect, int act, float slope, int M, int Ktot, int m_base, double* __restrict__ part,
-    int spk, float* __restrict__ slab, const float* __restrict__ addend, int oph) {
+    int spk, float* __restrict__ slab, const float* __restrict__ addend, int oph,
+    const float* __restrict__ nst = nullptr) {
   static_assert(!SPLIT || KSL, "split-K needs the channel-slice-major K walk");
+  static_assert(!NRM || (KSL && REFL == 1), "normalised A: the channel-slice K walk, reflect padding");
   static_assert(REFL < 4 || (SPLIT && KSL), "border rows run as split-K slabs");
   __shared__ __attribute__((aligned(16))) char smem[2 * T::STAGE];
   constexpr int A_LD = T::A_LD, B_LD = T::B_LD, RPP = T::RPP, NP = T::NP;
@@ -809,9 +831,16 @@ __device__ __forceinline__ void conv_fprop_bf_body(
 
   float4 ra[2][A_LD][2];
   u32x4_t rbv[2][B_LD][NP];
+  float4 nr[2][NRM ? 4 : 1];  // NRM: (mean, rstd) of the stage's 8 channels, per register set
+  const float* nimg = NRM ? nst + (long)(m0 / (Ho * Wo)) * C * 2 : nullptr;
   auto load_all = [&](int set) __attribute__((always_inline)) {
     const bool kin = KSL || kcur < Ktot;  // the K tail reads zeros (A) against row 0 (B)
     const int ka = KSL ? ksb + kq8 : kc;
+    if constexpr (NRM) {
+      const float4* q = reinterpret_cast<const float4*>(nimg + ka * 2);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) nr[set][u] = q[u];
+    }
     // REFL 5: tap (2, ts) top, (0, ts) bottom, (tr, 2) left, (tr, 0) right of the 3x3 weight rows
     const int tap5 = seg == 0 ? 6 + ts : (seg == 1 ? ts : 3 * tr + (seg == 2 ? 2 : 0));
     const int kb = KSL ? (REFL == 5 ? tap5 : tr * S + ts) * C + ksb + kq8 : (kin ? kcur : 0);
@@ -885,11 +914,27 @@ __device__ __forceinline__ void conv_fprop_bf_body(
     }
   };
 
+  // NRM: the IN + ReLU apply on register set `set` before its split (a no-op otherwise)
+  auto prep = [&](int set) __attribute__((always_inline)) {
+    if constexpr (NRM) {
+#pragma unroll
+      for (int j = 0; j < A_LD; ++j)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          float4& v = ra[set][j][h];
+          const float4 s0 = nr[set][2 * h], s1 = nr[set][2 * h + 1];  // {m0, r0, m1, r1}, {m2, r2, m3, r3}
+          v.x = apply_act((v.x - s0.x) * s0.y, VST_ACT_RELU, 0.f);
+          v.y = apply_act((v.y - s0.z) * s0.w, VST_ACT_RELU, 0.f);
+          v.z = apply_act((v.z - s1.x) * s1.y, VST_ACT_RELU, 0.f);
+          v.w = apply_act((v.w - s1.z) * s1.w, VST_ACT_RELU, 0.f);
+        }
+    }
+  };
   const int wm0 = (wave / T::WAVES_N) * T::WM, wn0 = (wave % T::WAVES_N) * T::WN;
   if constexpr (T::M16) {
     f32x4v acc[T::MI16][T::NI16];
     zero_acc4(acc);
-    main_loop16<T>(smem, nk, acc, ra, rbv, rb, kq, load_all, adv);
+    main_loop16<T>(smem, nk, acc, ra, rbv, rb, kq, load_all, adv, prep);
     if constexpr (SPLIT) {
       float* sl = slab + (long)zs * (M - m_base) * Cop;
 #pragma unroll
@@ -972,7 +1017,7 @@ __device__ __forceinline__ void conv_fprop_bf_body(
   }
   f32x16 acc[T::MI][T::NI];
   zero_acc(acc);
-  main_loop<T>(smem, nk, acc, ra, rbv, rb, kq, load_all, adv);
+  main_loop<T>(smem, nk, acc, ra, rbv, rb, kq, load_all, adv, prep);
   if constexpr (SPLIT) {
     float* sl = slab + (long)zs * (M - m_base) * Cop;
 #pragma unroll
@@ -1032,6 +1077,17 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_k(
     int spk = 0, float* __restrict__ slab = nullptr, const float* __restrict__ addend = nullptr, int oph = 0) {
   conv_fprop_bf_body<T, KSL, REFL, SPLIT>(blockIdx.x, x, ws, wps, bias, y, H, W, C, Ho, Wo, Cop, S, st, padh, padw,
                                           reflect, act, slope, M, Ktot, m_base, part, spk, slab, addend, oph);
+}
+
+// conv_fprop_bf_k over relu(IN(x)) (NRM: the normalisation in the A staging; nst = x's IN statistics)
+template <class T, bool SPLIT>
+__global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_nrm_k(
+    const float* __restrict__ x, const __bf16* __restrict__ ws, long wps, const float* __restrict__ bias,
+    float* __restrict__ y, int H, int W, int C, int Ho, int Wo, int Cop, int S, int st, int padh,
+    int padw, int act, float slope, int M, int Ktot, int m_base, double* __restrict__ part,
+    int spk, float* __restrict__ slab, const float* __restrict__ nst) {
+  conv_fprop_bf_body<T, true, 1, SPLIT, true>(blockIdx.x, x, ws, wps, bias, y, H, W, C, Ho, Wo, Cop, S, st, padh, padw,
+                                              1, act, slope, M, Ktot, m_base, part, spk, slab, nullptr, 0, nst);
 }
 
 // All four phases of a stride-2 ConvTranspose2d(k3, p1, op1) forward in ONE launch, each stored
@@ -1185,7 +1241,7 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_wgrad_bf_k(
   if constexpr (T::M16) {
     f32x4v acc[T::MI16][T::NI16];
     zero_acc4(acc);
-    main_loop16<T>(smem, nk, acc, ra, rbv, rb, kq, load_all, adv);
+    main_loop16<T>(smem, nk, acc, ra, rbv, rb, kq, load_all, adv, [](int) {});
 #pragma unroll
     for (int i = 0; i < T::MI16; ++i)
 #pragma unroll
@@ -1202,7 +1258,7 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_wgrad_bf_k(
   }
   f32x16 acc[T::MI][T::NI];
   zero_acc(acc);
-  main_loop<T>(smem, nk, acc, ra, rbv, rb, kq, load_all, adv);
+  main_loop<T>(smem, nk, acc, ra, rbv, rb, kq, load_all, adv, [](int) {});
 
 #pragma unroll
   for (int i = 0; i < T::MI; ++i)
@@ -1541,10 +1597,31 @@ size_t bf_fprop_ws_floats(long M, int Cop, int C, int R, int S, int math) {
   return ks ? (size_t)ks * (M - mf) * Cop : 0;
 }
 
+// The NRM route (conv_fprop_bf_nrm_k): x6, channel-slice K walk, reflect padding, and a plan of whole
+// 256x128 rounds or the all-split-K form (the kernels it instantiates), every tile in one image.
+bool bf_fprop_nrm_ok(int N, int H, int W, int C, int Cop, int R, int S, int st, int pad, int reflect, int math) {
+  if (math != VST_MATH_BF16X6 || !VST_BF_KSLICE || C % 32 || !reflect || st != 1 || R != S || Cop % 4) return false;
+  const int Ho = H + 2 * pad - R + 1, Wo = W + 2 * pad - S + 1;
+  if (Ho <= 0 || Wo <= 0 || ((long)Ho * Wo) % 256) return false;
+  const long M = (long)N * Ho * Wo;
+  int kd, m_split, tail_kind, m_first, ks;
+  bf_plan(M, Cop, math, -1, &kd, &m_split, &tail_kind);
+  bf_split_plan(M, Cop, C, R, S, math, -1, &m_first, &ks);
+  return (kd == 7 && (!m_split || ks)) || (ks && !m_first);
+}
+
 int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* bias, float* y, int N,
                     int H, int W, int C, int Ho, int Wo, int Cop, int R, int S, int st, int padh, int padw,
                     int reflect, int act, float slope, int math, int kind, hipStream_t s, double* part,
-                    float* tws, size_t tws_floats, const float* addend, int oph) {
+                    float* tws, size_t tws_floats, const float* addend, int oph, const float* nst) {
+  if (nst) {
+    VST_REQUIRE(kind < 0 && !addend && !oph && padh == padw &&
+                    bf_fprop_nrm_ok(N, H, W, C, Cop, R, S, st, padh, reflect, math),
+                "conv fprop over relu(IN(x)): needs x6, C %% 32 == 0, reflect, stride 1, Ho*Wo %% 256 == 0 and a "
+                "256x128 / split-K plan (bf_fprop_nrm_ok)");
+    VST_REQUIRE(tws || (size_t)0 == bf_fprop_ws_floats((long)N * Ho * Wo, Cop, C, R, S, math),
+                "conv fprop over relu(IN(x)): this shape's plan needs the split-K workspace");
+  }
   if (oph) tws = nullptr;  // phase stores: no split-K slabs (their reduce stores unmapped)
   // the epilogue routes differ on whether an addend enters the IN partials (the per-element store
   // counts it, the LDS-staged one adds it at the row store): no caller needs both, so refuse it
@@ -1593,7 +1670,10 @@ int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* b
       using T = bf::Tile<256, 128, 64, 64, 32, 3>;
       const int nk = (K + T::BK - 1) / T::BK, spk = (nk + ks - 1) / ks;
       const dim3 grid(ceil_div(M - mb, 256) * ceil_div(Cop, 128) * ks);
-      if (reflect)
+      if (nst)
+        hipLaunchKernelGGL((bf::conv_fprop_bf_nrm_k<T, true>), grid, dim3(T::NT), 0, s, x, ws, wps, bias, y, H, W, C,
+                           Ho, Wo, Cop, S, st, padh, padw, act, slope, M, K, mb, part, spk, tws, nst);
+      else if (reflect)
         hipLaunchKernelGGL((bf::conv_fprop_bf_k<T, true, 1, true>), grid, dim3(T::NT), 0, s, x, ws, wps, bias, y, H,
                            W, C, Ho, Wo, Cop, S, st, padh, padw, reflect, act, slope, M, K, mb, part, spk, tws,
                            nullptr);
@@ -1603,6 +1683,14 @@ int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* b
                            nullptr);
       hipLaunchKernelGGL(bf::fprop_splitk_reduce_k, dim3(ceil_div(M - mb, 32), ceil_div(Cop, 64)), dim3(256), 0, s,
                          tws, ks, mb, M, Cop, bias, act, slope, y, part, Ho * Wo, addend);
+      continue;
+    }
+    if (nst) {  // bf_fprop_nrm_ok: whole 256x128 rounds here
+      using T = bf::Tile<256, 128, 64, 64, 32, 3>;
+      VST_REQUIRE(kp == 7, "conv fprop over relu(IN(x)): unexpected tile kind %d", kp);
+      const dim3 grid(ceil_div(Mend - mb, 256) * ceil_div(Cop, 128));
+      hipLaunchKernelGGL((bf::conv_fprop_bf_nrm_k<T, false>), grid, dim3(T::NT), 0, s, x, ws, wps, bias, y, H, W, C,
+                         Ho, Wo, Cop, S, st, padh, padw, act, slope, Mend, K, mb, part, 0, nullptr, nst);
       continue;
     }
     if (math == VST_MATH_BF16X6) {

@@ -58,6 +58,19 @@ __device__ __forceinline__ uint32_t pack2(float a, float b) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
 }
 
+#ifndef VST_C4_DPP
+#define VST_C4_DPP 1  // ring kernel: IN-partial butterflies on DPP lane moves instead of ds_bpermute
+#endif
+// a double moved across lanes by a DPP control (both halves): row_mirror 0x140 (l <-> 15 - l in a
+// 16-lane row), row_half_mirror 0x141 (l <-> 7 - l in 8), quad_perm 0x4E (l ^ 2) / 0xB1 (l ^ 1)
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, CTRL, 0xf, 0xf, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTRL, 0xf, 0xf, false);
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+
 // one output-row segment: image n, output row ho, columns [wo0, wo0 + L)
 struct Seg {
   int n, ho, wo0, L;
@@ -541,20 +554,24 @@ __global__ __launch_bounds__(NT, 1) void conv_c4_ring_k(const float* __restrict_
         d[2 * q] = (double)v[0][q] + (double)v[1][q];
         d[2 * q + 1] = (double)v[0][q] * v[0][q] + (double)v[1][q] * v[1][q];
       }
+      // reduce-scatter over the row's 16 lanes: levels pair lane l with 15 - l, 7 - l (in its half),
+      // l ^ 2, l ^ 1 (DPP moves; each level's partner differs in the bit the level halves on, so lane l
+      // ends with the same index, 4 b3 + 2 b2 + b1, as the xor butterfly of conv_c4_direct_k)
       auto half = [&](auto M, auto Nn) __attribute__((always_inline)) {
         constexpr int m = decltype(M)::value, n = decltype(Nn)::value;
+        constexpr int ctrl = m == 8 ? 0x140 : m == 4 ? 0x141 : m == 2 ? 0x4E : 0xB1;
         const bool up = (lane & m) != 0;
 #pragma unroll
         for (int u = 0; u < n / 2; ++u) {
           const double send = up ? d[u] : d[u + n / 2];
           const double keep = up ? d[u + n / 2] : d[u];
-          d[u] = keep + __shfl_xor(send, m);
+          d[u] = keep + (VST_C4_DPP ? dpp_f64<ctrl>(send) : __shfl_xor(send, m));
         }
       };
       half(std::integral_constant<int, 8>(), std::integral_constant<int, 8>());
       half(std::integral_constant<int, 4>(), std::integral_constant<int, 4>());
       half(std::integral_constant<int, 2>(), std::integral_constant<int, 2>());
-      d[0] += __shfl_xor(d[0], 1);
+      d[0] += VST_C4_DPP ? dpp_f64<0xB1>(d[0]) : __shfl_xor(d[0], 1);
       const int co = c0 + 2 * ((lane >> 3) & 1) + ((lane >> 2) & 1);
       const int off = ((z * COP + co) * 2 + ((lane >> 1) & 1)) * (int)sizeof(double) + pskip;
       __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2v, d[0]), prs, off, 0, 0);

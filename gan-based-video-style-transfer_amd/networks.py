@@ -587,9 +587,16 @@ class _GeneratorFn(torch.autograd.Function):
         sv["d1"] = (y, s, a)
         h = a
         for i in range(nb):
-            t, s1, uu = conv_in_relu(h, f"b{i}a", 4 * ngf, 3, 1, 1, "reflect", nxt=(4 * ngf, 1, "reflect"))
             kc, _, b = P[f"b{i}b"]
-            v, s2 = ops.conv2d_fwd_in(uu, kc, b, 4 * ngf, 3, 3, 1, 1, "reflect", role=role)
+            if role == "infer" and ops.conv2d_fwd_in_nrm_ok(h, 4 * ngf, 3, 1, "reflect", role):
+                # inference: the block's IN + ReLU applied inside the second conv's A staging
+                ka, _, ba = P[f"b{i}a"]
+                t, s1 = ops.conv2d_fwd_in(h, ka, ba, 4 * ngf, 3, 3, 1, 1, "reflect", role=role)
+                v, s2 = ops.conv2d_fwd_in_nrm(t, s1, kc, b, 4 * ngf, 3, 1, "reflect", role=role)
+                uu = None
+            else:
+                t, s1, uu = conv_in_relu(h, f"b{i}a", 4 * ngf, 3, 1, 1, "reflect", nxt=(4 * ngf, 1, "reflect"))
+                v, s2 = ops.conv2d_fwd_in(uu, kc, b, 4 * ngf, 3, 3, 1, 1, "reflect", role=role)
             hn, hnt = in_act(v, s2, "none", cp_for(v, 4 * ngf, 1, "reflect") if i + 1 < nb else None, residual=h)
             sv["xt"][id(hn)] = hnt
             sv[f"b{i}"] = (h, t, s1, uu, v, s2)

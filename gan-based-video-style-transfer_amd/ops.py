@@ -265,6 +265,42 @@ def conv2d_fwd_in(x, wp, bias, cop, R, S, stride, pad, pad_mode="zero", role="fw
     return y, stats
 
 
+# The ResnetBlock's second conv over relu(IN(t)) normalising in its A staging (vst_conv2d_fwd_nrm_ws)
+# instead of an IN + ReLU apply pass that writes the activation (inference: the activation has no
+# other reader).  Opt-in (VST_NRM_FWD=1): measured slower (same box, alternating runs) — B=1 256^2
+# 1.24 vs 1.18-1.20 ms, B=16 9.04-9.09 vs 8.57-8.61 ms, 436x1024 equal: the stage's four statistics
+# loads and 32 VALU cost the 256x128 main loop more than the 4-8 us apply pass they remove.
+NRM_FWD = os.environ.get("VST_NRM_FWD", "0") == "1"
+
+
+def conv2d_fwd_in_nrm_ok(y_in, cop, R, pad, pad_mode="reflect", role="infer"):
+    N, H, W, C = y_in.shape
+    return NRM_FWD and bool(lib().vst_conv2d_fwd_nrm_ok(N, H, W, C, cop, R, R, 1, pad, PAD[pad_mode], _math(role)))
+
+
+def conv2d_fwd_in_nrm(y_in, stats_in, wp, bias, cop, R, pad, pad_mode="reflect", role="infer"):
+    """conv2d_fwd_in (stride 1) over relu(IN(y_in)), stats_in = y_in's IN statistics: the IN + ReLU apply
+    runs inside the conv's A staging (vst_conv2d_fwd_nrm_ws) -> (y, stats of y)."""
+    import ctypes
+    _dev_check(y_in, stats_in, wp, bias)
+    N, H, W, Cx = y_in.shape
+    Ho, Wo = H + 2 * pad - R + 1, W + 2 * pad - R + 1
+    y = torch.empty((N, Ho, Wo, cop), device=y_in.device)
+    part = torch.empty((N * (Ho * Wo // 32) * cop * 2,), device=y_in.device, dtype=torch.float64)
+    nsplit = ctypes.c_int(0)
+    m = _math(role)
+    nb = int(lib().vst_conv2d_fwd_ws_bytes(N, H, W, Cx, cop, R, R, 1, pad, m))
+    ws = torch.empty((nb + 3) // 4, device=y_in.device) if nb else None
+    h = _probe_begin("fwd", (N, H, W, Cx, cop, R, 1, pad, pad_mode)) if _probes else None
+    _call("vst_conv2d_fwd_nrm_ws", _p(y_in), _p(stats_in), _p(getattr(wp, "vst_split", None)), _p(bias), _p(y), N, H,
+          W, Cx, cop, R, R, 1, pad, PAD[pad_mode], ACT["none"], 0.0, m, _p(part), ctypes.addressof(nsplit), _p(ws), nb,
+          _stream())
+    _probe_end(h)
+    stats = torch.empty((N, cop, 2), device=y_in.device)
+    _call("vst_instnorm_finalize", _p(part), _p(stats), N, Ho * Wo, cop, nsplit.value, IN_EPS, _stream())
+    return y, stats
+
+
 def conv2d_tfwd(x, wp, bias, Ho, Wo, cx, R, S, stride, pad, act="none", slope=0.0,
                 pad_mode="zero", addend=None, role="bwd"):
     """Transposed conv / data gradient (vst_conv2d_tfwd).  pad_mode='reflect' (stride 1) is the

@@ -133,6 +133,18 @@ size_t vst_conv2d_fwd_ws_bytes(int N, int H, int W, int Cx, int Cop, int R, int 
 int vst_conv2d_fwd_ws(const float* x, const float* wp, const void* wsplit, const float* bias, float* y, int N,
                       int H, int W, int Cx, int Cop, int R, int S, int stride, int pad, int pad_mode, int act,
                       float slope, int math, double* part, int* nsplit, float* ws, size_t ws_bytes, void* stream);
+/* A forward conv over relu(IN(x)) without the normalised activation: x = the raw output of the previous
+ * conv, nst = its InstanceNorm statistics [N][Cx][2] (mean, rstd); every gathered A value enters as
+ * relu((v - mean) * rstd) (in_apply's expression), inside the GEMM's A staging.  Replaces
+ * vst_instnorm_act_fwd(relu) + vst_conv2d_fwd_ws on the ResnetBlock's second conv
+ * (networks.py:340-367: ReflectionPad2d(1), Conv2d, InstanceNorm2d, ReLU, ReflectionPad2d(1), Conv2d).
+ * vst_conv2d_fwd_nrm_ok (host-only) says whether a shape takes it: bf16x6, Cx % 32 == 0, reflect
+ * padding, stride 1, Ho*Wo % 256 == 0; workspace = vst_conv2d_fwd_ws_bytes. */
+int vst_conv2d_fwd_nrm_ok(int N, int H, int W, int Cx, int Cop, int R, int S, int stride, int pad, int pad_mode,
+                          int math);
+int vst_conv2d_fwd_nrm_ws(const float* x, const float* nst, const void* wsplit, const float* bias, float* y, int N,
+                          int H, int W, int Cx, int Cop, int R, int S, int stride, int pad, int pad_mode, int act,
+                          float slope, int math, double* part, int* nsplit, float* ws, size_t ws_bytes, void* stream);
 /* Host-only: the split-K count (0 = none) vst_conv2d_fwd_ws uses for this shape and arithmetic: of
  * the tail launch, or — for grids of at most 128 256x128 tiles (PatchGAN layers, half batches) — of
  * the whole conv, run as one split-K launch + the reduction. */

@@ -1007,3 +1007,27 @@ def test_dgrad_refl_in_fused(ops, case):
         _close(_nchw(dx1, Ci, ops), yt.grad, tol=1e-4, what=name + " IN bwd")
     finally:
         ops.set_conv_math(prev)
+
+
+@pytest.mark.parametrize("N", [1, 2, 8, 12, 16])
+def test_conv_fwd_nrm_matches_apply_then_conv(ops, N):
+    """vst_conv2d_fwd_nrm_ws (the ResnetBlock's second conv normalising relu(IN(t)) in its A staging)
+    is bit-identical to the IN + ReLU apply pass followed by the forward conv (same expression, same
+    products): output and its IN statistics; N = 1 / 2 run the all-split-K plan, 12 a 256x128 round
+    plus a split-K tail, 8 / 16 whole rounds."""
+    prev = ops.set_conv_math("bf16x6")
+    try:
+        H, C = 64, 256
+        t = _g(91, (N, H, H, C)).to(DEV) * 0.7 + 0.2
+        w = _g(92, (C, C, 3, 3), 0.02)
+        b = _g(93, (C,), 0.1).to(DEV)
+        kc = ops.weight_pack(w.to(DEV), ops.PACK_FWD)
+        s1 = ops.instnorm_stats(t)
+        assert ops.conv2d_fwd_in_nrm_ok(t, C, 3, 1, "reflect", "infer")
+        a = ops.instnorm_act_fwd(t, s1, "relu")
+        y_ref, s_ref = ops.conv2d_fwd_in(a, kc, b, C, 3, 3, 1, 1, "reflect", role="infer")
+        y, s = ops.conv2d_fwd_in_nrm(t, s1, kc, b, C, 3, 1, "reflect", role="infer")
+        assert torch.equal(y, y_ref)
+        assert torch.equal(s, s_ref)
+    finally:
+        ops.set_conv_math(prev)

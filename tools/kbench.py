@@ -2,7 +2,7 @@
 times (batch KB_B, default 8) — the target of rocprofv3 --pmc passes.  usage: kbench.py fprop|dgrad|tconv|wgrad|wgrad_pre|warp|c0 [reps]
 (wgrad_pre: the weight gradient as the train step runs it, on the IN passes' premade x image / dy planes)
 warp: vst_warp_fwd on bench.py's warp_roofline shape (N=32, C=64, 436x1024, its smooth flow; KB_FLOW=iid:
-the i.i.d. worst case).  c0: the generator's first conv (conv_c4_direct_k) at N=KB_B, 256x256."""
+the i.i.d. worst case).  c0: the generator's first conv (conv_c4_ring_k; VST_C4_RING=0: conv_c4_direct_k) at N=KB_B, 256x256."""
 import os
 import sys
 

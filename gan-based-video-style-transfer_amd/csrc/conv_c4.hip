@@ -28,7 +28,13 @@
 #ifndef VST_C4_NOSTORE
 #define VST_C4_NOSTORE 0    // developer timing experiment only: every output / partial store dropped
 #endif
-#if (VST_C4_NOCOMPUTE || VST_C4_NOSTORE) && !defined(VST_DEV_VARIANT)
+#ifndef VST_C4_NOEPI
+#define VST_C4_NOEPI 0      // developer timing experiment only (ring kernel): no epilogue at all
+#endif
+#ifndef VST_C4_NOWLDS
+#define VST_C4_NOWLDS 0     // developer timing experiment only (ring kernel): weight fragments read once per segment
+#endif
+#if (VST_C4_NOCOMPUTE || VST_C4_NOSTORE || VST_C4_NOEPI || VST_C4_NOWLDS) && !defined(VST_DEV_VARIANT)
 #error "VST_C4_NOCOMPUTE / VST_C4_NOSTORE are developer-only timing modes: build them with tools/build_variant.py"
 #endif
 
@@ -58,19 +64,9 @@ __device__ __forceinline__ uint32_t pack2(float a, float b) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
 }
 
-#ifndef VST_C4_DPP
-#define VST_C4_DPP 1  // ring kernel: IN-partial butterflies on DPP lane moves instead of ds_bpermute
+#ifndef VST_C4_GRP
+#define VST_C4_GRP 0  // ring kernel wave groups: 0 = waves {0-3} / {4-7}, 1 = even / odd waves
 #endif
-// a double moved across lanes by a DPP control (both halves): row_mirror 0x140 (l <-> 15 - l in a
-// 16-lane row), row_half_mirror 0x141 (l <-> 7 - l in 8), quad_perm 0x4E (l ^ 2) / 0xB1 (l ^ 1)
-template <int CTRL>
-__device__ __forceinline__ double dpp_f64(double v) {
-  const uint64_t u = __builtin_bit_cast(uint64_t, v);
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, CTRL, 0xf, 0xf, false);
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTRL, 0xf, 0xf, false);
-  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
-}
-
 // one output-row segment: image n, output row ho, columns [wo0, wo0 + L)
 struct Seg {
   int n, ho, wo0, L;
@@ -472,7 +468,7 @@ __global__ __launch_bounds__(NT, 1) void conv_c4_ring_k(const float* __restrict_
   const int sub = wave;      // this wave's 32-pixel sub-tile of every segment
   // one wave of each group per SIMD; an SGPR value, so `grp` branches are scalar (two exclusive paths,
   // each with its own counted waits) rather than exec-masked sequences of both
-  const int grp = __builtin_amdgcn_readfirstlane(wave >> 2);
+  const int grp = __builtin_amdgcn_readfirstlane(VST_C4_GRP ? (wave & 1) : (wave >> 2));
   const int HWo = Ho * Wo;
   f32x4v acc[2][4];
 
@@ -492,6 +488,7 @@ __global__ __launch_bounds__(NT, 1) void conv_c4_ring_k(const float* __restrict_
         f.x[p][i] = __builtin_bit_cast(bf16x8_t, make_uint4(lo.x, lo.y, hi.x, hi.y));
       }
     }
+    if (VST_C4_NOWLDS && r > 0) return;
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -509,22 +506,23 @@ __global__ __launch_bounds__(NT, 1) void conv_c4_ring_k(const float* __restrict_
     for (int r = 0; r < R; ++r) {
       const Fr& f = fr[r & 1];
       if (r + 1 < R) load_fr(fr[(r + 1) & 1], ho, r + 1);
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-#define VST_C4MF(pa, pb) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.w[pb][j], f.x[pa][i], acc[i][j], 0, 0, 0)
-          if constexpr (NP == 3) {
-            VST_C4MF(1, 1); VST_C4MF(1, 0); VST_C4MF(0, 1); VST_C4MF(0, 0); VST_C4MF(2, 0); VST_C4MF(0, 2);
-          } else {
-            VST_C4MF(1, 0); VST_C4MF(0, 1); VST_C4MF(0, 0);
-          }
+      // product-major: the 8 accumulators' MFMAs of one (x-plane, w-plane) product back to back, so
+      // consecutive MFMAs are independent (an accumulator's six products in a row wait on each other);
+      // each accumulator still takes its products in conv_fprop_bf_k's order
+#define VST_C4MF(pa, pb)                                                                                       \
+  _Pragma("unroll") for (int i = 0; i < 2; ++i) _Pragma("unroll") for (int j = 0; j < 4; ++j) acc[i][j] =     \
+      __builtin_amdgcn_mfma_f32_16x16x32_bf16((VST_C4_NOWLDS ? fr[0].w : f.w)[pb][j], f.x[pa][i], acc[i][j], 0, 0, 0);
+      if constexpr (NP == 3) {
+        VST_C4MF(1, 1) VST_C4MF(1, 0) VST_C4MF(0, 1) VST_C4MF(0, 0) VST_C4MF(2, 0) VST_C4MF(0, 2)
+      } else {
+        VST_C4MF(1, 0) VST_C4MF(0, 1) VST_C4MF(0, 0)
+      }
 #undef VST_C4MF
-        }
       __builtin_amdgcn_sched_barrier(0);
     }
   };
   auto epilogue = [&](const Seg& cs, bool live) __attribute__((always_inline)) {
+    if (VST_C4_NOEPI) return;
     const float* yseg = y + (((long)cs.n * Ho + cs.ho) * Wo + cs.wo0) * COP;
     const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(yseg), 0, live && !VST_C4_NOSTORE ? cs.L * COP * (int)sizeof(float) : 0, 0x00020000);
@@ -548,70 +546,71 @@ __global__ __launch_bounds__(NT, 1) void conv_c4_ring_k(const float* __restrict_
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, f32x4v{v[i][0], v[i][1], v[i][2], v[i][3]}),
                                                yrs, (px * COP + c0) * (int)sizeof(float), 0, 0);
       }
-      double d[8];
+      // partials of the sub-tile's 32 pixels: a lane's two pixels and the butterfly in fp32 (each
+      // partial is a 32-term sum: relative error <= 32 * 2^-24 of its magnitude), stored as fp64 and
+      // combined over the image in fp64 by in_finalize_k
+      float d[8];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        d[2 * q] = (double)v[0][q] + (double)v[1][q];
-        d[2 * q + 1] = (double)v[0][q] * v[0][q] + (double)v[1][q] * v[1][q];
+        d[2 * q] = v[0][q] + v[1][q];
+        d[2 * q + 1] = v[0][q] * v[0][q] + v[1][q] * v[1][q];
       }
       // reduce-scatter over the row's 16 lanes: levels pair lane l with 15 - l, 7 - l (in its half),
       // l ^ 2, l ^ 1 (DPP moves; each level's partner differs in the bit the level halves on, so lane l
-      // ends with the same index, 4 b3 + 2 b2 + b1, as the xor butterfly of conv_c4_direct_k)
+      // ends with index 4 b3 + 2 b2 + b1, as the xor butterfly of conv_c4_direct_k)
       auto half = [&](auto M, auto Nn) __attribute__((always_inline)) {
         constexpr int m = decltype(M)::value, n = decltype(Nn)::value;
         constexpr int ctrl = m == 8 ? 0x140 : m == 4 ? 0x141 : m == 2 ? 0x4E : 0xB1;
         const bool up = (lane & m) != 0;
 #pragma unroll
         for (int u = 0; u < n / 2; ++u) {
-          const double send = up ? d[u] : d[u + n / 2];
-          const double keep = up ? d[u + n / 2] : d[u];
-          d[u] = keep + (VST_C4_DPP ? dpp_f64<ctrl>(send) : __shfl_xor(send, m));
+          const float send = up ? d[u] : d[u + n / 2];
+          const float keep = up ? d[u + n / 2] : d[u];
+          d[u] = keep + __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, send),
+                                                                                ctrl, 0xf, 0xf, false));
         }
       };
       half(std::integral_constant<int, 8>(), std::integral_constant<int, 8>());
       half(std::integral_constant<int, 4>(), std::integral_constant<int, 4>());
       half(std::integral_constant<int, 2>(), std::integral_constant<int, 2>());
-      d[0] += VST_C4_DPP ? dpp_f64<0xB1>(d[0]) : __shfl_xor(d[0], 1);
+      d[0] += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, d[0]), 0xB1, 0xf, 0xf, false));
       const int co = c0 + 2 * ((lane >> 3) & 1) + ((lane >> 2) & 1);
       const int off = ((z * COP + co) * 2 + ((lane >> 1) & 1)) * (int)sizeof(double) + pskip;
-      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2v, d[0]), prs, off, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2v, (double)d[0]), prs, off, 0, 0);
     }
   };
 
   if (tb >= T) return;  // block-uniform, before any barrier
   Seg g = segof(tb);
   full_stage(g);
-  float4 prow = load_row(g, g.ho + R);  // segment tb + 1's last row
-  // every path into the loop head carries the prefetch load followed by one epilogue's 12 stores (here
-  // dropped ones), so the wait before put_row stays vmcnt(12) instead of draining the stores
-  __builtin_amdgcn_sched_barrier(0);
-  epilogue(g, false);
   __syncthreads();
   Seg prev = g;
   bool have_prev = false;
   for (int s = tb; s < te; ++s) {
     const Seg cur = g;
-    // the prefetched row into its slot ((cur.ho + R) & 7 = (cur.ho - 1) & 7: segment s - 1's first row,
-    // free since the last barrier); junk when segment s + 1 starts a new run (restaged below)
-    put_row(cur.ho + R, prow);
-    prow = load_row(cur, cur.ho + R + 1);  // segment s + 2's last row
+    // segment s + 1's last row (padded row cur.ho + R; junk when s + 1 starts a new run, restaged
+    // below): loaded here, written at the end of this iteration into slot (cur.ho + R) & 7 =
+    // (cur.ho - 1) & 7, which segment s does not read — the load's wait then sits behind this
+    // iteration's own work, with no load live across the loop edge
+    // (put_row inside each group's path: after the group-0 / group-1 branches merge, the compiler's
+    // wait for prow would also count the path that skips both, and drain every store: vmcnt(0))
+    const float4 prow = load_row(cur, cur.ho + R);
     if (grp == 0) {
       if (32 * sub < cur.L && !VST_C4_NOCOMPUTE) compute(cur.ho);
+      put_row(cur.ho + R, prow);
       epilogue(cur, true);
     } else {
       epilogue(prev, have_prev);
       if (32 * sub < cur.L && !VST_C4_NOCOMPUTE) compute(cur.ho);
+      put_row(cur.ho + R, prow);
     }
     prev = cur;
     have_prev = true;
-    __syncthreads();  // segment s read, row cur.ho + R + ... written
+    __syncthreads();  // segment s read, segment s + 1's last row written
     if (s + 1 < te) {
       g = segof(s + 1);
       if (g.ho == 0) {  // a new image / column segment: all R rows (block-uniform)
         full_stage(g);
-        prow = load_row(g, g.ho + R);
-        __builtin_amdgcn_sched_barrier(0);
-        epilogue(g, false);
         __syncthreads();
       }
     }

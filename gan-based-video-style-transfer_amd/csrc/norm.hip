@@ -395,13 +395,25 @@ __device__ __forceinline__ bool fold_slices(const double* __restrict__ part, int
   return true;
 }
 
-// grid (C/16, N), 256 threads
+// Channels per finalize block: 16, or 4 when (C / 16) x N blocks would leave most CUs idle over many
+// slices (the first conv's 64 channels x 8 images over 2048 slices: 32 blocks, 14 us; B=1 inference's
+// 256 channels: 16 blocks) — 4x the blocks, each thread's slice chain 4x shorter.
+static const bool g_fin_narrow = [] {
+  const char* e = getenv("VST_FIN_NARROW");
+  return !(e && e[0] == '0');
+}();
+static int fin_cpb(int C, int N, int nsplit) {
+  return (!g_fin_narrow || (long)((C + 15) / 16) * N >= 128 || nsplit < 64) ? 16 : 4;
+}
+
+// grid (C/CPB, N), 256 threads
+template <int CPB>
 __global__ void in_finalize_k(const double* __restrict__ part, float* __restrict__ stats, int N,
                               int HW, int C, int nsplit, float eps) {
   double sq[2];
   const int n = blockIdx.y;
-  if (!fold_slices<2, 16>(part, n, C, nsplit, sq)) return;
-  const int idx = n * C + blockIdx.x * 16 + (threadIdx.x & 15);
+  if (!fold_slices<2, CPB>(part, n, C, nsplit, sq)) return;
+  const int idx = n * C + blockIdx.x * CPB + (threadIdx.x % CPB);
   const double mean = sq[0] / HW;
   double var = sq[1] / HW - mean * mean;
   if (var < 0) var = 0;
@@ -411,13 +423,14 @@ __global__ void in_finalize_k(const double* __restrict__ part, float* __restrict
 
 // coef[(n*C+c)] = {mean(g), mean(g*xhat)}; dbn[n*C+c] = sum_p dx = rstd*((sum g - HW*mean g)
 // - mean(g xhat)*sum xhat)  (the exact per-channel sum of the IN input gradient).
+template <int CPB>
 __global__ void in_bwd_finalize_k(const double* __restrict__ part, const float* __restrict__ stats,
                                   float2* __restrict__ coef, double* __restrict__ dbn, int N, int HW,
                                   int C, int nsplit) {
   double a[3];
   const int n = blockIdx.y;
-  if (!fold_slices<3, 16>(part, n, C, nsplit, a)) return;
-  const int idx = n * C + blockIdx.x * 16 + (threadIdx.x & 15);
+  if (!fold_slices<3, CPB>(part, n, C, nsplit, a)) return;
+  const int idx = n * C + blockIdx.x * CPB + (threadIdx.x % CPB);
   const double mg = a[0] / HW, mgx = a[1] / HW;
   coef[idx] = make_float2((float)mg, (float)mgx);
   const double rstd = stats[2 * idx + 1];
@@ -922,16 +935,23 @@ extern "C" int vst_instnorm_stats(const float* x, float* stats, float* ws, int N
   double* part = reinterpret_cast<double*>(ws);
   hipLaunchKernelGGL(in_partial_k<0>, dim3(g.nsplit, N), dim3(NRED), 0, s, x, (const float*)nullptr,
                      (const float*)nullptr, part, HW, C, g.LP, g.PG, g.SP, g.nsplit, 0, 0.f);
-  hipLaunchKernelGGL(in_finalize_k, dim3(ceil_div(C, 16), N), dim3(256), 0, s, part, stats, N, HW, C,
-                     g.nsplit, eps);
+  if (fin_cpb(C, N, g.nsplit) == 4)
+    hipLaunchKernelGGL(in_finalize_k<4>, dim3(ceil_div(C, 4), N), dim3(256), 0, s, part, stats, N, HW, C, g.nsplit, eps);
+  else
+    hipLaunchKernelGGL(in_finalize_k<16>, dim3(ceil_div(C, 16), N), dim3(256), 0, s, part, stats, N, HW, C, g.nsplit,
+                       eps);
   return check_launch("instnorm_stats");
 }
 
 extern "C" int vst_instnorm_finalize(const double* part, float* stats, int N, int HW, int C, int nsplit,
                                      float eps, void* stream) {
   VST_REQUIRE(part && stats && N > 0 && HW > 0 && C > 0 && nsplit > 0, "instnorm_finalize: bad args");
-  hipLaunchKernelGGL(in_finalize_k, dim3(ceil_div(C, 16), N), dim3(256), 0, (hipStream_t)stream, part, stats, N,
-                     HW, C, nsplit, eps);
+  if (fin_cpb(C, N, nsplit) == 4)
+    hipLaunchKernelGGL(in_finalize_k<4>, dim3(ceil_div(C, 4), N), dim3(256), 0, (hipStream_t)stream, part, stats, N,
+                       HW, C, nsplit, eps);
+  else
+    hipLaunchKernelGGL(in_finalize_k<16>, dim3(ceil_div(C, 16), N), dim3(256), 0, (hipStream_t)stream, part, stats,
+                       N, HW, C, nsplit, eps);
   return check_launch("instnorm_finalize");
 }
 
@@ -1070,7 +1090,11 @@ static int in_bwd_tail(const float* gy, const float* x, const float* stats, floa
   float2* coef = reinterpret_cast<float2*>(reinterpret_cast<char*>(ws) +
                                            (size_t)N * g.nsplit * C * 3 * sizeof(double));
   double* dbn = reinterpret_cast<double*>(reinterpret_cast<char*>(coef) + (size_t)N * C * sizeof(float2));
-  hipLaunchKernelGGL(in_bwd_finalize_k, dim3(ceil_div(C, 16), N), dim3(256), 0, s, part, stats, coef, dbn,
+  if (fin_cpb(C, N, g.nsplit) == 4)
+    hipLaunchKernelGGL(in_bwd_finalize_k<4>, dim3(ceil_div(C, 4), N), dim3(256), 0, s, part, stats, coef, dbn,
+                     N, HW, C, g.nsplit);
+  else
+    hipLaunchKernelGGL(in_bwd_finalize_k<16>, dim3(ceil_div(C, 16), N), dim3(256), 0, s, part, stats, coef, dbn,
                      N, HW, C, g.nsplit);
   // the bias gradient (sum over n of dbn) is taken by the apply pass's first blocks
   if (planes) {

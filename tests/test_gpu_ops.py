@@ -1023,7 +1023,7 @@ def test_conv_fwd_nrm_matches_apply_then_conv(ops, N):
         b = _g(93, (C,), 0.1).to(DEV)
         kc = ops.weight_pack(w.to(DEV), ops.PACK_FWD)
         s1 = ops.instnorm_stats(t)
-        assert ops.conv2d_fwd_in_nrm_ok(t, C, 3, 1, "reflect", "infer")
+        assert ops.lib().vst_conv2d_fwd_nrm_ok(N, H, H, C, C, 3, 3, 1, 1, ops.PAD["reflect"], ops._math("infer"))
         a = ops.instnorm_act_fwd(t, s1, "relu")
         y_ref, s_ref = ops.conv2d_fwd_in(a, kc, b, C, 3, 3, 1, 1, "reflect", role="infer")
         y, s = ops.conv2d_fwd_in_nrm(t, s1, kc, b, C, 3, 1, "reflect", role="infer")

@@ -292,22 +292,34 @@ def test_mogan_dp_world2_three_phases_equal_single_process():
     try:
         m = _mogan_setup()
         full = _mogan_run(m)
+        # each rank's half batch in one process: what the exchange must average
+        halves = [_mogan_run(_mogan_setup(slice(2 * r, 2 * r + 2))) for r in range(world)]
     finally:
         ops.set_deterministic(prev)
-    # the E-step gradients to 1e-4; the M-step ones (through RAFT on the fake frames, whose batch-size-
-    # dependent split-K plans round differently) to 1e-3
-    for phase, tol in (("E", 1e-4), ("M", 1e-3)):
+
+    def rel_by_param(net, a, b):
+        off = 0
+        for k, p in net.named_parameters():
+            n = p.numel()
+            in_bias = k.endswith("bias") and k not in ("model.26.bias", "model.0.bias", "model.11.bias")
+            if not in_bias:
+                x, y = a[off:off + n].astype(np.float64), b[off:off + n].astype(np.float64)
+                yield k, np.linalg.norm(x - y) / (np.linalg.norm(y) + 1e-30)
+            off += n
+
+    # (1) the exchange: every rank holds the mean of the ranks' half-batch gradients (to fp32 rounding
+    #     of the bucketed all-reduce).  (2) DP vs the whole batch in one process: the E-step to 1e-4; the
+    #     M-step's AM loss is an L1 of M(bf_real) against RAFT's flow of the fake frames, whose batch-size-
+    #     dependent plans round differently — sign flips of near-zero residuals move its gradients by
+    #     ~3e-3 (measured), so 1e-2 there
+    for phase, tol in (("E", 1e-4), ("M", 1e-2)):
         for name, ref in full[phase].items():
             r0, r1 = res[0][1][phase][name], res[1][1][phase][name]
             assert np.array_equal(r0, r1), (phase, name)
             net = getattr(m, "net" + name)
-            off = 0
-            for k, p in net.named_parameters():
-                n = p.numel()
-                in_bias = k.endswith("bias") and k not in ("model.26.bias", "model.0.bias", "model.11.bias")
-                if not in_bias:
-                    a, b = r0[off:off + n].astype(np.float64), ref[off:off + n].astype(np.float64)
-                    rel = np.linalg.norm(a - b) / (np.linalg.norm(b) + 1e-30)
-                    assert rel < tol, (phase, name, k, rel)
-                off += n
+            mean = (halves[0][phase][name].astype(np.float64) + halves[1][phase][name]) / world
+            for k, rel in rel_by_param(net, r0, mean):
+                assert rel < 1e-6, ("exchange", phase, name, k, rel)
+            for k, rel in rel_by_param(net, r0, ref):
+                assert rel < tol, (phase, name, k, rel)
             assert len(res[0][2][name]) > 0, (phase, name)   # buckets launched during backward

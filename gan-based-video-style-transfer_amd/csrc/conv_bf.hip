@@ -246,9 +246,17 @@ __device__ __forceinline__ void mma_frag(const Frag<T>& f, f32x16 (&acc)[T::MI][
 
 // Stage writer: A rows as fp32 pairs (split here), B rows as pre-split planes.  Masked rows were
 // loaded from the zero page, so every row is written unconditionally.
+#ifndef VST_BF_GLDS_B
+#define VST_BF_GLDS_B 1  // x6 M16 KSL forwards: the pre-split B operand LDS-DMA'd (global_load_lds_dwordx4)
+                         // instead of register-staged
+#endif
+#ifndef VST_BF_GLDS_W
+#define VST_BF_GLDS_W 0  // the same for the x6 weight gradient's dy planes (measured slower in the step: off)
+#endif
 template <class T>
 __device__ __forceinline__ void store_stage(char* st, const float4 (&ra)[T::A_LD][2],
-                                            const u32x4_t (&rbv)[T::B_LD][T::NP], int rb, int kq) {
+                                            const u32x4_t (&rbv)[T::B_LD][T::NP], int rb, int kq,
+                                            bool with_b = true) {
   char* Bs = st + T::A_BYTES;
 #pragma unroll
   for (int j = 0; j < T::A_LD; ++j) {
@@ -258,6 +266,7 @@ __device__ __forceinline__ void store_stage(char* st, const float4 (&ra)[T::A_LD
 #pragma unroll
     for (int p = 0; p < T::NP; ++p) *reinterpret_cast<uint4*>(st + p * T::A_PLANE + off) = s[p];
   }
+  if (!with_b) return;
 #pragma unroll
   for (int j = 0; j < T::B_LD; ++j) {
     const int off = swz_off<T>(rb + T::RPP * j, kq);
@@ -418,19 +427,34 @@ __device__ __forceinline__ void sched16() {
 //   C: barrier; (hi, hi), (lo, hi), (hi, lo)   read mid of stage kt + 1 (the freed mid set)
 // Every product term of the x6 sum is the 32x32x16 loop's; only the summation order of the six
 // terms into the fp32 accumulator differs (mid*mid first).
-template <class T, class LoadAll, class Adv, class Prep>
+struct NoDma {
+  static constexpr bool active = false;
+  __device__ __forceinline__ void operator()(char*) const {}
+};
+template <class F>
+struct DmaB {
+  static constexpr bool active = true;
+  F f;
+  __device__ __forceinline__ void operator()(char* st) const { f(st); }
+};
+typedef __attribute__((address_space(3))) void lds_void;
+
+// dmab(stage): VST_BF_GLDS_B's LDS-DMA of the B operand of the stage the K cursor points at into that
+// stage's LDS image (a no-op otherwise), issued at the prologue and at the start of every step.
+template <class T, class LoadAll, class Adv, class Prep, class DmaB>
 __device__ __forceinline__ void main_loop16(char* smem, int nk, f32x4v (&acc)[T::MI16][T::NI16],
                                             float4 (&ra)[2][T::A_LD][2], u32x4_t (&rbv)[2][T::B_LD][T::NP],
-                                            int rb, int kq, LoadAll load_all, Adv adv, Prep prep) {
+                                            int rb, int kq, LoadAll load_all, Adv adv, Prep prep, DmaB dmab) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int wm0 = (wave / T::WAVES_N) * T::WM, wn0 = (wave % T::WAVES_N) * T::WN;
   if (nk <= 0) return;
   constexpr int NM = T::MI16 * T::NI16, NR = T::MI16 + T::NI16;
   constexpr int NV = T::A_LD * 2 + T::B_LD * T::NP, NW = T::A_LD * T::NP + T::B_LD * T::NP;
   if (VST_M16_PRIO && wave >= T::NW / 2) __builtin_amdgcn_s_setprio(1);
+  dmab(smem);
   load_all(0);
   prep(0);
-  store_stage<T>(smem, ra[0], rbv[0], rb, kq);
+  store_stage<T>(smem, ra[0], rbv[0], rb, kq, !dmab.active);
   adv(nk > 1);
   load_all(1);
   __syncthreads();
@@ -441,6 +465,7 @@ __device__ __forceinline__ void main_loop16(char* smem, int nk, f32x4v (&acc)[T:
     const char* cur = smem + P * T::STAGE;
     char* nxt = smem + (P ^ 1) * T::STAGE;
     constexpr bool SA = VST_M16_STORE == 1, RA = VST_M16_RDLO == 1;
+    dmab(nxt);  // the cursor is on stage kt + 1 here (adv below moves it to kt + 2)
     if (VST_M16_LOADEARLY) {
       adv(kt + 2 < nk);
       load_all(P);
@@ -454,7 +479,7 @@ __device__ __forceinline__ void main_loop16(char* smem, int nk, f32x4v (&acc)[T:
     }
     if (SA) {
       prep(P ^ 1);
-      store_stage<T>(nxt, ra[P ^ 1], rbv[P ^ 1], rb, kq);
+      store_stage<T>(nxt, ra[P ^ 1], rbv[P ^ 1], rb, kq, !dmab.active);
     }
     mma16<T>(mid, mid, acc);
     if (VST_M16_SCHED) sched16<NM, RA ? 2 * NR : NR, NV, SA ? 4 : 0, SA ? NW : 0>();
@@ -462,7 +487,7 @@ __device__ __forceinline__ void main_loop16(char* smem, int nk, f32x4v (&acc)[T:
     if (!RA) read_plane16<T>(lo, cur, 2, wm0, wn0, lane);
     if (!SA) {
       prep(P ^ 1);
-      store_stage<T>(nxt, ra[P ^ 1], rbv[P ^ 1], rb, kq);
+      store_stage<T>(nxt, ra[P ^ 1], rbv[P ^ 1], rb, kq, !dmab.active);
     }
     mma16<T>(mid, hi, acc);
     mma16<T>(hi, mid, acc);
@@ -831,6 +856,7 @@ __device__ __forceinline__ void conv_fprop_bf_body(
 
   float4 ra[2][A_LD][2];
   u32x4_t rbv[2][B_LD][NP];
+  constexpr bool GLDS = VST_BF_GLDS_B && T::M16 && KSL && !C4 && REFL != 5;
   float4 nr[2][NRM ? 4 : 1];  // NRM: (mean, rstd) of the stage's 8 channels, per register set
   const float* nimg = NRM ? nst + (long)(m0 / (Ho * Wo)) * C * 2 : nullptr;
   auto load_all = [&](int set) __attribute__((always_inline)) {
@@ -879,6 +905,7 @@ __device__ __forceinline__ void conv_fprop_bf_body(
       ra[set][j][0] = *reinterpret_cast<const float4*>(p);
       ra[set][j][1] = *reinterpret_cast<const float4*>(p + 4);
     }
+    if constexpr (GLDS) return;  // B arrives by LDS-DMA (dma_b)
 #pragma unroll
     for (int j = 0; j < B_LD; ++j) {
 #pragma unroll
@@ -886,6 +913,26 @@ __device__ __forceinline__ void conv_fprop_bf_body(
         rbv[set][j][p] = *reinterpret_cast<const u32x4_t*>(
             VST_BF_FAKE_ZB == 1 ? reinterpret_cast<const __bf16*>(zp)
                                 : (VST_BF_FAKE_ZB == 2 ? ws : wrow[j]) + p * wps + kb);  // 2: weight row 0 for every row
+    }
+  };
+  // VST_BF_GLDS_B: the B image of the stage the cursor is on, one global_load_lds_dwordx4 per (row
+  // block, plane) and wave — a wave fills 16 whole 64-B rows (1 KiB, lane-linear): lane l's 16 B land
+  // at row 16 w + l / 4, slot l % 4, so it reads source chunk (l % 4) ^ swz(row) (the LDS image's
+  // chunk swizzle applied on the source address)
+  auto dma_b = [&](char* st) __attribute__((always_inline)) {
+    const int kbase = (tr * S + ts) * C + ksb;
+#pragma unroll
+    for (int j = 0; j < B_LD; ++j) {
+      const int row = rb + RPP * j;
+      const int csrc = (t % T::KC) ^ T::swz(row);
+      const int wrow0 = __builtin_amdgcn_readfirstlane(row - (lane / T::KC));  // the wave's first row
+#pragma unroll
+      for (int p = 0; p < NP; ++p) {
+#if defined(__HIP_DEVICE_COMPILE__)  // (a device builtin: the host pass only parses this body)
+        __builtin_amdgcn_global_load_lds(wrow[j] + p * wps + kbase + 8 * csrc,
+                                         (lds_void*)(st + T::A_BYTES + p * T::B_PLANE + wrow0 * T::ROWB), 16, 0, 0);
+#endif
+      }
     }
   };
   // go = false (the last two stages): the cursor stays on the final stage.  KSL: branch-free
@@ -934,7 +981,10 @@ __device__ __forceinline__ void conv_fprop_bf_body(
   if constexpr (T::M16) {
     f32x4v acc[T::MI16][T::NI16];
     zero_acc4(acc);
-    main_loop16<T>(smem, nk, acc, ra, rbv, rb, kq, load_all, adv, prep);
+    if constexpr (GLDS)
+      main_loop16<T>(smem, nk, acc, ra, rbv, rb, kq, load_all, adv, prep, DmaB<decltype(dma_b)>{dma_b});
+    else
+      main_loop16<T>(smem, nk, acc, ra, rbv, rb, kq, load_all, adv, prep, NoDma{});
     if constexpr (SPLIT) {
       float* sl = slab + (long)zs * (M - m_base) * Cop;
 #pragma unroll
@@ -1193,6 +1243,7 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_wgrad_bf_k(
   }
   float4 ra[2][A_LD][2];
   u32x4_t rbv[2][B_LD][NP];
+  constexpr bool GLDS = VST_BF_GLDS_W && T::M16;
   auto load_all = [&](int set) __attribute__((always_inline)) {
     const bool live = kp < pend;  // 8-pixel chunks never straddle pend (chunk, P multiples of 8)
 #pragma unroll
@@ -1203,12 +1254,34 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_wgrad_bf_k(
       ra[set][j][0] = make_float4(u0.x, u0.y, u0.z, u0.w);
       ra[set][j][1] = make_float4(u1.x, u1.y, u1.z, u1.w);
     }
+    if constexpr (GLDS) return;  // B arrives by LDS-DMA (dma_b)
 #pragma unroll
     for (int j = 0; j < B_LD; ++j) {
       const __bf16* q = live ? drow[j] + kp : zpb;
       const long ps = live ? dps : 0;
 #pragma unroll
       for (int p = 0; p < NP; ++p) rbv[set][j][p] = *reinterpret_cast<const u32x4_t*>(q + p * ps);
+    }
+  };
+  // VST_BF_GLDS_B: the dy planes' stage image by LDS-DMA (as conv_fprop_bf_body's dma_b: lane l fills
+  // row 16 w + l / 4, slot l % 4 from source chunk (l % 4) ^ swz(row); the cursor kp is on that stage)
+  auto dma_b = [&](char* stg) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < B_LD; ++j) {
+      const int row = rb + RPP * j;
+      const int csrc = (t % T::KC) ^ T::swz(row);
+      const int wrow0 = __builtin_amdgcn_readfirstlane(row - (lane / T::KC));
+      const int kpc = kp - 8 * kq + 8 * csrc;
+      const bool lv = kpc < pend;
+      const __bf16* q = lv ? drow[j] + kpc : zpb;
+      const long ps = lv ? dps : 0;
+#pragma unroll
+      for (int p = 0; p < NP; ++p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+        __builtin_amdgcn_global_load_lds(q + p * ps, (lds_void*)(stg + T::A_BYTES + p * T::B_PLANE + wrow0 * T::ROWB),
+                                         16, 0, 0);
+#endif
+      }
     }
   };
   const long row_step = (long)st * Wp - Wo, img_step = (long)(Hp - st * Ho) * Wp;
@@ -1241,7 +1314,10 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_wgrad_bf_k(
   if constexpr (T::M16) {
     f32x4v acc[T::MI16][T::NI16];
     zero_acc4(acc);
-    main_loop16<T>(smem, nk, acc, ra, rbv, rb, kq, load_all, adv, [](int) {});
+    if constexpr (GLDS)
+      main_loop16<T>(smem, nk, acc, ra, rbv, rb, kq, load_all, adv, [](int) {}, DmaB<decltype(dma_b)>{dma_b});
+    else
+      main_loop16<T>(smem, nk, acc, ra, rbv, rb, kq, load_all, adv, [](int) {}, NoDma{});
 #pragma unroll
     for (int i = 0; i < T::MI16; ++i)
 #pragma unroll

@@ -85,6 +85,7 @@ SIGNATURES = {
     "vst_conv2d_fwd_ws_bytes": (SZ, [I, I, I, I, I, I, I, I, I, I]),
     "vst_conv2d_fwd_ws": (I, [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, I, P, P, P, SZ, P]),
     "vst_conv2d_fwd_nrm_ok": (I, [I, I, I, I, I, I, I, I, I, I, I]),
+    "vst_c4_dgrad_frame": (I, [P, P, P, I, I, I, I, I, I, P]),
     "vst_conv2d_fwd_nrm_ws": (I, [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, I, P, P, P, SZ, P]),
     "vst_conv_plan_fwd_tail": (I, [I, I, I, I, I, I, I, I, I, I, P]),
     "vst_reflect_fold_instnorm_bwd": (I, [P, P, P, P, P, P, P, P, I, I, I, I, I, I, F, I, P, L, P]),

@@ -677,4 +677,90 @@ int c4_direct_launch(const float* x, const void* wsplit, long wps, const float* 
   return check_launch("conv2d_fwd(4-channel direct)");
 }
 
+// ------------------------------------------------- reflect-pad data gradient of a 4-channel 7x7 conv
+// The data gradient of ReflectionPad2d(p) + Conv2d(C -> 4, R x R) (the generator's last layer,
+// networks.py:365-366) is dx = fold(dxp), dxp = the zero-pad-(R-1) full correlation of dy with the
+// rotated taps over the (H+2p) x (W+2p) padded frame, fold = the reflect map back onto H x W.  Its
+// interior dxp[i+p][j+p] is the zero-pad-p conv of dy (the direct 4-channel kernel, 256-wide rows);
+// this pass adds the frame: every pixel whose row or column reflects a frame position (rows 1..p and
+// H-1-p..H-2, columns likewise) gets, in a fixed order (q, then p ascending), the dxp values of the
+// frame positions folding onto it — computed here in fp32 from dy (only the taps that reach dy: row
+// q of the frame reads dy rows q - (R-1) .. q).  One writer per dx element: deterministic.
+// grid (ceil(N * B / 64), C / 16), 256 threads: thread = (border pixel, 4-channel group of 16).
+__global__ __launch_bounds__(256) void c4_dgrad_frame_k(const float* __restrict__ dy, const float* __restrict__ w,
+                                                        float* __restrict__ dx, int N, int H, int W, int C, int R,
+                                                        int pad) {
+  const int rows = 2 * pad * W, B = rows + 2 * pad * (H - 2 * pad);
+  const long b = (long)blockIdx.x * 64 + (threadIdx.x >> 2);
+  const int cg = blockIdx.y * 16 + (threadIdx.x & 3) * 4;
+  if (b >= (long)N * B || cg >= C) return;
+  const int n = (int)(b / B), k = (int)(b - (long)n * B);
+  int i, j;
+  if (k < rows) {
+    const int rr = k / W;
+    i = rr < pad ? 1 + rr : H - 1 - pad + (rr - pad);
+    j = k - rr * W;
+  } else {  // the column bands over the rows the row bands do not hold: 0, pad + 1 .. H - 2 - pad, H - 1
+    const int kk = k - rows, hr = H - 2 * pad, cc = kk / hr, t = kk - cc * hr;
+    j = cc < pad ? 1 + cc : W - 1 - pad + (cc - pad);
+    i = t == 0 ? 0 : (t == hr - 1 ? H - 1 : t + pad);
+  }
+  // padded rows / columns folding onto i / j: the direct one (i + pad) and the mirror, if any
+  int qs[2], ps[2], nq = 0, np = 0;
+  if (i >= 1 && i <= pad) qs[nq++] = pad - i;
+  qs[nq++] = i + pad;
+  if (i >= H - 1 - pad && i <= H - 2) qs[nq++] = 2 * H - 2 + pad - i;
+  if (j >= 1 && j <= pad) ps[np++] = pad - j;
+  ps[np++] = j + pad;
+  if (j >= W - 1 - pad && j <= W - 2) ps[np++] = 2 * W - 2 + pad - j;
+  const int off = R - 1;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int a = 0; a < nq; ++a)
+    for (int c = 0; c < np; ++c) {
+      const int q = qs[a], pp = ps[c];
+      if (q == i + pad && pp == j + pad) continue;  // the interior term: the conv already wrote it
+      float v[4] = {0.f, 0.f, 0.f, 0.f};  // (plain arrays: HIP's float4 members are accessor objects)
+      for (int r = 0; r < R; ++r) {
+        const int h = q + r - off;
+        if ((unsigned)h >= (unsigned)H) continue;
+        for (int s = 0; s < R; ++s) {
+          const int x = pp + s - off;
+          if ((unsigned)x >= (unsigned)W) continue;
+          const float4 d = *reinterpret_cast<const float4*>(dy + (((long)n * H + h) * W + x) * 4);
+          const float* wp = w + ((long)cg * R * R + r * R + s) * 4;
+          const long cs = (long)R * R * 4;  // next output channel's taps
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const float4 ww = *reinterpret_cast<const float4*>(wp + u * cs);
+            v[u] += d.x * ww.x + d.y * ww.y + d.z * ww.z + d.w * ww.w;
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc[u] += v[u];
+    }
+  float4* o = reinterpret_cast<float4*>(dx + (((long)n * H + i) * W + j) * C + cg);
+  float4 y = *o;
+  y.x += acc[0];
+  y.y += acc[1];
+  y.z += acc[2];
+  y.w += acc[3];
+  *o = y;
+}
+
 }  // namespace vst
+
+using namespace vst;
+
+// dx (N, H, W, C; the interior conv's output) += the reflect-fold frame terms of the data gradient of
+// ReflectionPad2d(pad) + Conv2d(C -> 4, R x R); dy NHWC4, w = the VST_PACK_IKF pack [C][R][R][4] fp32.
+extern "C" int vst_c4_dgrad_frame(const float* dy, const float* w, float* dx, int N, int H, int W, int C, int R,
+                                  int pad, void* stream) {
+  VST_REQUIRE(dy && w && dx && N > 0 && C % 16 == 0 && R >= 1 && pad >= 1 && 2 * pad + 2 <= H && 2 * pad + 2 <= W &&
+                  R - 1 == 2 * pad,
+              "c4_dgrad_frame: bad args (C %% 16 == 0, R = 2 pad + 1, H, W > 2 pad + 1)");
+  const long B = 2L * pad * W + 2L * pad * (H - 2 * pad);
+  hipLaunchKernelGGL(c4_dgrad_frame_k, dim3((unsigned)ceil_div((long)N * B, 64), C / 16), dim3(256), 0,
+                     (hipStream_t)stream, dy, w, dx, N, H, W, C, R, pad);
+  return check_launch("c4_dgrad_frame");
+}

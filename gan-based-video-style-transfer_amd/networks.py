@@ -700,7 +700,9 @@ class _GeneratorFn(torch.autograd.Function):
         else:
             wgrad(f, a, g, 7, 1, 3, "reflect", db=True)
         done(f)
-        if "f4" in P["ikf"] and g.shape[-1] == 4:
+        if "f4" in P["ikf"] and g.shape[-1] == 4 and ops.c4_dgrad_reflect_ok(g, a.shape[-1], 7, 3):
+            ga = ops.c4_dgrad_reflect(g, P["ikf"]["f4"], a.shape[1], a.shape[2], a.shape[-1], 7, 3)
+        elif "f4" in P["ikf"] and g.shape[-1] == 4:
             ga = ops.conv2d_dgrad_s1(g, P["ikf"]["f4"], a.shape[1], a.shape[2], a.shape[-1], 7, 3, "reflect")
         elif "f8" in P["ikf"] and g.shape[-1] == 4:
             ga = ops.conv2d_dgrad_s1(_pad_channels(g, 8), P["ikf"]["f8"], a.shape[1], a.shape[2], a.shape[-1], 7,

@@ -487,6 +487,29 @@ def conv2d_dgrad_s1(dy, ikf, H, W, cx, R, pad, pad_mode="zero", addend=None, rol
     return dx
 
 
+# The data gradient of ReflectionPad2d(p) + Conv2d(C -> 4, 7x7) (the generator's last layer) as the
+# zero-pad-p conv of dy on the direct 4-channel kernel + the reflect-fold frame (vst_c4_dgrad_frame),
+# instead of the conv over the (H+2p) x (W+2p) padded frame + reflect_fold.  VST_C4_DGRAD=0: that route.
+C4_DGRAD = os.environ.get("VST_C4_DGRAD", "1") != "0"
+
+
+def c4_dgrad_reflect_ok(dy, cx, R, pad, role="bwd"):
+    N, H, W, C = dy.shape
+    return (C4_DGRAD and C == 4 and cx % 16 == 0 and R == 2 * pad + 1 and H > 2 * pad + 1 and W > 2 * pad + 1
+            and conv_plan_fwd(N, H, W, 4, cx, R, R, 1, pad, pad, role)[0] == PLAN_C4_DIRECT)
+
+
+def c4_dgrad_reflect(dy, ikf, H, W, cx, R, pad, role="bwd"):
+    """dx of ReflectionPad2d(pad) + Conv2d(cx -> 4, R x R) from the 4-channel dy (ikf: VST_PACK_IKF):
+    the interior dxp[i+pad][j+pad] as the zero-pad-pad forward conv over dy (the direct 4-channel
+    kernel), then vst_c4_dgrad_frame adds the reflect-fold terms of the padded frame's border."""
+    _dev_check(dy, ikf)
+    N = dy.shape[0]
+    dx = conv2d_fwd(dy, ikf, None, cx, R, R, 1, pad, "zero", role=role)
+    _call("vst_c4_dgrad_frame", _p(dy), _p(ikf), _p(dx), N, H, W, cx, R, pad, _stream())
+    return dx
+
+
 def conv2d_dgrad_s1_in(dy, ikf, H, W, cx, R, pad, y_in, stats, act="relu", slope=0.0, addend=None, db=None,
                        accumulate_db=True, planes=False, role="bwd"):
     """conv2d_dgrad_s1 (reflect) whose fold also runs the InstanceNorm(+act) backward of the layer

@@ -133,6 +133,14 @@ size_t vst_conv2d_fwd_ws_bytes(int N, int H, int W, int Cx, int Cop, int R, int 
 int vst_conv2d_fwd_ws(const float* x, const float* wp, const void* wsplit, const float* bias, float* y, int N,
                       int H, int W, int Cx, int Cop, int R, int S, int stride, int pad, int pad_mode, int act,
                       float slope, int math, double* part, int* nsplit, float* ws, size_t ws_bytes, void* stream);
+/* The data gradient of ReflectionPad2d(pad) + Conv2d(C -> 4, R x R) (the generator's last layer,
+ * networks.py:365-366) without the padded frame: dx = vst_conv2d_fwd(dy, the VST_PACK_IKF pack, zero
+ * padding pad) — the interior of the full correlation — then this pass adds, in a fixed order, the
+ * frame positions that the reflect fold maps onto rows / columns 1..pad and H-1-pad..H-2 (fp32, from dy;
+ * one writer per element).  dy NHWC4, w the fp32 IKF pack [C][R][R][4], dx NHWC C; R = 2 pad + 1,
+ * C % 16 == 0.  Replaces the conv over the (H+2pad) x (W+2pad) frame + vst_reflect_fold. */
+int vst_c4_dgrad_frame(const float* dy, const float* w, float* dx, int N, int H, int W, int C, int R, int pad,
+                       void* stream);
 /* A forward conv over relu(IN(x)) without the normalised activation: x = the raw output of the previous
  * conv, nst = its InstanceNorm statistics [N][Cx][2] (mean, rstd); every gathered A value enters as
  * relu((v - mean) * rstd) (in_apply's expression), inside the GEMM's A staging.  Replaces

@@ -1031,3 +1031,24 @@ def test_conv_fwd_nrm_matches_apply_then_conv(ops, N):
         assert torch.equal(s, s_ref)
     finally:
         ops.set_conv_math(prev)
+
+
+@pytest.mark.parametrize("N,H,W", [(2, 256, 256), (1, 20, 256), (3, 64, 64), (1, 436, 1024), (12, 256, 256)])
+def test_c4_dgrad_reflect(ops, N, H, W, conv_math):
+    """The last layer's data gradient (ReflectionPad2d(3) + Conv2d(64 -> 3, 7x7), networks.py:365-366)
+    as the direct-kernel interior conv + vst_c4_dgrad_frame, vs torch autograd and vs the padded-frame
+    conv + reflect fold route (same products; the frame terms are fp32 FMAs)."""
+    if conv_math == "fp32":
+        pytest.skip("the direct kernel is a split-bf16 kernel")
+    Ci, Co, R, pad = 64, 3, 7, 3
+    x = _g(101, (N, Ci, H, W)).to(DEV).requires_grad_(True)
+    w = _g(102, (Co, Ci, R, R), 0.05).to(DEV)
+    gy = _g(103, (N, Co, H, W)).to(DEV)
+    F.conv2d(F.pad(x, (pad,) * 4, mode="reflect"), w).backward(gy)
+    ikf = ops.weight_pack(w, ops.PACK_IKF)
+    g4 = _nhwc(gy.cpu(), ops)
+    assert ops.c4_dgrad_reflect_ok(g4, Ci, R, pad)
+    dx = ops.c4_dgrad_reflect(g4, ikf, H, W, Ci, R, pad)
+    _close(_nchw(dx, Ci, ops), x.grad, tol=CONV_TOL[conv_math], what="c4 dgrad vs torch")
+    ref = ops.conv2d_dgrad_s1(g4, ikf, H, W, Ci, R, pad, "reflect")
+    _close(dx, ref, tol=CONV_TOL[conv_math], what="c4 dgrad vs frame + fold")

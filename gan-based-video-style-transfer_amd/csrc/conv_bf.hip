@@ -743,7 +743,8 @@ __device__ __forceinline__ void conv_fprop_bf_body(
     float* __restrict__ y, int H, int W, int C, int Ho, int Wo, int Cop, int S, int st, int padh,
     int padw, int reflect, int act, float slope, int M, int Ktot, int m_base, double* __restrict__ part,
     int spk, float* __restrict__ slab, const float* __restrict__ addend, int oph,
-    const float* __restrict__ nst = nullptr) {
+    const float* __restrict__ nst = nullptr, const float* __restrict__ bslab = nullptr, int bks = 0, int bmb = 0,
+    int blt = 0, int bll = 0) {
   static_assert(!SPLIT || KSL, "split-K needs the channel-slice-major K walk");
   static_assert(!NRM || (KSL && REFL == 1), "normalised A: the channel-slice K walk, reflect padding");
   static_assert(REFL < 4 || (SPLIT && KSL), "border rows run as split-K slabs");
@@ -1008,7 +1009,7 @@ __device__ __forceinline__ void conv_fprop_bf_body(
     // (an addend — the residual gradient of a data gradient — is always added on this path: its float4
     // loads ride with the row stores instead of 4-byte reads per accumulator element)
     constexpr bool LFIT = T::BM * (T::BN + 16) * 4 <= 2 * T::STAGE;
-    const bool LEPI = LFIT && (VST_BF_LDS_EPI || addend != nullptr || oph != 0);
+    const bool LEPI = LFIT && (VST_BF_LDS_EPI || addend != nullptr || oph != 0 || bslab != nullptr);
     constexpr int LDE = T::BN + 16;
     float* ept = reinterpret_cast<float*>(smem);
     if (LEPI) __syncthreads();  // every wave is done reading the last stage
@@ -1059,6 +1060,22 @@ __device__ __forceinline__ void conv_fprop_bf_body(
         if (mm < M && n < Cop && orow >= 0) {
           float4 v = *reinterpret_cast<const float4*>(ept + row * LDE + c);
           if (addend) add_f4(v, *reinterpret_cast<const float4*>(addend + (long)mm * Cop + n));
+          if (bslab) {  // the reflect-pad-1 data gradient's border slabs (dgrad_border5_add_k's sums, same order)
+            const int hw = Ho * Wo, img = mm / hw, rem = mm - img * hw, h = rem / Wo, w = rem - h * Wo;
+            if (h == 1 || h == Ho - 2 || w == 1 || w == Wo - 2) {
+              int rows[3];
+              const int nr = dgrad_border_slab_rows(img, h, w, Ho, Wo, blt, bll, rows);
+              const long zst = (long)bmb * Cop;
+              float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+              for (int r = 0; r < nr; ++r) {
+                const float* base = bslab + (long)rows[r] * Cop + n;
+                float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+                for (int z = 0; z < bks; ++z) add_f4(acc, *reinterpret_cast<const float4*>(base + z * zst));
+                add_f4(bv, acc);
+              }
+              add_f4(v, bv);
+            }
+          }
           *reinterpret_cast<float4*>(y + (long)orow * Cop + n) = v;
         }
       }
@@ -1127,6 +1144,18 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_k(
     int spk = 0, float* __restrict__ slab = nullptr, const float* __restrict__ addend = nullptr, int oph = 0) {
   conv_fprop_bf_body<T, KSL, REFL, SPLIT>(blockIdx.x, x, ws, wps, bias, y, H, W, C, Ho, Wo, Cop, S, st, padh, padw,
                                           reflect, act, slope, M, Ktot, m_base, part, spk, slab, addend, oph);
+}
+
+// The interior conv of the reflect-pad-1 data gradient with the border GEMM's slabs (written before it)
+// added in its LDS-staged epilogue (the addend path): dgrad_border5_add_k's work without its launch.
+template <class T>
+__global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_bord_k(
+    const float* __restrict__ x, const __bf16* __restrict__ ws, long wps, float* __restrict__ y, int H, int W, int C,
+    int Cop, const float* __restrict__ addend, int M, int Ktot, const float* __restrict__ bslab, int bks, int bmb,
+    int blt, int bll) {
+  conv_fprop_bf_body<T, true, 0, false>(blockIdx.x, x, ws, wps, nullptr, y, H, W, C, H, W, Cop, 3, 1, 1, 1, 0,
+                                        VST_ACT_NONE, 0.f, M, Ktot, 0, nullptr, 0, nullptr, addend, 0, nullptr, bslab,
+                                        bks, bmb, blt, bll);
 }
 
 // conv_fprop_bf_k over relu(IN(x)) (NRM: the normalisation in the A staging; nst = x's IN statistics)
@@ -1853,6 +1882,14 @@ size_t bf_dgrad_refl1_ws_floats(int N, int H, int W, int Cy, int Cx, int math) {
 // on: the K-restricted border GEMM and dgrad_border5_add_k).  Replaces the conv over the
 // (H+2) x (W+2) zero-padded frame + reflect fold.  add_border = false: the slabs (bf_dgrad_refl1_slabs)
 // are left for the caller (vst_conv2d_dgrad_refl_in adds them in its InstanceNorm-backward partial pass).
+#ifndef VST_BORDER_FUSE
+#define VST_BORDER_FUSE 0  // the border slabs added by the interior conv's epilogue (border GEMM first): measured +0.5 ms/step, off
+#endif
+static const bool g_border_fuse = [] {  // VST_BORDER_FUSE=1 in the environment turns the variant on
+  const char* e = getenv("VST_BORDER_FUSE");
+  return e ? e[0] == '1' : VST_BORDER_FUSE != 0;
+}();
+
 int bf_dgrad_refl1_launch(const float* dy, const void* wsplit, long wps, const float* addend, float* dx, int N, int H,
                           int W, int Cy, int Cx, int math, hipStream_t s, float* ws, size_t ws_floats, bool add_border) {
   int ks;
@@ -1860,6 +1897,35 @@ int bf_dgrad_refl1_launch(const float* dy, const void* wsplit, long wps, const f
   bf_border_plan(N, H, W, Cy, Cx, math, &ks, &Mb);
   const size_t main_ws = bf_fprop_ws_floats((long)N * H * W, Cx, Cy, 3, 3, math);
   VST_REQUIRE(ws_floats >= main_ws + (size_t)ks * Mb * Cx, "dgrad_refl: workspace too small");
+  {
+    // whole 256x128 rounds (no split-K tail), x6: the K-restricted border GEMM first, then the interior
+    // conv adding the slabs in its LDS-staged epilogue (bit-identical to interior + dgrad_border5_add_k)
+    int kd, m_split, tail_kind, m_first, fks;
+    const long M = (long)N * H * W;
+    bf_plan(M, Cx, math, -1, &kd, &m_split, &tail_kind);
+    bf_split_plan(M, Cx, Cy, 3, 3, math, -1, &m_first, &fks);
+    if (g_border_fuse && g_border5 && add_border && math == VST_MATH_BF16X6 && kd == 7 && !m_split && !fks &&
+        Cy % 32 == 0 && Cx % 4 == 0) {
+      int ks5, lt, ll;
+      bf_border5_plan(N, H, W, Cy, Cx, &ks5, &lt, &ll);
+      const int Mt = 2 * lt + 2 * ll, K5 = 3 * Cy;
+      VST_REQUIRE(ws_floats >= main_ws + (size_t)ks5 * Mt * Cx, "dgrad_refl: workspace too small");
+      float* slab5 = ws + main_ws;
+      const __bf16* wb = reinterpret_cast<const __bf16*>(wsplit);
+      {
+        using T = bf::Tile<128, 128, 64, 32, 32, 3>;
+        const int nk = (K5 + T::BK - 1) / T::BK, spk = (nk + ks5 - 1) / ks5;
+        const dim3 grid(Mt / 128 * ceil_div(Cx, 128) * ks5);
+        hipLaunchKernelGGL((bf::conv_fprop_bf_k<T, true, 5, true>), grid, dim3(T::NT), 0, s, dy, wb, wps, nullptr, dx, H,
+                           W, Cy, lt, ll, Cx, 3, N, 1, 1, 0, VST_ACT_NONE, 0.f, Mt, K5, 0, nullptr, spk, slab5, nullptr);
+      }
+      using T = bf::Tile<256, 128, 64, 64, 32, 3>;
+      const dim3 grid(ceil_div(M, 256) * ceil_div(Cx, 128));
+      hipLaunchKernelGGL((bf::conv_fprop_bf_bord_k<T>), grid, dim3(T::NT), 0, s, dy, wb, wps, dx, H, W, Cy, Cx, addend,
+                         (int)M, 9 * Cy, slab5, ks5, Mt, lt, ll);
+      return check_launch("conv2d_dgrad_refl(fused border)");
+    }
+  }
   if (int e = bf_fprop_launch(dy, wsplit, wps, nullptr, dx, N, H, W, Cy, H, W, Cx, 3, 3, 1, 1, 1, 0, VST_ACT_NONE, 0.f,
                               math, -1, s, nullptr, main_ws ? ws : nullptr, main_ws, addend))
     return e;

@@ -79,6 +79,7 @@ SIGNATURES = {
     "vst_instnorm_act_bwd_planes": (I, [P, P, P, P, P, P, I, I, I, I, F, I, P, L, P]),
     "vst_conv2d_wgrad_pre": (I, [P, P, P, P, P, P, SZ, I, I, I, I, I, I, I, I, I, I, I, I, I, I, L, L, I, I, P]),
     "vst_instnorm_act_fwd_cp": (I, [P, P, P, P, P, I, I, I, I, I, F, I, I, I, P]),
+    "vst_instnorm_act_fwd_planes": (I, [P, P, P, P, P, I, I, I, I, I, F, I, I, I, P]),
     "vst_cp_ld": (L, [L]),
     "vst_conv2d_fwd_co": (I, [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, I, I, P]),
     "vst_tapfold_planes": (I, [P, P, L, I, I, I, I, I, I, I, P]),
@@ -144,6 +145,9 @@ SIGNATURES = {
     "vst_tapsum_fwd": (I, [P, I, P, P, I, I, I, I, I, I, I, I, F, P]),
     "vst_tapfold": (I, [P, P, I, I, I, I, I, I, I, P]),
     "vst_tap_wgrad_scatter": (I, [P, P, I, I, I, I, I, P]),
+    "vst_tap_wgrad_swap": (I, [P, P, P, P, SZ, I, I, I, I, I, I, I, I, P]),
+    "vst_tap_wgrad_swap_ws_bytes": (SZ, [I, I, I, I, I]),
+    "vst_tap_wgrad_swap_ld": (L, [I, I, I, I]),
     "vst_tapgather": (I, [P, P, I, I, I, I, I, I, I, P]),
     "vst_interleave_phases": (I, [P, P, P, P, P, I, I, I, I, P]),
     "vst_interleave_phases_full": (I, [P, P, P, P, P, I, I, I, I, P]),

@@ -1152,10 +1152,12 @@ extern "C" int vst_conv2d_wgrad_pre(const float* x, const float* x_t, const floa
                                     long si, int accumulate, int math, void* stream) {
   VST_REQUIRE(x && dy && dw && ws, "conv2d_wgrad: null pointer");
   VST_REQUIRE(math >= VST_MATH_F32 && math <= VST_MATH_BF16X6, "conv2d_wgrad: bad math %d", math);
-  VST_REQUIRE(Cx % 4 == 0 && Cyp % 4 == 0, "conv2d_wgrad: channel strides must be multiples of 4");
+  const WgradPlan p = plan_wgrad(N, H, W, Ho, Wo, Cx, Cyp, R, S, stride, math);
+  // any Cx when the split-bf16 kernel reads a caller-made channel-major x image (no NHWC vector loads of x)
+  VST_REQUIRE((Cx % 4 == 0 || (x_t && p.bfk && !p.wpad)) && Cyp % 4 == 0,
+              "conv2d_wgrad: channel strides must be multiples of 4");
   VST_REQUIRE(Co <= Cyp && Ci <= Cx, "conv2d_wgrad: logical channels exceed strides");
   VST_REQUIRE(pad_mode == VST_PAD_ZERO || (pad < H && pad < W), "conv2d_wgrad: reflect pad >= size");
-  const WgradPlan p = plan_wgrad(N, H, W, Ho, Wo, Cx, Cyp, R, S, stride, math);
   VST_REQUIRE(ws_bytes >= wgrad_ws_floats(p, Cyp) * sizeof(float),
               "conv2d_wgrad: workspace too small (%zu bytes)", ws_bytes);
   hipStream_t s = (hipStream_t)stream;

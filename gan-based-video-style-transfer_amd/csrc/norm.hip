@@ -457,20 +457,31 @@ __global__ void in_apply_k(const float4* __restrict__ x, const float* __restrict
   y[i] = v;
 }
 
+// RNE bf16 pair (the split of vst_weight_split / nhwc_to_cp_planes_k)
+__device__ __forceinline__ uint32_t bf16_pack2(float a, float b) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  typedef __bf16 b2 __attribute__((ext_vector_type(2)));
+  const f2 v = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, b2));
+}
+
 // in_apply_k fused with the weight gradient's A-operand image of the conv that consumes the result:
 // a = act(IN(y)) (+ residual) written NHWC (the next conv's input) AND as the padded channel-major
 // copy [C][N][H+2p][W+2p] (reflect or zero border; phase: stride-2 column-phase rows) that
 // nhwc_to_cp_pad_k would make from a in the backward pass — the backward's read of a and its
 // launch are gone.  Walks padded pixels in 64 x 64 LDS tiles (as nhwc_to_cp_pad_k); the interior
-// positions also store a.  grid (ceil(N (H+2p)(W+2p) / 64), ceil(C / 64)), 256 threads.
+// positions also store a.  grid (ceil(N (H+2p)(W+2p+wx) / 64), ceil(C / 64)), 256 threads.
+// planes != null: the image goes out as three bf16 planes [3][C][ld] (the RNE split of
+// nhwc_to_cp_planes_k) instead of fp32 — the x6 weight gradient's B operand when a is the "output"
+// side of the GEMM (tap_wgrad_swap) — and each padded row carries wx more zero columns.
 __global__ __launch_bounds__(256) void in_apply_cp_pad_k(const float* __restrict__ x, const float* __restrict__ stats,
                                                           const float* __restrict__ res, float* __restrict__ a,
                                                           float* __restrict__ xt, int N, int H, int W, int C,
                                                           int pad, int reflect, int phase, long ld, int act,
-                                                          float slope) {
+                                                          float slope, int wx = 0, __bf16* __restrict__ planes = nullptr) {
   __shared__ float tile[64][65];
-  const int Hp = H + 2 * pad, Wp = W + 2 * pad;
-  const long P = (long)N * Hp * Wp;
+  const int Hp = H + 2 * pad, Wp = W + 2 * pad, Wq = Wp + wx;
+  const long P = (long)N * Hp * Wq;
   const long p0 = (long)blockIdx.x * 64;
   const int c0 = blockIdx.y * 64;
   const int t = threadIdx.x;
@@ -480,9 +491,10 @@ __global__ __launch_bounds__(256) void in_apply_cp_pad_k(const float* __restrict
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     const long q = p0 + pr;
     if (q < P && c0 + c4 < C) {
-      const int n = (int)(q / ((long)Hp * Wp));
-      const int rem = (int)(q - (long)n * Hp * Wp);
-      int h = rem / Wp - pad, w = rem % Wp;
+      const int n = (int)(q / ((long)Hp * Wq));
+      const int rem = (int)(q - (long)n * Hp * Wq);
+      int h = rem / Wq - pad, w = rem % Wq;
+      const bool xcol = w >= Wp;  // one of the wx zero columns
       if (phase) {
         const int wh = Wp >> 1;
         w = w < wh ? 2 * w : 2 * (w - wh) + 1;
@@ -490,7 +502,7 @@ __global__ __launch_bounds__(256) void in_apply_cp_pad_k(const float* __restrict
       w -= pad;
       const bool inner = (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
       bool ok = inner;
-      if (reflect) {
+      if (reflect && !xcol) {
         h = reflect_idx(h, H);
         w = reflect_idx(w, W);
         ok = true;
@@ -514,6 +526,33 @@ __global__ __launch_bounds__(256) void in_apply_cp_pad_k(const float* __restrict
     tile[pr][c4 + 3] = v.w;
   }
   __syncthreads();
+  if (planes) {
+    const long plane = (long)C * ld;
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int idx = t + 256 * it, cr = idx >> 4, p4 = (idx & 15) * 4;
+      if (c0 + cr >= C || p0 + p4 >= P) continue;
+      float r[4] = {tile[p4][cr], tile[p4 + 1][cr], tile[p4 + 2][cr], tile[p4 + 3][cr]};
+      __bf16* dst = planes + (long)(c0 + cr) * ld + p0 + p4;
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) {
+        const uint32_t q0 = bf16_pack2(r[0], r[1]), q1 = bf16_pack2(r[2], r[3]);
+        if (p0 + p4 + 3 < P) {
+          *reinterpret_cast<uint2*>(dst + pl * plane) = make_uint2(q0, q1);
+        } else {
+          const uint16_t h[4] = {(uint16_t)q0, (uint16_t)(q0 >> 16), (uint16_t)q1, (uint16_t)(q1 >> 16)};
+          for (int e = 0; e < 4 && p0 + p4 + e < P; ++e) reinterpret_cast<uint16_t*>(dst + pl * plane)[e] = h[e];
+        }
+        if (pl < 2) {
+          r[0] -= __uint_as_float(q0 << 16);
+          r[1] -= __uint_as_float(q0 & 0xffff0000u);
+          r[2] -= __uint_as_float(q1 << 16);
+          r[3] -= __uint_as_float(q1 & 0xffff0000u);
+        }
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int it = 0; it < 4; ++it) {
     const int idx = t + 256 * it, cr = idx >> 4, p4 = (idx & 15) * 4;
@@ -576,12 +615,6 @@ __global__ void in_bwd_apply_k(const float4* __restrict__ gy, const float4* __re
 // the RNE split of vst_weight_split / nhwc_to_cp_planes_k) through a 64-pixel x 64-channel LDS
 // transpose tile — the conv below the IN consumes dx both ways, so the plane copy's extra read of dx
 // is gone.  grid (ceil(P / 64), ceil(C / 64)), 256 threads.
-__device__ __forceinline__ uint32_t bf16_pack2(float a, float b) {
-  typedef float f2 __attribute__((ext_vector_type(2)));
-  typedef __bf16 b2 __attribute__((ext_vector_type(2)));
-  const f2 v = {a, b};
-  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, b2));
-}
 
 __global__ __launch_bounds__(256) void in_bwd_apply_planes_k(const float* __restrict__ gy, const float* __restrict__ x,
                                                               const float* __restrict__ stats,
@@ -982,6 +1015,18 @@ extern "C" int vst_instnorm_act_fwd_cp(const float* x, const float* stats, const
                      x, stats, residual, y, xt, N, H, W, C, pad, pad_mode == VST_PAD_REFLECT, stride == 2,
                      rk_cp_ld(P), act, slope);
   return check_launch("instnorm_act_fwd_cp");
+}
+
+extern "C" int vst_instnorm_act_fwd_planes(const float* x, const float* stats, const float* residual, float* y,
+                                           void* planes, int N, int H, int W, int C, int act, float slope, int pad,
+                                           int pad_mode, int wx, void* stream) {
+  VST_REQUIRE(x && stats && y && planes && C % 4 == 0 && pad >= 0 && wx >= 0, "instnorm_act_fwd_planes: bad args");
+  VST_REQUIRE(pad_mode == VST_PAD_ZERO || (pad < H && pad < W), "instnorm_act_fwd_planes: reflect pad >= size");
+  const long P = (long)N * (H + 2 * pad) * (W + 2 * pad + wx);
+  hipLaunchKernelGGL(in_apply_cp_pad_k, dim3(ceil_div(P, 64), ceil_div(C, 64)), dim3(256), 0, (hipStream_t)stream,
+                     x, stats, residual, y, nullptr, N, H, W, C, pad, pad_mode == VST_PAD_REFLECT, 0, rk_cp_ld(P), act,
+                     slope, wx, reinterpret_cast<__bf16*>(planes));
+  return check_launch("instnorm_act_fwd_planes");
 }
 
 extern "C" int vst_instnorm_act_bwd(const float* gy, const float* x, const float* stats, float* dx,

@@ -378,6 +378,36 @@ __global__ void tap_wgrad_scatter_h_k(const float* __restrict__ t, float* __rest
   dw[i] = accumulate ? dw[i] + v : v;
 }
 
+// The swapped weight-gradient form (vst_tap_wgrad_swap): the first cx (3 or 4) channels of dy (NHWC4) as
+// the zero-padded channel-major fp32 image [cx][ld] of an Hp x Wp frame (pad rows / columns before, the
+// rest after), the "x" side of the GEMM.  grid (ceil(N Hp Wp / 256)), one thread per frame pixel
+// (coalesced along each channel row).
+__global__ __launch_bounds__(256) void tap_swap_dy_cp_k(const float4* __restrict__ g, float* __restrict__ xt, int H,
+                                                        int W, int pad, int Hp, int Wp, long P, long ld, int cx) {
+  const long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= P) return;
+  const int wp = q % Wp;
+  const long t = q / Wp;
+  const int h = (int)(t % Hp) - pad, w = wp - pad;
+  const long n = t / Hp;
+  const float4 a = ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W) ? g[(n * H + h) * (long)W + w]
+                                                                            : make_float4(0.f, 0.f, 0.f, 0.f);
+  xt[q] = a.x;
+  xt[ld + q] = a.y;
+  xt[2 * ld + q] = a.z;
+  if (cx == 4) xt[3 * ld + q] = a.w;
+}
+
+// dw[co][ci][tap] (+)= t[co][ci][RS-1-tap]: the swapped GEMM's taps run rotated by 180 degrees
+__global__ void tap_wgrad_scatter_flip_k(const float* __restrict__ t, float* __restrict__ dw, int RS, int accumulate,
+                                         long total) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int tap = i % RS;
+  const float v = t[i - tap + (RS - 1 - tap)];
+  dw[i] = accumulate ? dw[i] + v : v;
+}
+
 __global__ void tap_wgrad_scatter_k(const float* __restrict__ t, float* __restrict__ dw, int Co, int Ci, int RS,
                                     int accumulate, long total) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -488,6 +518,59 @@ extern "C" int vst_tap_wgrad_scatter_h(const float* t, float* dw, int Co, int Ci
   hipLaunchKernelGGL(tap_wgrad_scatter_h_k, dim3(ceil_div(total, 256)), dim3(256), 0, (hipStream_t)stream, t, dw, Ci,
                      R, S, accumulate, total);
   return check_launch("tap_wgrad_scatter_h");
+}
+
+// The swapped form's geometry: frame Hf x (Wf + wx) with wx zero columns so rows are whole 8-pixel chunks.
+static void tap_swap_geom(int N, int H, int W, int R, int* Hf, int* Wq, int* wx) {
+  *Hf = H + R - 1;
+  *wx = (8 - (W + R - 1) % 8) % 8;
+  *Wq = W + R - 1 + *wx;
+}
+
+extern "C" long vst_tap_wgrad_swap_ld(int N, int H, int W, int R) {
+  int Hf, Wq, wx;
+  tap_swap_geom(N, H, W, R, &Hf, &Wq, &wx);
+  return rk_cp_ld((long)N * Hf * Wq);
+}
+
+extern "C" size_t vst_tap_wgrad_swap_ws_bytes(int N, int H, int W, int Ci, int R) {
+  int Hf, Wq, wx;
+  tap_swap_geom(N, H, W, R, &Hf, &Wq, &wx);
+  const int pad = R - 1;
+  const long ldx = rk_cp_ld((long)N * (H + 2 * pad) * (W + wx + 2 * pad));
+  const size_t wg = vst_conv2d_wgrad_ws_bytes(N, H, W + wx, 4, Hf, Wq, Ci, R, R, 1);
+  return (size_t)(4 * ldx + 4 * (long)Ci * R * R) * sizeof(float) + wg;
+}
+
+extern "C" int vst_tap_wgrad_swap(const float* g, const void* x_planes, float* dw, float* ws, size_t ws_bytes, int N,
+                                  int H, int W, int Ci, int R, int Co, int accumulate, int math, void* stream) {
+  VST_REQUIRE(g && x_planes && dw && ws && N > 0 && H > 0 && W > 0 && Co > 0 && Co <= 4 && R % 2 == 1 &&
+                  Ci % 4 == 0 && (R - 1) / 2 < H && (R - 1) / 2 < W,
+              "tap_wgrad_swap: bad args");
+  VST_REQUIRE(ws_bytes >= vst_tap_wgrad_swap_ws_bytes(N, H, W, Ci, R), "tap_wgrad_swap: workspace too small");
+  int Hf, Wq, wx;
+  tap_swap_geom(N, H, W, R, &Hf, &Wq, &wx);
+  const int pad = R - 1, Hp = H + 2 * pad, Wp = W + wx + 2 * pad;
+  const long Pp = (long)N * Hp * Wp, ldx = rk_cp_ld(Pp);
+  hipStream_t s = (hipStream_t)stream;
+  float* xt = ws;
+  float* t = xt + 4 * ldx;
+  float* wsg = t + 4 * (long)Ci * R * R;
+  // Co <= 3: only three dy channels become GEMM rows (M = 3 R^2: 147 rows = 3 tiles of 64 at R = 7, not 4)
+  const int cx = Co <= 3 ? 3 : 4;
+  hipLaunchKernelGGL(tap_swap_dy_cp_k, dim3(ceil_div(Pp, 256)), dim3(256), 0, s, reinterpret_cast<const float4*>(g),
+                     xt, H, W, pad, Hp, Wp, Pp, ldx, cx);
+  int rc = check_launch("tap_wgrad_swap");
+  if (rc) return rc;
+  // t[c][ci][tap'] = sum_q dyP[q + tap'][c] * xf[q][ci]  (the frame's "output" channels ci: so = R*R, si = Ci*R*R)
+  const size_t wsb = ws_bytes - (size_t)(wsg - ws) * sizeof(float);
+  rc = vst_conv2d_wgrad_pre(g, xt, g, x_planes, t, wsg, wsb, N, H, W + wx, cx, Hf, Wq, Ci, R, R, 1, pad, VST_PAD_ZERO,
+                            Ci, cx, (long)R * R, (long)Ci * R * R, 0, math, stream);
+  if (rc) return rc;
+  const long total = (long)Co * Ci * R * R;
+  hipLaunchKernelGGL(tap_wgrad_scatter_flip_k, dim3(ceil_div(total, 256)), dim3(256), 0, s, t, dw, R * R, accumulate,
+                     total);
+  return check_launch("tap_wgrad_swap");
 }
 
 extern "C" int vst_tap_wgrad_scatter(const float* t, float* dw, int Co, int Ci, int R, int S, int accumulate,

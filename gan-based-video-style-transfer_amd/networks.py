@@ -358,7 +358,8 @@ TAP_LAST = os.environ.get("VST_TAP_CONV", "1") != "0"
 TAP_H = os.environ.get("VST_TAP_H", "1") != "0"
 # the image-input first layer's data gradient the same way (ops.tap_conv_dgrad_h); VST_TAP_HD=0: tap gather.
 TAP_HD = os.environ.get("VST_TAP_HD", "1") != "0"
-# ... and the last layer's weight gradient as the 7x1 conv's (ops.tap_conv_wgrad_h); VST_TAP_HW=0: tap fold.
+# ... and the last layer's weight gradient as the swapped GEMM (ops.tap_conv_wgrad_swap, VST_TAP_SWAP) or the
+# 7x1 conv's (ops.tap_conv_wgrad_h); VST_TAP_HW=0: tap fold.
 TAP_HW = os.environ.get("VST_TAP_HW", "1") != "0"
 # The up-sampling ConvTranspose2d (k3 s2 p1 op1) forward as four sub-pixel phase convs on the
 # split-bf16 forward kernel + an interleave (ops.convT3s2_fwd); VST_CONVT_PHASES=0 disables.
@@ -555,6 +556,8 @@ class _GeneratorFn(torch.autograd.Function):
         def in_act(y, s, act, cp, residual=None):
             if cp is None:
                 return ops.instnorm_act_fwd(y, s, act, residual=residual), None
+            if cp[0] == "planes":
+                return ops.instnorm_act_fwd(y, s, act, residual=residual, xpl=cp[1])
             return ops.instnorm_act_fwd(y, s, act, residual=residual, cp=cp)
 
         def conv_in_relu(inp, key, cout, R, st, pad, mode, nxt=None):
@@ -615,10 +618,13 @@ class _GeneratorFn(torch.autograd.Function):
             if i == 1 and "ftap" in P:
                 # the last layer's weight gradient: the 7x1 conv's (x padded by 4, reflect) or the tap fold's
                 # (1x1, pad 0); decided here so the x image below matches the route the backward takes
-                sv["ftap_h"] = TAP_HW and ops.tap_conv_wgrad_h_ok(y, 7, 3, "reflect")
+                sv["ftap_sw"] = ops.tap_conv_wgrad_swap_ok(y, 7, 3, "reflect")
+                sv["ftap_h"] = not sv["ftap_sw"] and TAP_HW and ops.tap_conv_wgrad_h_ok(y, 7, 3, "reflect")
             if i == 1 and "ftap" in P and train_w and IN_XT:
                 N_, H_, W_, C_ = y.shape
-                if sv["ftap_h"]:
+                if sv["ftap_sw"]:
+                    cp = ("planes", (3, "reflect", ops.tap_swap_geom(W_, 7)[0]))
+                elif sv["ftap_h"]:
                     cp = (4, "reflect", 1)
                 elif _wgrad_on_bf(N_, H_, W_, C_, H_, W_, 4 * 49, 1, 1, ops.get_conv_math()):
                     cp = (0, "zero", 1)
@@ -691,7 +697,10 @@ class _GeneratorFn(torch.autograd.Function):
         g = ops.act_bwd(gout, out, "tanh")
         if "ftap" in P:
             if train_w:
-                if sv.get("ftap_h"):
+                if sv.get("ftap_sw"):
+                    ops.tap_conv_wgrad_swap(a, g, f.weight.grad, 7, 3, "reflect", accumulate=True,
+                                            x_pl=xts.get(id(a)))
+                elif sv.get("ftap_h"):
                     ops.tap_conv_wgrad_h(a, g, f.weight.grad, 7, 3, "reflect", accumulate=True, x_t=xts.get(id(a)))
                 else:
                     ops.tap_conv_wgrad(a, g, f.weight.grad, 7, 3, "reflect", accumulate=True, x_t=xts.get(id(a)))

@@ -592,13 +592,22 @@ def instnorm_stats(y):
     return stats
 
 
-def instnorm_act_fwd(y, stats, act="relu", slope=0.0, residual=None, cp=None):
+def instnorm_act_fwd(y, stats, act="relu", slope=0.0, residual=None, cp=None, xpl=None):
     """a = act(IN(y)) (+ residual).  cp = (pad, pad_mode, stride) of the conv that consumes a:
     returns (a, a_t) where a_t is a's padded channel-major image for that conv's x6 weight gradient
-    (vst_instnorm_act_fwd_cp; conv2d_wgrad(x_t=a_t))."""
+    (vst_instnorm_act_fwd_cp; conv2d_wgrad(x_t=a_t)).  xpl = (pad, pad_mode, wx): returns (a, planes),
+    a's padded image as the bf16 planes [3][C][ld] with wx zero columns per row
+    (vst_instnorm_act_fwd_planes; tap_conv_wgrad_swap(x_pl=planes))."""
     _dev_check(y, stats, residual)
     N, H, W, C = y.shape
     a = torch.empty_like(y)
+    if xpl is not None:
+        pad, mode, wx = xpl
+        ld = lib().vst_cp_ld(N * (H + 2 * pad) * (W + 2 * pad + wx))
+        pl = torch.empty((3, C, ld), device=y.device, dtype=torch.bfloat16)
+        _call("vst_instnorm_act_fwd_planes", _p(y), _p(stats), _p(residual), _p(a), _p(pl), N, H, W, C, ACT[act],
+              float(slope), pad, PAD[mode], wx, _stream())
+        return a, pl
     if cp is not None:
         pad, mode, st = cp
         at = torch.empty((C, lib().vst_cp_ld(N * (H + 2 * pad) * (W + 2 * pad))), device=y.device)
@@ -1105,6 +1114,9 @@ TAP_CHUNK_BYTES = int(float(os.environ.get("VST_TAP_CHUNK_MB", "0")) * (1 << 20)
 # tap_conv_wgrad: the folded dy written as the x6 wgrad's bf16 planes (vst_tapfold_planes);
 # VST_TAP_PLANES=0 writes the fp32 D and lets the wgrad copy it into planes.
 TAP_PLANES = os.environ.get("VST_TAP_PLANES", "1") != "0"
+# The generator's last-layer weight gradient as the swapped GEMM (tap_conv_wgrad_swap); VST_TAP_SWAP=0:
+# the R x 1 form (tap_conv_wgrad_h).
+TAP_SWAP = os.environ.get("VST_TAP_SWAP", "1") != "0"
 
 
 def _tap_chunks(N, per_image_bytes):
@@ -1200,6 +1212,47 @@ def tap_conv_wgrad_h(x, dy, dw, R, pad, pad_mode="reflect", accumulate=True, rol
     _call("vst_conv2d_wgrad_pre", _p(x), _p(x_t), _p(pl), _p(pl), _p(t), _p(ws), nbytes, N, H, W, Cx, Ho, Wo, K, R, 1,
           1, pad + 1, PAD["reflect"], K, Ci, Ci * R, R, 0, _math(role), _stream())
     _call("vst_tap_wgrad_scatter_h", _p(t), _p(dw), Co, Ci, R, R, 1 if accumulate else 0, _stream())
+
+
+def tap_swap_geom(W, R):
+    """(wx, frame width) of tap_conv_wgrad_swap: the (W+R-1)-wide reflect-padded x rows get wx zero
+    columns so that every row is whole 8-pixel chunks."""
+    wx = (8 - (W + R - 1) % 8) % 8
+    return wx, W + R - 1 + wx
+
+
+def tap_conv_wgrad_swap_ok(x, R, pad, pad_mode, role="bwd"):
+    """Does tap_conv_wgrad_swap take this shape: a reflect 'same' conv whose swapped GEMM (the R x R wgrad
+    of the 4-channel dy against x's padded frame as Ci outputs) runs on the x6 split-bf16 kernel."""
+    N, H, W, Cx = x.shape
+    wx, Wq = tap_swap_geom(W, R)
+    return (TAP_SWAP and pad_mode == "reflect" and 2 * pad == R - 1 and pad < min(H, W) and Cx % 4 == 0 and
+            conv_plan_wgrad(N, H, W + wx, 4, H + R - 1, Wq, Cx, R, R, 1, role)[0] == 2)
+
+
+def tap_conv_wgrad_swap(x, dy, dw, R, pad, pad_mode="reflect", accumulate=True, role="bwd", x_pl=None):
+    """tap_conv_wgrad with the GEMM's roles swapped (vst_tap_wgrad_swap): M = R*R*3 (tap, co) rows of the
+    zero-padded dy against x's reflect-padded frame as Cx columns.  x_pl: that frame's bf16 planes as the
+    IN apply writes them (instnorm_act_fwd(xpl=(pad, "reflect", wx))); None: made here from x."""
+    _dev_check(x, dy, dw)
+    N, H, W, Cx = x.shape
+    Co, Ci = dw.shape[0], dw.shape[1]
+    if pad_mode != "reflect" or 2 * pad != R - 1:
+        raise NotImplementedError("tap_conv_wgrad_swap: reflect 'same' convs only")
+    if tuple(dy.shape) != (N, H, W, 4) or Co > 4 or Ci != Cx:
+        raise ValueError("tap_conv_wgrad_swap: dy %s / dw %s do not match x %s" % (tuple(dy.shape), tuple(dw.shape),
+                                                                               tuple(x.shape)))
+    if x_pl is None:  # the identity IN (mean 0, rstd 1): a == x, plus the planes
+        st = torch.zeros((N, Cx, 2), device=x.device)
+        st[..., 1] = 1.0
+        _, x_pl = instnorm_act_fwd(x, st, "none", xpl=(pad, "reflect", tap_swap_geom(W, R)[0]))
+    ld = lib().vst_tap_wgrad_swap_ld(N, H, W, R)
+    if x_pl.shape != (3, Cx, ld) or x_pl.dtype != torch.bfloat16:
+        raise ValueError("tap_conv_wgrad_swap: x planes %s do not match (3, %d, %d) bf16" % (tuple(x_pl.shape), Cx, ld))
+    nbytes = lib().vst_tap_wgrad_swap_ws_bytes(N, H, W, Cx, R)
+    ws = torch.empty((nbytes + 3) // 4, device=x.device)
+    _call("vst_tap_wgrad_swap", _p(dy), _p(x_pl), _p(dw), _p(ws), nbytes, N, H, W, Cx, R, Co,
+          1 if accumulate else 0, _math(role), _stream())
 
 
 def tap_conv_dgrad(dy, kc, R, pad, pad_mode="zero", role="bwd"):

@@ -214,7 +214,8 @@ int vst_conv2d_dgrad_refl(const float* dy, const void* wsplit, const float* adde
  * padded channel-major image of x that vst_instnorm_act_fwd_cp writes (same pad / mode / stride);
  * dy_planes (or NULL) = the three bf16 planes [3][Cyp][vst_cp_ld(N*Ho*Wo)] of dy that
  * vst_instnorm_act_bwd_planes writes.  Used only when vst_conv_plan_wgrad reports VST_WPLAN_BF (the
- * x6 split-bf16 kernel); on other paths both are ignored and x / dy are read as in vst_conv2d_wgrad. */
+ * x6 split-bf16 kernel); on other paths both are ignored and x / dy are read as in vst_conv2d_wgrad.
+ * With x_t on that path Cx need not be a multiple of 4 (x itself is not read). */
 int vst_conv2d_wgrad_pre(const float* x, const float* x_t, const float* dy, const void* dy_planes, float* dw,
                          float* ws, size_t ws_bytes, int N, int H, int W, int Cx, int Ho, int Wo, int Cyp, int R,
                          int S, int stride, int pad, int pad_mode, int Co, int Ci, long so, long si, int accumulate,
@@ -225,6 +226,13 @@ int vst_conv2d_wgrad_pre(const float* x, const float* x_t, const float* dy, cons
 int vst_instnorm_act_fwd_cp(const float* x, const float* stats, const float* residual, float* y, float* x_t,
                             int N, int H, int W, int C, int act, float slope, int pad, int pad_mode, int stride,
                             void* stream);
+/* vst_instnorm_act_fwd that also writes the padded image of its output as three bf16 planes
+ * [3][C][vst_cp_ld(N (H+2 pad) (W+2 pad+wx))] (the RNE hi / mid / lo split), each padded row followed
+ * by wx zero columns: the B operand of vst_tap_wgrad_swap (pad = (R-1)/2, wx from
+ * vst_tap_wgrad_swap_ld's geometry). */
+int vst_instnorm_act_fwd_planes(const float* x, const float* stats, const float* residual, float* y, void* planes,
+                                int N, int H, int W, int C, int act, float slope, int pad, int pad_mode, int wx,
+                                void* stream);
 /* Plane stride (elements) of the channel-major operand images over P pixels. */
 long vst_cp_ld(long P);
 /* Debug/benchmark only: force the GEMM tile of fprop / tconv / wgrad (-1 = automatic) for calls
@@ -483,6 +491,19 @@ int vst_tapconv_h_fwd(const float* x, const float* wp, const void* wsplit, const
  * 4RS. */
 int vst_tapshift_planes(const float* g, void* planes, long ldp, int N, int H, int W, int S, void* stream);
 int vst_tap_wgrad_scatter_h(const float* t, float* dw, int Co, int Ci, int R, int S, int accumulate, void* stream);
+/* The same weight gradient with the GEMM's roles swapped (replaces the R x 1 form in the train step):
+ * dw[co][ci][r][s] = sum_q xf[q][ci] * dyP[q + (R-1-r, R-1-s)][co] over the (H+R-1) x (W+R-1+wx) frame q
+ * of x reflect-padded by (R-1)/2 (x_planes: its bf16 planes as vst_instnorm_act_fwd_planes writes them,
+ * wx = (8 - (W+R-1) % 8) % 8 zero columns) and dy zero-padded by R-1 (made here in ws).  M = R*R*3
+ * (tap, co) rows (R*R*4 when Co == 4) instead of the R x 1 form's 4R (column tap, co) x R*Ci (the
+ * 3-channel x image: vst_conv2d_wgrad_pre takes any Cx with a caller-made x_t): no tap-shifted dy planes,
+ * and the x operand is read once per 64 rows of (tap, co) instead of once per row tap.  Then
+ * dw (+)= the result with its taps rotated 180 degrees.  ws: vst_tap_wgrad_swap_ws_bytes. */
+int vst_tap_wgrad_swap(const float* g, const void* x_planes, float* dw, float* ws, size_t ws_bytes, int N, int H,
+                       int W, int Ci, int R, int Co, int accumulate, int math, void* stream);
+size_t vst_tap_wgrad_swap_ws_bytes(int N, int H, int W, int Ci, int R);
+/* Plane stride of x_planes: vst_cp_ld(N (H+R-1) (W+R-1+wx)). */
+long vst_tap_wgrad_swap_ld(int N, int H, int W, int R);
 /* Adjoint gather of the weight gradient: d[q][(r*S+s)*4 + co] = sum_{p: src(p,r,s) = q} g[p][co]
  * (g NHWC4); then vst_conv2d_wgrad(x, d) as a 1x1 wgrad gives t[(r*S+s)*4 + co][ci], and
  * vst_tap_wgrad_scatter writes dw[co][ci][r][s] (+)= t (co < Co <= 4). */

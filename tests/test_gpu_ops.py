@@ -375,6 +375,58 @@ def test_tap_conv_wgrad_h(ops, N, ci, H, W, k, xt):
         ops.set_conv_math(prev)
 
 
+@pytest.mark.parametrize("N,ci,H,W,k,xpl,co", [(2, 64, 12, 56, 7, False, 3), (2, 64, 12, 56, 7, True, 3),
+                                              (3, 32, 9, 60, 3, True, 3), (2, 16, 10, 50, 7, True, 3),
+                                              (1, 64, 40, 17, 5, True, 3), (2, 32, 12, 56, 7, True, 4),
+                                              (1, 8, 11, 13, 7, True, 2), (2, 64, 256, 256, 7, True, 3)])
+def test_tap_conv_wgrad_swap(ops, N, ci, H, W, k, xpl, co):
+    """Weight gradient of a reflect 'same' conv with <= 4 outputs as the swapped GEMM (vst_tap_wgrad_swap: the
+    k x k wgrad of the zero-padded dy against x's reflect-padded frame), x6, against torch autograd and the
+    k x 1 form; x's frame planes made by the IN apply (vst_instnorm_act_fwd_planes) or inside the op."""
+    prev = ops.set_conv_math("bf16x6")
+    try:
+        pad = (k - 1) // 2
+        x = _g(111, (N, ci, H, W))
+        w = (_g(112, (co, ci, k, k), 0.05)).requires_grad_(True)
+        y = F.conv2d(F.pad(x, (pad,) * 4, mode="reflect"), w)
+        gy = _g(113, tuple(y.shape))
+        y.backward(gy)
+        xn, g = _nhwc(x, ops), _nhwc(gy, ops)
+        assert ops.tap_conv_wgrad_swap_ok(xn, k, pad, "reflect")
+        x_pl = None
+        if xpl:  # the IN apply's planes of x itself (identity stats)
+            st = torch.zeros((N, ci, 2), device=DEV)
+            st[..., 1] = 1.0
+            a, x_pl = ops.instnorm_act_fwd(xn, st, "none", xpl=(pad, "reflect", ops.tap_swap_geom(W, k)[0]))
+            assert torch.equal(a, xn)
+        dw = torch.full((co, ci, k, k), 0.25, device=DEV)
+        ops.tap_conv_wgrad_swap(xn, g, dw, k, pad, "reflect", accumulate=True, x_pl=x_pl)
+        _close(dw.cpu() - 0.25, w.grad, tol=CONV_TOL["bf16x6"], what="tap wgrad (swapped form)")
+        if co == 3 and ops.tap_conv_wgrad_h_ok(xn, k, pad, "reflect"):
+            dwh = torch.zeros((co, ci, k, k), device=DEV)
+            ops.tap_conv_wgrad_h(xn, g, dwh, k, pad, "reflect", accumulate=False)
+            _close(dw.cpu() - 0.25, dwh.cpu(), tol=CONV_TOL["bf16x6"], what="vs k x 1 form")
+    finally:
+        ops.set_conv_math(prev)
+
+
+@pytest.mark.parametrize("N,C,H,W,pad,wx,act", [(2, 64, 12, 20, 3, 2, "relu"), (1, 8, 9, 7, 1, 5, "none")])
+def test_instnorm_act_fwd_planes(ops, N, C, H, W, pad, wx, act):
+    """vst_instnorm_act_fwd_planes: a as vst_instnorm_act_fwd gives it, and the three bf16 planes of its
+    reflect-padded frame (wx zero columns per row) sum to that frame exactly (hi = RNE bf16 of it)."""
+    y = _g(121, (N, H, W, C)).to(DEV)
+    st = torch.stack([_g(122, (N, C)) * 0.1, _g(123, (N, C)).abs() + 0.5], -1).to(DEV)
+    a0 = ops.instnorm_act_fwd(y, st, act)
+    a, pl = ops.instnorm_act_fwd(y, st, act, xpl=(pad, "reflect", wx))
+    assert torch.equal(a, a0)
+    fr = F.pad(a0.permute(0, 3, 1, 2), (pad,) * 4, mode="reflect")
+    fr = F.pad(fr, (0, wx)).permute(1, 0, 2, 3).reshape(C, -1).cpu()
+    P = fr.shape[1]
+    p = pl[:, :, :P].float().cpu()
+    assert torch.equal(p[0], fr.to(torch.bfloat16).float())
+    assert torch.allclose(p[0] + p[1] + p[2], fr, rtol=2.0 ** -22, atol=0)
+
+
 def test_tap_conv_fwd_h_production(ops, conv_math):
     """The generator's last layer (64 -> 3, 7x7 reflect, tanh) at 256x256 through vst_tapconv_h_fwd vs torch
     fp32 and vs the 1x1-conv + full tap-sum route; the SOK pack built by a PackBatch equals the direct one."""

@@ -63,7 +63,7 @@ def fl_tap(a, k):
 
 OPS = {"conv2d_fwd": fl_fwd, "conv2d_fwd_in": fl_fwd, "conv2d_wgrad": fl_wgrad, "conv2d_dgrad_s1": fl_dgrad_s1,
        "convT3s2_fwd": fl_convT, "conv4s2_dgrad": fl_c4s2, "tap_conv_fwd_h": fl_tap, "tap_conv_dgrad_h": fl_tap,
-       "tap_conv_wgrad_h": fl_tap}
+       "tap_conv_wgrad_h": fl_tap, "tap_conv_wgrad_swap": fl_tap, "c4_dgrad_reflect": fl_tap}
 rec, depth = {}, [0]
 
 

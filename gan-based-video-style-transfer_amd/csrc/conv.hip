@@ -1097,6 +1097,28 @@ extern "C" int vst_conv2d_tfwd(const float* in, const float* wp, const float* bi
 // Two-level split-K reduction (slab_group_sum_k first) when the fused reduce + store kernel would
 // run on few blocks with a long serial slab chain per element.
 static constexpr int WG_GROUP = 16;
+// Image-input layers (x NHWC4 holding 3 logical channels) on the split-bf16 kernel: the GEMM takes only
+// the rows (tap, ci < 3) of the 4-plane x image — M = 3RS instead of 4RS (the generator's first 7x7
+// conv: 147 rows = 3 tiles of 64 instead of 4).  VST_WG_C3=0: all four planes.
+static const bool g_wg_c3 = [] {
+  const char* e = getenv("VST_WG_C3");
+  return !(e && e[0] == '0');
+}();
+
+// The GEMM's plan for (Cx, logical Ci): p planned with Cx = 3 when the rule above applies; its
+// operand-copy sizes stay those of the Cx-channel images.
+static WgradPlan plan_wgrad_gemm(const WgradPlan& p, int N, int H, int W, int Ho, int Wo, int Cx, int Ci, int Cyp,
+                                 int R, int S, int stride, int math, int* Cxg) {
+  *Cxg = Cx;
+  if (!(g_wg_c3 && p.bfk && Cx == 4 && Ci == 3)) return p;
+  WgradPlan q = plan_wgrad(N, H, W, Ho, Wo, 3, Cyp, R, S, stride, math);
+  if (!q.bfk || q.wpad != p.wpad || q.pad != p.pad) return p;
+  q.xt_floats = p.xt_floats;
+  q.dyt_floats = p.dyt_floats;
+  *Cxg = 3;
+  return q;
+}
+
 static bool wgrad_two_level(const WgradPlan& p, int Cyp, int Ci, int RS, int Co) {
   return p.nsplit > 2 * WG_GROUP && (long)ceil_div(Ci * RS, 64) * ceil_div(Co, 64) < 128;
 }
@@ -1125,8 +1147,12 @@ extern "C" size_t vst_conv2d_wgrad_ws_bytes(int N, int H, int W, int Cx, int Ho,
   // the plan (split count, tile) depends on the arithmetic: size for the largest
   size_t mx = 0;
   for (int math = VST_MATH_F32; math <= VST_MATH_BF16X6; ++math) {
-    const size_t b = wgrad_ws_floats(plan_wgrad(N, H, W, Ho, Wo, Cx, Cyp, R, S, stride, math), Cyp) * sizeof(float);
+    const WgradPlan p = plan_wgrad(N, H, W, Ho, Wo, Cx, Cyp, R, S, stride, math);
+    int cxg;
+    const WgradPlan pg = plan_wgrad_gemm(p, N, H, W, Ho, Wo, Cx, 3, Cyp, R, S, stride, math, &cxg);
+    const size_t b = wgrad_ws_floats(p, Cyp) * sizeof(float), bg = wgrad_ws_floats(pg, Cyp) * sizeof(float);
     mx = b > mx ? b : mx;
+    mx = bg > mx ? bg : mx;
   }
   return mx;
 }
@@ -1152,12 +1178,14 @@ extern "C" int vst_conv2d_wgrad_pre(const float* x, const float* x_t, const floa
                                     long si, int accumulate, int math, void* stream) {
   VST_REQUIRE(x && dy && dw && ws, "conv2d_wgrad: null pointer");
   VST_REQUIRE(math >= VST_MATH_F32 && math <= VST_MATH_BF16X6, "conv2d_wgrad: bad math %d", math);
-  const WgradPlan p = plan_wgrad(N, H, W, Ho, Wo, Cx, Cyp, R, S, stride, math);
+  const WgradPlan p0 = plan_wgrad(N, H, W, Ho, Wo, Cx, Cyp, R, S, stride, math);
   // any Cx when the split-bf16 kernel reads a caller-made channel-major x image (no NHWC vector loads of x)
-  VST_REQUIRE((Cx % 4 == 0 || (x_t && p.bfk && !p.wpad)) && Cyp % 4 == 0,
+  VST_REQUIRE((Cx % 4 == 0 || (x_t && p0.bfk && !p0.wpad)) && Cyp % 4 == 0,
               "conv2d_wgrad: channel strides must be multiples of 4");
   VST_REQUIRE(Co <= Cyp && Ci <= Cx, "conv2d_wgrad: logical channels exceed strides");
   VST_REQUIRE(pad_mode == VST_PAD_ZERO || (pad < H && pad < W), "conv2d_wgrad: reflect pad >= size");
+  int Cxg;  // the GEMM's channel count (3 for image-input layers, g_wg_c3)
+  const WgradPlan p = plan_wgrad_gemm(p0, N, H, W, Ho, Wo, Cx, Ci, Cyp, R, S, stride, math, &Cxg);
   VST_REQUIRE(ws_bytes >= wgrad_ws_floats(p, Cyp) * sizeof(float),
               "conv2d_wgrad: workspace too small (%zu bytes)", ws_bytes);
   hipStream_t s = (hipStream_t)stream;
@@ -1184,7 +1212,7 @@ extern "C" int vst_conv2d_wgrad_pre(const float* x, const float* x_t, const floa
       if (!x_t) rk_nhwc_to_cp_pad(x, xt, N, H, W, Cx, pad, refl, stride == 2, 0, s, p.wpad);  // else: vst_instnorm_act_fwd_cp
       if (!dy_planes)  // else: made by vst_instnorm_act_bwd_planes
         bf_nhwc_to_planes(dy, dyt, (long)N * Ho * Wo8, Cyp, 3, s, p.wpad ? Wo : 0, p.wpad ? Wo8 : 0);
-      bf_wgrad_launch(x_t ? x_t : xt, dy_planes ? dy_planes : dyt, ws, N, H, W + p.wpad, Cx, Ho, Wo8, Cyp, S, pad,
+      bf_wgrad_launch(x_t ? x_t : xt, dy_planes ? dy_planes : dyt, ws, N, H, W + p.wpad, Cxg, Ho, Wo8, Cyp, S, pad,
                       stride, p.Mw, p.chunk, p.nsplit, (int)p.tile, math, s);
     } else {
       const int pack = math == VST_MATH_BF16X3;  // the x3 kernel stages pre-split (hi, lo) words
@@ -1217,10 +1245,10 @@ extern "C" int vst_conv2d_wgrad_pre(const float* x, const float* x_t, const floa
   }
   if (g_wg_red16)  // 16-row blocks: twice the blocks (the 2304 x 256 ResnetBlock gradient: 288 -> 576)
     hipLaunchKernelGGL(wgrad_reduce_store_k<1>, dim3(ceil_div(Ci * R * S, 16), ceil_div(Co, 64)), dim3(256), 0, s,
-                       red, dw, Cx, Cyp, R * S, Co, Ci, so, si, accumulate, nred, slab);
+                       red, dw, Cxg, Cyp, R * S, Co, Ci, so, si, accumulate, nred, slab);
   else
     hipLaunchKernelGGL(wgrad_reduce_store_k<2>, dim3(ceil_div(Ci * R * S, 32), ceil_div(Co, 64)), dim3(256), 0, s,
-                       red, dw, Cx, Cyp, R * S, Co, Ci, so, si, accumulate, nred, slab);
+                       red, dw, Cxg, Cyp, R * S, Co, Ci, so, si, accumulate, nred, slab);
   return check_launch("conv2d_wgrad_reduce");
 }
 

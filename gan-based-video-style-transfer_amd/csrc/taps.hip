@@ -538,7 +538,9 @@ extern "C" size_t vst_tap_wgrad_swap_ws_bytes(int N, int H, int W, int Ci, int R
   tap_swap_geom(N, H, W, R, &Hf, &Wq, &wx);
   const int pad = R - 1;
   const long ldx = rk_cp_ld((long)N * (H + 2 * pad) * (W + wx + 2 * pad));
-  const size_t wg = vst_conv2d_wgrad_ws_bytes(N, H, W + wx, 4, Hf, Wq, Ci, R, R, 1);
+  // the GEMM runs over 3 or 4 dy channels (Co <= 3 or not, see vst_tap_wgrad_swap): size for either plan
+  const size_t wg = std::max(vst_conv2d_wgrad_ws_bytes(N, H, W + wx, 4, Hf, Wq, Ci, R, R, 1),
+                             vst_conv2d_wgrad_ws_bytes(N, H, W + wx, 3, Hf, Wq, Ci, R, R, 1));
   return (size_t)(4 * ldx + 4 * (long)Ci * R * R) * sizeof(float) + wg;
 }
 

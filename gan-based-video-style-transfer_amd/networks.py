@@ -263,12 +263,13 @@ class FlatNet(nn.Module):
 
     def graphed_forward(self, x):
         """No-grad forward replayed from a HIP graph captured once per (shape, device, conv policy,
-        pack set): the ~100 kernel launches of a generator forward (forward_eval,
+        pack set, route switches — ops.route_flags(), so flipping e.g. ops.CONVT_DIRECT in-process
+        captures a new graph instead of replaying the old route): the ~100 kernel launches of a generator forward (forward_eval,
         CycleGAN/models/cycle_gan_model.py:164-171) become one graph launch, so small batches are
         not bound by host launch latency.  The packs are refreshed in place before each replay
         (weight updates keep the captured buffers valid).  Returns a fresh output tensor."""
         P = self.packs()
-        key = (tuple(x.shape), x.device, ops.get_conv_math(), id(P))
+        key = (tuple(x.shape), x.device, ops.get_conv_math(), id(P), ops.route_flags())
         cache = self._graphs
         ent = cache.get(key)
         if ent is None:
@@ -618,7 +619,7 @@ class _GeneratorFn(torch.autograd.Function):
             if i == 1 and "ftap" in P:
                 # the last layer's weight gradient: the 7x1 conv's (x padded by 4, reflect) or the tap fold's
                 # (1x1, pad 0); decided here so the x image below matches the route the backward takes
-                sv["ftap_sw"] = ops.tap_conv_wgrad_swap_ok(y, 7, 3, "reflect")
+                sv["ftap_sw"] = ops.tap_conv_wgrad_swap_ok(y, 7, 3, "reflect", co=self.output_nc)
                 sv["ftap_h"] = not sv["ftap_sw"] and TAP_HW and ops.tap_conv_wgrad_h_ok(y, 7, 3, "reflect")
             if i == 1 and "ftap" in P and train_w and IN_XT:
                 N_, H_, W_, C_ = y.shape

@@ -1221,13 +1221,16 @@ def tap_swap_geom(W, R):
     return wx, W + R - 1 + wx
 
 
-def tap_conv_wgrad_swap_ok(x, R, pad, pad_mode, role="bwd"):
+def tap_conv_wgrad_swap_ok(x, R, pad, pad_mode, role="bwd", co=4):
     """Does tap_conv_wgrad_swap take this shape: a reflect 'same' conv whose swapped GEMM (the R x R wgrad
-    of the 4-channel dy against x's padded frame as Ci outputs) runs on the x6 split-bf16 kernel."""
+    of the dy channels against x's padded frame as Ci outputs) runs on the x6 split-bf16 kernel.  co: the
+    layer's real output channels — vst_tap_wgrad_swap runs the GEMM over 3 dy channels when co <= 3, 4
+    otherwise, and the plan is queried with that same count."""
     N, H, W, Cx = x.shape
     wx, Wq = tap_swap_geom(W, R)
+    cx = 3 if co <= 3 else 4
     return (TAP_SWAP and pad_mode == "reflect" and 2 * pad == R - 1 and pad < min(H, W) and Cx % 4 == 0 and
-            conv_plan_wgrad(N, H, W + wx, 4, H + R - 1, Wq, Cx, R, R, 1, role)[0] == 2)
+            conv_plan_wgrad(N, H, W + wx, cx, H + R - 1, Wq, Cx, R, R, 1, role)[0] == 2)
 
 
 def tap_conv_wgrad_swap(x, dy, dw, R, pad, pad_mode="reflect", accumulate=True, role="bwd", x_pl=None):
@@ -1389,3 +1392,14 @@ def convT3s2_fwd(x, packs, bias, cop, act="none", role="fwd"):
     _call("vst_interleave_phases", _p(outs[0]), _p(outs[1]), _p(outs[2]), _p(outs[3]), _p(y), N, H, W, cop,
           _stream())
     return y
+
+
+_ROUTE_FLAGS = ("FWD_SPLITK", "NRM_FWD", "DGRAD_BORDER", "C4_DGRAD", "TAP_CHUNK_BYTES", "TAP_PLANES", "TAP_SWAP",
+                "C4S2_GROUPED", "CONVT_DIRECT", "CONVT_GROUPED")
+
+
+def route_flags():
+    """The module-level route switches that change which kernels a forward launches (tests and tools
+    flip them in-process): part of FlatNet.graphed_forward's capture key."""
+    g = globals()
+    return tuple(g[n] for n in _ROUTE_FLAGS)

@@ -83,18 +83,27 @@ class _VGG(FlatNet):
             self.to(device)
 
     def load_torchvision_features(self, sd):
-        """Load a torchvision ``vgg16/vgg19().features`` state dict ('N.weight' or 'features.N.weight')."""
+        """Load a torchvision ``vgg16/vgg19().features`` state dict ('N.weight', 'features.N.weight' or
+        either under a DataParallel 'module.' prefix).  Every conv weight and bias of the sliced net
+        must be present: a dict that maps none or only some of them (another architecture, a
+        classifier-only dict) raises instead of leaving the seeded weights in place."""
         own = {}
         for k, (a, b) in enumerate(self.slices_idx):
             for x in range(a, b):
                 own[str(x)] = "slice%d.%d" % (k + 1, x)
         mapped = {}
         for key, v in sd.items():
-            key = key[len("features."):] if key.startswith("features.") else key
+            for pre in ("module.", "features."):
+                key = key[len(pre):] if key.startswith(pre) else key
             idx, _, name = key.partition(".")
-            if idx in own:
+            if idx in own and name in ("weight", "bias"):
                 mapped[own[idx] + "." + name] = v
-        self.load_state_dict(mapped, strict=False)
+        expected = [n for n, _ in self.named_parameters()]
+        missing = [n for n in expected if n not in mapped]
+        if missing:
+            raise KeyError("VGG state dict lacks %d of %d conv tensors (first: %s)" % (len(missing), len(expected),
+                                                                                      missing[0]))
+        self.load_state_dict(mapped, strict=True)
         self.bump_version()
 
     def _make_packs(self):

@@ -127,3 +127,29 @@ def test_c3_loss_weight_defaults_follow_vgg_source():
     o = resolve_loss_weights(parse_options(["--model", "cycle_gan_vgg", "--vgg_weights", "v.pth",
                                             "--lambda_style", "3"], True))
     assert (o.lambda_content, o.lambda_style) == (1.0, 3.0)
+
+
+def test_vgg_torchvision_load_is_complete_or_raises():
+    """load_torchvision_features maps 'N.*', 'features.N.*' and 'module.features.N.*' keys and
+    raises when any conv tensor of the sliced net is missing (a partial or foreign dict must not leave
+    the seeded weights under the pretrained loss weights)."""
+    import pytest
+    import torch
+    from gbvst import perceptual
+    net = perceptual.Vgg19(seed=3)
+    src = perceptual.Vgg19(seed=4)
+    sd = {}
+    for x, kind, _, _, m in src.layers:
+        if kind == "conv":
+            sd["module.features.%d.weight" % x] = m.weight.detach().clone()
+            sd["module.features.%d.bias" % x] = m.bias.detach().clone() + 0.5
+    sd["classifier.0.weight"] = torch.zeros(2, 2)
+    net.load_torchvision_features(sd)
+    for (x, kind, _, _, m), (_, _, _, _, ms) in zip(net.layers, src.layers):
+        if kind == "conv":
+            assert torch.equal(m.weight, ms.weight) and torch.equal(m.bias, ms.bias + 0.5)
+    part = {k: v for k, v in sd.items() if not k.endswith(".bias")}
+    with pytest.raises(KeyError):
+        perceptual.Vgg19(seed=3).load_torchvision_features(part)
+    with pytest.raises(KeyError):
+        perceptual.Vgg19(seed=3).load_torchvision_features({"classifier.0.weight": torch.zeros(2, 2)})

@@ -61,7 +61,14 @@ def fl_tap(a, k):
     return 2.0 * N * H * W * 64 * 3 * 49, "7x7 64<->3 tap route @%dx%d N=%d" % (H, W, N)
 
 
-OPS = {"conv2d_fwd": fl_fwd, "conv2d_fwd_in": fl_fwd, "conv2d_wgrad": fl_wgrad, "conv2d_dgrad_s1": fl_dgrad_s1,
+def fl_tfwd(a, k):
+    dy, Ho, Wo, cx, R, S, st = a[0], a[3], a[4], a[5], a[6], a[7], a[8]
+    N, Hi, Wi, Cy = dy.shape
+    cy = 1 if Cy == 4 and cx == 512 else real(Cy)  # the PatchGAN head's data gradient: 1 real channel
+    return 2.0 * N * Hi * Wi * cy * real(cx) * R * S, "tdgrad %dx%d s%d %d->%d out %dx%d N=%d" % (R, S, st, cy, real(cx), Ho, Wo, N)
+
+
+OPS = {"conv2d_fwd": fl_fwd, "conv2d_tfwd": fl_tfwd, "conv2d_fwd_in": fl_fwd, "conv2d_wgrad": fl_wgrad, "conv2d_dgrad_s1": fl_dgrad_s1,
        "convT3s2_fwd": fl_convT, "conv4s2_dgrad": fl_c4s2, "tap_conv_fwd_h": fl_tap, "tap_conv_dgrad_h": fl_tap,
        "tap_conv_wgrad_h": fl_tap, "tap_conv_wgrad_swap": fl_tap, "c4_dgrad_reflect": fl_tap}
 rec, depth = {}, [0]

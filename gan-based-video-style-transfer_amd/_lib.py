@@ -64,6 +64,8 @@ SIGNATURES = {
     "vst_conv2d_fwd_in": (I, [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, I, P, P, P]),
     "vst_instnorm_finalize": (I, [P, P, I, I, I, I, F, P]),
     "vst_conv2d_tfwd": (I, [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, F, I, P]),
+    "vst_conv2d_tfwd_co": (I, [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, F, I, I, P]),
+    "vst_conv2d_wgrad_bias": (I, [P, P, P, P, P, SZ, I, I, I, I, I, I, I, I, I, I, I, I, I, I, L, L, I, I, P]),
     "vst_conv2d_wgrad_ws_bytes": (SZ, [I, I, I, I, I, I, I, I, I, I]),
     "vst_conv2d_wgrad": (I, [P, P, P, P, SZ, I, I, I, I, I, I, I, I, I, I, I, I, I, I, L, L, I, I, P]),
     "vst_debug_set_tiles": (None, [I, I, I]),

@@ -192,6 +192,25 @@ void rk_tconv_launch(const float* in, const float* wp, const float* bias, const 
                      float* out, int N, int Hi, int Wi, int Cy, int Ho, int Wo, int Cx, int R, int S,
                      int st, int pad, int reflect, int act, float slope, int kind, int math,
                      hipStream_t s);
+// VST_HEAD=0 turns the head kernels below off (skinny.hip)
+extern const bool g_head;
+// the PatchGAN head (one real output channel, stride 1, zero pad, <= 4x4 taps): patch.hip
+bool head_ok(int Cin, int R, int S, int st, int reflect, int Wo);
+int head_fwd_launch(const float* x, const float* wp, const float* bias, float* out, int N, int Hi, int Wi, int Cin,
+                    int Ho, int Wo, int R, int S, int pad, int act, float slope, hipStream_t s);
+size_t head_wgrad_ws_floats(int N, int Hi, int Cin, int R, int S);
+int head_wgrad_launch(const float* x, const float* dy, float* dw, float* ws, int N, int Hi, int Wi, int Cin, int Ci,
+                      int Ho, int Wo, int R, int S, int pad, long si, int accumulate, hipStream_t s,
+                      float* db = nullptr);
+extern const bool g_img_wgrad;
+// image-input (4-channel x, <= 3 real) weight gradient with the bias gradient folded in (patch.hip)
+bool img_wgrad_ok(int Cx, int Cyp, int R, int S, int st, int reflect, int Ci, int Wo);
+size_t img_wgrad_ws_floats(int N, int Ho, int Wo);
+int img_wgrad_launch(const float* x, const float* dy, float* dw, float* db, float* ws, int N, int H, int W, int Ho,
+                     int Wo, int Cyp, int R, int S, int st, int pad, int Co, int Ci, long so, long si, int accumulate,
+                     hipStream_t s);
+int head_dgrad_launch(const float* dy, const float* wp, const float* addend, float* dx, int N, int Hd, int Wd, int Cx,
+                      int H, int W, int R, int S, int pad, hipStream_t s);
 int skinny_wgrad_launch(const float* x, const float* dy, float* slab, int H, int W, int Cx, int Ho,
                         int Wo, int S, int st, int pad, int reflect, int Mw, int P, int chunk,
                         int nsplit, hipStream_t s);

@@ -1094,6 +1094,19 @@ extern "C" int vst_conv2d_tfwd(const float* in, const float* wp, const float* bi
   return check_launch("conv2d_tfwd");
 }
 
+extern "C" int vst_conv2d_tfwd_co(const float* in, const float* wp, const float* bias, const float* addend, float* out,
+                                  int N, int Hi, int Wi, int Cy, int Ho, int Wo, int Cx, int R, int S, int stride,
+                                  int pad, int pad_mode, int act, float slope, int math, int co_real, void* stream) {
+  VST_REQUIRE(co_real >= 1 && co_real <= Cy, "conv2d_tfwd_co: bad real channel count %d", co_real);
+  const int refl = pad_mode == VST_PAD_REFLECT;
+  if (in && wp && out && co_real == 1 && Cy == 4 && !bias && act == VST_ACT_NONE && g_head && N > 0 && Hi > 0 &&
+      Wi > 0 && pad >= 0 && head_ok(Cx, R, S, stride, refl, Wi) && Ho == Hi + R - 1 - 2 * pad &&
+      Wo == Wi + S - 1 - 2 * pad)
+    return head_dgrad_launch(in, wp, addend, out, N, Hi, Wi, Cx, Ho, Wo, R, S, pad, (hipStream_t)stream);
+  return vst_conv2d_tfwd(in, wp, bias, addend, out, N, Hi, Wi, Cy, Ho, Wo, Cx, R, S, stride, pad, pad_mode, act, slope,
+                         math, stream);
+}
+
 // Two-level split-K reduction (slab_group_sum_k first) when the fused reduce + store kernel would
 // run on few blocks with a long serial slab chain per element.
 static constexpr int WG_GROUP = 16;
@@ -1154,6 +1167,14 @@ extern "C" size_t vst_conv2d_wgrad_ws_bytes(int N, int H, int W, int Cx, int Ho,
     mx = b > mx ? b : mx;
     mx = bg > mx ? bg : mx;
   }
+  if (Cyp == 4 && stride == 1) {  // a one-channel head may take patch.hip's row kernel
+    const size_t hb = head_wgrad_ws_floats(N, H, Cx, R, S) * sizeof(float);
+    mx = hb > mx ? hb : mx;
+  }
+  if (Cx == 4) {  // an image-input layer may take patch.hip's fp32-MFMA kernel
+    const size_t ib = img_wgrad_ws_floats(N, Ho, Wo) * sizeof(float);
+    mx = ib > mx ? ib : mx;
+  }
   return mx;
 }
 
@@ -1184,6 +1205,10 @@ extern "C" int vst_conv2d_wgrad_pre(const float* x, const float* x_t, const floa
               "conv2d_wgrad: channel strides must be multiples of 4");
   VST_REQUIRE(Co <= Cyp && Ci <= Cx, "conv2d_wgrad: logical channels exceed strides");
   VST_REQUIRE(pad_mode == VST_PAD_ZERO || (pad < H && pad < W), "conv2d_wgrad: reflect pad >= size");
+  if (!x_t && !dy_planes && g_img_wgrad && img_wgrad_ok(Cx, Cyp, R, S, stride, pad_mode == VST_PAD_REFLECT, Ci, Wo) &&
+      Co <= Cyp && ws_bytes >= img_wgrad_ws_floats(N, Ho, Wo) * sizeof(float))
+    return img_wgrad_launch(x, dy, dw, nullptr, ws, N, H, W, Ho, Wo, Cyp, R, S, stride, pad, Co, Ci, so, si, accumulate,
+                            (hipStream_t)stream);
   int Cxg;  // the GEMM's channel count (3 for image-input layers, g_wg_c3)
   const WgradPlan p = plan_wgrad_gemm(p0, N, H, W, Ho, Wo, Cx, Ci, Cyp, R, S, stride, math, &Cxg);
   VST_REQUIRE(ws_bytes >= wgrad_ws_floats(p, Cyp) * sizeof(float),
@@ -1221,6 +1246,10 @@ extern "C" int vst_conv2d_wgrad_pre(const float* x, const float* x_t, const floa
       rk_wgrad_launch(xt, dyt, ws, N, H, W, Cx, Ho, Wo, Cyp, S, pad, stride, p.Mw, p.chunk, p.nsplit,
                       (int)p.tile, math, s);
     }
+  } else if (Cyp == 4 && Co == 1 && g_head && head_ok(Cx, R, S, stride, refl, Wo) &&
+             ws_bytes >= head_wgrad_ws_floats(N, H, Cx, R, S) * sizeof(float)) {
+    // the PatchGAN head: the activation read once, partials reduced in a fixed order straight into dw
+    return head_wgrad_launch(x, dy, dw, ws, N, H, W, Cx, Ci, Ho, Wo, R, S, pad, si, accumulate, s);
   } else if (Cyp == 4) {
     int rc0 = skinny_wgrad_launch(x, dy, ws, H, W, Cx, Ho, Wo, S, stride, pad, refl, p.Mw, P, p.chunk,
                                   p.nsplit, s);
@@ -1250,6 +1279,26 @@ extern "C" int vst_conv2d_wgrad_pre(const float* x, const float* x_t, const floa
     hipLaunchKernelGGL(wgrad_reduce_store_k<2>, dim3(ceil_div(Ci * R * S, 32), ceil_div(Co, 64)), dim3(256), 0, s,
                        red, dw, Cxg, Cyp, R * S, Co, Ci, so, si, accumulate, nred, slab);
   return check_launch("conv2d_wgrad_reduce");
+}
+
+extern "C" int vst_conv2d_wgrad_bias(const float* x, const float* dy, float* dw, float* db, float* ws, size_t ws_bytes,
+                                     int N, int H, int W, int Cx, int Ho, int Wo, int Cyp, int R, int S, int stride,
+                                     int pad, int pad_mode, int Co, int Ci, long so, long si, int accumulate, int math,
+                                     void* stream) {
+  (void)math;
+  VST_REQUIRE(x && dy && dw && db && ws && N > 0 && H > 0 && W > 0 && Ho > 0 && Wo > 0 && R > 0 && S > 0 &&
+                  stride > 0 && pad >= 0 && Co >= 1 && Co <= Cyp && Ci >= 1 && Ci <= Cx,
+              "conv2d_wgrad_bias: bad args");
+  const int refl = pad_mode == VST_PAD_REFLECT;
+  hipStream_t s = (hipStream_t)stream;
+  if (g_img_wgrad && img_wgrad_ok(Cx, Cyp, R, S, stride, refl, Ci, Wo) &&
+      ws_bytes >= img_wgrad_ws_floats(N, Ho, Wo) * sizeof(float))
+    return img_wgrad_launch(x, dy, dw, db, ws, N, H, W, Ho, Wo, Cyp, R, S, stride, pad, Co, Ci, so, si, accumulate, s);
+  if (Cyp == 4 && Co == 1 && g_head && head_ok(Cx, R, S, stride, refl, Wo) &&
+      ws_bytes >= head_wgrad_ws_floats(N, H, Cx, R, S) * sizeof(float))
+    return head_wgrad_launch(x, dy, dw, ws, N, H, W, Cx, Ci, Ho, Wo, R, S, pad, si, accumulate, s, db);
+  ::vst::set_error("conv2d_wgrad_bias: no fused route for this shape (use vst_conv2d_wgrad + vst_channel_sum)");
+  return VST_EUNSUPPORTED;
 }
 
 extern "C" int vst_reflect_fold(const float* dxp, const float* addend, float* dx, int N, int H,

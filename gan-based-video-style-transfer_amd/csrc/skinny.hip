@@ -208,6 +208,12 @@ __global__ __launch_bounds__(256) void skinny_wgrad_k(
     *reinterpret_cast<float4*>(sl + 4 * a) = make_float4(acc[a][0], acc[a][1], acc[a][2], acc[a][3]);
 }
 
+// the PatchGAN head's one-channel forward on its row kernel (patch.hip); VST_HEAD=0: the per-pixel gather here
+const bool g_head = [] {
+  const char* e = getenv("VST_HEAD");
+  return !(e && e[0] == '0');
+}();
+
 int skinny_out_launch(int mode, const float* in, const float* wp, const float* bias,
                       const float* addend, float* out, int N, int Hi, int Wi, int Cin, int Ho,
                       int Wo, int R, int S, int st, int pad, int reflect, int act, float slope,
@@ -230,6 +236,8 @@ int skinny_out_launch(int mode, const float* in, const float* wp, const float* b
     case 8: VST_SK(M_, ST_, 8); break;          \
     default: VST_SK(M_, ST_, 16); break;        \
   }
+  if (mode == 0 && co_real == 1 && g_head && head_ok(Cin, R, S, st, reflect, Wo) && !addend)
+    return head_fwd_launch(in, wp, bias, out, N, Hi, Wi, Cin, Ho, Wo, R, S, pad, act, slope, s);
   if (mode == 0 && co_real == 1) {
 #define VST_SK1(KS_)                                                                                  \
   hipLaunchKernelGGL((skinny_out_k<0, 0, KS_, true>), dim3(ceil_div(pix * KS_, 256), 1, classes), dim3(256), 0, s, \

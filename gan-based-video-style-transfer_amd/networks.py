@@ -511,6 +511,10 @@ DGRAD_IN = os.environ.get("VST_DGRAD_IN", "0") == "1"
 # The discriminator head (1 real output channel of 4) runs the one-channel skinny forward
 # (ops.conv2d_fwd(co_real=1)); VST_D_CO1=0 keeps the 4-channel sums.
 D_CO1 = os.environ.get("VST_D_CO1", "1") != "0"
+# The first PatchGAN layer's data gradient (onto the 4-channel image) as ONE parity-class gather launch
+# (ops.conv2d_tfwd -> skinny.hip MODE 1) instead of four 2x2 phase convs + the interleave pass;
+# VST_D0_TFWD=0 keeps the phases.
+D0_TFWD = os.environ.get("VST_D0_TFWD", "1") != "0"
 _WPLAN_BF = 2  # ops.WPLAN_NAMES: copies + conv_wgrad_bf_k
 
 
@@ -619,7 +623,7 @@ class _GeneratorFn(torch.autograd.Function):
             if i == 1 and "ftap" in P:
                 # the last layer's weight gradient: the 7x1 conv's (x padded by 4, reflect) or the tap fold's
                 # (1x1, pad 0); decided here so the x image below matches the route the backward takes
-                sv["ftap_sw"] = ops.tap_conv_wgrad_swap_ok(y, 7, 3, "reflect", co=self.output_nc)
+                sv["ftap_sw"] = ops.tap_conv_wgrad_swap_ok(y, 7, 3, "reflect", co=net.output_nc)
                 sv["ftap_h"] = not sv["ftap_sw"] and TAP_HW and ops.tap_conv_wgrad_h_ok(y, 7, 3, "reflect")
             if i == 1 and "ftap" in P and train_w and IN_XT:
                 N_, H_, W_, C_ = y.shape
@@ -925,12 +929,13 @@ class _DiscriminatorFn(torch.autograd.Function):
                 ikf, ph = net._ikf[i], net._ph[i]
                 if ikf is not None:
                     g = ops.conv2d_dgrad_s1(dy, ikf, a_in.shape[1], a_in.shape[2], a_in.shape[-1], 4, 1)
-                elif ph is not None and a_in.shape[1] == 2 * dy.shape[1] and a_in.shape[2] == 2 * dy.shape[2]:
+                elif ph is not None and a_in.shape[1] == 2 * dy.shape[1] and a_in.shape[2] == 2 * dy.shape[2] and \
+                        not (D0_TFWD and a_in.shape[-1] == 4):
                     g = ops.conv4s2_dgrad(dy, ph, a_in.shape[-1])
                 else:
                     _, ck, _ = P[i]
                     g = ops.conv2d_tfwd(dy, ck, None, a_in.shape[1], a_in.shape[2], a_in.shape[-1], 4, 4,
-                                        st, 1)
+                                        st, 1, co_real=cout if (D_CO1 and cout < dy.shape[-1]) else None)
                 if i == 0:
                     gx = g
         ctx.saved = None

@@ -15,6 +15,7 @@ PAD = {"zero": 0, "reflect": 1}
 PACK_KC, PACK_CK, PACK_OK, PACK_IK, PACK_IKF, PACK_SOK = 0, 1, 2, 3, 4, 5
 # the conv kernels consume: forward conv -> PACK_OK, data-gradient / transposed conv -> PACK_IK
 PACK_FWD, PACK_DGRAD = PACK_OK, PACK_IK
+EUNSUPPORTED = 2  # VST_EUNSUPPORTED (include/vst_hip.h)
 IN_EPS = 1e-5
 
 
@@ -302,12 +303,17 @@ def conv2d_fwd_in_nrm(y_in, stats_in, wp, bias, cop, R, pad, pad_mode="reflect",
 
 
 def conv2d_tfwd(x, wp, bias, Ho, Wo, cx, R, S, stride, pad, act="none", slope=0.0,
-                pad_mode="zero", addend=None, role="bwd"):
+                pad_mode="zero", addend=None, role="bwd", co_real=None):
     """Transposed conv / data gradient (vst_conv2d_tfwd).  pad_mode='reflect' (stride 1) is the
-    exact gradient of ReflectionPad2d(pad)+conv; addend is added in the epilogue."""
+    exact gradient of ReflectionPad2d(pad)+conv; addend is added in the epilogue.  co_real: the real
+    channels of x when Cy pads them (vst_conv2d_tfwd_co: the PatchGAN head's data gradient)."""
     _dev_check(x, wp, bias, addend)
     N, Hi, Wi, Cy = x.shape
     y = torch.empty((N, Ho, Wo, cx), device=x.device)
+    if co_real is not None and co_real < Cy:
+        _call("vst_conv2d_tfwd_co", _p(x), _p(wp), _p(bias), _p(addend), _p(y), N, Hi, Wi, Cy, Ho, Wo, cx,
+              R, S, stride, pad, PAD[pad_mode], ACT[act], float(slope), _math(role), int(co_real), _stream())
+        return y
     _call("vst_conv2d_tfwd", _p(x), _p(wp), _p(bias), _p(addend), _p(y), N, Hi, Wi, Cy, Ho, Wo, cx,
           R, S, stride, pad, PAD[pad_mode], ACT[act], float(slope), _math(role), _stream())
     return y
@@ -325,6 +331,16 @@ def conv2d_wgrad(x, dy, dw, db, R, S, stride, pad, pad_mode, co, ci, so, si, acc
     nbytes = lib().vst_conv2d_wgrad_ws_bytes(N, H, W, Cx, Ho, Wo, Cyp, R, S, stride)
     ws = torch.empty((nbytes + 3) // 4, device=x.device)
     h = _probe_begin("wgrad", (N, H, W, Cx, Cyp, R, stride, pad, pad_mode)) if _probes else None
+    if db is not None and dy_planes is None and x_t is None:
+        # the weight and bias gradient in one fused pass where a route takes the shape (vst_conv2d_wgrad_bias)
+        rc = lib().vst_conv2d_wgrad_bias(_p(x), _p(dy), _p(dw), _p(db), _p(ws), nbytes, N, H, W, Cx, Ho, Wo, Cyp, R, S,
+                                         stride, pad, PAD[pad_mode], co, ci, so, si, 1 if accumulate else 0,
+                                         _math(role), _stream())
+        if rc == 0:
+            _probe_end(h)
+            return
+        if rc != EUNSUPPORTED:
+            _lib.check(rc, "vst_conv2d_wgrad_bias")
     _call("vst_conv2d_wgrad_pre", _p(x), _p(x_t), _p(dy), _p(dy_planes), _p(dw), _p(ws), nbytes, N, H, W, Cx, Ho, Wo,
           Cyp, R, S, stride, pad, PAD[pad_mode], co, ci, so, si, 1 if accumulate else 0, _math(role),
           _stream())

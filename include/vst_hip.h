@@ -185,6 +185,13 @@ int vst_conv2d_tfwd(const float* in, const float* wp, const float* bias, const f
                     float* out, int N, int Hi, int Wi, int Cy, int Ho, int Wo, int Cx, int R,
                     int S, int stride, int pad, int pad_mode, int act, float slope, int math,
                     void* stream);
+/* vst_conv2d_tfwd when only the first co_real of the Cy dy channels are real (the rest and their weight
+ * rows zero): with co_real = 1, Cy = 4, stride 1, zero padding, R, S <= 4, no bias / activation — the
+ * data gradient of the PatchGAN head Conv2d(8*ndf, 1, 4, 1, 1) (networks.py:578) — a row kernel writes
+ * dx once (patch.hip); any other shape runs vst_conv2d_tfwd. */
+int vst_conv2d_tfwd_co(const float* in, const float* wp, const float* bias, const float* addend, float* out, int N,
+                       int Hi, int Wi, int Cy, int Ho, int Wo, int Cx, int R, int S, int stride, int pad, int pad_mode,
+                       int act, float slope, int math, int co_real, void* stream);
 /* Weight gradient of y = conv(x, w):  dw[co][ci][r][s] (+)= sum_pix x_gather * dy (bias gradient:
  * vst_channel_sum of dy).  x: [N][H][W][Cx], dy: [N][Ho][Wo][Cyp].  dw is written
  * with strides (so, si) for (co, ci) and r*S+s contiguous, for co < Co, ci < Ci (logical); pass
@@ -200,6 +207,16 @@ int vst_conv2d_wgrad(const float* x, const float* dy, float* dw, float* ws, size
                      int H, int W, int Cx, int Ho, int Wo, int Cyp, int R, int S, int stride,
                      int pad, int pad_mode, int Co, int Ci, long so, long si, int accumulate,
                      int math, void* stream);
+/* Weight AND bias gradient of y = conv(x, w) + b in one pass, for the shapes a fused route takes:
+ *   - image-input layers (Cx == 4 with Ci <= 3 real channels, R*S <= 16, zero padding, Cyp <= 64 even:
+ *     the PatchGAN first layer Conv2d(3, ndf, 4, 2, 1), networks.py:556) — fp32 MFMA over the fp32 dy
+ *     stream, db from a constant-1 operand column;
+ *   - the one-channel PatchGAN head (Cyp == 4, Co == 1, stride 1, zero pad, R, S <= 4, networks.py:578).
+ * Arguments as vst_conv2d_wgrad; db[co] (+)= sum_pix dy[pix][co] for co < Co.  Any other shape returns
+ * VST_EUNSUPPORTED without launching anything: use vst_conv2d_wgrad + vst_channel_sum. */
+int vst_conv2d_wgrad_bias(const float* x, const float* dy, float* dw, float* db, float* ws, size_t ws_bytes, int N,
+                          int H, int W, int Cx, int Ho, int Wo, int Cyp, int R, int S, int stride, int pad,
+                          int pad_mode, int Co, int Ci, long so, long si, int accumulate, int math, void* stream);
 /* Data gradient of ReflectionPad2d(1) + 3x3 conv, stride 1 (the ResnetBlock convs, networks.py:404-426):
  * dx[N][H][W][Cx] (+= addend, or NULL) from dy[N][H][W][Cy], wsplit = the bf16 planes of the
  * VST_PACK_IKF pack of the conv weight.  The interior term runs as the zero-pad-1 forward conv of dy

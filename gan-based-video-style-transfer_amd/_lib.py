@@ -84,6 +84,8 @@ SIGNATURES = {
     "vst_instnorm_act_fwd_planes": (I, [P, P, P, P, P, I, I, I, I, I, F, I, I, I, P]),
     "vst_cp_ld": (L, [L]),
     "vst_conv2d_fwd_co": (I, [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, I, I, P]),
+    "vst_conv2d_fwd_co_ws_bytes": (SZ, [I, I, I, I, I, I, I, I, I, I, I]),
+    "vst_conv2d_fwd_co_ws": (I, [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, I, I, P, SZ, P]),
     "vst_tapfold_planes": (I, [P, P, L, I, I, I, I, I, I, I, P]),
     "vst_conv2d_fwd_ws_bytes": (SZ, [I, I, I, I, I, I, I, I, I, I]),
     "vst_conv2d_fwd_ws": (I, [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, I, P, P, P, SZ, P]),

@@ -199,6 +199,11 @@ bool head_ok(int Cin, int R, int S, int st, int reflect, int Wo);
 int head_fwd_launch(const float* x, const float* wp, const float* bias, float* out, int N, int Hi, int Wi, int Cin,
                     int Ho, int Wo, int R, int S, int pad, int act, float slope, hipStream_t s);
 size_t head_wgrad_ws_floats(int N, int Hi, int Cin, int R, int S);
+// the forward as a per-row tap GEMM (z = N*Hi*Wi*16 floats of workspace) + a tap sum
+bool head_tap_ok(int Cin);
+size_t head_tap_ws_floats(int N, int Hi, int Wi);
+int head_tap_fwd_launch(const float* x, const float* wp, const float* bias, float* out, float* ws, int N, int Hi,
+                        int Wi, int Cin, int Ho, int Wo, int R, int S, int pad, int act, float slope, hipStream_t s);
 int head_wgrad_launch(const float* x, const float* dy, float* dw, float* ws, int N, int Hi, int Wi, int Cin, int Ci,
                       int Ho, int Wo, int R, int S, int pad, long si, int accumulate, hipStream_t s,
                       float* db = nullptr);

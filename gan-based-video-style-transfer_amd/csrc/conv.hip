@@ -931,6 +931,27 @@ extern "C" int vst_conv2d_fwd_co(const float* x, const float* wp, const void* ws
                        math, (hipStream_t)stream, nullptr, nullptr, nullptr, 0, co_real);
 }
 
+extern "C" size_t vst_conv2d_fwd_co_ws_bytes(int N, int H, int W, int Cx, int Cop, int R, int S, int stride, int pad,
+                                             int pad_mode, int co_real) {
+  if (N <= 0 || H <= 0 || W <= 0 || co_real != 1 || Cop != 4 || !g_head) return 0;
+  const int Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - S) / stride + 1;
+  if (Ho <= 0 || Wo <= 0 || !head_ok(Cx, R, S, stride, pad_mode == VST_PAD_REFLECT, Wo) || !head_tap_ok(Cx)) return 0;
+  return head_tap_ws_floats(N, H, W) * sizeof(float);
+}
+
+extern "C" int vst_conv2d_fwd_co_ws(const float* x, const float* wp, const void* wsplit, const float* bias, float* y,
+                                    int N, int H, int W, int Cx, int Cop, int R, int S, int stride, int pad,
+                                    int pad_mode, int act, float slope, int math, int co_real, float* ws,
+                                    size_t ws_bytes, void* stream) {
+  const size_t need = vst_conv2d_fwd_co_ws_bytes(N, H, W, Cx, Cop, R, S, stride, pad, pad_mode, co_real);
+  if (need && ws && ws_bytes >= need && x && wp && y) {
+    const int Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - S) / stride + 1;
+    return head_tap_fwd_launch(x, wp, bias, y, ws, N, H, W, Cx, Ho, Wo, R, S, pad, act, slope, (hipStream_t)stream);
+  }
+  return vst_conv2d_fwd_co(x, wp, wsplit, bias, y, N, H, W, Cx, Cop, R, S, stride, pad, pad_mode, act, slope, math,
+                           co_real, stream);
+}
+
 extern "C" int vst_conv2d_fwd_in(const float* x, const float* wp, const void* wsplit, const float* bias,
                                  float* y, int N, int H, int W, int Cx, int Cop, int R, int S, int stride,
                                  int pad, int pad_mode, int act, float slope, int math, double* part,

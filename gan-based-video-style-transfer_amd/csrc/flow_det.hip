@@ -43,6 +43,11 @@ __global__ void warp_det_emit_k(const float* __restrict__ flow, unsigned long lo
   }
 }
 
+// One key walk per run serves up to GC channels (the run's keys, flow and bilinear weights are read and
+// recomputed once per GC channels, not once per channel); each channel's sum is still added in the
+// run's key order, so the result is the same sequence of roundings as a channel-at-a-time walk.
+constexpr int GC = 8;
+
 __global__ void warp_det_gather_k(const unsigned long long* __restrict__ keys, long nkeys,
                                   const float* __restrict__ gout, const float* __restrict__ flow,
                                   float* __restrict__ gx, int N, int H, int W, int Cs, int Cl, int align,
@@ -54,8 +59,11 @@ __global__ void warp_det_gather_k(const unsigned long long* __restrict__ keys, l
   const unsigned long long t = key >> 32;
   if (i > 0 && (keys[i - 1] >> 32) == t) return;  // not the head of its target's run
   const long plane = (long)H * W;
-  for (int c = 0; c < Cl; ++c) {
-    float s = gx[(long)t * Cs + c];
+  for (int c0 = 0; c0 < Cl; c0 += GC) {
+    const int nc = Cl - c0 < GC ? Cl - c0 : GC;
+    float s[GC];
+#pragma unroll
+    for (int c = 0; c < GC; ++c) s[c] = c < nc ? gx[(long)t * Cs + c0 + c] : 0.f;
     for (long j = i; j < nkeys; ++j) {
       const unsigned long long kj = keys[j];
       if (kj == kSentinel || (kj >> 32) != t) break;
@@ -66,10 +74,16 @@ __global__ void warp_det_gather_k(const unsigned long long* __restrict__ keys, l
       const long fo = (long)n * 2 * plane + (long)h * W + w;
       const Bilin b = bilin(h, w, flow[fo], flow[fo + plane], H, W, align);
       const float wt = k == 0 ? b.nw : k == 1 ? b.ne : k == 2 ? b.sw : b.se;
-      const float v = wt * gout[p * Cs + c];
-      s = s + (negate ? -v : v);
+#pragma unroll
+      for (int c = 0; c < GC; ++c) {
+        if (c >= nc) break;
+        const float v = wt * gout[p * Cs + c0 + c];
+        s[c] = s[c] + (negate ? -v : v);
+      }
     }
-    gx[(long)t * Cs + c] = s;
+#pragma unroll
+    for (int c = 0; c < GC; ++c)
+      if (c < nc) gx[(long)t * Cs + c0 + c] = s[c];
   }
 }
 

@@ -30,75 +30,79 @@ namespace patch {
 
 constexpr int RMAX = 4, SMAX = 4;  // kernel taps per dimension (the head is 4 x 4)
 
+// Every kernel here issues its global loads in explicit batches before using them: on gfx950 a
+// vector load waited on right after issue costs a full memory latency (~1 us under load), and a wait
+// inside a loop that also stores drains the stores too (loads and stores share vmcnt).
+
 // ---- forward -------------------------------------------------------------------------------------
 // wp: the VST_PACK_OK pack [Cop][R][S][Cin]; only output channel 0 is computed (co_real = 1), the
-// padded channels get act(bias[c]) like the 4-channel path's zero sums.
+// padded channels get act(bias[c]) like the 4-channel path's zero sums.  1024 threads: wave w takes
+// input row h - pad + (w & 3) and channel quarter w >> 2; KS lanes per column split the quarter.
+constexpr int HF_THREADS = 1024, HF_NQ = 4, HF_B = 16;
+
 template <int KS>
-__global__ __launch_bounds__(256) void head_fwd_k(const float* __restrict__ x, const float* __restrict__ wp,
-                                                  const float* __restrict__ bias, float* __restrict__ out, int Hi,
-                                                  int Wi, int Cin, int Ho, int Wo, int R, int S, int pad, int act,
-                                                  float slope, int seg) {
+__global__ __launch_bounds__(HF_THREADS) void head_fwd_k(const float* __restrict__ x, const float* __restrict__ wp,
+                                                         const float* __restrict__ bias, float* __restrict__ out,
+                                                         int Hi, int Wi, int Cin, int Ho, int Wo, int R, int S,
+                                                         int pad, int act, float slope, int seg) {
   constexpr int NCOL = 64 / KS;
   extern __shared__ float lds[];
-  float* wl = lds;                        // [R][S][Cin]
-  float* z = lds + RMAX * SMAX * Cin;     // [RMAX][NCOL][SMAX]
-  const int t = threadIdx.x, lane = t & 63;
-  const int r = __builtin_amdgcn_readfirstlane(t >> 6);
+  float* wl = lds;                     // [R][S][Cin]
+  float* zq = lds + RMAX * SMAX * Cin;  // [HF_NQ][RMAX][NCOL][SMAX]
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int r = wave & 3, qq = wave >> 2;
   const int n = blockIdx.z, h = blockIdx.y, w0 = blockIdx.x * seg;
-  const long wn = (long)R * S * Cin;
-  for (long e = 4 * t; e < wn; e += 4 * 256)
+  const int wn = R * S * Cin;
+  for (int e = 4 * t; e < wn; e += 4 * HF_THREADS)
     *reinterpret_cast<float4*>(wl + e) = *reinterpret_cast<const float4*>(wp + e);
   __syncthreads();
   const int col = lane / KS, k = lane % KS;
   const int hi = h - pad + r, wi = w0 - pad + col;
   const int ncol = seg + S - 1;
+  const bool valid = r < R && (unsigned)hi < (unsigned)Hi && col < ncol && (unsigned)wi < (unsigned)Wi;
+  // channel slice (quarter qq, lane k): a contiguous run of cw channels
+  const int cw = Cin / (HF_NQ * KS), c0 = (qq * KS + k) * cw;
+  const float* src = x + (valid ? (((long)n * Hi + hi) * Wi + wi) * Cin : 0) + c0;
+  const float* wr = wl + r * S * Cin + c0;
   float acc[SMAX] = {0.f, 0.f, 0.f, 0.f};
-  if (r < R && (unsigned)hi < (unsigned)Hi && col < ncol && (unsigned)wi < (unsigned)Wi) {
-    // lane k of a column takes the channel range [k * Cin / KS, (k + 1) * Cin / KS): a contiguous stream
-    const int cw = Cin / KS, c0 = k * cw;
-    const float* src = x + (((long)n * Hi + hi) * Wi + wi) * Cin + c0;
-    const float* wr = wl + (long)r * S * Cin + c0;
-    if (S == 4) {
-#pragma unroll 4
-      for (int c = 0; c < cw; c += 4) {
-        const float4 v = *reinterpret_cast<const float4*>(src + c);
+  if (r < R) {
+    for (int cb = 0; cb < cw; cb += 4 * HF_B) {
+      float4 v[HF_B];
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          const float4 w = *reinterpret_cast<const float4*>(wr + s * Cin + c);
-          acc[s] = fmaf(v.x, w.x, acc[s]);
-          acc[s] = fmaf(v.y, w.y, acc[s]);
-          acc[s] = fmaf(v.z, w.z, acc[s]);
-          acc[s] = fmaf(v.w, w.w, acc[s]);
-        }
-      }
-    } else {
-      for (int c = 0; c < cw; c += 4) {
-        const float4 v = *reinterpret_cast<const float4*>(src + c);
+      for (int u = 0; u < HF_B; ++u)
+        if (cb + 4 * u < cw) v[u] = *reinterpret_cast<const float4*>(src + cb + 4 * u);
+#pragma unroll
+      for (int u = 0; u < HF_B; ++u) {
+        if (cb + 4 * u >= cw) break;
 #pragma unroll
         for (int s = 0; s < SMAX; ++s) {
           if (s >= S) break;
-          const float4 w = *reinterpret_cast<const float4*>(wr + s * Cin + c);
-          acc[s] = fmaf(v.x, w.x, acc[s]);
-          acc[s] = fmaf(v.y, w.y, acc[s]);
-          acc[s] = fmaf(v.z, w.z, acc[s]);
-          acc[s] = fmaf(v.w, w.w, acc[s]);
+          const float4 w = *reinterpret_cast<const float4*>(wr + s * Cin + cb + 4 * u);
+          acc[s] = fmaf(v[u].x, w.x, acc[s]);
+          acc[s] = fmaf(v[u].y, w.y, acc[s]);
+          acc[s] = fmaf(v[u].z, w.z, acc[s]);
+          acc[s] = fmaf(v[u].w, w.w, acc[s]);
         }
       }
     }
   }
 #pragma unroll
-  for (int s = 0; s < SMAX; ++s)
+  for (int s = 0; s < SMAX; ++s) {
+    acc[s] = valid ? acc[s] : 0.f;
 #pragma unroll
     for (int o = KS / 2; o > 0; o >>= 1) acc[s] += __shfl_xor(acc[s], o, 64);
-  if (k == 0 && r < RMAX) {
+  }
+  if (k == 0) {
 #pragma unroll
-    for (int s = 0; s < SMAX; ++s) z[(r * NCOL + col) * SMAX + s] = acc[s];
+    for (int s = 0; s < SMAX; ++s) zq[((qq * RMAX + r) * NCOL + col) * SMAX + s] = acc[s];
   }
   __syncthreads();
   if (t < seg && w0 + t < Wo) {
     float v = 0.f;
     for (int rr = 0; rr < R; ++rr)
-      for (int s = 0; s < S; ++s) v += z[(rr * NCOL + t + s) * SMAX + s];
+      for (int s = 0; s < S; ++s)
+#pragma unroll
+        for (int q4 = 0; q4 < HF_NQ; ++q4) v += zq[((q4 * RMAX + rr) * NCOL + t + s) * SMAX + s];
     const float4 b4 = bias ? *reinterpret_cast<const float4*>(bias) : make_float4(0.f, 0.f, 0.f, 0.f);
     float4 o;
     o.x = apply_act(v + b4.x, act, slope);
@@ -109,77 +113,189 @@ __global__ __launch_bounds__(256) void head_fwd_k(const float* __restrict__ x, c
   }
 }
 
-// ---- weight gradient -----------------------------------------------------------------------------
-// part[zb][(r*S + s)*Cin + c] = sum over the block's input rows i and columns j of
-// x[n][i][j][c] * dy[n][i+pad-r][j+pad-s][0]   (zero outside dy).  Thread: channel quad q = t % Q
-// (Q = Cin / 4), column group g = t / Q (NG = 256 / Q groups stride the row's columns).
-__global__ __launch_bounds__(256) void head_wgrad_k(const float* __restrict__ x, const float* __restrict__ dy,
-                                                    float* __restrict__ part, int Hi, int Wi, int Cin, int Ho,
-                                                    int Wo, int R, int S, int pad, int G) {
+// The forward as a tap GEMM over each input row, read ONCE (the row kernel above reads every input row
+// once per kernel row r, i.e. R times, and is bound by that traffic):
+//   head_tap_k     block = (input row i, image n): the row (JC columns at a time) and the channel-0
+//                  weights [R*S][Cin] are staged in LDS with every load issued up front, then
+//                  z[n][i][j][tap] = sum_c x[n][i][j][c] * w[tap][c] on v_mfma_f32_16x16x4_f32 (exact fp32
+//                  products): M = 16 columns per block, N = the 16 taps, K = Cin split over the waves.
+//                  A lane's ds_read_b128 of 4 consecutive channels feeds 4 MFMAs (channel c + 4(l>>4) + t
+//                  to MFMA t, for both operands: the reduction order within a 16-channel group is free).
+//   head_tapsum_k  out[n][h][w] = act(b + sum_{r,s} z[n][h-pad+r][w-pad+s][r*S+s]) in a fixed order.
+constexpr int HT_THREADS = 256, HT_JC = 32;
+
+__global__ __launch_bounds__(HT_THREADS) void head_tap_k(const float* __restrict__ x, const float* __restrict__ wp,
+                                                         float* __restrict__ z, int Hi, int Wi, int Cin, int RS) {
   extern __shared__ float lds[];
-  // dl[r][SMAX + ww]: dy row i + pad - r (channel 0), zero outside the image, so the tap loop has no
-  // bounds tests; then the cross-group partials [NG - 1][R*S][Cin]
-  const int DW = Wo + 2 * SMAX;
-  float* dl = lds;
-  float* xg = lds + RMAX * DW;
-  const int t = threadIdx.x, Q = Cin / 4, NG = 256 / Q;
-  const int q = t % Q, g = t / Q;
-  const int n = blockIdx.y, i0 = blockIdx.x * G;
-  float4 acc[RMAX * SMAX];
+  const int LD = Cin + 4;           // padded row stride (floats): the 16 rows of a read start 16 B apart
+  float* xs = lds;                  // [HT_JC][LD]
+  float* ws = lds + HT_JC * LD;     // [16][LD] (taps >= RS zero)
+  float* zs = ws + 16 * LD;         // [4][HT_JC][16] per-wave partial z
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int n = blockIdx.y, i = blockIdx.x;
+  const int Q = Cin / 4;
+  // weights: 16 x Cin floats (rows >= RS zero), loads issued together
+  {
+    float4 v[16];
 #pragma unroll
-  for (int e = 0; e < RMAX * SMAX; ++e) acc[e] = make_float4(0.f, 0.f, 0.f, 0.f);
-  const float* dyn = dy + (long)n * Ho * Wo * 4;
-  for (int i = i0; i < i0 + G && i < Hi; ++i) {
-    __syncthreads();
-    for (int e = t; e < RMAX * DW; e += 256) {
-      const int r = e / DW, ww = e - r * DW - SMAX, hh = i + pad - r;
-      dl[e] = (r < R && (unsigned)hh < (unsigned)Ho && (unsigned)ww < (unsigned)Wo) ? dyn[((long)hh * Wo + ww) * 4]
-                                                                                     : 0.f;
+    for (int u = 0; u < 16; ++u) {
+      const int e = t + u * HT_THREADS, tap = e / Q, c4 = e - tap * Q;
+      if (e < 16 * Q) v[u] = tap < RS ? *reinterpret_cast<const float4*>(wp + (long)tap * Cin + 4 * c4)
+                                      : make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    __syncthreads();
-    const float* xr = x + ((long)n * Hi + i) * Wi * Cin + 4 * q;
-    for (int j = g; j < Wi; j += NG) {
-      const float4 v = *reinterpret_cast<const float4*>(xr + (long)j * Cin);
-      const float* dj = dl + SMAX + j + pad;
 #pragma unroll
-      for (int r = 0; r < RMAX; ++r)
-#pragma unroll
-        for (int s = 0; s < SMAX; ++s) {
-          const float d = dj[r * DW - s];
-          float4& a = acc[r * SMAX + s];
-          a.x = fmaf(v.x, d, a.x);
-          a.y = fmaf(v.y, d, a.y);
-          a.z = fmaf(v.z, d, a.z);
-          a.w = fmaf(v.w, d, a.w);
-        }
+    for (int u = 0; u < 16; ++u) {
+      const int e = t + u * HT_THREADS, tap = e / Q, c4 = e - tap * Q;
+      if (e < 16 * Q) *reinterpret_cast<float4*>(ws + tap * LD + 4 * c4) = v[u];
     }
   }
-  const int RS = R * S;
-  if (g > 0) {
+  const float* xr = x + ((long)n * Hi + i) * Wi * Cin;
+  float* zr = z + ((long)n * Hi + i) * Wi * 16;
+  const int l16 = lane & 15, kq = lane >> 4;
+  for (int j0 = 0; j0 < Wi; j0 += HT_JC) {
+    const int jn = Wi - j0 < HT_JC ? Wi - j0 : HT_JC;
+    {
+      float4 v[16];
 #pragma unroll
-    for (int r = 0; r < RMAX; ++r)
-#pragma unroll
-      for (int s = 0; s < SMAX; ++s)
-        if (r < R && s < S)
-          *reinterpret_cast<float4*>(xg + ((long)(g - 1) * RS + r * S + s) * Cin + 4 * q) = acc[r * SMAX + s];
-  }
-  __syncthreads();
-  if (g == 0) {
-    float* dst = part + (long)(blockIdx.y * gridDim.x + blockIdx.x) * RS * Cin + 4 * q;
-#pragma unroll
-    for (int r = 0; r < RMAX; ++r)
-#pragma unroll
-      for (int s = 0; s < SMAX; ++s) {
-        if (r >= R || s >= S) continue;
-        float4 a = acc[r * SMAX + s];
-        for (int gg = 1; gg < NG; ++gg)
-          add_f4(a, *reinterpret_cast<const float4*>(xg + ((long)(gg - 1) * RS + r * S + s) * Cin + 4 * q));
-        *reinterpret_cast<float4*>(dst + (long)(r * S + s) * Cin) = a;
+      for (int u = 0; u < 16; ++u) {
+        const int e = t + u * HT_THREADS, j = e / Q, c4 = e - j * Q;
+        if (e < HT_JC * Q) v[u] = j < jn ? *reinterpret_cast<const float4*>(xr + (long)(j0 + j) * Cin + 4 * c4)
+                                         : make_float4(0.f, 0.f, 0.f, 0.f);
       }
+      __syncthreads();  // weights written / the previous chunk consumed
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int e = t + u * HT_THREADS, j = e / Q, c4 = e - j * Q;
+        if (e < HT_JC * Q) *reinterpret_cast<float4*>(xs + j * LD + 4 * c4) = v[u];
+      }
+      __syncthreads();
+    }
+    // wave w: column block mb = w & 1 (16 columns), channel half kh = w >> 1
+    const int mb = wave & 1, kh = wave >> 1, ch = Cin / 2;
+    const float* pa = xs + (mb * 16 + l16) * LD + kh * ch + 4 * kq;
+    const float* pb = ws + l16 * LD + kh * ch + 4 * kq;
+    f32x4v acc = {0.f, 0.f, 0.f, 0.f};
+    for (int c = 0; c < ch; c += 16) {
+      const float4 a = *reinterpret_cast<const float4*>(pa + c);
+      const float4 b = *reinterpret_cast<const float4*>(pb + c);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b.x, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b.y, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b.z, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b.w, acc, 0, 0, 0);
+    }
+    // C: column (tap) l & 15, rows (columns j) 4 (l >> 4) + reg
+#pragma unroll
+    for (int e = 0; e < 4; ++e) zs[(wave * HT_JC + mb * 16 + 4 * kq + e) * 16 + l16] = acc[e];
+    __syncthreads();
+    for (int e = t; e < jn * 16; e += HT_THREADS) {
+      const int j = e >> 4, tap = e & 15, m = j >> 4;
+      zr[(long)(j0 + j) * 16 + tap] = zs[(m * HT_JC + j) * 16 + tap] + zs[((2 + m) * HT_JC + j) * 16 + tap];
+    }
   }
 }
 
-// Fixed-order sum of the 256 threads' values v (the block's, in thread order of 16-groups) -> thread 0.
+__global__ __launch_bounds__(256) void head_tapsum_k(const float* __restrict__ z, const float* __restrict__ bias,
+                                                     float* __restrict__ out, int N, int Hi, int Wi, int Ho, int Wo,
+                                                     int R, int S, int pad, int act, float slope) {
+  const long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= (long)N * Ho * Wo) return;
+  const int w = (int)(p % Wo), h = (int)((p / Wo) % Ho), n = (int)(p / ((long)Wo * Ho));
+  float zv[RMAX * SMAX];
+#pragma unroll
+  for (int r = 0; r < RMAX; ++r)
+#pragma unroll
+    for (int s = 0; s < SMAX; ++s) {
+      const int hi = h - pad + r, wi = w - pad + s;
+      const bool ok = r < R && s < S && (unsigned)hi < (unsigned)Hi && (unsigned)wi < (unsigned)Wi;
+      zv[r * SMAX + s] = ok ? z[(((long)n * Hi + hi) * Wi + wi) * 16 + r * S + s] : 0.f;
+    }
+  float v = 0.f;
+#pragma unroll
+  for (int e = 0; e < RMAX * SMAX; ++e) v += zv[e];
+  const float4 b4 = bias ? *reinterpret_cast<const float4*>(bias) : make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 o;
+  o.x = apply_act(v + b4.x, act, slope);
+  o.y = apply_act(b4.y, act, slope);
+  o.z = apply_act(b4.z, act, slope);
+  o.w = apply_act(b4.w, act, slope);
+  *reinterpret_cast<float4*>(out + p * 4) = o;
+}
+
+// ---- weight gradient -----------------------------------------------------------------------------
+// part[zb][(r*S + s)*Cin + c] = sum over input row i (block zb = (n, i)) and its columns j of
+// x[n][i][j][c] * dy[n][i+pad-r][j+pad-s][0]   (zero outside dy).  1024 threads: channel quad q = t % Q
+// (Q = Cin / 4), kernel row r = (t / Q) % 4, column group g = t / (4Q) (NG = 256 / Q groups).  The row
+// is staged into LDS in chunks of JC columns (all of a thread's loads issued together), dy's rows
+// i + pad - r too (zero outside the image, so the tap loop has no bounds tests).
+constexpr int HW_THREADS = 1024;
+
+__global__ __launch_bounds__(HW_THREADS) void head_wgrad_k(const float* __restrict__ x, const float* __restrict__ dy,
+                                                           float* __restrict__ part, int Hi, int Wi, int Cin, int Ho,
+                                                           int Wo, int R, int S, int pad, int JC) {
+  extern __shared__ float lds[];
+  const int DW = Wo + 2 * SMAX;
+  const int Q = Cin / 4, NG = HW_THREADS / (4 * Q);
+  float* xs = lds;                    // [JC][Cin]
+  float* dl = xs + JC * Cin;          // [RMAX][DW]
+  float* xg = dl + RMAX * DW;         // [NG - 1][RMAX*SMAX][Cin]
+  const int t = threadIdx.x, q = t % Q, r = (t / Q) & 3, g = t / (4 * Q);
+  const int n = blockIdx.y, i = blockIdx.x;
+  const float* dyn = dy + (long)n * Ho * Wo * 4;
+  for (int e = t; e < RMAX * DW; e += HW_THREADS) {
+    const int rr = e / DW, ww = e - rr * DW - SMAX, hh = i + pad - rr;
+    dl[e] = (rr < R && (unsigned)hh < (unsigned)Ho && (unsigned)ww < (unsigned)Wo) ? dyn[((long)hh * Wo + ww) * 4]
+                                                                                   : 0.f;
+  }
+  float4 acc[SMAX];
+#pragma unroll
+  for (int s = 0; s < SMAX; ++s) acc[s] = make_float4(0.f, 0.f, 0.f, 0.f);
+  const float* xr = x + ((long)n * Hi + i) * Wi * Cin;
+  for (int j0 = 0; j0 < Wi; j0 += JC) {
+    const int jn = Wi - j0 < JC ? Wi - j0 : JC;
+    const int nf4 = jn * Q;  // float4s of this chunk: <= 4 per thread (JC * Cin <= 16384)
+    float4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (t + u * HW_THREADS < nf4) v[u] = *reinterpret_cast<const float4*>(xr + (long)j0 * Cin + 4 * (t + u * HW_THREADS));
+    __syncthreads();  // the previous chunk is consumed
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (t + u * HW_THREADS < nf4) *reinterpret_cast<float4*>(xs + 4 * (t + u * HW_THREADS)) = v[u];
+    __syncthreads();
+    const float* dj = dl + r * DW + SMAX + j0 + pad;
+    for (int j = g; j < jn; j += NG) {
+      const float4 xv = *reinterpret_cast<const float4*>(xs + j * Cin + 4 * q);
+#pragma unroll
+      for (int s = 0; s < SMAX; ++s) {
+        const float d = dj[j - s];
+        acc[s].x = fmaf(xv.x, d, acc[s].x);
+        acc[s].y = fmaf(xv.y, d, acc[s].y);
+        acc[s].z = fmaf(xv.z, d, acc[s].z);
+        acc[s].w = fmaf(xv.w, d, acc[s].w);
+      }
+    }
+  }
+  const int RS = R * S;
+  if (g > 0 && r < R) {
+#pragma unroll
+    for (int s = 0; s < SMAX; ++s)
+      if (s < S) *reinterpret_cast<float4*>(xg + ((long)(g - 1) * RS + r * S + s) * Cin + 4 * q) = acc[s];
+  }
+  __syncthreads();
+  if (g == 0 && r < R) {
+    float* dst = part + ((long)n * gridDim.x + i) * RS * Cin + 4 * q;
+#pragma unroll
+    for (int s = 0; s < SMAX; ++s) {
+      if (s >= S) continue;
+      float4 a = acc[s];
+      for (int gg = 1; gg < NG; ++gg)
+        add_f4(a, *reinterpret_cast<const float4*>(xg + ((long)(gg - 1) * RS + r * S + s) * Cin + 4 * q));
+      *reinterpret_cast<float4*>(dst + (long)(r * S + s) * Cin) = a;
+    }
+  }
+}
+
+// Fixed-order sum of the 256 threads' values v (thread order in 16-groups) -> thread 0.
 __device__ __forceinline__ float block_sum_fixed(float v, float* red) {
   red[threadIdx.x] = v;
   __syncthreads();
@@ -200,13 +316,47 @@ __device__ __forceinline__ float block_sum_fixed(float v, float* red) {
 __device__ void bias_sum_c0(const float* __restrict__ dy, long P, float* __restrict__ db, int accumulate) {
   __shared__ float red[256];
   float a = 0.f;
-  for (long p = threadIdx.x; p < P; p += 256) a += dy[p * 4];
+  long p = threadIdx.x;
+  for (; p + 768 < P; p += 1024) {
+    const float a0 = dy[p * 4], a1 = dy[(p + 256) * 4], a2 = dy[(p + 512) * 4], a3 = dy[(p + 768) * 4];
+    a += a0;
+    a += a1;
+    a += a2;
+    a += a3;
+  }
+  for (; p < P; p += 256) a += dy[p * 4];
   const float s = block_sum_fixed(a, red);
   if (threadIdx.x == 0) db[0] = accumulate ? db[0] + s : s;
 }
 
-// dw[ci*si + rs] (+)= sum_z part[z][rs*Cin + ci] in a fixed order: block = 16 outputs x 16 slab
-// groups (group u sums slabs u, u + 16, ... in order), the 16 group sums are then added in order.
+// out[m] = sum_z part[z][m] for one output m of a 16-wide block column, slab group u = 0..15 (slabs
+// u, u + 16, ... in order, loaded 8 at a time), then the 16 group sums in order.
+__device__ __forceinline__ float slab_sum16(const float* __restrict__ part, long Mw, long m, int nz, bool ok,
+                                            float (*red)[17]) {
+  const int t = threadIdx.x, o = t & 15, u = t >> 4;
+  float a = 0.f;
+  if (ok) {
+    for (int z0 = u; z0 < nz; z0 += 128) {
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (z0 + 16 * e < nz) v[e] = part[(long)(z0 + 16 * e) * Mw + m];
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (z0 + 16 * e < nz) a += v[e];
+    }
+  }
+  red[u][o] = a;
+  __syncthreads();
+  float s = 0.f;
+  if (u == 0) {
+    s = red[0][o];
+    for (int k = 1; k < 16; ++k) s += red[k][o];
+  }
+  return s;
+}
+
+// dw[ci*si + rs] (+)= sum_z part[z][rs*Cin + ci] in a fixed order (block = 16 outputs x 16 slab groups).
 // db != null: one more block sums dy's channel 0 (the bias gradient).
 __global__ __launch_bounds__(256) void head_wgrad_reduce_k(const float* __restrict__ part, float* __restrict__ dw,
                                                            int Mw, int Cin, int Ci, int RS, long si,
@@ -217,27 +367,10 @@ __global__ __launch_bounds__(256) void head_wgrad_reduce_k(const float* __restri
     return;
   }
   __shared__ float red[16][17];
-  const int t = threadIdx.x, o = t & 15, u = t >> 4;
-  const int m = blockIdx.x * 16 + o;
-  float a = 0.f;
-  if (m < Mw) {
-    int zz = u;
-    for (; zz + 48 < nz; zz += 64) {
-      const float p0 = part[(long)zz * Mw + m], p1 = part[(long)(zz + 16) * Mw + m];
-      const float p2 = part[(long)(zz + 32) * Mw + m], p3 = part[(long)(zz + 48) * Mw + m];
-      a += p0;
-      a += p1;
-      a += p2;
-      a += p3;
-    }
-    for (; zz < nz; zz += 16) a += part[(long)zz * Mw + m];
-  }
-  red[u][o] = a;
-  __syncthreads();
+  const int m = blockIdx.x * 16 + (threadIdx.x & 15);
+  const float s = slab_sum16(part, Mw, m, nz, m < Mw, red);
   const int rs = m / Cin, ci = m - rs * Cin;
-  if (u == 0 && m < Mw && ci < Ci) {
-    float s = red[0][o];
-    for (int k = 1; k < 16; ++k) s += red[k][o];
+  if (threadIdx.x < 16 && m < Mw && ci < Ci) {
     float* d = dw + (long)ci * si + rs;
     *d = accumulate ? *d + s : s;
   }
@@ -245,35 +378,53 @@ __global__ __launch_bounds__(256) void head_wgrad_reduce_k(const float* __restri
 
 // ---- data gradient -------------------------------------------------------------------------------
 // dx[n][i][j][c] = sum_{r,s} dy[n][i+pad-r][j+pad-s][0] * w[c][r][s][0] (+ addend): wp = the VST_PACK_IK
-// pack [Cx][R][S][Cy] with Cy = 4 of which only channel 0 is real (co_real = 1).
-__global__ __launch_bounds__(256) void head_dgrad_k(const float* __restrict__ dy, const float* __restrict__ wp,
-                                                    const float* __restrict__ addend, float* __restrict__ dx,
-                                                    int Hd, int Wd, int Cx, int H, int W, int R, int S, int pad) {
-  extern __shared__ float dl[];  // dl[r][SMAX + ww] = dy row i + pad - r (channel 0), zero outside
-  const int DW = Wd + 2 * SMAX;
-  const int t = threadIdx.x, Q = Cx / 4, NG = 256 / Q;
+// pack [Cx][R][S][Cy] with Cy = 4 of which only channel 0 is real (co_real = 1).  Block = (input row i,
+// image n): the channel-0 weights [R*S][Cx] and dy's rows i + pad - r go to LDS first (loads batched),
+// each thread then holds its 4 channels' R*S weights in registers, so the column loop issues only LDS
+// reads and the stores.
+constexpr int HD_THREADS = 256;
+
+__global__ __launch_bounds__(HD_THREADS) void head_dgrad_k(const float* __restrict__ dy, const float* __restrict__ wp,
+                                                           const float* __restrict__ addend, float* __restrict__ dx,
+                                                           int Hd, int Wd, int Cx, int H, int W, int R, int S,
+                                                           int pad) {
+  extern __shared__ float lds[];
+  const int DW = Wd + 2 * SMAX, RS = R * S;
+  float* wl = lds;                   // [RMAX*SMAX][Cx]
+  float* dl = lds + RMAX * SMAX * Cx;  // [RMAX][DW]
+  const int t = threadIdx.x, Q = Cx / 4, NG = HD_THREADS / Q;
   const int q = t % Q, g = t / Q;
   const int n = blockIdx.y, i = blockIdx.x;
   const float* dyn = dy + (long)n * Hd * Wd * 4;
-  for (int e = t; e < RMAX * DW; e += 256) {
-    const int r = e / DW, ww = e - r * DW - SMAX, hh = i + pad - r;
-    dl[e] = (r < R && (unsigned)hh < (unsigned)Hd && (unsigned)ww < (unsigned)Wd) ? dyn[((long)hh * Wd + ww) * 4]
+  // weights: element e = c * RS + tap of the channel-0 column (IK pack stride 4 floats)
+  const int nw = Cx * RS;
+  for (int e0 = 0; e0 < nw; e0 += 16 * HD_THREADS) {
+    float v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u)
+      if (e0 + t + u * HD_THREADS < nw) v[u] = wp[(long)(e0 + t + u * HD_THREADS) * 4];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int e = e0 + t + u * HD_THREADS;
+      if (e < nw) {
+        const int c = e / RS, tap = e - c * RS;
+        wl[tap * Cx + c] = v[u];
+      }
+    }
+  }
+  for (int e = t; e < RMAX * DW; e += HD_THREADS) {
+    const int rr = e / DW, ww = e - rr * DW - SMAX, hh = i + pad - rr;
+    dl[e] = (rr < R && (unsigned)hh < (unsigned)Hd && (unsigned)ww < (unsigned)Wd) ? dyn[((long)hh * Wd + ww) * 4]
                                                                                   : 0.f;
   }
+  __syncthreads();
   float4 wv[RMAX * SMAX];
-  const long cs = (long)R * S * 4;  // between input channels of the IK pack
 #pragma unroll
   for (int r = 0; r < RMAX; ++r)
 #pragma unroll
-    for (int s = 0; s < SMAX; ++s) {
-      float4 w = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (r < R && s < S) {
-        const float* p = wp + (long)(4 * q) * cs + (r * S + s) * 4;  // [c][r][s][0], c = 4q..4q+3
-        w = make_float4(p[0], p[cs], p[2 * cs], p[3 * cs]);
-      }
-      wv[r * SMAX + s] = w;
-    }
-  __syncthreads();
+    for (int s = 0; s < SMAX; ++s)
+      wv[r * SMAX + s] = (r < R && s < S) ? *reinterpret_cast<const float4*>(wl + (r * S + s) * Cx + 4 * q)
+                                          : make_float4(0.f, 0.f, 0.f, 0.f);
   for (int j = g; j < W; j += NG) {
     float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
     const float* dj = dl + SMAX + j + pad;
@@ -294,7 +445,6 @@ __global__ __launch_bounds__(256) void head_dgrad_k(const float* __restrict__ dy
   }
 }
 
-
 // ---- image-input weight gradient (the PatchGAN first layer Conv2d(3, ndf, 4, 2, 1), networks.py:556) ----
 // C[co][j] = sum_p dy[p][co] * X[p][j] over the output pixels p, j = (r*S + s)*4 + c, X[p][j] =
 // x[n][st*ho - pad + r][st*wo - pad + s][c] (zero outside; c < Ci real, the rest zero) and, when the
@@ -303,9 +453,10 @@ __global__ __launch_bounds__(256) void head_dgrad_k(const float* __restrict__ dy
 // HBM-bound on the fp32 dy stream, which is read once and never converted to planes).  Lane l = (i =
 // l % 32, k = l / 32) feeds pixel p0 + k of a pair: A block mi takes co = 2i + mi (one float2 load of dy's
 // row), B block nj takes j = 2i + nj (one float2 of x: tap i / 2, channels 2 (i % 2) + {0, 1}).  A wave
-// walks a contiguous run of pixel pairs; the block's waves add their 64 x 64 tiles in LDS in a fixed
-// order into one partial slab part[block][j][co], reduced by img_wgrad_reduce_k.
-constexpr int IW_WAVES = 8;
+// walks a contiguous run of pixel pairs, IW_B pairs' loads issued before their MFMAs; the block's waves
+// add their 64 x 64 tiles in LDS in a fixed order into one partial slab part[block][j][co], reduced by
+// img_wgrad_reduce_k.
+constexpr int IW_WAVES = 8, IW_B = 16;
 
 __global__ __launch_bounds__(64 * IW_WAVES) void img_wgrad_k(const float* __restrict__ x, const float* __restrict__ dy,
                                                             float* __restrict__ part, int H, int W, int Ho, int Wo,
@@ -318,9 +469,8 @@ __global__ __launch_bounds__(64 * IW_WAVES) void img_wgrad_k(const float* __rest
   const int r = rs / S, s = rs - (rs / S) * S;
   const bool tap_ok = rs < R * S;
   const bool co_ok = 2 * i < Cyp;
-  // which of this lane's two B channels are real / the bias slot
-  const bool cx_ok = c0 < Ci, cy_ok = c0 + 1 < Ci;
-  const float cy_bias = (want_db && rs == 0 && c0 + 1 == 3) ? 1.f : 0.f;
+  const float mx = c0 < Ci ? 1.f : 0.f, my = c0 + 1 < Ci ? 1.f : 0.f;
+  const bool bias_slot = want_db && rs == 0 && c0 + 1 == 3;
   f32x16 acc[2][2];
 #pragma unroll
   for (int a = 0; a < 2; ++a)
@@ -330,86 +480,92 @@ __global__ __launch_bounds__(64 * IW_WAVES) void img_wgrad_k(const float* __rest
       for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
   const long wid = (long)blockIdx.x * IW_WAVES + wave;
   const long p0 = wid * ppw, p1 = p0 + ppw < P ? p0 + ppw : P;
-  const long HWo = (long)Ho * Wo;
-  for (long p = p0 + kk; p - kk < p1; p += 2) {
-    float2 av = make_float2(0.f, 0.f), bv = make_float2(0.f, cy_bias);
-    if (p < p1) {
-      const long n = p / HWo;
-      const int rem = (int)(p - n * HWo), ho = rem / Wo, wo = rem - (rem / Wo) * Wo;
-      if (co_ok) av = *reinterpret_cast<const float2*>(dy + p * Cyp + 2 * i);
-      const int hi = st * ho - pad + r, wi = st * wo - pad + s;
-      if (tap_ok && (unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W) {
-        const float2 v = *reinterpret_cast<const float2*>(x + (((n * H + hi) * W + wi) << 2) + c0);
-        bv.x = cx_ok ? v.x : 0.f;
-        if (cy_ok) bv.y = v.y;
+  // this lane's pixel cursor (n, ho, wo) for p = pb + kk, advanced 2 pixels per pair
+  long p = p0 + kk;
+  int cn, cho, cwo;
+  {
+    const long HWo = (long)Ho * Wo;
+    const long pp = p < P ? p : P - 1;
+    cn = (int)(pp / HWo);
+    const int rem = (int)(pp - (long)cn * HWo);
+    cho = rem / Wo;
+    cwo = rem - cho * Wo;
+  }
+  for (long pb = p0; pb < p1; pb += 2 * IW_B) {
+    float2 av[IW_B], bv[IW_B];
+    float live[IW_B];
+#pragma unroll
+    for (int u = 0; u < IW_B; ++u) {
+      const bool ok = p < p1;
+      const int hi = st * cho - pad + r, wi = st * cwo - pad + s;
+      const bool in = ok && tap_ok && (unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W;
+      const long pd = ok ? p : p0;  // p0 < P: a valid row to read when this lane is past its run
+      av[u] = co_ok ? *reinterpret_cast<const float2*>(dy + pd * Cyp + 2 * i) : make_float2(0.f, 0.f);
+      bv[u] = in ? *reinterpret_cast<const float2*>(x + ((((long)cn * H + hi) * W + wi) << 2) + c0)
+                 : make_float2(0.f, 0.f);
+      live[u] = ok ? 1.f : 0.f;
+      p += 2;
+      cwo += 2;
+      while (cwo >= Wo) {
+        cwo -= Wo;
+        if (++cho == Ho) {
+          cho = 0;
+          ++cn;
+        }
       }
-    } else {
-      bv.y = 0.f;
     }
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int b = 0; b < 2; ++b)
-        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(a ? av.y : av.x, b ? bv.y : bv.x, acc[a][b], 0, 0, 0);
+    for (int u = 0; u < IW_B; ++u) {
+      const float a0 = av[u].x * live[u], a1 = av[u].y * live[u];
+      const float b0 = bv[u].x * mx, b1 = bias_slot ? live[u] : bv[u].y * my;
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+    }
   }
-  // C block (a, b): lane column jj = i, rows ii = 8 (e / 4) + 4 kk + e % 4  ->  co = 2 ii + a, j = 2 jj + b
+  // The block's 8 wave tiles are summed in register order (tl[w][(2a + b) * 16 + e][lane]: conflict-free
+  // LDS rows) and the partial slab keeps that order; img_wgrad_reduce_k maps it to (co, j).
   if (wave > 0) {
-    float* d = tl + (long)(wave - 1) * 4096;
+    float* d = tl + (long)(wave - 1) * 4096 + lane;
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
       for (int b = 0; b < 2; ++b)
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int ii = 8 * (e >> 2) + 4 * kk + (e & 3);
-          d[(2 * i + b) * 64 + 2 * ii + a] = acc[a][b][e];
-        }
+        for (int e = 0; e < 16; ++e) d[((2 * a + b) * 16 + e) * 64] = acc[a][b][e];
   }
   __syncthreads();
   if (wave == 0) {
-    float* dst = part + (long)blockIdx.x * 4096;
+    float* dst = part + (long)blockIdx.x * 4096 + lane;
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
       for (int b = 0; b < 2; ++b)
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
-          const int ii = 8 * (e >> 2) + 4 * kk + (e & 3);
-          const int o = (2 * i + b) * 64 + 2 * ii + a;
+          const int o = ((2 * a + b) * 16 + e) * 64;
           float v = acc[a][b][e];
-          for (int w = 0; w < IW_WAVES - 1; ++w) v += tl[(long)w * 4096 + o];
+          for (int w = 0; w < IW_WAVES - 1; ++w) v += tl[(long)w * 4096 + o + lane];
           dst[o] = v;
         }
   }
 }
 
-// dw[co*so + ci*si + rs] (+)= sum_z part[z][rs*4 + ci][co] (ci < Ci, co < Co), db[co] (+)= sum_z
-// part[z][3][co]; fixed order: block = 16 outputs x 16 slab groups.
+// dw[co*so + ci*si + rs] (+)= sum_z C[co][j] (j = rs*4 + ci, ci < Ci, co < Co), db[co] (+)= sum_z C[co][3];
+// part[z] holds C in the MFMA register order [(2a + b) * 16 + e][lane]: lane = i + 32 kk, column j =
+// 2 i + b, row co = 2 (8 (e / 4) + 4 kk + e % 4) + a.  Fixed order: block = 16 outputs x 16 slab groups.
 __global__ __launch_bounds__(256) void img_wgrad_reduce_k(const float* __restrict__ part, float* __restrict__ dw,
                                                           float* __restrict__ db, int RS, int Co, int Ci, long so,
                                                           long si, int accumulate, int nz) {
   __shared__ float red[16][17];
-  const int t = threadIdx.x, o = t & 15, u = t >> 4;
-  const int m = blockIdx.x * 16 + o;  // (j, co) = (m / 64, m % 64)
-  float a = 0.f;
-  {
-    int zz = u;
-    for (; zz + 48 < nz; zz += 64) {
-      const float p0 = part[(long)zz * 4096 + m], p1 = part[(long)(zz + 16) * 4096 + m];
-      const float p2 = part[(long)(zz + 32) * 4096 + m], p3 = part[(long)(zz + 48) * 4096 + m];
-      a += p0;
-      a += p1;
-      a += p2;
-      a += p3;
-    }
-    for (; zz < nz; zz += 16) a += part[(long)zz * 4096 + m];
-  }
-  red[u][o] = a;
-  __syncthreads();
-  const int j = m >> 6, co = m & 63, rs = j >> 2, ci = j & 3;
-  if (u != 0 || co >= Co) return;
-  float v = red[0][o];
-  for (int k = 1; k < 16; ++k) v += red[k][o];
+  const int m = blockIdx.x * 16 + (threadIdx.x & 15);
+  const float v = slab_sum16(part, 4096, m, nz, true, red);
+  const int lane = m & 63, ab = m >> 10, e = (m >> 6) & 15;
+  const int a = ab >> 1, b = ab & 1, i = lane & 31, kk = lane >> 5;
+  const int j = 2 * i + b, co = 2 * (8 * (e >> 2) + 4 * kk + (e & 3)) + a;
+  const int rs = j >> 2, ci = j & 3;
+  if (threadIdx.x >= 16 || co >= Co) return;
   if (ci < Ci && rs < RS) {
     float* d = dw + (long)co * so + (long)ci * si + rs;
     *d = accumulate ? *d + v : v;
@@ -423,62 +579,77 @@ __global__ __launch_bounds__(256) void img_wgrad_reduce_k(const float* __restric
 using namespace patch;
 
 bool head_ok(int Cin, int R, int S, int st, int reflect, int Wo) {
-  // Cin / 4 must divide the 256 threads (the channel quads x column groups layout); the LDS images
-  // (the forward's weights, the weight gradient's cross-group partials + dy rows) must fit
-  if (!(st == 1 && !reflect && R >= 1 && R <= RMAX && S >= 1 && S <= SMAX && Cin % 4 == 0 && Cin >= 4 &&
-        256 % (Cin / 4) == 0 && Wo >= 1 && Wo <= 4096))
+  // Cin / 4 channel quads must divide the threads (quads x kernel rows x column groups), Cin % 16 for
+  // the forward's channel quarters; the LDS images (weights, the weight gradient's row chunk and
+  // cross-group partials, dy rows) must fit
+  if (!(st == 1 && !reflect && R >= 1 && R <= RMAX && S >= 1 && S <= SMAX && Cin % 16 == 0 && Cin >= 16 &&
+        Cin <= 1024 && (Cin & (Cin - 1)) == 0 && Wo >= 1 && Wo <= 2048))
     return false;
-  const long fwd = (long)RMAX * SMAX * Cin + RMAX * 64 * SMAX;
-  const long wg = (long)(256 / (Cin / 4) - 1) * R * S * Cin + RMAX * (Wo + 2 * SMAX);
-  return (fwd > wg ? fwd : wg) * 4 <= 160 * 1024;
+  const long fwd = (long)RMAX * SMAX * Cin + HF_NQ * RMAX * 64 * SMAX;
+  const long wg = 16384 + RMAX * (Wo + 2 * SMAX) + (long)(HW_THREADS / Cin - 1) * RMAX * SMAX * Cin;
+  const long dg = (long)RMAX * SMAX * Cin + RMAX * (Wo + 2 * SMAX);
+  const long mx = fwd > wg ? (fwd > dg ? fwd : dg) : (wg > dg ? wg : dg);
+  return mx * 4 <= 160 * 1024;
 }
 
 int head_fwd_launch(const float* x, const float* wp, const float* bias, float* out, int N, int Hi, int Wi, int Cin,
                     int Ho, int Wo, int R, int S, int pad, int act, float slope, hipStream_t s) {
   // KS = 2 lanes per column when the row's columns fit 32 lanes, else one lane per column and
   // segments of 64 - S + 1 outputs
-  const int ks = (Wo + S - 1 <= 32 && Cin % 8 == 0) ? 2 : 1;
+  const int ks = (Wo + S - 1 <= 32 && Cin % 32 == 0) ? 2 : 1;
   const int seg = ks == 2 ? Wo : (Wo + S - 1 <= 64 ? Wo : 64 - S + 1);
-  const size_t lds = ((size_t)RMAX * SMAX * Cin + RMAX * (64 / ks) * SMAX) * sizeof(float);
+  const size_t lds = ((size_t)RMAX * SMAX * Cin + HF_NQ * RMAX * (64 / ks) * SMAX) * sizeof(float);
   const dim3 grid(ceil_div(Wo, seg), Ho, N);
   if (ks == 2)
-    hipLaunchKernelGGL(head_fwd_k<2>, grid, dim3(256), lds, s, x, wp, bias, out, Hi, Wi, Cin, Ho, Wo, R, S, pad, act,
-                       slope, seg);
+    hipLaunchKernelGGL(head_fwd_k<2>, grid, dim3(HF_THREADS), lds, s, x, wp, bias, out, Hi, Wi, Cin, Ho, Wo, R, S, pad,
+                       act, slope, seg);
   else
-    hipLaunchKernelGGL(head_fwd_k<1>, grid, dim3(256), lds, s, x, wp, bias, out, Hi, Wi, Cin, Ho, Wo, R, S, pad, act,
-                       slope, seg);
+    hipLaunchKernelGGL(head_fwd_k<1>, grid, dim3(HF_THREADS), lds, s, x, wp, bias, out, Hi, Wi, Cin, Ho, Wo, R, S, pad,
+                       act, slope, seg);
   return check_launch("head_fwd");
 }
 
-// rows per weight-gradient block: about 160 blocks (the partial slabs stay small)
-static int head_wgrad_rows(int N, int Hi) {
-  const int G = ceil_div((long)N * Hi, 160);
-  return G < 1 ? 1 : G;
+size_t head_tap_ws_floats(int N, int Hi, int Wi) { return (size_t)N * Hi * Wi * 16; }
+
+bool head_tap_ok(int Cin) {
+  // K halves of whole 16-channel groups; the row chunk + weights + partials fit the LDS
+  return Cin % 32 == 0 && ((size_t)(HT_JC + 16) * (Cin + 4) + 4 * HT_JC * 16) * 4 <= 160 * 1024;
 }
 
-size_t head_wgrad_ws_floats(int N, int Hi, int Cin, int R, int S) {
-  const int G = head_wgrad_rows(N, Hi);
-  return (size_t)N * ceil_div(Hi, G) * R * S * Cin;
+int head_tap_fwd_launch(const float* x, const float* wp, const float* bias, float* out, float* ws, int N, int Hi,
+                        int Wi, int Cin, int Ho, int Wo, int R, int S, int pad, int act, float slope, hipStream_t s) {
+  const size_t lds = ((size_t)(HT_JC + 16) * (Cin + 4) + 4 * HT_JC * 16) * sizeof(float);
+  hipLaunchKernelGGL(head_tap_k, dim3(Hi, N), dim3(HT_THREADS), lds, s, x, wp, ws, Hi, Wi, Cin, R * S);
+  int rc = check_launch("head_tap");
+  if (rc) return rc;
+  hipLaunchKernelGGL(head_tapsum_k, dim3(ceil_div((long)N * Ho * Wo, 256)), dim3(256), 0, s, ws, bias, out, N, Hi, Wi,
+                     Ho, Wo, R, S, pad, act, slope);
+  return check_launch("head_tapsum");
 }
+
+size_t head_wgrad_ws_floats(int N, int Hi, int Cin, int R, int S) { return (size_t)N * Hi * R * S * Cin; }
 
 int head_wgrad_launch(const float* x, const float* dy, float* dw, float* ws, int N, int Hi, int Wi, int Cin, int Ci,
                       int Ho, int Wo, int R, int S, int pad, long si, int accumulate, hipStream_t s, float* db) {
-  const int G = head_wgrad_rows(N, Hi), nb = ceil_div(Hi, G);
-  const int NG = 256 / (Cin / 4);
-  const size_t lds = ((size_t)(NG - 1) * R * S * Cin + RMAX * (Wo + 2 * SMAX)) * sizeof(float);
-  hipLaunchKernelGGL(head_wgrad_k, dim3(nb, N), dim3(256), lds, s, x, dy, ws, Hi, Wi, Cin, Ho, Wo, R, S, pad, G);
+  int JC = 16384 / Cin;
+  if (JC > Wi) JC = Wi;
+  const int NG = HW_THREADS / Cin;  // column groups: 1024 threads / (Cin / 4 quads x 4 kernel rows)
+  const size_t lds = ((size_t)JC * Cin + RMAX * (Wo + 2 * SMAX) + (size_t)(NG - 1) * R * S * Cin) * sizeof(float);
+  hipLaunchKernelGGL(head_wgrad_k, dim3(Hi, N), dim3(HW_THREADS), lds, s, x, dy, ws, Hi, Wi, Cin, Ho, Wo, R, S, pad,
+                     JC);
   int rc = check_launch("head_wgrad");
   if (rc) return rc;
   const int Mw = R * S * Cin;
   hipLaunchKernelGGL(head_wgrad_reduce_k, dim3(ceil_div(Mw, 16) + (db ? 1 : 0)), dim3(256), 0, s, ws, dw, Mw, Cin, Ci,
-                     R * S, si, accumulate, N * nb, dy, (long)N * Ho * Wo, db);
+                     R * S, si, accumulate, N * Hi, dy, (long)N * Ho * Wo, db);
   return check_launch("head_wgrad_reduce");
 }
 
 int head_dgrad_launch(const float* dy, const float* wp, const float* addend, float* dx, int N, int Hd, int Wd, int Cx,
                       int H, int W, int R, int S, int pad, hipStream_t s) {
-  const size_t lds = (size_t)RMAX * (Wd + 2 * SMAX) * sizeof(float);
-  hipLaunchKernelGGL(head_dgrad_k, dim3(H, N), dim3(256), lds, s, dy, wp, addend, dx, Hd, Wd, Cx, H, W, R, S, pad);
+  const size_t lds = ((size_t)RMAX * SMAX * Cx + RMAX * (Wd + 2 * SMAX)) * sizeof(float);
+  hipLaunchKernelGGL(head_dgrad_k, dim3(H, N), dim3(HD_THREADS), lds, s, dy, wp, addend, dx, Hd, Wd, Cx, H, W, R, S,
+                     pad);
   return check_launch("head_dgrad");
 }
 
@@ -497,9 +668,9 @@ bool img_wgrad_ok(int Cx, int Cyp, int R, int S, int st, int reflect, int Ci, in
 }
 
 static long img_wgrad_blocks(long P) {
-  // ~2 pixel-pair runs of >= 32 pairs per wave, at most 256 blocks (the partial slabs stay <= 4 MB)
+  // 2 x IW_B pixel pairs (64 pixels) per wave, at most 512 blocks (the partial slabs stay <= 8 MB)
   long b = (P + 64L * IW_WAVES - 1) / (64L * IW_WAVES);
-  return b < 1 ? 1 : (b > 256 ? 256 : b);
+  return b < 1 ? 1 : (b > 512 ? 512 : b);
 }
 
 size_t img_wgrad_ws_floats(int N, int Ho, int Wo) { return (size_t)img_wgrad_blocks((long)N * Ho * Wo) * 4096; }
@@ -516,8 +687,8 @@ int img_wgrad_launch(const float* x, const float* dy, float* dw, float* db, floa
                      st, pad, Ci, db ? 1 : 0, P, (int)ppw);
   int rc = check_launch("img_wgrad");
   if (rc) return rc;
-  hipLaunchKernelGGL(img_wgrad_reduce_k, dim3(256), dim3(256), 0, s, ws, dw, db, R * S, Co, Ci, so, si, accumulate,
-                     (int)nb);
+  hipLaunchKernelGGL(img_wgrad_reduce_k, dim3(4096 / 16), dim3(256), 0, s, ws, dw, db, R * S, Co, Ci, so, si,
+                     accumulate, (int)nb);
   return check_launch("img_wgrad_reduce");
 }
 

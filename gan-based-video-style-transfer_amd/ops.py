@@ -217,8 +217,11 @@ def conv2d_fwd(x, wp, bias, cop, R, S, stride, pad, pad_mode="zero", act="none",
         Ho = (H + 2 * pad - R) // stride + 1
         Wo = (W + 2 * pad - S) // stride + 1
         y = out if out is not None else torch.empty((N, Ho, Wo, cop), device=x.device)
-        _call("vst_conv2d_fwd_co", _p(x), _p(wp), _p(getattr(wp, "vst_split", None)), _p(bias), _p(y), N, H, W, Cx,
-              cop, R, S, stride, pad, PAD[pad_mode], ACT[act], float(slope), _math(role), int(co_real), _stream())
+        nb = int(lib().vst_conv2d_fwd_co_ws_bytes(N, H, W, Cx, cop, R, S, stride, pad, PAD[pad_mode], int(co_real)))
+        ws = torch.empty((nb + 3) // 4, device=x.device) if nb else None
+        _call("vst_conv2d_fwd_co_ws", _p(x), _p(wp), _p(getattr(wp, "vst_split", None)), _p(bias), _p(y), N, H, W,
+              Cx, cop, R, S, stride, pad, PAD[pad_mode], ACT[act], float(slope), _math(role), int(co_real), _p(ws), nb,
+              _stream())
         return y
     N, H, W, Cx = x.shape
     Ho = (H + 2 * pad - R) // stride + 1

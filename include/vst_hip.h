@@ -164,6 +164,15 @@ int vst_conv_plan_fwd_tail(int N, int H, int W, int Cx, int Cop, int R, int S, i
 int vst_conv2d_fwd_co(const float* x, const float* wp, const void* wsplit, const float* bias, float* y, int N, int H,
                       int W, int Cx, int Cop, int R, int S, int stride, int pad, int pad_mode, int act, float slope,
                       int math, int co_real, void* stream);
+/* vst_conv2d_fwd_co with a caller workspace of vst_conv2d_fwd_co_ws_bytes bytes (0: the shape takes no
+ * workspace route, ws may be NULL): with co_real = 1 the PatchGAN head (networks.py:578; stride 1, zero
+ * padding, R, S <= 4, Cx a power of two in 32..1024) runs as a per-input-row tap GEMM that reads x once
+ * (z[n][h][w][tap] in ws) plus a fixed-order tap sum (patch.hip). */
+size_t vst_conv2d_fwd_co_ws_bytes(int N, int H, int W, int Cx, int Cop, int R, int S, int stride, int pad,
+                                  int pad_mode, int co_real);
+int vst_conv2d_fwd_co_ws(const float* x, const float* wp, const void* wsplit, const float* bias, float* y, int N,
+                         int H, int W, int Cx, int Cop, int R, int S, int stride, int pad, int pad_mode, int act,
+                         float slope, int math, int co_real, float* ws, size_t ws_bytes, void* stream);
 /* vst_conv2d_fwd plus the InstanceNorm statistics partials of its output, from the GEMM epilogue
  * (the conv that feeds an InstanceNorm): when the split-bf16 kernels run the conv and Ho*Wo % 32 == 0,
  * part (fp64, N * (Ho*Wo/32) * Cop * 2) receives {sum y, sum y^2} per (image, 32-pixel group,

@@ -275,8 +275,22 @@ def johnson_train_fps(device, B=4, S=256, steps=5):
         J.train_step(x)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / steps
+    tf = _count_tflop(lambda: J.train_step(x))
     return {"metric": "Johnson fast-style train step frames/s %dx%d" % (S, S), "batch": B,
-            "value": round(B / dt, 2), "unit": "frames/s", "ms_per_step": round(dt * 1e3, 3)}
+            "value": round(B / dt, 2), "unit": "frames/s", "ms_per_step": round(dt * 1e3, 3),
+            "tflop_per_step": round(tf, 4),
+            "roofline": _mfma_roofline(tf / dt, "FastStyleNet + VGG-16 conv / Gram FLOPs of one step "
+                                               "(tools/convflops) over the step time")}
+
+
+def _count_tflop(fn):
+    """Algorithmic conv TFLOPs of one call of fn (tools/convflops.Counter: every gbvst.ops conv entry,
+    real channel counts), run once untimed after the timed region."""
+    from tools import convflops
+    with convflops.Counter() as c:
+        fn()
+    torch.cuda.synchronize()
+    return c.flops / 1e12
 
 
 def stargan_train_fps(device, B=4, S=256, c_dim=4, cycles=2):
@@ -297,8 +311,17 @@ def stargan_train_fps(device, B=4, S=256, c_dim=4, cycles=2):
         sol.train_step(x, lo, lt)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / (5 * cycles)
+
+    def cycle():
+        for _ in range(5):
+            sol.train_step(x, lo, lt)
+    tf = _count_tflop(cycle) / 5.0  # per D iteration (a cycle's G step shared over its 5)
     return {"metric": "StarGAN train images/s per D iteration %dx%d (n_critic 5)" % (S, S), "batch": B,
-            "value": round(B / dt, 2), "unit": "images/s", "ms_per_d_iteration": round(dt * 1e3, 3)}
+            "value": round(B / dt, 2), "unit": "images/s", "ms_per_d_iteration": round(dt * 1e3, 3),
+            "tflop_per_d_iteration": round(tf, 4),
+            "roofline": _mfma_roofline(tf / dt, "G/D conv FLOPs of one n_critic cycle (5 D iterations with the "
+                                               "WGAN-GP double backward + 1 G step, counted per conv op by "
+                                               "tools/convflops) / 5, over the D-iteration time")}
 
 
 def raft_inference(device, B=1, H=436, W=1024, iters=20, reps=3):
@@ -320,7 +343,9 @@ def raft_inference(device, B=1, H=436, W=1024, iters=20, reps=3):
     pads = raft.InputPadder((B, 3, H, W)).pads
     fl = raft.raft_flops(B, H + pads[2] + pads[3], W + pads[0] + pads[1], iters)
     return {"metric": "RAFT flow %dx%d, %d iterations" % (H, W, iters), "batch": B, "ms_per_call": round(dt * 1e3, 3),
-            "pairs_per_s": round(B / dt, 2), "tflops": round(fl / dt / 1e12, 2)}
+            "pairs_per_s": round(B / dt, 2), "tflops": round(fl / dt / 1e12, 2),
+            "roofline": _mfma_roofline(fl / dt / 1e12, "RAFT conv + correlation FLOPs (raft.raft_flops) over the "
+                                                       "call time")}
 
 
 def mogan_train_fps(device, B=4, S=256, pairs=2, H=None, W=None):
@@ -343,8 +368,16 @@ def mogan_train_fps(device, B=4, S=256, pairs=2, H=None, W=None):
         m.optimize_parameters()
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / (2 * pairs)
+
+    def pair():
+        m.optimize_parameters()
+        m.optimize_parameters()
+    tf = _count_tflop(pair) / 2.0  # per optimize_parameters (E and M averaged)
     return {"metric": "MoGAN optimize_parameters frames/s %dx%d (8 RAFT flows x 20 iterations per step)" % (W, H),
-            "batch": B, "value": round(B / dt, 2), "unit": "frames/s", "ms_per_step": round(dt * 1e3, 3)}
+            "batch": B, "value": round(B / dt, 2), "unit": "frames/s", "ms_per_step": round(dt * 1e3, 3),
+            "tflop_per_step": round(tf, 4),
+            "roofline": _mfma_roofline(tf / dt, "conv FLOPs of one E + one M step (G/D/motion nets and the 8 RAFT "
+                                               "flows' convs, tools/convflops) / 2, over the step time")}
 
 
 VGG19_TO_RELU5_1 = [(3, 64), (64, 64), "pool", (64, 128), (128, 128), "pool", (128, 256), (256, 256), (256, 256),

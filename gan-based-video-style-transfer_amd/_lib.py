@@ -150,6 +150,7 @@ SIGNATURES = {
     "vst_tapfold": (I, [P, P, I, I, I, I, I, I, I, P]),
     "vst_tap_wgrad_scatter": (I, [P, P, I, I, I, I, I, P]),
     "vst_tap_wgrad_swap": (I, [P, P, P, P, SZ, I, I, I, I, I, I, I, I, P]),
+    "vst_tap_wgrad_swap_db": (I, [P, P, P, P, P, SZ, I, I, I, I, I, I, I, I, P]),
     "vst_tap_wgrad_swap_ws_bytes": (SZ, [I, I, I, I, I]),
     "vst_tap_wgrad_swap_ld": (L, [I, I, I, I]),
     "vst_tapgather": (I, [P, P, I, I, I, I, I, I, I, P]),

@@ -754,6 +754,11 @@ static int pick_splits(int tiles, int slots, int max_ns, int min_ns = 1) {
 #define VST_WG_BF 1   // x6 weight gradients on the split-bf16 kernel (conv_wgrad_bf_k)
 #endif
 
+static const int g_wg_kind_s2 = [] {
+  const char* e = getenv("VST_WG_KIND_S2");
+  return e ? atoi(e) : -1;
+}();
+
 static WgradPlan plan_wgrad(int N, int H, int W, int Ho, int Wo, int Cx, int Cyp, int R, int S,
                             int stride, int math) {
   WgradPlan p;
@@ -778,7 +783,12 @@ static WgradPlan plan_wgrad(int N, int H, int W, int Ho, int Wo, int Cx, int Cyp
     p.trans = p.bfk = true;
     p.pad = s1 ? pd2 / 2 : -1;
     p.wpad = wpad;
-    const int kind = Cyp > 64 ? (p.Mw >= VST_WG_BIGM ? 7 : 3) : (p.Mw >= 1024 ? 1 : 8);
+    int kind = Cyp > 64 ? (p.Mw >= VST_WG_BIGM ? 7 : 3) : (p.Mw >= 1024 ? 1 : 8);
+    // M rows (tap, ci) that 256-row tiles pad more than 128-row ones (the generator's stride-2 3x3 layers:
+    // 576 rows = 2.25 x 256, 1152 = 4.5 x 256) run on 128x128 tiles of 8 waves (64x32); round-5 sweep
+    // (profiles/r05e_convT_wgrad_tiles.jsonl): 178 -> 172 / 149 -> 136 us at N = 8
+    if (kind == 7 && ceil_div(p.Mw, 256) * 256 > ceil_div(p.Mw, 128) * 128) kind = 0;
+    if (g_wg_kind_s2 >= 0 && stride == 2) kind = g_wg_kind_s2;  // developer A/B (VST_WG_KIND_S2)
     p.tile = (TileKind)kind;
     int bm, bn, bk, slots;
     bf_wgrad_geom(kind, math, &bm, &bn, &bk, &slots);

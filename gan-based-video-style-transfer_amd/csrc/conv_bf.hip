@@ -1975,10 +1975,22 @@ bool bf_convT_phases_ok(int C, int Cop, int math) {
   return math != VST_MATH_F32 && VST_BF_KSLICE && C % 32 == 0 && Cop % 4 == 0;
 }
 
+// The phase tile (x6): Cop > 64 on 256x128 (8 waves of 64x64), Cop <= 64 on 64x64 (4 waves of 32x32).  Round 5
+// sweep (profiles/r05e_convT_wgrad_tiles.jsonl, same box): the 256 -> 128 ConvTranspose / stride-2 data
+// gradient 144 -> 124 us at N = 8 (188 -> 167 at N = 12) against 128x128 tiles of 8 x (64x32) waves; the
+// 128 -> 64 one 150 -> 145 us against 128x64.  VST_CONVT_TILE (developer A/B): 0 = the round-4 tiles
+// (128x128 8 waves / 128x64 4 waves), 1 = 256x128 / 128x64, 2 = 128x128 4 waves / 64x64; -1 = the default.
+static const int g_convt_tile = [] {
+  const char* e = getenv("VST_CONVT_TILE");
+  return e ? atoi(e) : -1;
+}();
+
 int bf_convT_phases_launch(const float* x, const void* const ws[4], const float* bias, float* y, int N, int H, int W,
                            int C, int Cop, int act, float slope, int math, hipStream_t s, int full) {
   VST_REQUIRE(bf_convT_phases_ok(C, Cop, math), "convT phases: unsupported shape / arithmetic");
-  const int bm = 128, bn = Cop <= 64 ? 64 : 128;
+  const int bn = Cop <= 64 ? 64 : 128;
+  const int tk = math != VST_MATH_BF16X6 ? 0 : (g_convt_tile >= 0 ? g_convt_tile : (bn == 128 ? 1 : 2));
+  const int bm = (tk == 1 && bn == 128) ? 256 : ((tk == 2 && bn == 64) ? 64 : 128);
   bf::PhaseJobs jobs;
   int t = 0;
   for (int j = 0; j < 4; ++j) {
@@ -1990,18 +2002,29 @@ int bf_convT_phases_launch(const float* x, const void* const ws[4], const float*
     t += (int)((tiles + 7) / 8 * 8);
   }
   jobs.t0[4] = t;
+#define VST_CTB(BM_, BN_, WM_, WN_)                                                                       \
+  {                                                                                                        \
+    using T = bf::Tile<BM_, BN_, WM_, WN_, 32, 3>;                                                         \
+    hipLaunchKernelGGL(bf::conv_convT_phases_k<T>, dim3(t), dim3(T::NT), 0, s, x, jobs, bias, y, N, H, W, C, Cop, \
+                       act, slope, full);                                                                  \
+  }
 #define VST_CT(BN_, WN_, NP_)                                                                             \
   {                                                                                                        \
     using T = bf::Tile<128, BN_, 64, WN_, 32, NP_>;                                                        \
     hipLaunchKernelGGL(bf::conv_convT_phases_k<T>, dim3(t), dim3(T::NT), 0, s, x, jobs, bias, y, N, H, W, C, Cop, \
                        act, slope, full);                                                                  \
   }
-  if (math == VST_MATH_BF16X6) {
+  if (math == VST_MATH_BF16X6 && tk == 1) {
+    if (bn == 64) VST_CT(64, 32, 3) else VST_CTB(256, 128, 64, 64)
+  } else if (math == VST_MATH_BF16X6 && tk == 2) {
+    if (bn == 64) VST_CTB(64, 64, 32, 32) else VST_CTB(128, 128, 64, 64)
+  } else if (math == VST_MATH_BF16X6) {
     if (bn == 64) VST_CT(64, 32, 3) else VST_CT(128, 32, 3)
   } else {
     if (bn == 64) VST_CT(64, 32, 2) else VST_CT(128, 32, 2)
   }
 #undef VST_CT
+#undef VST_CTB
   return check_launch("conv2d_convT_s2");
 }
 

@@ -382,25 +382,55 @@ __global__ void tap_wgrad_scatter_h_k(const float* __restrict__ t, float* __rest
 // the zero-padded channel-major fp32 image [cx][ld] of an Hp x Wp frame (pad rows / columns before, the
 // rest after), the "x" side of the GEMM.  grid (ceil(N Hp Wp / 256)), one thread per frame pixel
 // (coalesced along each channel row).
+// part != null: the block's per-channel sums of g (the bias gradient of the conv, in fp64), folded in
+// thread order: wave butterflies (a fixed tree) then the 4 waves in order -> part[block][4].
 __global__ __launch_bounds__(256) void tap_swap_dy_cp_k(const float4* __restrict__ g, float* __restrict__ xt, int H,
-                                                        int W, int pad, int Hp, int Wp, long P, long ld, int cx) {
+                                                        int W, int pad, int Hp, int Wp, long P, long ld, int cx,
+                                                        double* __restrict__ part) {
   const long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= P) return;
-  const int wp = q % Wp;
-  const long t = q / Wp;
-  const int h = (int)(t % Hp) - pad, w = wp - pad;
-  const long n = t / Hp;
-  const float4 a = ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W) ? g[(n * H + h) * (long)W + w]
-                                                                            : make_float4(0.f, 0.f, 0.f, 0.f);
-  xt[q] = a.x;
-  xt[ld + q] = a.y;
-  xt[2 * ld + q] = a.z;
-  if (cx == 4) xt[3 * ld + q] = a.w;
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (q < P) {
+    const int wp = q % Wp;
+    const long t = q / Wp;
+    const int h = (int)(t % Hp) - pad, w = wp - pad;
+    const long n = t / Hp;
+    if ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W) a = g[(n * H + h) * (long)W + w];
+    xt[q] = a.x;
+    xt[ld + q] = a.y;
+    xt[2 * ld + q] = a.z;
+    if (cx == 4) xt[3 * ld + q] = a.w;
+  }
+  if (!part) return;
+  double v[4] = {a.x, a.y, a.z, a.w};
+  __shared__ double red[4][4];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    v[c] = wave_sum_d(v[c]);
+    if (lane == 0) red[wv][c] = v[c];
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    const int c = threadIdx.x;
+    part[(long)blockIdx.x * 4 + c] = ((red[0][c] + red[1][c]) + red[2][c]) + red[3][c];
+  }
 }
 
-// dw[co][ci][tap] (+)= t[co][ci][RS-1-tap]: the swapped GEMM's taps run rotated by 180 degrees
+// dw[co][ci][tap] (+)= t[co][ci][RS-1-tap]: the swapped GEMM's taps run rotated by 180 degrees.  db != null:
+// the grid's last block folds the tap_swap_dy_cp_k block sums into db[c < Co] (thread c*64 + l sums blocks
+// l, l + 64, ... in order; then the 64 lanes' butterfly, a fixed tree).
 __global__ void tap_wgrad_scatter_flip_k(const float* __restrict__ t, float* __restrict__ dw, int RS, int accumulate,
-                                         long total) {
+                                         long total, const double* __restrict__ part, int nblk,
+                                         float* __restrict__ db, int Co) {
+  if (db && blockIdx.x == gridDim.x - 1) {
+    const int c = threadIdx.x >> 6, l = threadIdx.x & 63;
+    double s = 0.0;
+    if (c < Co)
+      for (int b = l; b < nblk; b += 64) s += part[(long)b * 4 + c];
+    s = wave_sum_d(s);
+    if (c < Co && l == 0) db[c] = accumulate ? db[c] + (float)s : (float)s;
+    return;
+  }
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total) return;
   const int tap = i % RS;
@@ -541,11 +571,24 @@ extern "C" size_t vst_tap_wgrad_swap_ws_bytes(int N, int H, int W, int Ci, int R
   // the GEMM runs over 3 or 4 dy channels (Co <= 3 or not, see vst_tap_wgrad_swap): size for either plan
   const size_t wg = std::max(vst_conv2d_wgrad_ws_bytes(N, H, W + wx, 4, Hf, Wq, Ci, R, R, 1),
                              vst_conv2d_wgrad_ws_bytes(N, H, W + wx, 3, Hf, Wq, Ci, R, R, 1));
-  return (size_t)(4 * ldx + 4 * (long)Ci * R * R) * sizeof(float) + wg;
+  // + the bias gradient's block sums (vst_tap_wgrad_swap_db: ceil(Pp / 256) x 4 doubles, 8-byte aligned)
+  const long Pp = (long)N * (H + 2 * pad) * (W + wx + 2 * pad);
+  return (size_t)(4 * ldx + 4 * (long)Ci * R * R + 2) * sizeof(float) + (size_t)ceil_div(Pp, 256) * 4 * sizeof(double) +
+         wg;
 }
+
+extern "C" int vst_tap_wgrad_swap_db(const float* g, const void* x_planes, float* dw, float* db, float* ws,
+                                     size_t ws_bytes, int N, int H, int W, int Ci, int R, int Co, int accumulate,
+                                     int math, void* stream);
 
 extern "C" int vst_tap_wgrad_swap(const float* g, const void* x_planes, float* dw, float* ws, size_t ws_bytes, int N,
                                   int H, int W, int Ci, int R, int Co, int accumulate, int math, void* stream) {
+  return vst_tap_wgrad_swap_db(g, x_planes, dw, nullptr, ws, ws_bytes, N, H, W, Ci, R, Co, accumulate, math, stream);
+}
+
+extern "C" int vst_tap_wgrad_swap_db(const float* g, const void* x_planes, float* dw, float* db, float* ws,
+                                     size_t ws_bytes, int N, int H, int W, int Ci, int R, int Co, int accumulate,
+                                     int math, void* stream) {
   VST_REQUIRE(g && x_planes && dw && ws && N > 0 && H > 0 && W > 0 && Co > 0 && Co <= 4 && R % 2 == 1 &&
                   Ci % 4 == 0 && (R - 1) / 2 < H && (R - 1) / 2 < W,
               "tap_wgrad_swap: bad args");
@@ -557,21 +600,23 @@ extern "C" int vst_tap_wgrad_swap(const float* g, const void* x_planes, float* d
   hipStream_t s = (hipStream_t)stream;
   float* xt = ws;
   float* t = xt + 4 * ldx;
-  float* wsg = t + 4 * (long)Ci * R * R;
+  const int nblk = ceil_div(Pp, 256);
+  double* bpart = reinterpret_cast<double*>(((uintptr_t)(t + 4 * (long)Ci * R * R) + 7) & ~(uintptr_t)7);
+  float* wsg = reinterpret_cast<float*>(bpart + (long)nblk * 4);
   // Co <= 3: only three dy channels become GEMM rows (M = 3 R^2: 147 rows = 3 tiles of 64 at R = 7, not 4)
   const int cx = Co <= 3 ? 3 : 4;
-  hipLaunchKernelGGL(tap_swap_dy_cp_k, dim3(ceil_div(Pp, 256)), dim3(256), 0, s, reinterpret_cast<const float4*>(g),
-                     xt, H, W, pad, Hp, Wp, Pp, ldx, cx);
+  hipLaunchKernelGGL(tap_swap_dy_cp_k, dim3(nblk), dim3(256), 0, s, reinterpret_cast<const float4*>(g), xt, H, W, pad,
+                     Hp, Wp, Pp, ldx, cx, db ? bpart : nullptr);
   int rc = check_launch("tap_wgrad_swap");
   if (rc) return rc;
   // t[c][ci][tap'] = sum_q dyP[q + tap'][c] * xf[q][ci]  (the frame's "output" channels ci: so = R*R, si = Ci*R*R)
-  const size_t wsb = ws_bytes - (size_t)(wsg - ws) * sizeof(float);
+  const size_t wsb = ws_bytes - (size_t)((char*)wsg - (char*)ws);
   rc = vst_conv2d_wgrad_pre(g, xt, g, x_planes, t, wsg, wsb, N, H, W + wx, cx, Hf, Wq, Ci, R, R, 1, pad, VST_PAD_ZERO,
                             Ci, cx, (long)R * R, (long)Ci * R * R, 0, math, stream);
   if (rc) return rc;
   const long total = (long)Co * Ci * R * R;
-  hipLaunchKernelGGL(tap_wgrad_scatter_flip_k, dim3(ceil_div(total, 256)), dim3(256), 0, s, t, dw, R * R, accumulate,
-                     total);
+  hipLaunchKernelGGL(tap_wgrad_scatter_flip_k, dim3(ceil_div(total, 256) + (db ? 1 : 0)), dim3(256), 0, s, t, dw,
+                     R * R, accumulate, total, bpart, nblk, db, Co);
   return check_launch("tap_wgrad_swap");
 }
 

@@ -702,15 +702,17 @@ class _GeneratorFn(torch.autograd.Function):
         g = ops.act_bwd(gout, out, "tanh")
         if "ftap" in P:
             if train_w:
-                if sv.get("ftap_sw"):
+                db = f.bias.grad if f.bias is not None else None
+                if sv.get("ftap_sw"):  # the bias gradient taken by the GEMM's dy staging pass
                     ops.tap_conv_wgrad_swap(a, g, f.weight.grad, 7, 3, "reflect", accumulate=True,
-                                            x_pl=xts.get(id(a)))
+                                            x_pl=xts.get(id(a)), db=db)
+                    db = None
                 elif sv.get("ftap_h"):
                     ops.tap_conv_wgrad_h(a, g, f.weight.grad, 7, 3, "reflect", accumulate=True, x_t=xts.get(id(a)))
                 else:
                     ops.tap_conv_wgrad(a, g, f.weight.grad, 7, 3, "reflect", accumulate=True, x_t=xts.get(id(a)))
-                if f.bias is not None:
-                    ops.channel_sum(g, f.bias.grad, f.weight.shape[0], accumulate=True)
+                if db is not None:
+                    ops.channel_sum(g, db, f.weight.shape[0], accumulate=True)
         else:
             wgrad(f, a, g, 7, 1, 3, "reflect", db=True)
         done(f)

@@ -1252,7 +1252,7 @@ def tap_conv_wgrad_swap_ok(x, R, pad, pad_mode, role="bwd", co=4):
             conv_plan_wgrad(N, H, W + wx, cx, H + R - 1, Wq, Cx, R, R, 1, role)[0] == 2)
 
 
-def tap_conv_wgrad_swap(x, dy, dw, R, pad, pad_mode="reflect", accumulate=True, role="bwd", x_pl=None):
+def tap_conv_wgrad_swap(x, dy, dw, R, pad, pad_mode="reflect", accumulate=True, role="bwd", x_pl=None, db=None):
     """tap_conv_wgrad with the GEMM's roles swapped (vst_tap_wgrad_swap): M = R*R*3 (tap, co) rows of the
     zero-padded dy against x's reflect-padded frame as Cx columns.  x_pl: that frame's bf16 planes as the
     IN apply writes them (instnorm_act_fwd(xpl=(pad, "reflect", wx))); None: made here from x."""
@@ -1273,7 +1273,8 @@ def tap_conv_wgrad_swap(x, dy, dw, R, pad, pad_mode="reflect", accumulate=True, 
         raise ValueError("tap_conv_wgrad_swap: x planes %s do not match (3, %d, %d) bf16" % (tuple(x_pl.shape), Cx, ld))
     nbytes = lib().vst_tap_wgrad_swap_ws_bytes(N, H, W, Cx, R)
     ws = torch.empty((nbytes + 3) // 4, device=x.device)
-    _call("vst_tap_wgrad_swap", _p(dy), _p(x_pl), _p(dw), _p(ws), nbytes, N, H, W, Cx, R, Co,
+    # db: the bias gradient (+)= the channel sums of dy, taken by the same pass (vst_tap_wgrad_swap_db)
+    _call("vst_tap_wgrad_swap_db", _p(dy), _p(x_pl), _p(dw), _p(db), _p(ws), nbytes, N, H, W, Cx, R, Co,
           1 if accumulate else 0, _math(role), _stream())
 
 

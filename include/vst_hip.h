@@ -527,6 +527,11 @@ int vst_tap_wgrad_scatter_h(const float* t, float* dw, int Co, int Ci, int R, in
  * dw (+)= the result with its taps rotated 180 degrees.  ws: vst_tap_wgrad_swap_ws_bytes. */
 int vst_tap_wgrad_swap(const float* g, const void* x_planes, float* dw, float* ws, size_t ws_bytes, int N, int H,
                        int W, int Ci, int R, int Co, int accumulate, int math, void* stream);
+/* vst_tap_wgrad_swap plus the conv's bias gradient db[c] (+)= sum_pix g[pix][c] (c < Co; db may be NULL):
+ * block sums taken by the pass that stages g for the GEMM, folded in a fixed order (fp64) by the last
+ * block of the tap scatter — no separate channel-sum launches (networks.py:365-366's bias). */
+int vst_tap_wgrad_swap_db(const float* g, const void* x_planes, float* dw, float* db, float* ws, size_t ws_bytes, int N,
+                          int H, int W, int Ci, int R, int Co, int accumulate, int math, void* stream);
 size_t vst_tap_wgrad_swap_ws_bytes(int N, int H, int W, int Ci, int R);
 /* Plane stride of x_planes: vst_cp_ld(N (H+R-1) (W+R-1+wx)). */
 long vst_tap_wgrad_swap_ld(int N, int H, int W, int R);

@@ -400,8 +400,10 @@ def test_tap_conv_wgrad_swap(ops, N, ci, H, W, k, xpl, co):
             a, x_pl = ops.instnorm_act_fwd(xn, st, "none", xpl=(pad, "reflect", ops.tap_swap_geom(W, k)[0]))
             assert torch.equal(a, xn)
         dw = torch.full((co, ci, k, k), 0.25, device=DEV)
-        ops.tap_conv_wgrad_swap(xn, g, dw, k, pad, "reflect", accumulate=True, x_pl=x_pl)
+        db = torch.full((co,), 0.5, device=DEV)  # the bias gradient from the same pass (vst_tap_wgrad_swap_db)
+        ops.tap_conv_wgrad_swap(xn, g, dw, k, pad, "reflect", accumulate=True, x_pl=x_pl, db=db)
         _close(dw.cpu() - 0.25, w.grad, tol=CONV_TOL["bf16x6"], what="tap wgrad (swapped form)")
+        _close(db.cpu() - 0.5, gy.sum(dim=(0, 2, 3)), tol=1e-5, what="bias gradient (swapped form)")
         if co == 3 and ops.tap_conv_wgrad_h_ok(xn, k, pad, "reflect"):
             dwh = torch.zeros((co, ci, k, k), device=DEV)
             ops.tap_conv_wgrad_h(xn, g, dwh, k, pad, "reflect", accumulate=False)

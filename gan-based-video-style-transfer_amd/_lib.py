@@ -173,6 +173,10 @@ SIGNATURES = {
     "vst_conv2d_dgrad_refl": (I, [P, P, P, P, P, SZ, I, I, I, I, I, I, P]),
     "vst_conv2d_dgrad_refl_in_ws_bytes": (SZ, [I, I, I, I, I, I]),
     "vst_conv2d_dgrad_refl_in": (I, [P, P, P, P, P, P, P, P, P, SZ, I, I, I, I, I, I, F, I, P, L, I, P]),
+    "vst_conv2d_dgrad_refl_in_epi_ws_bytes": (SZ, [I, I, I, I, I, I]),
+    "vst_conv2d_dgrad_refl_in_epi": (I, [P, P, P, P, P, P, P, P, P, SZ, I, I, I, I, I, I, F, I, P, L, I, P]),
+    "vst_conv2d_dgrad_refl_epi_part": (I, [P, P, P, P, P, P, P, SZ, I, I, I, I, I, I, F, I, P]),
+    "vst_instnorm_act_bwd_epi_tail": (I, [P, P, P, P, P, P, I, I, I, I, I, F, I, P, L, P]),
     "vst_conv2d_dgrad_refl_slabs": (I, [P, P, P, P, P, SZ, I, I, I, I, I, I, P]),
     "vst_instnorm_act_bwd_refl_border": (I, [P, P, P, P, P, P, P, I, I, I, I, I, I, F, I, P, L, I, P]),
     # SURVEY §8b spelling (abi.hip)

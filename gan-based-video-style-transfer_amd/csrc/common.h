@@ -169,6 +169,13 @@ size_t bf_dgrad_refl1_ws_floats(int N, int H, int W, int Cy, int Cx, int math);
 size_t bf_dgrad_refl1_slabs(int N, int H, int W, int Cy, int Cx, int math, BorderSlabs* b);
 int bf_dgrad_refl1_launch(const float* dy, const void* wsplit, long wps, const float* addend, float* dx, int N, int H,
                           int W, int Cy, int Cx, int math, hipStream_t s, float* ws, size_t ws_floats, bool add_border);
+// ... with the IN-backward partials of the layer below taken by the interior GEMM's epilogue and the border
+// add (vst_conv2d_dgrad_refl_in_epi): part [N][bf_dgrad_refl1_inb_slices][Cx][3] fp64
+bool bf_dgrad_refl1_inb_ok(int N, int H, int W, int Cy, int Cx, int math);
+int bf_dgrad_refl1_inb_slices(int H, int W);
+int bf_dgrad_refl1_inb_launch(const float* dy, const void* wsplit, long wps, const float* addend, float* dx, int N,
+                              int H, int W, int Cy, int Cx, int math, hipStream_t s, float* ws, size_t ws_floats,
+                              const float* z, const float* st, double* part, int act, float slope);
 size_t bf_fprop_ws_floats(long M, int Cop, int C, int R, int S, int math);
 int bf_tail_ks(long M, int Cop, int m_split, int nk);
 void bf_split_plan(long M, int Cop, int C, int R, int S, int math, int kind, int* m_first, int* ks_out);

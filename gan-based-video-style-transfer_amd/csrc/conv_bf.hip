@@ -541,6 +541,31 @@ __device__ __forceinline__ void tile_of(int L, int Mt, int Nt, int& mt, int& nt)
   nt = t - mt * Nt;
 }
 
+// The InstanceNorm(+act) backward partials of the layer below a data gradient, taken by the GEMM's
+// epilogue (vst_conv2d_dgrad_refl_in_epi): the stored output g (+ addend) is the IN output's gradient;
+// z = the IN input [M][Cop] NHWC, st = its statistics [N][Cop][2] (mean, rstd); per 32-row group of an
+// image (slice zg = group index) and channel the fp64 sums {sum g', sum g' xh, sum xh} (xh = (z - mean)
+// rstd, g' = g act'(xh)) go to part[n][zg][Cop][3] — in_partial_k<1>'s per-element arithmetic, ns
+// slices per image (the groups, then the border-correction slices of dgrad_border5_add_inb_k).
+struct InbArgs {
+  const float* z;
+  const float* st;
+  double* part;
+  int act;
+  float slope;
+  int ns;
+};
+
+// g' = g act'(xh) of element (g, z) under (mean, rstd): in_partial_k<1>'s expression
+__device__ __forceinline__ void inb_term(float g, float z, float mean, float rstd, int act, float slope, float& gd,
+                                         float& xh) {
+  xh = (z - mean) * rstd;
+  float d = 1.f;
+  if (act == VST_ACT_RELU) d = xh > 0.f ? 1.f : 0.f;
+  else if (act == VST_ACT_LRELU) d = xh > 0.f ? 1.f : slope;
+  gd = g * d;
+}
+
 // ---------------------------------------------------------- reflect-pad-1 data gradient border
 // The data gradient of ReflectionPad2d(1) + 3x3 conv (stride 1) on an H x W map is
 //   dx(j) = sum over padded positions q with r(q) = j of dxp(q),   r(-1) = 1, r(H) = H - 2,
@@ -686,6 +711,90 @@ __global__ __launch_bounds__(256) void dgrad_border5_add_k(const float* __restri
   *d = o;
 }
 
+// dgrad_border5_add_k with the IN-backward partials' border correction (vst_conv2d_dgrad_refl_in_epi): the
+// interior GEMM's epilogue summed g' of the pre-border g over every pixel (InbArgs), so a target whose
+// g moves from g0 to g1 = g0 + its slab sum adds (g1' - g0') and (g1' - g0') xh (fp64, from the fp32 g'
+// products) to the partials.  grid (ceil(T / 16), N, ceil(C / 64)), T = 2W + 2H targets per image: a block
+// takes 16 targets of one image; its 16 target-threads' sums fold through LDS in a fixed order into
+// slice first_slice + blockIdx.x of part (sum xh gets 0: the border add leaves z alone).
+__device__ __forceinline__ void border5_target(int b, int W, int H, int& th, int& tw, bool& live) {
+  live = true;
+  if (b < 2 * W) {
+    th = b < W ? 1 : H - 2;
+    tw = b < W ? b : b - W;
+  } else {
+    const int b2 = b - 2 * W;
+    th = b2 < H ? b2 : b2 - H;
+    tw = b2 < H ? 1 : W - 2;
+    if (th == 1 || th == H - 2) live = false;  // a row target
+  }
+}
+
+__global__ __launch_bounds__(256) void dgrad_border5_add_inb_k(const float* __restrict__ slab, int ks, int Mb, int C,
+                                                               float* __restrict__ dx, int H, int W, int Lt, int Ll,
+                                                               InbArgs inb, int first_slice) {
+  __shared__ double red[2][16][65];
+  const int t = threadIdx.x, c4 = (t & 15) * 4, sub = t >> 4;
+  const int c = blockIdx.z * 64 + c4, n = blockIdx.y;
+  const int T = 2 * W + 2 * H;
+  const int b = blockIdx.x * 16 + sub;
+  double a0[4] = {0, 0, 0, 0}, a1[4] = {0, 0, 0, 0};
+  int th = 0, tw = 0;
+  bool live = false;
+  if (b < T && c < C) border5_target(b, W, H, th, tw, live);
+  if (live) {
+    int rows[3];
+    const int nr = dgrad_border_slab_rows(n, th, tw, H, W, Lt, Ll, rows);
+    const long zst = (long)Mb * C;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int r = 0; r < nr; ++r) {
+      const float* base = slab + (long)rows[r] * C + c;
+      float4 u[16];
+#pragma unroll
+      for (int z = 0; z < 16; ++z)
+        if (z < ks) u[z] = *reinterpret_cast<const float4*>(base + z * zst);
+      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int z = 0; z < 16; ++z)
+        if (z < ks) add_f4(acc, u[z]);
+      add_f4(v, acc);
+    }
+    const long e = (((long)n * H + th) * W + tw) * C + c;
+    float4* d = reinterpret_cast<float4*>(dx + e);
+    const float4 o0 = *d;
+    float4 o = o0;
+    add_f4(o, v);
+    *d = o;
+    const float4 zz = *reinterpret_cast<const float4*>(inb.z + e);
+    const float4 s0 = reinterpret_cast<const float4*>(inb.st)[((long)n * C + c) / 2];
+    const float4 s1 = reinterpret_cast<const float4*>(inb.st)[((long)n * C + c) / 2 + 1];
+    const float mu[4] = {s0.x, s0.z, s1.x, s1.z}, rs[4] = {s0.y, s0.w, s1.y, s1.w};
+    const float g0[4] = {o0.x, o0.y, o0.z, o0.w}, g1[4] = {o.x, o.y, o.z, o.w}, zv[4] = {zz.x, zz.y, zz.z, zz.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float d0, d1, xh;
+      inb_term(g0[k], zv[k], mu[k], rs[k], inb.act, inb.slope, d0, xh);
+      inb_term(g1[k], zv[k], mu[k], rs[k], inb.act, inb.slope, d1, xh);
+      a0[k] = (double)d1 - (double)d0;
+      a1[k] = (double)d1 * xh - (double)d0 * xh;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    red[0][sub][c4 + k] = a0[k];
+    red[1][sub][c4 + k] = a1[k];
+  }
+  __syncthreads();
+  if (t < 192) {
+    const int v = t >> 6, cc = t & 63, nn = blockIdx.z * 64 + cc;
+    if (nn >= C) return;
+    double acc = 0.0;
+    if (v < 2)
+      for (int q = 0; q < 16; ++q) acc += red[v][q][cc];
+    inb.part[(((long)n * inb.ns + first_slice + blockIdx.x) * C + nn) * 3 + v] = acc;
+  }
+}
+
 // ------------------------------------------------------------------------ ConvTranspose phases
 // Stride-2 ConvTranspose2d(k3, p1, op1) as four phase convs (vst_interleave_phases): phase (a, b) =
 // oph - 1 = 2a + b is an (H+a) x (W+b) conv whose pixel (ph, pw) is output pixel (2(ph-a)+a,
@@ -744,7 +853,7 @@ __device__ __forceinline__ void conv_fprop_bf_body(
     int padw, int reflect, int act, float slope, int M, int Ktot, int m_base, double* __restrict__ part,
     int spk, float* __restrict__ slab, const float* __restrict__ addend, int oph,
     const float* __restrict__ nst = nullptr, const float* __restrict__ bslab = nullptr, int bks = 0, int bmb = 0,
-    int blt = 0, int bll = 0) {
+    int blt = 0, int bll = 0, InbArgs inb = InbArgs{}) {
   static_assert(!SPLIT || KSL, "split-K needs the channel-slice-major K walk");
   static_assert(!NRM || (KSL && REFL == 1), "normalised A: the channel-slice K walk, reflect padding");
   static_assert(REFL < 4 || (SPLIT && KSL), "border rows run as split-K slabs");
@@ -1009,7 +1118,7 @@ __device__ __forceinline__ void conv_fprop_bf_body(
     // (an addend — the residual gradient of a data gradient — is always added on this path: its float4
     // loads ride with the row stores instead of 4-byte reads per accumulator element)
     constexpr bool LFIT = T::BM * (T::BN + 16) * 4 <= 2 * T::STAGE;
-    const bool LEPI = LFIT && (VST_BF_LDS_EPI || addend != nullptr || oph != 0 || bslab != nullptr);
+    const bool LEPI = LFIT && (VST_BF_LDS_EPI || addend != nullptr || oph != 0 || bslab != nullptr || inb.part != nullptr);
     constexpr int LDE = T::BN + 16;
     float* ept = reinterpret_cast<float*>(smem);
     if (LEPI) __syncthreads();  // every wave is done reading the last stage
@@ -1052,6 +1161,65 @@ __device__ __forceinline__ void conv_fprop_bf_body(
     if (LEPI) {
       __syncthreads();
       constexpr int C4 = T::BN / 4;
+      if constexpr (LFIT && 64 % C4 == 0 && T::BM % 32 == 0 && C4 >= 4) {
+        if (inb.part) {
+          // IN-backward partials (InbArgs): wave w stores the 32-row groups w, w + NW, ...; lane l owns
+          // channels 4 (l % C4) .. + 3 and rows l / C4 + RW k of the group (whole 4*C4-float rows per
+          // instruction, as the loop below); per-lane fixed-order fp64 sums, then xor over the RW lanes
+          // of a channel group.  Every group lies in one image (HW % 32 == 0, checked by the launcher).
+          constexpr int RW = 64 / C4;
+          const int c = 4 * (lane % C4), n = n0 + c, hw = Ho * Wo;
+          for (int G = wave; G < T::BM / 32; G += T::NW) {
+            const int gm0 = m0 + 32 * G;
+            if (gm0 >= M) break;
+            const int img = gm0 / hw;
+            float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0;
+            if (n < Cop) {
+              s0 = reinterpret_cast<const float4*>(inb.st)[((long)img * Cop + n) / 2];
+              s1 = reinterpret_cast<const float4*>(inb.st)[((long)img * Cop + n) / 2 + 1];
+            }
+            const float mu[4] = {s0.x, s0.z, s1.x, s1.z}, rs[4] = {s0.y, s0.w, s1.y, s1.w};
+            double a0[4] = {0, 0, 0, 0}, a1[4] = {0, 0, 0, 0}, a2[4] = {0, 0, 0, 0};
+#pragma unroll 4
+            for (int k = 0; k < 32 / RW; ++k) {
+              const int row = 32 * G + lane / C4 + RW * k, mm = m0 + row;
+              if (n < Cop && mm < M) {
+                float4 v = *reinterpret_cast<const float4*>(ept + row * LDE + c);
+                if (addend) add_f4(v, *reinterpret_cast<const float4*>(addend + (long)mm * Cop + n));
+                *reinterpret_cast<float4*>(y + (long)mm * Cop + n) = v;
+                const float4 zz = *reinterpret_cast<const float4*>(inb.z + (long)mm * Cop + n);
+                const float gv[4] = {v.x, v.y, v.z, v.w}, zv[4] = {zz.x, zz.y, zz.z, zz.w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                  float gd, xh;
+                  inb_term(gv[e], zv[e], mu[e], rs[e], inb.act, inb.slope, gd, xh);
+                  a0[e] += gd;
+                  a1[e] += (double)gd * xh;
+                  a2[e] += xh;
+                }
+              }
+            }
+#pragma unroll
+            for (int off = C4; off < 64; off <<= 1)
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                a0[e] += __shfl_xor(a0[e], off);
+                a1[e] += __shfl_xor(a1[e], off);
+                a2[e] += __shfl_xor(a2[e], off);
+              }
+            if (lane < C4 && n < Cop) {
+              double* d = inb.part + (((long)img * inb.ns + ((gm0 - img * hw) >> 5)) * Cop + n) * 3;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                d[3 * e] = a0[e];
+                d[3 * e + 1] = a1[e];
+                d[3 * e + 2] = a2[e];
+              }
+            }
+          }
+          return;
+        }
+      }
 #pragma unroll 4
       for (int idx = t; idx < T::BM * C4; idx += T::NT) {
         const int row = idx / C4, c = 4 * (idx - row * C4);
@@ -1156,6 +1324,17 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_bord_k(
   conv_fprop_bf_body<T, true, 0, false>(blockIdx.x, x, ws, wps, nullptr, y, H, W, C, H, W, Cop, 3, 1, 1, 1, 0,
                                         VST_ACT_NONE, 0.f, M, Ktot, 0, nullptr, 0, nullptr, addend, 0, nullptr, bslab,
                                         bks, bmb, blt, bll);
+}
+
+// The interior conv of the reflect-pad-1 data gradient (+ addend) with the IN-backward partials of the
+// layer below in its epilogue (InbArgs); M = the rows of this launch (whole 256x128 rounds).
+template <class T>
+__global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_inb_k(
+    const float* __restrict__ x, const __bf16* __restrict__ ws, long wps, float* __restrict__ y, int H, int W, int C,
+    int Cop, const float* __restrict__ addend, int M, int Ktot, InbArgs inb) {
+  conv_fprop_bf_body<T, true, 0, false>(blockIdx.x, x, ws, wps, nullptr, y, H, W, C, H, W, Cop, 3, 1, 1, 1, 0,
+                                        VST_ACT_NONE, 0.f, M, Ktot, 0, nullptr, 0, nullptr, addend, 0, nullptr, nullptr,
+                                        0, 0, 0, 0, inb);
 }
 
 // conv_fprop_bf_k over relu(IN(x)) (NRM: the normalisation in the A staging; nst = x's IN statistics)
@@ -1377,6 +1556,59 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_wgrad_bf_k(
         if (mm < Mw) sl[(long)mm * Cyp + n] = acc[i][j][r];
       }
     }
+}
+
+// fprop_splitk_reduce_k of a data gradient's split-K tail (no bias / act) with the IN-backward partials
+// of the layer below (InbArgs, one 32-row group per block: slice (m - image start) / 32); same block
+// geometry, the 16 row-threads' fp64 sums folded through LDS in a fixed order.
+__global__ __launch_bounds__(256) void fprop_splitk_reduce_inb_k(const float* __restrict__ slab, int ks, int m_base,
+                                                                 int M, int Cop, float* __restrict__ y, int hw,
+                                                                 const float* __restrict__ addend, InbArgs inb) {
+  __shared__ double red[3][16][65];
+  const int t = threadIdx.x, c4 = (t & 15) * 4, sub = t >> 4;
+  const int n = blockIdx.y * 64 + c4;
+  const long rows = M - m_base, zst = rows * Cop;
+  const int r0 = blockIdx.x * 32;
+  const int g0 = m_base + r0, img = g0 / hw;
+  double a0[4] = {0, 0, 0, 0}, a1[4] = {0, 0, 0, 0}, a2[4] = {0, 0, 0, 0};
+  if (n < Cop) {
+    const float4 s0 = reinterpret_cast<const float4*>(inb.st)[((long)img * Cop + n) / 2];
+    const float4 s1 = reinterpret_cast<const float4*>(inb.st)[((long)img * Cop + n) / 2 + 1];
+    const float mu[4] = {s0.x, s0.z, s1.x, s1.z}, rs[4] = {s0.y, s0.w, s1.y, s1.w};
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const long r = r0 + sub + 16 * h;
+      if (r >= rows) break;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int z = 0; z < ks; ++z) add_f4(v, *reinterpret_cast<const float4*>(slab + z * zst + r * Cop + n));
+      if (addend) add_f4(v, *reinterpret_cast<const float4*>(addend + (m_base + r) * Cop + n));
+      *reinterpret_cast<float4*>(y + (m_base + r) * Cop + n) = v;
+      const float4 zz = *reinterpret_cast<const float4*>(inb.z + (m_base + r) * Cop + n);
+      const float gv[4] = {v.x, v.y, v.z, v.w}, zv[4] = {zz.x, zz.y, zz.z, zz.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float gd, xh;
+        inb_term(gv[e], zv[e], mu[e], rs[e], inb.act, inb.slope, gd, xh);
+        a0[e] += gd;
+        a1[e] += (double)gd * xh;
+        a2[e] += xh;
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    red[0][sub][c4 + e] = a0[e];
+    red[1][sub][c4 + e] = a1[e];
+    red[2][sub][c4 + e] = a2[e];
+  }
+  __syncthreads();
+  if (t < 192) {
+    const int v = t >> 6, c = t & 63, nn = blockIdx.y * 64 + c;
+    if (nn >= Cop) return;
+    double acc = 0.0;
+    for (int q = 0; q < 16; ++q) acc += red[v][q][c];
+    inb.part[(((long)img * inb.ns + ((g0 - img * hw) >> 5)) * Cop + nn) * 3 + v] = acc;
+  }
 }
 
 // Split-K tail: y[m][n] = act(sum_z slab[z][m - m_base][n] + bias[n]) (splits summed in order) and,
@@ -1715,6 +1947,11 @@ bool bf_fprop_nrm_ok(int N, int H, int W, int C, int Cop, int R, int S, int st, 
   return (kd == 7 && (!m_split || ks)) || (ks && !m_first);
 }
 
+static const int g_fs_tile = [] {  // developer A/B of the all-split-K tile (bf_fprop_launch)
+  const char* e = getenv("VST_FULLSPLIT_TILE");
+  return e ? atoi(e) : 0;
+}();
+
 int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* bias, float* y, int N,
                     int H, int W, int C, int Ho, int Wo, int Cop, int R, int S, int st, int padh, int padw,
                     int reflect, int act, float slope, int math, int kind, hipStream_t s, double* part,
@@ -1771,6 +2008,27 @@ int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* b
   for (int ph = (ks && !m_first) ? 1 : 0; ph < ((m_split || (ks && !m_first)) ? 2 : 1); ++ph) {
     const int mb = ph ? m_split : 0, Mend = (m_split && !ph) ? m_split : M;
     const int kp = ph ? tail_kind : kd;
+    if (ph == 1 && ks && !m_first && !nst && g_fs_tile == 128) {
+      // developer A/B (VST_FULLSPLIT_TILE=128): the all-split-K form on 128x128 tiles (4 waves of 64x64),
+      // as many K-splits as fill the CUs within the 256x128 plan's slab workspace
+      using T = bf::Tile<128, 128, 64, 64, 32, 3>;
+      const long tiles = ceil_div(M, 128) * ceil_div(Cop, 128);
+      const int nk = (K + T::BK - 1) / T::BK;
+      int ks2 = (int)(VST_NUM_CUS / tiles);
+      ks2 = ks2 < 1 ? 1 : (ks2 > 32 ? 32 : ks2);
+      while (ks2 > 1 && ((size_t)ks2 * M * Cop > tws_floats || (ks2 - 1) * ((nk + ks2 - 1) / ks2) >= nk)) --ks2;
+      const int spk = (nk + ks2 - 1) / ks2;
+      const dim3 grid(tiles * ks2);
+      if (reflect)
+        hipLaunchKernelGGL((bf::conv_fprop_bf_k<T, true, 1, true>), grid, dim3(T::NT), 0, s, x, ws, wps, bias, y, H, W,
+                           C, Ho, Wo, Cop, S, st, padh, padw, reflect, act, slope, M, K, 0, part, spk, tws, nullptr);
+      else
+        hipLaunchKernelGGL((bf::conv_fprop_bf_k<T, true, 0, true>), grid, dim3(T::NT), 0, s, x, ws, wps, bias, y, H, W,
+                           C, Ho, Wo, Cop, S, st, padh, padw, reflect, act, slope, M, K, 0, part, spk, tws, nullptr);
+      hipLaunchKernelGGL(bf::fprop_splitk_reduce_k, dim3(ceil_div(M, 32), ceil_div(Cop, 64)), dim3(256), 0, s, tws, ks2,
+                         0, M, Cop, bias, act, slope, y, part, Ho * Wo, addend);
+      continue;
+    }
     if (ph == 1 && ks) {
       using T = bf::Tile<256, 128, 64, 64, 32, 3>;
       const int nk = (K + T::BK - 1) / T::BK, spk = (nk + ks - 1) / ks;
@@ -1966,6 +2224,66 @@ int bf_dgrad_refl1_launch(const float* dy, const void* wsplit, long wps, const f
     hipLaunchKernelGGL(bf::dgrad_border_add_k, dim3(ceil_div(Mb, 16), ceil_div(Cx, 64)), dim3(256), 0, s, slab, ks,
                        (int)Mb, Cx, dx, H, W, NB);
   return check_launch("conv2d_dgrad_refl");
+}
+
+// vst_conv2d_dgrad_refl_in_epi's data-gradient half: the interior conv (whole 256x128 x6 rounds; a split-K
+// tail, or the all-split form, through fprop_splitk_reduce_inb_k) with the IN-backward partials of the layer
+// below in its epilogue (InbArgs), the K-restricted border GEMM, and dgrad_border5_add_inb_k (the border add
+// + the partials' correction slices).  part = [N][ns][Cx][3], ns = bf_dgrad_refl1_inb_slices: the H W / 32
+// row groups, then ceil((2W + 2H) / 16) border slices.
+int bf_dgrad_refl1_inb_slices(int H, int W) { return H * W / 32 + (2 * W + 2 * H + 15) / 16; }
+
+bool bf_dgrad_refl1_inb_ok(int N, int H, int W, int Cy, int Cx, int math) {
+  if (math != VST_MATH_BF16X6 || !g_border5 || !bf_dgrad_refl1_ok(N, H, W, Cy, Cx, math) || (H * W) % 32) return false;
+  int kd, m_split, tail_kind, m_first, fks;
+  const long M = (long)N * H * W;
+  if (M > (1L << 30)) return false;
+  bf_plan(M, Cx, math, -1, &kd, &m_split, &tail_kind);
+  bf_split_plan(M, Cx, Cy, 3, 3, math, -1, &m_first, &fks);
+  if (fks && !m_first) return true;  // the whole conv as split-K 256x128 tiles
+  return kd == 7 && (!m_split || (fks && m_first == m_split));
+}
+
+int bf_dgrad_refl1_inb_launch(const float* dy, const void* wsplit, long wps, const float* addend, float* dx, int N,
+                              int H, int W, int Cy, int Cx, int math, hipStream_t s, float* ws, size_t ws_floats,
+                              const float* z, const float* st, double* part, int act, float slope) {
+  VST_REQUIRE(bf_dgrad_refl1_inb_ok(N, H, W, Cy, Cx, math), "conv2d_dgrad_refl_in_epi: unsupported shape / arithmetic");
+  const long M = (long)N * H * W;
+  int kd, m_split, tail_kind, m_first, fks;
+  bf_plan(M, Cx, math, -1, &kd, &m_split, &tail_kind);
+  bf_split_plan(M, Cx, Cy, 3, 3, math, -1, &m_first, &fks);
+  const size_t main_ws = bf_fprop_ws_floats(M, Cx, Cy, 3, 3, math);
+  int ks5, lt, ll;
+  bf_border5_plan(N, H, W, Cy, Cx, &ks5, &lt, &ll);
+  const int Mt = 2 * lt + 2 * ll, K5 = 3 * Cy, K = 9 * Cy;
+  VST_REQUIRE(ws_floats >= main_ws + (size_t)ks5 * Mt * Cx, "conv2d_dgrad_refl_in_epi: workspace too small");
+  const bf::InbArgs inb{z, st, part, act, slope, bf_dgrad_refl1_inb_slices(H, W)};
+  const __bf16* wb = reinterpret_cast<const __bf16*>(wsplit);
+  using T = bf::Tile<256, 128, 64, 64, 32, 3>;
+  // rows [0, mb): whole rounds with the partials in the epilogue; [mb, M): split-K + the reducing pass
+  const long mb = (fks && !m_first) ? 0 : (m_split ? m_split : M);
+  if (mb > 0)
+    hipLaunchKernelGGL((bf::conv_fprop_bf_inb_k<T>), dim3(ceil_div(mb, 256) * ceil_div(Cx, 128)), dim3(T::NT), 0, s, dy,
+                       wb, wps, dx, H, W, Cy, Cx, addend, (int)mb, K, inb);
+  if (mb < M) {
+    const int nk = (K + T::BK - 1) / T::BK, spk = (nk + fks - 1) / fks;
+    hipLaunchKernelGGL((bf::conv_fprop_bf_k<T, true, 0, true>), dim3(ceil_div(M - mb, 256) * ceil_div(Cx, 128) * fks),
+                       dim3(T::NT), 0, s, dy, wb, wps, nullptr, dx, H, W, Cy, H, W, Cx, 3, 1, 1, 1, 0, VST_ACT_NONE, 0.f,
+                       (int)M, K, (int)mb, nullptr, spk, ws, nullptr);
+    hipLaunchKernelGGL(bf::fprop_splitk_reduce_inb_k, dim3(ceil_div(M - mb, 32), ceil_div(Cx, 64)), dim3(256), 0, s, ws,
+                       fks, (int)mb, (int)M, Cx, dx, H * W, addend, inb);
+  }
+  float* slab = ws + main_ws;
+  {
+    using T5 = bf::Tile<128, 128, 64, 32, 32, 3>;
+    const int nk = (K5 + T5::BK - 1) / T5::BK, spk = (nk + ks5 - 1) / ks5;
+    hipLaunchKernelGGL((bf::conv_fprop_bf_k<T5, true, 5, true>), dim3(Mt / 128 * ceil_div(Cx, 128) * ks5), dim3(T5::NT),
+                       0, s, dy, wb, wps, nullptr, dx, H, W, Cy, lt, ll, Cx, 3, N, 1, 1, 0, VST_ACT_NONE, 0.f, Mt, K5, 0,
+                       nullptr, spk, slab, nullptr);
+  }
+  hipLaunchKernelGGL(bf::dgrad_border5_add_inb_k, dim3(ceil_div(2 * W + 2 * H, 16), N, ceil_div(Cx, 64)), dim3(256), 0,
+                     s, slab, ks5, Mt, Cx, dx, H, W, lt, ll, inb, H * W / 32);
+  return check_launch("conv2d_dgrad_refl_in_epi");
 }
 
 // The four phases of a stride-2 ConvTranspose2d(k3, p1, op1) forward as one conv_convT_phases_k launch

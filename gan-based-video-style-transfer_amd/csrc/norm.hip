@@ -1128,6 +1128,60 @@ extern "C" int vst_conv2d_dgrad_refl_in(const float* dy, const void* wsplit, con
                                           accumulate_db, planes, ldp, math, stream);
 }
 
+// vst_conv2d_dgrad_refl_in with the IN-backward partials taken by the data gradient itself: the interior
+// GEMM's epilogue (per 32-row group) and the border add (its correction slices) write them, so the
+// partial pass (a read of g and z and a launch) is gone; then the same finalize / apply.  Workspace: the
+// IN partials [N][ns][C][3] + coefficients, then the data gradient's.  x6 arithmetic, H W % 32 == 0.
+static size_t in_epi_ws_bytes_al(int N, int H, int W, int C) {
+  const size_t ns = bf_dgrad_refl1_inb_slices(H, W);
+  return ((size_t)N * ns * C * 3 * sizeof(double) + (size_t)N * C * (sizeof(float2) + sizeof(double)) + 256 + 255) /
+         256 * 256;
+}
+
+extern "C" size_t vst_conv2d_dgrad_refl_in_epi_ws_bytes(int N, int H, int W, int Cy, int Cx, int math) {
+  if (Cx % 4 || !bf_dgrad_refl1_inb_ok(N, H, W, Cy, Cx, math)) return 0;
+  return in_epi_ws_bytes_al(N, H, W, Cx) + bf_dgrad_refl1_ws_floats(N, H, W, Cy, Cx, math) * sizeof(float);
+}
+
+// the two halves (the data gradient can then be timed on its own): the data gradient + partials, the tail
+extern "C" int vst_conv2d_dgrad_refl_epi_part(const float* dy, const void* wsplit, const float* addend, float* gout,
+                                              const float* x, const float* stats, float* ws, size_t ws_bytes, int N,
+                                              int H, int W, int Cy, int Cx, int act, float slope, int math,
+                                              void* stream) {
+  const size_t need = vst_conv2d_dgrad_refl_in_epi_ws_bytes(N, H, W, Cy, Cx, math);
+  VST_REQUIRE(dy && wsplit && gout && x && stats && ws, "conv2d_dgrad_refl_in_epi: null pointer");
+  VST_REQUIRE(need > 0 && ws_bytes >= need,
+              "conv2d_dgrad_refl_in_epi: unsupported shape or workspace too small (%zu of %zu bytes)", ws_bytes, need);
+  const size_t inb = in_epi_ws_bytes_al(N, H, W, Cx);
+  float* dws = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + inb);
+  return bf_dgrad_refl1_inb_launch(dy, wsplit, (long)Cx * 9 * Cy, addend, gout, N, H, W, Cy, Cx, math,
+                                   (hipStream_t)stream, dws, (ws_bytes - inb) / sizeof(float), x, stats,
+                                   reinterpret_cast<double*>(ws), act, slope);
+}
+
+extern "C" int vst_instnorm_act_bwd_epi_tail(const float* gout, const float* x, const float* stats, float* dx,
+                                             float* db, float* ws, int N, int H, int W, int Cx, int act, float slope,
+                                             int accumulate_db, void* planes, long ldp, void* stream) {
+  VST_REQUIRE(gout && x && stats && dx && ws && Cx % 4 == 0 && (H * W) % 32 == 0, "instnorm_act_bwd_epi_tail: bad args");
+  VST_REQUIRE(!planes || ldp >= (long)N * H * W, "instnorm_act_bwd_epi_tail: plane stride %ld < N*HW", ldp);
+  RedGeom g{};
+  g.nsplit = bf_dgrad_refl1_inb_slices(H, W);
+  return in_bwd_tail(gout, x, stats, dx, db, ws, N, H * W, Cx, act, slope, accumulate_db, planes, ldp, g,
+                     (hipStream_t)stream);
+}
+
+extern "C" int vst_conv2d_dgrad_refl_in_epi(const float* dy, const void* wsplit, const float* addend, float* gout,
+                                            const float* x, const float* stats, float* dx, float* db, float* ws,
+                                            size_t ws_bytes, int N, int H, int W, int Cy, int Cx, int act, float slope,
+                                            int accumulate_db, void* planes, long ldp, int math, void* stream) {
+  VST_REQUIRE(dx, "conv2d_dgrad_refl_in_epi: null pointer");
+  if (int e = vst_conv2d_dgrad_refl_epi_part(dy, wsplit, addend, gout, x, stats, ws, ws_bytes, N, H, W, Cy, Cx, act,
+                                             slope, math, stream))
+    return e;
+  return vst_instnorm_act_bwd_epi_tail(gout, x, stats, dx, db, ws, N, H, W, Cx, act, slope, accumulate_db, planes, ldp,
+                                       stream);
+}
+
 static int in_bwd_tail(const float* gy, const float* x, const float* stats, float* dx, float* db, float* ws,
                        int N, int HW, int C, int act, float slope, int accumulate_db, void* planes, long ldp,
                        const RedGeom& g, hipStream_t s) {

@@ -508,6 +508,11 @@ FOLD_IN = os.environ.get("VST_FOLD_IN", "0") == "1"
 # 64.75 ms) — the per-pixel border test and the target pixels' slab loads stall the partial pass's
 # load stream more than the separate border pass costs.
 DGRAD_IN = os.environ.get("VST_DGRAD_IN", "0") == "1"
+# The IN backward partials of the layer below taken by the ResnetBlock data gradient's own GEMM epilogue and
+# border add (ops.conv2d_dgrad_refl_in(epi=True): no partial pass reading g and the IN input again).
+# C2 step A/B, same box: 53.52-53.57 vs 53.79-53.80 ms (profiles/r05h_dgrad_epi_step_ab.jsonl); VST_DGRAD_EPI=0
+# restores the separate partial pass.
+DGRAD_EPI = os.environ.get("VST_DGRAD_EPI", "1") != "0"
 # The discriminator head (1 real output channel of 4) runs the one-channel skinny forward
 # (ops.conv2d_fwd(co_real=1)); VST_D_CO1=0 keeps the 4-channel sums.
 D_CO1 = os.environ.get("VST_D_CO1", "1") != "0"
@@ -747,6 +752,16 @@ class _GeneratorFn(torch.autograd.Function):
             separately."""
             ikf = P["ikf"].get(key)
             cin_p = y_in.shape[-1]
+            if DGRAD_EPI and ikf is not None and dy.shape[-1] % 8 == 0:
+                db = mod.bias.grad if (train_w and mod.bias is not None) else None
+                N = x_w.shape[0]
+                want = (train_w and IN_PLANES and
+                        _wgrad_on_bf(N, x_w.shape[1], x_w.shape[2], x_w.shape[3], y_in.shape[1], y_in.shape[2],
+                                     cin_p, R_w, st_w, ops.get_conv_math()))
+                r = ops.conv2d_dgrad_refl_in(dy, ikf, H, W, cin_p, y_in, s_in, act, 0.0, addend=addend, db=db,
+                                             planes=want, epi=True)
+                if r is not None:
+                    return r if want else (r[0], r[1], None)
             if DGRAD_IN and not FOLD_IN and ikf is not None and dy.shape[-1] % 8 == 0:
                 db = mod.bias.grad if (train_w and mod.bias is not None) else None
                 N = x_w.shape[0]

@@ -553,11 +553,13 @@ def conv2d_dgrad_s1_in(dy, ikf, H, W, cx, R, pad, y_in, stats, act="relu", slope
 
 
 def conv2d_dgrad_refl_in(dy, ikf, H, W, cx, y_in, stats, act="relu", slope=0.0, addend=None, db=None,
-                         accumulate_db=True, planes=False, role="bwd"):
+                         accumulate_db=True, planes=False, role="bwd", epi=False):
     """ReflectionPad2d(1) + 3x3 data gradient (conv2d_dgrad_s1's interior conv + border GEMM) fused with
     the InstanceNorm(+act) backward of the layer below it (vst_conv2d_dgrad_refl_in): returns (g, dy_in[,
     dy_in_planes]) — g = the data gradient (+ addend), dy_in = instnorm_act_bwd(g, y_in, stats, act) —
-    or None when the fused route does not support the shape / arithmetic."""
+    or None when the fused route does not support the shape / arithmetic.
+    epi: the IN partials taken by the data gradient's GEMM epilogue and border add instead
+    (vst_conv2d_dgrad_refl_in_epi: no partial pass; x6 arithmetic, H W % 32 == 0)."""
     _dev_check(dy, ikf, addend, y_in, stats)
     if not DGRAD_BORDER or getattr(ikf, "vst_split", None) is None:
         return None
@@ -566,6 +568,24 @@ def conv2d_dgrad_refl_in(dy, ikf, H, W, cx, y_in, stats, act="relu", slope=0.0, 
     if (Hy, Wy) != (H, W) or cx != C:
         return None
     m = _math(role)
+    if epi:
+        nb = int(lib().vst_conv2d_dgrad_refl_in_epi_ws_bytes(N, H, W, Cy, C, m))
+        if not nb:
+            return None
+        g = torch.empty((N, H, W, C), device=dy.device)
+        dyi = torch.empty_like(g)
+        ws = torch.empty((nb + 3) // 4, device=dy.device)
+        pl, ldp = None, 0
+        if planes:
+            ldp = lib().vst_cp_ld(N * H * W)
+            pl = torch.empty((3, C, ldp), device=dy.device, dtype=torch.bfloat16)
+        h = _probe_begin("dgrad", (N, H, W, Cy, C, 3, 1, 1, "reflect")) if _probes else None
+        _call("vst_conv2d_dgrad_refl_epi_part", _p(dy), _p(ikf.vst_split), _p(addend), _p(g), _p(y_in), _p(stats),
+              _p(ws), nb, N, H, W, Cy, C, ACT[act], float(slope), m, _stream())
+        _probe_end(h)
+        _call("vst_instnorm_act_bwd_epi_tail", _p(g), _p(y_in), _p(stats), _p(dyi), _p(db), _p(ws), N, H, W, C, ACT[act],
+              float(slope), 1 if accumulate_db else 0, _p(pl), ldp, _stream())
+        return (g, dyi, pl) if planes else (g, dyi)
     nbd = int(lib().vst_conv2d_dgrad_refl_ws_bytes(N, H, W, Cy, C, m))
     if not nbd or not int(lib().vst_conv2d_dgrad_refl_in_ws_bytes(N, H, W, Cy, C, m)):
         return None

@@ -339,6 +339,24 @@ int vst_conv2d_dgrad_refl_in(const float* dy, const void* wsplit, const float* a
                              const float* stats, float* dx, float* db, float* ws, size_t ws_bytes, int N, int H,
                              int W, int Cy, int Cx, int act, float slope, int accumulate_db, void* planes, long ldp,
                              int math, void* stream);
+/* vst_conv2d_dgrad_refl_in with the IN backward partials taken by the data gradient itself: the interior
+ * GEMM's epilogue sums {g', g' xhat, xhat} per 32-pixel group of its output tile and the border add adds
+ * the correction of the pixels it changes, so the separate partial pass (a read of gout and x and a launch)
+ * is gone.  gout is bit-identical to vst_conv2d_dgrad_refl; dx / planes / db to the separate passes up to
+ * the fp64 summation order of the partials.  x6 arithmetic only, H*W % 32 == 0 (ws_bytes query 0 =
+ * unsupported).  Same arguments as vst_conv2d_dgrad_refl_in. */
+size_t vst_conv2d_dgrad_refl_in_epi_ws_bytes(int N, int H, int W, int Cy, int Cx, int math);
+int vst_conv2d_dgrad_refl_in_epi(const float* dy, const void* wsplit, const float* addend, float* gout,
+                                 const float* x, const float* stats, float* dx, float* db, float* ws, size_t ws_bytes,
+                                 int N, int H, int W, int Cy, int Cx, int act, float slope, int accumulate_db,
+                                 void* planes, long ldp, int math, void* stream);
+/* its halves: the data gradient + the partials (into the front of ws), then finalize + apply from them */
+int vst_conv2d_dgrad_refl_epi_part(const float* dy, const void* wsplit, const float* addend, float* gout,
+                                   const float* x, const float* stats, float* ws, size_t ws_bytes, int N, int H, int W,
+                                   int Cy, int Cx, int act, float slope, int math, void* stream);
+int vst_instnorm_act_bwd_epi_tail(const float* gout, const float* x, const float* stats, float* dx, float* db,
+                                  float* ws, int N, int H, int W, int Cx, int act, float slope, int accumulate_db,
+                                  void* planes, long ldp, void* stream);
 int vst_conv2d_dgrad_refl_slabs(const float* dy, const void* wsplit, const float* addend, float* gout, float* ws,
                                 size_t ws_bytes, int N, int H, int W, int Cy, int Cx, int math, void* stream);
 int vst_instnorm_act_bwd_refl_border(float* gout, const float* x, const float* stats, float* dx, float* db,

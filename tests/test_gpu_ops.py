@@ -1063,6 +1063,72 @@ def test_dgrad_refl_in_fused(ops, case):
         ops.set_conv_math(prev)
 
 
+@pytest.mark.parametrize("case", [
+    # name, N, C_in (= dx = IN channels), C_out (= dy), H, W, act, addend
+    ("small_relu", 2, 256, 256, 16, 16, "relu", True),      # all split-K tiles
+    ("all_split_N1", 1, 256, 256, 64, 64, "relu", False),  # the whole conv as split-K tiles (B=1)
+    ("prod_N8", 8, 256, 256, 64, 64, "relu", False),       # whole 256x128 rounds
+    ("prod_N8_add", 8, 256, 256, 64, 64, "none", True),
+    ("prod_N12", 12, 256, 256, 64, 64, "none", True),      # a round + the split-K tail
+], ids=lambda c: c[0])
+def test_dgrad_refl_in_epi(ops, case):
+    """vst_conv2d_dgrad_refl_in_epi (the IN backward partials taken by the data gradient's GEMM epilogue /
+    split-K reduce and the border add's correction slices) vs the separate passes (vst_conv2d_dgrad_refl +
+    vst_instnorm_act_bwd_planes): g bit-identical; the IN input gradient, its planes and the bias gradient
+    equal up to the partials' fp64 summation order (1e-6 of max); and vs torch autograd."""
+    name, N, Ci, Co, H, W, act, with_add = case
+    prev = ops.set_conv_math("bf16x6")
+    try:
+        w = _g(131, (Co, Ci, 3, 3), 0.05)
+        ikf = ops.weight_pack(w.to(DEV), ops.PACK_IKF)
+        dy = _nhwc(_g(132, (N, Co, H, W)), ops)
+        add = _nhwc(_g(133, (N, Ci, H, W)), ops) if with_add else None
+        y_in = _nhwc(_g(134, (N, Ci, H, W)), ops)
+        s = ops.instnorm_stats(y_in)
+        db0 = torch.zeros(Ci, device=DEV)
+        db1 = torch.zeros(Ci, device=DEV)
+        r = ops.conv2d_dgrad_refl_in(dy, ikf, H, W, Ci, y_in, s, act, addend=add, db=db1, planes=True, epi=True)
+        assert r is not None, name
+        g1, dx1, pl1 = r
+        g0 = ops.conv2d_dgrad_s1(dy, ikf, H, W, Ci, 3, 1, "reflect", addend=add)
+        dx0, pl0 = ops.instnorm_act_bwd(g0, y_in, s, act, db=db0, planes=True)
+        assert torch.equal(g1, g0), name
+        sc = dx0.abs().max().item()
+        assert (dx1 - dx0).abs().max().item() <= 1e-6 * sc, name
+        P = N * H * W
+        assert (pl1[:, :, :P].float().sum(0) - pl0[:, :, :P].float().sum(0)).abs().max().item() <= 1e-6 * sc, name
+        assert (db1 - db0).abs().max().item() <= 1e-6 * max(db0.abs().max().item(), 1e-30), name
+        x = _g(135, (N, Ci, H, W)).requires_grad_(True)
+        yy = F.conv2d(F.pad(x, (1,) * 4, mode="reflect"), w)
+        yy.backward(_nchw(dy, Co, ops))
+        gref = x.grad + (_nchw(add, Ci, ops) if with_add else 0)
+        _close(_nchw(g1, Ci, ops), gref, tol=CONV_TOL["bf16x6"], what=name + " g")
+        yt = _nchw(y_in, Ci, ops).requires_grad_(True)
+        a = F.instance_norm(yt, eps=1e-5)
+        a = F.relu(a) if act == "relu" else a
+        a.backward(_nchw(g1, Ci, ops))
+        _close(_nchw(dx1, Ci, ops), yt.grad, tol=1e-4, what=name + " IN bwd")
+    finally:
+        ops.set_conv_math(prev)
+
+
+def test_dgrad_refl_in_epi_unsupported(ops):
+    """H W not a multiple of 32, or a plan that is neither whole 256x128 rounds (+ a split-K tail) nor all
+    split-K (the 436x1024 ResnetBlocks: 218 tiles of 128x128): the epi route declines (None), the caller
+    keeps the separate passes."""
+    prev = ops.set_conv_math("bf16x6")
+    try:
+        for (N, C, H, W) in ((2, 64, 13, 20), (1, 256, 109, 256)):
+            w = _g(141, (C, C, 3, 3), 0.05)
+            ikf = ops.weight_pack(w.to(DEV), ops.PACK_IKF)
+            dy = _nhwc(_g(142, (N, C, H, W)), ops)
+            y_in = _nhwc(_g(143, (N, C, H, W)), ops)
+            s = ops.instnorm_stats(y_in)
+            assert ops.conv2d_dgrad_refl_in(dy, ikf, H, W, C, y_in, s, "relu", epi=True) is None
+    finally:
+        ops.set_conv_math(prev)
+
+
 @pytest.mark.parametrize("N", [1, 2, 8, 12, 16])
 def test_conv_fwd_nrm_matches_apply_then_conv(ops, N):
     """vst_conv2d_fwd_nrm_ws (the ResnetBlock's second conv normalising relu(IN(t)) in its A staging)

@@ -55,7 +55,14 @@ if which == "wgrad_pre":  # the step's form: x's padded image and dy's planes ma
     _, x_t = ops.instnorm_act_fwd(x, st, "none", cp=(1, "reflect", 1))
     gy, dy_planes = ops.instnorm_act_bwd(gy, x, st, "none", planes=True)
     torch.cuda.synchronize()
+# KB_FLUSH=1: a 1 GiB write before every call (L2 and the MALL hold none of the operands: the cold-operand
+# time); KB_FLUSH=2 (wgrad_pre): then the dy planes re-made by their producer (hot, as in the step; x's image cold)
+flush = torch.empty(1 << 28, device=dev) if os.environ.get("KB_FLUSH") else None
 for _ in range(reps):
+    if flush is not None:
+        flush.fill_(1.0)
+        if which == "wgrad_pre" and os.environ.get("KB_FLUSH") == "2":
+            gy, dy_planes = ops.instnorm_act_bwd(gy, x, st, "none", planes=True)
     if which == "fprop":
         ops.conv2d_fwd(x, kc, None, C, 3, 3, 1, 1, "reflect")
     elif which == "dgrad":  # stride-1 data gradient as a forward conv over rotated taps (train path)

@@ -157,10 +157,13 @@ __device__ __forceinline__ uint32_t pack2(float a, float b) {
 #ifndef VST_BF_FAKE_ZA
 #define VST_BF_FAKE_ZA 0  // developer timing experiment only: every A gather reads the zero page (WRONG results)
 #endif
+#ifndef VST_BF_FAKE_ADMA
+#define VST_BF_FAKE_ADMA 0  // developer timing experiment only: A LDS-DMA'd from x's own bytes (WRONG results)
+#endif
 #ifndef VST_BF_FAKE_ZB
 #define VST_BF_FAKE_ZB 0  // developer timing experiment only: every B load reads the zero page (WRONG results)
 #endif
-#if (VST_BF_FAKESPLIT || VST_BF_FAKE16 || VST_BF_FAKE_ZA || VST_BF_FAKE_ZB) && !defined(VST_DEV_VARIANT)
+#if (VST_BF_FAKESPLIT || VST_BF_FAKE16 || VST_BF_FAKE_ZA || VST_BF_FAKE_ZB || VST_BF_FAKE_ADMA) && !defined(VST_DEV_VARIANT)
 #error "VST_BF_FAKESPLIT / VST_BF_FAKE16 are developer-only timing modes (wrong results): build them with tools/build_variant.py"
 #endif
 template <int NP>
@@ -256,10 +259,11 @@ __device__ __forceinline__ void mma_frag(const Frag<T>& f, f32x16 (&acc)[T::MI][
 template <class T>
 __device__ __forceinline__ void store_stage(char* st, const float4 (&ra)[T::A_LD][2],
                                             const u32x4_t (&rbv)[T::B_LD][T::NP], int rb, int kq,
-                                            bool with_b = true) {
+                                            bool with_b = true, bool with_a = true) {
   char* Bs = st + T::A_BYTES;
 #pragma unroll
   for (int j = 0; j < T::A_LD; ++j) {
+    if (!with_a) break;
     uint4 s[T::NP];
     split8<T::NP>(ra[j][0], ra[j][1], s);
     const int off = swz_off<T>(rb + T::RPP * j, kq);
@@ -428,12 +432,12 @@ __device__ __forceinline__ void sched16() {
 // Every product term of the x6 sum is the 32x32x16 loop's; only the summation order of the six
 // terms into the fp32 accumulator differs (mid*mid first).
 struct NoDma {
-  static constexpr bool active = false;
+  static constexpr bool active = false, a_active = false;
   __device__ __forceinline__ void operator()(char*) const {}
 };
-template <class F>
+template <class F, bool A = false>
 struct DmaB {
-  static constexpr bool active = true;
+  static constexpr bool active = true, a_active = A;  // B (and with A: the A operand too) by LDS-DMA
   F f;
   __device__ __forceinline__ void operator()(char* st) const { f(st); }
 };
@@ -454,7 +458,7 @@ __device__ __forceinline__ void main_loop16(char* smem, int nk, f32x4v (&acc)[T:
   dmab(smem);
   load_all(0);
   prep(0);
-  store_stage<T>(smem, ra[0], rbv[0], rb, kq, !dmab.active);
+  store_stage<T>(smem, ra[0], rbv[0], rb, kq, !dmab.active, !dmab.a_active);
   adv(nk > 1);
   load_all(1);
   __syncthreads();
@@ -479,7 +483,7 @@ __device__ __forceinline__ void main_loop16(char* smem, int nk, f32x4v (&acc)[T:
     }
     if (SA) {
       prep(P ^ 1);
-      store_stage<T>(nxt, ra[P ^ 1], rbv[P ^ 1], rb, kq, !dmab.active);
+      store_stage<T>(nxt, ra[P ^ 1], rbv[P ^ 1], rb, kq, !dmab.active, !dmab.a_active);
     }
     mma16<T>(mid, mid, acc);
     if (VST_M16_SCHED) sched16<NM, RA ? 2 * NR : NR, NV, SA ? 4 : 0, SA ? NW : 0>();
@@ -487,7 +491,7 @@ __device__ __forceinline__ void main_loop16(char* smem, int nk, f32x4v (&acc)[T:
     if (!RA) read_plane16<T>(lo, cur, 2, wm0, wn0, lane);
     if (!SA) {
       prep(P ^ 1);
-      store_stage<T>(nxt, ra[P ^ 1], rbv[P ^ 1], rb, kq, !dmab.active);
+      store_stage<T>(nxt, ra[P ^ 1], rbv[P ^ 1], rb, kq, !dmab.active, !dmab.a_active);
     }
     mma16<T>(mid, hi, acc);
     mma16<T>(hi, mid, acc);
@@ -846,14 +850,14 @@ __device__ __attribute__((aligned(256))) float g_zero_page[64];
 // writes the normalised activation.  Reflect padding only (a zero-padding tap must stay zero), and
 // every tile's rows in one image (Ho*Wo a multiple of BM): the 8 channels' statistics of a K-step are
 // four float4 loads beside the A gathers.
-template <class T, bool KSL, int REFL, bool SPLIT, bool NRM = false>
+template <class T, bool KSL, int REFL, bool SPLIT, bool NRM = false, bool APRE = false>
 __device__ __forceinline__ void conv_fprop_bf_body(
     int bid, const float* __restrict__ x, const __bf16* __restrict__ ws, long wps, const float* __restrict__ bias,
     float* __restrict__ y, int H, int W, int C, int Ho, int Wo, int Cop, int S, int st, int padh,
     int padw, int reflect, int act, float slope, int M, int Ktot, int m_base, double* __restrict__ part,
     int spk, float* __restrict__ slab, const float* __restrict__ addend, int oph,
     const float* __restrict__ nst = nullptr, const float* __restrict__ bslab = nullptr, int bks = 0, int bmb = 0,
-    int blt = 0, int bll = 0, InbArgs inb = InbArgs{}) {
+    int blt = 0, int bll = 0, InbArgs inb = InbArgs{}, const __bf16* __restrict__ apl = nullptr, long pps = 0) {
   static_assert(!SPLIT || KSL, "split-K needs the channel-slice-major K walk");
   static_assert(!NRM || (KSL && REFL == 1), "normalised A: the channel-slice K walk, reflect padding");
   static_assert(REFL < 4 || (SPLIT && KSL), "border rows run as split-K slabs");
@@ -967,6 +971,13 @@ __device__ __forceinline__ void conv_fprop_bf_body(
   float4 ra[2][A_LD][2];
   u32x4_t rbv[2][B_LD][NP];
   constexpr bool GLDS = VST_BF_GLDS_B && T::M16 && KSL && !C4 && REFL != 5;
+  // APRE: the A operand arrives pre-split (apl: three bf16 planes of x's NHWC layout, plane stride pps
+  // elements) by LDS-DMA like B — no fp32 A image, no split in the staging.  VST_BF_FAKE_ADMA (developer timing
+  // only, WRONG results): every GLDS kernel DMAs A from x's own bytes read as planes.
+  constexpr bool GLDS_A = (APRE || VST_BF_FAKE_ADMA) && GLDS && !NRM;
+  static_assert(!APRE || GLDS_A, "pre-split A: the x6 M16 channel-slice kernels with LDS-DMA B");
+  const __bf16* apl_ = VST_BF_FAKE_ADMA ? reinterpret_cast<const __bf16*>(x) : apl;
+  const long pps_ = VST_BF_FAKE_ADMA ? (long)(M / (Ho * Wo)) * H * W * C / 2 : pps;
   float4 nr[2][NRM ? 4 : 1];  // NRM: (mean, rstd) of the stage's 8 channels, per register set
   const float* nimg = NRM ? nst + (long)(m0 / (Ho * Wo)) * C * 2 : nullptr;
   auto load_all = [&](int set) __attribute__((always_inline)) {
@@ -1006,6 +1017,7 @@ __device__ __forceinline__ void conv_fprop_bf_body(
     }
 #pragma unroll
     for (int j = 0; j < A_LD; ++j) {
+      if constexpr (GLDS_A) break;  // A arrives by LDS-DMA (dma_b)
       // FAKE_ZA 1: every A gather from the zero page; 2: all but the first tap of each channel slice
       // (only the L2-miss-prone loads stay real); 3: only the first tap's loads from the zero page
       const bool tap0 = KSL && tr == 0 && ts == 0;
@@ -1030,6 +1042,24 @@ __device__ __forceinline__ void conv_fprop_bf_body(
   // at row 16 w + l / 4, slot l % 4, so it reads source chunk (l % 4) ^ swz(row) (the LDS image's
   // chunk swizzle applied on the source address)
   auto dma_b = [&](char* st) __attribute__((always_inline)) {
+    if constexpr (GLDS_A) {  // the A rows of the stage (row rb + RPP j: this thread's aoff[j]), planes apl_
+      const __bf16* zb = reinterpret_cast<const __bf16*>(zp);
+#pragma unroll
+      for (int j = 0; j < A_LD; ++j) {
+        const int row = rb + RPP * j;
+        const int csrc = (t % T::KC) ^ T::swz(row);
+        const int wrow0 = __builtin_amdgcn_readfirstlane(row - (lane / T::KC));
+        const bool live = aoff[j] >= 0;
+        const __bf16* src = live ? apl_ + aoff[j] + ksb + 8 * csrc : zb + 8 * csrc;
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+          __builtin_amdgcn_global_load_lds(src + (live ? p * pps_ : 0), (lds_void*)(st + p * T::A_PLANE + wrow0 * T::ROWB),
+                                           16, 0, 0);
+#endif
+        }
+      }
+    }
     const int kbase = (tr * S + ts) * C + ksb;
 #pragma unroll
     for (int j = 0; j < B_LD; ++j) {
@@ -1092,7 +1122,7 @@ __device__ __forceinline__ void conv_fprop_bf_body(
     f32x4v acc[T::MI16][T::NI16];
     zero_acc4(acc);
     if constexpr (GLDS)
-      main_loop16<T>(smem, nk, acc, ra, rbv, rb, kq, load_all, adv, prep, DmaB<decltype(dma_b)>{dma_b});
+      main_loop16<T>(smem, nk, acc, ra, rbv, rb, kq, load_all, adv, prep, DmaB<decltype(dma_b), GLDS_A>{dma_b});
     else
       main_loop16<T>(smem, nk, acc, ra, rbv, rb, kq, load_all, adv, prep, NoDma{});
     if constexpr (SPLIT) {
@@ -1121,6 +1151,24 @@ __device__ __forceinline__ void conv_fprop_bf_body(
     const bool LEPI = LFIT && (VST_BF_LDS_EPI || addend != nullptr || oph != 0 || bslab != nullptr || inb.part != nullptr);
     constexpr int LDE = T::BN + 16;
     float* ept = reinterpret_cast<float*>(smem);
+    // InbArgs: the IN input z (and the addend) of the wave's 32-row group (wave w: rows 32 w .., one group per
+    // wave) loaded before the tile goes through LDS, so their latency overlaps the staging
+    constexpr int IC4 = T::BN / 4, IRW = 64 / (IC4 > 0 ? IC4 : 1);
+    constexpr bool IOK = LFIT && 64 % IC4 == 0 && T::BM == 32 * T::NW && IC4 >= 4;
+    float4 izr[IOK ? 32 / IRW : 1], iar[IOK ? 32 / IRW : 1];
+    if constexpr (IOK) {
+      if (inb.part) {
+        const int n = n0 + 4 * (lane % IC4);
+#pragma unroll
+        for (int k = 0; k < 32 / IRW; ++k) {
+          const int mm = m0 + 32 * wave + lane / IC4 + IRW * k;
+          const bool ok = n < Cop && mm < M;
+          izr[k] = ok ? *reinterpret_cast<const float4*>(inb.z + (long)mm * Cop + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+          iar[k] = (ok && addend) ? *reinterpret_cast<const float4*>(addend + (long)mm * Cop + n)
+                                  : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      }
+    }
     if (LEPI) __syncthreads();  // every wave is done reading the last stage
 #pragma unroll
     for (int g = 0; g < T::MI16 / 2; ++g)
@@ -1161,17 +1209,16 @@ __device__ __forceinline__ void conv_fprop_bf_body(
     if (LEPI) {
       __syncthreads();
       constexpr int C4 = T::BN / 4;
-      if constexpr (LFIT && 64 % C4 == 0 && T::BM % 32 == 0 && C4 >= 4) {
+      if constexpr (IOK) {
         if (inb.part) {
-          // IN-backward partials (InbArgs): wave w stores the 32-row groups w, w + NW, ...; lane l owns
-          // channels 4 (l % C4) .. + 3 and rows l / C4 + RW k of the group (whole 4*C4-float rows per
-          // instruction, as the loop below); per-lane fixed-order fp64 sums, then xor over the RW lanes
-          // of a channel group.  Every group lies in one image (HW % 32 == 0, checked by the launcher).
-          constexpr int RW = 64 / C4;
+          // IN-backward partials (InbArgs): wave w stores the 32-row group w (z / addend prefetched above);
+          // lane l owns channels 4 (l % C4) .. + 3 and rows l / C4 + RW k of the group (whole 4*C4-float rows
+          // per instruction, as the loop below); per-lane fixed-order fp64 sums, then xor over the RW lanes of
+          // a channel group.  Every group lies in one image (HW % 32 == 0, checked by the launcher).
+          constexpr int RW = IRW;
           const int c = 4 * (lane % C4), n = n0 + c, hw = Ho * Wo;
-          for (int G = wave; G < T::BM / 32; G += T::NW) {
-            const int gm0 = m0 + 32 * G;
-            if (gm0 >= M) break;
+          const int gm0 = m0 + 32 * wave;
+          if (gm0 < M) {
             const int img = gm0 / hw;
             float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0;
             if (n < Cop) {
@@ -1180,15 +1227,14 @@ __device__ __forceinline__ void conv_fprop_bf_body(
             }
             const float mu[4] = {s0.x, s0.z, s1.x, s1.z}, rs[4] = {s0.y, s0.w, s1.y, s1.w};
             double a0[4] = {0, 0, 0, 0}, a1[4] = {0, 0, 0, 0}, a2[4] = {0, 0, 0, 0};
-#pragma unroll 4
+#pragma unroll
             for (int k = 0; k < 32 / RW; ++k) {
-              const int row = 32 * G + lane / C4 + RW * k, mm = m0 + row;
+              const int row = 32 * wave + lane / C4 + RW * k, mm = m0 + row;
               if (n < Cop && mm < M) {
                 float4 v = *reinterpret_cast<const float4*>(ept + row * LDE + c);
-                if (addend) add_f4(v, *reinterpret_cast<const float4*>(addend + (long)mm * Cop + n));
+                add_f4(v, iar[k]);
                 *reinterpret_cast<float4*>(y + (long)mm * Cop + n) = v;
-                const float4 zz = *reinterpret_cast<const float4*>(inb.z + (long)mm * Cop + n);
-                const float gv[4] = {v.x, v.y, v.z, v.w}, zv[4] = {zz.x, zz.y, zz.z, zz.w};
+                const float gv[4] = {v.x, v.y, v.z, v.w}, zv[4] = {izr[k].x, izr[k].y, izr[k].z, izr[k].w};
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                   float gd, xh;
@@ -2293,7 +2339,9 @@ bool bf_convT_phases_ok(int C, int Cop, int math) {
   return math != VST_MATH_F32 && VST_BF_KSLICE && C % 32 == 0 && Cop % 4 == 0;
 }
 
-// The phase tile (x6): Cop > 64 on 256x128 (8 waves of 64x64), Cop <= 64 on 64x64 (4 waves of 32x32).  Round 5
+// The phase tile (x6): Cop > 64 on 256x128 (8 waves of 64x64) unless its grid's rounds cost more than the
+// 128x128 tile's (the N = 4 PatchGAN data gradients: 68 blocks, 77 us vs 51 us), Cop <= 64 on 64x64 (4 waves of
+// 32x32).  Round 5
 // sweep (profiles/r05e_convT_wgrad_tiles.jsonl, same box): the 256 -> 128 ConvTranspose / stride-2 data
 // gradient 144 -> 124 us at N = 8 (188 -> 167 at N = 12) against 128x128 tiles of 8 x (64x32) waves; the
 // 128 -> 64 one 150 -> 145 us against 128x64.  VST_CONVT_TILE (developer A/B): 0 = the round-4 tiles
@@ -2307,19 +2355,34 @@ int bf_convT_phases_launch(const float* x, const void* const ws[4], const float*
                            int C, int Cop, int act, float slope, int math, hipStream_t s, int full) {
   VST_REQUIRE(bf_convT_phases_ok(C, Cop, math), "convT phases: unsupported shape / arithmetic");
   const int bn = Cop <= 64 ? 64 : 128;
-  const int tk = math != VST_MATH_BF16X6 ? 0 : (g_convt_tile >= 0 ? g_convt_tile : (bn == 128 ? 1 : 2));
+  // the concatenated grid of the four phases on bm-row tiles (each job on a multiple of 8 blocks)
+  auto grid_of = [&](int bm_, bf::PhaseJobs* jb) {
+    int tt = 0;
+    for (int j = 0; j < 4; ++j) {
+      const int ph = j == 0 ? 3 : (j == 1 ? 1 : (j == 2 ? 2 : 0)), a = ph >> 1, b = ph & 1;
+      if (jb) {
+        jb->ws[j] = reinterpret_cast<const __bf16*>(ws[ph]);
+        jb->t0[j] = tt;
+      }
+      const long rows = (long)N * (H + (full ? 1 : a)) * (W + (full ? 1 : b));
+      const long tiles = (rows + bm_ - 1) / bm_ * ((Cop + bn - 1) / bn);
+      tt += (int)((tiles + 7) / 8 * 8);
+    }
+    if (jb) jb->t0[4] = tt;
+    return tt;
+  };
+  int tk = math != VST_MATH_BF16X6 ? 0 : (g_convt_tile >= 0 ? g_convt_tile : (bn == 128 ? 1 : 2));
+  if (math == VST_MATH_BF16X6 && g_convt_tile < 0 && bn == 128) {
+    // 256x128 only where its rounds cost less than the 8-wave 128x128 tile's (one block per CU either way;
+    // a 32-deep K-step ~2.25 vs ~1.5 us): the small grids (the PatchGAN k4s2 data gradients at N = 4, 68
+    // blocks of 256x128) keep 128x128
+    const long r256 = (grid_of(256, nullptr) + VST_NUM_CUS - 1) / VST_NUM_CUS;
+    const long r128 = (grid_of(128, nullptr) + VST_NUM_CUS - 1) / VST_NUM_CUS;
+    tk = r256 * 2.25 <= r128 * 1.5 ? 1 : 0;
+  }
   const int bm = (tk == 1 && bn == 128) ? 256 : ((tk == 2 && bn == 64) ? 64 : 128);
   bf::PhaseJobs jobs;
-  int t = 0;
-  for (int j = 0; j < 4; ++j) {
-    const int ph = j == 0 ? 3 : (j == 1 ? 1 : (j == 2 ? 2 : 0)), a = ph >> 1, b = ph & 1;
-    jobs.ws[j] = reinterpret_cast<const __bf16*>(ws[ph]);
-    jobs.t0[j] = t;
-    const long rows = (long)N * (H + (full ? 1 : a)) * (W + (full ? 1 : b));
-    const long tiles = (rows + bm - 1) / bm * ((Cop + bn - 1) / bn);
-    t += (int)((tiles + 7) / 8 * 8);
-  }
-  jobs.t0[4] = t;
+  const int t = grid_of(bm, &jobs);
 #define VST_CTB(BM_, BN_, WM_, WN_)                                                                       \
   {                                                                                                        \
     using T = bf::Tile<BM_, BN_, WM_, WN_, 32, 3>;                                                         \

@@ -149,6 +149,75 @@ __global__ __launch_bounds__(256) void skinny_out_k(
   *reinterpret_cast<float4*>(out + o) = v;
 }
 
+// skinny_out_k MODE 0 for few output pixels over a long K (the StarGAN discriminator heads: 3x3 / 4x4 taps over
+// 2048 channels at 4x4, <= 128 pixels — one workgroup of the per-pixel kernel ran 150-360 us): the K range split
+// over blockIdx.y = (tap, channel chunk of CC) blocks, thread (pixel, KS lane) as skinny_out_k, the lane sums
+// shuffled together and the raw partial stored to g_skinny_slab[z][pixel][4]; skinny_split_reduce_k sums the
+// splits in order + bias + act (+ addend).  Deterministic.
+constexpr long SKINNY_SLAB = 1L << 18;  // floats
+__device__ float g_skinny_slab[SKINNY_SLAB];
+
+template <int KS>
+__global__ __launch_bounds__(256) void skinny_split_k(const float* __restrict__ in, const float* __restrict__ wp,
+                                                      int Nimg, int Hi, int Wi, int Cin, int Ho, int Wo, int S, int st,
+                                                      int pad, int reflect, int CC) {
+  const int CB = Cin / CC, z = blockIdx.y, tap = z / CB, cb = z - tap * CB;
+  const int r = tap / S, s = tap - r * S;
+  const long total = (long)Nimg * Ho * Wo;
+  const long gid = ((long)blockIdx.x * blockDim.x + threadIdx.x) / KS;
+  const int ks = threadIdx.x % KS;
+  const bool valid = gid < total;
+  const long gq = valid ? gid : 0;
+  const int ww = gq % Wo;
+  const long q = gq / Wo;
+  const int hh = q % Ho, n = q / Ho;
+  const long wstride = (long)gridDim.y / CB * Cin;  // R*S*Cin: between output channels of the OK pack
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  int hi = hh * st - pad + r, wi = ww * st - pad + s;
+  bool ok = valid;
+  if (reflect) {
+    hi = reflect_idx(hi, Hi);
+    wi = reflect_idx(wi, Wi);
+  } else {
+    ok = ok && (unsigned)hi < (unsigned)Hi && (unsigned)wi < (unsigned)Wi;
+  }
+  if (ok) {
+    const float* wt = wp + (long)tap * Cin;
+    const float* src = in + (((long)n * Hi + hi) * Wi + wi) * Cin;
+#pragma unroll 4
+    for (int c = cb * CC + 4 * ks; c < (cb + 1) * CC; c += 4 * KS) {
+      const float4 v = *reinterpret_cast<const float4*>(src + c);
+      fma4x4(acc, v, *reinterpret_cast<const float4*>(wt + c), *reinterpret_cast<const float4*>(wt + wstride + c),
+             *reinterpret_cast<const float4*>(wt + 2 * wstride + c),
+             *reinterpret_cast<const float4*>(wt + 3 * wstride + c));
+    }
+  }
+#pragma unroll
+  for (int o = KS / 2; o > 0; o >>= 1) {
+    acc.x += __shfl_xor(acc.x, o, 64);
+    acc.y += __shfl_xor(acc.y, o, 64);
+    acc.z += __shfl_xor(acc.z, o, 64);
+    acc.w += __shfl_xor(acc.w, o, 64);
+  }
+  if (valid && ks == 0) *reinterpret_cast<float4*>(g_skinny_slab + ((long)z * total + gid) * 4) = acc;
+}
+
+__global__ __launch_bounds__(256) void skinny_split_reduce_k(const float* __restrict__ bias,
+                                                             const float* __restrict__ addend, float* __restrict__ out,
+                                                             long total, int nsplit, int act, float slope) {
+  const long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= total) return;
+  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int z = 0; z < nsplit; ++z) add_f4(v, *reinterpret_cast<const float4*>(g_skinny_slab + ((long)z * total + p) * 4));
+  const float4 b4 = bias ? *reinterpret_cast<const float4*>(bias) : make_float4(0.f, 0.f, 0.f, 0.f);
+  v.x = apply_act(v.x + b4.x, act, slope);
+  v.y = apply_act(v.y + b4.y, act, slope);
+  v.z = apply_act(v.z + b4.z, act, slope);
+  v.w = apply_act(v.w + b4.w, act, slope);
+  if (addend) add_f4(v, *reinterpret_cast<const float4*>(addend + p * 4));
+  *reinterpret_cast<float4*>(out + p * 4) = v;
+}
+
 // slab[z][(r*S+s)*Cx + ci][co] for co < 4, ci block of 4 per thread, pixels of split z.
 __global__ __launch_bounds__(256) void skinny_wgrad_k(
     const float* __restrict__ x, const float* __restrict__ dy, float* __restrict__ slab, int H,
@@ -208,6 +277,12 @@ __global__ __launch_bounds__(256) void skinny_wgrad_k(
     *reinterpret_cast<float4*>(sl + 4 * a) = make_float4(acc[a][0], acc[a][1], acc[a][2], acc[a][3]);
 }
 
+// few-pixel long-K forwards on the split kernel (skinny_split_k); VST_SKINNY_SPLIT=0: the per-pixel kernel
+static const bool g_skinny_split = [] {
+  const char* e = getenv("VST_SKINNY_SPLIT");
+  return !(e && e[0] == '0');
+}();
+
 // the PatchGAN head's one-channel forward on its row kernel (patch.hip); VST_HEAD=0: the per-pixel gather here
 const bool g_head = [] {
   const char* e = getenv("VST_HEAD");
@@ -238,6 +313,19 @@ int skinny_out_launch(int mode, const float* in, const float* wp, const float* b
   }
   if (mode == 0 && co_real == 1 && g_head && head_ok(Cin, R, S, st, reflect, Wo) && !addend)
     return head_fwd_launch(in, wp, bias, out, N, Hi, Wi, Cin, Ho, Wo, R, S, pad, act, slope, s);
+  if (mode == 0 && g_skinny_split && pix * 16 <= 4096 && (long)R * S * Cin >= 4096 && Cin % 64 == 0) {
+    // few pixels, long K: split the K range over workgroups (skinny_split_k)
+    int CC = Cin;
+    while (CC > 256 && CC % 2 == 0 && (CC / 2) % 64 == 0) CC /= 2;
+    const int nsplit = R * S * (Cin / CC);
+    if ((long)nsplit * pix * 4 <= SKINNY_SLAB) {
+      hipLaunchKernelGGL(skinny_split_k<16>, dim3(ceil_div(pix * 16, 256), nsplit), dim3(256), 0, s, in, wp, N, Hi, Wi,
+                         Cin, Ho, Wo, S, st, pad, reflect, CC);
+      hipLaunchKernelGGL(skinny_split_reduce_k, dim3(ceil_div(pix, 256)), dim3(256), 0, s, bias, addend, out, pix,
+                         nsplit, act, slope);
+      return check_launch("skinny_out(split)");
+    }
+  }
   if (mode == 0 && co_real == 1) {
 #define VST_SK1(KS_)                                                                                  \
   hipLaunchKernelGGL((skinny_out_k<0, 0, KS_, true>), dim3(ceil_div(pix * KS_, 256), 1, classes), dim3(256), 0, s, \

@@ -1387,7 +1387,10 @@ def conv4s2_dgrad(dy, packs, cop, role="bwd"):
     _dev_check(dy)
     N, Hd, Wd, Cy = dy.shape
     m = _math(role)
-    if C4S2_GROUPED and m != _lib.MATH_MODES["fp32"] and Cy % 32 == 0 and cop != 4 and \
+    # a grid of fewer than half a CU round of 128x128 phase tiles (the StarGAN discriminator's deep layers: 100
+    # rows x 1024 channels per phase at B = 4, K = 8192) runs as four split-K forwards + the interleave instead
+    small = 4 * (-(-N * (Hd + 1) * (Wd + 1) // 128)) * (-(-cop // 128)) < 128
+    if C4S2_GROUPED and m != _lib.MATH_MODES["fp32"] and Cy % 32 == 0 and cop != 4 and not small and \
             all(getattr(wp, "vst_split", None) is not None for wp in packs):
         # one launch, stored straight into the interleaved gradient (vst_conv4s2_dgrad)
         y = torch.empty((N, 2 * Hd, 2 * Wd, cop), device=dy.device)

@@ -25,7 +25,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import ops
-from .networks import TAP_LAST, Conv2d, ConvTranspose2d, FlatNet, _Marker
+from .networks import TAP_LAST, Conv2d, ConvTranspose2d, FlatNet, _Marker, _padded_bias
 from .ops import cpad
 from .optim import FusedAdam
 
@@ -55,6 +55,17 @@ class _ToNCHW2(torch.autograd.Function):
         return _ToNHWC2.apply(g.contiguous(), ctx.cs), None
 
 
+# The Conv2d(k4, s2, p1) data gradients on the four-phase kernel (ops.conv4s2_dgrad: the 2x2 phase convs in one
+# launch, stored interleaved) instead of the generic transposed-conv gather; VST_SG_PHASES=0 keeps the latter.
+SG_PHASES = __import__("os").environ.get("VST_SG_PHASES", "1") != "0"
+# The gradient penalty's first-order pass (autograd.grad of D's output w.r.t. x_hat) computes only the data
+# gradients: the reference's native conv backward skips the weight / bias gradients there (the engine's
+# output mask: only x_hat's gradient is requested), which are never part of the penalty's graph.  Set by
+# gradient_penalty around its autograd.grad call (a module global: the autograd engine runs the backward on
+# its device thread).
+_INPUT_GRAD_ONLY = [False]
+
+
 class ConvSpec:
     """Geometry of one conv layer plus its cached weight packs (per weight version)."""
 
@@ -63,21 +74,25 @@ class ConvSpec:
         w = mod.weight
         self.co, self.ci, self.R = w.shape[0], w.shape[1], w.shape[2]
         self.cop, self.cip = cpad(self.co), cpad(self.ci)
-        self._key, self._packs = None, None
+        self.index = 0  # position in the owner's pack list (Discriminator.specs)
+        self.phased = SG_PHASES and stride == 2 and self.R == 4 and pad == 1 and self.cop % 32 == 0 and self.cip != 4
+
+    def _make(self):
+        """This layer's packs (inside the owner's ops.PackBatch: one launch for the network, re-run in place
+        after each weight update): forward pack, transposed pack (unphased layers), padded bias, phase packs."""
+        m = self.mod
+        ok = ops.weight_pack(m.weight, ops.PACK_FWD)
+        ik = None if self.phased else ops.weight_pack(m.weight, ops.PACK_DGRAD)
+        ph = ops.conv4s2_dgrad_phase_packs(m.weight) if self.phased else None
+        return ok, ik, _padded_bias(m), ph
 
     def packs(self):
-        # keyed on the owner's version (FusedAdam updates the flat buffer in place and bumps it)
-        key = self.owner._version_key()
-        w = self.mod.weight
-        if self._packs is None or self._key != key:
-            wd = w.detach()
-            b = None
-            if self.mod.bias is not None:
-                b = torch.zeros(self.cop, device=wd.device)
-                b[:self.co] = self.mod.bias.detach()
-            self._packs = (ops.weight_pack(wd, ops.PACK_FWD), ops.weight_pack(wd, ops.PACK_DGRAD), b)
-            self._key = key
-        return self._packs
+        """(forward pack, transposed pack or None, padded bias) of the current weight version."""
+        return self.owner.packs()[self.index][:3]
+
+    def phase_packs(self):
+        """conv4s2_dgrad's phase packs of the current weight version."""
+        return self.owner.packs()[self.index][3]
 
     def out_hw(self, H, W):
         return ((H + 2 * self.pad - self.R) // self.stride + 1, (W + 2 * self.pad - self.R) // self.stride + 1)
@@ -88,7 +103,11 @@ def _conv_raw(x, ok, spec, bias=None, act="none"):
                           slope=spec.slope, role="fwd")
 
 
-def _dgrad_raw(gz, ik, spec, H, W):
+def _dgrad_raw(gz, ik, spec, H, W, phases=None):
+    if phases is not None and H == 2 * gz.shape[1] and W == 2 * gz.shape[2]:
+        return ops.conv4s2_dgrad(gz, phases, spec.cip)
+    if ik is None:  # a phased layer on an odd-sized input
+        ik = ops.weight_pack(spec.mod.weight.detach(), ops.PACK_DGRAD)
     return ops.conv2d_tfwd(gz, ik, None, H, W, spec.cip, spec.R, spec.R, spec.stride, spec.pad)
 
 
@@ -117,8 +136,9 @@ class _Conv(torch.autograd.Function):
         g = g.contiguous()
         gz = _ActBwd.apply(g, a, spec.slope) if spec.act else g
         gx = _Dgrad.apply(gz, w, spec, x.shape[1], x.shape[2]) if ctx.needs_input_grad[0] else None
-        gw = _Wgrad.apply(x, gz, spec) if ctx.needs_input_grad[1] else None
-        gb = _ChSum.apply(gz, spec.co) if ctx.needs_input_grad[2] else None
+        only_x = _INPUT_GRAD_ONLY[0]
+        gw = _Wgrad.apply(x, gz, spec) if (ctx.needs_input_grad[1] and not only_x) else None
+        gb = _ChSum.apply(gz, spec.co) if (ctx.needs_input_grad[2] and not only_x) else None
         return gx, gw, gb, None
 
 
@@ -145,7 +165,7 @@ class _Dgrad(torch.autograd.Function):
         _, ik, _ = spec.packs()
         ctx.spec = spec
         ctx.save_for_backward(gz, w)
-        return _dgrad_raw(gz, ik, spec, H, W)
+        return _dgrad_raw(gz, ik, spec, H, W, spec.phase_packs() if spec.phased else None)
 
     @staticmethod
     def backward(ctx, ggx):
@@ -226,7 +246,12 @@ class Discriminator(FlatNet):
         if self._specs is None:
             main = [ConvSpec(self, m, 2, 1, act=True, slope=0.01) for m in self.main if isinstance(m, Conv2d)]
             self._specs = main + [ConvSpec(self, self.conv1, 1, 1), ConvSpec(self, self.conv2, 1, 0)]
+            for i, sp in enumerate(self._specs):
+                sp.index = i
         return self._specs
+
+    def _make_packs(self):
+        return [sp._make() for sp in self.specs()]
 
     def _flatten(self):
         super()._flatten()
@@ -479,8 +504,12 @@ def classification_loss(logit, target, dataset="CelebA"):
 def gradient_penalty(y, x):
     """solver.py:187-199: mean over the batch of (||dy/dx||_2 - 1)^2, differentiable (create_graph)."""
     weight = torch.ones(y.size(), device=y.device)
-    dydx = torch.autograd.grad(outputs=y, inputs=x, grad_outputs=weight, retain_graph=True, create_graph=True,
-                               only_inputs=True)[0]
+    _INPUT_GRAD_ONLY[0] = True
+    try:
+        dydx = torch.autograd.grad(outputs=y, inputs=x, grad_outputs=weight, retain_graph=True, create_graph=True,
+                                   only_inputs=True)[0]
+    finally:
+        _INPUT_GRAD_ONLY[0] = False
     dydx = dydx.view(dydx.size(0), -1)
     dydx_l2norm = torch.sqrt(torch.sum(dydx ** 2, dim=1))
     return torch.mean((dydx_l2norm - 1) ** 2)

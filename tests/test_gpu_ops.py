@@ -871,6 +871,27 @@ def test_tap_wgrad_with_forward_x_image(ops):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("shape", [
+    # N, Ci, H (= W), Co, k, pad: the StarGAN discriminator heads at 256^2 (conv1 3x3 -> 1, conv2 4x4 -> c_dim)
+    (8, 2048, 4, 1, 3, 1), (4, 2048, 4, 4, 4, 0), (16, 1024, 2, 4, 2, 0), (3, 512, 5, 3, 3, 1)])
+def test_conv_fwd_skinny_split(ops, shape):
+    """vst_conv2d_fwd on <= 4 output channels with few output pixels and a long K (skinny_split_k: the K range
+    split over workgroups, the slabs summed in order) vs torch; the padded channels stay exactly zero."""
+    N, Ci, H, Co, k, pad = shape
+    x = _g(151, (N, Ci, H, H))
+    w = _g(152, (Co, Ci, k, k), 0.05)
+    b = _g(153, (Co,), 0.1)
+    kc = ops.weight_pack(w.to(DEV), ops.PACK_FWD)
+    bp = torch.zeros(ops.cpad(Co), device=DEV)
+    bp[:Co] = b.to(DEV)
+    y = ops.conv2d_fwd(_nhwc(x, ops), kc, bp, ops.cpad(Co), k, k, 1, pad, "zero", act="lrelu", slope=0.01)
+    yr = F.leaky_relu(F.conv2d(x, w, b, padding=pad), 0.01)
+    _close(_nchw(y, Co, ops), yr, tol=2e-5, what="skinny split fwd")
+    if Co < 4:
+        assert torch.count_nonzero(y[..., Co:]).item() == 0
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("shape", [(2, 512, 31, 31, 1, "zero", "none"), (1, 64, 9, 7, 2, "zero", "lrelu"),
                                    (1, 36, 12, 10, 1, "reflect", "tanh")])
 def test_conv_fwd_one_real_channel(ops, shape):

@@ -44,6 +44,10 @@ if which == "c0":  # the generator's first conv (4-channel image -> 64, 7x7 refl
     sys.exit(0)
 B, H, C = int(os.environ.get("KB_B", "8")), 64, 256  # 8 = the batched G_A calls of the train step
 x = torch.randn(B, H, H, C, device=dev)
+# KB_RELU=1: x = relu(randn) (half zeros, as the step's post-IN/ReLU activations) — the operands' toggle rate sets
+# the clock the chip holds under MFMA load (MI355X_MICROARCH.md DVFS items)
+if os.environ.get("KB_RELU") == "1":
+    x = torch.relu(x)
 w = torch.randn(C, C, 3, 3, device=dev) * 0.02
 kc, ck = ops.weight_pack(w, ops.PACK_FWD), ops.weight_pack(w, ops.PACK_DGRAD)
 ikf = ops.weight_pack(w, ops.PACK_IKF)

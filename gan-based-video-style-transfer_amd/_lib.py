@@ -175,8 +175,12 @@ SIGNATURES = {
     "vst_conv2d_dgrad_refl_in": (I, [P, P, P, P, P, P, P, P, P, SZ, I, I, I, I, I, I, F, I, P, L, I, P]),
     "vst_conv2d_dgrad_refl_in_epi_ws_bytes": (SZ, [I, I, I, I, I, I]),
     "vst_conv2d_dgrad_refl_in_epi": (I, [P, P, P, P, P, P, P, P, P, SZ, I, I, I, I, I, I, F, I, P, L, I, P]),
-    "vst_conv2d_dgrad_refl_epi_part": (I, [P, P, P, P, P, P, P, SZ, I, I, I, I, I, I, F, I, P]),
-    "vst_instnorm_act_bwd_epi_tail": (I, [P, P, P, P, P, P, I, I, I, I, I, F, I, P, L, P]),
+    "vst_conv2d_dgrad_refl_epi_part": (I, [P, P, P, P, P, P, P, P, SZ, I, I, I, I, I, I, F, I, P]),
+    "vst_instnorm_act_bwd_epi_tail": (I, [P, P, P, P, P, P, I, I, I, I, I, F, I, P, L, P, P]),
+    "vst_conv2d_fwd_apre_ws": (I, [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, I, P, P, P, SZ, P]),
+    "vst_instnorm_act_fwd_cp_apre": (I, [P, P, P, P, P, P, I, I, I, I, I, F, I, I, I, P]),
+    "vst_instnorm_act_fwd_apre": (I, [P, P, P, P, P, I, I, I, I, F, P]),
+    "vst_instnorm_act_bwd_planes_apre": (I, [P, P, P, P, P, P, I, I, I, I, F, I, P, L, P, P]),
     "vst_conv2d_dgrad_refl_slabs": (I, [P, P, P, P, P, SZ, I, I, I, I, I, I, P]),
     "vst_instnorm_act_bwd_refl_border": (I, [P, P, P, P, P, P, P, I, I, I, I, I, I, F, I, P, L, I, P]),
     # SURVEY §8b spelling (abi.hip)

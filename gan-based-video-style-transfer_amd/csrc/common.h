@@ -175,7 +175,15 @@ bool bf_dgrad_refl1_inb_ok(int N, int H, int W, int Cy, int Cx, int math);
 int bf_dgrad_refl1_inb_slices(int H, int W);
 int bf_dgrad_refl1_inb_launch(const float* dy, const void* wsplit, long wps, const float* addend, float* dx, int N,
                               int H, int W, int Cy, int Cx, int math, hipStream_t s, float* ws, size_t ws_floats,
-                              const float* z, const float* st, double* part, int act, float slope);
+                              const float* z, const float* st, double* part, int act, float slope,
+                              const __bf16* apl = nullptr, long pps = 0);
+// The A operand of the x6 forwards as pre-split bf16 planes (NHWC, plane stride pps elements), for the next
+// bf_fprop_launch on this host thread (set and cleared around one call by vst_conv2d_fwd_apre_ws)
+struct ApreArgs {
+  const __bf16* apl;
+  long pps;
+};
+extern thread_local ApreArgs g_apre;
 size_t bf_fprop_ws_floats(long M, int Cop, int C, int R, int S, int math);
 int bf_tail_ks(long M, int Cop, int m_split, int nk);
 void bf_split_plan(long M, int Cop, int C, int R, int S, int math, int kind, int* m_first, int* ks_out);

@@ -754,6 +754,14 @@ static int pick_splits(int tiles, int slots, int max_ns, int min_ns = 1) {
 #define VST_WG_BF 1   // x6 weight gradients on the split-bf16 kernel (conv_wgrad_bf_k)
 #endif
 
+// x6 weight gradients of at most 256 (tap, ci) rows and 64 channels (the image-input layer's, M = 147, and the
+// last layer's swapped GEMM) on ONE 256x64 tile per split (kind 10: the dy / x planes read once per split instead of
+// once per 64-row tile); VST_WG_K256=1 (developer A/B)
+static const bool g_wg_k256 = [] {
+  const char* e = getenv("VST_WG_K256");
+  return e && e[0] == '1';
+}();
+
 static const int g_wg_kind_s2 = [] {
   const char* e = getenv("VST_WG_KIND_S2");
   return e ? atoi(e) : -1;
@@ -789,6 +797,7 @@ static WgradPlan plan_wgrad(int N, int H, int W, int Ho, int Wo, int Cx, int Cyp
     // (profiles/r05e_convT_wgrad_tiles.jsonl): 178 -> 172 / 149 -> 136 us at N = 8
     if (kind == 7 && ceil_div(p.Mw, 256) * 256 > ceil_div(p.Mw, 128) * 128) kind = 0;
     if (g_wg_kind_s2 >= 0 && stride == 2) kind = g_wg_kind_s2;  // developer A/B (VST_WG_KIND_S2)
+    if (kind == 8 && g_wg_k256 && p.Mw <= 256) kind = 10;
     p.tile = (TileKind)kind;
     int bm, bn, bk, slots;
     bf_wgrad_geom(kind, math, &bm, &bn, &bk, &slots);
@@ -985,6 +994,21 @@ extern "C" int vst_conv2d_fwd_ws(const float* x, const float* wp, const void* ws
                                  size_t ws_bytes, void* stream) {
   return conv_fwd_impl(x, wp, wsplit, bias, y, N, H, W, Cx, Cop, R, S, stride, pad, pad, pad_mode, act, slope,
                        math, (hipStream_t)stream, part, nsplit, ws, ws_bytes);
+}
+
+// vst_conv2d_fwd_ws with x's pre-split A planes apl [3][N*H*W*Cx] bf16 (NHWC, the RNE split of each value: written
+// by the producing IN pass, vst_instnorm_act_fwd_cp_apre / vst_instnorm_act_bwd_planes_apre): the x6 256x128 channel-
+// slice plans stage A from them by LDS-DMA (no fp32 A image, no split in the staging), results bit-identical; other
+// plans read x.
+extern "C" int vst_conv2d_fwd_apre_ws(const float* x, const void* apl, const float* wp, const void* wsplit,
+                                      const float* bias, float* y, int N, int H, int W, int Cx, int Cop, int R, int S,
+                                      int stride, int pad, int pad_mode, int act, float slope, int math, double* part,
+                                      int* nsplit, float* ws, size_t ws_bytes, void* stream) {
+  g_apre = ApreArgs{reinterpret_cast<const __bf16*>(apl), (long)N * H * W * Cx};
+  const int rc = conv_fwd_impl(x, wp, wsplit, bias, y, N, H, W, Cx, Cop, R, S, stride, pad, pad, pad_mode, act, slope,
+                               math, (hipStream_t)stream, part, nsplit, ws, ws_bytes);
+  g_apre = ApreArgs{nullptr, 0};
+  return rc;
 }
 
 // A forward conv over relu(IN(x)): x = the raw output of the previous conv, nst = its InstanceNorm

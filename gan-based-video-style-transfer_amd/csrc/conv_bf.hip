@@ -975,7 +975,10 @@ __device__ __forceinline__ void conv_fprop_bf_body(
   // elements) by LDS-DMA like B — no fp32 A image, no split in the staging.  VST_BF_FAKE_ADMA (developer timing
   // only, WRONG results): every GLDS kernel DMAs A from x's own bytes read as planes.
   constexpr bool GLDS_A = (APRE || VST_BF_FAKE_ADMA) && GLDS && !NRM;
-  static_assert(!APRE || GLDS_A, "pre-split A: the x6 M16 channel-slice kernels with LDS-DMA B");
+  // APRE without the DMA (the K-restricted border GEMM, REFL 5): A's planes loaded into registers and put back
+  // together as fp32 (hi + mid + lo is the value exactly), then staged as usual — the same planes in LDS
+  constexpr bool APRE_REG = APRE && !GLDS_A;
+  static_assert(!APRE || GLDS_A || REFL == 5, "pre-split A: the x6 M16 channel-slice kernels with LDS-DMA B, or REFL 5");
   const __bf16* apl_ = VST_BF_FAKE_ADMA ? reinterpret_cast<const __bf16*>(x) : apl;
   const long pps_ = VST_BF_FAKE_ADMA ? (long)(M / (Ho * Wo)) * H * W * C / 2 : pps;
   float4 nr[2][NRM ? 4 : 1];  // NRM: (mean, rstd) of the stage's 8 channels, per register set
@@ -1023,6 +1026,23 @@ __device__ __forceinline__ void conv_fprop_bf_body(
       const bool tap0 = KSL && tr == 0 && ts == 0;
       // 4: every row reads the first pixel's channel slice (real, changing values, one cache line)
       const bool fake = VST_BF_FAKE_ZA == 1 || (VST_BF_FAKE_ZA == 2 && !tap0) || (VST_BF_FAKE_ZA == 3 && tap0);
+      if constexpr (APRE_REG) {
+        const bool live = kin && aoff[j] >= 0;
+        const __bf16* q = live ? apl + aoff[j] + ka : reinterpret_cast<const __bf16*>(zp);
+        const long ps = live ? pps : 0;
+        const u32x4_t h = *reinterpret_cast<const u32x4_t*>(q), m = *reinterpret_cast<const u32x4_t*>(q + ps),
+                      l = *reinterpret_cast<const u32x4_t*>(q + 2 * ps);
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[2 * e] = (__uint_as_float(h[e] << 16) + __uint_as_float(m[e] << 16)) + __uint_as_float(l[e] << 16);
+          v[2 * e + 1] = (__uint_as_float(h[e] & 0xffff0000u) + __uint_as_float(m[e] & 0xffff0000u)) +
+                         __uint_as_float(l[e] & 0xffff0000u);
+        }
+        ra[set][j][0] = make_float4(v[0], v[1], v[2], v[3]);
+        ra[set][j][1] = make_float4(v[4], v[5], v[6], v[7]);
+        continue;
+      }
       const float* p = (kin && aoff[j] >= 0 && !fake) ? x + (VST_BF_FAKE_ZA == 4 ? 0 : aoff[j]) + ka : zp;
       ra[set][j][0] = *reinterpret_cast<const float4*>(p);
       ra[set][j][1] = *reinterpret_cast<const float4*>(p + 4);
@@ -1350,14 +1370,18 @@ __device__ __forceinline__ void conv_fprop_bf_body(
     }
 }
 
-template <class T, bool KSL, int REFL, bool SPLIT = false>
+// APRE: the A operand from apl (x's three bf16 planes, NHWC, plane stride pps elements) by LDS-DMA
+template <class T, bool KSL, int REFL, bool SPLIT = false, bool APRE = false>
 __global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_k(
     const float* __restrict__ x, const __bf16* __restrict__ ws, long wps, const float* __restrict__ bias,
     float* __restrict__ y, int H, int W, int C, int Ho, int Wo, int Cop, int S, int st, int padh,
     int padw, int reflect, int act, float slope, int M, int Ktot, int m_base, double* __restrict__ part,
-    int spk = 0, float* __restrict__ slab = nullptr, const float* __restrict__ addend = nullptr, int oph = 0) {
-  conv_fprop_bf_body<T, KSL, REFL, SPLIT>(blockIdx.x, x, ws, wps, bias, y, H, W, C, Ho, Wo, Cop, S, st, padh, padw,
-                                          reflect, act, slope, M, Ktot, m_base, part, spk, slab, addend, oph);
+    int spk = 0, float* __restrict__ slab = nullptr, const float* __restrict__ addend = nullptr, int oph = 0,
+    const __bf16* __restrict__ apl = nullptr, long pps = 0) {
+  conv_fprop_bf_body<T, KSL, REFL, SPLIT, false, APRE>(blockIdx.x, x, ws, wps, bias, y, H, W, C, Ho, Wo, Cop, S, st,
+                                                       padh, padw, reflect, act, slope, M, Ktot, m_base, part, spk,
+                                                       slab, addend, oph, nullptr, nullptr, 0, 0, 0, 0, InbArgs{}, apl,
+                                                       pps);
 }
 
 // The interior conv of the reflect-pad-1 data gradient with the border GEMM's slabs (written before it)
@@ -1374,13 +1398,14 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_bord_k(
 
 // The interior conv of the reflect-pad-1 data gradient (+ addend) with the IN-backward partials of the
 // layer below in its epilogue (InbArgs); M = the rows of this launch (whole 256x128 rounds).
-template <class T>
+template <class T, bool APRE = false>
 __global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_inb_k(
     const float* __restrict__ x, const __bf16* __restrict__ ws, long wps, float* __restrict__ y, int H, int W, int C,
-    int Cop, const float* __restrict__ addend, int M, int Ktot, InbArgs inb) {
-  conv_fprop_bf_body<T, true, 0, false>(blockIdx.x, x, ws, wps, nullptr, y, H, W, C, H, W, Cop, 3, 1, 1, 1, 0,
-                                        VST_ACT_NONE, 0.f, M, Ktot, 0, nullptr, 0, nullptr, addend, 0, nullptr, nullptr,
-                                        0, 0, 0, 0, inb);
+    int Cop, const float* __restrict__ addend, int M, int Ktot, InbArgs inb, const __bf16* __restrict__ apl = nullptr,
+    long pps = 0) {
+  conv_fprop_bf_body<T, true, 0, false, false, APRE>(blockIdx.x, x, ws, wps, nullptr, y, H, W, C, H, W, Cop, 3, 1, 1,
+                                                     1, 0, VST_ACT_NONE, 0.f, M, Ktot, 0, nullptr, 0, nullptr, addend, 0,
+                                                     nullptr, nullptr, 0, 0, 0, 0, inb, apl, pps);
 }
 
 // conv_fprop_bf_k over relu(IN(x)) (NRM: the normalisation in the A staging; nst = x's IN statistics)
@@ -1798,6 +1823,7 @@ __global__ void split3_k(const float* __restrict__ w, __bf16* __restrict__ out, 
 //   6: 64x64, 4 waves of 32x32, BK 32      7: 256x128, 8 waves of 64x64, BK 32
 //   8: 64x64, 4 waves of 32x32, BK 32 (x6) / 64 (x3)
 //   9: 128x128, 4 waves of 64x64, BK 16 (x6: two blocks / CU)
+//  10: 256x64, 4 waves of 64x64, BK 32 (x6: the image-layer weight gradients, M = 147 rows in one tile)
 #define VST_BF_DISPATCH(kind, np, L)                                   \
   switch (kind) {                                                      \
     case 1: L(128, 64, 64, 32, 32, np) break;                          \
@@ -1809,6 +1835,7 @@ __global__ void split3_k(const float* __restrict__ w, __bf16* __restrict__ out, 
     case 7: L(256, 128, 64, 64, 32, np) break;                         \
     case 8: L(64, 64, 32, 32, (np == 3 ? 32 : 64), np) break;          \
     case 9: L(128, 128, 64, 64, 16, np) break;                         \
+    case 10: L(256, 64, 64, 64, 32, np) break;                         \
     default: L(128, 128, 64, 32, 32, np) break;                        \
   }
 
@@ -1834,6 +1861,7 @@ static void bf_geom(int kind, int np, int* bm, int* bn, int* slots) {
     case 7: BM = 256; break;
     case 8: BM = 64; BN = 64; BK = np == 3 ? 32 : 64; break;
     case 9: BK = 16; break;
+    case 10: BM = 256; BN = 64; break;
     default: break;
   }
   const int stage = np * (BM + BN) * BK * 2;
@@ -1993,6 +2021,11 @@ bool bf_fprop_nrm_ok(int N, int H, int W, int C, int Cop, int R, int S, int st, 
   return (kd == 7 && (!m_split || ks)) || (ks && !m_first);
 }
 
+// The A operand's pre-split planes for the next bf_fprop_launch on this host thread (vst_conv2d_fwd_apre_ws sets
+// them around its call): taken by the x6 256x128 channel-slice launches (whole rounds and the split-K form),
+// ignored by every other plan (x itself stays valid).
+thread_local ApreArgs g_apre = {nullptr, 0};
+
 static const int g_fs_tile = [] {  // developer A/B of the all-split-K tile (bf_fprop_launch)
   const char* e = getenv("VST_FULLSPLIT_TILE");
   return e ? atoi(e) : 0;
@@ -2019,6 +2052,8 @@ int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* b
   if (kind < 0 && padh == padw && !addend && !oph && c4_direct_ok(C, Cop, R, S, st, Ho, Wo, math))
     return c4_direct_launch(x, wsplit, wps, bias, y, N, H, W, Ho, Wo, R, S, padh, reflect, act, slope, math, part, s);
   const __bf16* ws = reinterpret_cast<const __bf16*>(wsplit);
+  const __bf16* apl = (!nst && !oph && VST_BF_KSLICE && C % 32 == 0 && math == VST_MATH_BF16X6) ? g_apre.apl : nullptr;
+  const long pps = g_apre.pps;
   int kd, m_split, tail_kind;
   bf_plan(M, Cop, math, kind, &kd, &m_split, &tail_kind);
   int ks = 0, m_first = 0;
@@ -2082,6 +2117,14 @@ int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* b
       if (nst)
         hipLaunchKernelGGL((bf::conv_fprop_bf_nrm_k<T, true>), grid, dim3(T::NT), 0, s, x, ws, wps, bias, y, H, W, C,
                            Ho, Wo, Cop, S, st, padh, padw, act, slope, M, K, mb, part, spk, tws, nst);
+      else if (apl && reflect)
+        hipLaunchKernelGGL((bf::conv_fprop_bf_k<T, true, 1, true, true>), grid, dim3(T::NT), 0, s, x, ws, wps, bias, y,
+                           H, W, C, Ho, Wo, Cop, S, st, padh, padw, reflect, act, slope, M, K, mb, part, spk, tws,
+                           nullptr, 0, apl, pps);
+      else if (apl)
+        hipLaunchKernelGGL((bf::conv_fprop_bf_k<T, true, 0, true, true>), grid, dim3(T::NT), 0, s, x, ws, wps, bias, y,
+                           H, W, C, Ho, Wo, Cop, S, st, padh, padw, reflect, act, slope, M, K, mb, part, spk, tws,
+                           nullptr, 0, apl, pps);
       else if (reflect)
         hipLaunchKernelGGL((bf::conv_fprop_bf_k<T, true, 1, true>), grid, dim3(T::NT), 0, s, x, ws, wps, bias, y, H,
                            W, C, Ho, Wo, Cop, S, st, padh, padw, reflect, act, slope, M, K, mb, part, spk, tws,
@@ -2100,6 +2143,19 @@ int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* b
       const dim3 grid(ceil_div(Mend - mb, 256) * ceil_div(Cop, 128));
       hipLaunchKernelGGL((bf::conv_fprop_bf_nrm_k<T, false>), grid, dim3(T::NT), 0, s, x, ws, wps, bias, y, H, W, C,
                          Ho, Wo, Cop, S, st, padh, padw, act, slope, Mend, K, mb, part, 0, nullptr, nst);
+      continue;
+    }
+    if (apl && kp == 7) {  // whole 256x128 rounds on the pre-split A planes
+      using T = bf::Tile<256, 128, 64, 64, 32, 3>;
+      const dim3 grid(ceil_div(Mend - mb, 256) * ceil_div(Cop, 128));
+      if (reflect)
+        hipLaunchKernelGGL((bf::conv_fprop_bf_k<T, true, 1, false, true>), grid, dim3(T::NT), 0, s, x, ws, wps, bias, y,
+                           H, W, C, Ho, Wo, Cop, S, st, padh, padw, reflect, act, slope, Mend, K, mb, part, 0, nullptr,
+                           addend, 0, apl, pps);
+      else
+        hipLaunchKernelGGL((bf::conv_fprop_bf_k<T, true, 0, false, true>), grid, dim3(T::NT), 0, s, x, ws, wps, bias, y,
+                           H, W, C, Ho, Wo, Cop, S, st, padh, padw, reflect, act, slope, Mend, K, mb, part, 0, nullptr,
+                           addend, 0, apl, pps);
       continue;
     }
     if (math == VST_MATH_BF16X6) {
@@ -2292,7 +2348,8 @@ bool bf_dgrad_refl1_inb_ok(int N, int H, int W, int Cy, int Cx, int math) {
 
 int bf_dgrad_refl1_inb_launch(const float* dy, const void* wsplit, long wps, const float* addend, float* dx, int N,
                               int H, int W, int Cy, int Cx, int math, hipStream_t s, float* ws, size_t ws_floats,
-                              const float* z, const float* st, double* part, int act, float slope) {
+                              const float* z, const float* st, double* part, int act, float slope,
+                              const __bf16* apl, long pps) {
   VST_REQUIRE(bf_dgrad_refl1_inb_ok(N, H, W, Cy, Cx, math), "conv2d_dgrad_refl_in_epi: unsupported shape / arithmetic");
   const long M = (long)N * H * W;
   int kd, m_split, tail_kind, m_first, fks;
@@ -2308,14 +2365,26 @@ int bf_dgrad_refl1_inb_launch(const float* dy, const void* wsplit, long wps, con
   using T = bf::Tile<256, 128, 64, 64, 32, 3>;
   // rows [0, mb): whole rounds with the partials in the epilogue; [mb, M): split-K + the reducing pass
   const long mb = (fks && !m_first) ? 0 : (m_split ? m_split : M);
-  if (mb > 0)
-    hipLaunchKernelGGL((bf::conv_fprop_bf_inb_k<T>), dim3(ceil_div(mb, 256) * ceil_div(Cx, 128)), dim3(T::NT), 0, s, dy,
-                       wb, wps, dx, H, W, Cy, Cx, addend, (int)mb, K, inb);
+  if (mb > 0) {
+    const dim3 grid(ceil_div(mb, 256) * ceil_div(Cx, 128));
+    if (apl)
+      hipLaunchKernelGGL((bf::conv_fprop_bf_inb_k<T, true>), grid, dim3(T::NT), 0, s, dy, wb, wps, dx, H, W, Cy, Cx,
+                         addend, (int)mb, K, inb, apl, pps);
+    else
+      hipLaunchKernelGGL((bf::conv_fprop_bf_inb_k<T>), grid, dim3(T::NT), 0, s, dy, wb, wps, dx, H, W, Cy, Cx, addend,
+                         (int)mb, K, inb);
+  }
   if (mb < M) {
     const int nk = (K + T::BK - 1) / T::BK, spk = (nk + fks - 1) / fks;
-    hipLaunchKernelGGL((bf::conv_fprop_bf_k<T, true, 0, true>), dim3(ceil_div(M - mb, 256) * ceil_div(Cx, 128) * fks),
-                       dim3(T::NT), 0, s, dy, wb, wps, nullptr, dx, H, W, Cy, H, W, Cx, 3, 1, 1, 1, 0, VST_ACT_NONE, 0.f,
-                       (int)M, K, (int)mb, nullptr, spk, ws, nullptr);
+    const dim3 grid(ceil_div(M - mb, 256) * ceil_div(Cx, 128) * fks);
+    if (apl)
+      hipLaunchKernelGGL((bf::conv_fprop_bf_k<T, true, 0, true, true>), grid, dim3(T::NT), 0, s, dy, wb, wps, nullptr, dx,
+                         H, W, Cy, H, W, Cx, 3, 1, 1, 1, 0, VST_ACT_NONE, 0.f, (int)M, K, (int)mb, nullptr, spk, ws,
+                         nullptr, 0, apl, pps);
+    else
+      hipLaunchKernelGGL((bf::conv_fprop_bf_k<T, true, 0, true>), grid, dim3(T::NT), 0, s, dy, wb, wps, nullptr, dx, H,
+                         W, Cy, H, W, Cx, 3, 1, 1, 1, 0, VST_ACT_NONE, 0.f, (int)M, K, (int)mb, nullptr, spk, ws,
+                         nullptr);
     hipLaunchKernelGGL(bf::fprop_splitk_reduce_inb_k, dim3(ceil_div(M - mb, 32), ceil_div(Cx, 64)), dim3(256), 0, s, ws,
                        fks, (int)mb, (int)M, Cx, dx, H * W, addend, inb);
   }
@@ -2323,9 +2392,14 @@ int bf_dgrad_refl1_inb_launch(const float* dy, const void* wsplit, long wps, con
   {
     using T5 = bf::Tile<128, 128, 64, 32, 32, 3>;
     const int nk = (K5 + T5::BK - 1) / T5::BK, spk = (nk + ks5 - 1) / ks5;
-    hipLaunchKernelGGL((bf::conv_fprop_bf_k<T5, true, 5, true>), dim3(Mt / 128 * ceil_div(Cx, 128) * ks5), dim3(T5::NT),
-                       0, s, dy, wb, wps, nullptr, dx, H, W, Cy, lt, ll, Cx, 3, N, 1, 1, 0, VST_ACT_NONE, 0.f, Mt, K5, 0,
-                       nullptr, spk, slab, nullptr);
+    const dim3 grid(Mt / 128 * ceil_div(Cx, 128) * ks5);
+    if (apl)  // dy given as planes only (its fp32 image is not written): the border rows read them
+      hipLaunchKernelGGL((bf::conv_fprop_bf_k<T5, true, 5, true, true>), grid, dim3(T5::NT), 0, s, dy, wb, wps, nullptr,
+                         dx, H, W, Cy, lt, ll, Cx, 3, N, 1, 1, 0, VST_ACT_NONE, 0.f, Mt, K5, 0, nullptr, spk, slab,
+                         nullptr, 0, apl, pps);
+    else
+      hipLaunchKernelGGL((bf::conv_fprop_bf_k<T5, true, 5, true>), grid, dim3(T5::NT), 0, s, dy, wb, wps, nullptr, dx,
+                         H, W, Cy, lt, ll, Cx, 3, N, 1, 1, 0, VST_ACT_NONE, 0.f, Mt, K5, 0, nullptr, spk, slab, nullptr);
   }
   hipLaunchKernelGGL(bf::dgrad_border5_add_inb_k, dim3(ceil_div(2 * W + 2 * H, 16), N, ceil_div(Cx, 64)), dim3(256), 0,
                      s, slab, ks5, Mt, Cx, dx, H, W, lt, ll, inb, H * W / 32);

@@ -98,7 +98,10 @@ struct PackJob {
 };
 static_assert(sizeof(PackJob) == 168, "PackJob layout is part of the C ABI (include/vst_hip.h)");
 
-__global__ __launch_bounds__(256) void weight_pack_batch_k(const PackJob* __restrict__ jobs, int nj) {
+// One 64-lane block per 256-element job block (PackJob.block0 units): a lane packs 4 consecutive elements (their
+// gathers issued together), stores them as one float4 and each split plane as one 8-byte word — the per-element
+// form moved ~1.5 TB/s (narrow stores, one gather in flight per lane).
+__global__ __launch_bounds__(64) void weight_pack_batch_k(const PackJob* __restrict__ jobs, int nj) {
   const long b = blockIdx.x;
   int lo = 0, hi = nj - 1;
   while (lo < hi) {
@@ -107,15 +110,47 @@ __global__ __launch_bounds__(256) void weight_pack_batch_k(const PackJob* __rest
     else hi = mid - 1;
   }
   const PackJob& J = jobs[lo];
-  const long idx = (b - J.block0) * 256 + threadIdx.x;
-  if (idx >= J.total) return;
-  int o, i, rs;
-  pack_coords(idx, J.R, J.S, J.Op, J.Ip, J.mode, o, i, rs);
-  const int r = rs / J.S, s = rs - r * J.S;
-  const int rr = J.tr[0] < 0 ? r : J.tr[r], ss = J.ts[0] < 0 ? s : J.ts[s];  // tr[0] < 0: identity
-  const float v = (o < J.O && i < J.I) ? J.w[o * J.so + i * J.si + rr * J.sr + ss * J.ss] : 0.f;
-  J.out[idx] = v;
-  if (J.split) store_split(J.split, J.total, idx, v);
+  const long idx0 = (b - J.block0) * 256 + 4 * threadIdx.x;
+  if (idx0 >= J.total) return;
+  float v[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    v[e] = 0.f;
+    const long idx = idx0 + e;
+    if (idx >= J.total) continue;
+    int o, i, rs;
+    pack_coords(idx, J.R, J.S, J.Op, J.Ip, J.mode, o, i, rs);
+    const int r = rs / J.S, s = rs - r * J.S;
+    const int rr = J.tr[0] < 0 ? r : J.tr[r], ss = J.ts[0] < 0 ? s : J.ts[s];  // tr[0] < 0: identity
+    if (o < J.O && i < J.I) v[e] = J.w[o * J.so + i * J.si + rr * J.sr + ss * J.ss];
+  }
+  if (J.total % 4 == 0) {  // idx0 % 4 == 0: aligned float4 / 8-byte plane words
+    *reinterpret_cast<float4*>(J.out + idx0) = make_float4(v[0], v[1], v[2], v[3]);
+    if (J.split) {
+      uint16_t q[3][4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const __bf16 h = (__bf16)v[e];
+        const float r = v[e] - (float)h;
+        const __bf16 m = (__bf16)r;
+        const __bf16 l = (__bf16)(r - (float)m);
+        q[0][e] = __builtin_bit_cast(uint16_t, h);
+        q[1][e] = __builtin_bit_cast(uint16_t, m);
+        q[2][e] = __builtin_bit_cast(uint16_t, l);
+      }
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        *reinterpret_cast<uint2*>(J.split + p * J.total + idx0) =
+            make_uint2(q[p][0] | ((uint32_t)q[p][1] << 16), q[p][2] | ((uint32_t)q[p][3] << 16));
+    }
+    return;
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    if (idx0 + e >= J.total) break;
+    J.out[idx0 + e] = v[e];
+    if (J.split) store_split(J.split, J.total, idx0 + e, v[e]);
+  }
 }
 
 // w[O][I][R][S] -> one pack (modes as pack_coords), optionally with its split planes
@@ -204,7 +239,7 @@ extern "C" int vst_weight_pack_split(const float* w, float* out, void* split, in
 
 extern "C" int vst_weight_pack_batch(const void* jobs, int njobs, long nblocks, void* stream) {
   VST_REQUIRE(jobs && njobs > 0 && nblocks > 0 && nblocks < (1L << 31), "weight_pack_batch: bad args");
-  hipLaunchKernelGGL(weight_pack_batch_k, dim3((unsigned)nblocks), dim3(256), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(weight_pack_batch_k, dim3((unsigned)nblocks), dim3(64), 0, (hipStream_t)stream,
                      reinterpret_cast<const PackJob*>(jobs), njobs);
   return check_launch("weight_pack_batch");
 }

@@ -438,9 +438,11 @@ __global__ void in_bwd_finalize_k(const double* __restrict__ part, const float* 
 }
 
 
+__device__ __forceinline__ void store_planes4(__bf16* __restrict__ pl, long pps, long e, float4 v);
+
 __global__ void in_apply_k(const float4* __restrict__ x, const float* __restrict__ stats,
                            const float4* __restrict__ res, float4* __restrict__ y, long total4,
-                           int HW, int C4, int act, float slope) {
+                           int HW, int C4, int act, float slope, __bf16* __restrict__ apl = nullptr) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total4) return;
   const int c4 = i % C4;
@@ -455,6 +457,7 @@ __global__ void in_apply_k(const float4* __restrict__ x, const float* __restrict
   v.w = apply_act((v.w - s1.z) * s1.w, act, slope);
   if (res) add_f4(v, res[i]);
   y[i] = v;
+  if (apl) store_planes4(apl, total4 * 4, i * 4, v);
 }
 
 // RNE bf16 pair (the split of vst_weight_split / nhwc_to_cp_planes_k)
@@ -463,6 +466,23 @@ __device__ __forceinline__ uint32_t bf16_pack2(float a, float b) {
   typedef __bf16 b2 __attribute__((ext_vector_type(2)));
   const f2 v = {a, b};
   return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, b2));
+}
+
+// v's three bf16 planes (hi, mid, lo: the RNE split of nhwc_to_cp_planes_k / split8) at element e of planes
+// [3][pps] — the NHWC A-operand planes of an x6 forward that takes its A operand pre-split (APRE)
+__device__ __forceinline__ void store_planes4(__bf16* __restrict__ pl, long pps, long e, float4 v) {
+  float r[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int p = 0; p < 3; ++p) {
+    const uint32_t q0 = bf16_pack2(r[0], r[1]), q1 = bf16_pack2(r[2], r[3]);
+    *reinterpret_cast<uint2*>(pl + p * pps + e) = make_uint2(q0, q1);
+    if (p < 2) {
+      r[0] -= __uint_as_float(q0 << 16);
+      r[1] -= __uint_as_float(q0 & 0xffff0000u);
+      r[2] -= __uint_as_float(q1 << 16);
+      r[3] -= __uint_as_float(q1 & 0xffff0000u);
+    }
+  }
 }
 
 // in_apply_k fused with the weight gradient's A-operand image of the conv that consumes the result:
@@ -478,7 +498,8 @@ __global__ __launch_bounds__(256) void in_apply_cp_pad_k(const float* __restrict
                                                           const float* __restrict__ res, float* __restrict__ a,
                                                           float* __restrict__ xt, int N, int H, int W, int C,
                                                           int pad, int reflect, int phase, long ld, int act,
-                                                          float slope, int wx = 0, __bf16* __restrict__ planes = nullptr) {
+                                                          float slope, int wx = 0, __bf16* __restrict__ planes = nullptr,
+                                                          __bf16* __restrict__ apl = nullptr) {
   __shared__ float tile[64][65];
   const int Hp = H + 2 * pad, Wp = W + 2 * pad, Wq = Wp + wx;
   const long P = (long)N * Hp * Wq;
@@ -517,7 +538,10 @@ __global__ __launch_bounds__(256) void in_apply_cp_pad_k(const float* __restrict
         v.z = apply_act((v.z - s1.x) * s1.y, act, slope);
         v.w = apply_act((v.w - s1.z) * s1.w, act, slope);
         if (res) add_f4(v, *reinterpret_cast<const float4*>(res + e));
-        if (inner) *reinterpret_cast<float4*>(a + e) = v;
+        if (inner) {
+          *reinterpret_cast<float4*>(a + e) = v;
+          if (apl) store_planes4(apl, (long)N * H * W * C, e, v);
+        }
       }
     }
     tile[pr][c4] = v.x;
@@ -622,7 +646,7 @@ __global__ __launch_bounds__(256) void in_bwd_apply_planes_k(const float* __rest
                                                               __bf16* __restrict__ planes, long P, int HW, int C,
                                                               long ldp, int act, float slope,
                                                               const double* __restrict__ dbn, float* __restrict__ db,
-                                                              int N, int accumulate_db) {
+                                                              int N, int accumulate_db, __bf16* __restrict__ apl = nullptr) {
   __shared__ float tile[64][65];
   const long p0 = (long)blockIdx.x * 64;
   const int c0 = blockIdx.y * 64;
@@ -645,7 +669,8 @@ __global__ __launch_bounds__(256) void in_bwd_apply_planes_k(const float* __rest
       o.y = in_bwd1(g.y, v.y, s0.z, s0.w, make_float2(k01.z, k01.w), act, slope);
       o.z = in_bwd1(g.z, v.z, s1.x, s1.y, make_float2(k23.x, k23.y), act, slope);
       o.w = in_bwd1(g.w, v.w, s1.z, s1.w, make_float2(k23.z, k23.w), act, slope);
-      *reinterpret_cast<float4*>(dx + q * C + c0 + c4) = o;
+      if (apl) store_planes4(apl, P * C, q * C + c0 + c4, o);  // dx as its NHWC planes only
+      else *reinterpret_cast<float4*>(dx + q * C + c0 + c4) = o;
     }
     tile[pr][c4] = o.x;
     tile[pr][c4 + 1] = o.y;
@@ -1003,6 +1028,18 @@ extern "C" int vst_instnorm_act_bwd_planes(const float* gy, const float* x, cons
                                            float* db, float* ws, int N, int HW, int C, int act, float slope,
                                            int accumulate_db, void* planes, long ldp, void* stream);
 
+// vst_instnorm_act_fwd that also writes y's NHWC bf16 planes apl [3][N*HW*C] (the pre-split A operand of the x6
+// forward that consumes y: vst_conv2d_fwd_apre_ws)
+extern "C" int vst_instnorm_act_fwd_apre(const float* x, const float* stats, const float* residual, float* y, void* apl,
+                                         int N, int HW, int C, int act, float slope, void* stream) {
+  VST_REQUIRE(x && stats && y && apl && C % 4 == 0, "instnorm_act_fwd_apre: bad args");
+  const long total4 = (long)N * HW * C / 4;
+  hipLaunchKernelGGL(in_apply_k, dim3(ceil_div(total4, 256)), dim3(256), 0, (hipStream_t)stream,
+                     reinterpret_cast<const float4*>(x), stats, reinterpret_cast<const float4*>(residual),
+                     reinterpret_cast<float4*>(y), total4, HW, C / 4, act, slope, reinterpret_cast<__bf16*>(apl));
+  return check_launch("instnorm_act_fwd_apre");
+}
+
 extern "C" int vst_instnorm_act_fwd_cp(const float* x, const float* stats, const float* residual, float* y,
                                        float* xt, int N, int H, int W, int C, int act, float slope, int pad,
                                        int pad_mode, int stride, void* stream) {
@@ -1015,6 +1052,22 @@ extern "C" int vst_instnorm_act_fwd_cp(const float* x, const float* stats, const
                      x, stats, residual, y, xt, N, H, W, C, pad, pad_mode == VST_PAD_REFLECT, stride == 2,
                      rk_cp_ld(P), act, slope);
   return check_launch("instnorm_act_fwd_cp");
+}
+
+// vst_instnorm_act_fwd_cp that also writes the activation's NHWC bf16 planes apl [3][N*H*W*C] (the pre-split A
+// operand of the x6 forward that consumes it: vst_conv2d_fwd_apre_ws)
+extern "C" int vst_instnorm_act_fwd_cp_apre(const float* x, const float* stats, const float* residual, float* y,
+                                            float* xt, void* apl, int N, int H, int W, int C, int act, float slope,
+                                            int pad, int pad_mode, int stride, void* stream) {
+  VST_REQUIRE(x && stats && y && xt && apl && C % 4 == 0 && pad >= 0 && (stride == 1 || stride == 2),
+              "instnorm_act_fwd_cp_apre: bad args");
+  VST_REQUIRE(pad_mode == VST_PAD_ZERO || (pad < H && pad < W), "instnorm_act_fwd_cp_apre: reflect pad >= size");
+  VST_REQUIRE(stride == 1 || (W + 2 * pad) % 2 == 0, "instnorm_act_fwd_cp_apre: stride 2 needs W + 2 pad even");
+  const long P = (long)N * (H + 2 * pad) * (W + 2 * pad);
+  hipLaunchKernelGGL(in_apply_cp_pad_k, dim3(ceil_div(P, 64), ceil_div(C, 64)), dim3(256), 0, (hipStream_t)stream,
+                     x, stats, residual, y, xt, N, H, W, C, pad, pad_mode == VST_PAD_REFLECT, stride == 2,
+                     rk_cp_ld(P), act, slope, 0, nullptr, reinterpret_cast<__bf16*>(apl));
+  return check_launch("instnorm_act_fwd_cp_apre");
 }
 
 extern "C" int vst_instnorm_act_fwd_planes(const float* x, const float* stats, const float* residual, float* y,
@@ -1039,7 +1092,7 @@ extern "C" int vst_instnorm_act_bwd(const float* gy, const float* x, const float
 // IN backward after its partials are in ws: finalize, bias gradient, apply (+ planes).
 static int in_bwd_tail(const float* gy, const float* x, const float* stats, float* dx, float* db, float* ws,
                        int N, int HW, int C, int act, float slope, int accumulate_db, void* planes, long ldp,
-                       const RedGeom& g, hipStream_t s);
+                       const RedGeom& g, hipStream_t s, void* apl = nullptr);
 
 extern "C" int vst_instnorm_act_bwd_planes(const float* gy, const float* x, const float* stats, float* dx,
                                            float* db, float* ws, int N, int HW, int C, int act, float slope,
@@ -1052,6 +1105,21 @@ extern "C" int vst_instnorm_act_bwd_planes(const float* gy, const float* x, cons
   hipLaunchKernelGGL(in_partial_k<1>, dim3(g.nsplit, N), dim3(NRED), 0, s, x, gy, stats, part, HW, C,
                      g.LP, g.PG, g.SP, g.nsplit, act, slope);
   return in_bwd_tail(gy, x, stats, dx, db, ws, N, HW, C, act, slope, accumulate_db, planes, ldp, g, s);
+}
+
+// vst_instnorm_act_bwd_planes that also writes dx's NHWC bf16 planes apl [3][N*HW*C] (the A operand of the x6
+// data gradient that consumes dx, pre-split: vst_conv2d_dgrad_refl_epi_part's apl)
+extern "C" int vst_instnorm_act_bwd_planes_apre(const float* gy, const float* x, const float* stats, float* dx,
+                                                float* db, float* ws, int N, int HW, int C, int act, float slope,
+                                                int accumulate_db, void* planes, long ldp, void* apl, void* stream) {
+  RedGeom g;
+  VST_REQUIRE(gy && x && stats && dx && ws && planes && apl && red_geom(N, HW, C, g), "instnorm_act_bwd_apre: bad args");
+  VST_REQUIRE(ldp >= (long)N * HW, "instnorm_act_bwd_apre: plane stride %ld < N*HW", ldp);
+  hipStream_t s = (hipStream_t)stream;
+  double* part = reinterpret_cast<double*>(ws);
+  hipLaunchKernelGGL(in_partial_k<1>, dim3(g.nsplit, N), dim3(NRED), 0, s, x, gy, stats, part, HW, C,
+                     g.LP, g.PG, g.SP, g.nsplit, act, slope);
+  return in_bwd_tail(gy, x, stats, dx, db, ws, N, HW, C, act, slope, accumulate_db, planes, ldp, g, s, apl);
 }
 
 extern "C" int vst_reflect_fold_instnorm_bwd(const float* dxp, const float* addend, float* gout, const float* x,
@@ -1144,10 +1212,10 @@ extern "C" size_t vst_conv2d_dgrad_refl_in_epi_ws_bytes(int N, int H, int W, int
 }
 
 // the two halves (the data gradient can then be timed on its own): the data gradient + partials, the tail
-extern "C" int vst_conv2d_dgrad_refl_epi_part(const float* dy, const void* wsplit, const float* addend, float* gout,
-                                              const float* x, const float* stats, float* ws, size_t ws_bytes, int N,
-                                              int H, int W, int Cy, int Cx, int act, float slope, int math,
-                                              void* stream) {
+extern "C" int vst_conv2d_dgrad_refl_epi_part(const float* dy, const void* dy_apl, const void* wsplit,
+                                              const float* addend, float* gout, const float* x, const float* stats,
+                                              float* ws, size_t ws_bytes, int N, int H, int W, int Cy, int Cx, int act,
+                                              float slope, int math, void* stream) {
   const size_t need = vst_conv2d_dgrad_refl_in_epi_ws_bytes(N, H, W, Cy, Cx, math);
   VST_REQUIRE(dy && wsplit && gout && x && stats && ws, "conv2d_dgrad_refl_in_epi: null pointer");
   VST_REQUIRE(need > 0 && ws_bytes >= need,
@@ -1156,18 +1224,19 @@ extern "C" int vst_conv2d_dgrad_refl_epi_part(const float* dy, const void* wspli
   float* dws = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + inb);
   return bf_dgrad_refl1_inb_launch(dy, wsplit, (long)Cx * 9 * Cy, addend, gout, N, H, W, Cy, Cx, math,
                                    (hipStream_t)stream, dws, (ws_bytes - inb) / sizeof(float), x, stats,
-                                   reinterpret_cast<double*>(ws), act, slope);
+                                   reinterpret_cast<double*>(ws), act, slope, reinterpret_cast<const __bf16*>(dy_apl),
+                                   (long)N * H * W * Cy);
 }
 
 extern "C" int vst_instnorm_act_bwd_epi_tail(const float* gout, const float* x, const float* stats, float* dx,
                                              float* db, float* ws, int N, int H, int W, int Cx, int act, float slope,
-                                             int accumulate_db, void* planes, long ldp, void* stream) {
+                                             int accumulate_db, void* planes, long ldp, void* apl, void* stream) {
   VST_REQUIRE(gout && x && stats && dx && ws && Cx % 4 == 0 && (H * W) % 32 == 0, "instnorm_act_bwd_epi_tail: bad args");
   VST_REQUIRE(!planes || ldp >= (long)N * H * W, "instnorm_act_bwd_epi_tail: plane stride %ld < N*HW", ldp);
   RedGeom g{};
   g.nsplit = bf_dgrad_refl1_inb_slices(H, W);
   return in_bwd_tail(gout, x, stats, dx, db, ws, N, H * W, Cx, act, slope, accumulate_db, planes, ldp, g,
-                     (hipStream_t)stream);
+                     (hipStream_t)stream, apl);
 }
 
 extern "C" int vst_conv2d_dgrad_refl_in_epi(const float* dy, const void* wsplit, const float* addend, float* gout,
@@ -1175,16 +1244,16 @@ extern "C" int vst_conv2d_dgrad_refl_in_epi(const float* dy, const void* wsplit,
                                             size_t ws_bytes, int N, int H, int W, int Cy, int Cx, int act, float slope,
                                             int accumulate_db, void* planes, long ldp, int math, void* stream) {
   VST_REQUIRE(dx, "conv2d_dgrad_refl_in_epi: null pointer");
-  if (int e = vst_conv2d_dgrad_refl_epi_part(dy, wsplit, addend, gout, x, stats, ws, ws_bytes, N, H, W, Cy, Cx, act,
-                                             slope, math, stream))
+  if (int e = vst_conv2d_dgrad_refl_epi_part(dy, nullptr, wsplit, addend, gout, x, stats, ws, ws_bytes, N, H, W, Cy,
+                                             Cx, act, slope, math, stream))
     return e;
   return vst_instnorm_act_bwd_epi_tail(gout, x, stats, dx, db, ws, N, H, W, Cx, act, slope, accumulate_db, planes, ldp,
-                                       stream);
+                                       nullptr, stream);
 }
 
 static int in_bwd_tail(const float* gy, const float* x, const float* stats, float* dx, float* db, float* ws,
                        int N, int HW, int C, int act, float slope, int accumulate_db, void* planes, long ldp,
-                       const RedGeom& g, hipStream_t s) {
+                       const RedGeom& g, hipStream_t s, void* apl) {
   double* part = reinterpret_cast<double*>(ws);
   float2* coef = reinterpret_cast<float2*>(reinterpret_cast<char*>(ws) +
                                            (size_t)N * g.nsplit * C * 3 * sizeof(double));
@@ -1196,11 +1265,12 @@ static int in_bwd_tail(const float* gy, const float* x, const float* stats, floa
     hipLaunchKernelGGL(in_bwd_finalize_k<16>, dim3(ceil_div(C, 16), N), dim3(256), 0, s, part, stats, coef, dbn,
                      N, HW, C, g.nsplit);
   // the bias gradient (sum over n of dbn) is taken by the apply pass's first blocks
+  VST_REQUIRE(!apl || planes, "instnorm_act_bwd: the NHWC A planes come with the weight-gradient planes");
   if (planes) {
     const long P = (long)N * HW;
     hipLaunchKernelGGL(in_bwd_apply_planes_k, dim3(ceil_div(P, 64), ceil_div(C, 64)), dim3(256), 0, s, gy, x, stats,
                        coef, dx, reinterpret_cast<__bf16*>(planes), P, HW, C, ldp, act, slope, dbn, db, N,
-                       accumulate_db);
+                       accumulate_db, reinterpret_cast<__bf16*>(apl));
     return check_launch("instnorm_act_bwd_planes");
   }
   const long total4 = (long)N * HW * C / 4;

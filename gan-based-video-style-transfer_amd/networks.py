@@ -520,6 +520,14 @@ D_CO1 = os.environ.get("VST_D_CO1", "1") != "0"
 # (ops.conv2d_tfwd -> skinny.hip MODE 1) instead of four 2x2 phase convs + the interleave pass;
 # VST_D0_TFWD=0 keeps the phases.
 D0_TFWD = os.environ.get("VST_D0_TFWD", "1") != "0"
+# The ResnetBlock convs' A operands pre-split by their producers (the IN passes write the NHWC bf16 planes; the x6
+# 256x128 forwards and data gradients stage A from them by LDS-DMA, results bit-identical).
+# Forward (VST_APRE=1: the planes beside the fp32 activation, which the residual / fallback readers keep): +0.73 ms in
+# the C2 step A/B (profiles/r05l_apre_step_ab.jsonl; in-step the forward GEMM gains ~1 %, the IN apply pays 6 B/elem).
+APRE = os.environ.get("VST_APRE", "0") == "1"
+# Backward (VST_APRE_BWD): the ResnetBlock chain's data-gradient inputs as planes ONLY (the IN backward writes no fp32
+# image: their weight gradients read the channel-major planes, the border GEMM puts the values back together).
+APRE_BWD = os.environ.get("VST_APRE_BWD", "0") == "1"
 _WPLAN_BF = 2  # ops.WPLAN_NAMES: copies + conv_wgrad_bf_k
 
 
@@ -528,14 +536,14 @@ def _wgrad_on_bf(N, H, W, Cx, Ho, Wo, Cyp, R, st, policy):
     return ops.conv_plan_wgrad(N, H, W, Cx, Ho, Wo, Cyp, R, R, st, "bwd")[0] == _WPLAN_BF
 
 
-def _in_bwd_for_wgrad(g, y, s, act, slope, db, x_in, R, st, want):
+def _in_bwd_for_wgrad(g, y, s, act, slope, db, x_in, R, st, want, apre=False):
     """instnorm_act_bwd -> (dy, dy_planes or None); planes only when the wgrad of the conv below
-    (input x_in, kernel R, stride st) takes the x6 split-bf16 path."""
+    (input x_in, kernel R, stride st) takes the x6 split-bf16 path (apre: dy's NHWC planes too)."""
     if want and IN_PLANES:
         N, H, W, Cx = x_in.shape
         _, Ho, Wo, Cyp = y.shape
         if _wgrad_on_bf(N, H, W, Cx, Ho, Wo, Cyp, R, st, ops.get_conv_math()):
-            return ops.instnorm_act_bwd(g, y, s, act, slope, db=db, planes=True)
+            return ops.instnorm_act_bwd(g, y, s, act, slope, db=db, planes=True, apre=apre)
     return ops.instnorm_act_bwd(g, y, s, act, slope, db=db), None
 
 
@@ -563,18 +571,20 @@ class _GeneratorFn(torch.autograd.Function):
             return (1, mode, st) if _wgrad_on_bf(N_, H_, W_, C_, Ho_, Wo_, cpad(cout), 3, st,
                                                  ops.get_conv_math()) else None
 
-        def in_act(y, s, act, cp, residual=None):
+        def in_act(y, s, act, cp, residual=None, apre=False):
             if cp is None:
-                return ops.instnorm_act_fwd(y, s, act, residual=residual), None
+                return ops.instnorm_act_fwd(y, s, act, residual=residual, apre=apre), None
             if cp[0] == "planes":
                 return ops.instnorm_act_fwd(y, s, act, residual=residual, xpl=cp[1])
-            return ops.instnorm_act_fwd(y, s, act, residual=residual, cp=cp)
+            return ops.instnorm_act_fwd(y, s, act, residual=residual, cp=cp, apre=apre)
+
+        rb_in = (4 * ngf, 1, "reflect")  # the ResnetBlock convs' geometry (their inputs carry pre-split planes)
 
         def conv_in_relu(inp, key, cout, R, st, pad, mode, nxt=None):
             """conv + IN + ReLU; nxt = (cout, stride, pad mode) of the 3x3 conv consuming the output"""
             kc, _, b = P[key]
             y, s = ops.conv2d_fwd_in(inp, kc, b, cpad(cout), R, R, st, pad, mode, role=role)
-            a, at = in_act(y, s, "relu", cp_for(y, *nxt) if nxt else None)
+            a, at = in_act(y, s, "relu", cp_for(y, *nxt) if nxt else None, apre=APRE and nxt == rb_in)
             sv["xt"][id(a)] = at
             return y, s, a
 
@@ -610,7 +620,8 @@ class _GeneratorFn(torch.autograd.Function):
             else:
                 t, s1, uu = conv_in_relu(h, f"b{i}a", 4 * ngf, 3, 1, 1, "reflect", nxt=(4 * ngf, 1, "reflect"))
                 v, s2 = ops.conv2d_fwd_in(uu, kc, b, 4 * ngf, 3, 3, 1, 1, "reflect", role=role)
-            hn, hnt = in_act(v, s2, "none", cp_for(v, 4 * ngf, 1, "reflect") if i + 1 < nb else None, residual=h)
+            hn, hnt = in_act(v, s2, "none", cp_for(v, 4 * ngf, 1, "reflect") if i + 1 < nb else None, residual=h,
+                             apre=APRE and i + 1 < nb)
             sv["xt"][id(hn)] = hnt
             sv[f"b{i}"] = (h, t, s1, uu, v, s2)
             h = hn
@@ -678,14 +689,14 @@ class _GeneratorFn(torch.autograd.Function):
                              R, R, st, pad, mode, co, ci, ci * R * R, R * R, accumulate=True, dy_planes=dy_planes,
                              x_t=xts.get(id(inp)))
 
-        def in_bwd(g, y, s, act, mod, x_in=None, R=3, st=1):
+        def in_bwd(g, y, s, act, mod, x_in=None, R=3, st=1, apre=False):
             # IN(+act) backward; the bias gradient of the conv feeding the IN comes out of the
             # same reduction (sum of dy per channel).  x_in given: also the dy planes of that
             # conv's x6 weight gradient (None when it runs elsewhere) -> (dy, planes)
             db = mod.bias.grad if (train_w and mod.bias is not None) else None
             if x_in is None:
                 return ops.instnorm_act_bwd(g, y, s, act, db=db)
-            return _in_bwd_for_wgrad(g, y, s, act, 0.0, db, x_in, R, st, train_w)
+            return _in_bwd_for_wgrad(g, y, s, act, 0.0, db, x_in, R, st, train_w, apre=apre)
 
         def dgrad_reflect(dy, key, cin_p, R, p, H, W, addend=None):
             ikf = P["ikf"].get(key)
@@ -743,7 +754,7 @@ class _GeneratorFn(torch.autograd.Function):
             done(m)
             kc, _, _ = P[f"u{i}"]
             ga = ops.conv2d_fwd(dy, kc, None, a_in.shape[-1], 3, 3, 2, 1, "zero", role="bwd")
-        def dgrad_reflect_in(dy, key, H, W, y_in, s_in, act, mod, x_w, R_w, st_w, addend=None):
+        def dgrad_reflect_in(dy, key, H, W, y_in, s_in, act, mod, x_w, R_w, st_w, addend=None, apre=False):
             """dgrad_reflect (3x3, pad 1) + the IN(+act) backward of the layer below it (y_in, s_in;
             mod = the conv feeding that IN; x_w / R_w / st_w = that conv's weight-gradient input
             and geometry) -> (g, dy_in, dy_in planes or None).  On the border route the border add
@@ -759,9 +770,11 @@ class _GeneratorFn(torch.autograd.Function):
                         _wgrad_on_bf(N, x_w.shape[1], x_w.shape[2], x_w.shape[3], y_in.shape[1], y_in.shape[2],
                                      cin_p, R_w, st_w, ops.get_conv_math()))
                 r = ops.conv2d_dgrad_refl_in(dy, ikf, H, W, cin_p, y_in, s_in, act, 0.0, addend=addend, db=db,
-                                             planes=want, epi=True)
+                                             planes=want, epi=True, apre=apre)
                 if r is not None:
                     return r if want else (r[0], r[1], None)
+            if getattr(dy, "vst_planes_only", False):
+                raise RuntimeError("dgrad_reflect_in: a planes-only gradient reached a route that reads fp32")
             if DGRAD_IN and not FOLD_IN and ikf is not None and dy.shape[-1] % 8 == 0:
                 db = mod.bias.grad if (train_w and mod.bias is not None) else None
                 N = x_w.shape[0]
@@ -790,21 +803,29 @@ class _GeneratorFn(torch.autograd.Function):
         gh = ga
         nb = len(blocks)
         pre_d1 = None
+        # planes-only data-gradient inputs (APRE_BWD) only where every ResnetBlock data gradient takes the epi route
+        # (it reads the planes; the other routes read the fp32 image, which is then not written)
+        apre_bwd = False
+        if APRE_BWD and nb and train_w and DGRAD_EPI and not DGRAD_IN and not FOLD_IN:
+            Nb, Hb, Wb, Cb = sv["b0"][0].shape
+            apre_bwd = (Cb % 8 == 0 and all(P["ikf"].get(f"b{i}{c}") is not None for i in range(nb) for c in "ab")
+                        and ops.dgrad_refl_epi_ok(Nb, Hb, Wb, Cb, Cb))
         if nb:
             dv, dvp = in_bwd(gh, sv[f"b{nb - 1}"][4], sv[f"b{nb - 1}"][5], "none", blocks[-1].conv_block[5],
-                             sv[f"b{nb - 1}"][3])
+                             sv[f"b{nb - 1}"][3], apre=apre_bwd)
         for i in reversed(range(nb)):
             h, t, s1, uu, v, s2 = sv[f"b{i}"]
             blk = blocks[i].conv_block
             wgrad(blk[5], uu, dv, 3, 1, 1, "reflect", dy_planes=dvp)
             done(blk[5])
-            _, dt, dtp = dgrad_reflect_in(dv, f"b{i}b", uu.shape[1], uu.shape[2], t, s1, "relu", blk[1], h, 3, 1)
+            _, dt, dtp = dgrad_reflect_in(dv, f"b{i}b", uu.shape[1], uu.shape[2], t, s1, "relu", blk[1], h, 3, 1,
+                                          apre=apre_bwd)
             wgrad(blk[1], h, dt, 3, 1, 1, "reflect", dy_planes=dtp)
             done(blk[1])
             if i > 0:
                 _, _, _, uup, vp, s2p = sv[f"b{i - 1}"]
                 gh, dv, dvp = dgrad_reflect_in(dt, f"b{i}a", h.shape[1], h.shape[2], vp, s2p, "none",
-                                               blocks[i - 1].conv_block[5], uup, 3, 1, addend=gh)
+                                               blocks[i - 1].conv_block[5], uup, 3, 1, addend=gh, apre=apre_bwd)
             else:
                 y1, s1d, _ = sv["d1"]
                 gh, dy1, dyp1 = dgrad_reflect_in(dt, f"b{i}a", h.shape[1], h.shape[2], y1, s1d, "relu", d[1],

@@ -258,9 +258,15 @@ def conv2d_fwd_in(x, wp, bias, cop, R, S, stride, pad, pad_mode="zero", role="fw
     m = _math(role)
     ws, nb = _fwd_ws(N, H, W, Cx, cop, R, S, stride, pad, m, x.device) if S == R else (None, 0)
     h = _probe_begin("fwd", (N, H, W, Cx, cop, R, stride, pad, pad_mode)) if _probes else None
-    _call("vst_conv2d_fwd_ws", _p(x), _p(wp), _p(getattr(wp, "vst_split", None)), _p(bias), _p(y), N, H, W, Cx,
-          cop, R, S, stride, pad, PAD[pad_mode], ACT["none"], 0.0, m, _p(part),
-          ctypes.addressof(nsplit), _p(ws), nb, _stream())
+    apl = getattr(x, "vst_apl", None)
+    if apl is not None:  # x's pre-split planes (instnorm_act_fwd(apre=True)): the A operand by LDS-DMA
+        _call("vst_conv2d_fwd_apre_ws", _p(x), _p(apl), _p(wp), _p(getattr(wp, "vst_split", None)), _p(bias), _p(y),
+              N, H, W, Cx, cop, R, S, stride, pad, PAD[pad_mode], ACT["none"], 0.0, m, _p(part),
+              ctypes.addressof(nsplit), _p(ws), nb, _stream())
+    else:
+        _call("vst_conv2d_fwd_ws", _p(x), _p(wp), _p(getattr(wp, "vst_split", None)), _p(bias), _p(y), N, H, W, Cx,
+              cop, R, S, stride, pad, PAD[pad_mode], ACT["none"], 0.0, m, _p(part),
+              ctypes.addressof(nsplit), _p(ws), nb, _stream())
     _probe_end(h)
     if nsplit.value == 0:
         return y, instnorm_stats(y)
@@ -553,13 +559,16 @@ def conv2d_dgrad_s1_in(dy, ikf, H, W, cx, R, pad, y_in, stats, act="relu", slope
 
 
 def conv2d_dgrad_refl_in(dy, ikf, H, W, cx, y_in, stats, act="relu", slope=0.0, addend=None, db=None,
-                         accumulate_db=True, planes=False, role="bwd", epi=False):
+                         accumulate_db=True, planes=False, role="bwd", epi=False, apre=False):
     """ReflectionPad2d(1) + 3x3 data gradient (conv2d_dgrad_s1's interior conv + border GEMM) fused with
     the InstanceNorm(+act) backward of the layer below it (vst_conv2d_dgrad_refl_in): returns (g, dy_in[,
     dy_in_planes]) — g = the data gradient (+ addend), dy_in = instnorm_act_bwd(g, y_in, stats, act) —
     or None when the fused route does not support the shape / arithmetic.
     epi: the IN partials taken by the data gradient's GEMM epilogue and border add instead
-    (vst_conv2d_dgrad_refl_in_epi: no partial pass; x6 arithmetic, H W % 32 == 0)."""
+    (vst_conv2d_dgrad_refl_in_epi: no partial pass; x6 arithmetic, H W % 32 == 0); there dy's pre-split planes
+    (``dy.vst_apl``) are its A operand when present, and apre (with planes) writes dy_in as planes only."""
+    if getattr(dy, "vst_planes_only", False) and not epi:
+        raise ValueError("conv2d_dgrad_refl_in: dy has planes only (instnorm_act_bwd(apre=True)): use epi=True")
     _dev_check(dy, ikf, addend, y_in, stats)
     if not DGRAD_BORDER or getattr(ikf, "vst_split", None) is None:
         return None
@@ -579,12 +588,15 @@ def conv2d_dgrad_refl_in(dy, ikf, H, W, cx, y_in, stats, act="relu", slope=0.0, 
         if planes:
             ldp = lib().vst_cp_ld(N * H * W)
             pl = torch.empty((3, C, ldp), device=dy.device, dtype=torch.bfloat16)
+        if planes and apre:  # dy_in as planes only (instnorm_act_bwd(apre=True))
+            dyi.vst_apl = torch.empty((3, dyi.numel()), device=dy.device, dtype=torch.bfloat16)
+            dyi.vst_planes_only = True
         h = _probe_begin("dgrad", (N, H, W, Cy, C, 3, 1, 1, "reflect")) if _probes else None
-        _call("vst_conv2d_dgrad_refl_epi_part", _p(dy), _p(ikf.vst_split), _p(addend), _p(g), _p(y_in), _p(stats),
-              _p(ws), nb, N, H, W, Cy, C, ACT[act], float(slope), m, _stream())
+        _call("vst_conv2d_dgrad_refl_epi_part", _p(dy), _p(getattr(dy, "vst_apl", None)), _p(ikf.vst_split),
+              _p(addend), _p(g), _p(y_in), _p(stats), _p(ws), nb, N, H, W, Cy, C, ACT[act], float(slope), m, _stream())
         _probe_end(h)
         _call("vst_instnorm_act_bwd_epi_tail", _p(g), _p(y_in), _p(stats), _p(dyi), _p(db), _p(ws), N, H, W, C, ACT[act],
-              float(slope), 1 if accumulate_db else 0, _p(pl), ldp, _stream())
+              float(slope), 1 if accumulate_db else 0, _p(pl), ldp, _p(getattr(dyi, "vst_apl", None)), _stream())
         return (g, dyi, pl) if planes else (g, dyi)
     nbd = int(lib().vst_conv2d_dgrad_refl_ws_bytes(N, H, W, Cy, C, m))
     if not nbd or not int(lib().vst_conv2d_dgrad_refl_in_ws_bytes(N, H, W, Cy, C, m)):
@@ -605,6 +617,11 @@ def conv2d_dgrad_refl_in(dy, ikf, H, W, cx, y_in, stats, act="relu", slope=0.0, 
     _call("vst_instnorm_act_bwd_refl_border", _p(g), _p(y_in), _p(stats), _p(dyi), _p(db), _p(iws), _p(dws), N, H, W,
           Cy, C, ACT[act], float(slope), 1 if accumulate_db else 0, _p(pl), ldp, m, _stream())
     return (g, dyi, pl) if planes else (g, dyi)
+
+
+def dgrad_refl_epi_ok(N, H, W, Cy, Cx, role="bwd"):
+    """Does conv2d_dgrad_refl_in(epi=True) take this shape (vst_conv2d_dgrad_refl_in_epi_ws_bytes > 0)?"""
+    return DGRAD_BORDER and int(lib().vst_conv2d_dgrad_refl_in_epi_ws_bytes(N, H, W, Cy, Cx, _math(role))) > 0
 
 
 def reflect_fold(dxp, p, addend=None):
@@ -631,12 +648,14 @@ def instnorm_stats(y):
     return stats
 
 
-def instnorm_act_fwd(y, stats, act="relu", slope=0.0, residual=None, cp=None, xpl=None):
+def instnorm_act_fwd(y, stats, act="relu", slope=0.0, residual=None, cp=None, xpl=None, apre=False):
     """a = act(IN(y)) (+ residual).  cp = (pad, pad_mode, stride) of the conv that consumes a:
     returns (a, a_t) where a_t is a's padded channel-major image for that conv's x6 weight gradient
     (vst_instnorm_act_fwd_cp; conv2d_wgrad(x_t=a_t)).  xpl = (pad, pad_mode, wx): returns (a, planes),
     a's padded image as the bf16 planes [3][C][ld] with wx zero columns per row
-    (vst_instnorm_act_fwd_planes; tap_conv_wgrad_swap(x_pl=planes))."""
+    (vst_instnorm_act_fwd_planes; tap_conv_wgrad_swap(x_pl=planes)).
+    apre (with cp or alone): a also carries its NHWC bf16 planes as ``a.vst_apl`` (vst_instnorm_act_fwd_cp_apre /
+    vst_instnorm_act_fwd_apre), the pre-split A operand conv2d_fwd_in takes."""
     _dev_check(y, stats, residual)
     N, H, W, C = y.shape
     a = torch.empty_like(y)
@@ -650,18 +669,31 @@ def instnorm_act_fwd(y, stats, act="relu", slope=0.0, residual=None, cp=None, xp
     if cp is not None:
         pad, mode, st = cp
         at = torch.empty((C, lib().vst_cp_ld(N * (H + 2 * pad) * (W + 2 * pad))), device=y.device)
+        if apre:
+            a.vst_apl = torch.empty((3, y.numel()), device=y.device, dtype=torch.bfloat16)
+            _call("vst_instnorm_act_fwd_cp_apre", _p(y), _p(stats), _p(residual), _p(a), _p(at), _p(a.vst_apl), N, H,
+                  W, C, ACT[act], float(slope), pad, PAD[mode], st, _stream())
+            return a, at
         _call("vst_instnorm_act_fwd_cp", _p(y), _p(stats), _p(residual), _p(a), _p(at), N, H, W, C, ACT[act],
               float(slope), pad, PAD[mode], st, _stream())
         return a, at
+    if apre:
+        a.vst_apl = torch.empty((3, y.numel()), device=y.device, dtype=torch.bfloat16)
+        _call("vst_instnorm_act_fwd_apre", _p(y), _p(stats), _p(residual), _p(a), _p(a.vst_apl), N, H * W, C, ACT[act],
+              float(slope), _stream())
+        return a
     _call("vst_instnorm_act_fwd", _p(y), _p(stats), _p(residual), _p(a), N, H * W, C, ACT[act],
           float(slope), _stream())
     return a
 
 
-def instnorm_act_bwd(ga, y, stats, act="relu", slope=0.0, db=None, accumulate_db=True, planes=False):
+def instnorm_act_bwd(ga, y, stats, act="relu", slope=0.0, db=None, accumulate_db=True, planes=False, apre=False):
     """dy = backward of act(IN(y)); db (if given) (+)= sum of dy per channel (conv-bias grad).
     planes=True: returns (dy, dy_planes) — the apply pass also writes dy's three bf16 planes
-    [3][C][vst_cp_ld(N*H*W)], the x6 weight gradient's operand image (conv2d_wgrad(dy_planes=...))."""
+    [3][C][vst_cp_ld(N*H*W)], the x6 weight gradient's operand image (conv2d_wgrad(dy_planes=...)).
+    apre (with planes): dy is written ONLY as its NHWC bf16 planes ``dy.vst_apl`` (the pre-split A operand of the data
+    gradient that consumes it, conv2d_dgrad_refl_in(epi=True)) — dy's fp32 values are NOT written (dy.vst_planes_only):
+    its readers must take the planes (the weight gradient: dy_planes; the data gradient: vst_apl)."""
     _dev_check(ga, y, stats)
     N, H, W, C = y.shape
     dy = torch.empty_like(y)
@@ -670,6 +702,12 @@ def instnorm_act_bwd(ga, y, stats, act="relu", slope=0.0, db=None, accumulate_db
     if planes:
         ldp = lib().vst_cp_ld(N * H * W)
         pl = torch.empty((3, C, ldp), device=y.device, dtype=torch.bfloat16)
+    if planes and apre:
+        dy.vst_apl = torch.empty((3, dy.numel()), device=y.device, dtype=torch.bfloat16)
+        dy.vst_planes_only = True
+        _call("vst_instnorm_act_bwd_planes_apre", _p(ga), _p(y), _p(stats), _p(dy), _p(db), _p(ws), N, H * W, C,
+              ACT[act], float(slope), 1 if accumulate_db else 0, _p(pl), ldp, _p(dy.vst_apl), _stream())
+        return dy, pl
     _call("vst_instnorm_act_bwd_planes", _p(ga), _p(y), _p(stats), _p(dy), _p(db), _p(ws), N, H * W, C,
           ACT[act], float(slope), 1 if accumulate_db else 0, _p(pl), ldp, _stream())
     return (dy, pl) if planes else dy

@@ -337,6 +337,13 @@ class Generator(FlatNet):
              "last": (ops.weight_pack(last.weight, ops.PACK_FWD), ops.weight_pack(last.weight, ops.PACK_DGRAD))}
         if TAP_LAST:  # 64 -> 3 output channels: tap GEMM on the matrix cores (ops.tap_conv_fwd)
             P["last_tap"] = ops.weight_pack(last.weight, ops.PACK_CK)
+        if SG_PHASES:
+            # the last layer's data gradient as a forward conv over the 4-channel dy (the direct 4-channel kernel,
+            # ops.conv2d_dgrad_s1) and the Conv2d(k4, s2, p1) down convs' as phase convs (ops.conv4s2_dgrad),
+            # instead of the generic transposed-conv gathers
+            P["last_ikf"] = ops.weight_pack(last.weight, ops.PACK_IKF)
+            P["down_ph"] = [ops.conv4s2_dgrad_phase_packs(c.weight) if k == 4 and st == 2 and pd == 1 else None
+                            for c, _, k, st, pd in down]
         return P
 
     def forward(self, x, c):
@@ -445,7 +452,10 @@ class _StarGFn(torch.autograd.Function):
                 ops.tap_conv_wgrad(a, g, last.weight.grad, 7, 3, "zero", accumulate=True)
         else:
             wgrad(last, a, g, 7, 1, 3)
-        g = ops.conv2d_tfwd(g, P["last"][1], None, a.shape[1], a.shape[2], a.shape[-1], 7, 7, 1, 3)
+        if "last_ikf" in P and g.shape[-1] == 4:
+            g = ops.conv2d_dgrad_s1(g, P["last_ikf"], a.shape[1], a.shape[2], a.shape[-1], 7, 3, "zero")
+        else:
+            g = ops.conv2d_tfwd(g, P["last"][1], None, a.shape[1], a.shape[2], a.shape[-1], 7, 7, 1, 3)
         for i in (1, 0):
             conv, norm = up[i]
             a_in, y, s = sv[("up", i)]
@@ -475,8 +485,12 @@ class _StarGFn(torch.autograd.Function):
             dy = in_bwd(g, y, s, norm, "relu")
             wgrad(conv, a_in, dy, k, st, pad)
             if i > 0 or ctx.needs_input_grad[0]:
-                g = ops.conv2d_tfwd(dy, P["down"][i][1], None, a_in.shape[1], a_in.shape[2], a_in.shape[-1], k, k,
-                                    st, pad)
+                ph = P["down_ph"][i] if "down_ph" in P else None
+                if ph is not None and a_in.shape[1] == 2 * dy.shape[1] and a_in.shape[2] == 2 * dy.shape[2]:
+                    g = ops.conv4s2_dgrad(dy, ph, a_in.shape[-1])
+                else:
+                    g = ops.conv2d_tfwd(dy, P["down"][i][1], None, a_in.shape[1], a_in.shape[2], a_in.shape[-1], k,
+                                        k, st, pad)
                 if i == 0:
                     gx = g
         ctx.sv = None

@@ -351,12 +351,32 @@ int vst_conv2d_dgrad_refl_in_epi(const float* dy, const void* wsplit, const floa
                                  int N, int H, int W, int Cy, int Cx, int act, float slope, int accumulate_db,
                                  void* planes, long ldp, int math, void* stream);
 /* its halves: the data gradient + the partials (into the front of ws), then finalize + apply from them */
-int vst_conv2d_dgrad_refl_epi_part(const float* dy, const void* wsplit, const float* addend, float* gout,
-                                   const float* x, const float* stats, float* ws, size_t ws_bytes, int N, int H, int W,
-                                   int Cy, int Cx, int act, float slope, int math, void* stream);
+int vst_conv2d_dgrad_refl_epi_part(const float* dy, const void* dy_apl, const void* wsplit, const float* addend,
+                                   float* gout, const float* x, const float* stats, float* ws, size_t ws_bytes, int N,
+                                   int H, int W, int Cy, int Cx, int act, float slope, int math, void* stream);
 int vst_instnorm_act_bwd_epi_tail(const float* gout, const float* x, const float* stats, float* dx, float* db,
                                   float* ws, int N, int H, int W, int Cx, int act, float slope, int accumulate_db,
-                                  void* planes, long ldp, void* stream);
+                                  void* planes, long ldp, void* apl, void* stream);
+/* (dy_apl: dy's NHWC bf16 planes [3][N*H*W*Cy] or NULL — the interior GEMM then takes its A operand pre-split by
+ * LDS-DMA (vst_conv2d_fwd_apre_ws), the border GEMM from the planes too, and dy's fp32 image is not read; apl: the
+ * tail writes dx as its NHWC planes INSTEAD of fp32 (the next data gradient's dy_apl; dx is left unwritten), or NULL) */
+/* Pre-split A operands (the x6 forwards' A staged by LDS-DMA from bf16 planes instead of split in the staging): the
+ * producing IN pass writes the NHWC planes [3][N*H*W*C] (hi, mid, lo: each value's RNE split) beside its fp32 output;
+ * the consuming forward takes them on its x6 256x128 channel-slice plans (results bit-identical, other plans read
+ * x).  Same arguments as vst_instnorm_act_fwd_cp / vst_instnorm_act_bwd_planes / vst_conv2d_fwd_ws plus the planes. */
+int vst_instnorm_act_fwd_apre(const float* x, const float* stats, const float* residual, float* y, void* apl, int N,
+                              int HW, int C, int act, float slope, void* stream);
+int vst_instnorm_act_fwd_cp_apre(const float* x, const float* stats, const float* residual, float* y, float* x_t,
+                                 void* apl, int N, int H, int W, int C, int act, float slope, int pad, int pad_mode,
+                                 int stride, void* stream);
+/* (vst_instnorm_act_bwd_planes_apre: dx is written as apl only, not as fp32) */
+int vst_instnorm_act_bwd_planes_apre(const float* gy, const float* x, const float* stats, float* dx, float* db,
+                                     float* ws, int N, int HW, int C, int act, float slope, int accumulate_db,
+                                     void* planes, long ldp, void* apl, void* stream);
+int vst_conv2d_fwd_apre_ws(const float* x, const void* apl, const float* wp, const void* wsplit, const float* bias,
+                           float* y, int N, int H, int W, int Cx, int Cop, int R, int S, int stride, int pad,
+                           int pad_mode, int act, float slope, int math, double* part, int* nsplit, float* ws,
+                           size_t ws_bytes, void* stream);
 int vst_conv2d_dgrad_refl_slabs(const float* dy, const void* wsplit, const float* addend, float* gout, float* ws,
                                 size_t ws_bytes, int N, int H, int W, int Cy, int Cx, int math, void* stream);
 int vst_instnorm_act_bwd_refl_border(float* gout, const float* x, const float* stats, float* dx, float* db,

@@ -44,6 +44,11 @@ from oracle import fullsize_cases as fc
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
 MARGIN = 3.0
+# A gradient is ALSO held to its own fp32 deviation: <= max(floor, OWN_MARGIN x ||ref32 - ref64|| of that parameter),
+# so a layer-local regression cannot hide under its network's largest fp32 deviation.  Measured (round 5, every case,
+# both policies: tools/parity_ratios.py over VST_PARITY_LOG): the largest HIP / own-fp32 ratio above the floor is 12.1
+# (C5 MoGAN e_grad|D_B|model.2.weight: 2.26e-3 vs 1.87e-4).
+OWN_MARGIN = 20.0
 SKETCH_SLACK = 1.1
 F64 = torch.float64
 FLOORS = {"loss": 1e-3, "grad": 2e-3, "tensor": 1e-3}
@@ -91,7 +96,8 @@ def _check(name, got, fixture, skip=()):
     move the gradients happen in the network's activations and reach all of its layers, so one
     parameter's own fp32 deviation is a noisy estimate of it (the C5 D_B layers read 1.3-1.9e-4 in the
     fp32 run beside 9e-4 at its first layer, while D alone at that size — test_discriminator_sintel_
-    size_vs_fp64 — puts HIP at 1.6-1.9x the fp32 deviation on every layer)."""
+    size_vs_fp64 — puts HIP at 1.6-1.9x the fp32 deviation on every layer).  Each gradient is in addition
+    held to OWN_MARGIN x its own fp32 deviation (above the floor)."""
     sketched = {n.split(":", 1)[1] for n in fixture.files if n.startswith("S:")}
     devs = fc.deviations(got, fixture)
     scale = {}
@@ -105,6 +111,8 @@ def _check(name, got, fixture, skip=()):
         kind = fc.kind(key)
         ref_err = scale.get(_net_of(key), dref) if kind == "grad" else dref
         tol = FLOORS[kind] if kind == "loss" else max(FLOORS[kind], MARGIN * ref_err)
+        if kind == "grad":  # the layer-local bound (OWN_MARGIN)
+            tol = min(tol, max(FLOORS[kind], OWN_MARGIN * dref))
         if key in sketched:
             tol *= SKETCH_SLACK
         rows.append((key, dev, dref, tol))

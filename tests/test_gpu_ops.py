@@ -645,6 +645,19 @@ def test_convT3s2_phase_packs_batched_equal_single(ops):
         assert torch.equal(s_, b_) and torch.equal(s_.vst_split, b_.vst_split)
 
 
+@pytest.mark.parametrize("shape", [(64, 32, 3, 3), (3, 64, 7, 7), (1, 512, 4, 4), (130, 70, 3, 3)])
+def test_pack_batch_equals_single_every_mode(ops, shape):
+    """vst_weight_pack_batch (4 elements per lane, float4 / 8-byte plane stores) equals the per-element
+    vst_weight_pack_split for every pack mode, fp32 pack and the three bf16 planes."""
+    w = _g(99, shape, 0.05).to(DEV)
+    modes = [ops.PACK_FWD, ops.PACK_DGRAD, ops.PACK_IKF]
+    single = [ops.weight_pack(w, m) for m in modes]
+    with ops.PackBatch():
+        batched = [ops.weight_pack(w, m) for m in modes]
+    for s_, b_ in zip(single, batched):
+        assert torch.equal(s_, b_) and torch.equal(s_.vst_split, b_.vst_split)
+
+
 # ----------------------------------------------------- fused IN-backward producers (round 2)
 def _split3(x):
     hi = x.to(torch.bfloat16)
@@ -652,6 +665,72 @@ def _split3(x):
     mid = r.to(torch.bfloat16)
     lo = (r - mid.float()).to(torch.bfloat16)
     return hi, mid, lo
+
+
+@pytest.mark.parametrize("N", [1, 2, 8, 12])
+def test_apre_forward_bit_identical(ops, N):
+    """Pre-split A operands (APRE): instnorm_act_fwd(cp, apre=True) writes a's NHWC planes (exactly the RNE three-way
+    split of a) beside a / a_t unchanged; conv2d_fwd_in over a with the planes (the x6 256x128 plans stage A by
+    LDS-DMA) equals the plain conv bit for bit, statistics included.  N = 1 / 2: all split-K; 8: whole rounds;
+    12: a round + a split-K tail."""
+    prev = ops.set_conv_math("bf16x6")
+    try:
+        H, C = 64, 256
+        y = _g(161, (N, H, H, C)).to(DEV)
+        s = ops.instnorm_stats(y)
+        a0, at0 = ops.instnorm_act_fwd(y, s, "relu", cp=(1, "reflect", 1))
+        a1, at1 = ops.instnorm_act_fwd(y, s, "relu", cp=(1, "reflect", 1), apre=True)
+        P = N * (H + 2) * (H + 2)  # a_t rows are padded to vst_cp_ld(P): compare the written part
+        assert torch.equal(a0, a1) and torch.equal(at0[:, :P], at1[:, :P])
+        pl = a1.vst_apl.view(3, -1)
+        for p_, ref in zip(pl, _split3(a1.reshape(-1))):
+            assert torch.equal(p_, ref)
+        w = _g(162, (C, C, 3, 3), 0.02)
+        kc = ops.weight_pack(w.to(DEV), ops.PACK_FWD)
+        b = torch.zeros(C, device=DEV)
+        y0, s0 = ops.conv2d_fwd_in(a0, kc, b, C, 3, 3, 1, 1, "reflect")
+        y1, s1 = ops.conv2d_fwd_in(a1, kc, b, C, 3, 3, 1, 1, "reflect")
+        assert torch.equal(y0, y1) and torch.equal(s0, s1)
+    finally:
+        ops.set_conv_math(prev)
+
+
+@pytest.mark.parametrize("N", [1, 8, 12])
+def test_apre_dgrad_epi_bit_identical(ops, N):
+    """instnorm_act_bwd(planes, apre=True) writes dy ONLY as its NHWC planes (exactly the RNE split of the plain pass's
+    dy; the fp32 image stays unwritten); the epi data gradient over those planes (interior A by LDS-DMA, the border
+    GEMM from the planes, the split-K tail at N = 12) gives g / IN-backward planes / bias gradient bit-identical to
+    the plain route, and its own apre output dy_in is the RNE split of the plain route's dy_in."""
+    prev = ops.set_conv_math("bf16x6")
+    try:
+        H, C = 64, 256
+        z = _g(171, (N, H, H, C)).to(DEV)
+        s = ops.instnorm_stats(z)
+        ga = _g(172, (N, H, H, C)).to(DEV)
+        dy0, pl0 = ops.instnorm_act_bwd(ga, z, s, "none", planes=True)
+        dy1, pl1 = ops.instnorm_act_bwd(ga, z, s, "none", planes=True, apre=True)
+        P = N * H * H  # the channel-major plane rows are padded to vst_cp_ld(P): compare the written part
+        assert torch.equal(pl0[:, :, :P], pl1[:, :, :P]) and dy1.vst_planes_only
+        for p_, ref in zip(dy1.vst_apl.view(3, -1), _split3(dy0.reshape(-1))):
+            assert torch.equal(p_, ref)
+        dy1.fill_(float("nan"))  # never read
+        w = _g(173, (C, C, 3, 3), 0.05)
+        ikf = ops.weight_pack(w.to(DEV), ops.PACK_IKF)
+        y_in = _g(174, (N, H, H, C)).to(DEV)
+        s_in = ops.instnorm_stats(y_in)
+        add = _g(175, (N, H, H, C)).to(DEV)
+        db0, db1 = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+        r0 = ops.conv2d_dgrad_refl_in(dy0, ikf, H, H, C, y_in, s_in, "relu", addend=add, db=db0, planes=True, epi=True)
+        r1 = ops.conv2d_dgrad_refl_in(dy1, ikf, H, H, C, y_in, s_in, "relu", addend=add, db=db1, planes=True, epi=True,
+                                      apre=True)
+        assert r0 is not None and r1 is not None
+        assert torch.equal(r0[0], r1[0])
+        assert torch.equal(r0[2][:, :, :P], r1[2][:, :, :P])
+        assert torch.equal(db0, db1)
+        for p_, ref in zip(r1[1].vst_apl.view(3, -1), _split3(r0[1].reshape(-1))):
+            assert torch.equal(p_, ref)
+    finally:
+        ops.set_conv_math(prev)
 
 
 @pytest.mark.parametrize("N,H,C,act", [(2, 16, 64, "relu"), (3, 12, 128, "none"), (2, 10, 64, "lrelu")])

@@ -88,7 +88,7 @@ def DOMINANT_KEYS(B):
             "resblock_wgrad": ("wgrad", (N, 64, 64, 256, 256, 3, 1, 1, "reflect"))}
 
 
-PMC_FILE = os.path.join(HERE, "profiles", "r04f5_conv_pmc.json")
+PMC_FILE = os.path.join(HERE, "profiles", "r05z_conv_pmc.json")
 
 
 def _pmc_record(name, key):

@@ -101,6 +101,28 @@ static_assert(sizeof(PackJob) == 168, "PackJob layout is part of the C ABI (incl
 // One 64-lane block per 256-element job block (PackJob.block0 units): a lane packs 4 consecutive elements (their
 // gathers issued together), stores them as one float4 and each split plane as one 8-byte word — the per-element
 // form moved ~1.5 TB/s (narrow stores, one gather in flight per lane).
+// The per-element form (one element per lane, 256-lane blocks): VST_PACK_KERNEL=0.
+__global__ __launch_bounds__(256) void weight_pack_batch1_k(const PackJob* __restrict__ jobs, int nj) {
+  const long b = blockIdx.x;
+  int lo = 0, hi = nj - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (jobs[mid].block0 <= b) lo = mid;
+    else hi = mid - 1;
+  }
+  const PackJob& J = jobs[lo];
+  const long idx = (b - J.block0) * 256 + threadIdx.x;
+  if (idx >= J.total) return;
+  int o, i, rs;
+  pack_coords(idx, J.R, J.S, J.Op, J.Ip, J.mode, o, i, rs);
+  const int r = rs / J.S, s = rs - r * J.S;
+  const int rr = J.tr[0] < 0 ? r : J.tr[r], ss = J.ts[0] < 0 ? s : J.ts[s];
+  const float v = (o < J.O && i < J.I) ? J.w[o * J.so + i * J.si + rr * J.sr + ss * J.ss] : 0.f;
+  J.out[idx] = v;
+  if (J.split) store_split(J.split, J.total, idx, v);
+}
+
+template <bool TILED>
 __global__ __launch_bounds__(64) void weight_pack_batch_k(const PackJob* __restrict__ jobs, int nj) {
   const long b = blockIdx.x;
   int lo = 0, hi = nj - 1;
@@ -110,6 +132,39 @@ __global__ __launch_bounds__(64) void weight_pack_batch_k(const PackJob* __restr
     else hi = mid - 1;
   }
   const PackJob& J = jobs[lo];
+  const int RS = J.R * J.S;
+  // OK / IK / IKF packs with >= 4 taps and a 64-multiple inner extent: tiled.  Block = (outer index A, 64 inner
+  // indices B): the source rows (A, B) are read along their taps (contiguous for identity tap maps) into an LDS
+  // tile, then written as whole 64-float rows per tap (+ planes).  The job's 256-element blocks cover its
+  // A x Bp / 64 tiles when RS >= 4; the rest of them exit.
+  const bool ok_mode = J.mode == VST_PACK_OK;
+  if (TILED && (ok_mode || J.mode == VST_PACK_IK || J.mode == VST_PACK_IKF) && RS >= 4 && RS <= 16) {
+    const int Ap = ok_mode ? J.Op : J.Ip, Bp = ok_mode ? J.Ip : J.Op;
+    if (Bp % 64 == 0) {
+      __shared__ float tile[64 * 17];
+      const long jb = b - J.block0, nb = Bp / 64;
+      if (jb >= (long)Ap * nb) return;
+      const int A = (int)(jb / nb), B0 = (int)(jb - (long)A * nb) * 64;
+      const bool flip = J.mode == VST_PACK_IKF;
+      for (int q = threadIdx.x; q < 64 * RS; q += 64) {
+        const int bb = q / RS, rs = q - bb * RS;  // rs: the source tap
+        const int o = ok_mode ? A : B0 + bb, i = ok_mode ? B0 + bb : A;
+        const int r = rs / J.S, sx = rs - r * J.S;
+        const int rr = J.tr[0] < 0 ? r : J.tr[r], ss = J.ts[0] < 0 ? sx : J.ts[sx];
+        const float v = (o < J.O && i < J.I) ? J.w[o * J.so + i * J.si + rr * J.sr + ss * J.ss] : 0.f;
+        tile[bb * 17 + (flip ? RS - 1 - rs : rs)] = v;
+      }
+      __syncthreads();
+      for (int q = threadIdx.x; q < 64 * RS; q += 64) {
+        const int rs = q >> 6, bb = q & 63;  // rs: the pack's tap
+        const float v = tile[bb * 17 + rs];
+        const long idx = ((long)A * RS + rs) * Bp + B0 + bb;
+        J.out[idx] = v;
+        if (J.split) store_split(J.split, J.total, idx, v);
+      }
+      return;
+    }
+  }
   const long idx0 = (b - J.block0) * 256 + 4 * threadIdx.x;
   if (idx0 >= J.total) return;
   float v[4];
@@ -239,8 +294,17 @@ extern "C" int vst_weight_pack_split(const float* w, float* out, void* split, in
 
 extern "C" int vst_weight_pack_batch(const void* jobs, int njobs, long nblocks, void* stream) {
   VST_REQUIRE(jobs && njobs > 0 && nblocks > 0 && nblocks < (1L << 31), "weight_pack_batch: bad args");
-  hipLaunchKernelGGL(weight_pack_batch_k, dim3((unsigned)nblocks), dim3(64), 0, (hipStream_t)stream,
-                     reinterpret_cast<const PackJob*>(jobs), njobs);
+  static const int kind = [] {  // 0: per element, 1: 4 elements per lane, 2: + the tiled OK / IK / IKF path
+    const char* e = getenv("VST_PACK_KERNEL");
+    return e ? atoi(e) : 2;
+  }();
+  const PackJob* J = reinterpret_cast<const PackJob*>(jobs);
+  if (kind == 0)
+    hipLaunchKernelGGL(weight_pack_batch1_k, dim3((unsigned)nblocks), dim3(256), 0, (hipStream_t)stream, J, njobs);
+  else if (kind == 1)
+    hipLaunchKernelGGL(weight_pack_batch_k<false>, dim3((unsigned)nblocks), dim3(64), 0, (hipStream_t)stream, J, njobs);
+  else
+    hipLaunchKernelGGL(weight_pack_batch_k<true>, dim3((unsigned)nblocks), dim3(64), 0, (hipStream_t)stream, J, njobs);
   return check_launch("weight_pack_batch");
 }
 

@@ -525,9 +525,10 @@ D0_TFWD = os.environ.get("VST_D0_TFWD", "1") != "0"
 # Forward (VST_APRE=1: the planes beside the fp32 activation, which the residual / fallback readers keep): +0.73 ms in
 # the C2 step A/B (profiles/r05l_apre_step_ab.jsonl; in-step the forward GEMM gains ~1 %, the IN apply pays 6 B/elem).
 APRE = os.environ.get("VST_APRE", "0") == "1"
-# Backward (VST_APRE_BWD): the ResnetBlock chain's data-gradient inputs as planes ONLY (the IN backward writes no fp32
-# image: their weight gradients read the channel-major planes, the border GEMM puts the values back together).
-APRE_BWD = os.environ.get("VST_APRE_BWD", "0") == "1"
+# Backward (default; VST_APRE_BWD=0 restores the fp32 images): the ResnetBlock chain's data-gradient inputs as planes
+# ONLY (the IN backward writes no fp32 image: their weight gradients read the channel-major planes, the border GEMM
+# puts the values back together): C2 step A/B 53.81-53.82 vs 53.99-54.05 ms (profiles/r05n_apre_bwd_step_ab.jsonl).
+APRE_BWD = os.environ.get("VST_APRE_BWD", "1") != "0"
 _WPLAN_BF = 2  # ops.WPLAN_NAMES: copies + conv_wgrad_bf_k
 
 

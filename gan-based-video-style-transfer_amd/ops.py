@@ -1352,15 +1352,17 @@ def tap_conv_dgrad(dy, kc, R, pad, pad_mode="zero", role="bwd"):
     return y
 
 
-def dgrad_sok_pack(w):
+def dgrad_sok_pack(w, ci_real=None):
     """VST_PACK_SOK pack of the data gradient of a conv with <= 4 input channels, w [Co][Ci][R][S]: the
-    conv dy -> dx over the taps rotated 180 deg, w_d[o = ci][i = co][r][s] = w[co][ci][R-1-r][S-1-s]."""
+    conv dy -> dx over the taps rotated 180 deg, w_d[o = ci][i = co][r][s] = w[co][ci][R-1-r][S-1-s].
+    ci_real: only the first ci_real (<= 4) input channels' gradient (the others' is not wanted)."""
     Co, Ci, R, S = w.shape
+    Ci = ci_real or Ci
     pb = PackBatch._active
     if pb is not None:  # straight from w: transposed strides + reversed tap maps
-        return pb.add(w, PACK_SOK, Ci, Co, R, S, (R * S, Ci * R * S, S, 1), list(range(R - 1, -1, -1)),
+        return pb.add(w, PACK_SOK, Ci, Co, R, S, (R * S, w.shape[1] * R * S, S, 1), list(range(R - 1, -1, -1)),
                       list(range(S - 1, -1, -1)), Op=4)
-    return weight_pack(w.detach().permute(1, 0, 2, 3).flip(2, 3).contiguous(), PACK_SOK, Op=4)
+    return weight_pack(w.detach()[:, :Ci].permute(1, 0, 2, 3).flip(2, 3).contiguous(), PACK_SOK, Op=4)
 
 
 def tap_conv_dgrad_h(dy, sokd, R, pad, pad_mode="zero", role="bwd"):

@@ -344,6 +344,12 @@ class Generator(FlatNet):
             P["last_ikf"] = ops.weight_pack(last.weight, ops.PACK_IKF)
             P["down_ph"] = [ops.conv4s2_dgrad_phase_packs(c.weight) if k == 4 and st == 2 and pd == 1 else None
                             for c, _, k, st, pd in down]
+            # the ConvTranspose2d(k4, s2, p1) forwards: the data gradient of a Conv2d with the same weight (read as
+            # [out = Ci_t][in = Co_t]), i.e. its phase convs
+            P["up_ph"] = [ops.conv4s2_dgrad_phase_packs(c.weight) for c, _ in up]
+            # the first conv's data gradient onto the 3 image channels only (the label channels' is discarded):
+            # the R x 1 tap conv + column sums of the 4-channel route (ops.tap_conv_dgrad_h)
+            P["down0_sokd"] = ops.dgrad_sok_pack(down[0][0].weight, ci_real=3)
         return P
 
     def forward(self, x, c):
@@ -413,7 +419,10 @@ class _StarGFn(torch.autograd.Function):
         for i, (conv, norm) in enumerate(up):
             _, ik = P["up"][i]
             cout = conv.weight.shape[1]
-            y = ops.conv2d_tfwd(a, ik, None, 2 * a.shape[1], 2 * a.shape[2], cpad(cout), 4, 4, 2, 1, role=role)
+            if "up_ph" in P and a.shape[-1] % 32 == 0:  # ConvTranspose2d(k4, s2, p1) = the four 2x2 phase convs
+                y = ops.conv4s2_dgrad(a, P["up_ph"][i], cpad(cout), role=role)
+            else:
+                y = ops.conv2d_tfwd(a, ik, None, 2 * a.shape[1], 2 * a.shape[2], cpad(cout), 4, 4, 2, 1, role=role)
             s = _in_stats(y, norm, tr)
             g, b = _aff(norm)
             an = ops.instnorm_affine_fwd(y, s, g, b, "relu")
@@ -486,7 +495,11 @@ class _StarGFn(torch.autograd.Function):
             wgrad(conv, a_in, dy, k, st, pad)
             if i > 0 or ctx.needs_input_grad[0]:
                 ph = P["down_ph"][i] if "down_ph" in P else None
-                if ph is not None and a_in.shape[1] == 2 * dy.shape[1] and a_in.shape[2] == 2 * dy.shape[2]:
+                if i == 0 and "down0_sokd" in P and k == 7 and st == 1 and dy.shape[-1] % 8 == 0:
+                    g4 = ops.tap_conv_dgrad_h(dy, P["down0_sokd"], 7, pad, "zero")  # NHWC4: the 3 image channels
+                    g = torch.zeros(a_in.shape, device=g4.device)  # (the label channels' gradient: zero, unused)
+                    g[..., :4] = g4
+                elif ph is not None and a_in.shape[1] == 2 * dy.shape[1] and a_in.shape[2] == 2 * dy.shape[2]:
                     g = ops.conv4s2_dgrad(dy, ph, a_in.shape[-1])
                 else:
                     g = ops.conv2d_tfwd(dy, P["down"][i][1], None, a_in.shape[1], a_in.shape[2], a_in.shape[-1], k,

@@ -645,10 +645,12 @@ def test_convT3s2_phase_packs_batched_equal_single(ops):
         assert torch.equal(s_, b_) and torch.equal(s_.vst_split, b_.vst_split)
 
 
-@pytest.mark.parametrize("shape", [(64, 32, 3, 3), (3, 64, 7, 7), (1, 512, 4, 4), (130, 70, 3, 3)])
+@pytest.mark.parametrize("shape", [(64, 32, 3, 3), (3, 64, 7, 7), (1, 512, 4, 4), (130, 70, 3, 3), (128, 64, 3, 3),
+                                   (64, 256, 4, 4), (256, 128, 7, 7)])
 def test_pack_batch_equals_single_every_mode(ops, shape):
-    """vst_weight_pack_batch (4 elements per lane, float4 / 8-byte plane stores) equals the per-element
-    vst_weight_pack_split for every pack mode, fp32 pack and the three bf16 planes."""
+    """vst_weight_pack_batch (4 elements per lane, float4 / 8-byte plane stores; OK / IK / IKF packs with >= 4 taps
+    and a 64-multiple inner extent through an LDS transpose tile) equals the per-element vst_weight_pack_split for
+    every pack mode, fp32 pack and the three bf16 planes."""
     w = _g(99, shape, 0.05).to(DEV)
     modes = [ops.PACK_FWD, ops.PACK_DGRAD, ops.PACK_IKF]
     single = [ops.weight_pack(w, m) for m in modes]

@@ -112,7 +112,7 @@ def _dgrad_raw(gz, ik, spec, H, W, phases=None):
 
 
 def _wgrad_raw(x, gz, spec):
-    gw = torch.zeros((spec.co, spec.ci, spec.R, spec.R), device=x.device)
+    gw = torch.empty((spec.co, spec.ci, spec.R, spec.R), device=x.device)  # accumulate=False stores every element
     ops.conv2d_wgrad(x, gz, gw, None, spec.R, spec.R, spec.stride, spec.pad, "zero", spec.co, spec.ci,
                      spec.ci * spec.R * spec.R, spec.R * spec.R, accumulate=False)
     return gw
@@ -203,7 +203,7 @@ class _ChSum(torch.autograd.Function):
     @staticmethod
     def forward(ctx, gz, co):
         ctx.shape = gz.shape
-        db = torch.zeros(co, device=gz.device)
+        db = torch.empty(co, device=gz.device)
         ops.channel_sum(gz, db, co, accumulate=False)
         return db
 

@@ -167,12 +167,19 @@ def conv_roofline(name, probe, math):
         note = ("stride-1 data gradient as a forward conv over the rotated taps (66x66 padded frame)"
                 if name == "resblock_dgrad" else "ResnetBlock conv forward")
     elif op == "dgrad":
-        kernel = ("vst_conv2d_dgrad_refl: conv_fprop_bf_k interior (zero pad 1, %s) + the K-restricted border "
-                  "GEMM (split-K conv_fprop_bf_k<REFL=5>, 128x128) + dgrad_border5_add_k [%s]" % (m, _mfma(m)))
+        from gbvst import networks
         key = {"math": m, "N": N, "mfma": _mfma(m), "op": "dgrad_refl"}
-        note = ("stride-1 reflect data gradient: interior conv + border GEMM (no padded frame, no fold); "
-                "dgrad_border5_add_k adds the border slabs (VST_DGRAD_IN=1 moves that add into the "
-                "IN-backward partial pass)")
+        if networks.DGRAD_EPI:
+            kernel = ("vst_conv2d_dgrad_refl_in_epi: conv_fprop_bf_inb_k interior (zero pad 1, %s; the IN-backward "
+                      "partials of the layer below in its epilogue) + the K-restricted border GEMM (split-K "
+                      "conv_fprop_bf_k<REFL=5>, 128x128) + dgrad_border5_add_inb_k [%s]" % (m, _mfma(m)))
+            note = ("stride-1 reflect data gradient as the step runs it: interior conv + border GEMM + the border add "
+                    "with the IN-backward partials (traffic: the PMC record of the same GEMMs without the partials)")
+        else:
+            kernel = ("vst_conv2d_dgrad_refl: conv_fprop_bf_k interior (zero pad 1, %s) + the K-restricted border "
+                      "GEMM (split-K conv_fprop_bf_k<REFL=5>, 128x128) + dgrad_border5_add_k [%s]" % (m, _mfma(m)))
+            note = ("stride-1 reflect data gradient: interior conv + border GEMM (no padded frame, no fold); "
+                    "dgrad_border5_add_k adds the border slabs")
     else:
         # the step's route (networks.py IN_XT / IN_PLANES): the IN apply writes x's padded channel-major
         # image and the IN backward dy's bf16 planes, so the op is the GEMM + the split-K reduction

@@ -15,6 +15,7 @@ MI355X design:
     torchvision's VGG (kaiming-normal fan_out, zero bias) from a seed and accept
     ``load_torchvision_features`` / ``load_state_dict`` for real weights.
 """
+import os
 from collections import namedtuple
 
 import torch
@@ -49,6 +50,11 @@ def _features(cfg):
             out.append(("relu", v, v))
             cin = v
     return out
+
+
+# VGG data gradients (3x3, zero pad 1) as forward convs over the rotated taps on the split-bf16 kernel (the
+# generator's route) instead of the transposed conv on the fp32-operand kernel; VST_VGG_DGRAD_FPROP=0 keeps the latter
+VGG_DGRAD_FPROP = os.environ.get("VST_VGG_DGRAD_FPROP", "1") != "0"
 
 
 class _VGG(FlatNet):
@@ -110,8 +116,10 @@ class _VGG(FlatNet):
         P = {}
         for x, kind, cin, cout, m in self.layers:
             if kind == "conv":
+                # forward pack, transposed pack (the 3-channel first layer's data gradient), bias, and the
+                # rotated pack of the data gradient as a forward conv on the split-bf16 kernel (conv2d_dgrad_s1)
                 P[x] = (ops.weight_pack(m.weight, ops.PACK_FWD), ops.weight_pack(m.weight, ops.PACK_DGRAD),
-                        m.bias.detach())
+                        m.bias.detach(), ops.weight_pack(m.weight, ops.PACK_IKF) if cin > 4 else None)
         return P
 
     def forward_nhwc(self, x):
@@ -153,7 +161,7 @@ class _VggFn(torch.autograd.Function):
         ends = {b - 1 for _, b in net.slices_idx}
         for x_idx, kind, cin, cout, m in net.layers:
             if kind == "conv":
-                kc, _, b = P[x_idx]
+                kc, _, b, _ = P[x_idx]
                 # the ReLU at x_idx + 1 is fused into the conv epilogue
                 a = ops.conv2d_fwd(a, kc, b, cpad(cout), 3, 3, 1, 1, "zero", act="relu", role=role)
             elif kind == "pool":
@@ -189,8 +197,11 @@ class _VggFn(torch.autograd.Function):
                     g = None
                     break
                 xin = acts[i]
-                _, ck, _ = P[x_idx]
-                g = ops.conv2d_tfwd(g, ck, None, xin.shape[1], xin.shape[2], xin.shape[-1], 3, 3, 1, 1)
+                _, ck, _, ikf = P[x_idx]
+                if ikf is not None and VGG_DGRAD_FPROP:
+                    g = ops.conv2d_dgrad_s1(g, ikf, xin.shape[1], xin.shape[2], xin.shape[-1], 3, 1, "zero")
+                else:
+                    g = ops.conv2d_tfwd(g, ck, None, xin.shape[1], xin.shape[2], xin.shape[-1], 3, 3, 1, 1)
             else:
                 g = ops.maxpool2_bwd(g, acts[i])
         ctx.acts = None

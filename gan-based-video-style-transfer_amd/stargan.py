@@ -19,6 +19,8 @@ MI355X design:
     incoming gradient made on the fly; LeakyReLU' masks re-applied by the act-backward kernel.
     torch.autograd then composes the double backward of the gradient penalty from these.
 """
+import contextlib
+
 import numpy as np
 import torch
 import torch.nn as nn
@@ -64,6 +66,17 @@ SG_PHASES = __import__("os").environ.get("VST_SG_PHASES", "1") != "0"
 # gradient_penalty around its autograd.grad call (a module global: the autograd engine runs the backward on
 # its device thread).
 _INPUT_GRAD_ONLY = [False]
+# Set by StarGANSolver around d_loss.backward(), whose only consumers of the discriminator's parameter gradients
+# are their .grad views of the flat gradient buffer: the conv weight / bias gradients (the main pass's and the
+# penalty's double-backward contributions) are then accumulated there by the kernels' accumulate mode instead of
+# being returned to autograd, whose AccumulateGrad would add each one in a pass of its own (the 1024 -> 2048
+# layer's 134 MB three times per iteration).  Never set around autograd.grad calls.
+_ACCUM_PARAM_GRADS = [False]
+SG_DIRECT = __import__("os").environ.get("VST_SG_DIRECT", "1") != "0"  # 0: autograd accumulation, D trained in G step
+
+
+def _direct(p):
+    return _ACCUM_PARAM_GRADS[0] and p is not None and p.grad is not None and not torch.is_grad_enabled()
 
 
 class ConvSpec:
@@ -111,10 +124,11 @@ def _dgrad_raw(gz, ik, spec, H, W, phases=None):
     return ops.conv2d_tfwd(gz, ik, None, H, W, spec.cip, spec.R, spec.R, spec.stride, spec.pad)
 
 
-def _wgrad_raw(x, gz, spec):
-    gw = torch.empty((spec.co, spec.ci, spec.R, spec.R), device=x.device)  # accumulate=False stores every element
+def _wgrad_raw(x, gz, spec, out=None):
+    """The weight gradient as a new tensor, or (out: a .grad buffer) accumulated into out."""
+    gw = torch.empty((spec.co, spec.ci, spec.R, spec.R), device=x.device) if out is None else out
     ops.conv2d_wgrad(x, gz, gw, None, spec.R, spec.R, spec.stride, spec.pad, "zero", spec.co, spec.ci,
-                     spec.ci * spec.R * spec.R, spec.R * spec.R, accumulate=False)
+                     spec.ci * spec.R * spec.R, spec.R * spec.R, accumulate=out is not None)
     return gw
 
 
@@ -137,8 +151,18 @@ class _Conv(torch.autograd.Function):
         gz = _ActBwd.apply(g, a, spec.slope) if spec.act else g
         gx = _Dgrad.apply(gz, w, spec, x.shape[1], x.shape[2]) if ctx.needs_input_grad[0] else None
         only_x = _INPUT_GRAD_ONLY[0]
-        gw = _Wgrad.apply(x, gz, spec) if (ctx.needs_input_grad[1] and not only_x) else None
-        gb = _ChSum.apply(gz, spec.co) if (ctx.needs_input_grad[2] and not only_x) else None
+        gw = gb = None
+        m = spec.mod
+        if ctx.needs_input_grad[1] and not only_x:
+            if _direct(m.weight):
+                _wgrad_raw(x, gz, spec, out=m.weight.grad)
+            else:
+                gw = _Wgrad.apply(x, gz, spec)
+        if ctx.needs_input_grad[2] and not only_x:
+            if _direct(m.bias):
+                ops.channel_sum(gz, m.bias.grad, spec.co, accumulate=True)
+            else:
+                gb = _ChSum.apply(gz, spec.co)
         return gx, gw, gb, None
 
 
@@ -174,7 +198,12 @@ class _Dgrad(torch.autograd.Function):
         ggx = ggx.contiguous()
         ok, _, _ = spec.packs()
         d_gz = _conv_raw(ggx, ok, spec) if ctx.needs_input_grad[0] else None
-        d_w = _wgrad_raw(ggx, gz, spec) if ctx.needs_input_grad[1] else None
+        d_w = None
+        if ctx.needs_input_grad[1]:
+            if _direct(spec.mod.weight):
+                _wgrad_raw(ggx, gz, spec, out=spec.mod.weight.grad)
+            else:
+                d_w = _wgrad_raw(ggx, gz, spec)
         return d_gz, d_w, None, None, None
 
 
@@ -542,6 +571,18 @@ def gradient_penalty(y, x):
     return torch.mean((dydx_l2norm - 1) ** 2)
 
 
+@contextlib.contextmanager
+def _params_frozen(net):
+    ps = [p for p in net.parameters() if p.requires_grad and SG_DIRECT]
+    for p in ps:
+        p.requires_grad_(False)
+    try:
+        yield
+    finally:
+        for p in ps:
+            p.requires_grad_(True)
+
+
 class StarGANSolver:
     """The model/optimizer half of solver.py's Solver (build_model :125-140, train loop body
     :298-363, update_lr :170-175, reset_grad :177-180) on device-resident batches."""
@@ -592,7 +633,11 @@ class StarGANSolver:
         d_loss_gp = gradient_penalty(out_src, x_hat)
         d_loss = d_loss_real + d_loss_fake + self.lambda_cls * d_loss_cls + self.lambda_gp * d_loss_gp
         self.reset_grad()
-        d_loss.backward()
+        _ACCUM_PARAM_GRADS[0] = SG_DIRECT
+        try:
+            d_loss.backward()
+        finally:
+            _ACCUM_PARAM_GRADS[0] = False
         if self.grad_hook is not None:
             self.grad_hook([self.D])
         self.d_optimizer.step()
@@ -601,7 +646,10 @@ class StarGANSolver:
         # 3. generator
         if (self.i + 1) % self.n_critic == 0:
             x_fake = self.G(x_real, c_trg)
-            out_src, out_cls = self.D(x_fake)
+            # D's parameter gradients of the G step (the reference back-propagates into them) are zeroed by the
+            # next reset_grad before anything reads them: D runs here with its parameters frozen
+            with _params_frozen(self.D):
+                out_src, out_cls = self.D(x_fake)
             g_loss_fake = -torch.mean(out_src)
             g_loss_cls = classification_loss(out_cls, c_trg, self.dataset)
             x_reconst = self.G(x_fake, c_org)

@@ -25,6 +25,11 @@ from .networks import Conv2d, FlatNet, _Marker, _ToNCHW, _ToNHWC, _padded_bias
 from .ops import cpad
 from .optim import FusedAdam
 
+# The 3x3 stride-1 data gradients (residual blocks, upsampling convs) as forward convs over the rotated taps on the
+# split-bf16 kernel with the reflect border GEMM (ops.conv2d_dgrad_s1, the generator's route) instead of the
+# transposed conv on the fp32-operand kernel; VST_FS_DGRAD_FPROP=0 keeps the latter
+FS_DGRAD_FPROP = __import__("os").environ.get("VST_FS_DGRAD_FPROP", "1") != "0"
+
 
 class InstanceNormAffine(nn.Module):
     """Parameter holder with nn.InstanceNorm2d(affine=True)'s state (weight=1, bias=0)."""
@@ -148,8 +153,10 @@ class FastStyleNet(FlatNet):
         P = {}
         for name, m in self.named_modules():
             if isinstance(m, Conv2d):
+                # + the rotated pack of the 3x3 stride-1 layers' data gradient as a forward conv (conv2d_dgrad_s1)
+                s1 = m.kernel_size == 3 and m.stride == 1
                 P[name] = (ops.weight_pack(m.weight, ops.PACK_FWD), ops.weight_pack(m.weight, ops.PACK_DGRAD),
-                           _padded_bias(m))
+                           _padded_bias(m), ops.weight_pack(m.weight, ops.PACK_IKF) if s1 else None)
         return P
 
     def forward_nhwc(self, x, style_strength=1.0):
@@ -173,7 +180,7 @@ class _FastStyleFn(torch.autograd.Function):
         sv = {"x": x}
 
         def conv(inp, key, cout, k, st):
-            kc, _, b = P[key]
+            kc, _, b, _ = P[key]
             return ops.conv2d_fwd(inp, kc, b, cpad(cout), k, k, st, k // 2, "reflect", role=role)
 
         def cir(inp, layer, key, cout, k, st):
@@ -229,9 +236,11 @@ class _FastStyleFn(torch.autograd.Function):
                              co, ci, ci * k * k, k * k, accumulate=True)
 
         def dgrad(dy, key, xin, k, st, addend=None):
-            _, ck, _ = P[key]
+            _, ck, _, ikf = P[key]
             N, H, W, C = xin.shape
             p = k // 2
+            if st == 1 and ikf is not None and FS_DGRAD_FPROP:  # interior conv + border GEMM (the generator's route)
+                return ops.conv2d_dgrad_s1(dy, ikf, H, W, C, k, p, "reflect", addend=addend)
             if st == 1:
                 return ops.conv2d_tfwd(dy, ck, None, H, W, C, k, k, 1, p, pad_mode="reflect", addend=addend)
             # strided reflect conv: data gradient of the valid conv into the padded frame, then fold

@@ -15,5 +15,5 @@ if __name__ == "__main__":
     _lib.load()
     j = bench.johnson_train_fps(dev, steps=10)
     c = bench.c3_train_fps(dev)
-    print(json.dumps({"arm": os.environ.get("VST_VGG_DGRAD_FPROP", "default"), "johnson_ms": j["ms_per_step"],
+    print(json.dumps({"arm": os.environ.get("VST_VGG_DGRAD_FPROP", "default") + "/" + os.environ.get("VST_FS_DGRAD_FPROP", "default"), "johnson_ms": j["ms_per_step"],
                       "johnson_frac": j["roofline"]["frac"], "c3_ms": c["ms_per_step"], "c3_frac": c["roofline"]["frac"]}))

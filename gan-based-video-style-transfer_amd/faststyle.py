@@ -21,7 +21,7 @@ import torch
 import torch.nn as nn
 
 from . import ops, perceptual
-from .networks import Conv2d, FlatNet, _Marker, _ToNCHW, _ToNHWC, _padded_bias
+from .networks import Conv2d, FlatNet, _Marker, _ToNCHW, _ToNHWC, _pad_channels, _padded_bias
 from .ops import cpad
 from .optim import FusedAdam
 
@@ -29,6 +29,11 @@ from .optim import FusedAdam
 # split-bf16 kernel with the reflect border GEMM (ops.conv2d_dgrad_s1, the generator's route) instead of the
 # transposed conv on the fp32-operand kernel; VST_FS_DGRAD_FPROP=0 keeps the latter
 FS_DGRAD_FPROP = __import__("os").environ.get("VST_FS_DGRAD_FPROP", "1") != "0"
+# The 9x9 32 -> 3 output layer on the tap routes of the generator's 7x7 output layer: forward as the 1x1 conv into
+# (tap, co) channels + the tap sum (ops.tap_conv_fwd), weight gradient as the swapped GEMM (tap_conv_wgrad_swap),
+# data gradient as the forward conv of the 8-channel-padded dy over the rotated taps + reflect fold; instead of the
+# VALU skinny kernels and the fp32-operand transposed conv.  VST_FS_TAP=0 keeps those.
+FS_TAP = __import__("os").environ.get("VST_FS_TAP", "1") != "0"
 
 
 class InstanceNormAffine(nn.Module):
@@ -157,6 +162,9 @@ class FastStyleNet(FlatNet):
                 s1 = m.kernel_size == 3 and m.stride == 1
                 P[name] = (ops.weight_pack(m.weight, ops.PACK_FWD), ops.weight_pack(m.weight, ops.PACK_DGRAD),
                            _padded_bias(m), ops.weight_pack(m.weight, ops.PACK_IKF) if s1 else None)
+        if FS_TAP:  # the output layer's (CK pack of the tap forward, 8-output IKF pack of its data gradient)
+            w = self.deconv3.conv2d.weight
+            P["deconv3.tap"] = (ops.weight_pack(w, ops.PACK_CK), ops.weight_pack(w, ops.PACK_IKF, Op=8))
         return P
 
     def forward_nhwc(self, x, style_strength=1.0):
@@ -215,7 +223,10 @@ class _FastStyleFn(torch.autograd.Function):
             y, s, an = cir(up, getattr(net, name), name + ".conv2d", cout, 3, 1)
             sv[name] = (up, y, s)
             a = an
-        y = conv(a, "deconv3.conv2d", 3, 9, 1)
+        if "deconv3.tap" in P:
+            y = ops.tap_conv_fwd(a, P["deconv3.tap"][0], P["deconv3.conv2d"][2], 9, 4, "reflect", role=role)
+        else:
+            y = conv(a, "deconv3.conv2d", 3, 9, 1)
         out = ops.scaled_tanh(y, 3)
         sv["deconv3"] = (a, y)
         ctx.sv, ctx.net, ctx.P, ctx.strength = sv, net, P, strength
@@ -262,8 +273,17 @@ class _FastStyleFn(torch.autograd.Function):
             a, y = sv["deconv3"]
             gy = ops.scaled_tanh_bwd(y, gout.contiguous(), 3)
             m = net.deconv3.conv2d
-            wgrad(m, a, gy, 9, 1, db=True)
-            g = dgrad(gy, "deconv3.conv2d", a, 9, 1)
+            tap = P.get("deconv3.tap")
+            if tap is not None and train_w and ops.tap_conv_wgrad_swap_ok(a, 9, 4, "reflect", co=m.weight.shape[0]):
+                ops.tap_conv_wgrad_swap(a, gy, m.weight.grad, 9, 4, "reflect", accumulate=True, db=m.bias.grad)
+            else:
+                wgrad(m, a, gy, 9, 1, db=True)
+            if tap is not None:
+                gp = _pad_channels(gy, 8)
+                gp.vst_real_c = 3  # (tools/convflops: the MACs of the 3 real channels)
+                g = ops.conv2d_dgrad_s1(gp, tap[1], a.shape[1], a.shape[2], a.shape[-1], 9, 4, "reflect")
+            else:
+                g = dgrad(gy, "deconv3.conv2d", a, 9, 1)
             for name in ("deconv2", "deconv1"):
                 up, y, s = sv[name]
                 layer = getattr(net, name)

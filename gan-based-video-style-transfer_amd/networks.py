@@ -738,8 +738,9 @@ class _GeneratorFn(torch.autograd.Function):
         elif "f4" in P["ikf"] and g.shape[-1] == 4:
             ga = ops.conv2d_dgrad_s1(g, P["ikf"]["f4"], a.shape[1], a.shape[2], a.shape[-1], 7, 3, "reflect")
         elif "f8" in P["ikf"] and g.shape[-1] == 4:
-            ga = ops.conv2d_dgrad_s1(_pad_channels(g, 8), P["ikf"]["f8"], a.shape[1], a.shape[2], a.shape[-1], 7,
-                                     3, "reflect")
+            g8 = _pad_channels(g, 8)
+            g8.vst_real_c = 3  # (tools/convflops: the MACs of the 3 real channels)
+            ga = ops.conv2d_dgrad_s1(g8, P["ikf"]["f8"], a.shape[1], a.shape[2], a.shape[-1], 7, 3, "reflect")
         else:
             ga = dgrad_reflect(g, "f", a.shape[-1], 7, 3, a.shape[1], a.shape[2])
         # up-sampling convT layers

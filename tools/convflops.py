@@ -53,8 +53,9 @@ def _wgrad(a, k):
 def _dgrad_s1(a, k):
     dy, H, W, cx, R = a[0], a[2], a[3], a[4], a[5]
     N, _, _, C = dy.shape
-    return 2.0 * N * H * W * real(C) * real(cx) * R * R, "dgrad%dx%d s1 %d->%d @%dx%d N=%d" % (
-        R, R, real(C), real(cx), H, W, N)
+    C = getattr(dy, "vst_real_c", None) or real(C)  # a 3-channel dy padded to 8 (the tap layers' data gradients)
+    return 2.0 * N * H * W * C * real(cx) * R * R, "dgrad%dx%d s1 %d->%d @%dx%d N=%d" % (
+        R, R, C, real(cx), H, W, N)
 
 
 def _dgrad_refl(a, k):
@@ -86,7 +87,7 @@ def _c4s2(a, k):
 def _tap(a, k):
     x, R = a[0], a[3] if len(a) > 3 and isinstance(a[3], int) else a[2]
     N, H, W, C = x.shape
-    return 2.0 * N * H * W * 64 * 3 * R * R, "%dx%d 64<->3 tap route @%dx%d N=%d" % (R, R, H, W, N)
+    return 2.0 * N * H * W * C * 3 * R * R, "%dx%d %d<->3 tap route @%dx%d N=%d" % (R, R, C, H, W, N)
 
 
 def _tap_w(a, k):

@@ -138,6 +138,8 @@ SIGNATURES = {
     "vst_fc2_unpack": (I, [P, P, P, P, P, I, I, I, P]),
     "vst_weight_pack_split": (I, [P, P, P, I, I, I, I, I, I, I, P]),
     "vst_conv2d_fwd_hw": (I, [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, I, P]),
+    "vst_conv2d_fwd_hw_ws_bytes": (SZ, [I, I, I, I, I, I, I, I, I, I, I]),
+    "vst_conv2d_fwd_hw_ws": (I, [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, I, P, SZ, P]),
     "vst_conv2d_fwd_hwp": (I, [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, F, I, P]),
     "vst_tapconv_h_fwd": (I, [P, P, P, P, P, P, I, I, I, I, I, I, I, I, F, I, P]),
     "vst_tapshift_planes": (I, [P, P, L, I, I, I, I, P]),

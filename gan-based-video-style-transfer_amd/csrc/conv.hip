@@ -1069,6 +1069,24 @@ extern "C" int vst_conv2d_fwd_hw(const float* x, const float* wp, const void* ws
                        slope, math, (hipStream_t)stream);
 }
 
+// vst_conv2d_fwd_hw with a workspace: the split-K plans of vst_conv2d_fwd_ws for grids that cannot fill the CUs
+// (RAFT's SepConvGRU (1,5) / (5,1) convs at 1/8 resolution: M = 7040 rows at Sintel size)
+extern "C" size_t vst_conv2d_fwd_hw_ws_bytes(int N, int H, int W, int Cx, int Cop, int R, int S, int stride, int pad_h,
+                                             int pad_w, int math) {
+  if (N <= 0 || H <= 0 || W <= 0 || R <= 0 || S <= 0 || stride <= 0 || Cx % 8 || Cop == 4) return 0;
+  const int Ho = (H + 2 * pad_h - R) / stride + 1, Wo = (W + 2 * pad_w - S) / stride + 1;
+  if (Ho <= 0 || Wo <= 0 || g_tile_override[0] >= 0) return 0;
+  return bf_fprop_ws_floats((long)N * Ho * Wo, Cop, Cx, R, S, math) * sizeof(float);
+}
+
+extern "C" int vst_conv2d_fwd_hw_ws(const float* x, const float* wp, const void* wsplit, const float* bias, float* y,
+                                    int N, int H, int W, int Cx, int Cop, int R, int S, int stride, int pad_h,
+                                    int pad_w, int act, float slope, int math, float* ws, size_t ws_bytes,
+                                    void* stream) {
+  return conv_fwd_impl(x, wp, wsplit, bias, y, N, H, W, Cx, Cop, R, S, stride, pad_h, pad_w, VST_PAD_ZERO, act,
+                       slope, math, (hipStream_t)stream, nullptr, nullptr, ws, ws_bytes);
+}
+
 // One phase (a, b) of a stride-2 ConvTranspose2d(k3, p1, op1) stored straight into the interleaved
 // 2H x 2W output y (the phase conv of conv2d_fwd_hw(x, wp, R = 1 + a, S = 1 + b, pad a / b), whose pixel
 // (ph, pw) is y's (2(ph-a)+a, 2(pw-b)+b)): the four phases replace four phase images + the

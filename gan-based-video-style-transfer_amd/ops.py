@@ -1067,6 +1067,11 @@ def u8_image_to_nhwc4(x):
 
 
 # ----------------------------------------------------------------------------------- RAFT
+# conv2d_fwd_hw with the split-K plans of the square convs' workspace path (RAFT's SepConvGRU convs);
+# VST_FWD_HW_SPLITK=0: the one-launch plans
+FWD_HW_SPLITK = os.environ.get("VST_FWD_HW_SPLITK", "1") != "0"
+
+
 def conv2d_fwd_hw(x, wp, bias, cop, R, S, stride, pad_h, pad_w, act="none", role="fwd"):
     """Forward conv with separate row / column zero padding (vst_conv2d_fwd_hw)."""
     _dev_check(x, wp, bias)
@@ -1074,8 +1079,15 @@ def conv2d_fwd_hw(x, wp, bias, cop, R, S, stride, pad_h, pad_w, act="none", role
     Ho = (H + 2 * pad_h - R) // stride + 1
     Wo = (W + 2 * pad_w - S) // stride + 1
     y = torch.empty((N, Ho, Wo, cop), device=x.device)
+    m = _math(role)
+    nb = int(lib().vst_conv2d_fwd_hw_ws_bytes(N, H, W, Cx, cop, R, S, stride, pad_h, pad_w, m)) if FWD_HW_SPLITK else 0
+    if nb:  # the split-K plans for small grids (vst_conv2d_fwd_hw_ws)
+        ws = torch.empty((nb + 3) // 4, device=x.device)
+        _call("vst_conv2d_fwd_hw_ws", _p(x), _p(wp), _p(getattr(wp, "vst_split", None)), _p(bias), _p(y), N, H, W,
+              Cx, cop, R, S, stride, pad_h, pad_w, ACT[act], 0.0, m, _p(ws), nb, _stream())
+        return y
     _call("vst_conv2d_fwd_hw", _p(x), _p(wp), _p(getattr(wp, "vst_split", None)), _p(bias), _p(y), N, H, W, Cx,
-          cop, R, S, stride, pad_h, pad_w, ACT[act], 0.0, _math(role), _stream())
+          cop, R, S, stride, pad_h, pad_w, ACT[act], 0.0, m, _stream())
     return y
 
 

@@ -626,6 +626,13 @@ int vst_conv4s2_dgrad(const float* dy, const void* ws00, const void* ws01, const
 int vst_conv2d_fwd_hw(const float* x, const float* wp, const void* wsplit, const float* bias, float* y,
                       int N, int H, int W, int Cx, int Cop, int R, int S, int stride, int pad_h, int pad_w,
                       int act, float slope, int math, void* stream);
+/* vst_conv2d_fwd_hw with a caller-owned workspace: the split-K plans of vst_conv2d_fwd_ws for grids smaller than
+ * the CUs (ws_bytes >= vst_conv2d_fwd_hw_ws_bytes; ws may be NULL when that is 0). */
+size_t vst_conv2d_fwd_hw_ws_bytes(int N, int H, int W, int Cx, int Cop, int R, int S, int stride, int pad_h,
+                                  int pad_w, int math);
+int vst_conv2d_fwd_hw_ws(const float* x, const float* wp, const void* wsplit, const float* bias, float* y, int N,
+                         int H, int W, int Cx, int Cop, int R, int S, int stride, int pad_h, int pad_w, int act,
+                         float slope, int math, float* ws, size_t ws_bytes, void* stream);
 /* vst_conv2d_fwd_hw with a padding mode (VST_PAD_ZERO / VST_PAD_REFLECT). */
 int vst_conv2d_fwd_hwp(const float* x, const float* wp, const void* wsplit, const float* bias, float* y, int N, int H,
                        int W, int Cx, int Cop, int R, int S, int stride, int pad_h, int pad_w, int pad_mode, int act,

@@ -1,4 +1,5 @@
-"""RAFT inference timing standalone (bench.raft_inference) at the Sintel and MoGAN sizes."""
+"""RAFT timings (bench.raft_inference at 436x1024 B=1 and 256x256 B=4, 20 iterations) standalone: the A/B tool for
+the SepConvGRU convs' split-K plans (VST_FWD_HW_SPLITK)."""
 import json
 import os
 import sys
@@ -9,10 +10,10 @@ import torch  # noqa: E402
 import bench  # noqa: E402
 
 if __name__ == "__main__":
-    from gbvst import _lib, ops
-    _lib.load()
     dev = torch.device("cuda:0")
-    for pol in sys.argv[1:] or ["mixed"]:
-        ops.set_conv_math(pol)
-        print(pol, json.dumps(bench.raft_inference(dev)))
-        print(pol, json.dumps(bench.raft_inference(dev, B=4, H=256, W=256)))
+    from gbvst import _lib
+    _lib.load()
+    a = bench.raft_inference(dev, reps=5)
+    b = bench.raft_inference(dev, B=4, H=256, W=256, reps=5)
+    print(json.dumps({"arm": os.environ.get("VST_FWD_HW_SPLITK", "default"), "sintel_ms": a["ms_per_call"],
+                      "sintel_frac": a["roofline"]["frac"], "b4_256_ms": b["ms_per_call"], "b4_256_frac": b["roofline"]["frac"]}))

@@ -1001,10 +1001,11 @@ def corr_pyramid(pyr, P, H2, W2, ld0, levels):
     _call("vst_corr_pyramid", _p(pyr), P, H2, W2, ld0, levels, _stream())
 
 
-def corr_lookup(pyr, coords, B, H1, W1, H2, W2, ld0, levels, radius):
+def corr_lookup(pyr, coords, B, H1, W1, H2, W2, ld0, levels, radius, cs=None):
+    """cs: the output channel stride (default cpad; the padded channels are written as zeros)."""
     _dev_check(pyr, coords)
     K = 2 * radius + 1
-    cs = cpad(levels * K * K)
+    cs = cs or cpad(levels * K * K)
     out = torch.empty((B, H1, W1, cs), device=pyr.device)
     _call("vst_corr_lookup", _p(pyr), _p(coords), _p(out), B, H1, W1, H2, W2, ld0, levels, radius, cs,
           _stream())

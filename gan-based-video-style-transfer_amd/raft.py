@@ -144,14 +144,20 @@ class BasicUpdateBlock(nn.Module):
 ###############################################################################
 # packs
 ###############################################################################
-def _pack(w, b):
-    """OK pack (+ bf16 split planes) and the channel-padded bias of a conv weight [Co, Ci, kh, kw]."""
+# The correlation features' channel stride: 4 levels x 81 = 324 padded to 328, so that convc1 (1x1, 324 -> 256) runs
+# on the split-bf16 kernel (K in 8-channel chunks) instead of the fp32-operand one; VST_RAFT_CS8=0 keeps 324
+_CORR_CS = 328 if __import__("os").environ.get("VST_RAFT_CS8", "1") != "0" else None
+
+
+def _pack(w, b, ip=None):
+    """OK pack (+ bf16 split planes) and the channel-padded bias of a conv weight [Co, Ci, kh, kw]; ip: the input
+    channel stride the pack is laid out for (default cpad)."""
     co = w.shape[0]
     bp = None
     if b is not None:
         bp = torch.zeros(cpad(co), device=w.device)
         bp[:co] = b
-    return ops.weight_pack(w.contiguous(), ops.PACK_FWD), bp
+    return ops.weight_pack(w.contiguous(), ops.PACK_FWD, Ip=ip), bp
 
 
 def _fold_bn(conv, bn):
@@ -165,7 +171,7 @@ def _fold_bn(conv, bn):
 
 
 class _ConvOp:
-    def __init__(self, conv, bn=None, scale=None, cat_with=None):
+    def __init__(self, conv, bn=None, scale=None, cat_with=None, ip=None):
         w, b = _fold_bn(conv, bn) if bn is not None else (conv.weight.detach(), conv.bias.detach()
                                                           if conv.bias is not None else None)
         if cat_with is not None:
@@ -173,7 +179,7 @@ class _ConvOp:
             b = torch.cat([b, cat_with.bias.detach()], 0)
         if scale is not None:
             w, b = w * scale, b * scale
-        self.wp, self.bias = _pack(w, b)
+        self.wp, self.bias = _pack(w, b, ip)
         self.cop = cpad(w.shape[0])
         self.kh, self.kw, self.ph, self.pw, self.stride = conv.kh, conv.kw, conv.ph, conv.pw, conv.stride
 
@@ -267,7 +273,7 @@ class RAFT(nn.Module):
         u = self.update_block
         g = u.gru
         return {"fnet": enc(self.fnet), "cnet": enc(self.cnet),
-                "convc1": _ConvOp(u.encoder.convc1), "convc2": _ConvOp(u.encoder.convc2),
+                "convc1": _ConvOp(u.encoder.convc1, ip=_CORR_CS), "convc2": _ConvOp(u.encoder.convc2),
                 "convf1": _ConvOp(u.encoder.convf1), "convf2": _ConvOp(u.encoder.convf2),
                 "conv": _ConvOp(u.encoder.conv),
                 "zr1": _ConvOp(g.convz1, cat_with=g.convr1), "q1": _ConvOp(g.convq1),
@@ -332,7 +338,7 @@ class RAFT(nn.Module):
         cat = torch.empty((B, h8, w8, 256), device=dev)
         preds = []
         for it in range(iters):
-            corr = corr_fn.lookup_nhwc(coords1)
+            corr = corr_fn.lookup_nhwc(coords1, cs=_CORR_CS)
             ops.raft_flow4(coords1, flow4)
             # BasicMotionEncoder (update.py:88-98)
             cor = P["convc2"](P["convc1"](corr, "relu", role), "relu", role)

@@ -77,10 +77,11 @@ class CorrBlock:
                 off += P * h * w
         return self.pyr[off:off + P * h * w].view(P, 1, h, w)
 
-    def lookup_nhwc(self, coords):
-        """[B, H, W, cpad(L*(2r+1)^2)] window features at coords [B, 2, H, W] (x, y pixels)."""
+    def lookup_nhwc(self, coords, cs=None):
+        """[B, H, W, cs or cpad(L*(2r+1)^2)] window features at coords [B, 2, H, W] (x, y pixels); the channels
+        past L*(2r+1)^2 are zero."""
         return ops.corr_lookup(self.pyr, coords.float().contiguous(), self.B, self.H, self.W, self.H,
-                               self.W, self.ld0, self.num_levels, self.radius)
+                               self.W, self.ld0, self.num_levels, self.radius, cs=cs)
 
     def __call__(self, coords):
         K = 2 * self.radius + 1

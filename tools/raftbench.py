@@ -15,5 +15,5 @@ if __name__ == "__main__":
     _lib.load()
     a = bench.raft_inference(dev, reps=5)
     b = bench.raft_inference(dev, B=4, H=256, W=256, reps=5)
-    print(json.dumps({"arm": os.environ.get("VST_FWD_HW_SPLITK", "default"), "sintel_ms": a["ms_per_call"],
+    print(json.dumps({"arm": os.environ.get("VST_FWD_HW_SPLITK", "d") + "/" + os.environ.get("VST_RAFT_CS8", "d"), "sintel_ms": a["ms_per_call"],
                       "sintel_frac": a["roofline"]["frac"], "b4_256_ms": b["ms_per_call"], "b4_256_frac": b["roofline"]["frac"]}))

@@ -1345,7 +1345,10 @@ extern "C" int vst_conv2d_wgrad_pre(const float* x, const float* x_t, const floa
                        p.nsplit, WG_GROUP);
     red = l2;
   }
-  if (g_wg_red16)  // 16-row blocks: twice the blocks (the 2304 x 256 ResnetBlock gradient: 288 -> 576)
+  // 16-row blocks: twice the blocks (the 2304 x 256 ResnetBlock gradient: 288 -> 576); with at most 2 slabs the pass is
+  // a transpose whose stores / accumulate reads are 16 floats per channel row with 16-row blocks: 32-row blocks keep
+  // them whole 128-B lines (the StarGAN discriminator's 1024 -> 2048 layer, one slab, accumulated: 134 MB)
+  if (g_wg_red16 && nred > 2)
     hipLaunchKernelGGL(wgrad_reduce_store_k<1>, dim3(ceil_div(Ci * R * S, 16), ceil_div(Co, 64)), dim3(256), 0, s,
                        red, dw, Cxg, Cyp, R * S, Co, Ci, so, si, accumulate, nred, slab);
   else

@@ -526,15 +526,19 @@ def test_convT_phases(ops, conv_math, ci, co, h, w):
     xn = _nhwc(x, ops)
     y = ops.convT3s2_fwd(xn, packs, b.to(DEV), co)
     _close(_nchw(y, co, ops), ref, tol=CONV_TOL[conv_math], what="convT phases")
-    prev, prev_g = ops.CONVT_DIRECT, ops.CONVT_GROUPED
+    prev, prev_g, prev_s = ops.CONVT_DIRECT, ops.CONVT_GROUPED, ops.FWD_HW_SPLITK
     try:
         ops.CONVT_GROUPED = False
         y_ph = ops.convT3s2_fwd(xn, packs, b.to(DEV), co)
         ops.CONVT_DIRECT = False
+        ops.FWD_HW_SPLITK = False  # the phase images on the same one-launch plans as the phase stores
         y_il = ops.convT3s2_fwd(xn, packs, b.to(DEV), co)
+        ops.FWD_HW_SPLITK = True   # ... and on the small grids' split-K plans: within fp32 rounding
+        y_sk = ops.convT3s2_fwd(xn, packs, b.to(DEV), co)
     finally:
-        ops.CONVT_DIRECT, ops.CONVT_GROUPED = prev, prev_g
+        ops.CONVT_DIRECT, ops.CONVT_GROUPED, ops.FWD_HW_SPLITK = prev, prev_g, prev_s
     assert torch.equal(y_ph, y_il)
+    _close(y_sk, y_il, tol=1e-6, what="phase images on split-K plans")
     _close(y, y_ph, tol=1e-6, what="grouped vs per-phase launches")
 
 

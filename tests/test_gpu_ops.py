@@ -538,7 +538,7 @@ def test_convT_phases(ops, conv_math, ci, co, h, w):
     finally:
         ops.CONVT_DIRECT, ops.CONVT_GROUPED, ops.FWD_HW_SPLITK = prev, prev_g, prev_s
     assert torch.equal(y_ph, y_il)
-    _close(y_sk, y_il, tol=1e-6, what="phase images on split-K plans")
+    _close(y_sk, y_il, tol=5e-6, what="phase images on split-K plans")  # fp32 summation order over K = 4 Ci
     _close(y, y_ph, tol=1e-6, what="grouped vs per-phase launches")
 
 

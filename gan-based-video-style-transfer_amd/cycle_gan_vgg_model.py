@@ -23,6 +23,8 @@ from . import ops, perceptual
 from .cycle_gan_model import CycleGANModel
 
 CONTENT_LEVEL = 3  # relu4_1
+# the loss's three VGG forwards as one batch (perceptual._VggMultiFn); VST_VGG_BATCHED=0: three calls
+VGG_BATCHED = __import__("os").environ.get("VST_VGG_BATCHED", "1") != "0"
 SEEDED_LAMBDA = (100.0, 500.0)       # (content, style) for the seeded kaiming fan_out VGG-19
 PRETRAINED_LAMBDA = (1.0, 0.01)      # for real (or fan_in-scale) VGG-19 weights
 
@@ -71,18 +73,31 @@ class CycleGANVGGModel(CycleGANModel):
         mean, std = perceptual._mean_std(self.device)
         self._vgg_mean, self._vgg_std = (mean - 0.5).contiguous(), std
 
+    def _vgg_in(self, img_nhwc4):
+        """normalize((x + 1) / 2) of an NHWC4 image in [-1, 1] (the VGG input)."""
+        return perceptual._NormalizeFn.apply(img_nhwc4, self._vgg_mean, self._vgg_std, 2.0, 3)
+
     def vgg_features(self, img_nhwc4):
         """Vgg19(normalize((x + 1) / 2)) of an NHWC4 image in [-1, 1] -> 5 NHWC slice outputs."""
-        x = perceptual._NormalizeFn.apply(img_nhwc4, self._vgg_mean, self._vgg_std, 2.0, 3)
-        return self.netVGG.forward_nhwc(x)
+        return self.netVGG.forward_nhwc(self._vgg_in(img_nhwc4))
 
     def extra_G_loss(self):
         if not self.temporal:
             raise NotImplementedError('cycle_gan_vgg composes the temporal (CycleGANCon) step: lambda_T > 0')
-        f = self.vgg_features(self.fake_B2)
-        with torch.no_grad():
-            fc = self.vgg_features(self.real_A2)[CONTENT_LEVEL]
-            gs = [perceptual.gram_nhwc(t) for t in self.vgg_features(self.real_B)]
+        if VGG_BATCHED:  # the three forwards as one batch (perceptual._VggMultiFn): fake_B2 (differentiated), real_B
+            # (all levels: style Grams), real_A2 (through the content level only)
+            nl = len(self.netVGG.slices_idx)
+            with torch.no_grad():
+                xb, xa = self._vgg_in(self.real_B), self._vgg_in(self.real_A2)
+            f, fb, fa = self.netVGG.forward_multi_nhwc([self._vgg_in(self.fake_B2), xb, xa], [nl, nl, CONTENT_LEVEL + 1])
+            fc = fa[CONTENT_LEVEL]
+            with torch.no_grad():
+                gs = [perceptual.gram_nhwc(t) for t in fb]
+        else:
+            f = self.vgg_features(self.fake_B2)
+            with torch.no_grad():
+                fc = self.vgg_features(self.real_A2)[CONTENT_LEVEL]
+                gs = [perceptual.gram_nhwc(t) for t in self.vgg_features(self.real_B)]
         self.loss_G_C = perceptual.mse_loss(f[CONTENT_LEVEL], fc, self.opt.lambda_content)
         style = None
         for fi, gi in zip(f, gs):

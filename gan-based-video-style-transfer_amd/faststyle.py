@@ -34,6 +34,9 @@ FS_DGRAD_FPROP = __import__("os").environ.get("VST_FS_DGRAD_FPROP", "1") != "0"
 # data gradient as the forward conv of the 8-channel-padded dy over the rotated taps + reflect fold; instead of the
 # VALU skinny kernels and the fp32-operand transposed conv.  VST_FS_TAP=0 keeps those.
 FS_TAP = __import__("os").environ.get("VST_FS_TAP", "1") != "0"
+# The loss network's two forwards (styled image, content image) as one batch (perceptual._VggMultiFn);
+# VST_VGG_BATCHED=0: two calls
+VGG_BATCHED = __import__("os").environ.get("VST_VGG_BATCHED", "1") != "0"
 
 
 class InstanceNormAffine(nn.Module):
@@ -361,9 +364,16 @@ class Johnson:
     def losses_nhwc(self, img_nhwc):
         """train_method's loss graph on an NHWC4 [0,1] image batch -> (loss, cl, sl, tv, styled)."""
         _, styled = self.model.forward_nhwc(img_nhwc)
-        styled_f = self.vgg.forward_nhwc(perceptual.normalize_nhwc(styled, d0=255.0))
-        with torch.no_grad():
-            img_f = self.vgg.forward_nhwc(perceptual.normalize_nhwc(img_nhwc))
+        if VGG_BATCHED:  # styled (differentiated) and the content image through the VGG as one batch, the content
+            # image through the slices its loss reads only (relu3_3)
+            with torch.no_grad():
+                xc = perceptual.normalize_nhwc(img_nhwc)
+            styled_f, img_f = self.vgg.forward_multi_nhwc([perceptual.normalize_nhwc(styled, d0=255.0), xc],
+                                                          [len(self.vgg.slices_idx), 3])
+        else:
+            styled_f = self.vgg.forward_nhwc(perceptual.normalize_nhwc(styled, d0=255.0))
+            with torch.no_grad():
+                img_f = self.vgg.forward_nhwc(perceptual.normalize_nhwc(img_nhwc))
         content = perceptual.mse_loss(styled_f[2], img_f[2], self.alpha)
         grams = self._style_targets(img_nhwc.shape[0])
         style = None

@@ -126,6 +126,16 @@ class _VGG(FlatNet):
         """x: NHWC4 normalised image -> tuple of NHWC slice outputs."""
         return _VggFn.apply(x, self)
 
+    def forward_multi_nhwc(self, xs, levels):
+        """Images xs (NHWC4, normalised; the first one differentiable) through the net as one batch, xs[k] through its
+        first levels[k] slices (non-increasing) -> a list per image of its slice outputs (_VggMultiFn)."""
+        flat = _VggMultiFn.apply(xs[0], self, tuple(levels), *xs[1:])
+        out, off = [], 0
+        for n in levels:
+            out.append(flat[off:off + n])
+            off += n
+        return out
+
     def forward(self, X):
         outs = self.forward_nhwc(_ToNHWC.apply(X, cpad(3)))
         names = VGG_NAMES[self.arch]
@@ -174,38 +184,97 @@ class _VggFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, *gouts):
-        acts, net, P = ctx.acts, ctx.net, ctx.P
-        ends = [b - 1 for _, b in net.slices_idx]
-        gmap = {e: g for e, g in zip(ends, gouts)}
-        g = None
-        for i in reversed(range(len(net.layers))):
-            x_idx, kind, cin, cout, m = net.layers[i]
-            go = gmap.get(x_idx)
-            if go is not None:
-                go = go.contiguous()
-                if g is None:
-                    g = go.clone()
-                else:
-                    ops.axpby(go, g, 1.0, 1.0)
-            if g is None:
-                continue
-            if kind == "relu":
-                # acts[i + 1] is the fused conv+ReLU output
-                g = ops.act_bwd(g, acts[i + 1], "relu")
-            elif kind == "conv":
-                if i == 0 and not ctx.needs_input_grad[0]:
-                    g = None
-                    break
-                xin = acts[i]
-                _, ck, _, ikf = P[x_idx]
-                if ikf is not None and VGG_DGRAD_FPROP:
-                    g = ops.conv2d_dgrad_s1(g, ikf, xin.shape[1], xin.shape[2], xin.shape[-1], 3, 1, "zero")
-                else:
-                    g = ops.conv2d_tfwd(g, ck, None, xin.shape[1], xin.shape[2], xin.shape[-1], 3, 3, 1, 1)
-            else:
-                g = ops.maxpool2_bwd(g, acts[i])
+        g = _vgg_backward(ctx.acts, ctx.net, ctx.P, gouts, ctx.needs_input_grad[0])
         ctx.acts = None
         return g, None
+
+
+def _vgg_backward(acts, net, P, gouts, need_x, B0=None):
+    """The input gradient from the slice outputs' gradients (None = no gradient); B0: the activations hold a
+    larger batch whose first B0 images are the differentiated ones (_VggMultiFn)."""
+    cut = (lambda t: t[:B0]) if B0 is not None else (lambda t: t)
+    ends = [b - 1 for _, b in net.slices_idx]
+    gmap = {e: g for e, g in zip(ends, gouts)}
+    g = None
+    for i in reversed(range(len(net.layers))):
+        x_idx, kind, cin, cout, m = net.layers[i]
+        go = gmap.get(x_idx)
+        if go is not None:
+            go = go.contiguous()
+            if g is None:
+                g = go.clone()
+            else:
+                ops.axpby(go, g, 1.0, 1.0)
+        if g is None:
+            continue
+        if kind == "relu":
+            # acts[i + 1] is the fused conv+ReLU output
+            g = ops.act_bwd(g, cut(acts[i + 1]), "relu")
+        elif kind == "conv":
+            if i == 0 and not need_x:
+                return None
+            xin = acts[i]
+            _, ck, _, ikf = P[x_idx]
+            if ikf is not None and VGG_DGRAD_FPROP:
+                g = ops.conv2d_dgrad_s1(g, ikf, xin.shape[1], xin.shape[2], xin.shape[-1], 3, 1, "zero")
+            else:
+                g = ops.conv2d_tfwd(g, ck, None, xin.shape[1], xin.shape[2], xin.shape[-1], 3, 3, 1, 1)
+        else:
+            g = ops.maxpool2_bwd(g, cut(acts[i]))
+    return g
+
+
+class _VggMultiFn(torch.autograd.Function):
+    """Several NHWC4 images through the VGG as ONE batch (the perceptual losses: the differentiated image first, then
+    the no-grad targets), image k through its first levels[k] slices only: the inputs are ordered by non-increasing
+    levels, so the images a slice no longer needs are cut from the end of the batch (a contiguous prefix stays).
+    Per-image arithmetic is the separate calls' (every layer is per sample); only the GEMM plans see a larger M.
+    Returns the first image's slice outputs, then each other image's (detached copies)."""
+
+    @staticmethod
+    def forward(ctx, x0, net, levels, *rest):
+        if any(p.requires_grad for p in net.parameters()):
+            raise NotImplementedError("VGG weights are frozen on the HIP path (network.py:30-31, 69-70)")
+        ins = (x0,) + rest
+        if len(levels) != len(ins) or any(levels[k] < levels[k + 1] for k in range(len(ins) - 1)):
+            raise ValueError("_VggMultiFn: one level count per image, non-increasing")
+        ctx.set_materialize_grads(False)
+        P = net.packs()
+        role = "fwd" if ctx.needs_input_grad[0] else "infer"
+        Bs = [t.shape[0] for t in ins]
+        a = torch.cat([t.contiguous() for t in ins]) if len(ins) > 1 else x0
+        acts = [a]
+        ends = [b - 1 for _, b in net.slices_idx]
+        outs = [[] for _ in ins]
+        live = len(ins)
+        for x_idx, kind, cin, cout, m in net.layers:
+            if kind == "conv":
+                kc, _, b, _ = P[x_idx]
+                a = ops.conv2d_fwd(a, kc, b, cpad(cout), 3, 3, 1, 1, "zero", act="relu", role=role)
+            elif kind == "pool":
+                a = ops.maxpool2(a)
+            acts.append(a)
+            if x_idx in ends:
+                lvl = ends.index(x_idx) + 1
+                off = 0
+                for k in range(live):
+                    outs[k].append(a[off:off + Bs[k]])
+                    off += Bs[k]
+                if lvl == levels[0]:
+                    break
+                while live > 1 and levels[live - 1] == lvl:
+                    live -= 1
+                a = a[:sum(Bs[:live])]
+        rest_outs = [o.clone() for k in range(1, len(ins)) for o in outs[k]]
+        ctx.mark_non_differentiable(*rest_outs)
+        ctx.acts, ctx.net, ctx.P, ctx.B0, ctx.n0, ctx.nrest = acts, net, P, Bs[0], len(outs[0]), len(rest)
+        return tuple(outs[0]) + tuple(rest_outs)
+
+    @staticmethod
+    def backward(ctx, *gouts):
+        g = _vgg_backward(ctx.acts, ctx.net, ctx.P, gouts[:ctx.n0], ctx.needs_input_grad[0], ctx.B0)
+        ctx.acts = None
+        return (g, None, None) + (None,) * ctx.nrest
 
 
 # ------------------------------------------------------------------------------------ losses

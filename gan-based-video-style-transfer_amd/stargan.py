@@ -72,7 +72,7 @@ _INPUT_GRAD_ONLY = [False]
 # being returned to autograd, whose AccumulateGrad would add each one in a pass of its own (the 1024 -> 2048
 # layer's 134 MB three times per iteration).  Never set around autograd.grad calls.
 _ACCUM_PARAM_GRADS = [False]
-# 0: autograd accumulation, D's parameter gradients in the G step, the D step's fake generation with autograd
+# 0: autograd accumulation, D's parameter gradients in the G step
 SG_DIRECT = __import__("os").environ.get("VST_SG_DIRECT", "1") != "0"
 
 
@@ -619,11 +619,10 @@ class StarGANSolver:
         x_real = x_real.to(self.device).float().contiguous()
         c_org = label2onehot(label_org, self.c_dim, self.device)
         c_trg = label2onehot(label_trg, self.c_dim, self.device)
-        # 2. discriminator (real and fake through D as one batch: D is per-sample).  The reference builds G's graph
-        # here and only ever reads x_fake detached: the forward runs without it (same values, same running-stat
-        # updates)
-        with torch.no_grad() if SG_DIRECT else contextlib.nullcontext():
-            x_fake = self.G(x_real, c_trg)
+        # 2. discriminator (real and fake through D as one batch: D is per-sample).  x_fake is only read detached, but
+        # G runs with autograd as in the reference: its training-role arithmetic (the "mixed" policy computes
+        # no-grad forwards at bf16x3) is what the reference's fp32 forward is matched against
+        x_fake = self.G(x_real, c_trg)
         B = x_real.shape[0]
         out_src, out_cls = self.D(torch.cat([x_real, x_fake.detach()]))
         d_loss_real = -torch.mean(out_src[:B])

@@ -15,6 +15,6 @@ for r in 1 2; do
   done
 done
 TAG=r05cc/sg_new bash tools/gpu_sgtrace.sh > /dev/null || exit 1
-VST_SG_DIRECT=0 TAG=r05cc/sg_old bash tools/gpu_sgtrace.sh > /dev/null || exit 1
-head -1 $O/sg_new/sg_summary.txt; head -1 $O/sg_old/sg_summary.txt
+true
+head -1 $O/sg_new/sg_summary.txt
 exit 0

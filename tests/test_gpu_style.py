@@ -197,6 +197,36 @@ def test_vgg_vs_reference_golden(gb, golden, arch, base):
     assert _rel(x.grad, g[f"{arch}_dx"]) < 1e-4
 
 
+@pytest.mark.parametrize("arch,levels", [("vgg16", (4, 3)), ("vgg19", (5, 5, 4))])
+def test_vgg_multi_batch_equals_separate_calls(gb, arch, levels):
+    """perceptual._VggMultiFn (the perceptual losses' VGG forwards as one batch, image k through its first levels[k]
+    slices) vs one call per image: the slice outputs, the no-grad images' outputs (detached), and the first image's
+    input gradient, within fp32 GEMM-plan rounding (the batch only changes M)."""
+    from gbvst import ops
+    net = _vgg(gb, arch, 510 if arch == "vgg16" else 520)
+    xs = [_nhwc(_g(300 + k, (2, 3, 48, 64)), ops) for k in range(len(levels))]
+    wts = [_nhwc(_g(400 + i, (2, c, 48 >> i, 64 >> i)), ops)
+           for i, c in enumerate([64, 128, 256, 512, 512][:levels[0]])]
+    # separate calls
+    a = xs[0].clone().requires_grad_(True)
+    sep = net.forward_nhwc(a)
+    with torch.no_grad():
+        sep_rest = [net.forward_nhwc(x) for x in xs[1:]]
+    sum((f * w).sum() for f, w in zip(sep, wts)).backward()
+    # one batch
+    b = xs[0].clone().requires_grad_(True)
+    outs = net.forward_multi_nhwc([b] + xs[1:], list(levels))
+    assert [len(o) for o in outs] == list(levels)
+    assert all(not t.requires_grad for o in outs[1:] for t in o)
+    sum((f * w).sum() for f, w in zip(outs[0], wts)).backward()
+    for f, r in zip(outs[0], sep):
+        assert _rel(f, r) < 1e-5
+    for o, rs in zip(outs[1:], sep_rest):
+        for f, r in zip(o, rs):
+            assert _rel(f, r) < 1e-5
+    assert _rel(b.grad, a.grad) < 1e-5
+
+
 def _fsn(gb, base):
     from gbvst import faststyle
     from oracle import style_ref

@@ -5,22 +5,17 @@ discriminator backward passes (networks.FlatNet._grad_done).  Checks: buckets we
 the phase's join (during backward), and the averaged gradients equal the single-process B=4
 gradients (InstanceNorm per sample, batch-mean losses)."""
 import os
-import socket
+import shutil
+import tempfile
 
 import numpy as np
 import pytest
 import torch
 import torch.multiprocessing as mp
 
+from dist_harness import run_ranks
+
 pytestmark = pytest.mark.gpu
-
-
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
 
 
 def _setup(B_slice=None):
@@ -51,49 +46,26 @@ def _grads_hook(store, ex=None):
     return hook
 
 
-def _worker(rank, world, port, q):
-    import sys
-    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    import torch.distributed as dist
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    try:
-        import gbvst
-        from gbvst import dp
-        gbvst._lib.load()
-        torch.cuda.set_device(0)
-        m = _setup(slice(rank * 2, rank * 2 + 2))
-        nets = [m.netG_A, m.netG_B, m.netD_A, m.netD_B]
-        ex = dp.GradExchange(world, bucket_bytes=64 << 10).attach(nets)
-        grads = {}
-        m.optimize_parameters(_grads_hook(grads, ex), _grads_hook(grads, ex))
-        torch.cuda.synchronize()
-        logs = {name: list(ex._state(getattr(m, "net" + name)).last_log) for name in ("G_A", "G_B", "D_A", "D_B")}
-        out = {name: grads[id(getattr(m, "net" + name))].numpy() for name in ("G_A", "G_B", "D_A", "D_B")}
-        q.put((rank, out, logs, None))
-    except Exception as e:  # report, do not hang the parent
-        import traceback
-        q.put((rank, None, None, traceback.format_exc()))
-    dist.barrier()
-    dist.destroy_process_group()
+def _worker(rank, world):
+    import gbvst
+    from gbvst import dp
+    gbvst._lib.load()
+    torch.cuda.set_device(0)
+    m = _setup(slice(rank * 2, rank * 2 + 2))
+    nets = [m.netG_A, m.netG_B, m.netD_A, m.netD_B]
+    ex = dp.GradExchange(world, bucket_bytes=64 << 10).attach(nets)
+    grads = {}
+    m.optimize_parameters(_grads_hook(grads, ex), _grads_hook(grads, ex))
+    torch.cuda.synchronize()
+    logs = {name: list(ex._state(getattr(m, "net" + name)).last_log) for name in ("G_A", "G_B", "D_A", "D_B")}
+    out = {name: grads[id(getattr(m, "net" + name))].numpy() for name in ("G_A", "G_B", "D_A", "D_B")}
+    return out, logs
 
 
 @pytest.mark.timeout(600)
 def test_dp_world2_overlap_equals_single_process():
     world = 2
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    res = sorted([q.get(timeout=400) for _ in range(world)], key=lambda r: r[0])
-    for p in procs:
-        p.join(timeout=120)
-    for r in res:
-        assert r[3] is None, r[3]
-    for p in procs:
-        assert p.exitcode == 0
+    res = [(r, out, logs) for r, (out, logs) in enumerate(run_ranks(_worker, world, timeout=400))]
     import gbvst
     gbvst._lib.load()
     m = _setup()
@@ -119,14 +91,14 @@ def test_dp_world2_overlap_equals_single_process():
         assert len(res[0][2][name]) > 0, (name, res[0][2][name])
 
 
-def _nccl_worker(port, q):
+def _nccl_worker(init_file, q):
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch.distributed as dist
     try:
         torch.cuda.set_device(0)
-        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+        dist.init_process_group("nccl", init_method="file://" + init_file, rank=0, world_size=1,
+                                device_id=torch.device("cuda", 0))
         import gbvst
         from gbvst import dp, ops
         gbvst._lib.load()
@@ -159,10 +131,12 @@ def test_dp_nccl_world1_forced_buckets():
     back, or the join's scaling racing the collective) shows as a differing gradient or weight."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    p = ctx.Process(target=_nccl_worker, args=(_free_port(), q))
+    tmp = tempfile.mkdtemp(prefix="vst_pg_")
+    p = ctx.Process(target=_nccl_worker, args=(os.path.join(tmp, "store"), q))
     p.start()
     out, logs, w, backend, err = q.get(timeout=400)
     p.join(timeout=120)
+    shutil.rmtree(tmp, ignore_errors=True)
     assert err is None, err
     assert p.exitcode == 0
     assert backend == "nccl"
@@ -244,47 +218,24 @@ def _mogan_run(m, ex=None):
     return out
 
 
-def _mogan_worker(rank, world, port, q):
-    import sys
-    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    import torch.distributed as dist
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    try:
-        import gbvst
-        from gbvst import dp, ops
-        gbvst._lib.load()
-        torch.cuda.set_device(0)
-        ops.set_deterministic(True)
-        m = _mogan_setup(slice(rank * 2, rank * 2 + 2))
-        nets = [getattr(m, "net" + n) for n in _MG_NAMES]
-        ex = dp.GradExchange(world, bucket_bytes=64 << 10).attach(nets)
-        out = _mogan_run(m, ex)
-        logs = {n: list(ex._state(getattr(m, "net" + n)).last_log) for n in _MG_NAMES}
-        q.put((rank, out, logs, None))
-    except Exception:  # report, do not hang the parent
-        import traceback
-        q.put((rank, None, None, traceback.format_exc()))
-    dist.barrier()
-    dist.destroy_process_group()
+def _mogan_worker(rank, world):
+    import gbvst
+    from gbvst import dp, ops
+    gbvst._lib.load()
+    torch.cuda.set_device(0)
+    ops.set_deterministic(True)
+    m = _mogan_setup(slice(rank * 2, rank * 2 + 2))
+    nets = [getattr(m, "net" + n) for n in _MG_NAMES]
+    ex = dp.GradExchange(world, bucket_bytes=64 << 10).attach(nets)
+    out = _mogan_run(m, ex)
+    logs = {n: list(ex._state(getattr(m, "net" + n)).last_log) for n in _MG_NAMES}
+    return out, logs
 
 
 @pytest.mark.timeout(600)
 def test_mogan_dp_world2_three_phases_equal_single_process():
     world = 2
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_mogan_worker, args=(r, world, port, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    res = sorted([q.get(timeout=500) for _ in range(world)], key=lambda r: r[0])
-    for p in procs:
-        p.join(timeout=120)
-    for r in res:
-        assert r[3] is None, r[3]
-    for p in procs:
-        assert p.exitcode == 0
+    res = [(r, out, logs) for r, (out, logs) in enumerate(run_ranks(_mogan_worker, world, timeout=500))]
     import gbvst
     from gbvst import ops
     gbvst._lib.load()

@@ -89,11 +89,8 @@ SIGNATURES = {
     "vst_tapfold_planes": (I, [P, P, L, I, I, I, I, I, I, I, P]),
     "vst_conv2d_fwd_ws_bytes": (SZ, [I, I, I, I, I, I, I, I, I, I]),
     "vst_conv2d_fwd_ws": (I, [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, I, P, P, P, SZ, P]),
-    "vst_conv2d_fwd_nrm_ok": (I, [I, I, I, I, I, I, I, I, I, I, I]),
     "vst_c4_dgrad_frame": (I, [P, P, P, I, I, I, I, I, I, P]),
-    "vst_conv2d_fwd_nrm_ws": (I, [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, I, P, P, P, SZ, P]),
     "vst_conv_plan_fwd_tail": (I, [I, I, I, I, I, I, I, I, I, I, P]),
-    "vst_reflect_fold_instnorm_bwd": (I, [P, P, P, P, P, P, P, P, I, I, I, I, I, I, F, I, P, L, P]),
     "vst_act_bwd": (I, [P, P, P, L, I, F, P]),
     "vst_warp_fwd": (I, [P, P, P, I, I, I, I, I, P]),
     "vst_warp_bwd_input": (I, [P, P, P, I, I, I, I, I, P]),
@@ -173,18 +170,11 @@ SIGNATURES = {
     "vst_u8_image_to_nhwc4": (I, [P, P, L, P]),
     "vst_conv2d_dgrad_refl_ws_bytes": (SZ, [I, I, I, I, I, I]),
     "vst_conv2d_dgrad_refl": (I, [P, P, P, P, P, SZ, I, I, I, I, I, I, P]),
-    "vst_conv2d_dgrad_refl_in_ws_bytes": (SZ, [I, I, I, I, I, I]),
-    "vst_conv2d_dgrad_refl_in": (I, [P, P, P, P, P, P, P, P, P, SZ, I, I, I, I, I, I, F, I, P, L, I, P]),
     "vst_conv2d_dgrad_refl_in_epi_ws_bytes": (SZ, [I, I, I, I, I, I]),
     "vst_conv2d_dgrad_refl_in_epi": (I, [P, P, P, P, P, P, P, P, P, SZ, I, I, I, I, I, I, F, I, P, L, I, P]),
     "vst_conv2d_dgrad_refl_epi_part": (I, [P, P, P, P, P, P, P, P, SZ, I, I, I, I, I, I, F, I, P]),
     "vst_instnorm_act_bwd_epi_tail": (I, [P, P, P, P, P, P, I, I, I, I, I, F, I, P, L, P, P]),
-    "vst_conv2d_fwd_apre_ws": (I, [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, I, P, P, P, SZ, P]),
-    "vst_instnorm_act_fwd_cp_apre": (I, [P, P, P, P, P, P, I, I, I, I, I, F, I, I, I, P]),
-    "vst_instnorm_act_fwd_apre": (I, [P, P, P, P, P, I, I, I, I, F, P]),
     "vst_instnorm_act_bwd_planes_apre": (I, [P, P, P, P, P, P, I, I, I, I, F, I, P, L, P, P]),
-    "vst_conv2d_dgrad_refl_slabs": (I, [P, P, P, P, P, SZ, I, I, I, I, I, I, P]),
-    "vst_instnorm_act_bwd_refl_border": (I, [P, P, P, P, P, P, P, I, I, I, I, I, I, F, I, P, L, I, P]),
     # SURVEY §8b spelling (abi.hip)
     "vst_conv_desc_out_hw": (I, [P, P, P]),
     "vst_workspace_size": (SZ, [P, I]),

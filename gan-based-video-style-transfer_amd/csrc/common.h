@@ -150,9 +150,7 @@ int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* b
                     int H, int W, int C, int Ho, int Wo, int Cop, int R, int S, int st, int padh, int padw,
                     int reflect, int act, float slope, int math, int kind, hipStream_t s,
                     double* part = nullptr, float* tws = nullptr, size_t tws_floats = 0, const float* addend = nullptr,
-                    int oph = 0, const float* nst = nullptr);
-// can the forward over relu(IN(x)) (nst = x's statistics) normalise in its A staging for this shape?
-bool bf_fprop_nrm_ok(int N, int H, int W, int C, int Cop, int R, int S, int st, int pad, int reflect, int math);
+                    int oph = 0);
 // direct patch-staged 4-channel-input convs (conv_c4.hip)
 // the 64 -> 4-output 7 x 7 tap conv as one direct kernel (conv_tap64.hip)
 bool tap64_ok(int Cx, int R, int W, int math);
@@ -177,13 +175,6 @@ int bf_dgrad_refl1_inb_launch(const float* dy, const void* wsplit, long wps, con
                               int H, int W, int Cy, int Cx, int math, hipStream_t s, float* ws, size_t ws_floats,
                               const float* z, const float* st, double* part, int act, float slope,
                               const __bf16* apl = nullptr, long pps = 0);
-// The A operand of the x6 forwards as pre-split bf16 planes (NHWC, plane stride pps elements), for the next
-// bf_fprop_launch on this host thread (set and cleared around one call by vst_conv2d_fwd_apre_ws)
-struct ApreArgs {
-  const __bf16* apl;
-  long pps;
-};
-extern thread_local ApreArgs g_apre;
 size_t bf_fprop_ws_floats(long M, int Cop, int C, int R, int S, int math);
 int bf_tail_ks(long M, int Cop, int m_split, int nk);
 void bf_split_plan(long M, int Cop, int C, int R, int S, int math, int kind, int* m_first, int* ks_out);
@@ -207,7 +198,7 @@ void rk_tconv_launch(const float* in, const float* wp, const float* bias, const 
                      float* out, int N, int Hi, int Wi, int Cy, int Ho, int Wo, int Cx, int R, int S,
                      int st, int pad, int reflect, int act, float slope, int kind, int math,
                      hipStream_t s);
-// VST_HEAD=0 turns the head kernels below off (skinny.hip)
+// g_head = false turns the head kernels below off (skinny.hip; a constant: developer A/Bs recompile)
 extern const bool g_head;
 // the PatchGAN head (one real output channel, stride 1, zero pad, <= 4x4 taps): patch.hip
 bool head_ok(int Cin, int R, int S, int st, int reflect, int Wo);

@@ -754,18 +754,7 @@ static int pick_splits(int tiles, int slots, int max_ns, int min_ns = 1) {
 #define VST_WG_BF 1   // x6 weight gradients on the split-bf16 kernel (conv_wgrad_bf_k)
 #endif
 
-// x6 weight gradients of at most 256 (tap, ci) rows and 64 channels (the image-input layer's, M = 147, and the
-// last layer's swapped GEMM) on ONE 256x64 tile per split (kind 10: the dy / x planes read once per split instead of
-// once per 64-row tile); VST_WG_K256=1 (developer A/B)
-static const bool g_wg_k256 = [] {
-  const char* e = getenv("VST_WG_K256");
-  return e && e[0] == '1';
-}();
-
-static const int g_wg_kind_s2 = [] {
-  const char* e = getenv("VST_WG_KIND_S2");
-  return e ? atoi(e) : -1;
-}();
+static constexpr int g_wg_kind_s2 = -1;
 
 static WgradPlan plan_wgrad(int N, int H, int W, int Ho, int Wo, int Cx, int Cyp, int R, int S,
                             int stride, int math) {
@@ -796,8 +785,7 @@ static WgradPlan plan_wgrad(int N, int H, int W, int Ho, int Wo, int Cx, int Cyp
     // 576 rows = 2.25 x 256, 1152 = 4.5 x 256) run on 128x128 tiles of 8 waves (64x32); round-5 sweep
     // (profiles/r05e_convT_wgrad_tiles.jsonl): 178 -> 172 / 149 -> 136 us at N = 8
     if (kind == 7 && ceil_div(p.Mw, 256) * 256 > ceil_div(p.Mw, 128) * 128) kind = 0;
-    if (g_wg_kind_s2 >= 0 && stride == 2) kind = g_wg_kind_s2;  // developer A/B (VST_WG_KIND_S2)
-    if (kind == 8 && g_wg_k256 && p.Mw <= 256) kind = 10;
+    if (g_wg_kind_s2 >= 0 && stride == 2) kind = g_wg_kind_s2;  // developer A/B (g_wg_kind_s2)
     p.tile = (TileKind)kind;
     int bm, bn, bk, slots;
     bf_wgrad_geom(kind, math, &bm, &bn, &bk, &slots);
@@ -861,18 +849,12 @@ static WgradPlan plan_wgrad(int N, int H, int W, int Ho, int Wo, int Cx, int Cyp
 using namespace vst;
 
 // 4-channel inputs (images) on the split-bf16 kernels (conv_fprop_bf_k<.., false, 3>) rather than
-// the fp32 [row][k] kernels; VST_BF_C4=0 restores the latter.
-// wgrad_reduce_store_k on 16-row blocks (VST_WG_RED16=0: 32-row): twice the blocks for the same slabs,
+// the fp32 [row][k] kernels; g_bf_c4 = false restores the latter (route selectors like this are compile-time constants).
+// wgrad_reduce_store_k on 16-row blocks (g_wg_red16 = false: 32-row): twice the blocks for the same slabs,
 // -0.16 ms/step in the same-box A/B (profiles/r03d_wgred_step_ab.jsonl)
-static const bool g_wg_red16 = [] {
-  const char* e = getenv("VST_WG_RED16");
-  return !(e && e[0] == '0');
-}();
+static constexpr bool g_wg_red16 = true;
 
-static const bool g_bf_c4 = [] {
-  const char* e = getenv("VST_BF_C4");
-  return !(e && e[0] == '0');
-}();
+static constexpr bool g_bf_c4 = true;
 
 extern "C" void vst_debug_set_tiles(int fprop, int tconv, int wgrad) {
   g_tile_override[0] = fprop;
@@ -994,51 +976,6 @@ extern "C" int vst_conv2d_fwd_ws(const float* x, const float* wp, const void* ws
                                  size_t ws_bytes, void* stream) {
   return conv_fwd_impl(x, wp, wsplit, bias, y, N, H, W, Cx, Cop, R, S, stride, pad, pad, pad_mode, act, slope,
                        math, (hipStream_t)stream, part, nsplit, ws, ws_bytes);
-}
-
-// vst_conv2d_fwd_ws with x's pre-split A planes apl [3][N*H*W*Cx] bf16 (NHWC, the RNE split of each value: written
-// by the producing IN pass, vst_instnorm_act_fwd_cp_apre / vst_instnorm_act_bwd_planes_apre): the x6 256x128 channel-
-// slice plans stage A from them by LDS-DMA (no fp32 A image, no split in the staging), results bit-identical; other
-// plans read x.
-extern "C" int vst_conv2d_fwd_apre_ws(const float* x, const void* apl, const float* wp, const void* wsplit,
-                                      const float* bias, float* y, int N, int H, int W, int Cx, int Cop, int R, int S,
-                                      int stride, int pad, int pad_mode, int act, float slope, int math, double* part,
-                                      int* nsplit, float* ws, size_t ws_bytes, void* stream) {
-  g_apre = ApreArgs{reinterpret_cast<const __bf16*>(apl), (long)N * H * W * Cx};
-  const int rc = conv_fwd_impl(x, wp, wsplit, bias, y, N, H, W, Cx, Cop, R, S, stride, pad, pad, pad_mode, act, slope,
-                               math, (hipStream_t)stream, part, nsplit, ws, ws_bytes);
-  g_apre = ApreArgs{nullptr, 0};
-  return rc;
-}
-
-// A forward conv over relu(IN(x)): x = the raw output of the previous conv, nst = its InstanceNorm
-// statistics [N][Cx][2] (mean, rstd; vst_instnorm_finalize / _stats), normalised in the A staging
-// (conv_fprop_bf_nrm_k) — no normalised activation is written.  vst_conv2d_fwd_nrm_ok says whether a
-// shape takes it (x6, Cx % 32 == 0, reflect padding, stride 1, Ho*Wo % 256 == 0, a 256x128 or split-K
-// plan); the workspace is vst_conv2d_fwd_ws_bytes's.
-extern "C" int vst_conv2d_fwd_nrm_ok(int N, int H, int W, int Cx, int Cop, int R, int S, int stride, int pad,
-                                     int pad_mode, int math) {
-  return bf_fprop_nrm_ok(N, H, W, Cx, Cop, R, S, stride, pad, pad_mode == VST_PAD_REFLECT, math) &&
-         g_tile_override[0] < 0;
-}
-
-extern "C" int vst_conv2d_fwd_nrm_ws(const float* x, const float* nst, const void* wsplit, const float* bias, float* y,
-                                     int N, int H, int W, int Cx, int Cop, int R, int S, int stride, int pad,
-                                     int pad_mode, int act, float slope, int math, double* part, int* nsplit, float* ws,
-                                     size_t ws_bytes, void* stream) {
-  if (nsplit) *nsplit = 0;
-  VST_REQUIRE(x && nst && wsplit && y, "conv2d_fwd_nrm: null pointer");
-  VST_REQUIRE(vst_conv2d_fwd_nrm_ok(N, H, W, Cx, Cop, R, S, stride, pad, pad_mode, math),
-              "conv2d_fwd_nrm: unsupported shape / arithmetic (vst_conv2d_fwd_nrm_ok)");
-  VST_REQUIRE(ws_bytes >= vst_conv2d_fwd_ws_bytes(N, H, W, Cx, Cop, R, S, stride, pad, math),
-              "conv2d_fwd_nrm: workspace too small");
-  const int Ho = H + 2 * pad - R + 1, Wo = W + 2 * pad - S + 1;
-  const bool stats = part && nsplit;
-  const int rc = bf_fprop_launch(x, wsplit, (long)Cop * R * S * Cx, bias, y, N, H, W, Cx, Ho, Wo, Cop, R, S, 1, pad,
-                                 pad, 1, act, slope, math, -1, (hipStream_t)stream, stats ? part : nullptr, ws,
-                                 ws_bytes / sizeof(float), nullptr, 0, nst);
-  if (stats && rc == 0) *nsplit = Ho * Wo / 32;
-  return rc;
 }
 
 extern "C" int vst_conv_plan_fwd_tail(int N, int H, int W, int Cx, int Cop, int R, int S, int stride, int pad,
@@ -1185,11 +1122,8 @@ extern "C" int vst_conv2d_tfwd_co(const float* in, const float* wp, const float*
 static constexpr int WG_GROUP = 16;
 // Image-input layers (x NHWC4 holding 3 logical channels) on the split-bf16 kernel: the GEMM takes only
 // the rows (tap, ci < 3) of the 4-plane x image — M = 3RS instead of 4RS (the generator's first 7x7
-// conv: 147 rows = 3 tiles of 64 instead of 4).  VST_WG_C3=0: all four planes.
-static const bool g_wg_c3 = [] {
-  const char* e = getenv("VST_WG_C3");
-  return !(e && e[0] == '0');
-}();
+// conv: 147 rows = 3 tiles of 64 instead of 4).  g_wg_c3 = false: all four planes.
+static constexpr bool g_wg_c3 = true;
 
 // The GEMM's plan for (Cx, logical Ci): p planned with Cx = 3 when the rule above applies; its
 // operand-copy sizes stay those of the Cx-channel images.

@@ -253,9 +253,6 @@ __device__ __forceinline__ void mma_frag(const Frag<T>& f, f32x16 (&acc)[T::MI][
 #define VST_BF_GLDS_B 1  // x6 M16 KSL forwards: the pre-split B operand LDS-DMA'd (global_load_lds_dwordx4)
                          // instead of register-staged
 #endif
-#ifndef VST_BF_GLDS_W
-#define VST_BF_GLDS_W 0  // the same for the x6 weight gradient's dy planes (measured slower in the step: off)
-#endif
 template <class T>
 __device__ __forceinline__ void store_stage(char* st, const float4 (&ra)[T::A_LD][2],
                                             const u32x4_t (&rbv)[T::B_LD][T::NP], int rb, int kq,
@@ -844,22 +841,14 @@ __device__ __attribute__((aligned(256))) float g_zero_page[64];
 // [z * spk, z * spk + spk) and stores its raw partial tile to slab[z][m - m_base][Cop]
 // (fprop_splitk_reduce_k sums the splits in order and applies bias / act / IN partials).
 // (body of conv_fprop_bf_k and conv_convT_phases_k; bid = the block's index in its tile grid)
-// NRM (KSL, REFL 1 only): x is the raw output of the previous conv and every gathered A value enters as
-// relu((v - mean) * rstd) with the InstanceNorm statistics nst [N][C][2] (mean, rstd) — the IN + ReLU
-// apply of in_apply_k (same expression, same rounding) done in the A staging instead of a pass that
-// writes the normalised activation.  Reflect padding only (a zero-padding tap must stay zero), and
-// every tile's rows in one image (Ho*Wo a multiple of BM): the 8 channels' statistics of a K-step are
-// four float4 loads beside the A gathers.
-template <class T, bool KSL, int REFL, bool SPLIT, bool NRM = false, bool APRE = false>
+template <class T, bool KSL, int REFL, bool SPLIT, bool APRE = false>
 __device__ __forceinline__ void conv_fprop_bf_body(
     int bid, const float* __restrict__ x, const __bf16* __restrict__ ws, long wps, const float* __restrict__ bias,
     float* __restrict__ y, int H, int W, int C, int Ho, int Wo, int Cop, int S, int st, int padh,
     int padw, int reflect, int act, float slope, int M, int Ktot, int m_base, double* __restrict__ part,
     int spk, float* __restrict__ slab, const float* __restrict__ addend, int oph,
-    const float* __restrict__ nst = nullptr, const float* __restrict__ bslab = nullptr, int bks = 0, int bmb = 0,
-    int blt = 0, int bll = 0, InbArgs inb = InbArgs{}, const __bf16* __restrict__ apl = nullptr, long pps = 0) {
+    InbArgs inb = InbArgs{}, const __bf16* __restrict__ apl = nullptr, long pps = 0) {
   static_assert(!SPLIT || KSL, "split-K needs the channel-slice-major K walk");
-  static_assert(!NRM || (KSL && REFL == 1), "normalised A: the channel-slice K walk, reflect padding");
   static_assert(REFL < 4 || (SPLIT && KSL), "border rows run as split-K slabs");
   __shared__ __attribute__((aligned(16))) char smem[2 * T::STAGE];
   constexpr int A_LD = T::A_LD, B_LD = T::B_LD, RPP = T::RPP, NP = T::NP;
@@ -974,23 +963,16 @@ __device__ __forceinline__ void conv_fprop_bf_body(
   // APRE: the A operand arrives pre-split (apl: three bf16 planes of x's NHWC layout, plane stride pps
   // elements) by LDS-DMA like B — no fp32 A image, no split in the staging.  VST_BF_FAKE_ADMA (developer timing
   // only, WRONG results): every GLDS kernel DMAs A from x's own bytes read as planes.
-  constexpr bool GLDS_A = (APRE || VST_BF_FAKE_ADMA) && GLDS && !NRM;
+  constexpr bool GLDS_A = (APRE || VST_BF_FAKE_ADMA) && GLDS;
   // APRE without the DMA (the K-restricted border GEMM, REFL 5): A's planes loaded into registers and put back
   // together as fp32 (hi + mid + lo is the value exactly), then staged as usual — the same planes in LDS
   constexpr bool APRE_REG = APRE && !GLDS_A;
   static_assert(!APRE || GLDS_A || REFL == 5, "pre-split A: the x6 M16 channel-slice kernels with LDS-DMA B, or REFL 5");
   const __bf16* apl_ = VST_BF_FAKE_ADMA ? reinterpret_cast<const __bf16*>(x) : apl;
   const long pps_ = VST_BF_FAKE_ADMA ? (long)(M / (Ho * Wo)) * H * W * C / 2 : pps;
-  float4 nr[2][NRM ? 4 : 1];  // NRM: (mean, rstd) of the stage's 8 channels, per register set
-  const float* nimg = NRM ? nst + (long)(m0 / (Ho * Wo)) * C * 2 : nullptr;
   auto load_all = [&](int set) __attribute__((always_inline)) {
     const bool kin = KSL || kcur < Ktot;  // the K tail reads zeros (A) against row 0 (B)
     const int ka = KSL ? ksb + kq8 : kc;
-    if constexpr (NRM) {
-      const float4* q = reinterpret_cast<const float4*>(nimg + ka * 2);
-#pragma unroll
-      for (int u = 0; u < 4; ++u) nr[set][u] = q[u];
-    }
     // REFL 5: tap (2, ts) top, (0, ts) bottom, (tr, 2) left, (tr, 0) right of the 3x3 weight rows
     const int tap5 = seg == 0 ? 6 + ts : (seg == 1 ? ts : 3 * tr + (seg == 2 ? 2 : 0));
     const int kb = KSL ? (REFL == 5 ? tap5 : tr * S + ts) * C + ksb + kq8 : (kin ? kcur : 0);
@@ -1121,22 +1103,8 @@ __device__ __forceinline__ void conv_fprop_bf_body(
     }
   };
 
-  // NRM: the IN + ReLU apply on register set `set` before its split (a no-op otherwise)
-  auto prep = [&](int set) __attribute__((always_inline)) {
-    if constexpr (NRM) {
-#pragma unroll
-      for (int j = 0; j < A_LD; ++j)
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          float4& v = ra[set][j][h];
-          const float4 s0 = nr[set][2 * h], s1 = nr[set][2 * h + 1];  // {m0, r0, m1, r1}, {m2, r2, m3, r3}
-          v.x = apply_act((v.x - s0.x) * s0.y, VST_ACT_RELU, 0.f);
-          v.y = apply_act((v.y - s0.z) * s0.w, VST_ACT_RELU, 0.f);
-          v.z = apply_act((v.z - s1.x) * s1.y, VST_ACT_RELU, 0.f);
-          v.w = apply_act((v.w - s1.z) * s1.w, VST_ACT_RELU, 0.f);
-        }
-    }
-  };
+  // the main loops' per-register-set hook before the split (unused by the forward)
+  auto prep = [](int) __attribute__((always_inline)) {};
   const int wm0 = (wave / T::WAVES_N) * T::WM, wn0 = (wave % T::WAVES_N) * T::WN;
   if constexpr (T::M16) {
     f32x4v acc[T::MI16][T::NI16];
@@ -1168,7 +1136,7 @@ __device__ __forceinline__ void conv_fprop_bf_body(
     // (an addend — the residual gradient of a data gradient — is always added on this path: its float4
     // loads ride with the row stores instead of 4-byte reads per accumulator element)
     constexpr bool LFIT = T::BM * (T::BN + 16) * 4 <= 2 * T::STAGE;
-    const bool LEPI = LFIT && (VST_BF_LDS_EPI || addend != nullptr || oph != 0 || bslab != nullptr || inb.part != nullptr);
+    const bool LEPI = LFIT && (VST_BF_LDS_EPI || addend != nullptr || oph != 0 || inb.part != nullptr);
     constexpr int LDE = T::BN + 16;
     float* ept = reinterpret_cast<float*>(smem);
     // InbArgs: the IN input z (and the addend) of the wave's 32-row group (wave w: rows 32 w .., one group per
@@ -1294,22 +1262,6 @@ __device__ __forceinline__ void conv_fprop_bf_body(
         if (mm < M && n < Cop && orow >= 0) {
           float4 v = *reinterpret_cast<const float4*>(ept + row * LDE + c);
           if (addend) add_f4(v, *reinterpret_cast<const float4*>(addend + (long)mm * Cop + n));
-          if (bslab) {  // the reflect-pad-1 data gradient's border slabs (dgrad_border5_add_k's sums, same order)
-            const int hw = Ho * Wo, img = mm / hw, rem = mm - img * hw, h = rem / Wo, w = rem - h * Wo;
-            if (h == 1 || h == Ho - 2 || w == 1 || w == Wo - 2) {
-              int rows[3];
-              const int nr = dgrad_border_slab_rows(img, h, w, Ho, Wo, blt, bll, rows);
-              const long zst = (long)bmb * Cop;
-              float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
-              for (int r = 0; r < nr; ++r) {
-                const float* base = bslab + (long)rows[r] * Cop + n;
-                float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-                for (int z = 0; z < bks; ++z) add_f4(acc, *reinterpret_cast<const float4*>(base + z * zst));
-                add_f4(bv, acc);
-              }
-              add_f4(v, bv);
-            }
-          }
           *reinterpret_cast<float4*>(y + (long)orow * Cop + n) = v;
         }
       }
@@ -1378,22 +1330,9 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_k(
     int padw, int reflect, int act, float slope, int M, int Ktot, int m_base, double* __restrict__ part,
     int spk = 0, float* __restrict__ slab = nullptr, const float* __restrict__ addend = nullptr, int oph = 0,
     const __bf16* __restrict__ apl = nullptr, long pps = 0) {
-  conv_fprop_bf_body<T, KSL, REFL, SPLIT, false, APRE>(blockIdx.x, x, ws, wps, bias, y, H, W, C, Ho, Wo, Cop, S, st,
-                                                       padh, padw, reflect, act, slope, M, Ktot, m_base, part, spk,
-                                                       slab, addend, oph, nullptr, nullptr, 0, 0, 0, 0, InbArgs{}, apl,
-                                                       pps);
-}
-
-// The interior conv of the reflect-pad-1 data gradient with the border GEMM's slabs (written before it)
-// added in its LDS-staged epilogue (the addend path): dgrad_border5_add_k's work without its launch.
-template <class T>
-__global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_bord_k(
-    const float* __restrict__ x, const __bf16* __restrict__ ws, long wps, float* __restrict__ y, int H, int W, int C,
-    int Cop, const float* __restrict__ addend, int M, int Ktot, const float* __restrict__ bslab, int bks, int bmb,
-    int blt, int bll) {
-  conv_fprop_bf_body<T, true, 0, false>(blockIdx.x, x, ws, wps, nullptr, y, H, W, C, H, W, Cop, 3, 1, 1, 1, 0,
-                                        VST_ACT_NONE, 0.f, M, Ktot, 0, nullptr, 0, nullptr, addend, 0, nullptr, bslab,
-                                        bks, bmb, blt, bll);
+  conv_fprop_bf_body<T, KSL, REFL, SPLIT, APRE>(blockIdx.x, x, ws, wps, bias, y, H, W, C, Ho, Wo, Cop, S, st, padh,
+                                                padw, reflect, act, slope, M, Ktot, m_base, part, spk, slab, addend, oph,
+                                                InbArgs{}, apl, pps);
 }
 
 // The interior conv of the reflect-pad-1 data gradient (+ addend) with the IN-backward partials of the
@@ -1403,20 +1342,8 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_inb_k(
     const float* __restrict__ x, const __bf16* __restrict__ ws, long wps, float* __restrict__ y, int H, int W, int C,
     int Cop, const float* __restrict__ addend, int M, int Ktot, InbArgs inb, const __bf16* __restrict__ apl = nullptr,
     long pps = 0) {
-  conv_fprop_bf_body<T, true, 0, false, false, APRE>(blockIdx.x, x, ws, wps, nullptr, y, H, W, C, H, W, Cop, 3, 1, 1,
-                                                     1, 0, VST_ACT_NONE, 0.f, M, Ktot, 0, nullptr, 0, nullptr, addend, 0,
-                                                     nullptr, nullptr, 0, 0, 0, 0, inb, apl, pps);
-}
-
-// conv_fprop_bf_k over relu(IN(x)) (NRM: the normalisation in the A staging; nst = x's IN statistics)
-template <class T, bool SPLIT>
-__global__ __launch_bounds__(T::NT, T::MINB) void conv_fprop_bf_nrm_k(
-    const float* __restrict__ x, const __bf16* __restrict__ ws, long wps, const float* __restrict__ bias,
-    float* __restrict__ y, int H, int W, int C, int Ho, int Wo, int Cop, int S, int st, int padh,
-    int padw, int act, float slope, int M, int Ktot, int m_base, double* __restrict__ part,
-    int spk, float* __restrict__ slab, const float* __restrict__ nst) {
-  conv_fprop_bf_body<T, true, 1, SPLIT, true>(blockIdx.x, x, ws, wps, bias, y, H, W, C, Ho, Wo, Cop, S, st, padh, padw,
-                                              1, act, slope, M, Ktot, m_base, part, spk, slab, nullptr, 0, nst);
+  conv_fprop_bf_body<T, true, 0, false, APRE>(blockIdx.x, x, ws, wps, nullptr, y, H, W, C, H, W, Cop, 3, 1, 1, 1, 0,
+                                              VST_ACT_NONE, 0.f, M, Ktot, 0, nullptr, 0, nullptr, addend, 0, inb, apl, pps);
 }
 
 // All four phases of a stride-2 ConvTranspose2d(k3, p1, op1) forward in ONE launch, each stored
@@ -1522,7 +1449,6 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_wgrad_bf_k(
   }
   float4 ra[2][A_LD][2];
   u32x4_t rbv[2][B_LD][NP];
-  constexpr bool GLDS = VST_BF_GLDS_W && T::M16;
   auto load_all = [&](int set) __attribute__((always_inline)) {
     const bool live = kp < pend;  // 8-pixel chunks never straddle pend (chunk, P multiples of 8)
 #pragma unroll
@@ -1533,34 +1459,12 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_wgrad_bf_k(
       ra[set][j][0] = make_float4(u0.x, u0.y, u0.z, u0.w);
       ra[set][j][1] = make_float4(u1.x, u1.y, u1.z, u1.w);
     }
-    if constexpr (GLDS) return;  // B arrives by LDS-DMA (dma_b)
 #pragma unroll
     for (int j = 0; j < B_LD; ++j) {
       const __bf16* q = live ? drow[j] + kp : zpb;
       const long ps = live ? dps : 0;
 #pragma unroll
       for (int p = 0; p < NP; ++p) rbv[set][j][p] = *reinterpret_cast<const u32x4_t*>(q + p * ps);
-    }
-  };
-  // VST_BF_GLDS_B: the dy planes' stage image by LDS-DMA (as conv_fprop_bf_body's dma_b: lane l fills
-  // row 16 w + l / 4, slot l % 4 from source chunk (l % 4) ^ swz(row); the cursor kp is on that stage)
-  auto dma_b = [&](char* stg) __attribute__((always_inline)) {
-#pragma unroll
-    for (int j = 0; j < B_LD; ++j) {
-      const int row = rb + RPP * j;
-      const int csrc = (t % T::KC) ^ T::swz(row);
-      const int wrow0 = __builtin_amdgcn_readfirstlane(row - (lane / T::KC));
-      const int kpc = kp - 8 * kq + 8 * csrc;
-      const bool lv = kpc < pend;
-      const __bf16* q = lv ? drow[j] + kpc : zpb;
-      const long ps = lv ? dps : 0;
-#pragma unroll
-      for (int p = 0; p < NP; ++p) {
-#if defined(__HIP_DEVICE_COMPILE__)
-        __builtin_amdgcn_global_load_lds(q + p * ps, (lds_void*)(stg + T::A_BYTES + p * T::B_PLANE + wrow0 * T::ROWB),
-                                         16, 0, 0);
-#endif
-      }
     }
   };
   const long row_step = (long)st * Wp - Wo, img_step = (long)(Hp - st * Ho) * Wp;
@@ -1593,10 +1497,7 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_wgrad_bf_k(
   if constexpr (T::M16) {
     f32x4v acc[T::MI16][T::NI16];
     zero_acc4(acc);
-    if constexpr (GLDS)
-      main_loop16<T>(smem, nk, acc, ra, rbv, rb, kq, load_all, adv, [](int) {}, DmaB<decltype(dma_b)>{dma_b});
-    else
-      main_loop16<T>(smem, nk, acc, ra, rbv, rb, kq, load_all, adv, [](int) {}, NoDma{});
+    main_loop16<T>(smem, nk, acc, ra, rbv, rb, kq, load_all, adv, [](int) {}, NoDma{});
 #pragma unroll
     for (int i = 0; i < T::MI16; ++i)
 #pragma unroll
@@ -2008,41 +1909,10 @@ size_t bf_fprop_ws_floats(long M, int Cop, int C, int R, int S, int math) {
   return ks ? (size_t)ks * (M - mf) * Cop : 0;
 }
 
-// The NRM route (conv_fprop_bf_nrm_k): x6, channel-slice K walk, reflect padding, and a plan of whole
-// 256x128 rounds or the all-split-K form (the kernels it instantiates), every tile in one image.
-bool bf_fprop_nrm_ok(int N, int H, int W, int C, int Cop, int R, int S, int st, int pad, int reflect, int math) {
-  if (math != VST_MATH_BF16X6 || !VST_BF_KSLICE || C % 32 || !reflect || st != 1 || R != S || Cop % 4) return false;
-  const int Ho = H + 2 * pad - R + 1, Wo = W + 2 * pad - S + 1;
-  if (Ho <= 0 || Wo <= 0 || ((long)Ho * Wo) % 256) return false;
-  const long M = (long)N * Ho * Wo;
-  int kd, m_split, tail_kind, m_first, ks;
-  bf_plan(M, Cop, math, -1, &kd, &m_split, &tail_kind);
-  bf_split_plan(M, Cop, C, R, S, math, -1, &m_first, &ks);
-  return (kd == 7 && (!m_split || ks)) || (ks && !m_first);
-}
-
-// The A operand's pre-split planes for the next bf_fprop_launch on this host thread (vst_conv2d_fwd_apre_ws sets
-// them around its call): taken by the x6 256x128 channel-slice launches (whole rounds and the split-K form),
-// ignored by every other plan (x itself stays valid).
-thread_local ApreArgs g_apre = {nullptr, 0};
-
-static const int g_fs_tile = [] {  // developer A/B of the all-split-K tile (bf_fprop_launch)
-  const char* e = getenv("VST_FULLSPLIT_TILE");
-  return e ? atoi(e) : 0;
-}();
-
 int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* bias, float* y, int N,
                     int H, int W, int C, int Ho, int Wo, int Cop, int R, int S, int st, int padh, int padw,
                     int reflect, int act, float slope, int math, int kind, hipStream_t s, double* part,
-                    float* tws, size_t tws_floats, const float* addend, int oph, const float* nst) {
-  if (nst) {
-    VST_REQUIRE(kind < 0 && !addend && !oph && padh == padw &&
-                    bf_fprop_nrm_ok(N, H, W, C, Cop, R, S, st, padh, reflect, math),
-                "conv fprop over relu(IN(x)): needs x6, C %% 32 == 0, reflect, stride 1, Ho*Wo %% 256 == 0 and a "
-                "256x128 / split-K plan (bf_fprop_nrm_ok)");
-    VST_REQUIRE(tws || (size_t)0 == bf_fprop_ws_floats((long)N * Ho * Wo, Cop, C, R, S, math),
-                "conv fprop over relu(IN(x)): this shape's plan needs the split-K workspace");
-  }
+                    float* tws, size_t tws_floats, const float* addend, int oph) {
   if (oph) tws = nullptr;  // phase stores: no split-K slabs (their reduce stores unmapped)
   // the epilogue routes differ on whether an addend enters the IN partials (the per-element store
   // counts it, the LDS-staged one adds it at the row store): no caller needs both, so refuse it
@@ -2052,8 +1922,6 @@ int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* b
   if (kind < 0 && padh == padw && !addend && !oph && c4_direct_ok(C, Cop, R, S, st, Ho, Wo, math))
     return c4_direct_launch(x, wsplit, wps, bias, y, N, H, W, Ho, Wo, R, S, padh, reflect, act, slope, math, part, s);
   const __bf16* ws = reinterpret_cast<const __bf16*>(wsplit);
-  const __bf16* apl = (!nst && !oph && VST_BF_KSLICE && C % 32 == 0 && math == VST_MATH_BF16X6) ? g_apre.apl : nullptr;
-  const long pps = g_apre.pps;
   int kd, m_split, tail_kind;
   bf_plan(M, Cop, math, kind, &kd, &m_split, &tail_kind);
   int ks = 0, m_first = 0;
@@ -2089,43 +1957,11 @@ int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* b
   for (int ph = (ks && !m_first) ? 1 : 0; ph < ((m_split || (ks && !m_first)) ? 2 : 1); ++ph) {
     const int mb = ph ? m_split : 0, Mend = (m_split && !ph) ? m_split : M;
     const int kp = ph ? tail_kind : kd;
-    if (ph == 1 && ks && !m_first && !nst && g_fs_tile == 128) {
-      // developer A/B (VST_FULLSPLIT_TILE=128): the all-split-K form on 128x128 tiles (4 waves of 64x64),
-      // as many K-splits as fill the CUs within the 256x128 plan's slab workspace
-      using T = bf::Tile<128, 128, 64, 64, 32, 3>;
-      const long tiles = ceil_div(M, 128) * ceil_div(Cop, 128);
-      const int nk = (K + T::BK - 1) / T::BK;
-      int ks2 = (int)(VST_NUM_CUS / tiles);
-      ks2 = ks2 < 1 ? 1 : (ks2 > 32 ? 32 : ks2);
-      while (ks2 > 1 && ((size_t)ks2 * M * Cop > tws_floats || (ks2 - 1) * ((nk + ks2 - 1) / ks2) >= nk)) --ks2;
-      const int spk = (nk + ks2 - 1) / ks2;
-      const dim3 grid(tiles * ks2);
-      if (reflect)
-        hipLaunchKernelGGL((bf::conv_fprop_bf_k<T, true, 1, true>), grid, dim3(T::NT), 0, s, x, ws, wps, bias, y, H, W,
-                           C, Ho, Wo, Cop, S, st, padh, padw, reflect, act, slope, M, K, 0, part, spk, tws, nullptr);
-      else
-        hipLaunchKernelGGL((bf::conv_fprop_bf_k<T, true, 0, true>), grid, dim3(T::NT), 0, s, x, ws, wps, bias, y, H, W,
-                           C, Ho, Wo, Cop, S, st, padh, padw, reflect, act, slope, M, K, 0, part, spk, tws, nullptr);
-      hipLaunchKernelGGL(bf::fprop_splitk_reduce_k, dim3(ceil_div(M, 32), ceil_div(Cop, 64)), dim3(256), 0, s, tws, ks2,
-                         0, M, Cop, bias, act, slope, y, part, Ho * Wo, addend);
-      continue;
-    }
     if (ph == 1 && ks) {
       using T = bf::Tile<256, 128, 64, 64, 32, 3>;
       const int nk = (K + T::BK - 1) / T::BK, spk = (nk + ks - 1) / ks;
       const dim3 grid(ceil_div(M - mb, 256) * ceil_div(Cop, 128) * ks);
-      if (nst)
-        hipLaunchKernelGGL((bf::conv_fprop_bf_nrm_k<T, true>), grid, dim3(T::NT), 0, s, x, ws, wps, bias, y, H, W, C,
-                           Ho, Wo, Cop, S, st, padh, padw, act, slope, M, K, mb, part, spk, tws, nst);
-      else if (apl && reflect)
-        hipLaunchKernelGGL((bf::conv_fprop_bf_k<T, true, 1, true, true>), grid, dim3(T::NT), 0, s, x, ws, wps, bias, y,
-                           H, W, C, Ho, Wo, Cop, S, st, padh, padw, reflect, act, slope, M, K, mb, part, spk, tws,
-                           nullptr, 0, apl, pps);
-      else if (apl)
-        hipLaunchKernelGGL((bf::conv_fprop_bf_k<T, true, 0, true, true>), grid, dim3(T::NT), 0, s, x, ws, wps, bias, y,
-                           H, W, C, Ho, Wo, Cop, S, st, padh, padw, reflect, act, slope, M, K, mb, part, spk, tws,
-                           nullptr, 0, apl, pps);
-      else if (reflect)
+      if (reflect)
         hipLaunchKernelGGL((bf::conv_fprop_bf_k<T, true, 1, true>), grid, dim3(T::NT), 0, s, x, ws, wps, bias, y, H,
                            W, C, Ho, Wo, Cop, S, st, padh, padw, reflect, act, slope, M, K, mb, part, spk, tws,
                            nullptr);
@@ -2135,27 +1971,6 @@ int bf_fprop_launch(const float* x, const void* wsplit, long wps, const float* b
                            nullptr);
       hipLaunchKernelGGL(bf::fprop_splitk_reduce_k, dim3(ceil_div(M - mb, 32), ceil_div(Cop, 64)), dim3(256), 0, s,
                          tws, ks, mb, M, Cop, bias, act, slope, y, part, Ho * Wo, addend);
-      continue;
-    }
-    if (nst) {  // bf_fprop_nrm_ok: whole 256x128 rounds here
-      using T = bf::Tile<256, 128, 64, 64, 32, 3>;
-      VST_REQUIRE(kp == 7, "conv fprop over relu(IN(x)): unexpected tile kind %d", kp);
-      const dim3 grid(ceil_div(Mend - mb, 256) * ceil_div(Cop, 128));
-      hipLaunchKernelGGL((bf::conv_fprop_bf_nrm_k<T, false>), grid, dim3(T::NT), 0, s, x, ws, wps, bias, y, H, W, C,
-                         Ho, Wo, Cop, S, st, padh, padw, act, slope, Mend, K, mb, part, 0, nullptr, nst);
-      continue;
-    }
-    if (apl && kp == 7) {  // whole 256x128 rounds on the pre-split A planes
-      using T = bf::Tile<256, 128, 64, 64, 32, 3>;
-      const dim3 grid(ceil_div(Mend - mb, 256) * ceil_div(Cop, 128));
-      if (reflect)
-        hipLaunchKernelGGL((bf::conv_fprop_bf_k<T, true, 1, false, true>), grid, dim3(T::NT), 0, s, x, ws, wps, bias, y,
-                           H, W, C, Ho, Wo, Cop, S, st, padh, padw, reflect, act, slope, Mend, K, mb, part, 0, nullptr,
-                           addend, 0, apl, pps);
-      else
-        hipLaunchKernelGGL((bf::conv_fprop_bf_k<T, true, 0, false, true>), grid, dim3(T::NT), 0, s, x, ws, wps, bias, y,
-                           H, W, C, Ho, Wo, Cop, S, st, padh, padw, reflect, act, slope, Mend, K, mb, part, 0, nullptr,
-                           addend, 0, apl, pps);
       continue;
     }
     if (math == VST_MATH_BF16X6) {
@@ -2186,16 +2001,10 @@ static void bf_border_plan(int N, int H, int W, int Cy, int Cx, int math, int* k
 }
 
 // The K-restricted border GEMM (REFL 5, 128x128 tiles): segment lengths and K-split count.  ks: at
-// least 4 K-steps per split and at most one CU round (VST_BORDER_KS overrides; VST_BORDER5=0 keeps the
+// least 4 K-steps per split and at most one CU round (g_border_ks overrides; g_border5 = false keeps the
 // full-K border rows of bf_border_plan).
-static const bool g_border5 = [] {
-  const char* e = getenv("VST_BORDER5");
-  return !(e && e[0] == '0');
-}();
-static const int g_border_ks = [] {
-  const char* e = getenv("VST_BORDER_KS");
-  return e ? atoi(e) : 0;
-}();
+static constexpr bool g_border5 = true;
+static constexpr int g_border_ks = 0;
 static void bf_border5_plan(int N, int H, int W, int Cy, int Cx, int* ks_out, int* lt, int* ll) {
   *lt = bf::border5_seg_rows(N, W + 2, 128);
   *ll = bf::border5_seg_rows(N, H, 128);
@@ -2242,14 +2051,6 @@ size_t bf_dgrad_refl1_ws_floats(int N, int H, int W, int Cy, int Cx, int math) {
 // on: the K-restricted border GEMM and dgrad_border5_add_k).  Replaces the conv over the
 // (H+2) x (W+2) zero-padded frame + reflect fold.  add_border = false: the slabs (bf_dgrad_refl1_slabs)
 // are left for the caller (vst_conv2d_dgrad_refl_in adds them in its InstanceNorm-backward partial pass).
-#ifndef VST_BORDER_FUSE
-#define VST_BORDER_FUSE 0  // the border slabs added by the interior conv's epilogue (border GEMM first): measured +0.5 ms/step, off
-#endif
-static const bool g_border_fuse = [] {  // VST_BORDER_FUSE=1 in the environment turns the variant on
-  const char* e = getenv("VST_BORDER_FUSE");
-  return e ? e[0] == '1' : VST_BORDER_FUSE != 0;
-}();
-
 int bf_dgrad_refl1_launch(const float* dy, const void* wsplit, long wps, const float* addend, float* dx, int N, int H,
                           int W, int Cy, int Cx, int math, hipStream_t s, float* ws, size_t ws_floats, bool add_border) {
   int ks;
@@ -2257,35 +2058,6 @@ int bf_dgrad_refl1_launch(const float* dy, const void* wsplit, long wps, const f
   bf_border_plan(N, H, W, Cy, Cx, math, &ks, &Mb);
   const size_t main_ws = bf_fprop_ws_floats((long)N * H * W, Cx, Cy, 3, 3, math);
   VST_REQUIRE(ws_floats >= main_ws + (size_t)ks * Mb * Cx, "dgrad_refl: workspace too small");
-  {
-    // whole 256x128 rounds (no split-K tail), x6: the K-restricted border GEMM first, then the interior
-    // conv adding the slabs in its LDS-staged epilogue (bit-identical to interior + dgrad_border5_add_k)
-    int kd, m_split, tail_kind, m_first, fks;
-    const long M = (long)N * H * W;
-    bf_plan(M, Cx, math, -1, &kd, &m_split, &tail_kind);
-    bf_split_plan(M, Cx, Cy, 3, 3, math, -1, &m_first, &fks);
-    if (g_border_fuse && g_border5 && add_border && math == VST_MATH_BF16X6 && kd == 7 && !m_split && !fks &&
-        Cy % 32 == 0 && Cx % 4 == 0) {
-      int ks5, lt, ll;
-      bf_border5_plan(N, H, W, Cy, Cx, &ks5, &lt, &ll);
-      const int Mt = 2 * lt + 2 * ll, K5 = 3 * Cy;
-      VST_REQUIRE(ws_floats >= main_ws + (size_t)ks5 * Mt * Cx, "dgrad_refl: workspace too small");
-      float* slab5 = ws + main_ws;
-      const __bf16* wb = reinterpret_cast<const __bf16*>(wsplit);
-      {
-        using T = bf::Tile<128, 128, 64, 32, 32, 3>;
-        const int nk = (K5 + T::BK - 1) / T::BK, spk = (nk + ks5 - 1) / ks5;
-        const dim3 grid(Mt / 128 * ceil_div(Cx, 128) * ks5);
-        hipLaunchKernelGGL((bf::conv_fprop_bf_k<T, true, 5, true>), grid, dim3(T::NT), 0, s, dy, wb, wps, nullptr, dx, H,
-                           W, Cy, lt, ll, Cx, 3, N, 1, 1, 0, VST_ACT_NONE, 0.f, Mt, K5, 0, nullptr, spk, slab5, nullptr);
-      }
-      using T = bf::Tile<256, 128, 64, 64, 32, 3>;
-      const dim3 grid(ceil_div(M, 256) * ceil_div(Cx, 128));
-      hipLaunchKernelGGL((bf::conv_fprop_bf_bord_k<T>), grid, dim3(T::NT), 0, s, dy, wb, wps, dx, H, W, Cy, Cx, addend,
-                         (int)M, 9 * Cy, slab5, ks5, Mt, lt, ll);
-      return check_launch("conv2d_dgrad_refl(fused border)");
-    }
-  }
   if (int e = bf_fprop_launch(dy, wsplit, wps, nullptr, dx, N, H, W, Cy, H, W, Cx, 3, 3, 1, 1, 1, 0, VST_ACT_NONE, 0.f,
                               math, -1, s, nullptr, main_ws ? ws : nullptr, main_ws, addend))
     return e;
@@ -2418,12 +2190,9 @@ bool bf_convT_phases_ok(int C, int Cop, int math) {
 // 32x32).  Round 5
 // sweep (profiles/r05e_convT_wgrad_tiles.jsonl, same box): the 256 -> 128 ConvTranspose / stride-2 data
 // gradient 144 -> 124 us at N = 8 (188 -> 167 at N = 12) against 128x128 tiles of 8 x (64x32) waves; the
-// 128 -> 64 one 150 -> 145 us against 128x64.  VST_CONVT_TILE (developer A/B): 0 = the round-4 tiles
+// 128 -> 64 one 150 -> 145 us against 128x64.  g_convt_tile (developer A/B): 0 = the round-4 tiles
 // (128x128 8 waves / 128x64 4 waves), 1 = 256x128 / 128x64, 2 = 128x128 4 waves / 64x64; -1 = the default.
-static const int g_convt_tile = [] {
-  const char* e = getenv("VST_CONVT_TILE");
-  return e ? atoi(e) : -1;
-}();
+static constexpr int g_convt_tile = -1;
 
 int bf_convT_phases_launch(const float* x, const void* const ws[4], const float* bias, float* y, int N, int H, int W,
                            int C, int Cop, int act, float slope, int math, hipStream_t s, int full) {

@@ -625,14 +625,8 @@ __global__ __launch_bounds__(NT, 1) void conv_c4_ring_k(const float* __restrict_
 // shorter one): a short last segment would cost a whole segment's time.  Its InstanceNorm partials
 // are per 32-pixel row piece, so an image whose H*W is a multiple of 32 (the callers then ask for
 // partials) must also have Wo % 32 == 0: a conv is routed the same way with and without partials.
-static const bool g_c4_direct = [] {
-  const char* e = getenv("VST_C4_DIRECT");
-  return !(e && e[0] == '0');
-}();
-static const bool g_c4_ring = [] {
-  const char* e = getenv("VST_C4_RING");
-  return !(e && e[0] == '0');
-}();
+static constexpr bool g_c4_direct = true;
+static constexpr bool g_c4_ring = true;
 
 bool c4_direct_ok(int C, int Cop, int R, int S, int st, int Ho, int Wo, int math) {
   return g_c4_direct && C == 4 && Cop == c4::COP && st == 1 && R == 7 && S >= 1 && S <= c4::MAXR &&

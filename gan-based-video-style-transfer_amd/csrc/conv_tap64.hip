@@ -232,10 +232,7 @@ __global__ __launch_bounds__(NT, 1) void tap64_k(const float* __restrict__ x, co
 
 }  // namespace tap64
 
-static const bool g_tap64 = [] {
-  const char* e = getenv("VST_TAP64");
-  return !(e && e[0] == '0');
-}();
+static constexpr bool g_tap64 = true;
 
 // Does the direct kernel take this tap conv?  64 input channels, 7 x 7, 4 (padded) outputs, x6 / x3
 // math, W in {256, 512, 1024} (a group is 1024 / W whole rows), reflect 'same' or zero padding.

@@ -101,7 +101,7 @@ static_assert(sizeof(PackJob) == 168, "PackJob layout is part of the C ABI (incl
 // One 64-lane block per 256-element job block (PackJob.block0 units): a lane packs 4 consecutive elements (their
 // gathers issued together), stores them as one float4 and each split plane as one 8-byte word — the per-element
 // form moved ~1.5 TB/s (narrow stores, one gather in flight per lane).
-// The per-element form (one element per lane, 256-lane blocks): VST_PACK_KERNEL=0.
+// The per-element form (one element per lane, 256-lane blocks): kind 0.
 __global__ __launch_bounds__(256) void weight_pack_batch1_k(const PackJob* __restrict__ jobs, int nj) {
   const long b = blockIdx.x;
   int lo = 0, hi = nj - 1;
@@ -294,10 +294,7 @@ extern "C" int vst_weight_pack_split(const float* w, float* out, void* split, in
 
 extern "C" int vst_weight_pack_batch(const void* jobs, int njobs, long nblocks, void* stream) {
   VST_REQUIRE(jobs && njobs > 0 && nblocks > 0 && nblocks < (1L << 31), "weight_pack_batch: bad args");
-  static const int kind = [] {  // 0: per element, 1: 4 elements per lane, 2: + the tiled OK / IK / IKF path
-    const char* e = getenv("VST_PACK_KERNEL");
-    return e ? atoi(e) : 2;
-  }();
+  constexpr int kind = 2;  // 0: per element, 1: 4 elements per lane, 2: + the tiled OK / IK / IKF path
   const PackJob* J = reinterpret_cast<const PackJob*>(jobs);
   if (kind == 0)
     hipLaunchKernelGGL(weight_pack_batch1_k, dim3((unsigned)nblocks), dim3(256), 0, (hipStream_t)stream, J, njobs);

@@ -132,221 +132,6 @@ __global__ __launch_bounds__(NRED) void in_partial_k(const float* __restrict__ x
   }
 }
 
-// The reflect fold of a stride-1 data gradient computed over the padded frame (vst_reflect_fold:
-// g[n][h][w] = addend + sum of dxp over the padded positions that mirror onto (h, w)), fused with
-// the backward partials of the InstanceNorm(+act) below it (in_partial_k<1> over g): g is written
-// once and reduced while in registers, so the IN backward's separate read of g (and of its launch)
-// is gone.  Same block geometry / partial layout / summation order as in_partial_k<1>.
-__global__ __launch_bounds__(NRED) void fold_in_partial_k(const float* __restrict__ dxp,
-                                                          const float* __restrict__ addend,
-                                                          float* __restrict__ gout, const float* __restrict__ x,
-                                                          const float* __restrict__ stats,
-                                                          double* __restrict__ part, int H, int W, int C,
-                                                          int pad, int LP, int PG, int SP, int nsplit, int act,
-                                                          float slope) {
-  constexpr int NV = 3;
-  __shared__ double red[NV * 4][NRED];
-  const int t = threadIdx.x, c4 = t % LP, pg = t / LP;
-  const int n = blockIdx.y, z = blockIdx.x;
-  const int HW = H * W, Hp = H + 2 * pad, Wp = W + 2 * pad;
-  const int p0 = z * SP, p1 = min(HW, p0 + SP);
-  double acc[NV][4];
-#pragma unroll
-  for (int v = 0; v < NV; ++v)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[v][j] = 0.0;
-  float mean[4], rstd[4];
-  {
-    const float4 s0 = reinterpret_cast<const float4*>(stats)[((long)n * C + 4 * c4) / 2];
-    const float4 s1 = reinterpret_cast<const float4*>(stats)[((long)n * C + 4 * c4) / 2 + 1];
-    mean[0] = s0.x; rstd[0] = s0.y; mean[1] = s0.z; rstd[1] = s0.w;
-    mean[2] = s1.x; rstd[2] = s1.y; mean[3] = s1.z; rstd[3] = s1.w;
-  }
-  const float4* src = reinterpret_cast<const float4*>(dxp) + (long)n * Hp * Wp * LP + c4;
-  const float4* xb = reinterpret_cast<const float4*>(x) + (long)n * HW * LP + c4;
-  const float4* ab = addend ? reinterpret_cast<const float4*>(addend) + (long)n * HW * LP + c4 : nullptr;
-  float4* gb = reinterpret_cast<float4*>(gout) + (long)n * HW * LP + c4;
-  auto fold = [&](int p) {
-    const int h = p / W, w = p - (p / W) * W;
-    float4 g = ab ? ab[(long)p * LP] : make_float4(0.f, 0.f, 0.f, 0.f);
-    if (h > pad && h < H - 1 - pad && w > pad && w < W - 1 - pad) {  // interior: one source
-      add_f4(g, src[((long)(h + pad) * Wp + w + pad) * LP]);
-      gb[(long)p * LP] = g;
-      return g;
-    }
-    int hs[3], wsx[3], nh = 0, nw = 0;
-    hs[nh++] = h + pad;
-    if (h >= 1 && h <= pad) hs[nh++] = pad - h;
-    if (h >= H - 1 - pad && h <= H - 2) hs[nh++] = 2 * H - 2 - h + pad;
-    wsx[nw++] = w + pad;
-    if (w >= 1 && w <= pad) wsx[nw++] = pad - w;
-    if (w >= W - 1 - pad && w <= W - 2) wsx[nw++] = 2 * W - 2 - w + pad;
-    for (int a = 0; a < nh; ++a)
-      for (int b = 0; b < nw; ++b) add_f4(g, src[((long)hs[a] * Wp + wsx[b]) * LP]);
-    gb[(long)p * LP] = g;
-    return g;
-  };
-  auto accum = [&](const float4 v, const float4 gv) {
-    const float xv[4] = {v.x, v.y, v.z, v.w}, gg[4] = {gv.x, gv.y, gv.z, gv.w};
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float xh = (xv[j] - mean[j]) * rstd[j];
-      float d = 1.f;
-      if (act == VST_ACT_RELU) d = xh > 0.f ? 1.f : 0.f;
-      else if (act == VST_ACT_LRELU) d = xh > 0.f ? 1.f : slope;
-      const float g = gg[j] * d;
-      acc[0][j] += g;
-      acc[1][j] += (double)g * xh;
-      acc[2][j] += xh;
-    }
-  };
-  constexpr int UR = 4;
-  if (pg < PG) {
-    int p = p0 + pg;
-    for (; p + (UR - 1) * PG < p1; p += UR * PG) {
-      float4 v[UR], gv[UR];
-#pragma unroll
-      for (int k = 0; k < UR; ++k) {
-        v[k] = xb[(long)(p + k * PG) * LP];
-        gv[k] = fold(p + k * PG);
-      }
-#pragma unroll
-      for (int k = 0; k < UR; ++k) accum(v[k], gv[k]);
-    }
-    for (; p < p1; p += PG) accum(xb[(long)p * LP], fold(p));
-  }
-#pragma unroll
-  for (int v = 0; v < NV; ++v)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) red[v * 4 + j][t] = acc[v][j];
-  __syncthreads();
-  if (pg == 0) {
-    double out[NV][4];
-#pragma unroll
-    for (int v = 0; v < NV; ++v)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        double sum = 0.0;
-        for (int q = 0; q < PG; ++q) sum += red[v * 4 + j][q * LP + c4];
-        out[v][j] = sum;
-      }
-    double* dst = part + (((long)n * nsplit + z) * C + 4 * c4) * NV;
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int v = 0; v < NV; ++v) dst[j * NV + v] = out[v][j];
-  }
-}
-
-// The border add of a ReflectionPad2d(1) + 3x3 data gradient (conv_bf.hip: the interior conv left g
-// without the padded border positions, whose GEMM left ks split-K slabs [ks][Mb][C], BorderSlabs) fused with the
-// backward partials of the InstanceNorm(+act) below it: the pixels a padded position mirrors onto
-// (rows / columns 1 and H-2 / W-2: ~6 % at 64 x 64) get the slab sums added (split order, then row
-// order: dgrad_border_add_k's arithmetic) and written back; every pixel's g is then reduced while in
-// registers.  Replaces dgrad_border_add_k + in_partial_k<1>: one read of g and two launches fewer.
-// Same block geometry / partial layout / summation order as in_partial_k<1>.
-__global__ __launch_bounds__(NRED) void border_in_partial_k(float* __restrict__ g, const float* __restrict__ slab,
-                                                            int ks, int Mb, int Lt, int Ll,
-                                                            const float* __restrict__ x,
-                                                            const float* __restrict__ stats, double* __restrict__ part,
-                                                            int H, int W, int C, int LP, int PG, int SP, int nsplit,
-                                                            int act, float slope) {
-  constexpr int NV = 3;
-  __shared__ double red[NV * 4][NRED];
-  const int t = threadIdx.x, c4 = t % LP, pg = t / LP;
-  const int n = blockIdx.y, z = blockIdx.x;
-  const int HW = H * W;
-  const int p0 = z * SP, p1 = min(HW, p0 + SP);
-  double acc[NV][4];
-#pragma unroll
-  for (int v = 0; v < NV; ++v)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[v][j] = 0.0;
-  float mean[4], rstd[4];
-  {
-    const float4 s0 = reinterpret_cast<const float4*>(stats)[((long)n * C + 4 * c4) / 2];
-    const float4 s1 = reinterpret_cast<const float4*>(stats)[((long)n * C + 4 * c4) / 2 + 1];
-    mean[0] = s0.x; rstd[0] = s0.y; mean[1] = s0.z; rstd[1] = s0.w;
-    mean[2] = s1.x; rstd[2] = s1.y; mean[3] = s1.z; rstd[3] = s1.w;
-  }
-  const float4* xb = reinterpret_cast<const float4*>(x) + (long)n * HW * LP + c4;
-  float4* gb = reinterpret_cast<float4*>(g) + (long)n * HW * LP + c4;
-  const long zst = (long)Mb * C;
-  // g of pixel p: + its border rows' slab sums where a padded position mirrors onto it (written back)
-  auto border = [&](int p, float4 gv) {
-    int rows[3];
-    const int nr = dgrad_border_slab_rows(n, p / W, p - (p / W) * W, H, W, Lt, Ll, rows);
-    if (nr == 0) return gv;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int r = 0; r < nr; ++r) {
-      // a row's (<= 16) split slabs loaded together, then summed in split order
-      const float* base = slab + (long)rows[r] * C + 4 * c4;
-      float4 u[16];
-#pragma unroll
-      for (int q = 0; q < 16; ++q)
-        if (q < ks) u[q] = *reinterpret_cast<const float4*>(base + q * zst);
-      float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-      for (int q = 0; q < 16; ++q)
-        if (q < ks) add_f4(a, u[q]);
-      add_f4(v, a);
-    }
-    add_f4(gv, v);
-    gb[(long)p * LP] = gv;
-    return gv;
-  };
-  auto accum = [&](const float4 v, const float4 gv) {
-    const float xv[4] = {v.x, v.y, v.z, v.w}, gg[4] = {gv.x, gv.y, gv.z, gv.w};
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float xh = (xv[j] - mean[j]) * rstd[j];
-      float d = 1.f;
-      if (act == VST_ACT_RELU) d = xh > 0.f ? 1.f : 0.f;
-      else if (act == VST_ACT_LRELU) d = xh > 0.f ? 1.f : slope;
-      const float gm = gg[j] * d;
-      acc[0][j] += gm;
-      acc[1][j] += (double)gm * xh;
-      acc[2][j] += xh;
-    }
-  };
-  constexpr int UR = IN_UNROLL;
-  if (pg < PG) {
-    int p = p0 + pg;
-    for (; p + (UR - 1) * PG < p1; p += UR * PG) {
-      float4 v[UR], gv[UR];
-#pragma unroll
-      for (int k = 0; k < UR; ++k) {
-        v[k] = xb[(long)(p + k * PG) * LP];
-        gv[k] = gb[(long)(p + k * PG) * LP];
-      }
-#pragma unroll
-      for (int k = 0; k < UR; ++k) accum(v[k], border(p + k * PG, gv[k]));
-    }
-    for (; p < p1; p += PG) accum(xb[(long)p * LP], border(p, gb[(long)p * LP]));
-  }
-#pragma unroll
-  for (int v = 0; v < NV; ++v)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) red[v * 4 + j][t] = acc[v][j];
-  __syncthreads();
-  if (pg == 0) {
-    double out[NV][4];
-#pragma unroll
-    for (int v = 0; v < NV; ++v)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        double sum = 0.0;
-        for (int q = 0; q < PG; ++q) sum += red[v * 4 + j][q * LP + c4];
-        out[v][j] = sum;
-      }
-    double* dst = part + (((long)n * nsplit + z) * C + 4 * c4) * NV;
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int v = 0; v < NV; ++v) dst[j * NV + v] = out[v][j];
-  }
-}
-
 // Fold the per-slice partials of one (n, CPB-channel group): G = 256 / CPB thread groups stride the
 // slices (coalesced over c), then combine through LDS in a fixed order.  out[v] = sum_z
 // part[n][z][c][v].  CPB = 16 for the IN finalizes (4x the blocks of CPB = 64: these small kernels are
@@ -398,10 +183,7 @@ __device__ __forceinline__ bool fold_slices(const double* __restrict__ part, int
 // Channels per finalize block: 16, or 4 when (C / 16) x N blocks would leave most CUs idle over many
 // slices (the first conv's 64 channels x 8 images over 2048 slices: 32 blocks, 14 us; B=1 inference's
 // 256 channels: 16 blocks) — 4x the blocks, each thread's slice chain 4x shorter.
-static const bool g_fin_narrow = [] {
-  const char* e = getenv("VST_FIN_NARROW");
-  return !(e && e[0] == '0');
-}();
+static constexpr bool g_fin_narrow = true;
 static int fin_cpb(int C, int N, int nsplit) {
   return (!g_fin_narrow || (long)((C + 15) / 16) * N >= 128 || nsplit < 64) ? 16 : 4;
 }
@@ -442,7 +224,7 @@ __device__ __forceinline__ void store_planes4(__bf16* __restrict__ pl, long pps,
 
 __global__ void in_apply_k(const float4* __restrict__ x, const float* __restrict__ stats,
                            const float4* __restrict__ res, float4* __restrict__ y, long total4,
-                           int HW, int C4, int act, float slope, __bf16* __restrict__ apl = nullptr) {
+                           int HW, int C4, int act, float slope) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total4) return;
   const int c4 = i % C4;
@@ -457,7 +239,6 @@ __global__ void in_apply_k(const float4* __restrict__ x, const float* __restrict
   v.w = apply_act((v.w - s1.z) * s1.w, act, slope);
   if (res) add_f4(v, res[i]);
   y[i] = v;
-  if (apl) store_planes4(apl, total4 * 4, i * 4, v);
 }
 
 // RNE bf16 pair (the split of vst_weight_split / nhwc_to_cp_planes_k)
@@ -469,7 +250,7 @@ __device__ __forceinline__ uint32_t bf16_pack2(float a, float b) {
 }
 
 // v's three bf16 planes (hi, mid, lo: the RNE split of nhwc_to_cp_planes_k / split8) at element e of planes
-// [3][pps] — the NHWC A-operand planes of an x6 forward that takes its A operand pre-split (APRE)
+// [3][pps] — the NHWC A-operand planes of an x6 data gradient that takes its A operand pre-split (APRE_BWD)
 __device__ __forceinline__ void store_planes4(__bf16* __restrict__ pl, long pps, long e, float4 v) {
   float r[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -498,8 +279,7 @@ __global__ __launch_bounds__(256) void in_apply_cp_pad_k(const float* __restrict
                                                           const float* __restrict__ res, float* __restrict__ a,
                                                           float* __restrict__ xt, int N, int H, int W, int C,
                                                           int pad, int reflect, int phase, long ld, int act,
-                                                          float slope, int wx = 0, __bf16* __restrict__ planes = nullptr,
-                                                          __bf16* __restrict__ apl = nullptr) {
+                                                          float slope, int wx = 0, __bf16* __restrict__ planes = nullptr) {
   __shared__ float tile[64][65];
   const int Hp = H + 2 * pad, Wp = W + 2 * pad, Wq = Wp + wx;
   const long P = (long)N * Hp * Wq;
@@ -538,10 +318,7 @@ __global__ __launch_bounds__(256) void in_apply_cp_pad_k(const float* __restrict
         v.z = apply_act((v.z - s1.x) * s1.y, act, slope);
         v.w = apply_act((v.w - s1.z) * s1.w, act, slope);
         if (res) add_f4(v, *reinterpret_cast<const float4*>(res + e));
-        if (inner) {
-          *reinterpret_cast<float4*>(a + e) = v;
-          if (apl) store_planes4(apl, (long)N * H * W * C, e, v);
-        }
+        if (inner) *reinterpret_cast<float4*>(a + e) = v;
       }
     }
     tile[pr][c4] = v.x;
@@ -1028,18 +805,6 @@ extern "C" int vst_instnorm_act_bwd_planes(const float* gy, const float* x, cons
                                            float* db, float* ws, int N, int HW, int C, int act, float slope,
                                            int accumulate_db, void* planes, long ldp, void* stream);
 
-// vst_instnorm_act_fwd that also writes y's NHWC bf16 planes apl [3][N*HW*C] (the pre-split A operand of the x6
-// forward that consumes y: vst_conv2d_fwd_apre_ws)
-extern "C" int vst_instnorm_act_fwd_apre(const float* x, const float* stats, const float* residual, float* y, void* apl,
-                                         int N, int HW, int C, int act, float slope, void* stream) {
-  VST_REQUIRE(x && stats && y && apl && C % 4 == 0, "instnorm_act_fwd_apre: bad args");
-  const long total4 = (long)N * HW * C / 4;
-  hipLaunchKernelGGL(in_apply_k, dim3(ceil_div(total4, 256)), dim3(256), 0, (hipStream_t)stream,
-                     reinterpret_cast<const float4*>(x), stats, reinterpret_cast<const float4*>(residual),
-                     reinterpret_cast<float4*>(y), total4, HW, C / 4, act, slope, reinterpret_cast<__bf16*>(apl));
-  return check_launch("instnorm_act_fwd_apre");
-}
-
 extern "C" int vst_instnorm_act_fwd_cp(const float* x, const float* stats, const float* residual, float* y,
                                        float* xt, int N, int H, int W, int C, int act, float slope, int pad,
                                        int pad_mode, int stride, void* stream) {
@@ -1052,22 +817,6 @@ extern "C" int vst_instnorm_act_fwd_cp(const float* x, const float* stats, const
                      x, stats, residual, y, xt, N, H, W, C, pad, pad_mode == VST_PAD_REFLECT, stride == 2,
                      rk_cp_ld(P), act, slope);
   return check_launch("instnorm_act_fwd_cp");
-}
-
-// vst_instnorm_act_fwd_cp that also writes the activation's NHWC bf16 planes apl [3][N*H*W*C] (the pre-split A
-// operand of the x6 forward that consumes it: vst_conv2d_fwd_apre_ws)
-extern "C" int vst_instnorm_act_fwd_cp_apre(const float* x, const float* stats, const float* residual, float* y,
-                                            float* xt, void* apl, int N, int H, int W, int C, int act, float slope,
-                                            int pad, int pad_mode, int stride, void* stream) {
-  VST_REQUIRE(x && stats && y && xt && apl && C % 4 == 0 && pad >= 0 && (stride == 1 || stride == 2),
-              "instnorm_act_fwd_cp_apre: bad args");
-  VST_REQUIRE(pad_mode == VST_PAD_ZERO || (pad < H && pad < W), "instnorm_act_fwd_cp_apre: reflect pad >= size");
-  VST_REQUIRE(stride == 1 || (W + 2 * pad) % 2 == 0, "instnorm_act_fwd_cp_apre: stride 2 needs W + 2 pad even");
-  const long P = (long)N * (H + 2 * pad) * (W + 2 * pad);
-  hipLaunchKernelGGL(in_apply_cp_pad_k, dim3(ceil_div(P, 64), ceil_div(C, 64)), dim3(256), 0, (hipStream_t)stream,
-                     x, stats, residual, y, xt, N, H, W, C, pad, pad_mode == VST_PAD_REFLECT, stride == 2,
-                     rk_cp_ld(P), act, slope, 0, nullptr, reinterpret_cast<__bf16*>(apl));
-  return check_launch("instnorm_act_fwd_cp_apre");
 }
 
 extern "C" int vst_instnorm_act_fwd_planes(const float* x, const float* stats, const float* residual, float* y,
@@ -1122,83 +871,10 @@ extern "C" int vst_instnorm_act_bwd_planes_apre(const float* gy, const float* x,
   return in_bwd_tail(gy, x, stats, dx, db, ws, N, HW, C, act, slope, accumulate_db, planes, ldp, g, s, apl);
 }
 
-extern "C" int vst_reflect_fold_instnorm_bwd(const float* dxp, const float* addend, float* gout, const float* x,
-                                             const float* stats, float* dx, float* db, float* ws, int N, int H,
-                                             int W, int C, int pad, int act, float slope, int accumulate_db,
-                                             void* planes, long ldp, void* stream) {
-  RedGeom g;
-  const int HW = H * W;
-  VST_REQUIRE(dxp && gout && x && stats && dx && ws && pad >= 0 && pad < H && pad < W && red_geom(N, HW, C, g),
-              "reflect_fold_instnorm_bwd: bad args");
-  VST_REQUIRE(!planes || ldp >= (long)N * HW, "reflect_fold_instnorm_bwd: plane stride %ld < N*HW", ldp);
-  hipStream_t s = (hipStream_t)stream;
-  double* part = reinterpret_cast<double*>(ws);
-  hipLaunchKernelGGL(fold_in_partial_k, dim3(g.nsplit, N), dim3(NRED), 0, s, dxp, addend, gout, x, stats, part,
-                     H, W, C, pad, g.LP, g.PG, g.SP, g.nsplit, act, slope);
-  return in_bwd_tail(gout, x, stats, dx, db, ws, N, HW, C, act, slope, accumulate_db, planes, ldp, g, s);
-}
-
-// ReflectionPad2d(1) + 3x3 conv data gradient (vst_conv2d_dgrad_refl) and the InstanceNorm(+act)
-// backward of the layer below it: the interior GEMM (+ addend) writes g, the border GEMM leaves its
-// slabs (vst_conv2d_dgrad_refl_slabs, in the dgrad workspace), then border_in_partial_k adds them into
-// g while taking the IN partials, the finalize and the apply (+ dy planes) follow
-// (vst_instnorm_act_bwd_refl_border).  vst_conv2d_dgrad_refl_in = both, one workspace: the IN
-// partials / coefficients, then the dgrad's.
-static size_t in_ws_bytes_al(int N, int HW, int C) { return (vst_instnorm_ws_bytes(N, HW, C) + 255) / 256 * 256; }
-
-extern "C" int vst_conv2d_dgrad_refl_slabs(const float* dy, const void* wsplit, const float* addend, float* gout,
-                                           float* ws, size_t ws_bytes, int N, int H, int W, int Cy, int Cx, int math,
-                                           void* stream) {
-  VST_REQUIRE(dy && wsplit && gout && ws, "conv2d_dgrad_refl_slabs: null pointer");
-  VST_REQUIRE(bf_dgrad_refl1_ok(N, H, W, Cy, Cx, math),
-              "conv2d_dgrad_refl_slabs: needs split-bf16 math, Cy %% 32 == 0, Cx %% 4 == 0, H, W >= 4");
-  return bf_dgrad_refl1_launch(dy, wsplit, (long)Cx * 9 * Cy, addend, gout, N, H, W, Cy, Cx, math, (hipStream_t)stream,
-                               ws, ws_bytes / sizeof(float), false);
-}
-
-extern "C" int vst_instnorm_act_bwd_refl_border(float* gout, const float* x, const float* stats, float* dx, float* db,
-                                                float* in_ws, const float* dgrad_ws, int N, int H, int W, int Cy,
-                                                int Cx, int act, float slope, int accumulate_db, void* planes,
-                                                long ldp, int math, void* stream) {
-  RedGeom g;
-  const int HW = H * W;
-  VST_REQUIRE(gout && x && stats && dx && in_ws && dgrad_ws, "instnorm_act_bwd_refl_border: null pointer");
-  VST_REQUIRE(bf_dgrad_refl1_ok(N, H, W, Cy, Cx, math) && red_geom(N, HW, Cx, g),
-              "instnorm_act_bwd_refl_border: unsupported shape / arithmetic");
-  VST_REQUIRE(!planes || ldp >= (long)N * HW, "instnorm_act_bwd_refl_border: plane stride %ld < N*HW", ldp);
-  BorderSlabs b;
-  const size_t off = bf_dgrad_refl1_slabs(N, H, W, Cy, Cx, math, &b);
-  hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(border_in_partial_k, dim3(g.nsplit, N), dim3(NRED), 0, s, gout, dgrad_ws + off, b.ks, b.Mb, b.Lt,
-                     b.Ll, x, stats, reinterpret_cast<double*>(in_ws), H, W, Cx, g.LP, g.PG, g.SP, g.nsplit, act, slope);
-  return in_bwd_tail(gout, x, stats, dx, db, in_ws, N, HW, Cx, act, slope, accumulate_db, planes, ldp, g, s);
-}
-
-extern "C" size_t vst_conv2d_dgrad_refl_in_ws_bytes(int N, int H, int W, int Cy, int Cx, int math) {
-  RedGeom g;
-  if (!bf_dgrad_refl1_ok(N, H, W, Cy, Cx, math) || !red_geom(N, H * W, Cx, g)) return 0;
-  return in_ws_bytes_al(N, H * W, Cx) + bf_dgrad_refl1_ws_floats(N, H, W, Cy, Cx, math) * sizeof(float);
-}
-
-extern "C" int vst_conv2d_dgrad_refl_in(const float* dy, const void* wsplit, const float* addend, float* gout,
-                                        const float* x, const float* stats, float* dx, float* db, float* ws,
-                                        size_t ws_bytes, int N, int H, int W, int Cy, int Cx, int act, float slope,
-                                        int accumulate_db, void* planes, long ldp, int math, void* stream) {
-  VST_REQUIRE(ws && ws_bytes >= vst_conv2d_dgrad_refl_in_ws_bytes(N, H, W, Cy, Cx, math) &&
-                  vst_conv2d_dgrad_refl_in_ws_bytes(N, H, W, Cy, Cx, math) > 0,
-              "conv2d_dgrad_refl_in: unsupported shape or workspace too small (%zu bytes)", ws_bytes);
-  const size_t inb = in_ws_bytes_al(N, H * W, Cx);
-  float* dws = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + inb);
-  if (int e = vst_conv2d_dgrad_refl_slabs(dy, wsplit, addend, gout, dws, ws_bytes - inb, N, H, W, Cy, Cx, math,
-                                          stream))
-    return e;
-  return vst_instnorm_act_bwd_refl_border(gout, x, stats, dx, db, ws, dws, N, H, W, Cy, Cx, act, slope,
-                                          accumulate_db, planes, ldp, math, stream);
-}
-
-// vst_conv2d_dgrad_refl_in with the IN-backward partials taken by the data gradient itself: the interior
-// GEMM's epilogue (per 32-row group) and the border add (its correction slices) write them, so the
-// partial pass (a read of g and z and a launch) is gone; then the same finalize / apply.  Workspace: the
+// ReflectionPad2d(1) + 3x3 conv data gradient (vst_conv2d_dgrad_refl) and the InstanceNorm(+act) backward of the
+// layer below it, with the IN-backward partials taken by the data gradient itself: the interior GEMM's epilogue
+// (per 32-row group) and the border add (its correction slices) write them, so no partial pass (a read of g and z
+// and a launch) is needed; then the finalize / apply (+ dy planes).  Workspace: the
 // IN partials [N][ns][C][3] + coefficients, then the data gradient's.  x6 arithmetic, H W % 32 == 0.
 static size_t in_epi_ws_bytes_al(int N, int H, int W, int C) {
   const size_t ns = bf_dgrad_refl1_inb_slices(H, W);

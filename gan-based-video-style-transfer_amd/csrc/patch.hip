@@ -657,11 +657,8 @@ int head_dgrad_launch(const float* dy, const float* wp, const float* addend, flo
 
 namespace vst {
 
-// VST_IMG_WGRAD=0: image-input weight gradients on the split-bf16 GEMM (conv.hip) instead
-const bool g_img_wgrad = [] {
-  const char* e = getenv("VST_IMG_WGRAD");
-  return !(e && e[0] == '0');
-}();
+// g_img_wgrad = false: image-input weight gradients on the split-bf16 GEMM (conv.hip) instead
+const bool g_img_wgrad = true;
 
 bool img_wgrad_ok(int Cx, int Cyp, int R, int S, int st, int reflect, int Ci, int Wo) {
   return Cx == 4 && Ci <= 3 && Cyp % 2 == 0 && Cyp <= 64 && R * S <= 16 && st >= 1 && !reflect && Wo >= 1;

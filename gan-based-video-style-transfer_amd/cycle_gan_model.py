@@ -23,8 +23,8 @@ from .optim import FusedAdam
 
 
 # Group the step's generator passes per network into batched calls (and real+fake per D);
-# VST_BATCH_PASSES=0 runs them one by one as the reference does.
-BATCH_PASSES = os.environ.get("VST_BATCH_PASSES", "1") != "0"
+# False runs them one by one as the reference does.
+BATCH_PASSES = True
 
 
 class _TemporalFn(torch.autograd.Function):

@@ -23,8 +23,8 @@ from . import ops, perceptual
 from .cycle_gan_model import CycleGANModel
 
 CONTENT_LEVEL = 3  # relu4_1
-# the loss's three VGG forwards as one batch (perceptual._VggMultiFn); VST_VGG_BATCHED=0: three calls
-VGG_BATCHED = __import__("os").environ.get("VST_VGG_BATCHED", "1") != "0"
+# the loss's three VGG forwards as one batch (perceptual._VggMultiFn); False: three calls
+VGG_BATCHED = True
 SEEDED_LAMBDA = (100.0, 500.0)       # (content, style) for the seeded kaiming fan_out VGG-19
 PRETRAINED_LAMBDA = (1.0, 0.01)      # for real (or fan_in-scale) VGG-19 weights
 

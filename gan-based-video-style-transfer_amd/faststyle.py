@@ -27,16 +27,16 @@ from .optim import FusedAdam
 
 # The 3x3 stride-1 data gradients (residual blocks, upsampling convs) as forward convs over the rotated taps on the
 # split-bf16 kernel with the reflect border GEMM (ops.conv2d_dgrad_s1, the generator's route) instead of the
-# transposed conv on the fp32-operand kernel; VST_FS_DGRAD_FPROP=0 keeps the latter
-FS_DGRAD_FPROP = __import__("os").environ.get("VST_FS_DGRAD_FPROP", "1") != "0"
+# transposed conv on the fp32-operand kernel; False keeps the latter
+FS_DGRAD_FPROP = True
 # The 9x9 32 -> 3 output layer on the tap routes of the generator's 7x7 output layer: forward as the 1x1 conv into
 # (tap, co) channels + the tap sum (ops.tap_conv_fwd), weight gradient as the swapped GEMM (tap_conv_wgrad_swap),
 # data gradient as the forward conv of the 8-channel-padded dy over the rotated taps + reflect fold; instead of the
-# VALU skinny kernels and the fp32-operand transposed conv.  VST_FS_TAP=0 keeps those.
-FS_TAP = __import__("os").environ.get("VST_FS_TAP", "1") != "0"
+# VALU skinny kernels and the fp32-operand transposed conv.  False keeps those.
+FS_TAP = True
 # The loss network's two forwards (styled image, content image) as one batch (perceptual._VggMultiFn);
-# VST_VGG_BATCHED=0: two calls
-VGG_BATCHED = __import__("os").environ.get("VST_VGG_BATCHED", "1") != "0"
+# False: two calls
+VGG_BATCHED = True
 
 
 class InstanceNormAffine(nn.Module):

@@ -155,16 +155,17 @@ class _Marker(nn.Module):
 # The generator's image-side layers (c0: 3 -> ngf 7x7, and the data gradient of f: ngf -> 3 7x7) carry
 # their 3-channel side padded to 8 channels, so the 7x7 implicit GEMMs run on the split-bf16 kernels
 # (8-channel K chunks; half the K is zeros) instead of the fp32-image [row][k] kernels they otherwise
-# need at 4 channels (~40 TF): VST_C8_EDGES=0 restores those.
-C8_EDGES = os.environ.get("VST_C8_EDGES", "1") != "0"
+# need at 4 channels (~40 TF).
+C8_EDGES = True
 # The generator's first conv runs on the 4-channel image itself (conv_fprop_bf_k's 4-channel variant,
 # K = 49*4 instead of 49*8); the 8-channel copy is still made for its weight gradient.  Likewise the
-# data gradient of the last conv (a forward conv over its 4-channel output gradient).  VST_C4_FWD=0
-# runs both on 8-channel copies.
-C4_FWD = os.environ.get("VST_C4_FWD", "1") != "0" and os.environ.get("VST_BF_C4", "1") != "0"
+# data gradient of the last conv (a forward conv over its 4-channel output gradient).  (Module flags
+# like this one are route selectors the tests flip in-process to compare routes; they are not read
+# from the environment.)
+C4_FWD = True
 # ... and the first conv's weight gradient reads the 4-channel image too (the split-bf16 wgrad takes any
-# channel count: K rows 49*4 instead of 49*8, and no 8-channel copy at all); VST_C4_WGRAD=0 keeps the copy.
-C4_WGRAD = C4_FWD and os.environ.get("VST_C4_WGRAD", "1") != "0"
+# channel count: K rows 49*4 instead of 49*8, and no 8-channel copy at all).
+C4_WGRAD = C4_FWD
 
 
 def _pad_channels(x, cs):
@@ -180,8 +181,8 @@ GRAPH_CACHE = 8  # captured input shapes kept per network
 
 
 # Pack every layer of a network in one launch and refresh in place after updates (ops.PackBatch);
-# VST_PACK_BATCH=0: one vst_weight_pack_split launch per pack, rebuilt per weight version.
-PACK_BATCH = os.environ.get("VST_PACK_BATCH", "1") != "0"
+# False: one vst_weight_pack_split launch per pack, rebuilt per weight version.
+PACK_BATCH = True
 
 
 class FlatNet(nn.Module):
@@ -350,21 +351,21 @@ def _pack_conv(m):
 # Stride-1 data gradients whose output-gradient channel count suits the split-bf16 forward kernel
 # run as forward convs over rotated weights (ops.conv2d_dgrad_s1): the fprop kernel (pre-split
 # weight planes) sustains ~1.8x the transposed-conv kernel on the ResnetBlock shape.
-DGRAD_AS_FPROP = os.environ.get("VST_DGRAD_FPROP", "1") != "0"
+DGRAD_AS_FPROP = True
 # The generator's last conv (4 padded output channels) runs as a tap GEMM on the matrix cores
-# (ops.tap_conv_fwd / tap_conv_wgrad) instead of the VALU skinny kernel; VST_TAP_CONV=0 disables.
-TAP_LAST = os.environ.get("VST_TAP_CONV", "1") != "0"
+# (ops.tap_conv_fwd / tap_conv_wgrad) instead of the VALU skinny kernel.
+TAP_LAST = True
 # ... its forward as the 7x1 conv with (column tap, channel) outputs + a column tap sum (ops.tap_conv_fwd_h:
-# a 28-wide intermediate instead of the 196-wide one); VST_TAP_H=0 keeps the 1x1 conv + full tap sum.
-TAP_H = os.environ.get("VST_TAP_H", "1") != "0"
-# the image-input first layer's data gradient the same way (ops.tap_conv_dgrad_h); VST_TAP_HD=0: tap gather.
-TAP_HD = os.environ.get("VST_TAP_HD", "1") != "0"
-# ... and the last layer's weight gradient as the swapped GEMM (ops.tap_conv_wgrad_swap, VST_TAP_SWAP) or the
-# 7x1 conv's (ops.tap_conv_wgrad_h); VST_TAP_HW=0: tap fold.
-TAP_HW = os.environ.get("VST_TAP_HW", "1") != "0"
+# a 28-wide intermediate instead of the 196-wide one); False keeps the 1x1 conv + full tap sum.
+TAP_H = True
+# the image-input first layer's data gradient the same way (ops.tap_conv_dgrad_h); False: tap gather.
+TAP_HD = True
+# ... and the last layer's weight gradient as the swapped GEMM (ops.tap_conv_wgrad_swap, ops.TAP_SWAP) or the
+# 7x1 conv's (ops.tap_conv_wgrad_h); False: tap fold.
+TAP_HW = True
 # The up-sampling ConvTranspose2d (k3 s2 p1 op1) forward as four sub-pixel phase convs on the
-# split-bf16 forward kernel + an interleave (ops.convT3s2_fwd); VST_CONVT_PHASES=0 disables.
-CONVT_PHASES = os.environ.get("VST_CONVT_PHASES", "1") != "0"
+# split-bf16 forward kernel (ops.convT3s2_fwd).
+CONVT_PHASES = True
 
 
 def _ikf(m):
@@ -491,44 +492,30 @@ class ResnetGenerator(FlatNet):
 
 # The IN backward writes the weight gradient's dy operand image itself (bf16 planes,
 # ops.instnorm_act_bwd(planes=True)) when that weight gradient runs on the x6 split-bf16 kernel;
-# VST_IN_PLANES=0 keeps the separate plane copy inside vst_conv2d_wgrad.
-IN_PLANES = os.environ.get("VST_IN_PLANES", "1") != "0"
+# False keeps the separate plane copy inside vst_conv2d_wgrad.
+IN_PLANES = True
 # The forward IN apply writes the padded channel-major image of its output that the x6 weight
-# gradient of the consuming conv reads (ops.instnorm_act_fwd(cp=...)); VST_IN_XT=0 makes that copy
+# gradient of the consuming conv reads (ops.instnorm_act_fwd(cp=...)); False makes that copy
 # inside vst_conv2d_wgrad instead.
-IN_XT = os.environ.get("VST_IN_XT", "1") != "0"
-# The reflect fold of a stride-1 data gradient and the IN backward partials of the layer below it as
-# one pass (ops.conv2d_dgrad_s1_in, VST_FOLD_IN=1).  Off by default: the fused pass is bit-identical
-# but its per-thread fp64 reduction chains run on the fold's (nsplit x N)-block geometry, slower
-# than the elementwise fold + separate partials (C2 step A/B: 65.43 vs 65.24 ms; planes-only 64.80).
-FOLD_IN = os.environ.get("VST_FOLD_IN", "0") == "1"
-# The ReflectionPad2d(1) data gradient's border add taken by the IN backward partial pass of the layer
-# below (ops.conv2d_dgrad_refl_in: one read of g and one launch fewer per ResnetBlock data gradient,
-# results bit-identical).  Opt-in (VST_DGRAD_IN=1): slower in the step (C2 A/B, same box: 65.6 vs
-# 64.75 ms) — the per-pixel border test and the target pixels' slab loads stall the partial pass's
-# load stream more than the separate border pass costs.
-DGRAD_IN = os.environ.get("VST_DGRAD_IN", "0") == "1"
+IN_XT = True
 # The IN backward partials of the layer below taken by the ResnetBlock data gradient's own GEMM epilogue and
-# border add (ops.conv2d_dgrad_refl_in(epi=True): no partial pass reading g and the IN input again).
-# C2 step A/B, same box: 53.52-53.57 vs 53.79-53.80 ms (profiles/r05h_dgrad_epi_step_ab.jsonl); VST_DGRAD_EPI=0
-# restores the separate partial pass.
-DGRAD_EPI = os.environ.get("VST_DGRAD_EPI", "1") != "0"
+# border add (ops.conv2d_dgrad_refl_in: no partial pass reading g and the IN input again).
+# C2 step A/B, same box: 53.52-53.57 vs 53.79-53.80 ms (profiles/r05h_dgrad_epi_step_ab.jsonl); False
+# restores the separate data gradient + IN-backward partial pass.  (Round 6 deleted the two measured-slower
+# fusions of that step: the border add in the partial pass, +0.85 ms, and the fold + partials pass.)
+DGRAD_EPI = True
 # The discriminator head (1 real output channel of 4) runs the one-channel skinny forward
-# (ops.conv2d_fwd(co_real=1)); VST_D_CO1=0 keeps the 4-channel sums.
-D_CO1 = os.environ.get("VST_D_CO1", "1") != "0"
+# (ops.conv2d_fwd(co_real=1)); False keeps the 4-channel sums.
+D_CO1 = True
 # The first PatchGAN layer's data gradient (onto the 4-channel image) as ONE parity-class gather launch
-# (ops.conv2d_tfwd -> skinny.hip MODE 1) instead of four 2x2 phase convs + the interleave pass;
-# VST_D0_TFWD=0 keeps the phases.
-D0_TFWD = os.environ.get("VST_D0_TFWD", "1") != "0"
-# The ResnetBlock convs' A operands pre-split by their producers (the IN passes write the NHWC bf16 planes; the x6
-# 256x128 forwards and data gradients stage A from them by LDS-DMA, results bit-identical).
-# Forward (VST_APRE=1: the planes beside the fp32 activation, which the residual / fallback readers keep): +0.73 ms in
-# the C2 step A/B (profiles/r05l_apre_step_ab.jsonl; in-step the forward GEMM gains ~1 %, the IN apply pays 6 B/elem).
-APRE = os.environ.get("VST_APRE", "0") == "1"
-# Backward (default; VST_APRE_BWD=0 restores the fp32 images): the ResnetBlock chain's data-gradient inputs as planes
-# ONLY (the IN backward writes no fp32 image: their weight gradients read the channel-major planes, the border GEMM
-# puts the values back together): C2 step A/B 53.81-53.82 vs 53.99-54.05 ms (profiles/r05n_apre_bwd_step_ab.jsonl).
-APRE_BWD = os.environ.get("VST_APRE_BWD", "1") != "0"
+# (ops.conv2d_tfwd -> skinny.hip MODE 1) instead of four 2x2 phase convs + the interleave pass.
+D0_TFWD = True
+# The ResnetBlock chain's data-gradient inputs as pre-split planes ONLY (the IN backward writes the NHWC bf16
+# planes and no fp32 image; the data gradient's 256x128 GEMM stages A from them by LDS-DMA, its weight gradient
+# reads the channel-major planes, the border GEMM puts the values back together): C2 step A/B 53.81-53.82 vs
+# 53.99-54.05 ms (profiles/r05n_apre_bwd_step_ab.jsonl).  (The forward half — planes written beside the fp32
+# activation — measured +0.73 ms in round 5, profiles/r05l_apre_step_ab.jsonl, and was deleted in round 6.)
+APRE_BWD = True
 _WPLAN_BF = 2  # ops.WPLAN_NAMES: copies + conv_wgrad_bf_k
 
 
@@ -572,20 +559,18 @@ class _GeneratorFn(torch.autograd.Function):
             return (1, mode, st) if _wgrad_on_bf(N_, H_, W_, C_, Ho_, Wo_, cpad(cout), 3, st,
                                                  ops.get_conv_math()) else None
 
-        def in_act(y, s, act, cp, residual=None, apre=False):
+        def in_act(y, s, act, cp, residual=None):
             if cp is None:
-                return ops.instnorm_act_fwd(y, s, act, residual=residual, apre=apre), None
+                return ops.instnorm_act_fwd(y, s, act, residual=residual), None
             if cp[0] == "planes":
                 return ops.instnorm_act_fwd(y, s, act, residual=residual, xpl=cp[1])
-            return ops.instnorm_act_fwd(y, s, act, residual=residual, cp=cp, apre=apre)
-
-        rb_in = (4 * ngf, 1, "reflect")  # the ResnetBlock convs' geometry (their inputs carry pre-split planes)
+            return ops.instnorm_act_fwd(y, s, act, residual=residual, cp=cp)
 
         def conv_in_relu(inp, key, cout, R, st, pad, mode, nxt=None):
             """conv + IN + ReLU; nxt = (cout, stride, pad mode) of the 3x3 conv consuming the output"""
             kc, _, b = P[key]
             y, s = ops.conv2d_fwd_in(inp, kc, b, cpad(cout), R, R, st, pad, mode, role=role)
-            a, at = in_act(y, s, "relu", cp_for(y, *nxt) if nxt else None, apre=APRE and nxt == rb_in)
+            a, at = in_act(y, s, "relu", cp_for(y, *nxt) if nxt else None)
             sv["xt"][id(a)] = at
             return y, s, a
 
@@ -612,17 +597,9 @@ class _GeneratorFn(torch.autograd.Function):
         h = a
         for i in range(nb):
             kc, _, b = P[f"b{i}b"]
-            if role == "infer" and ops.conv2d_fwd_in_nrm_ok(h, 4 * ngf, 3, 1, "reflect", role):
-                # inference: the block's IN + ReLU applied inside the second conv's A staging
-                ka, _, ba = P[f"b{i}a"]
-                t, s1 = ops.conv2d_fwd_in(h, ka, ba, 4 * ngf, 3, 3, 1, 1, "reflect", role=role)
-                v, s2 = ops.conv2d_fwd_in_nrm(t, s1, kc, b, 4 * ngf, 3, 1, "reflect", role=role)
-                uu = None
-            else:
-                t, s1, uu = conv_in_relu(h, f"b{i}a", 4 * ngf, 3, 1, 1, "reflect", nxt=(4 * ngf, 1, "reflect"))
-                v, s2 = ops.conv2d_fwd_in(uu, kc, b, 4 * ngf, 3, 3, 1, 1, "reflect", role=role)
-            hn, hnt = in_act(v, s2, "none", cp_for(v, 4 * ngf, 1, "reflect") if i + 1 < nb else None, residual=h,
-                             apre=APRE and i + 1 < nb)
+            t, s1, uu = conv_in_relu(h, f"b{i}a", 4 * ngf, 3, 1, 1, "reflect", nxt=(4 * ngf, 1, "reflect"))
+            v, s2 = ops.conv2d_fwd_in(uu, kc, b, 4 * ngf, 3, 3, 1, 1, "reflect", role=role)
+            hn, hnt = in_act(v, s2, "none", cp_for(v, 4 * ngf, 1, "reflect") if i + 1 < nb else None, residual=h)
             sv["xt"][id(hn)] = hnt
             sv[f"b{i}"] = (h, t, s1, uu, v, s2)
             h = hn
@@ -759,10 +736,9 @@ class _GeneratorFn(torch.autograd.Function):
         def dgrad_reflect_in(dy, key, H, W, y_in, s_in, act, mod, x_w, R_w, st_w, addend=None, apre=False):
             """dgrad_reflect (3x3, pad 1) + the IN(+act) backward of the layer below it (y_in, s_in;
             mod = the conv feeding that IN; x_w / R_w / st_w = that conv's weight-gradient input
-            and geometry) -> (g, dy_in, dy_in planes or None).  On the border route the border add
-            rides in the IN backward partial pass (ops.conv2d_dgrad_refl_in); with VST_FOLD_IN=1 the
-            fold and the partials are one pass (ops.conv2d_dgrad_s1_in); otherwise the two steps run
-            separately."""
+            and geometry) -> (g, dy_in, dy_in planes or None).  The IN-backward partials come from the
+            data gradient's epilogue and border add (ops.conv2d_dgrad_refl_in) where it takes
+            the shape; otherwise the two steps run separately."""
             ikf = P["ikf"].get(key)
             cin_p = y_in.shape[-1]
             if DGRAD_EPI and ikf is not None and dy.shape[-1] % 8 == 0:
@@ -772,30 +748,11 @@ class _GeneratorFn(torch.autograd.Function):
                         _wgrad_on_bf(N, x_w.shape[1], x_w.shape[2], x_w.shape[3], y_in.shape[1], y_in.shape[2],
                                      cin_p, R_w, st_w, ops.get_conv_math()))
                 r = ops.conv2d_dgrad_refl_in(dy, ikf, H, W, cin_p, y_in, s_in, act, 0.0, addend=addend, db=db,
-                                             planes=want, epi=True, apre=apre)
+                                             planes=want, apre=apre)
                 if r is not None:
                     return r if want else (r[0], r[1], None)
             if getattr(dy, "vst_planes_only", False):
                 raise RuntimeError("dgrad_reflect_in: a planes-only gradient reached a route that reads fp32")
-            if DGRAD_IN and not FOLD_IN and ikf is not None and dy.shape[-1] % 8 == 0:
-                db = mod.bias.grad if (train_w and mod.bias is not None) else None
-                N = x_w.shape[0]
-                want = (train_w and IN_PLANES and
-                        _wgrad_on_bf(N, x_w.shape[1], x_w.shape[2], x_w.shape[3], y_in.shape[1], y_in.shape[2],
-                                     cin_p, R_w, st_w, ops.get_conv_math()))
-                r = ops.conv2d_dgrad_refl_in(dy, ikf, H, W, cin_p, y_in, s_in, act, 0.0, addend=addend, db=db,
-                                             planes=want)
-                if r is not None:
-                    return r if want else (r[0], r[1], None)
-            if FOLD_IN and ikf is not None and dy.shape[-1] % 8 == 0 and ikf.shape[0] == cin_p:
-                db = mod.bias.grad if (train_w and mod.bias is not None) else None
-                N = x_w.shape[0]
-                want = (train_w and IN_PLANES and
-                        _wgrad_on_bf(N, x_w.shape[1], x_w.shape[2], x_w.shape[3], y_in.shape[1], y_in.shape[2],
-                                     cin_p, R_w, st_w, ops.get_conv_math()))
-                r = ops.conv2d_dgrad_s1_in(dy, ikf, H, W, cin_p, 3, 1, y_in, s_in, act, 0.0, addend=addend,
-                                           db=db, planes=want)
-                return r if want else (r[0], r[1], None)
             g = dgrad_reflect(dy, key, cin_p, 3, 1, H, W, addend=addend)
             dyi, pl = in_bwd(g, y_in, s_in, act, mod, x_w, R_w, st_w)
             return g, dyi, pl
@@ -808,7 +765,7 @@ class _GeneratorFn(torch.autograd.Function):
         # planes-only data-gradient inputs (APRE_BWD) only where every ResnetBlock data gradient takes the epi route
         # (it reads the planes; the other routes read the fp32 image, which is then not written)
         apre_bwd = False
-        if APRE_BWD and nb and train_w and DGRAD_EPI and not DGRAD_IN and not FOLD_IN:
+        if APRE_BWD and nb and train_w and DGRAD_EPI:
             Nb, Hb, Wb, Cb = sv["b0"][0].shape
             apre_bwd = (Cb % 8 == 0 and all(P["ikf"].get(f"b{i}{c}") is not None for i in range(nb) for c in "ab")
                         and ops.dgrad_refl_epi_ok(Nb, Hb, Wb, Cb, Cb))

@@ -190,8 +190,10 @@ def _probe_end(h):
         p.events.append(ev)
 
 
-# Split-K tails of x6 forward grids (vst_conv2d_fwd_ws); VST_FWD_SPLITK=0 keeps the small-tile tails.
-FWD_SPLITK = os.environ.get("VST_FWD_SPLITK", "1") != "0"
+# Split-K tails of x6 forward grids (vst_conv2d_fwd_ws); False keeps the small-tile tails.  (Module flags
+# like this one are route selectors the tests flip in-process to compare routes; they are not read from the
+# environment.)
+FWD_SPLITK = True
 _fws_cache = {}
 
 
@@ -258,56 +260,14 @@ def conv2d_fwd_in(x, wp, bias, cop, R, S, stride, pad, pad_mode="zero", role="fw
     m = _math(role)
     ws, nb = _fwd_ws(N, H, W, Cx, cop, R, S, stride, pad, m, x.device) if S == R else (None, 0)
     h = _probe_begin("fwd", (N, H, W, Cx, cop, R, stride, pad, pad_mode)) if _probes else None
-    apl = getattr(x, "vst_apl", None)
-    if apl is not None:  # x's pre-split planes (instnorm_act_fwd(apre=True)): the A operand by LDS-DMA
-        _call("vst_conv2d_fwd_apre_ws", _p(x), _p(apl), _p(wp), _p(getattr(wp, "vst_split", None)), _p(bias), _p(y),
-              N, H, W, Cx, cop, R, S, stride, pad, PAD[pad_mode], ACT["none"], 0.0, m, _p(part),
-              ctypes.addressof(nsplit), _p(ws), nb, _stream())
-    else:
-        _call("vst_conv2d_fwd_ws", _p(x), _p(wp), _p(getattr(wp, "vst_split", None)), _p(bias), _p(y), N, H, W, Cx,
-              cop, R, S, stride, pad, PAD[pad_mode], ACT["none"], 0.0, m, _p(part),
-              ctypes.addressof(nsplit), _p(ws), nb, _stream())
+    _call("vst_conv2d_fwd_ws", _p(x), _p(wp), _p(getattr(wp, "vst_split", None)), _p(bias), _p(y), N, H, W, Cx,
+          cop, R, S, stride, pad, PAD[pad_mode], ACT["none"], 0.0, m, _p(part),
+          ctypes.addressof(nsplit), _p(ws), nb, _stream())
     _probe_end(h)
     if nsplit.value == 0:
         return y, instnorm_stats(y)
     stats = torch.empty((N, cop, 2), device=x.device)
     _call("vst_instnorm_finalize", _p(part), _p(stats), N, hw, cop, nsplit.value, IN_EPS, _stream())
-    return y, stats
-
-
-# The ResnetBlock's second conv over relu(IN(t)) normalising in its A staging (vst_conv2d_fwd_nrm_ws)
-# instead of an IN + ReLU apply pass that writes the activation (inference: the activation has no
-# other reader).  Opt-in (VST_NRM_FWD=1): measured slower (same box, alternating runs) — B=1 256^2
-# 1.24 vs 1.18-1.20 ms, B=16 9.04-9.09 vs 8.57-8.61 ms, 436x1024 equal: the stage's four statistics
-# loads and 32 VALU cost the 256x128 main loop more than the 4-8 us apply pass they remove.
-NRM_FWD = os.environ.get("VST_NRM_FWD", "0") == "1"
-
-
-def conv2d_fwd_in_nrm_ok(y_in, cop, R, pad, pad_mode="reflect", role="infer"):
-    N, H, W, C = y_in.shape
-    return NRM_FWD and bool(lib().vst_conv2d_fwd_nrm_ok(N, H, W, C, cop, R, R, 1, pad, PAD[pad_mode], _math(role)))
-
-
-def conv2d_fwd_in_nrm(y_in, stats_in, wp, bias, cop, R, pad, pad_mode="reflect", role="infer"):
-    """conv2d_fwd_in (stride 1) over relu(IN(y_in)), stats_in = y_in's IN statistics: the IN + ReLU apply
-    runs inside the conv's A staging (vst_conv2d_fwd_nrm_ws) -> (y, stats of y)."""
-    import ctypes
-    _dev_check(y_in, stats_in, wp, bias)
-    N, H, W, Cx = y_in.shape
-    Ho, Wo = H + 2 * pad - R + 1, W + 2 * pad - R + 1
-    y = torch.empty((N, Ho, Wo, cop), device=y_in.device)
-    part = torch.empty((N * (Ho * Wo // 32) * cop * 2,), device=y_in.device, dtype=torch.float64)
-    nsplit = ctypes.c_int(0)
-    m = _math(role)
-    nb = int(lib().vst_conv2d_fwd_ws_bytes(N, H, W, Cx, cop, R, R, 1, pad, m))
-    ws = torch.empty((nb + 3) // 4, device=y_in.device) if nb else None
-    h = _probe_begin("fwd", (N, H, W, Cx, cop, R, 1, pad, pad_mode)) if _probes else None
-    _call("vst_conv2d_fwd_nrm_ws", _p(y_in), _p(stats_in), _p(getattr(wp, "vst_split", None)), _p(bias), _p(y), N, H,
-          W, Cx, cop, R, R, 1, pad, PAD[pad_mode], ACT["none"], 0.0, m, _p(part), ctypes.addressof(nsplit), _p(ws), nb,
-          _stream())
-    _probe_end(h)
-    stats = torch.empty((N, cop, 2), device=y_in.device)
-    _call("vst_instnorm_finalize", _p(part), _p(stats), N, Ho * Wo, cop, nsplit.value, IN_EPS, _stream())
     return y, stats
 
 
@@ -476,8 +436,8 @@ def channel_sum(x, db, cl, accumulate=True):
 
 
 # ReflectionPad2d(1) + 3x3 data gradients as the interior conv + border GEMM (vst_conv2d_dgrad_refl)
-# instead of the conv over the zero-padded frame + reflect fold; VST_DGRAD_BORDER=0 keeps the fold.
-DGRAD_BORDER = os.environ.get("VST_DGRAD_BORDER", "1") != "0"
+# instead of the conv over the zero-padded frame + reflect fold; False keeps the fold.
+DGRAD_BORDER = True
 
 
 def conv2d_dgrad_s1(dy, ikf, H, W, cx, R, pad, pad_mode="zero", addend=None, role="bwd"):
@@ -514,8 +474,8 @@ def conv2d_dgrad_s1(dy, ikf, H, W, cx, R, pad, pad_mode="zero", addend=None, rol
 
 # The data gradient of ReflectionPad2d(p) + Conv2d(C -> 4, 7x7) (the generator's last layer) as the
 # zero-pad-p conv of dy on the direct 4-channel kernel + the reflect-fold frame (vst_c4_dgrad_frame),
-# instead of the conv over the (H+2p) x (W+2p) padded frame + reflect_fold.  VST_C4_DGRAD=0: that route.
-C4_DGRAD = os.environ.get("VST_C4_DGRAD", "1") != "0"
+# instead of the conv over the (H+2p) x (W+2p) padded frame + reflect_fold.  False: that route.
+C4_DGRAD = True
 
 
 def c4_dgrad_reflect_ok(dy, cx, R, pad, role="bwd"):
@@ -535,40 +495,15 @@ def c4_dgrad_reflect(dy, ikf, H, W, cx, R, pad, role="bwd"):
     return dx
 
 
-def conv2d_dgrad_s1_in(dy, ikf, H, W, cx, R, pad, y_in, stats, act="relu", slope=0.0, addend=None, db=None,
-                       accumulate_db=True, planes=False, role="bwd"):
-    """conv2d_dgrad_s1 (reflect) whose fold also runs the InstanceNorm(+act) backward of the layer
-    below (vst_reflect_fold_instnorm_bwd): returns (g, dy_in[, dy_in_planes]) where g = the folded
-    data gradient (+ addend) and dy_in = instnorm_act_bwd(g, y_in, stats, act)."""
-    _dev_check(dy, ikf, addend, y_in, stats)
-    dxp = conv2d_fwd(dy, ikf, None, cx, R, R, 1, R - 1, "zero", role=role)
-    N = dy.shape[0]
-    C = y_in.shape[-1]
-    if cx != C:
-        raise ValueError("conv2d_dgrad_s1_in: data-gradient channels %d != IN channels %d" % (cx, C))
-    g = torch.empty((N, H, W, C), device=dy.device)
-    dyi = torch.empty_like(g)
-    ws = _in_ws(N, H * W, C, dy.device)
-    pl, ldp = None, 0
-    if planes:
-        ldp = lib().vst_cp_ld(N * H * W)
-        pl = torch.empty((3, C, ldp), device=dy.device, dtype=torch.bfloat16)
-    _call("vst_reflect_fold_instnorm_bwd", _p(dxp), _p(addend), _p(g), _p(y_in), _p(stats), _p(dyi), _p(db), _p(ws),
-          N, H, W, C, pad, ACT[act], float(slope), 1 if accumulate_db else 0, _p(pl), ldp, _stream())
-    return (g, dyi, pl) if planes else (g, dyi)
-
-
 def conv2d_dgrad_refl_in(dy, ikf, H, W, cx, y_in, stats, act="relu", slope=0.0, addend=None, db=None,
-                         accumulate_db=True, planes=False, role="bwd", epi=False, apre=False):
+                         accumulate_db=True, planes=False, role="bwd", apre=False):
     """ReflectionPad2d(1) + 3x3 data gradient (conv2d_dgrad_s1's interior conv + border GEMM) fused with
-    the InstanceNorm(+act) backward of the layer below it (vst_conv2d_dgrad_refl_in): returns (g, dy_in[,
-    dy_in_planes]) — g = the data gradient (+ addend), dy_in = instnorm_act_bwd(g, y_in, stats, act) —
-    or None when the fused route does not support the shape / arithmetic.
-    epi: the IN partials taken by the data gradient's GEMM epilogue and border add instead
-    (vst_conv2d_dgrad_refl_in_epi: no partial pass; x6 arithmetic, H W % 32 == 0); there dy's pre-split planes
-    (``dy.vst_apl``) are its A operand when present, and apre (with planes) writes dy_in as planes only."""
-    if getattr(dy, "vst_planes_only", False) and not epi:
-        raise ValueError("conv2d_dgrad_refl_in: dy has planes only (instnorm_act_bwd(apre=True)): use epi=True")
+    the InstanceNorm(+act) backward of the layer below it: returns (g, dy_in[, dy_in_planes]) — g = the
+    data gradient (+ addend), dy_in = instnorm_act_bwd(g, y_in, stats, act) — or None when the fused route
+    does not support the shape / arithmetic.  The IN partials are taken by the data gradient's GEMM
+    epilogue and border add (vst_conv2d_dgrad_refl_epi_part: no partial pass; x6 arithmetic, H W % 32 ==
+    0); dy's pre-split planes (``dy.vst_apl``) are its A operand when present, and apre (with planes)
+    writes dy_in as planes only."""
     _dev_check(dy, ikf, addend, y_in, stats)
     if not DGRAD_BORDER or getattr(ikf, "vst_split", None) is None:
         return None
@@ -577,50 +512,30 @@ def conv2d_dgrad_refl_in(dy, ikf, H, W, cx, y_in, stats, act="relu", slope=0.0, 
     if (Hy, Wy) != (H, W) or cx != C:
         return None
     m = _math(role)
-    if epi:
-        nb = int(lib().vst_conv2d_dgrad_refl_in_epi_ws_bytes(N, H, W, Cy, C, m))
-        if not nb:
-            return None
-        g = torch.empty((N, H, W, C), device=dy.device)
-        dyi = torch.empty_like(g)
-        ws = torch.empty((nb + 3) // 4, device=dy.device)
-        pl, ldp = None, 0
-        if planes:
-            ldp = lib().vst_cp_ld(N * H * W)
-            pl = torch.empty((3, C, ldp), device=dy.device, dtype=torch.bfloat16)
-        if planes and apre:  # dy_in as planes only (instnorm_act_bwd(apre=True))
-            dyi.vst_apl = torch.empty((3, dyi.numel()), device=dy.device, dtype=torch.bfloat16)
-            dyi.vst_planes_only = True
-        h = _probe_begin("dgrad", (N, H, W, Cy, C, 3, 1, 1, "reflect")) if _probes else None
-        _call("vst_conv2d_dgrad_refl_epi_part", _p(dy), _p(getattr(dy, "vst_apl", None)), _p(ikf.vst_split),
-              _p(addend), _p(g), _p(y_in), _p(stats), _p(ws), nb, N, H, W, Cy, C, ACT[act], float(slope), m, _stream())
-        _probe_end(h)
-        _call("vst_instnorm_act_bwd_epi_tail", _p(g), _p(y_in), _p(stats), _p(dyi), _p(db), _p(ws), N, H, W, C, ACT[act],
-              float(slope), 1 if accumulate_db else 0, _p(pl), ldp, _p(getattr(dyi, "vst_apl", None)), _stream())
-        return (g, dyi, pl) if planes else (g, dyi)
-    nbd = int(lib().vst_conv2d_dgrad_refl_ws_bytes(N, H, W, Cy, C, m))
-    if not nbd or not int(lib().vst_conv2d_dgrad_refl_in_ws_bytes(N, H, W, Cy, C, m)):
+    nb = int(lib().vst_conv2d_dgrad_refl_in_epi_ws_bytes(N, H, W, Cy, C, m))
+    if not nb:
         return None
     g = torch.empty((N, H, W, C), device=dy.device)
     dyi = torch.empty_like(g)
-    dws = torch.empty((nbd + 3) // 4, device=dy.device)
-    iws = _in_ws(N, H * W, C, dy.device)
+    ws = torch.empty((nb + 3) // 4, device=dy.device)
     pl, ldp = None, 0
     if planes:
         ldp = lib().vst_cp_ld(N * H * W)
         pl = torch.empty((3, C, ldp), device=dy.device, dtype=torch.bfloat16)
-    # two calls (vst_conv2d_dgrad_refl_in's halves) so the data gradient alone carries the launch probe
+    if planes and apre:  # dy_in as planes only (instnorm_act_bwd(apre=True))
+        dyi.vst_apl = torch.empty((3, dyi.numel()), device=dy.device, dtype=torch.bfloat16)
+        dyi.vst_planes_only = True
     h = _probe_begin("dgrad", (N, H, W, Cy, C, 3, 1, 1, "reflect")) if _probes else None
-    _call("vst_conv2d_dgrad_refl_slabs", _p(dy), _p(ikf.vst_split), _p(addend), _p(g), _p(dws), nbd, N, H, W, Cy, C, m,
-          _stream())
+    _call("vst_conv2d_dgrad_refl_epi_part", _p(dy), _p(getattr(dy, "vst_apl", None)), _p(ikf.vst_split),
+          _p(addend), _p(g), _p(y_in), _p(stats), _p(ws), nb, N, H, W, Cy, C, ACT[act], float(slope), m, _stream())
     _probe_end(h)
-    _call("vst_instnorm_act_bwd_refl_border", _p(g), _p(y_in), _p(stats), _p(dyi), _p(db), _p(iws), _p(dws), N, H, W,
-          Cy, C, ACT[act], float(slope), 1 if accumulate_db else 0, _p(pl), ldp, m, _stream())
+    _call("vst_instnorm_act_bwd_epi_tail", _p(g), _p(y_in), _p(stats), _p(dyi), _p(db), _p(ws), N, H, W, C, ACT[act],
+          float(slope), 1 if accumulate_db else 0, _p(pl), ldp, _p(getattr(dyi, "vst_apl", None)), _stream())
     return (g, dyi, pl) if planes else (g, dyi)
 
 
 def dgrad_refl_epi_ok(N, H, W, Cy, Cx, role="bwd"):
-    """Does conv2d_dgrad_refl_in(epi=True) take this shape (vst_conv2d_dgrad_refl_in_epi_ws_bytes > 0)?"""
+    """Does conv2d_dgrad_refl_in take this shape (vst_conv2d_dgrad_refl_in_epi_ws_bytes > 0)?"""
     return DGRAD_BORDER and int(lib().vst_conv2d_dgrad_refl_in_epi_ws_bytes(N, H, W, Cy, Cx, _math(role))) > 0
 
 
@@ -648,14 +563,12 @@ def instnorm_stats(y):
     return stats
 
 
-def instnorm_act_fwd(y, stats, act="relu", slope=0.0, residual=None, cp=None, xpl=None, apre=False):
+def instnorm_act_fwd(y, stats, act="relu", slope=0.0, residual=None, cp=None, xpl=None):
     """a = act(IN(y)) (+ residual).  cp = (pad, pad_mode, stride) of the conv that consumes a:
     returns (a, a_t) where a_t is a's padded channel-major image for that conv's x6 weight gradient
     (vst_instnorm_act_fwd_cp; conv2d_wgrad(x_t=a_t)).  xpl = (pad, pad_mode, wx): returns (a, planes),
     a's padded image as the bf16 planes [3][C][ld] with wx zero columns per row
-    (vst_instnorm_act_fwd_planes; tap_conv_wgrad_swap(x_pl=planes)).
-    apre (with cp or alone): a also carries its NHWC bf16 planes as ``a.vst_apl`` (vst_instnorm_act_fwd_cp_apre /
-    vst_instnorm_act_fwd_apre), the pre-split A operand conv2d_fwd_in takes."""
+    (vst_instnorm_act_fwd_planes; tap_conv_wgrad_swap(x_pl=planes))."""
     _dev_check(y, stats, residual)
     N, H, W, C = y.shape
     a = torch.empty_like(y)
@@ -669,19 +582,9 @@ def instnorm_act_fwd(y, stats, act="relu", slope=0.0, residual=None, cp=None, xp
     if cp is not None:
         pad, mode, st = cp
         at = torch.empty((C, lib().vst_cp_ld(N * (H + 2 * pad) * (W + 2 * pad))), device=y.device)
-        if apre:
-            a.vst_apl = torch.empty((3, y.numel()), device=y.device, dtype=torch.bfloat16)
-            _call("vst_instnorm_act_fwd_cp_apre", _p(y), _p(stats), _p(residual), _p(a), _p(at), _p(a.vst_apl), N, H,
-                  W, C, ACT[act], float(slope), pad, PAD[mode], st, _stream())
-            return a, at
         _call("vst_instnorm_act_fwd_cp", _p(y), _p(stats), _p(residual), _p(a), _p(at), N, H, W, C, ACT[act],
               float(slope), pad, PAD[mode], st, _stream())
         return a, at
-    if apre:
-        a.vst_apl = torch.empty((3, y.numel()), device=y.device, dtype=torch.bfloat16)
-        _call("vst_instnorm_act_fwd_apre", _p(y), _p(stats), _p(residual), _p(a), _p(a.vst_apl), N, H * W, C, ACT[act],
-              float(slope), _stream())
-        return a
     _call("vst_instnorm_act_fwd", _p(y), _p(stats), _p(residual), _p(a), N, H * W, C, ACT[act],
           float(slope), _stream())
     return a
@@ -692,7 +595,7 @@ def instnorm_act_bwd(ga, y, stats, act="relu", slope=0.0, db=None, accumulate_db
     planes=True: returns (dy, dy_planes) — the apply pass also writes dy's three bf16 planes
     [3][C][vst_cp_ld(N*H*W)], the x6 weight gradient's operand image (conv2d_wgrad(dy_planes=...)).
     apre (with planes): dy is written ONLY as its NHWC bf16 planes ``dy.vst_apl`` (the pre-split A operand of the data
-    gradient that consumes it, conv2d_dgrad_refl_in(epi=True)) — dy's fp32 values are NOT written (dy.vst_planes_only):
+    gradient that consumes it, conv2d_dgrad_refl_in) — dy's fp32 values are NOT written (dy.vst_planes_only):
     its readers must take the planes (the weight gradient: dy_planes; the data gradient: vst_apl)."""
     _dev_check(ga, y, stats)
     N, H, W, C = y.shape
@@ -1069,8 +972,8 @@ def u8_image_to_nhwc4(x):
 
 # ----------------------------------------------------------------------------------- RAFT
 # conv2d_fwd_hw with the split-K plans of the square convs' workspace path (RAFT's SepConvGRU convs);
-# VST_FWD_HW_SPLITK=0: the one-launch plans
-FWD_HW_SPLITK = os.environ.get("VST_FWD_HW_SPLITK", "1") != "0"
+# False: the one-launch plans
+FWD_HW_SPLITK = True
 
 
 def conv2d_fwd_hw(x, wp, bias, cop, R, S, stride, pad_h, pad_w, act="none", role="fwd"):
@@ -1200,13 +1103,13 @@ def loss_masked_l1_bwd(a, b, mask, gout, scale, cl):
 # 7x7) in chunks of images sized for the 256 MB Infinity Cache, each chunk overwriting one buffer.
 # Off by default: the C2 step A/B measured 63.15-63.27 ms with 128 MB chunks, 64.12 with 64 MB,
 # 62.85-62.87 in one pass (the smaller GEMM launches lose more than the cache hits save).
-TAP_CHUNK_BYTES = int(float(os.environ.get("VST_TAP_CHUNK_MB", "0")) * (1 << 20))
+TAP_CHUNK_BYTES = 0
 # tap_conv_wgrad: the folded dy written as the x6 wgrad's bf16 planes (vst_tapfold_planes);
-# VST_TAP_PLANES=0 writes the fp32 D and lets the wgrad copy it into planes.
-TAP_PLANES = os.environ.get("VST_TAP_PLANES", "1") != "0"
-# The generator's last-layer weight gradient as the swapped GEMM (tap_conv_wgrad_swap); VST_TAP_SWAP=0:
+# False writes the fp32 D and lets the wgrad copy it into planes.
+TAP_PLANES = True
+# The generator's last-layer weight gradient as the swapped GEMM (tap_conv_wgrad_swap); False:
 # the R x 1 form (tap_conv_wgrad_h).
-TAP_SWAP = os.environ.get("VST_TAP_SWAP", "1") != "0"
+TAP_SWAP = True
 
 
 def _tap_chunks(N, per_image_bytes):
@@ -1430,8 +1333,8 @@ def conv4s2_dgrad_phase_packs(w):
     return packs
 
 
-# the four phases in one launch stored interleaved (vst_conv4s2_dgrad); VST_C4S2_GROUPED=0: images + interleave
-C4S2_GROUPED = os.environ.get("VST_C4S2_GROUPED", "1") != "0"
+# the four phases in one launch stored interleaved (vst_conv4s2_dgrad); False: images + interleave
+C4S2_GROUPED = True
 
 
 def conv4s2_dgrad(dy, packs, cop, role="bwd"):
@@ -1458,10 +1361,10 @@ def conv4s2_dgrad(dy, packs, cop, role="bwd"):
 
 
 # ConvTranspose2d phase convs storing straight into the interleaved output (vst_conv2d_fwd_phase)
-# instead of four phase images + vst_interleave_phases; VST_CONVT_DIRECT=0 keeps the latter.
-CONVT_DIRECT = os.environ.get("VST_CONVT_DIRECT", "1") != "0"
-# ... and all four in one launch (vst_conv2d_convT_s2) where Cx % 32 == 0; VST_CONVT_GROUPED=0: one per phase.
-CONVT_GROUPED = os.environ.get("VST_CONVT_GROUPED", "1") != "0"
+# instead of four phase images + vst_interleave_phases; False keeps the latter.
+CONVT_DIRECT = True
+# ... and all four in one launch (vst_conv2d_convT_s2) where Cx % 32 == 0; False: one per phase.
+CONVT_GROUPED = True
 
 
 def convT3s2_fwd(x, packs, bias, cop, act="none", role="fwd"):
@@ -1490,12 +1393,16 @@ def convT3s2_fwd(x, packs, bias, cop, act="none", role="fwd"):
     return y
 
 
-_ROUTE_FLAGS = ("FWD_SPLITK", "NRM_FWD", "DGRAD_BORDER", "C4_DGRAD", "TAP_CHUNK_BYTES", "TAP_PLANES", "TAP_SWAP",
+_ROUTE_FLAGS = ("FWD_SPLITK", "FWD_HW_SPLITK", "DGRAD_BORDER", "C4_DGRAD", "TAP_CHUNK_BYTES", "TAP_PLANES", "TAP_SWAP",
                 "C4S2_GROUPED", "CONVT_DIRECT", "CONVT_GROUPED")
+# the forward-route switches of networks.py (the generator's / discriminator's layer routes)
+_NET_ROUTE_FLAGS = ("C8_EDGES", "C4_FWD", "DGRAD_AS_FPROP", "TAP_LAST", "TAP_H", "CONVT_PHASES", "IN_XT", "D_CO1")
 
 
 def route_flags():
     """The module-level route switches that change which kernels a forward launches (tests and tools
     flip them in-process): part of FlatNet.graphed_forward's capture key."""
+    import sys
     g = globals()
-    return tuple(g[n] for n in _ROUTE_FLAGS)
+    net = sys.modules.get(__name__.rsplit(".", 1)[0] + ".networks")
+    return tuple(g[n] for n in _ROUTE_FLAGS) + (tuple(getattr(net, n) for n in _NET_ROUTE_FLAGS) if net else ())

@@ -53,8 +53,8 @@ def _features(cfg):
 
 
 # VGG data gradients (3x3, zero pad 1) as forward convs over the rotated taps on the split-bf16 kernel (the
-# generator's route) instead of the transposed conv on the fp32-operand kernel; VST_VGG_DGRAD_FPROP=0 keeps the latter
-VGG_DGRAD_FPROP = os.environ.get("VST_VGG_DGRAD_FPROP", "1") != "0"
+# generator's route) instead of the transposed conv on the fp32-operand kernel; False keeps the latter
+VGG_DGRAD_FPROP = True
 
 
 class _VGG(FlatNet):

@@ -145,8 +145,8 @@ class BasicUpdateBlock(nn.Module):
 # packs
 ###############################################################################
 # The correlation features' channel stride: 4 levels x 81 = 324 padded to 328, so that convc1 (1x1, 324 -> 256) runs
-# on the split-bf16 kernel (K in 8-channel chunks) instead of the fp32-operand one; VST_RAFT_CS8=0 keeps 324
-_CORR_CS = 328 if __import__("os").environ.get("VST_RAFT_CS8", "1") != "0" else None
+# on the split-bf16 kernel (K in 8-channel chunks) instead of the fp32-operand one; False keeps 324
+_CORR_CS = 328
 
 
 def _pack(w, b, ip=None):

@@ -58,8 +58,8 @@ class _ToNCHW2(torch.autograd.Function):
 
 
 # The Conv2d(k4, s2, p1) data gradients on the four-phase kernel (ops.conv4s2_dgrad: the 2x2 phase convs in one
-# launch, stored interleaved) instead of the generic transposed-conv gather; VST_SG_PHASES=0 keeps the latter.
-SG_PHASES = __import__("os").environ.get("VST_SG_PHASES", "1") != "0"
+# launch, stored interleaved) instead of the generic transposed-conv gather; False keeps the latter.
+SG_PHASES = True
 # The gradient penalty's first-order pass (autograd.grad of D's output w.r.t. x_hat) computes only the data
 # gradients: the reference's native conv backward skips the weight / bias gradients there (the engine's
 # output mask: only x_hat's gradient is requested), which are never part of the penalty's graph.  Set by
@@ -73,7 +73,7 @@ _INPUT_GRAD_ONLY = [False]
 # layer's 134 MB three times per iteration).  Never set around autograd.grad calls.
 _ACCUM_PARAM_GRADS = [False]
 # 0: autograd accumulation, D's parameter gradients in the G step
-SG_DIRECT = __import__("os").environ.get("VST_SG_DIRECT", "1") != "0"
+SG_DIRECT = True
 
 
 def _direct(p):

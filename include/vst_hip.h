@@ -141,18 +141,6 @@ int vst_conv2d_fwd_ws(const float* x, const float* wp, const void* wsplit, const
  * C % 16 == 0.  Replaces the conv over the (H+2pad) x (W+2pad) frame + vst_reflect_fold. */
 int vst_c4_dgrad_frame(const float* dy, const float* w, float* dx, int N, int H, int W, int C, int R, int pad,
                        void* stream);
-/* A forward conv over relu(IN(x)) without the normalised activation: x = the raw output of the previous
- * conv, nst = its InstanceNorm statistics [N][Cx][2] (mean, rstd); every gathered A value enters as
- * relu((v - mean) * rstd) (in_apply's expression), inside the GEMM's A staging.  Replaces
- * vst_instnorm_act_fwd(relu) + vst_conv2d_fwd_ws on the ResnetBlock's second conv
- * (networks.py:340-367: ReflectionPad2d(1), Conv2d, InstanceNorm2d, ReLU, ReflectionPad2d(1), Conv2d).
- * vst_conv2d_fwd_nrm_ok (host-only) says whether a shape takes it: bf16x6, Cx % 32 == 0, reflect
- * padding, stride 1, Ho*Wo % 256 == 0; workspace = vst_conv2d_fwd_ws_bytes. */
-int vst_conv2d_fwd_nrm_ok(int N, int H, int W, int Cx, int Cop, int R, int S, int stride, int pad, int pad_mode,
-                          int math);
-int vst_conv2d_fwd_nrm_ws(const float* x, const float* nst, const void* wsplit, const float* bias, float* y, int N,
-                          int H, int W, int Cx, int Cop, int R, int S, int stride, int pad, int pad_mode, int act,
-                          float slope, int math, double* part, int* nsplit, float* ws, size_t ws_bytes, void* stream);
 /* Host-only: the split-K count (0 = none) vst_conv2d_fwd_ws uses for this shape and arithmetic: of
  * the tail launch, or — for grids of at most 128 256x128 tiles (PatchGAN layers, half batches) — of
  * the whole conv, run as one split-K launch + the reduction. */
@@ -315,36 +303,14 @@ int vst_instnorm_act_fwd(const float* x, const float* stats, const float* residu
 int vst_instnorm_act_bwd(const float* gy, const float* x, const float* stats, float* dx, float* db,
                          float* ws, int N, int HW, int C, int act, float slope, int accumulate_db,
                          void* stream);
-/* The reflect fold of a stride-1 data gradient over the padded frame (vst_reflect_fold: gout = addend
- * (or 0) + the mirrored sums of dxp [N][H+2p][W+2p][C]) fused with the InstanceNorm(+act) backward
- * below it: gout is written and, in the same pass, reduced into the IN backward partials, then
- * dx = IN(+act) input gradient of gout (db, planes as vst_instnorm_act_bwd_planes).  ws:
- * vst_instnorm_ws_bytes(N, H*W, C). */
-int vst_reflect_fold_instnorm_bwd(const float* dxp, const float* addend, float* gout, const float* x,
-                                  const float* stats, float* dx, float* db, float* ws, int N, int H, int W,
-                                  int C, int pad, int act, float slope, int accumulate_db, void* planes, long ldp,
-                                  void* stream);
-/* vst_conv2d_dgrad_refl fused with the InstanceNorm(+act) backward of the layer below it (the
- * ResnetBlock data gradients, networks.py:404-426, each followed by the IN backward of the block's
- * previous layer): gout = the data gradient (+ addend), x / stats = that IN's input and statistics,
- * dx = its input gradient (db, planes as vst_instnorm_act_bwd_planes).  The border GEMM's slabs are
- * added into gout by the same pass that takes the IN partials (one read of gout instead of a border
- * pass + a partial pass).  gout and dx equal vst_conv2d_dgrad_refl + vst_instnorm_act_bwd_planes bit for
- * bit.  Same support as vst_conv2d_dgrad_refl (ws_bytes query 0 = unsupported).  In two calls (the
- * data gradient can then be timed on its own): vst_conv2d_dgrad_refl_slabs (gout without the border,
- * slabs left in its ws: vst_conv2d_dgrad_refl_ws_bytes) and vst_instnorm_act_bwd_refl_border (in_ws:
- * vst_instnorm_ws_bytes(N, H*W, Cx); dgrad_ws: that same dgrad workspace). */
-size_t vst_conv2d_dgrad_refl_in_ws_bytes(int N, int H, int W, int Cy, int Cx, int math);
-int vst_conv2d_dgrad_refl_in(const float* dy, const void* wsplit, const float* addend, float* gout, const float* x,
-                             const float* stats, float* dx, float* db, float* ws, size_t ws_bytes, int N, int H,
-                             int W, int Cy, int Cx, int act, float slope, int accumulate_db, void* planes, long ldp,
-                             int math, void* stream);
-/* vst_conv2d_dgrad_refl_in with the IN backward partials taken by the data gradient itself: the interior
- * GEMM's epilogue sums {g', g' xhat, xhat} per 32-pixel group of its output tile and the border add adds
- * the correction of the pixels it changes, so the separate partial pass (a read of gout and x and a launch)
- * is gone.  gout is bit-identical to vst_conv2d_dgrad_refl; dx / planes / db to the separate passes up to
- * the fp64 summation order of the partials.  x6 arithmetic only, H*W % 32 == 0 (ws_bytes query 0 =
- * unsupported).  Same arguments as vst_conv2d_dgrad_refl_in. */
+/* vst_conv2d_dgrad_refl fused with the InstanceNorm(+act) backward of the layer below it (the ResnetBlock data
+ * gradients, networks.py:404-426, each followed by the IN backward of the block's previous layer): gout = the data
+ * gradient (+ addend), x / stats = that IN's input and statistics, dx = its input gradient (db, planes as
+ * vst_instnorm_act_bwd_planes).  The IN backward partials are taken by the data gradient itself: the interior
+ * GEMM's epilogue sums {g', g' xhat, xhat} per 32-pixel group of its output tile and the border add adds the
+ * correction of the pixels it changes, so no separate partial pass (a read of gout and x and a launch) runs.
+ * gout is bit-identical to vst_conv2d_dgrad_refl; dx / planes / db to the separate passes up to the fp64
+ * summation order of the partials.  x6 arithmetic only, H*W % 32 == 0 (ws_bytes query 0 = unsupported). */
 size_t vst_conv2d_dgrad_refl_in_epi_ws_bytes(int N, int H, int W, int Cy, int Cx, int math);
 int vst_conv2d_dgrad_refl_in_epi(const float* dy, const void* wsplit, const float* addend, float* gout,
                                  const float* x, const float* stats, float* dx, float* db, float* ws, size_t ws_bytes,
@@ -358,30 +324,13 @@ int vst_instnorm_act_bwd_epi_tail(const float* gout, const float* x, const float
                                   float* ws, int N, int H, int W, int Cx, int act, float slope, int accumulate_db,
                                   void* planes, long ldp, void* apl, void* stream);
 /* (dy_apl: dy's NHWC bf16 planes [3][N*H*W*Cy] or NULL — the interior GEMM then takes its A operand pre-split by
- * LDS-DMA (vst_conv2d_fwd_apre_ws), the border GEMM from the planes too, and dy's fp32 image is not read; apl: the
- * tail writes dx as its NHWC planes INSTEAD of fp32 (the next data gradient's dy_apl; dx is left unwritten), or NULL) */
-/* Pre-split A operands (the x6 forwards' A staged by LDS-DMA from bf16 planes instead of split in the staging): the
- * producing IN pass writes the NHWC planes [3][N*H*W*C] (hi, mid, lo: each value's RNE split) beside its fp32 output;
- * the consuming forward takes them on its x6 256x128 channel-slice plans (results bit-identical, other plans read
- * x).  Same arguments as vst_instnorm_act_fwd_cp / vst_instnorm_act_bwd_planes / vst_conv2d_fwd_ws plus the planes. */
-int vst_instnorm_act_fwd_apre(const float* x, const float* stats, const float* residual, float* y, void* apl, int N,
-                              int HW, int C, int act, float slope, void* stream);
-int vst_instnorm_act_fwd_cp_apre(const float* x, const float* stats, const float* residual, float* y, float* x_t,
-                                 void* apl, int N, int H, int W, int C, int act, float slope, int pad, int pad_mode,
-                                 int stride, void* stream);
-/* (vst_instnorm_act_bwd_planes_apre: dx is written as apl only, not as fp32) */
+ * LDS-DMA, the border GEMM from the planes too, and dy's fp32 image is not read; apl: the tail writes dx as its
+ * NHWC planes INSTEAD of fp32 (the next data gradient's dy_apl; dx is left unwritten), or NULL) */
+/* vst_instnorm_act_bwd_planes whose dx is written ONLY as its NHWC bf16 planes apl [3][N*HW*C] (hi, mid, lo: each
+ * value's RNE split) — the pre-split A operand of the ResnetBlock data gradient that consumes it (dy_apl above). */
 int vst_instnorm_act_bwd_planes_apre(const float* gy, const float* x, const float* stats, float* dx, float* db,
                                      float* ws, int N, int HW, int C, int act, float slope, int accumulate_db,
                                      void* planes, long ldp, void* apl, void* stream);
-int vst_conv2d_fwd_apre_ws(const float* x, const void* apl, const float* wp, const void* wsplit, const float* bias,
-                           float* y, int N, int H, int W, int Cx, int Cop, int R, int S, int stride, int pad,
-                           int pad_mode, int act, float slope, int math, double* part, int* nsplit, float* ws,
-                           size_t ws_bytes, void* stream);
-int vst_conv2d_dgrad_refl_slabs(const float* dy, const void* wsplit, const float* addend, float* gout, float* ws,
-                                size_t ws_bytes, int N, int H, int W, int Cy, int Cx, int math, void* stream);
-int vst_instnorm_act_bwd_refl_border(float* gout, const float* x, const float* stats, float* dx, float* db,
-                                     float* in_ws, const float* dgrad_ws, int N, int H, int W, int Cy, int Cx, int act,
-                                     float slope, int accumulate_db, void* planes, long ldp, int math, void* stream);
 /* vst_instnorm_act_bwd whose apply pass also writes dx as the three bf16 planes [3][C][ldp] (hi, mid,
  * lo; ldp >= N*HW, vst_cp_ld(N*HW)) the x6 weight gradient of the conv below consumes
  * (vst_conv2d_wgrad_pre).  planes == NULL: identical to vst_instnorm_act_bwd. */

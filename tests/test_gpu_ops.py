@@ -673,34 +673,6 @@ def _split3(x):
     return hi, mid, lo
 
 
-@pytest.mark.parametrize("N", [1, 2, 8, 12])
-def test_apre_forward_bit_identical(ops, N):
-    """Pre-split A operands (APRE): instnorm_act_fwd(cp, apre=True) writes a's NHWC planes (exactly the RNE three-way
-    split of a) beside a / a_t unchanged; conv2d_fwd_in over a with the planes (the x6 256x128 plans stage A by
-    LDS-DMA) equals the plain conv bit for bit, statistics included.  N = 1 / 2: all split-K; 8: whole rounds;
-    12: a round + a split-K tail."""
-    prev = ops.set_conv_math("bf16x6")
-    try:
-        H, C = 64, 256
-        y = _g(161, (N, H, H, C)).to(DEV)
-        s = ops.instnorm_stats(y)
-        a0, at0 = ops.instnorm_act_fwd(y, s, "relu", cp=(1, "reflect", 1))
-        a1, at1 = ops.instnorm_act_fwd(y, s, "relu", cp=(1, "reflect", 1), apre=True)
-        P = N * (H + 2) * (H + 2)  # a_t rows are padded to vst_cp_ld(P): compare the written part
-        assert torch.equal(a0, a1) and torch.equal(at0[:, :P], at1[:, :P])
-        pl = a1.vst_apl.view(3, -1)
-        for p_, ref in zip(pl, _split3(a1.reshape(-1))):
-            assert torch.equal(p_, ref)
-        w = _g(162, (C, C, 3, 3), 0.02)
-        kc = ops.weight_pack(w.to(DEV), ops.PACK_FWD)
-        b = torch.zeros(C, device=DEV)
-        y0, s0 = ops.conv2d_fwd_in(a0, kc, b, C, 3, 3, 1, 1, "reflect")
-        y1, s1 = ops.conv2d_fwd_in(a1, kc, b, C, 3, 3, 1, 1, "reflect")
-        assert torch.equal(y0, y1) and torch.equal(s0, s1)
-    finally:
-        ops.set_conv_math(prev)
-
-
 @pytest.mark.parametrize("N", [1, 8, 12])
 def test_apre_dgrad_epi_bit_identical(ops, N):
     """instnorm_act_bwd(planes, apre=True) writes dy ONLY as its NHWC planes (exactly the RNE split of the plain pass's
@@ -726,8 +698,8 @@ def test_apre_dgrad_epi_bit_identical(ops, N):
         s_in = ops.instnorm_stats(y_in)
         add = _g(175, (N, H, H, C)).to(DEV)
         db0, db1 = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
-        r0 = ops.conv2d_dgrad_refl_in(dy0, ikf, H, H, C, y_in, s_in, "relu", addend=add, db=db0, planes=True, epi=True)
-        r1 = ops.conv2d_dgrad_refl_in(dy1, ikf, H, H, C, y_in, s_in, "relu", addend=add, db=db1, planes=True, epi=True,
+        r0 = ops.conv2d_dgrad_refl_in(dy0, ikf, H, H, C, y_in, s_in, "relu", addend=add, db=db0, planes=True)
+        r1 = ops.conv2d_dgrad_refl_in(dy1, ikf, H, H, C, y_in, s_in, "relu", addend=add, db=db1, planes=True,
                                       apre=True)
         assert r0 is not None and r1 is not None
         assert torch.equal(r0[0], r1[0])
@@ -778,33 +750,6 @@ def test_wgrad_with_premade_planes_exact(ops, st):
         assert torch.equal(dw0, dw1)
     finally:
         ops.set_conv_math(prev)
-
-
-@pytest.mark.parametrize("act,addend", [("relu", False), ("none", True)])
-def test_dgrad_fold_instnorm_bwd_exact(ops, act, addend):
-    """conv2d_dgrad_s1_in (fold + IN-backward partials in one pass) == conv2d_dgrad_s1 (reflect) then
-    instnorm_act_bwd: folded gradient, IN input gradient, bias gradient and planes bit-identical."""
-    N, H, C = 2, 16, 64
-    dy = _g(6, (N, H, H, C)).to(DEV)
-    w = _g(7, (C, C, 3, 3), 0.05).to(DEV)
-    ikf = ops.weight_pack(w, ops.PACK_IKF)
-    y_in = _g(8, (N, H, H, C)).to(DEV)
-    s_in = ops.instnorm_stats(y_in)
-    add = _g(9, (N, H, H, C)).to(DEV) if addend else None
-    prev, ops.DGRAD_BORDER = ops.DGRAD_BORDER, False   # the padded-frame + fold route it fuses
-    try:
-        g0 = ops.conv2d_dgrad_s1(dy, ikf, H, H, C, 3, 1, "reflect", addend=add)
-    finally:
-        ops.DGRAD_BORDER = prev
-    db0 = torch.zeros(C, device=DEV)
-    d0, p0 = ops.instnorm_act_bwd(g0, y_in, s_in, act, db=db0, planes=True)
-    db1 = torch.zeros(C, device=DEV)
-    g1, d1, p1 = ops.conv2d_dgrad_s1_in(dy, ikf, H, H, C, 3, 1, y_in, s_in, act, addend=add, db=db1, planes=True)
-    assert torch.equal(g0, g1)
-    assert torch.equal(d0, d1)
-    assert torch.equal(db0, db1)
-    P = N * H * H  # the planes' row padding past P is never written (nor read)
-    assert torch.equal(p0[:, :, :P], p1[:, :, :P])
 
 
 @pytest.mark.parametrize("st,mode,res", [(1, "reflect", False), (1, "reflect", True), (2, "zero", False)])
@@ -1123,54 +1068,6 @@ def test_conv_c4_direct(ops, shape, conv_math):
 
 @pytest.mark.parametrize("case", [
     # name, N, C_in (= dx = IN channels), C_out (= dy), H, W, act, addend
-    ("small_relu", 2, 32, 32, 16, 16, "relu", True),
-    ("odd_HW_none", 3, 64, 64, 13, 20, "none", False),
-    ("minimal", 1, 32, 64, 4, 4, "relu", True),
-    ("prod_N8", 8, 256, 256, 64, 64, "relu", False),   # the batched G_A calls
-    ("prod_N12", 12, 256, 256, 64, 64, "none", True),  # interior with the split-K tail
-], ids=lambda c: c[0])
-def test_dgrad_refl_in_fused(ops, case):
-    """vst_conv2d_dgrad_refl_in (the border add taken by the IN backward partial pass) vs the separate
-    passes it replaces (vst_conv2d_dgrad_refl + vst_instnorm_act_bwd_planes): g, the IN input gradient,
-    its bf16 planes and the conv-bias gradient all bit-identical; and vs torch autograd."""
-    name, N, Ci, Co, H, W, act, with_add = case
-    prev = ops.set_conv_math("bf16x6")
-    try:
-        w = _g(121, (Co, Ci, 3, 3), 0.05)
-        ikf = ops.weight_pack(w.to(DEV), ops.PACK_IKF)
-        dy = _nhwc(_g(122, (N, Co, H, W)), ops)
-        add = _nhwc(_g(123, (N, Ci, H, W)), ops) if with_add else None
-        y_in = _nhwc(_g(124, (N, Ci, H, W)), ops)
-        s = ops.instnorm_stats(y_in)
-        db0 = torch.zeros(Ci, device=DEV)
-        db1 = torch.zeros(Ci, device=DEV)
-        r = ops.conv2d_dgrad_refl_in(dy, ikf, H, W, Ci, y_in, s, act, addend=add, db=db1, planes=True)
-        assert r is not None
-        g1, dx1, pl1 = r
-        g0 = ops.conv2d_dgrad_s1(dy, ikf, H, W, Ci, 3, 1, "reflect", addend=add)
-        dx0, pl0 = ops.instnorm_act_bwd(g0, y_in, s, act, db=db0, planes=True)
-        assert torch.equal(g1, g0), name
-        assert torch.equal(dx1, dx0), name
-        P = N * H * W  # the plane rows are padded to vst_cp_ld(P): compare the written part
-        assert torch.equal(pl1[:, :, :P], pl0[:, :, :P]), name
-        assert torch.equal(db1, db0), name
-        # vs torch: g = reflect-pad conv data gradient (+ addend); dx = IN(+act) backward of g
-        x = _g(125, (N, Ci, H, W)).requires_grad_(True)
-        yy = F.conv2d(F.pad(x, (1,) * 4, mode="reflect"), w)
-        yy.backward(_nchw(dy, Co, ops))
-        gref = x.grad + (_nchw(add, Ci, ops) if with_add else 0)
-        _close(_nchw(g1, Ci, ops), gref, tol=CONV_TOL["bf16x6"], what=name + " g")
-        yt = _nchw(y_in, Ci, ops).requires_grad_(True)
-        a = F.instance_norm(yt, eps=1e-5)
-        a = F.relu(a) if act == "relu" else a
-        a.backward(_nchw(g1, Ci, ops))
-        _close(_nchw(dx1, Ci, ops), yt.grad, tol=1e-4, what=name + " IN bwd")
-    finally:
-        ops.set_conv_math(prev)
-
-
-@pytest.mark.parametrize("case", [
-    # name, N, C_in (= dx = IN channels), C_out (= dy), H, W, act, addend
     ("small_relu", 2, 256, 256, 16, 16, "relu", True),      # all split-K tiles
     ("all_split_N1", 1, 256, 256, 64, 64, "relu", False),  # the whole conv as split-K tiles (B=1)
     ("prod_N8", 8, 256, 256, 64, 64, "relu", False),       # whole 256x128 rounds
@@ -1178,7 +1075,7 @@ def test_dgrad_refl_in_fused(ops, case):
     ("prod_N12", 12, 256, 256, 64, 64, "none", True),      # a round + the split-K tail
 ], ids=lambda c: c[0])
 def test_dgrad_refl_in_epi(ops, case):
-    """vst_conv2d_dgrad_refl_in_epi (the IN backward partials taken by the data gradient's GEMM epilogue /
+    """ops.conv2d_dgrad_refl_in / vst_conv2d_dgrad_refl_in_epi (the IN backward partials taken by the data gradient's GEMM epilogue /
     split-K reduce and the border add's correction slices) vs the separate passes (vst_conv2d_dgrad_refl +
     vst_instnorm_act_bwd_planes): g bit-identical; the IN input gradient, its planes and the bias gradient
     equal up to the partials' fp64 summation order (1e-6 of max); and vs torch autograd."""
@@ -1193,7 +1090,7 @@ def test_dgrad_refl_in_epi(ops, case):
         s = ops.instnorm_stats(y_in)
         db0 = torch.zeros(Ci, device=DEV)
         db1 = torch.zeros(Ci, device=DEV)
-        r = ops.conv2d_dgrad_refl_in(dy, ikf, H, W, Ci, y_in, s, act, addend=add, db=db1, planes=True, epi=True)
+        r = ops.conv2d_dgrad_refl_in(dy, ikf, H, W, Ci, y_in, s, act, addend=add, db=db1, planes=True)
         assert r is not None, name
         g1, dx1, pl1 = r
         g0 = ops.conv2d_dgrad_s1(dy, ikf, H, W, Ci, 3, 1, "reflect", addend=add)
@@ -1230,31 +1127,7 @@ def test_dgrad_refl_in_epi_unsupported(ops):
             dy = _nhwc(_g(142, (N, C, H, W)), ops)
             y_in = _nhwc(_g(143, (N, C, H, W)), ops)
             s = ops.instnorm_stats(y_in)
-            assert ops.conv2d_dgrad_refl_in(dy, ikf, H, W, C, y_in, s, "relu", epi=True) is None
-    finally:
-        ops.set_conv_math(prev)
-
-
-@pytest.mark.parametrize("N", [1, 2, 8, 12, 16])
-def test_conv_fwd_nrm_matches_apply_then_conv(ops, N):
-    """vst_conv2d_fwd_nrm_ws (the ResnetBlock's second conv normalising relu(IN(t)) in its A staging)
-    is bit-identical to the IN + ReLU apply pass followed by the forward conv (same expression, same
-    products): output and its IN statistics; N = 1 / 2 run the all-split-K plan, 12 a 256x128 round
-    plus a split-K tail, 8 / 16 whole rounds."""
-    prev = ops.set_conv_math("bf16x6")
-    try:
-        H, C = 64, 256
-        t = _g(91, (N, H, H, C)).to(DEV) * 0.7 + 0.2
-        w = _g(92, (C, C, 3, 3), 0.02)
-        b = _g(93, (C,), 0.1).to(DEV)
-        kc = ops.weight_pack(w.to(DEV), ops.PACK_FWD)
-        s1 = ops.instnorm_stats(t)
-        assert ops.lib().vst_conv2d_fwd_nrm_ok(N, H, H, C, C, 3, 3, 1, 1, ops.PAD["reflect"], ops._math("infer"))
-        a = ops.instnorm_act_fwd(t, s1, "relu")
-        y_ref, s_ref = ops.conv2d_fwd_in(a, kc, b, C, 3, 3, 1, 1, "reflect", role="infer")
-        y, s = ops.conv2d_fwd_in_nrm(t, s1, kc, b, C, 3, 1, "reflect", role="infer")
-        assert torch.equal(y, y_ref)
-        assert torch.equal(s, s_ref)
+            assert ops.conv2d_dgrad_refl_in(dy, ikf, H, W, C, y_in, s, "relu") is None
     finally:
         ops.set_conv_math(prev)
 

@@ -1291,6 +1291,66 @@ extern "C" int vst_conv2d_wgrad_pre(const float* x, const float* x_t, const floa
   return check_launch("conv2d_wgrad_reduce");
 }
 
+// The weight gradient over the NHWC operands the convs themselves use (round 6): x fp32 NHWC and dy as its NHWC
+// bf16 planes dy_apl [3][N*Ho*Wo*Cyp] (the pre-split A operand the data gradient of the same layer reads), on the
+// x6 256x128 plans of the split-bf16 kernel (conv_wgrad_nhwc_k: k-major stage images read by ds_read_b64_tr_b16).
+// Same split plan, slabs and reduction as vst_conv2d_wgrad_pre (bit-identical results), but no padded
+// channel-major x image and no channel-major dy planes: their producers (the IN apply / IN backward passes) need
+// not write them.
+static bool wgrad_nhwc_plan(int N, int H, int W, int Cx, int Ho, int Wo, int Cyp, int R, int S, int stride, int pad,
+                            int math, WgradPlan* out) {
+  if (math != VST_MATH_BF16X6 || R != S || Cx < 8) return false;
+  const WgradPlan p = plan_wgrad(N, H, W, Ho, Wo, Cx, Cyp, R, S, stride, math);
+  if (!p.bfk || p.wpad || !bf_wgrad_nhwc_ok((int)p.tile, Wo, Cx, Cyp)) return false;
+  if (wgrad_two_level(p, Cyp, Cx, R * S, Cyp)) return false;  // (the one-level reduction of the pre path's plan)
+  if (stride == 1 && p.pad != pad) return false;
+  if (Ho != (H + 2 * pad - R) / stride + 1 || Wo != (W + 2 * pad - S) / stride + 1) return false;
+  *out = p;
+  return true;
+}
+
+extern "C" int vst_conv2d_wgrad_nhwc_ok(int N, int H, int W, int Cx, int Ho, int Wo, int Cyp, int R, int S, int stride,
+                                        int pad, int math) {
+  WgradPlan p;
+  return wgrad_nhwc_plan(N, H, W, Cx, Ho, Wo, Cyp, R, S, stride, pad, math, &p) ? 1 : 0;
+}
+
+extern "C" size_t vst_conv2d_wgrad_nhwc_ws_bytes(int N, int H, int W, int Cx, int Ho, int Wo, int Cyp, int R, int S,
+                                                 int stride, int pad, int math) {
+  WgradPlan p;
+  if (!wgrad_nhwc_plan(N, H, W, Cx, Ho, Wo, Cyp, R, S, stride, pad, math, &p)) return 0;
+  return (size_t)p.nsplit * p.Mw * Cyp * sizeof(float);
+}
+
+extern "C" int vst_conv2d_wgrad_nhwc(const float* x, const void* dy_apl, float* dw, float* ws, size_t ws_bytes, int N,
+                                     int H, int W, int Cx, int Ho, int Wo, int Cyp, int R, int S, int stride, int pad,
+                                     int pad_mode, int Co, int Ci, long so, long si, int accumulate, int math,
+                                     void* stream) {
+  VST_REQUIRE(x && dy_apl && dw && ws, "conv2d_wgrad_nhwc: null pointer");
+  VST_REQUIRE(Co <= Cyp && Ci <= Cx && pad >= 0 && (pad_mode == VST_PAD_ZERO || (pad < H && pad < W)),
+              "conv2d_wgrad_nhwc: bad args");
+  WgradPlan p;
+  if (!wgrad_nhwc_plan(N, H, W, Cx, Ho, Wo, Cyp, R, S, stride, pad, math, &p)) {
+    ::vst::set_error("conv2d_wgrad_nhwc: unsupported shape / arithmetic (vst_conv2d_wgrad_nhwc_ok)");
+    return VST_EUNSUPPORTED;
+  }
+  VST_REQUIRE(ws_bytes >= (size_t)p.nsplit * p.Mw * Cyp * sizeof(float),
+              "conv2d_wgrad_nhwc: workspace too small (%zu bytes)", ws_bytes);
+  hipStream_t s = (hipStream_t)stream;
+  bf_wgrad_nhwc_launch(x, dy_apl, (long)N * Ho * Wo * Cyp, ws, N, H, W, Cx, Ho, Wo, Cyp, S, pad, stride,
+                       pad_mode == VST_PAD_REFLECT, p.Mw, p.chunk, p.nsplit, s);
+  int rc = check_launch("conv2d_wgrad_nhwc");
+  if (rc) return rc;
+  const long slab = (long)p.Mw * Cyp;
+  if (p.nsplit > 2)
+    hipLaunchKernelGGL(wgrad_reduce_store_k<1>, dim3(ceil_div(Ci * R * S, 16), ceil_div(Co, 64)), dim3(256), 0, s,
+                       ws, dw, Cx, Cyp, R * S, Co, Ci, so, si, accumulate, p.nsplit, slab);
+  else
+    hipLaunchKernelGGL(wgrad_reduce_store_k<2>, dim3(ceil_div(Ci * R * S, 32), ceil_div(Co, 64)), dim3(256), 0, s,
+                       ws, dw, Cx, Cyp, R * S, Co, Ci, so, si, accumulate, p.nsplit, slab);
+  return check_launch("conv2d_wgrad_nhwc_reduce");
+}
+
 extern "C" int vst_conv2d_wgrad_bias(const float* x, const float* dy, float* dw, float* db, float* ws, size_t ws_bytes,
                                      int N, int H, int W, int Cx, int Ho, int Wo, int Cyp, int R, int S, int stride,
                                      int pad, int pad_mode, int Co, int Ci, long so, long si, int accumulate, int math,

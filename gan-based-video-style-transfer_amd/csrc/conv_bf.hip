@@ -1530,6 +1530,226 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_wgrad_bf_k(
     }
 }
 
+// ---- The weight gradient over NHWC operands (round 6).  conv_wgrad_bf_k reads x as a padded channel-major fp32
+// image and dy as channel-major bf16 planes — layouts with the pixel (the GEMM's K) contiguous, made for it by the
+// producing IN passes in addition to the NHWC tensors the convs read.  This kernel reads the NHWC tensors
+// themselves: x fp32 NHWC (the activation the forward conv read; reflect / zero padding applied per gathered
+// pixel) and dy as its NHWC bf16 planes [3][P][Cyp] (the data gradient's pre-split A operand), both with the
+// channels (the GEMM's M / N) contiguous.  The stage image is therefore k-major — per plane, [32 k rows] x
+// [128 columns] sub-images — and the MFMA operands are read with ds_read_b64_tr_b16 (cdna_hip_programming.md T10:
+// per 16-lane group a 4-row x 16-column block delivered column-major; two reads give a lane its 8 k values).  The
+// rows are KM_PITCH = 272 B apart (256 B of data + 16): a 32-lane half of a transposed read touches rows 8g + q and
+// 8g + 8 + q (q < 4), whose 32-B pieces then sit 4 banks apart (at most 2-way, as the channel-major kernel's
+// 16x16x32 row reads) and, unlike a chunk XOR, a fragment's address differs from the next fragment's by an
+// immediate, so the operand reads need one address register per stage.  The K split, the per-stage MFMA sequence
+// and the lanes' k assignment are conv_wgrad_bf_k's, so the slabs are bit-identical to it.
+constexpr int KM_PITCH = 272, KM_GROUP = 32 * KM_PITCH;
+__device__ __forceinline__ int km_off(int grp, int row, int col) { return grp * KM_GROUP + KM_PITCH * row + 2 * col; }
+template <class T>
+struct KmGeom {
+  static constexpr int A_PLANE = (T::BM / 128) * KM_GROUP, B_PLANE = (T::BN / 128) * KM_GROUP;
+  static constexpr int A_BYTES = T::NP * A_PLANE, STAGE = T::NP * (A_PLANE + B_PLANE);
+  static_assert(2 * STAGE <= 160 * 1024, "LDS");
+};
+
+// A chunks (8 consecutive M columns of one k row, fp32 -> split here), B chunks (8 columns of one k row per plane,
+// pre-split): thread t's chunk j is c = t + NT j, row c / (cols / 8), chunk c % (cols / 8)
+template <class T>
+__device__ __forceinline__ void store_stage_km(char* st, const float4 (&ra)[T::A_LD][2],
+                                               const u32x4_t (&rbv)[T::B_LD][T::NP], int t) {
+  using G = KmGeom<T>;
+  char* Bs = st + G::A_BYTES;
+  constexpr int AC = T::BM / 8, BC = T::BN / 8;
+#pragma unroll
+  for (int j = 0; j < T::A_LD; ++j) {
+    const int c = t + T::NT * j, k = c / AC, mc = c % AC;
+    uint4 sp[T::NP];
+    split8<T::NP>(ra[j][0], ra[j][1], sp);
+    const int off = km_off(mc >> 4, k, 8 * (mc & 15));
+#pragma unroll
+    for (int p = 0; p < T::NP; ++p) *reinterpret_cast<uint4*>(st + p * G::A_PLANE + off) = sp[p];
+  }
+#pragma unroll
+  for (int j = 0; j < T::B_LD; ++j) {
+    const int c = t + T::NT * j, k = c / BC, nc = c % BC;
+    const int off = km_off(nc >> 4, k, 8 * (nc & 15));
+#pragma unroll
+    for (int p = 0; p < T::NP; ++p) *reinterpret_cast<u32x4_t*>(Bs + p * G::B_PLANE + off) = rbv[j][p];
+  }
+}
+
+typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) bf16x4_t lds_bf16x4;
+
+// the 16x16x32 operand of columns cb .. cb + 15 (k = 8 g .. 8 g + 7 for lane group g) from a k-major image:
+// lane 4q + p of group g supplies row 8g + q (then 8g + 4 + q), columns cb + 4p .. + 3
+__device__ __forceinline__ bf16x8_t read_km16(const char* __restrict__ img, int cb, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+  const char* a0 = img + km_off(cb >> 7, 8 * g + q, (cb & 127) + 4 * pp);
+  const char* a1 = a0 + 4 * KM_PITCH;
+  bf16x4_t lo = {}, hi = {};
+#if defined(__HIP_DEVICE_COMPILE__)
+  lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(a0));
+  hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(a1));
+#endif
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+template <class T>
+__device__ __forceinline__ void read_plane16_km(Plane16<T>& f, const char* __restrict__ st, int p, int wm0, int wn0,
+                                                int lane) {
+  using G = KmGeom<T>;
+  const char* As = st + p * G::A_PLANE;
+  const char* Bs = st + G::A_BYTES + p * G::B_PLANE;
+#pragma unroll
+  for (int i = 0; i < T::MI16; ++i) f.a[i] = read_km16(As, wm0 + 16 * i, lane);
+#pragma unroll
+  for (int j = 0; j < T::NI16; ++j) f.b[j] = read_km16(Bs, wn0 + 16 * j, lane);
+}
+
+// main_loop16 (same stage / group / MFMA order) on k-major stage images
+template <class T, class LoadAll, class Adv>
+__device__ __forceinline__ void main_loop16_km(char* smem, int nk, f32x4v (&acc)[T::MI16][T::NI16],
+                                               float4 (&ra)[2][T::A_LD][2], u32x4_t (&rbv)[2][T::B_LD][T::NP],
+                                               LoadAll load_all, Adv adv) {
+  constexpr int STAGE = KmGeom<T>::STAGE;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wm0 = (wave / T::WAVES_N) * T::WM, wn0 = (wave % T::WAVES_N) * T::WN;
+  if (nk <= 0) return;
+  load_all(0);
+  store_stage_km<T>(smem, ra[0], rbv[0], t);
+  adv(nk > 1);
+  load_all(1);
+  __syncthreads();
+  Plane16<T> hi, mid, lo;
+  read_plane16_km<T>(mid, smem, 1, wm0, wn0, lane);
+  auto step = [&](int kt, auto par) __attribute__((always_inline)) {
+    constexpr int P = decltype(par)::value;
+    const char* cur = smem + P * STAGE;
+    char* nxt = smem + (P ^ 1) * STAGE;
+    read_plane16_km<T>(hi, cur, 0, wm0, wn0, lane);
+    adv(kt + 2 < nk);
+    load_all(P);
+    mma16<T>(mid, mid, acc);
+    read_plane16_km<T>(lo, cur, 2, wm0, wn0, lane);
+    store_stage_km<T>(nxt, ra[P ^ 1], rbv[P ^ 1], t);
+    mma16<T>(mid, hi, acc);
+    mma16<T>(hi, mid, acc);
+    __builtin_amdgcn_sched_barrier(0);
+    __syncthreads();
+    read_plane16_km<T>(mid, nxt, 1, wm0, wn0, lane);
+    mma16<T>(hi, hi, acc);
+    mma16<T>(lo, hi, acc);
+    mma16<T>(hi, lo, acc);
+  };
+  int kt = 0;
+  for (; kt + 1 < nk; kt += 2) {
+    step(kt, std::integral_constant<int, 0>());
+    step(kt + 1, std::integral_constant<int, 1>());
+  }
+  if (kt < nk) step(kt, std::integral_constant<int, 0>());
+}
+
+// dW = x^T dy over split-K pixel chunks, x fp32 NHWC [N][H][W][Cx], dy NHWC bf16 planes dyp [3][P][Cyp] (plane
+// stride pps); M rows (tap, ci), N columns co; the same tile grid / XCD order / chunks / slab layout as
+// conv_wgrad_bf_k.  Needs Wo % 32 == 0 (a 32-pixel K step inside one output row), Cx % 8 == 0, Cyp % 8 == 0.
+template <class T>
+__global__ __launch_bounds__(T::NT, T::MINB) void conv_wgrad_nhwc_k(
+    const float* __restrict__ x, const __bf16* __restrict__ dyp, long pps, float* __restrict__ slab, int H, int W,
+    int Cx, int Ho, int Wo, int Cyp, int S, int pad, int st, int reflect, int Mw, int P, int chunk) {
+  static_assert(T::M16 && T::BK == 32 && T::BM % 128 == 0 && T::BN % 128 == 0, "k-major images of 128 columns");
+  static_assert((T::NT % (T::BM / 8)) == 0 && (T::NT % (T::BN / 8)) == 0, "a thread's chunk column is fixed");
+  __shared__ __attribute__((aligned(16))) char smem[2 * KmGeom<T>::STAGE];
+  constexpr int A_LD = T::A_LD, B_LD = T::B_LD, NP = T::NP, AC = T::BM / 8, BC = T::BN / 8;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int Mt = (Mw + T::BM - 1) / T::BM, Nt = (Cyp + T::BN - 1) / T::BN, Zt = (P + chunk - 1) / chunk;
+  int mx, ny, zz;
+  {
+    const int tt = xcd_tile(blockIdx.x, Mt * Nt * Zt);
+    zz = tt / (Mt * Nt);
+    const int rem = tt - zz * Mt * Nt;
+    ny = rem / Mt;
+    mx = rem - ny * Mt;
+  }
+  const int m0 = mx * T::BM, n0 = ny * T::BN;
+  const int pbeg = zz * chunk, pend = min(P, pbeg + chunk);
+  const float* zp = g_zero_page;
+  const __bf16* zpb = reinterpret_cast<const __bf16*>(g_zero_page);
+  // this thread's A column chunk (tap, ci .. ci + 7) (columns past Mw read column chunk Mw - 8: never stored)
+  int r_, s_, ci;
+  {
+    const int m = min(m0 + 8 * (t % AC), Mw - 8);
+    const int tap = m / Cx;
+    ci = m - tap * Cx;
+    r_ = tap / S;
+    s_ = tap - r_ * S;
+  }
+  const int ka = t / AC;  // + (NT / AC) j: its pixel rows
+  // its B column chunk (channels past Cyp read the last chunk: never stored)
+  const int co = min(n0 + 8 * (t % BC), Cyp - 8), kb = t / BC;
+  // the stage's first output pixel: (n, ho, wo0), flattened pb
+  int pb = pbeg, n, ho, wo0;
+  {
+    const int hw = Ho * Wo;
+    n = pb / hw;
+    const int rem = pb - n * hw;
+    ho = rem / Wo;
+    wo0 = rem - ho * Wo;
+  }
+  float4 ra[2][A_LD][2];
+  u32x4_t rbv[2][B_LD][NP];
+  auto load_all = [&](int set) __attribute__((always_inline)) {
+    const bool live = pb < pend;
+    const int hi = ho * st + r_ - pad;
+    const int hr = reflect ? reflect_idx(hi, H) : hi;
+    const bool hok = (unsigned)hr < (unsigned)H;
+#pragma unroll
+    for (int j = 0; j < A_LD; ++j) {
+      const int wi = (wo0 + ka + (T::NT / AC) * j) * st + s_ - pad;
+      const int wr = reflect ? reflect_idx(wi, W) : wi;
+      const bool ok = live && hok && (unsigned)wr < (unsigned)W;
+      const float* p = ok ? x + (((long)n * H + hr) * W + wr) * Cx + ci : zp;
+      ra[set][j][0] = *reinterpret_cast<const float4*>(p);
+      ra[set][j][1] = *reinterpret_cast<const float4*>(p + 4);
+    }
+#pragma unroll
+    for (int j = 0; j < B_LD; ++j) {
+      const __bf16* q = live ? dyp + (long)(pb + kb + (T::NT / BC) * j) * Cyp + co : zpb;
+      const long ps = live ? pps : 0;
+#pragma unroll
+      for (int p = 0; p < NP; ++p) rbv[set][j][p] = *reinterpret_cast<const u32x4_t*>(q + p * ps);
+    }
+  };
+  auto adv = [&](bool go) __attribute__((always_inline)) {
+    const int w1 = wo0 + T::BK;
+    const bool e1 = w1 == Wo;
+    const int h1 = ho + (e1 ? 1 : 0);
+    const bool e2 = h1 == Ho;
+    pb = go ? pb + T::BK : pb;
+    wo0 = go ? (e1 ? 0 : w1) : wo0;
+    ho = go ? (e2 ? 0 : h1) : ho;
+    n = go ? (e2 ? n + 1 : n) : n;
+  };
+  const int nk = pend > pbeg ? (pend - pbeg + T::BK - 1) / T::BK : 0;
+  const int wm0 = (wave / T::WAVES_N) * T::WM, wn0 = (wave % T::WAVES_N) * T::WN;
+  float* sl = slab + (long)zz * Mw * Cyp;
+  f32x4v acc[T::MI16][T::NI16];
+  zero_acc4(acc);
+  main_loop16_km<T>(smem, nk, acc, ra, rbv, load_all, adv);
+#pragma unroll
+  for (int i = 0; i < T::MI16; ++i)
+#pragma unroll
+    for (int j = 0; j < T::NI16; ++j) {
+      const int nn = n0 + wn0 + 16 * j + (lane & 15);
+      if (nn >= Cyp) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int mm = m0 + wm0 + 16 * i + 4 * (lane >> 4) + r;
+        if (mm < Mw) sl[(long)mm * Cyp + nn] = acc[i][j][r];
+      }
+    }
+}
+
 // fprop_splitk_reduce_k of a data gradient's split-K tail (no bias / act) with the IN-backward partials
 // of the layer below (InbArgs, one 32-row group per block: slice (m - image start) / 32); same block
 // geometry, the 16 row-threads' fp64 sums folded through LDS in a fixed order.
@@ -1814,6 +2034,12 @@ void bf_plan(long M, int Cop, int math, int kind, int* kind_out, int* m_split_ou
         m_split = (int)ms;
         tail_kind = bk;
       }
+    } else if (b256 < VST_NUM_CUS && b256 > VST_BF_FULLSPLIT_MAX) {
+      // one partial round of 256x128 tiles (more than the all-split form takes) against the 128x128 grid's
+      // rounds at the same one block per CU (a 32-deep K step ~2.25 vs ~1.5 us): the 436x1024 ResnetBlocks
+      // (M = 27904, 218 tiles) ran 436 128x128 blocks = 2 rounds
+      const long r128 = ((M + 127) / 128 * nt + VST_NUM_CUS - 1) / VST_NUM_CUS;
+      if (2.25 < 1.5 * r128) kd = 7;
     }
   }
 #endif
@@ -2285,6 +2511,20 @@ void bf_wgrad_launch(const float* xt, const void* dyp, float* slab, int N, int H
     VST_BF_DISPATCH(kind, 2, VST_BW)
   }
 #undef VST_BW
+}
+
+bool bf_wgrad_nhwc_ok(int kind, int Wo, int Cx, int Cyp) {
+  return VST_BF_MF16 && kind == 7 && Wo % 32 == 0 && Cx % 8 == 0 && Cyp % 8 == 0;
+}
+
+void bf_wgrad_nhwc_launch(const float* x, const void* dyp, long pps, float* slab, int N, int H, int W, int Cx, int Ho,
+                          int Wo, int Cyp, int S, int pad, int st, int reflect, int Mw, int chunk, int nsplit,
+                          hipStream_t s) {
+  using T = bf::Tile<256, 128, 64, 64, 32, 3>;
+  const int P = N * Ho * Wo;
+  const dim3 grid(ceil_div(Mw, T::BM) * ceil_div(Cyp, T::BN) * nsplit);
+  hipLaunchKernelGGL(bf::conv_wgrad_nhwc_k<T>, grid, dim3(T::NT), 0, s, x, reinterpret_cast<const __bf16*>(dyp), pps,
+                     slab, H, W, Cx, Ho, Wo, Cyp, S, pad, st, reflect, Mw, P, chunk);
 }
 
 void bf_wgrad_geom(int kind, int math, int* bm, int* bn, int* bk, int* slots) {

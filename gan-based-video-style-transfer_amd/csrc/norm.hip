@@ -390,7 +390,7 @@ __global__ void in_bwd_apply_k(const float4* __restrict__ gy, const float4* __re
                                const float* __restrict__ stats, const float2* __restrict__ coef,
                                float4* __restrict__ dx, long total4, int HW, int C4, int act,
                                float slope, const double* __restrict__ dbn, float* __restrict__ db, int N,
-                               int accumulate_db) {
+                               int accumulate_db, __bf16* __restrict__ apl = nullptr) {
   if (db && blockIdx.x * blockDim.x < 4 * C4)
     in_bias_grad_blocks(dbn, db, N, 4 * C4, accumulate_db, blockIdx.x * blockDim.x + threadIdx.x);
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -408,7 +408,10 @@ __global__ void in_bwd_apply_k(const float4* __restrict__ gy, const float4* __re
   o.y = in_bwd1(g.y, v.y, s0.z, s0.w, make_float2(k01.z, k01.w), act, slope);
   o.z = in_bwd1(g.z, v.z, s1.x, s1.y, make_float2(k23.x, k23.y), act, slope);
   o.w = in_bwd1(g.w, v.w, s1.z, s1.w, make_float2(k23.z, k23.w), act, slope);
-  dx[i] = o;
+  if (apl)  // dx as its NHWC planes only (the data gradient's pre-split A operand and the NHWC weight gradient's B)
+    store_planes4(apl, total4 * 4, i * 4, o);
+  else
+    dx[i] = o;
 }
 
 // in_bwd_apply_k fused with the weight gradient's B-operand image: dx = the IN(+act) input gradient
@@ -856,14 +859,15 @@ extern "C" int vst_instnorm_act_bwd_planes(const float* gy, const float* x, cons
   return in_bwd_tail(gy, x, stats, dx, db, ws, N, HW, C, act, slope, accumulate_db, planes, ldp, g, s);
 }
 
-// vst_instnorm_act_bwd_planes that also writes dx's NHWC bf16 planes apl [3][N*HW*C] (the A operand of the x6
-// data gradient that consumes dx, pre-split: vst_conv2d_dgrad_refl_epi_part's apl)
+// vst_instnorm_act_bwd_planes that writes dx ONLY as its NHWC bf16 planes apl [3][N*HW*C] (the A operand of the x6
+// data gradient that consumes dx, pre-split: vst_conv2d_dgrad_refl_epi_part's apl; and the B operand of
+// vst_conv2d_wgrad_nhwc) — with planes (!= NULL) the channel-major planes [3][C][ldp] too, without them none
 extern "C" int vst_instnorm_act_bwd_planes_apre(const float* gy, const float* x, const float* stats, float* dx,
                                                 float* db, float* ws, int N, int HW, int C, int act, float slope,
                                                 int accumulate_db, void* planes, long ldp, void* apl, void* stream) {
   RedGeom g;
-  VST_REQUIRE(gy && x && stats && dx && ws && planes && apl && red_geom(N, HW, C, g), "instnorm_act_bwd_apre: bad args");
-  VST_REQUIRE(ldp >= (long)N * HW, "instnorm_act_bwd_apre: plane stride %ld < N*HW", ldp);
+  VST_REQUIRE(gy && x && stats && dx && ws && apl && red_geom(N, HW, C, g), "instnorm_act_bwd_apre: bad args");
+  VST_REQUIRE(!planes || ldp >= (long)N * HW, "instnorm_act_bwd_apre: plane stride %ld < N*HW", ldp);
   hipStream_t s = (hipStream_t)stream;
   double* part = reinterpret_cast<double*>(ws);
   hipLaunchKernelGGL(in_partial_k<1>, dim3(g.nsplit, N), dim3(NRED), 0, s, x, gy, stats, part, HW, C,
@@ -941,7 +945,6 @@ static int in_bwd_tail(const float* gy, const float* x, const float* stats, floa
     hipLaunchKernelGGL(in_bwd_finalize_k<16>, dim3(ceil_div(C, 16), N), dim3(256), 0, s, part, stats, coef, dbn,
                      N, HW, C, g.nsplit);
   // the bias gradient (sum over n of dbn) is taken by the apply pass's first blocks
-  VST_REQUIRE(!apl || planes, "instnorm_act_bwd: the NHWC A planes come with the weight-gradient planes");
   if (planes) {
     const long P = (long)N * HW;
     hipLaunchKernelGGL(in_bwd_apply_planes_k, dim3(ceil_div(P, 64), ceil_div(C, 64)), dim3(256), 0, s, gy, x, stats,
@@ -954,7 +957,7 @@ static int in_bwd_tail(const float* gy, const float* x, const float* stats, floa
   hipLaunchKernelGGL(in_bwd_apply_k, dim3(ceil_div(total4, 256)), dim3(256), 0, s,
                      reinterpret_cast<const float4*>(gy), reinterpret_cast<const float4*>(x), stats,
                      coef, reinterpret_cast<float4*>(dx), total4, HW, C / 4, act, slope, dbn, db, N,
-                     accumulate_db);
+                     accumulate_db, reinterpret_cast<__bf16*>(apl));
   return check_launch("instnorm_act_bwd");
 }
 

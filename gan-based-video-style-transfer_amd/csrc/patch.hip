@@ -612,8 +612,10 @@ int head_fwd_launch(const float* x, const float* wp, const float* bias, float* o
 size_t head_tap_ws_floats(int N, int Hi, int Wi) { return (size_t)N * Hi * Wi * 16; }
 
 bool head_tap_ok(int Cin) {
-  // K halves of whole 16-channel groups; the row chunk + weights + partials fit the LDS
-  return Cin % 32 == 0 && ((size_t)(HT_JC + 16) * (Cin + 4) + 4 * HT_JC * 16) * 4 <= 160 * 1024;
+  // K halves of whole 16-channel groups; the row chunk + weights + partials fit the LDS; head_tap_k stages a row
+  // chunk (HT_JC pixels x Cin / 4 float4) in at most 16 passes of HT_THREADS lanes: Cin <= 512
+  return Cin % 32 == 0 && HT_JC * Cin / 4 <= 16 * HT_THREADS &&
+         ((size_t)(HT_JC + 16) * (Cin + 4) + 4 * HT_JC * 16) * 4 <= 160 * 1024;
 }
 
 int head_tap_fwd_launch(const float* x, const float* wp, const float* bias, float* out, float* ws, int N, int Hi,

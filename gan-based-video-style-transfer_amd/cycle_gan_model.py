@@ -234,3 +234,7 @@ class CycleGANModel(BaseModel):
         if torch.is_tensor(t) and t.dim() == 4 and t.shape[-1] == ops.cpad(self.opt.input_nc):
             return ops.nhwc_to_nchw(t.detach().contiguous(), self.opt.input_nc)
         return t
+
+
+from . import _lib as _lib_routes  # noqa: E402
+_lib_routes.apply_route_overrides(__name__, globals())

@@ -105,3 +105,7 @@ class CycleGANVGGModel(CycleGANModel):
             style = term if style is None else style + term
         self.loss_G_S = style
         return self.loss_G_C + self.loss_G_S
+
+
+from . import _lib as _lib_routes  # noqa: E402
+_lib_routes.apply_route_overrides(__name__, globals())

@@ -399,3 +399,7 @@ class Johnson:
         """fs_johnson.py:50-52: styled frame / 255."""
         _, styled = self.model(frame.to(self.device).float())
         return styled / 255.0
+
+
+from . import _lib as _lib_routes  # noqa: E402
+_lib_routes.apply_route_overrides(__name__, globals())

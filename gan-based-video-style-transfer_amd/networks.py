@@ -524,12 +524,24 @@ def _wgrad_on_bf(N, H, W, Cx, Ho, Wo, Cyp, R, st, policy):
     return ops.conv_plan_wgrad(N, H, W, Cx, Ho, Wo, Cyp, R, R, st, "bwd")[0] == _WPLAN_BF
 
 
+def _rb_wgrad_nhwc(N, H, W, C):
+    """Do the ResnetBlock convs (3x3, stride 1, reflect pad 1, C -> C at H x W) take their weight gradients on the
+    NHWC operands (ops.conv2d_wgrad(dy_apl=...)): x = the conv's own NHWC input, dy = the NHWC planes the
+    planes-only backward chain (APRE_BWD) writes?  Then the IN passes write neither the padded channel-major
+    x image nor dy's channel-major planes."""
+    return (APRE_BWD and DGRAD_EPI and ops.dgrad_refl_epi_ok(N, H, W, C, C) and
+            ops.wgrad_nhwc_ok(N, H, W, C, H, W, C, 3, 1, 1, ops.get_conv_math()))
+
+
 def _in_bwd_for_wgrad(g, y, s, act, slope, db, x_in, R, st, want, apre=False):
     """instnorm_act_bwd -> (dy, dy_planes or None); planes only when the wgrad of the conv below
-    (input x_in, kernel R, stride st) takes the x6 split-bf16 path (apre: dy's NHWC planes too)."""
+    (input x_in, kernel R, stride st) takes the x6 split-bf16 path (apre: dy's NHWC planes too; with the
+    NHWC-operand weight gradient those alone, dy_planes None)."""
     if want and IN_PLANES:
         N, H, W, Cx = x_in.shape
         _, Ho, Wo, Cyp = y.shape
+        if apre and ops.wgrad_nhwc_ok(N, H, W, Cx, Ho, Wo, Cyp, R, st, (R - 1) // 2, ops.get_conv_math()):
+            return ops.instnorm_act_bwd(g, y, s, act, slope, db=db, apre=True), None
         if _wgrad_on_bf(N, H, W, Cx, Ho, Wo, Cyp, R, st, ops.get_conv_math()):
             return ops.instnorm_act_bwd(g, y, s, act, slope, db=db, planes=True, apre=apre)
     return ops.instnorm_act_bwd(g, y, s, act, slope, db=db), None
@@ -555,6 +567,8 @@ class _GeneratorFn(torch.autograd.Function):
             if not (train_w and IN_XT):
                 return None
             N_, H_, W_, C_ = y.shape
+            if st == 1 and mode == "reflect" and cout == C_ and _rb_wgrad_nhwc(N_, H_, W_, C_):
+                return None  # a ResnetBlock conv: its weight gradient reads y's NHWC activation itself
             Ho_, Wo_ = (H_ + 2 - 3) // st + 1, (W_ + 2 - 3) // st + 1
             return (1, mode, st) if _wgrad_on_bf(N_, H_, W_, C_, Ho_, Wo_, cpad(cout), 3, st,
                                                  ops.get_conv_math()) else None
@@ -747,6 +761,10 @@ class _GeneratorFn(torch.autograd.Function):
                 want = (train_w and IN_PLANES and
                         _wgrad_on_bf(N, x_w.shape[1], x_w.shape[2], x_w.shape[3], y_in.shape[1], y_in.shape[2],
                                      cin_p, R_w, st_w, ops.get_conv_math()))
+                if want and apre and ops.wgrad_nhwc_ok(N, x_w.shape[1], x_w.shape[2], x_w.shape[3], y_in.shape[1],
+                                                       y_in.shape[2], cin_p, R_w, st_w, (R_w - 1) // 2,
+                                                       ops.get_conv_math()):
+                    want = False  # the NHWC-operand weight gradient reads dy_in's NHWC planes (apre)
                 r = ops.conv2d_dgrad_refl_in(dy, ikf, H, W, cin_p, y_in, s_in, act, 0.0, addend=addend, db=db,
                                              planes=want, apre=apre)
                 if r is not None:
@@ -1037,3 +1055,7 @@ class GANLoss(nn.Module):
         if self.gan_mode in ['lsgan', 'vanilla']:
             return self.loss(prediction, self.get_target_tensor(prediction, target_is_real))
         return -prediction.mean() if target_is_real else prediction.mean()
+
+
+from . import _lib as _lib_routes  # noqa: E402
+_lib_routes.apply_route_overrides(__name__, globals())

@@ -4,6 +4,7 @@ Every function launches on torch's current HIP stream, takes/returns torch tenso
 GPU, and raises on a non-zero status.  Activations are NHWC fp32 with a channel stride that is a
 multiple of 4 (``cpad``); images are NHWC4.  There is no CPU fallback: a CPU tensor is an error.
 """
+import functools
 import os
 
 import torch
@@ -288,15 +289,50 @@ def conv2d_tfwd(x, wp, bias, Ho, Wo, cx, R, S, stride, pad, act="none", slope=0.
     return y
 
 
+# The weight gradient over the NHWC operands (vst_conv2d_wgrad_nhwc: x fp32 NHWC, dy as its NHWC bf16 planes) where
+# the shape takes it; False: the channel-major operand images of vst_conv2d_wgrad_pre.
+WGRAD_NHWC = True
+
+
+@functools.lru_cache(maxsize=512)
+def _wgrad_nhwc_plan_ok(N, H, W, Cx, Ho, Wo, Cyp, R, stride, pad, math):
+    return bool(lib().vst_conv2d_wgrad_nhwc_ok(N, H, W, Cx, Ho, Wo, Cyp, R, R, stride, pad, math))
+
+
+def wgrad_nhwc_ok(N, H, W, Cx, Ho, Wo, Cyp, R, stride, pad, policy=None, role="bwd"):
+    """Does vst_conv2d_wgrad_nhwc take this shape under the current policy (policy: accepted for the callers' cache
+    keys; the arithmetic is the current policy's)?"""
+    return WGRAD_NHWC and _wgrad_nhwc_plan_ok(N, H, W, Cx, Ho, Wo, Cyp, R, stride, pad, _math(role))
+
+
 def conv2d_wgrad(x, dy, dw, db, R, S, stride, pad, pad_mode, co, ci, so, si, accumulate=True,
-                 role="bwd", dy_planes=None, x_t=None):
+                 role="bwd", dy_planes=None, x_t=None, dy_apl=None):
     """dw (+)= weight gradient written with strides (so, si) — see vst_conv2d_wgrad; db (if not
     None) (+)= per-channel sum of dy (the bias gradient).  dy_planes: dy's bf16 plane image made by
     instnorm_act_bwd(..., planes=True), x_t: x's padded channel-major image made by
-    instnorm_act_fwd(..., cp=...) (vst_conv2d_wgrad_pre; both used on the x6 split-bf16 path)."""
+    instnorm_act_fwd(..., cp=...) (vst_conv2d_wgrad_pre; both used on the x6 split-bf16 path).
+    dy_apl: dy's NHWC bf16 planes (``dy.vst_apl``, instnorm_act_bwd(apre=True)): with x itself (no x_t) the
+    NHWC-operand kernel (vst_conv2d_wgrad_nhwc) where the shape takes it."""
     _dev_check(x, dy)
     N, H, W, Cx = x.shape
     _, Ho, Wo, Cyp = dy.shape
+    if dy_apl is None and getattr(dy, "vst_planes_only", False) and dy_planes is None:
+        dy_apl = getattr(dy, "vst_apl", None)
+    if (dy_apl is not None and x_t is None and S == R and
+            wgrad_nhwc_ok(N, H, W, Cx, Ho, Wo, Cyp, R, stride, pad, _policy_name, role)):
+        nbytes = int(lib().vst_conv2d_wgrad_nhwc_ws_bytes(N, H, W, Cx, Ho, Wo, Cyp, R, S, stride, pad, _math(role)))
+        ws = torch.empty((nbytes + 3) // 4, device=x.device)
+        h = _probe_begin("wgrad", (N, H, W, Cx, Cyp, R, stride, pad, pad_mode)) if _probes else None
+        _call("vst_conv2d_wgrad_nhwc", _p(x), _p(dy_apl), _p(dw), _p(ws), nbytes, N, H, W, Cx, Ho, Wo, Cyp, R, S, stride,
+              pad, PAD[pad_mode], co, ci, so, si, 1 if accumulate else 0, _math(role), _stream())
+        _probe_end(h)
+        if db is not None:
+            if getattr(dy, "vst_planes_only", False):
+                raise RuntimeError("conv2d_wgrad: the bias gradient of a planes-only dy comes from its IN backward")
+            channel_sum(dy, db, co, accumulate)
+        return
+    if getattr(dy, "vst_planes_only", False) and dy_planes is None:
+        raise RuntimeError("conv2d_wgrad: dy has NHWC planes only and this shape needs its fp32 image / plane copy")
     nbytes = lib().vst_conv2d_wgrad_ws_bytes(N, H, W, Cx, Ho, Wo, Cyp, R, S, stride)
     ws = torch.empty((nbytes + 3) // 4, device=x.device)
     h = _probe_begin("wgrad", (N, H, W, Cx, Cyp, R, stride, pad, pad_mode)) if _probes else None
@@ -502,7 +538,7 @@ def conv2d_dgrad_refl_in(dy, ikf, H, W, cx, y_in, stats, act="relu", slope=0.0, 
     data gradient (+ addend), dy_in = instnorm_act_bwd(g, y_in, stats, act) — or None when the fused route
     does not support the shape / arithmetic.  The IN partials are taken by the data gradient's GEMM
     epilogue and border add (vst_conv2d_dgrad_refl_epi_part: no partial pass; x6 arithmetic, H W % 32 ==
-    0); dy's pre-split planes (``dy.vst_apl``) are its A operand when present, and apre (with planes)
+    0); dy's pre-split planes (``dy.vst_apl``) are its A operand when present, and apre
     writes dy_in as planes only."""
     _dev_check(dy, ikf, addend, y_in, stats)
     if not DGRAD_BORDER or getattr(ikf, "vst_split", None) is None:
@@ -522,7 +558,7 @@ def conv2d_dgrad_refl_in(dy, ikf, H, W, cx, y_in, stats, act="relu", slope=0.0, 
     if planes:
         ldp = lib().vst_cp_ld(N * H * W)
         pl = torch.empty((3, C, ldp), device=dy.device, dtype=torch.bfloat16)
-    if planes and apre:  # dy_in as planes only (instnorm_act_bwd(apre=True))
+    if apre:  # dy_in as NHWC planes only (instnorm_act_bwd(apre=True))
         dyi.vst_apl = torch.empty((3, dyi.numel()), device=dy.device, dtype=torch.bfloat16)
         dyi.vst_planes_only = True
     h = _probe_begin("dgrad", (N, H, W, Cy, C, 3, 1, 1, "reflect")) if _probes else None
@@ -594,7 +630,7 @@ def instnorm_act_bwd(ga, y, stats, act="relu", slope=0.0, db=None, accumulate_db
     """dy = backward of act(IN(y)); db (if given) (+)= sum of dy per channel (conv-bias grad).
     planes=True: returns (dy, dy_planes) — the apply pass also writes dy's three bf16 planes
     [3][C][vst_cp_ld(N*H*W)], the x6 weight gradient's operand image (conv2d_wgrad(dy_planes=...)).
-    apre (with planes): dy is written ONLY as its NHWC bf16 planes ``dy.vst_apl`` (the pre-split A operand of the data
+    apre: dy is written ONLY as its NHWC bf16 planes ``dy.vst_apl`` (the pre-split A operand of the data
     gradient that consumes it, conv2d_dgrad_refl_in) — dy's fp32 values are NOT written (dy.vst_planes_only):
     its readers must take the planes (the weight gradient: dy_planes; the data gradient: vst_apl)."""
     _dev_check(ga, y, stats)
@@ -605,12 +641,12 @@ def instnorm_act_bwd(ga, y, stats, act="relu", slope=0.0, db=None, accumulate_db
     if planes:
         ldp = lib().vst_cp_ld(N * H * W)
         pl = torch.empty((3, C, ldp), device=y.device, dtype=torch.bfloat16)
-    if planes and apre:
+    if apre:
         dy.vst_apl = torch.empty((3, dy.numel()), device=y.device, dtype=torch.bfloat16)
         dy.vst_planes_only = True
         _call("vst_instnorm_act_bwd_planes_apre", _p(ga), _p(y), _p(stats), _p(dy), _p(db), _p(ws), N, H * W, C,
               ACT[act], float(slope), 1 if accumulate_db else 0, _p(pl), ldp, _p(dy.vst_apl), _stream())
-        return dy, pl
+        return (dy, pl) if planes else dy
     _call("vst_instnorm_act_bwd_planes", _p(ga), _p(y), _p(stats), _p(dy), _p(db), _p(ws), N, H * W, C,
           ACT[act], float(slope), 1 if accumulate_db else 0, _p(pl), ldp, _stream())
     return (dy, pl) if planes else dy
@@ -1406,3 +1442,6 @@ def route_flags():
     g = globals()
     net = sys.modules.get(__name__.rsplit(".", 1)[0] + ".networks")
     return tuple(g[n] for n in _ROUTE_FLAGS) + (tuple(getattr(net, n) for n in _NET_ROUTE_FLAGS) if net else ())
+
+
+_lib.apply_route_overrides(__name__, globals())

@@ -387,3 +387,7 @@ def style_grams(vgg, style_img_nchw):
     with torch.no_grad():
         feats = vgg.forward_nhwc(normalize_nhwc(ops.nchw_to_nhwc(style_img_nchw.contiguous())))
         return [gram_nhwc(f) for f in feats]
+
+
+from . import _lib as _lib_routes  # noqa: E402
+_lib_routes.apply_route_overrides(__name__, globals())

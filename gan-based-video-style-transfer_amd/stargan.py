@@ -667,3 +667,7 @@ class StarGANSolver:
                          "G/loss_cls": g_loss_cls.detach()})
         self.i += 1
         return loss
+
+
+from . import _lib as _lib_routes  # noqa: E402
+_lib_routes.apply_route_overrides(__name__, globals())

@@ -260,3 +260,16 @@ def test_conv_desc_host_validation():
         assert lib.vst_workspace_size(ctypes.byref(d), 0) == 0
         setattr(d, field, old)
     assert lib.vst_conv_desc_out_hw(None, ctypes.byref(ho), ctypes.byref(wo)) == 1
+
+
+def test_convflops_counter_wraps_live_ops():
+    """bench.py's FLOP counter (tools/convflops.Counter) wraps ops functions by name: every name it lists must
+    exist in gbvst.ops (a route deleted from ops must leave the counter too, or bench.py fails on the box)."""
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import convflops
+    from gbvst import ops
+    missing = [n for n in convflops.OPS if not hasattr(ops, n)]
+    assert not missing, missing
+    with convflops.Counter():
+        pass

@@ -1073,6 +1073,7 @@ def test_conv_c4_direct(ops, shape, conv_math):
     ("prod_N8", 8, 256, 256, 64, 64, "relu", False),       # whole 256x128 rounds
     ("prod_N8_add", 8, 256, 256, 64, 64, "none", True),
     ("prod_N12", 12, 256, 256, 64, 64, "none", True),      # a round + the split-K tail
+    ("c3_436x1024", 1, 256, 256, 109, 256, "relu", True),  # one partial round of 256x128 tiles (218 blocks)
 ], ids=lambda c: c[0])
 def test_dgrad_refl_in_epi(ops, case):
     """ops.conv2d_dgrad_refl_in / vst_conv2d_dgrad_refl_in_epi (the IN backward partials taken by the data gradient's GEMM epilogue /
@@ -1116,12 +1117,12 @@ def test_dgrad_refl_in_epi(ops, case):
 
 
 def test_dgrad_refl_in_epi_unsupported(ops):
-    """H W not a multiple of 32, or a plan that is neither whole 256x128 rounds (+ a split-K tail) nor all
-    split-K (the 436x1024 ResnetBlocks: 218 tiles of 128x128): the epi route declines (None), the caller
-    keeps the separate passes."""
+    """H W not a multiple of 32, or a plan that is neither 256x128 rounds (+ a split-K tail) nor all split-K
+    (N = 4 at 64 x 64: one round of 128x128 tiles): the epi route declines (None), the caller keeps the separate
+    passes."""
     prev = ops.set_conv_math("bf16x6")
     try:
-        for (N, C, H, W) in ((2, 64, 13, 20), (1, 256, 109, 256)):
+        for (N, C, H, W) in ((2, 64, 13, 20), (4, 256, 64, 64)):
             w = _g(141, (C, C, 3, 3), 0.05)
             ikf = ops.weight_pack(w.to(DEV), ops.PACK_IKF)
             dy = _nhwc(_g(142, (N, C, H, W)), ops)

@@ -1,0 +1,86 @@
+"""The weight gradient over NHWC operands (vst_conv2d_wgrad_nhwc, round 6): x fp32 NHWC and dy as its NHWC bf16
+planes (instnorm_act_bwd(apre=True)), read through k-major stage images and ds_read_b64_tr_b16.  Same split plan,
+per-stage MFMA sequence and lane k assignment as the channel-major route (vst_conv2d_wgrad_pre with the IN
+backward's channel-major planes), so the two must agree BIT FOR BIT; and both against torch's fp32 weight gradient
+(conv tolerance CONV_TOL["bf16x6"], relative to max|ref|).  Reference: the ResnetBlock convs'
+weight gradients, methods/GAN-based/CycleGAN/models/networks.py:404-426."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import CONV_TOL
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module")
+def ops():
+    import gbvst
+    from gbvst import ops as o
+    gbvst._lib.load()
+    return o
+
+
+def _g(seed, shape, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(*shape, generator=g) * scale
+
+
+CASES = [
+    # name, N, H, W, C, stride, pad mode
+    ("res_N8", 8, 64, 64, 256, 1, "reflect"),    # the batched G_A calls (whole 256x128 rounds)
+    ("res_N12", 12, 64, 64, 256, 1, "reflect"),  # the N=12 calls
+    ("res_N1", 1, 64, 64, 256, 1, "reflect"),    # B=1 (many splits)
+    ("res_N2_32", 2, 32, 32, 256, 1, "reflect"),
+    ("res_C3_size", 1, 109, 256, 256, 1, "reflect"),  # the 436x1024 ResnetBlocks (C3 / C5)
+    ("zero_pad", 2, 32, 64, 256, 1, "zero"),
+    ("stride2", 2, 64, 64, 256, 2, "zero"),
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
+def test_wgrad_nhwc_bit_identical(ops, case):
+    name, N, H, W, C, st, mode = case
+    prev = ops.set_conv_math("bf16x6")
+    try:
+        Ho, Wo = (H + 2 - 3) // st + 1, (W + 2 - 3) // st + 1
+        assert ops.wgrad_nhwc_ok(N, H, W, C, Ho, Wo, C, 3, st, 1, "bf16x6"), name
+        x = _g(11, (N, H, W, C)).to(DEV)
+        y = _g(12, (N, Ho, Wo, C)).to(DEV)
+        ga = _g(13, (N, Ho, Wo, C)).to(DEV)
+        s = ops.instnorm_stats(y)
+        dy, pl = ops.instnorm_act_bwd(ga, y, s, "relu", planes=True)   # fp32 dy + its channel-major planes
+        dyn = ops.instnorm_act_bwd(ga, y, s, "relu", apre=True)         # its NHWC planes only
+        assert dyn.vst_planes_only
+        dw0 = torch.zeros(C, C, 3, 3, device=DEV)
+        dw1 = torch.zeros(C, C, 3, 3, device=DEV)
+        ops.conv2d_wgrad(x, dy, dw0, None, 3, 3, st, 1, mode, C, C, C * 9, 9, dy_planes=pl)
+        ops.conv2d_wgrad(x, dyn, dw1, None, 3, 3, st, 1, mode, C, C, C * 9, 9)  # -> vst_conv2d_wgrad_nhwc
+        assert torch.equal(dw0, dw1), (name, (dw0 - dw1).abs().max().item())
+        # accumulate: a second call adds in place
+        ops.conv2d_wgrad(x, dyn, dw1, None, 3, 3, st, 1, mode, C, C, C * 9, 9)
+        assert torch.allclose(dw1, 2 * dw0, rtol=1e-6, atol=0), name
+        # vs torch fp32 (NCHW): dW of conv(pad(x), W) with output gradient dy
+        xc = x.permute(0, 3, 1, 2).cpu().double()
+        gy = dy.permute(0, 3, 1, 2).cpu().double()
+        xp = F.pad(xc, (1,) * 4, mode="reflect") if mode == "reflect" else F.pad(xc, (1,) * 4)
+        ref = torch.nn.grad.conv2d_weight(xp, (C, C, 3, 3), gy, stride=st)
+        err = (dw0.cpu().double() - ref).abs().max().item()
+        assert err <= CONV_TOL["bf16x6"] * ref.abs().max().item(), (name, err)
+    finally:
+        ops.set_conv_math(prev)
+
+
+def test_wgrad_nhwc_declines(ops):
+    """Shapes off the 256x128 x6 plans (fewer channels, Wo not a multiple of 32, other policies) decline: the caller
+    keeps the channel-major route."""
+    prev = ops.set_conv_math("bf16x6")
+    try:
+        assert not ops.wgrad_nhwc_ok(2, 64, 64, 128, 64, 64, 128, 3, 1, 1, "bf16x6")
+        assert not ops.wgrad_nhwc_ok(2, 20, 20, 256, 20, 20, 256, 3, 1, 1, "bf16x6")
+        ops.set_conv_math("fp32")
+        assert not ops.wgrad_nhwc_ok(2, 64, 64, 256, 64, 64, 256, 3, 1, 1, ops.get_conv_math())
+    finally:
+        ops.set_conv_math(prev)

@@ -29,13 +29,6 @@ def _fwd(a, k):
     return 2.0 * N * Ho * Wo * real(C) * co * R * S, "conv%dx%d s%d %d->%d @%dx%d N=%d" % (R, S, st, real(C), co, H, W, N)
 
 
-def _fwd_nrm(a, k):
-    x, cop, R, pad = a[0], a[4], a[5], a[6]
-    N, H, W, C = x.shape
-    Ho, Wo = H + 2 * pad - R + 1, W + 2 * pad - R + 1
-    return 2.0 * N * Ho * Wo * C * real(cop) * R * R, "conv%dx%d s1 %d->%d @%dx%d N=%d" % (R, R, C, real(cop), H, W, N)
-
-
 def _fwd_hw(a, k):
     x, cop, R, S, st, ph, pw = a[0], a[3], a[4], a[5], a[6], a[7], a[8]
     N, H, W, C = x.shape
@@ -115,8 +108,8 @@ def _gram(a, k):
     return 2.0 * N * C * C * H * W, "gram %d @%dx%d N=%d" % (C, H, W, N)
 
 
-OPS = {"conv2d_fwd": _fwd, "conv2d_fwd_in": _fwd, "conv2d_fwd_in_nrm": _fwd_nrm, "conv2d_fwd_hw": _fwd_hw,
-       "conv2d_wgrad": _wgrad, "conv2d_dgrad_s1": _dgrad_s1, "conv2d_dgrad_s1_in": _dgrad_s1,
+OPS = {"conv2d_fwd": _fwd, "conv2d_fwd_in": _fwd, "conv2d_fwd_hw": _fwd_hw,
+       "conv2d_wgrad": _wgrad, "conv2d_dgrad_s1": _dgrad_s1,
        "conv2d_dgrad_refl_in": _dgrad_refl, "conv2d_tfwd": _tfwd, "convT3s2_fwd": _convT, "conv4s2_dgrad": _c4s2,
        "tap_conv_fwd": _tap, "tap_conv_fwd_h": _tap, "tap_conv_wgrad": _tap_w, "tap_conv_wgrad_h": _tap_w,
        "tap_conv_wgrad_swap": _tap_w, "tap_conv_dgrad": _tap_d, "tap_conv_dgrad_h": _tap_d,

@@ -1,5 +1,5 @@
 """Developer: launch one conv family on the ResnetBlock shape (B=4, 64x64x256, 3x3 reflect) a few
-times (batch KB_B, default 8) — the target of rocprofv3 --pmc passes.  usage: kbench.py fprop|dgrad|tconv|wgrad|wgrad_pre|warp|c0 [reps]
+times (batch KB_B, default 8) — the target of rocprofv3 --pmc passes.  usage: kbench.py fprop|dgrad|tconv|wgrad|wgrad_pre|wgrad_nhwc|warp|c0 [reps]
 (wgrad_pre: the weight gradient as the train step runs it, on the IN passes' premade x image / dy planes)
 warp: vst_warp_fwd on bench.py's warp_roofline shape (N=32, C=64, 436x1024, its smooth flow; KB_FLOW=iid:
 the i.i.d. worst case).  c0: the generator's first conv (conv_c4_ring_k; VST_C4_RING=0: conv_c4_direct_k) at N=KB_B, 256x256."""
@@ -58,6 +58,11 @@ if which == "wgrad_pre":  # the step's form: x's padded image and dy's planes ma
     st[..., 1] = 1.0
     _, x_t = ops.instnorm_act_fwd(x, st, "none", cp=(1, "reflect", 1))
     gy, dy_planes = ops.instnorm_act_bwd(gy, x, st, "none", planes=True)
+    torch.cuda.synchronize()
+if which == "wgrad_nhwc":  # round 6: x NHWC itself, dy as its NHWC planes only (vst_conv2d_wgrad_nhwc)
+    st = torch.zeros((B, C, 2), device=dev)
+    st[..., 1] = 1.0
+    gy = ops.instnorm_act_bwd(gy, x, st, "none", apre=True)
     torch.cuda.synchronize()
 # KB_FLUSH=1: a 1 GiB write before every call (L2 and the MALL hold none of the operands: the cold-operand
 # time); KB_FLUSH=2 (wgrad_pre): then the dy planes re-made by their producer (hot, as in the step; x's image cold)

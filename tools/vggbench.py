@@ -1,5 +1,7 @@
-"""Johnson (B=4 256^2) and C3 (1x436x1024) train-step timings (bench.johnson_train_fps / c3_train_fps) standalone:
-the A/B tool for the VGG backward route (VST_VGG_DGRAD_FPROP)."""
+"""Johnson (B=4 256^2) and C3 (1x436x1024) train-step timings (bench.johnson_train_fps / c3_train_fps) standalone,
+with the peak device memory of each, under the batched VGG forwards (perceptual._VggMultiFn, the default) and the
+per-image calls (`python tools/vggbench.py unbatched`): the A/B of the batched route's time and memory (ADVICE r5:
+the batch keeps the target images' activations until backward)."""
 import json
 import os
 import sys
@@ -11,9 +13,17 @@ import bench  # noqa: E402
 
 if __name__ == "__main__":
     dev = torch.device("cuda:0")
-    from gbvst import _lib
+    from gbvst import _lib, cycle_gan_vgg_model, faststyle
     _lib.load()
+    arm = sys.argv[1] if len(sys.argv) > 1 else "batched"
+    faststyle.VGG_BATCHED = cycle_gan_vgg_model.VGG_BATCHED = arm == "batched"
+    torch.cuda.reset_peak_memory_stats(dev)
     j = bench.johnson_train_fps(dev, steps=10)
+    j_mem = torch.cuda.max_memory_allocated(dev)
+    torch.cuda.empty_cache()
+    torch.cuda.reset_peak_memory_stats(dev)
     c = bench.c3_train_fps(dev)
-    print(json.dumps({"arm": os.environ.get("VST_VGG_DGRAD_FPROP", "default") + "/" + os.environ.get("VST_FS_DGRAD_FPROP", "default"), "johnson_ms": j["ms_per_step"],
-                      "johnson_frac": j["roofline"]["frac"], "c3_ms": c["ms_per_step"], "c3_frac": c["roofline"]["frac"]}))
+    c_mem = torch.cuda.max_memory_allocated(dev)
+    print(json.dumps({"arm": arm, "johnson_ms": j["ms_per_step"], "johnson_frac": j["roofline"]["frac"],
+                      "johnson_peak_mib": round(j_mem / 2 ** 20, 1), "c3_ms": c["ms_per_step"],
+                      "c3_frac": c["roofline"]["frac"], "c3_peak_mib": round(c_mem / 2 ** 20, 1)}))

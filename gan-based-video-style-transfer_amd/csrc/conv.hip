@@ -1305,6 +1305,8 @@ static bool wgrad_nhwc_plan(int N, int H, int W, int Cx, int Ho, int Wo, int Cyp
   if (wgrad_two_level(p, Cyp, Cx, R * S, Cyp)) return false;  // (the one-level reduction of the pre path's plan)
   if (stride == 1 && p.pad != pad) return false;
   if (Ho != (H + 2 * pad - R) / stride + 1 || Wo != (W + 2 * pad - S) / stride + 1) return false;
+  // the kernel addresses x and the planes through buffer descriptors with 32-bit byte offsets
+  if ((long)N * H * W * Cx * 4 >= 0x7fff0000L || 3L * N * Ho * Wo * Cyp * 2 >= 0x7fff0000L) return false;
   *out = p;
   return true;
 }

@@ -1673,8 +1673,15 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_wgrad_nhwc_k(
   }
   const int m0 = mx * T::BM, n0 = ny * T::BN;
   const int pbeg = zz * chunk, pend = min(P, pbeg + chunk);
-  const float* zp = g_zero_page;
-  const __bf16* zpb = reinterpret_cast<const __bf16*>(g_zero_page);
+  // Both operands through buffer descriptors: a gathered pixel outside the frame (zero padding) or a stage past the
+  // split's end gets an offset past the descriptor's range and reads zeros — the loads stay unconditional and
+  // their 32-bit offsets cheap (the host keeps both tensors under 2 GiB), so the two-stage loop body stays one
+  // basic block (a select between two pointers compiled to branches around 64-bit address arithmetic).
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(x), 0, (int)((long)P / (Ho * Wo) * H * W * Cx * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<__bf16*>(dyp), 0, (int)(NP * pps * 2), 0x00020000);
+  constexpr int OOB = 0x7ffffff0;
   // this thread's A column chunk (tap, ci .. ci + 7) (columns past Mw read column chunk Mw - 8: never stored)
   int r_, s_, ci;
   {
@@ -1702,22 +1709,25 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_wgrad_nhwc_k(
     const bool live = pb < pend;
     const int hi = ho * st + r_ - pad;
     const int hr = reflect ? reflect_idx(hi, H) : hi;
-    const bool hok = (unsigned)hr < (unsigned)H;
+    const bool hok = live && (unsigned)hr < (unsigned)H;
+    const int rowb = (n * H + hr) * W;  // pixel index of (n, hr, 0)
 #pragma unroll
     for (int j = 0; j < A_LD; ++j) {
       const int wi = (wo0 + ka + (T::NT / AC) * j) * st + s_ - pad;
       const int wr = reflect ? reflect_idx(wi, W) : wi;
-      const bool ok = live && hok && (unsigned)wr < (unsigned)W;
-      const float* p = ok ? x + (((long)n * H + hr) * W + wr) * Cx + ci : zp;
-      ra[set][j][0] = *reinterpret_cast<const float4*>(p);
-      ra[set][j][1] = *reinterpret_cast<const float4*>(p + 4);
+      // (bitwise forms: a short-circuit / select form compiled to a branch around the offset arithmetic)
+      const int ok = (int)hok & (int)((unsigned)wr < (unsigned)W), msk = -ok;
+      const int off = ((((rowb + wr) * Cx + ci) * 4) & msk) | (OOB & ~msk);
+      ra[set][j][0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
+      ra[set][j][1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off + 16, 0, 0));
     }
 #pragma unroll
     for (int j = 0; j < B_LD; ++j) {
-      const __bf16* q = live ? dyp + (long)(pb + kb + (T::NT / BC) * j) * Cyp + co : zpb;
-      const long ps = live ? pps : 0;
+      const int off = live ? ((pb + kb + (T::NT / BC) * j) * Cyp + co) * 2 : OOB;
 #pragma unroll
-      for (int p = 0; p < NP; ++p) rbv[set][j][p] = *reinterpret_cast<const u32x4_t*>(q + p * ps);
+      for (int p = 0; p < NP; ++p)
+        rbv[set][j][p] = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(
+                                                         drs, live ? off + p * (int)pps * 2 : OOB, 0, 0));
     }
   };
   auto adv = [&](bool go) __attribute__((always_inline)) {

@@ -88,7 +88,7 @@ def DOMINANT_KEYS(B):
             "resblock_wgrad": ("wgrad", (N, 64, 64, 256, 256, 3, 1, 1, "reflect"))}
 
 
-PMC_FILE = os.path.join(HERE, "profiles", "r05z_conv_pmc.json")
+PMC_FILE = os.path.join(HERE, "profiles", "r06z_conv_pmc.json")
 
 
 def _pmc_record(name, key):
@@ -142,6 +142,11 @@ def _mfma(m):
     return "v_mfma_f32_%s_bf16" % shape
 
 
+def _rb_nhwc(N, H, W, C):
+    from gbvst import networks
+    return networks._rb_wgrad_nhwc(N, H, W, C)
+
+
 def conv_roofline(name, probe, math):
     """Roofline entry of one probed conv: algorithmic FLOPs (2*M*N*K of the conv it computes) per
     launch / the average duration of its launches inside the timed steps (HIP events on the launch
@@ -180,6 +185,14 @@ def conv_roofline(name, probe, math):
                       "GEMM (split-K conv_fprop_bf_k<REFL=5>, 128x128) + dgrad_border5_add_k [%s]" % (m, _mfma(m)))
             note = ("stride-1 reflect data gradient: interior conv + border GEMM (no padded frame, no fold); "
                     "dgrad_border5_add_k adds the border slabs")
+    elif m == "bf16x6" and _rb_nhwc(N, H, W, Cx):
+        # round 6: x = the conv's own NHWC fp32 input, dy = the NHWC bf16 planes the planes-only IN backward
+        # writes; the kernel stages both through k-major LDS images (ds_read_b64_tr_b16)
+        kernel = ("vst_conv2d_wgrad_nhwc: conv_wgrad_nhwc_k (x NHWC fp32 split in the kernel + dy NHWC planes, "
+                  "split-K slabs) + slab_group_sum_k / wgrad_reduce_store_k [%s]" % _mfma(m))
+        key = {"math": m, "N": N, "mfma": _mfma(m)}
+        note = "whole weight-gradient op as the train step runs it (its launches timed together)"
+        name = "resblock_wgrad_nhwc"  # the PMC record of this route (tools/kbench.py wgrad_nhwc)
     else:
         # the step's route (networks.py IN_XT / IN_PLANES): the IN apply writes x's padded channel-major
         # image and the IN backward dy's bf16 planes, so the op is the GEMM + the split-K reduction

@@ -188,9 +188,9 @@ void bf_wgrad_launch(const float* xt, const void* dyp, float* slab, int N, int H
 void bf_wgrad_geom(int kind, int math, int* bm, int* bn, int* bk, int* slots);
 // ... over the NHWC operands (x fp32 NHWC, dy as NHWC bf16 planes [3][P][Cyp], plane stride pps): conv_wgrad_nhwc_k
 bool bf_wgrad_nhwc_ok(int kind, int Wo, int Cx, int Cyp);
-void bf_wgrad_nhwc_launch(const float* x, const void* dyp, long pps, float* slab, int N, int H, int W, int Cx, int Ho,
-                          int Wo, int Cyp, int S, int pad, int st, int reflect, int Mw, int chunk, int nsplit,
-                          hipStream_t s);
+void bf_wgrad_nhwc_launch(const float* x, const void* dy, long pps, bool bf32, float* slab, int N, int H, int W,
+                          int Cx, int Ho, int Wo, int Cyp, int S, int pad, int st, int reflect, int Mw, int chunk,
+                          int nsplit, int kind, hipStream_t s);
 
 void rk_tile_geom(int kind, int math, int* bm, int* bn, int* bk, int* slots);
 void rk_nhwc_to_cp(const float* x, float* y, long P, int Cs, int pack, hipStream_t s);

@@ -1302,7 +1302,6 @@ static bool wgrad_nhwc_plan(int N, int H, int W, int Cx, int Ho, int Wo, int Cyp
   if (math != VST_MATH_BF16X6 || R != S || Cx < 8) return false;
   const WgradPlan p = plan_wgrad(N, H, W, Ho, Wo, Cx, Cyp, R, S, stride, math);
   if (!p.bfk || p.wpad || !bf_wgrad_nhwc_ok((int)p.tile, Wo, Cx, Cyp)) return false;
-  if (wgrad_two_level(p, Cyp, Cx, R * S, Cyp)) return false;  // (the one-level reduction of the pre path's plan)
   if (stride == 1 && p.pad != pad) return false;
   if (Ho != (H + 2 * pad - R) / stride + 1 || Wo != (W + 2 * pad - S) / stride + 1) return false;
   // the kernel addresses x and the planes through buffer descriptors with 32-bit byte offsets
@@ -1321,14 +1320,14 @@ extern "C" size_t vst_conv2d_wgrad_nhwc_ws_bytes(int N, int H, int W, int Cx, in
                                                  int stride, int pad, int math) {
   WgradPlan p;
   if (!wgrad_nhwc_plan(N, H, W, Cx, Ho, Wo, Cyp, R, S, stride, pad, math, &p)) return 0;
-  return (size_t)p.nsplit * p.Mw * Cyp * sizeof(float);
+  // the slabs, then (two-level reductions: many slabs of a small weight) the group sums
+  return ((size_t)p.nsplit + ceil_div(p.nsplit, WG_GROUP)) * p.Mw * Cyp * sizeof(float);
 }
 
-extern "C" int vst_conv2d_wgrad_nhwc(const float* x, const void* dy_apl, float* dw, float* ws, size_t ws_bytes, int N,
-                                     int H, int W, int Cx, int Ho, int Wo, int Cyp, int R, int S, int stride, int pad,
-                                     int pad_mode, int Co, int Ci, long so, long si, int accumulate, int math,
-                                     void* stream) {
-  VST_REQUIRE(x && dy_apl && dw && ws, "conv2d_wgrad_nhwc: null pointer");
+static int wgrad_nhwc_impl(const float* x, const void* dy, bool bf32, float* dw, float* ws, size_t ws_bytes, int N,
+                           int H, int W, int Cx, int Ho, int Wo, int Cyp, int R, int S, int stride, int pad,
+                           int pad_mode, int Co, int Ci, long so, long si, int accumulate, int math, void* stream) {
+  VST_REQUIRE(x && dy && dw && ws, "conv2d_wgrad_nhwc: null pointer");
   VST_REQUIRE(Co <= Cyp && Ci <= Cx && pad >= 0 && (pad_mode == VST_PAD_ZERO || (pad < H && pad < W)),
               "conv2d_wgrad_nhwc: bad args");
   WgradPlan p;
@@ -1336,21 +1335,48 @@ extern "C" int vst_conv2d_wgrad_nhwc(const float* x, const void* dy_apl, float* 
     ::vst::set_error("conv2d_wgrad_nhwc: unsupported shape / arithmetic (vst_conv2d_wgrad_nhwc_ok)");
     return VST_EUNSUPPORTED;
   }
-  VST_REQUIRE(ws_bytes >= (size_t)p.nsplit * p.Mw * Cyp * sizeof(float),
+  VST_REQUIRE(ws_bytes >= ((size_t)p.nsplit + ceil_div(p.nsplit, WG_GROUP)) * p.Mw * Cyp * sizeof(float),
               "conv2d_wgrad_nhwc: workspace too small (%zu bytes)", ws_bytes);
   hipStream_t s = (hipStream_t)stream;
-  bf_wgrad_nhwc_launch(x, dy_apl, (long)N * Ho * Wo * Cyp, ws, N, H, W, Cx, Ho, Wo, Cyp, S, pad, stride,
-                       pad_mode == VST_PAD_REFLECT, p.Mw, p.chunk, p.nsplit, s);
+  bf_wgrad_nhwc_launch(x, dy, (long)N * Ho * Wo * Cyp, bf32, ws, N, H, W, Cx, Ho, Wo, Cyp, S, pad, stride,
+                       pad_mode == VST_PAD_REFLECT, p.Mw, p.chunk, p.nsplit, (int)p.tile, s);
   int rc = check_launch("conv2d_wgrad_nhwc");
   if (rc) return rc;
+  // the split-K slabs reduced exactly as vst_conv2d_wgrad_pre's (same grouping and order: bit-identical)
   const long slab = (long)p.Mw * Cyp;
-  if (p.nsplit > 2)
+  const float* red = ws;
+  int nred = p.nsplit;
+  if (wgrad_two_level(p, Cyp, Ci, R * S, Co)) {
+    float* l2 = ws + (long)p.nsplit * slab;
+    nred = ceil_div(p.nsplit, WG_GROUP);
+    hipLaunchKernelGGL(slab_group_sum_k, dim3(ceil_div(slab / 4, 256), nred), dim3(256), 0, s, ws, l2, slab / 4,
+                       p.nsplit, WG_GROUP);
+    red = l2;
+  }
+  if (nred > 2)
     hipLaunchKernelGGL(wgrad_reduce_store_k<1>, dim3(ceil_div(Ci * R * S, 16), ceil_div(Co, 64)), dim3(256), 0, s,
-                       ws, dw, Cx, Cyp, R * S, Co, Ci, so, si, accumulate, p.nsplit, slab);
+                       red, dw, Cx, Cyp, R * S, Co, Ci, so, si, accumulate, nred, slab);
   else
     hipLaunchKernelGGL(wgrad_reduce_store_k<2>, dim3(ceil_div(Ci * R * S, 32), ceil_div(Co, 64)), dim3(256), 0, s,
-                       ws, dw, Cx, Cyp, R * S, Co, Ci, so, si, accumulate, p.nsplit, slab);
+                       red, dw, Cx, Cyp, R * S, Co, Ci, so, si, accumulate, nred, slab);
   return check_launch("conv2d_wgrad_nhwc_reduce");
+}
+
+extern "C" int vst_conv2d_wgrad_nhwc(const float* x, const void* dy_apl, float* dw, float* ws, size_t ws_bytes, int N,
+                                     int H, int W, int Cx, int Ho, int Wo, int Cyp, int R, int S, int stride, int pad,
+                                     int pad_mode, int Co, int Ci, long so, long si, int accumulate, int math,
+                                     void* stream) {
+  return wgrad_nhwc_impl(x, dy_apl, false, dw, ws, ws_bytes, N, H, W, Cx, Ho, Wo, Cyp, R, S, stride, pad, pad_mode, Co,
+                         Ci, so, si, accumulate, math, stream);
+}
+
+// ... with dy fp32 NHWC [N][Ho][Wo][Cyp] itself (split in the kernel's registers like x): no operand image at all
+extern "C" int vst_conv2d_wgrad_nhwc_f32(const float* x, const float* dy, float* dw, float* ws, size_t ws_bytes, int N,
+                                         int H, int W, int Cx, int Ho, int Wo, int Cyp, int R, int S, int stride,
+                                         int pad, int pad_mode, int Co, int Ci, long so, long si, int accumulate,
+                                         int math, void* stream) {
+  return wgrad_nhwc_impl(x, dy, true, dw, ws, ws_bytes, N, H, W, Cx, Ho, Wo, Cyp, R, S, stride, pad, pad_mode, Co, Ci,
+                         so, si, accumulate, math, stream);
 }
 
 extern "C" int vst_conv2d_wgrad_bias(const float* x, const float* dy, float* dw, float* db, float* ws, size_t ws_bytes,

@@ -1578,6 +1578,33 @@ __device__ __forceinline__ void store_stage_km(char* st, const float4 (&ra)[T::A
   }
 }
 
+// ... B chunks as fp32 (8 columns of one k row, split here like A)
+template <class T>
+__device__ __forceinline__ void store_stage_km(char* st, const float4 (&ra)[T::A_LD][2],
+                                               const float4 (&rbf)[T::B_LD][2], int t) {
+  using G = KmGeom<T>;
+  char* Bs = st + G::A_BYTES;
+  constexpr int AC = T::BM / 8, BC = T::BN / 8;
+#pragma unroll
+  for (int j = 0; j < T::A_LD; ++j) {
+    const int c = t + T::NT * j, k = c / AC, mc = c % AC;
+    uint4 sp[T::NP];
+    split8<T::NP>(ra[j][0], ra[j][1], sp);
+    const int off = km_off(mc >> 4, k, 8 * (mc & 15));
+#pragma unroll
+    for (int p = 0; p < T::NP; ++p) *reinterpret_cast<uint4*>(st + p * G::A_PLANE + off) = sp[p];
+  }
+#pragma unroll
+  for (int j = 0; j < T::B_LD; ++j) {
+    const int c = t + T::NT * j, k = c / BC, nc = c % BC;
+    uint4 sp[T::NP];
+    split8<T::NP>(rbf[j][0], rbf[j][1], sp);
+    const int off = km_off(nc >> 4, k, 8 * (nc & 15));
+#pragma unroll
+    for (int p = 0; p < T::NP; ++p) *reinterpret_cast<uint4*>(Bs + p * G::B_PLANE + off) = sp[p];
+  }
+}
+
 typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) bf16x4_t lds_bf16x4;
 
@@ -1608,10 +1635,10 @@ __device__ __forceinline__ void read_plane16_km(Plane16<T>& f, const char* __res
 }
 
 // main_loop16 (same stage / group / MFMA order) on k-major stage images
-template <class T, class LoadAll, class Adv>
+template <class T, class RB, class LoadAll, class Adv>
 __device__ __forceinline__ void main_loop16_km(char* smem, int nk, f32x4v (&acc)[T::MI16][T::NI16],
-                                               float4 (&ra)[2][T::A_LD][2], u32x4_t (&rbv)[2][T::B_LD][T::NP],
-                                               LoadAll load_all, Adv adv) {
+                                               float4 (&ra)[2][T::A_LD][2], RB (&rbv)[2], LoadAll load_all,
+                                               Adv adv) {
   constexpr int STAGE = KmGeom<T>::STAGE;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int wm0 = (wave / T::WAVES_N) * T::WM, wn0 = (wave % T::WAVES_N) * T::WN;
@@ -1651,11 +1678,12 @@ __device__ __forceinline__ void main_loop16_km(char* smem, int nk, f32x4v (&acc)
 }
 
 // dW = x^T dy over split-K pixel chunks, x fp32 NHWC [N][H][W][Cx], dy NHWC bf16 planes dyp [3][P][Cyp] (plane
-// stride pps); M rows (tap, ci), N columns co; the same tile grid / XCD order / chunks / slab layout as
-// conv_wgrad_bf_k.  Needs Wo % 32 == 0 (a 32-pixel K step inside one output row), Cx % 8 == 0, Cyp % 8 == 0.
-template <class T>
+// stride pps) or, BF32, dy itself fp32 NHWC [P][Cyp] (split in registers like x); M rows (tap, ci), N columns co;
+// the same tile grid / XCD order / chunks / slab layout as conv_wgrad_bf_k.  Needs Wo % 32 == 0 (a 32-pixel K
+// step inside one output row), Cx % 8 == 0, Cyp % 8 == 0.
+template <class T, bool BF32>
 __global__ __launch_bounds__(T::NT, T::MINB) void conv_wgrad_nhwc_k(
-    const float* __restrict__ x, const __bf16* __restrict__ dyp, long pps, float* __restrict__ slab, int H, int W,
+    const float* __restrict__ x, const void* __restrict__ dyv, long pps, float* __restrict__ slab, int H, int W,
     int Cx, int Ho, int Wo, int Cyp, int S, int pad, int st, int reflect, int Mw, int P, int chunk) {
   static_assert(T::M16 && T::BK == 32 && T::BM % 128 == 0 && T::BN % 128 == 0, "k-major images of 128 columns");
   static_assert((T::NT % (T::BM / 8)) == 0 && (T::NT % (T::BN / 8)) == 0, "a thread's chunk column is fixed");
@@ -1680,7 +1708,7 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_wgrad_nhwc_k(
   const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<float*>(x), 0, (int)((long)P / (Ho * Wo) * H * W * Cx * 4), 0x00020000);
   const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<__bf16*>(dyp), 0, (int)(NP * pps * 2), 0x00020000);
+      const_cast<void*>(dyv), 0, (int)(BF32 ? (long)P * Cyp * 4 : NP * pps * 2), 0x00020000);
   constexpr int OOB = 0x7ffffff0;
   // this thread's A column chunk (tap, ci .. ci + 7) (columns past Mw read column chunk Mw - 8: never stored)
   int r_, s_, ci;
@@ -1703,8 +1731,9 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_wgrad_nhwc_k(
     ho = rem / Wo;
     wo0 = rem - ho * Wo;
   }
+  typedef typename std::conditional<BF32, float4[B_LD][2], u32x4_t[B_LD][NP]>::type RBset;
   float4 ra[2][A_LD][2];
-  u32x4_t rbv[2][B_LD][NP];
+  RBset rbv[2];
   auto load_all = [&](int set) __attribute__((always_inline)) {
     const bool live = pb < pend;
     const int hi = ho * st + r_ - pad;
@@ -1723,11 +1752,17 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_wgrad_nhwc_k(
     }
 #pragma unroll
     for (int j = 0; j < B_LD; ++j) {
-      const int off = live ? ((pb + kb + (T::NT / BC) * j) * Cyp + co) * 2 : OOB;
+      const int e = (pb + kb + (T::NT / BC) * j) * Cyp + co;
+      if constexpr (BF32) {
+        const int off = live ? e * 4 : OOB;
+        rbv[set][j][0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(drs, off, 0, 0));
+        rbv[set][j][1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(drs, off + 16, 0, 0));
+      } else {
 #pragma unroll
-      for (int p = 0; p < NP; ++p)
-        rbv[set][j][p] = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(
-                                                         drs, live ? off + p * (int)pps * 2 : OOB, 0, 0));
+        for (int p = 0; p < NP; ++p)
+          rbv[set][j][p] = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(
+                                                           drs, live ? (e + p * (int)pps) * 2 : OOB, 0, 0));
+      }
     }
   };
   auto adv = [&](bool go) __attribute__((always_inline)) {
@@ -2524,17 +2559,27 @@ void bf_wgrad_launch(const float* xt, const void* dyp, float* slab, int N, int H
 }
 
 bool bf_wgrad_nhwc_ok(int kind, int Wo, int Cx, int Cyp) {
-  return VST_BF_MF16 && kind == 7 && Wo % 32 == 0 && Cx % 8 == 0 && Cyp % 8 == 0;
+  return VST_BF_MF16 && (kind == 7 || kind == 0) && Wo % 32 == 0 && Cx % 8 == 0 && Cyp % 8 == 0;
 }
 
-void bf_wgrad_nhwc_launch(const float* x, const void* dyp, long pps, float* slab, int N, int H, int W, int Cx, int Ho,
-                          int Wo, int Cyp, int S, int pad, int st, int reflect, int Mw, int chunk, int nsplit,
-                          hipStream_t s) {
-  using T = bf::Tile<256, 128, 64, 64, 32, 3>;
+// kind 7: 256x128 tiles (8 waves of 64x64); kind 0: 128x128 (8 waves of 64x32).  bf32: dy fp32 NHWC (pps unused)
+void bf_wgrad_nhwc_launch(const float* x, const void* dy, long pps, bool bf32, float* slab, int N, int H, int W,
+                          int Cx, int Ho, int Wo, int Cyp, int S, int pad, int st, int reflect, int Mw, int chunk,
+                          int nsplit, int kind, hipStream_t s) {
   const int P = N * Ho * Wo;
-  const dim3 grid(ceil_div(Mw, T::BM) * ceil_div(Cyp, T::BN) * nsplit);
-  hipLaunchKernelGGL(bf::conv_wgrad_nhwc_k<T>, grid, dim3(T::NT), 0, s, x, reinterpret_cast<const __bf16*>(dyp), pps,
-                     slab, H, W, Cx, Ho, Wo, Cyp, S, pad, st, reflect, Mw, P, chunk);
+#define VST_WN(BM_, WN_)                                                                                         \
+  {                                                                                                              \
+    using T = bf::Tile<BM_, 128, 64, WN_, 32, 3>;                                                                \
+    const dim3 grid(ceil_div(Mw, T::BM) * ceil_div(Cyp, T::BN) * nsplit);                                       \
+    if (bf32)                                                                                                    \
+      hipLaunchKernelGGL((bf::conv_wgrad_nhwc_k<T, true>), grid, dim3(T::NT), 0, s, x, dy, pps, slab, H, W, Cx,  \
+                         Ho, Wo, Cyp, S, pad, st, reflect, Mw, P, chunk);                                        \
+    else                                                                                                         \
+      hipLaunchKernelGGL((bf::conv_wgrad_nhwc_k<T, false>), grid, dim3(T::NT), 0, s, x, dy, pps, slab, H, W, Cx, \
+                         Ho, Wo, Cyp, S, pad, st, reflect, Mw, P, chunk);                                        \
+  }
+  if (kind == 7) VST_WN(256, 64) else VST_WN(128, 32)
+#undef VST_WN
 }
 
 void bf_wgrad_geom(int kind, int math, int* bm, int* bn, int* bk, int* slots) {

@@ -542,6 +542,8 @@ def _in_bwd_for_wgrad(g, y, s, act, slope, db, x_in, R, st, want, apre=False):
         _, Ho, Wo, Cyp = y.shape
         if apre and ops.wgrad_nhwc_ok(N, H, W, Cx, Ho, Wo, Cyp, R, st, (R - 1) // 2, ops.get_conv_math()):
             return ops.instnorm_act_bwd(g, y, s, act, slope, db=db, apre=True), None
+        if not apre and ops.wgrad_nhwc_f32_ok(N, H, W, Cx, Ho, Wo, Cyp, R, st, (R - 1) // 2):
+            return ops.instnorm_act_bwd(g, y, s, act, slope, db=db), None  # the wgrad reads dy's fp32 itself
         if _wgrad_on_bf(N, H, W, Cx, Ho, Wo, Cyp, R, st, ops.get_conv_math()):
             return ops.instnorm_act_bwd(g, y, s, act, slope, db=db, planes=True, apre=apre)
     return ops.instnorm_act_bwd(g, y, s, act, slope, db=db), None
@@ -570,6 +572,8 @@ class _GeneratorFn(torch.autograd.Function):
             if st == 1 and mode == "reflect" and cout == C_ and _rb_wgrad_nhwc(N_, H_, W_, C_):
                 return None  # a ResnetBlock conv: its weight gradient reads y's NHWC activation itself
             Ho_, Wo_ = (H_ + 2 - 3) // st + 1, (W_ + 2 - 3) // st + 1
+            if st == 2 and ops.wgrad_nhwc_f32_ok(N_, H_, W_, C_, Ho_, Wo_, cpad(cout), 3, 2, 1):
+                return None  # a stride-2 conv whose weight gradient reads the NHWC operands (fp32 dy)
             return (1, mode, st) if _wgrad_on_bf(N_, H_, W_, C_, Ho_, Wo_, cpad(cout), 3, st,
                                                  ops.get_conv_math()) else None
 
@@ -765,6 +769,10 @@ class _GeneratorFn(torch.autograd.Function):
                                                        y_in.shape[2], cin_p, R_w, st_w, (R_w - 1) // 2,
                                                        ops.get_conv_math()):
                     want = False  # the NHWC-operand weight gradient reads dy_in's NHWC planes (apre)
+                if want and not apre and ops.wgrad_nhwc_f32_ok(N, x_w.shape[1], x_w.shape[2], x_w.shape[3],
+                                                               y_in.shape[1], y_in.shape[2], cin_p, R_w, st_w,
+                                                               (R_w - 1) // 2):
+                    want = False  # ... or dy_in's fp32 itself
                 r = ops.conv2d_dgrad_refl_in(dy, ikf, H, W, cin_p, y_in, s_in, act, 0.0, addend=addend, db=db,
                                              planes=want, apre=apre)
                 if r is not None:

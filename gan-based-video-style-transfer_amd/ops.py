@@ -292,6 +292,9 @@ def conv2d_tfwd(x, wp, bias, Ho, Wo, cx, R, S, stride, pad, act="none", slope=0.
 # The weight gradient over the NHWC operands (vst_conv2d_wgrad_nhwc: x fp32 NHWC, dy as its NHWC bf16 planes) where
 # the shape takes it; False: the channel-major operand images of vst_conv2d_wgrad_pre.
 WGRAD_NHWC = True
+# ... and with dy fp32 NHWC itself (vst_conv2d_wgrad_nhwc_f32: the stride-2 convs, the ConvTranspose and
+# PatchGAN weight gradients, whose dy has no planes): no operand image at all.
+WGRAD_NHWC_F32 = True
 
 
 @functools.lru_cache(maxsize=512)
@@ -303,6 +306,12 @@ def wgrad_nhwc_ok(N, H, W, Cx, Ho, Wo, Cyp, R, stride, pad, policy=None, role="b
     """Does vst_conv2d_wgrad_nhwc take this shape under the current policy (policy: accepted for the callers' cache
     keys; the arithmetic is the current policy's)?"""
     return WGRAD_NHWC and _wgrad_nhwc_plan_ok(N, H, W, Cx, Ho, Wo, Cyp, R, stride, pad, _math(role))
+
+
+def wgrad_nhwc_f32_ok(N, H, W, Cx, Ho, Wo, Cyp, R, stride, pad, role="bwd"):
+    """... the fp32-dy form (vst_conv2d_wgrad_nhwc_f32): then no operand image need be made for this weight
+    gradient (the producers of x and dy write NHWC fp32 only)."""
+    return WGRAD_NHWC_F32 and _wgrad_nhwc_plan_ok(N, H, W, Cx, Ho, Wo, Cyp, R, stride, pad, _math(role))
 
 
 def conv2d_wgrad(x, dy, dw, db, R, S, stride, pad, pad_mode, co, ci, so, si, accumulate=True,
@@ -333,6 +342,17 @@ def conv2d_wgrad(x, dy, dw, db, R, S, stride, pad, pad_mode, co, ci, so, si, acc
         return
     if getattr(dy, "vst_planes_only", False) and dy_planes is None:
         raise RuntimeError("conv2d_wgrad: dy has NHWC planes only and this shape needs its fp32 image / plane copy")
+    if (dy_apl is None and x_t is None and dy_planes is None and S == R and
+            wgrad_nhwc_f32_ok(N, H, W, Cx, Ho, Wo, Cyp, R, stride, pad, role)):
+        nbytes = int(lib().vst_conv2d_wgrad_nhwc_ws_bytes(N, H, W, Cx, Ho, Wo, Cyp, R, S, stride, pad, _math(role)))
+        ws = torch.empty((nbytes + 3) // 4, device=x.device)
+        h = _probe_begin("wgrad", (N, H, W, Cx, Cyp, R, stride, pad, pad_mode)) if _probes else None
+        _call("vst_conv2d_wgrad_nhwc_f32", _p(x), _p(dy), _p(dw), _p(ws), nbytes, N, H, W, Cx, Ho, Wo, Cyp, R, S, stride,
+              pad, PAD[pad_mode], co, ci, so, si, 1 if accumulate else 0, _math(role), _stream())
+        _probe_end(h)
+        if db is not None:
+            channel_sum(dy, db, co, accumulate)
+        return
     nbytes = lib().vst_conv2d_wgrad_ws_bytes(N, H, W, Cx, Ho, Wo, Cyp, R, S, stride)
     ws = torch.empty((nbytes + 3) // 4, device=x.device)
     h = _probe_begin("wgrad", (N, H, W, Cx, Cyp, R, stride, pad, pad_mode)) if _probes else None

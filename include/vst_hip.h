@@ -239,7 +239,7 @@ int vst_conv2d_wgrad_pre(const float* x, const float* x_t, const float* dy, cons
  * lo: the RNE split that vst_instnorm_act_bwd_planes_apre / the epi tail's apl write), so the producing IN passes
  * need not write the padded channel-major x image or dy's channel-major planes.  The x6 256x128 plans of
  * vst_conv2d_wgrad_pre (same split plan and reduction: bit-identical results); vst_conv2d_wgrad_nhwc_ok (host-only)
- * says whether a shape takes it (bf16x6, R == S, Wo % 32 == 0, Cx, Cyp % 8 == 0, the 256x128 wgrad tile), ws:
+ * says whether a shape takes it (bf16x6, R == S, Wo % 32 == 0, Cx, Cyp % 8 == 0, a 256x128 / 128x128 wgrad tile), ws:
  * vst_conv2d_wgrad_nhwc_ws_bytes bytes (the split-K slabs).  Other arguments as vst_conv2d_wgrad. */
 int vst_conv2d_wgrad_nhwc_ok(int N, int H, int W, int Cx, int Ho, int Wo, int Cyp, int R, int S, int stride, int pad,
                              int math);
@@ -248,6 +248,11 @@ size_t vst_conv2d_wgrad_nhwc_ws_bytes(int N, int H, int W, int Cx, int Ho, int W
 int vst_conv2d_wgrad_nhwc(const float* x, const void* dy_apl, float* dw, float* ws, size_t ws_bytes, int N, int H,
                           int W, int Cx, int Ho, int Wo, int Cyp, int R, int S, int stride, int pad, int pad_mode,
                           int Co, int Ci, long so, long si, int accumulate, int math, void* stream);
+/* ... with dy fp32 NHWC [N][Ho][Wo][Cyp] itself, split in the kernel like x (the layers whose dy has no planes:
+ * the stride-2 convs and the ConvTranspose weight gradients); also the 128x128 wgrad plans. */
+int vst_conv2d_wgrad_nhwc_f32(const float* x, const float* dy, float* dw, float* ws, size_t ws_bytes, int N, int H,
+                              int W, int Cx, int Ho, int Wo, int Cyp, int R, int S, int stride, int pad, int pad_mode,
+                              int Co, int Ci, long so, long si, int accumulate, int math, void* stream);
 /* vst_instnorm_act_fwd that also writes x_t = the padded channel-major image [C][vst_cp_ld(N (H+2 pad)
  * (W+2 pad))] of its output (reflect / zero border by pad_mode; stride 2: column-phase rows) — the
  * A operand vst_conv2d_wgrad_pre takes for the conv that consumes y (its pad, pad_mode, stride). */

@@ -74,13 +74,54 @@ def test_wgrad_nhwc_bit_identical(ops, case):
 
 
 def test_wgrad_nhwc_declines(ops):
-    """Shapes off the 256x128 x6 plans (fewer channels, Wo not a multiple of 32, other policies) decline: the caller
-    keeps the channel-major route."""
+    """Shapes off the 256x128 / 128x128 x6 plans (image-layer channel counts, Wo not a multiple of 32, other
+    policies) decline: the caller keeps the channel-major route.  128 channels take the 128x128 plan."""
     prev = ops.set_conv_math("bf16x6")
     try:
-        assert not ops.wgrad_nhwc_ok(2, 64, 64, 128, 64, 64, 128, 3, 1, 1, "bf16x6")
+        assert ops.wgrad_nhwc_ok(2, 64, 64, 128, 64, 64, 128, 3, 1, 1, "bf16x6")
+        assert not ops.wgrad_nhwc_ok(2, 64, 64, 4, 64, 64, 64, 3, 1, 1, "bf16x6")
         assert not ops.wgrad_nhwc_ok(2, 20, 20, 256, 20, 20, 256, 3, 1, 1, "bf16x6")
         ops.set_conv_math("fp32")
         assert not ops.wgrad_nhwc_ok(2, 64, 64, 256, 64, 64, 256, 3, 1, 1, ops.get_conv_math())
     finally:
+        ops.set_conv_math(prev)
+
+
+F32_CASES = [
+    # name, N, H, W, Cx, Cyp, R, stride, pad mode  (x [N][H][W][Cx], dy fp32 [N][Ho][Wo][Cyp])
+    ("d0_s2", 2, 256, 256, 64, 128, 3, 2, "zero"),      # the generator's first down conv (128x128 tiles)
+    ("d1_s2", 2, 128, 128, 128, 256, 3, 2, "zero"),     # the second (also the u0 ConvTranspose's equivalent conv)
+    ("D_4x4_s2", 2, 128, 128, 64, 128, 4, 2, "zero"),   # PatchGAN layer 1 (256x128 tiles)
+    ("D_4x4_s2_b", 2, 64, 64, 128, 256, 4, 2, "zero"),
+    ("res_f32", 2, 64, 64, 256, 256, 3, 1, "reflect"),  # the ResnetBlock shape with an fp32 dy
+]
+
+
+@pytest.mark.parametrize("case", F32_CASES, ids=[c[0] for c in F32_CASES])
+def test_wgrad_nhwc_f32_bit_identical(ops, case):
+    """vst_conv2d_wgrad_nhwc_f32 (dy fp32 NHWC split in the kernel) == the channel-major route that copies x into
+    its padded channel-major image and dy into planes (same split, same plan) bit for bit; and vs torch fp32."""
+    name, N, H, W, Cx, Cyp, R, st, mode = case
+    prev = ops.set_conv_math("bf16x6")
+    prev_f = ops.WGRAD_NHWC_F32
+    try:
+        Ho, Wo = (H + 2 - R) // st + 1, (W + 2 - R) // st + 1
+        assert ops.wgrad_nhwc_f32_ok(N, H, W, Cx, Ho, Wo, Cyp, R, st, 1), name
+        x = _g(21, (N, H, W, Cx)).to(DEV)
+        dy = _g(22, (N, Ho, Wo, Cyp)).to(DEV)
+        dw0 = torch.zeros(Cyp, Cx, R, R, device=DEV)
+        dw1 = torch.zeros(Cyp, Cx, R, R, device=DEV)
+        ops.WGRAD_NHWC_F32 = False
+        ops.conv2d_wgrad(x, dy, dw0, None, R, R, st, 1, mode, Cyp, Cx, Cx * R * R, R * R)
+        ops.WGRAD_NHWC_F32 = True
+        ops.conv2d_wgrad(x, dy, dw1, None, R, R, st, 1, mode, Cyp, Cx, Cx * R * R, R * R)
+        assert torch.equal(dw0, dw1), (name, (dw0 - dw1).abs().max().item())
+        xc = x.permute(0, 3, 1, 2).cpu().double()
+        gy = dy.permute(0, 3, 1, 2).cpu().double()
+        xp = F.pad(xc, (1,) * 4, mode="reflect") if mode == "reflect" else F.pad(xc, (1,) * 4)
+        ref = torch.nn.grad.conv2d_weight(xp, (Cyp, Cx, R, R), gy, stride=st)
+        err = (dw1.cpu().double() - ref).abs().max().item()
+        assert err <= CONV_TOL["bf16x6"] * ref.abs().max().item(), (name, err)
+    finally:
+        ops.WGRAD_NHWC_F32 = prev_f
         ops.set_conv_math(prev)

@@ -19,10 +19,11 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 OPS = {"fprop": ("conv_fprop_bf_k",), "dgrad": ("conv_fprop_bf_k", "fprop_splitk_reduce_k", "dgrad_border_add_k", "dgrad_border5_add_k"),
        "wgrad": ("nhwc_to_cp", "conv_wgrad_bf_k", "wgrad_reduce_store_k", "slab_group_sum_k"),
        "wgrad_pre": ("conv_wgrad_bf_k", "wgrad_reduce_store_k", "slab_group_sum_k"),
+       "wgrad_nhwc": ("conv_wgrad_nhwc_k", "wgrad_reduce_store_k", "slab_group_sum_k"),
        "warp": ("warp_fwd_k",), "c0": ("conv_c4_", "in_finalize_k")}
 # the op's main GEMM dispatch (SQ metrics and its timing; the dgrad's 64x64 tail launch is excluded)
 MAIN = {"fprop": "3>, true, 1, false, false>", "dgrad": "3>, true, 0, false, false>", "wgrad": "conv_wgrad_bf_k",
-        "wgrad_pre": "conv_wgrad_bf_k",
+        "wgrad_pre": "conv_wgrad_bf_k", "wgrad_nhwc": "conv_wgrad_nhwc_k",
         "warp": "warp_fwd_k", "c0": "conv_c4_"}  # c0: the ring or the lock-step kernel
 WARP_BYTES = 32 * 436 * 1024 * (8.0 * 64 + 8.0)  # bench.py warp_roofline: N*H*W*(4C gather + 8 flow + 4C write)
 

@@ -89,6 +89,7 @@ def DOMINANT_KEYS(B):
 
 
 PMC_FILE = os.path.join(HERE, "profiles", "r06z_conv_pmc.json")
+PROBE_EVERY = 7  # conv_roofline's sampling stride (ops.LaunchProbe.every)
 
 
 def _pmc_record(name, key):
@@ -208,7 +209,9 @@ def conv_roofline(name, probe, math):
              "frac": round(achieved / peak, 4),
              "peak_basis": "dense bf16 MFMA %.0f TFLOP/s / products per fp32-equivalent MAC (%s)" % (BF16_MFMA_PEAK_TFLOPS, m),
              "traffic": _pmc_traffic(name, key), "avg_launch_ms": round(ms, 4), "flop_per_launch": flop,
-             "launches_timed": len(probe.events), "ms_per_step": round(ms * len(probe.events) / max(1, probe.steps), 3),
+             "launches_timed": len(probe.events), "launches_per_step": round(probe.seen / max(1, probe.steps), 2),
+             "timing": "HIP event pair around 1 launch in %d of this op inside the timed steps" % probe.every,
+             "ms_per_step": round(ms * probe.seen / max(1, probe.steps), 3),
              "fp32_mfma_peak": FP32_MFMA_PEAK_TFLOPS}
     return _held_clock(entry, name, key)
 
@@ -852,7 +855,8 @@ def main():
         model.optimize_parameters(hookG, hookD)
         if i == 0:
             losses0 = model.get_current_losses()  # step 0: what the parity leg checks
-    probes = {k: ops.LaunchProbe(v) for k, v in DOMINANT_KEYS(B).items()}
+    # one launch in 7 of each probed op timed (36 per step each): HIP event pairs idle the stream between kernels
+    probes = {k: ops.LaunchProbe(v, every=PROBE_EVERY) for k, v in DOMINANT_KEYS(B).items()}
     ops.set_launch_probes(list(probes.values()))
     elapsed = time_steps(model, args.steps, hookG, hookD, world, device)
     ops.set_launch_probes([])

@@ -154,12 +154,15 @@ def weight_pack(w, mode, transposed=False, Op=None, Ip=None):
 
 # --------------------------------------------------------------------------------------- conv
 class LaunchProbe:
-    """Measurement hook (bench.py): HIP events around every launch of one conv op ("fwd" =
+    """Measurement hook (bench.py): HIP events around the launches of one conv op ("fwd" =
     vst_conv2d_fwd, "wgrad" = vst_conv2d_wgrad) of one shape (N, H, W, Cx, Cop, R, stride, pad,
-    pad_mode), recorded on the stream the op is launched on."""
+    pad_mode), recorded on the stream the op is launched on.  every: events around one matching launch in
+    `every` (`seen` counts them all) — an event pair costs the stream a few microseconds of idle time between
+    kernels, so timing all 108 probed launches of a C2 step would add ~1 ms to the very step being measured;
+    a stride coprime to the per-step launch count (36) samples every launch position over the steps."""
 
-    def __init__(self, key):
-        self.key, self.events, self.steps = key, [], 1
+    def __init__(self, key, every=1):
+        self.key, self.events, self.steps, self.every, self.seen = key, [], 1, max(1, int(every)), 0
 
     def mean_ms(self):
         torch.cuda.synchronize()
@@ -178,6 +181,9 @@ def set_launch_probes(probes):
 def _probe_begin(op, key):
     for p in _probes:
         if p.key == (op, key):
+            p.seen += 1
+            if (p.seen - 1) % p.every:
+                return None
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
             return p, ev

@@ -82,6 +82,8 @@ SIGNATURES = {
     "vst_conv2d_wgrad_nhwc_ok": (I, [I, I, I, I, I, I, I, I, I, I, I, I]),
     "vst_conv2d_wgrad_nhwc_ws_bytes": (SZ, [I, I, I, I, I, I, I, I, I, I, I, I]),
     "vst_conv2d_wgrad_nhwc": (I, [P, P, P, P, SZ, I, I, I, I, I, I, I, I, I, I, I, I, I, I, L, L, I, I, P]),
+    "vst_conv2d_wgrad_nhwc_f32_ok": (I, [I, I, I, I, I, I, I, I, I, I, I, I]),
+    "vst_conv2d_wgrad_nhwc_f32_ws_bytes": (SZ, [I, I, I, I, I, I, I, I, I, I, I, I]),
     "vst_conv2d_wgrad_nhwc_f32": (I, [P, P, P, P, SZ, I, I, I, I, I, I, I, I, I, I, I, I, I, I, L, L, I, I, P]),
     "vst_conv2d_wgrad_pre": (I, [P, P, P, P, P, P, SZ, I, I, I, I, I, I, I, I, I, I, I, I, I, I, L, L, I, I, P]),
     "vst_instnorm_act_fwd_cp": (I, [P, P, P, P, P, I, I, I, I, I, F, I, I, I, P]),

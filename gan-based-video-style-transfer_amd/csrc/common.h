@@ -190,7 +190,7 @@ void bf_wgrad_geom(int kind, int math, int* bm, int* bn, int* bk, int* slots);
 bool bf_wgrad_nhwc_ok(int kind, int Wo, int Cx, int Cyp);
 void bf_wgrad_nhwc_launch(const float* x, const void* dy, long pps, bool bf32, float* slab, int N, int H, int W,
                           int Cx, int Ho, int Wo, int Cyp, int S, int pad, int st, int reflect, int Mw, int chunk,
-                          int nsplit, int kind, hipStream_t s);
+                          int nsplit, int kind, hipStream_t s, float* dwd = nullptr, int dco = 0, int dacc = 0);
 
 void rk_tile_geom(int kind, int math, int* bm, int* bn, int* bk, int* slots);
 void rk_nhwc_to_cp(const float* x, float* y, long P, int Cs, int pack, hipStream_t s);

@@ -1370,11 +1370,136 @@ extern "C" int vst_conv2d_wgrad_nhwc(const float* x, const void* dy_apl, float* 
                          Ci, so, si, accumulate, math, stream);
 }
 
+// ---- The im2col form of the fp32-dy NHWC weight gradient (round 6): output rows too short for the kernel's 32-pixel
+// K steps (Wo % 32 != 0: the StarGAN discriminator's 16x16 / 8x8 / 4x4 layers) over few pixels in all.  x's patches
+// are gathered once into xc [P][Cx R S] (a few MB), and conv_wgrad_nhwc_k runs as a 1x1 conv over the P pixels
+// (x = xc, Cx = Mw).  With one split (the wide layers: a CU round of tiles or more) the kernel writes the weight
+// gradient itself (xc's columns in the weight's (ci, r, s) order; no slab, no transposing reduction — the widest
+// layer's 134 MB slab and its pass); with several splits the columns are in the slab order
+// (r, s, ci) of the other routes and the usual reduction follows.
+static constexpr long WG_IM2COL_MAX_BYTES = 64L << 20;
+
+static bool wgrad_gemm_plan(int N, int H, int W, int Cx, int Ho, int Wo, int Cyp, int R, int S, int stride, int pad,
+                            int math, WgradPlan* out) {
+  if (math != VST_MATH_BF16X6 || Cx % 8 || Cyp % 8 || Wo % 32 == 0) return false;
+  if (Ho != (H + 2 * pad - R) / stride + 1 || Wo != (W + 2 * pad - S) / stride + 1) return false;
+  const long P = (long)N * Ho * Wo, Mw = (long)Cx * R * S;
+  if (P % 32 || P * Mw * 4 > WG_IM2COL_MAX_BYTES || P * Cyp * 4 >= 0x7fff0000L || Mw >= (1L << 30)) return false;
+  const WgradPlan p = plan_wgrad(1, 1, (int)P, 1, (int)P, (int)Mw, Cyp, 1, 1, 1, math);
+  if (!p.bfk || p.wpad || !bf_wgrad_nhwc_ok((int)p.tile, (int)P, (int)Mw, Cyp)) return false;
+  *out = p;
+  return true;
+}
+
+static size_t wgrad_gemm_xc_bytes(const WgradPlan& p, long P) {
+  return ((size_t)P * p.Mw * sizeof(float) + 255) / 256 * 256;
+}
+
+// xc, then the slabs (unused when the one split goes straight into the weight, which the caller's weight layout
+// decides — a reservation, not traffic)
+static size_t wgrad_gemm_ws_bytes(const WgradPlan& p, long P, int Cyp) {
+  const size_t slabs = p.nsplit == 1 ? 1 : (size_t)p.nsplit + ceil_div(p.nsplit, WG_GROUP);
+  return wgrad_gemm_xc_bytes(p, P) + slabs * p.Mw * Cyp * sizeof(float);
+}
+
+// xc[p][m] for output pixel p = (n, ho, wo) and column m = (ci, r, s) (cmajor) or (r, s, ci): x at the tap's input
+// pixel (zero / reflect padding).  One thread per output float: the writes coalesce, the reads gather from an
+// activation of a few MB.
+__global__ __launch_bounds__(256) void wgrad_im2col_k(const float* __restrict__ x, float* __restrict__ xc, long total,
+                                                      int Mw, int H, int W, int Cx, int Ho, int Wo, int R, int S,
+                                                      int st, int pad, int reflect, int cmajor) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const long p = i / Mw;
+  const int m = (int)(i - p * Mw), RS = R * S;
+  int ci, rs;
+  if (cmajor) {
+    ci = m / RS;
+    rs = m - ci * RS;
+  } else {
+    rs = m / Cx;
+    ci = m - rs * Cx;
+  }
+  const int r = rs / S, sx = rs - r * S, hw = Ho * Wo;
+  const int n = (int)(p / hw), rem = (int)(p - (long)n * hw), ho = rem / Wo, wo = rem - ho * Wo;
+  int hi = ho * st + r - pad, wi = wo * st + sx - pad;
+  if (reflect) {
+    hi = reflect_idx(hi, H);
+    wi = reflect_idx(wi, W);
+  }
+  xc[i] = ((unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W) ? x[(((long)n * H + hi) * W + wi) * Cx + ci] : 0.f;
+}
+
+static int wgrad_gemm_impl(const WgradPlan& p, const float* x, const float* dy, float* dw, float* ws, size_t ws_bytes,
+                           int N, int H, int W, int Cx, int Ho, int Wo, int Cyp, int R, int S, int stride, int pad,
+                           int pad_mode, int Co, int Ci, long so, long si, int accumulate, hipStream_t s) {
+  const long P = (long)N * Ho * Wo;
+  VST_REQUIRE(ws_bytes >= wgrad_gemm_ws_bytes(p, P, Cyp), "conv2d_wgrad_nhwc_f32: workspace too small (%zu bytes)",
+              ws_bytes);
+  // one split into the weight itself needs its layout to be xc's columns: dw [Co][Cx][R][S] contiguous
+  const bool direct = p.nsplit == 1 && Ci == Cx && si == (long)R * S && so == (long)p.Mw;
+  float* xc = ws;
+  const long total = P * p.Mw;
+  hipLaunchKernelGGL(wgrad_im2col_k, dim3((unsigned)ceil_div(total, 256)), dim3(256), 0, s, x, xc, total, p.Mw, H, W,
+                     Cx, Ho, Wo, R, S, stride, pad, pad_mode == VST_PAD_REFLECT ? 1 : 0, direct ? 1 : 0);
+  int rc = check_launch("conv2d_wgrad_im2col");
+  if (rc) return rc;
+  float* sl = ws + wgrad_gemm_xc_bytes(p, P) / sizeof(float);
+  bf_wgrad_nhwc_launch(xc, dy, P * Cyp, true, direct ? nullptr : sl, 1, 1, (int)P, p.Mw, 1, (int)P, Cyp, 1, 0, 1, 0,
+                       p.Mw, p.chunk, p.nsplit, (int)p.tile, s, direct ? dw : nullptr, Co, accumulate);
+  rc = check_launch("conv2d_wgrad_nhwc_gemm");
+  if (rc || direct) return rc;
+  const long slab = (long)p.Mw * Cyp;
+  const float* red = sl;
+  int nred = p.nsplit;
+  if (wgrad_two_level(p, Cyp, Ci, R * S, Co)) {
+    float* l2 = sl + (long)p.nsplit * slab;
+    nred = ceil_div(p.nsplit, WG_GROUP);
+    hipLaunchKernelGGL(slab_group_sum_k, dim3(ceil_div(slab / 4, 256), nred), dim3(256), 0, s, sl, l2, slab / 4,
+                       p.nsplit, WG_GROUP);
+    red = l2;
+  }
+  if (nred > 2)
+    hipLaunchKernelGGL(wgrad_reduce_store_k<1>, dim3(ceil_div(Ci * R * S, 16), ceil_div(Co, 64)), dim3(256), 0, s,
+                       red, dw, Cx, Cyp, R * S, Co, Ci, so, si, accumulate, nred, slab);
+  else
+    hipLaunchKernelGGL(wgrad_reduce_store_k<2>, dim3(ceil_div(Ci * R * S, 32), ceil_div(Co, 64)), dim3(256), 0, s,
+                       red, dw, Cx, Cyp, R * S, Co, Ci, so, si, accumulate, nred, slab);
+  return check_launch("conv2d_wgrad_nhwc_gemm_reduce");
+}
+
+extern "C" int vst_conv2d_wgrad_nhwc_f32_ok(int N, int H, int W, int Cx, int Ho, int Wo, int Cyp, int R, int S,
+                                            int stride, int pad, int math) {
+  WgradPlan p;
+  return (wgrad_nhwc_plan(N, H, W, Cx, Ho, Wo, Cyp, R, S, stride, pad, math, &p) ||
+          wgrad_gemm_plan(N, H, W, Cx, Ho, Wo, Cyp, R, S, stride, pad, math, &p)) ? 1 : 0;
+}
+
+extern "C" size_t vst_conv2d_wgrad_nhwc_f32_ws_bytes(int N, int H, int W, int Cx, int Ho, int Wo, int Cyp, int R,
+                                                     int S, int stride, int pad, int math) {
+  WgradPlan p;
+  if (wgrad_nhwc_plan(N, H, W, Cx, Ho, Wo, Cyp, R, S, stride, pad, math, &p))
+    return vst_conv2d_wgrad_nhwc_ws_bytes(N, H, W, Cx, Ho, Wo, Cyp, R, S, stride, pad, math);
+  if (wgrad_gemm_plan(N, H, W, Cx, Ho, Wo, Cyp, R, S, stride, pad, math, &p))
+    return wgrad_gemm_ws_bytes(p, (long)N * Ho * Wo, Cyp);
+  return 0;
+}
+
 // ... with dy fp32 NHWC [N][Ho][Wo][Cyp] itself (split in the kernel's registers like x): no operand image at all
+// (shapes with Wo % 32 != 0 and few pixels: the im2col form above)
 extern "C" int vst_conv2d_wgrad_nhwc_f32(const float* x, const float* dy, float* dw, float* ws, size_t ws_bytes, int N,
                                          int H, int W, int Cx, int Ho, int Wo, int Cyp, int R, int S, int stride,
                                          int pad, int pad_mode, int Co, int Ci, long so, long si, int accumulate,
                                          int math, void* stream) {
+  WgradPlan p;
+  if (!wgrad_nhwc_plan(N, H, W, Cx, Ho, Wo, Cyp, R, S, stride, pad, math, &p) &&
+      wgrad_gemm_plan(N, H, W, Cx, Ho, Wo, Cyp, R, S, stride, pad, math, &p)) {
+    VST_REQUIRE(x && dy && dw && ws, "conv2d_wgrad_nhwc_f32: null pointer");
+    VST_REQUIRE(Co <= Cyp && Ci <= Cx && pad >= 0 && (pad_mode == VST_PAD_ZERO || (pad < H && pad < W)),
+                "conv2d_wgrad_nhwc_f32: bad args");
+    return wgrad_gemm_impl(p, x, dy, dw, ws, ws_bytes, N, H, W, Cx, Ho, Wo, Cyp, R, S, stride, pad, pad_mode, Co, Ci,
+                           so, si, accumulate, (hipStream_t)stream);
+  }
   return wgrad_nhwc_impl(x, dy, true, dw, ws, ws_bytes, N, H, W, Cx, Ho, Wo, Cyp, R, S, stride, pad, pad_mode, Co, Ci,
                          so, si, accumulate, math, stream);
 }

@@ -1680,11 +1680,14 @@ __device__ __forceinline__ void main_loop16_km(char* smem, int nk, f32x4v (&acc)
 // dW = x^T dy over split-K pixel chunks, x fp32 NHWC [N][H][W][Cx], dy NHWC bf16 planes dyp [3][P][Cyp] (plane
 // stride pps) or, BF32, dy itself fp32 NHWC [P][Cyp] (split in registers like x); M rows (tap, ci), N columns co;
 // the same tile grid / XCD order / chunks / slab layout as conv_wgrad_bf_k.  Needs Wo % 32 == 0 (a 32-pixel K
-// step inside one output row), Cx % 8 == 0, Cyp % 8 == 0.
+// step inside one output row), Cx % 8 == 0, Cyp % 8 == 0.  dwd != null (one split only): the tile goes straight
+// into the weight gradient dwd[co][m] (co < dco; += when dacc) instead of a slab — rows m are then the weight's
+// inner index (the im2col form of vst_conv2d_wgrad_nhwc_f32 orders its columns (ci, r, s)).
 template <class T, bool BF32>
 __global__ __launch_bounds__(T::NT, T::MINB) void conv_wgrad_nhwc_k(
     const float* __restrict__ x, const void* __restrict__ dyv, long pps, float* __restrict__ slab, int H, int W,
-    int Cx, int Ho, int Wo, int Cyp, int S, int pad, int st, int reflect, int Mw, int P, int chunk) {
+    int Cx, int Ho, int Wo, int Cyp, int S, int pad, int st, int reflect, int Mw, int P, int chunk,
+    float* __restrict__ dwd, int dco, int dacc) {
   static_assert(T::M16 && T::BK == 32 && T::BM % 128 == 0 && T::BN % 128 == 0, "k-major images of 128 columns");
   static_assert((T::NT % (T::BM / 8)) == 0 && (T::NT % (T::BN / 8)) == 0, "a thread's chunk column is fixed");
   __shared__ __attribute__((aligned(16))) char smem[2 * KmGeom<T>::STAGE];
@@ -1781,6 +1784,23 @@ __global__ __launch_bounds__(T::NT, T::MINB) void conv_wgrad_nhwc_k(
   f32x4v acc[T::MI16][T::NI16];
   zero_acc4(acc);
   main_loop16_km<T>(smem, nk, acc, ra, rbv, load_all, adv);
+  if (dwd) {  // one split: the transposed tile into the weight gradient itself (4 consecutive m per lane: one float4)
+#pragma unroll
+    for (int i = 0; i < T::MI16; ++i)
+#pragma unroll
+      for (int j = 0; j < T::NI16; ++j) {
+        const int nn = n0 + wn0 + 16 * j + (lane & 15), mm = m0 + wm0 + 16 * i + 4 * (lane >> 4);
+        if (nn >= dco || mm >= Mw) continue;
+        float4* d = reinterpret_cast<float4*>(dwd + (long)nn * Mw + mm);
+        float4 v = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+        if (dacc) {
+          const float4 o = *d;
+          v = make_float4(o.x + v.x, o.y + v.y, o.z + v.z, o.w + v.w);
+        }
+        *d = v;
+      }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < T::MI16; ++i)
 #pragma unroll
@@ -2565,7 +2585,7 @@ bool bf_wgrad_nhwc_ok(int kind, int Wo, int Cx, int Cyp) {
 // kind 7: 256x128 tiles (8 waves of 64x64); kind 0: 128x128 (8 waves of 64x32).  bf32: dy fp32 NHWC (pps unused)
 void bf_wgrad_nhwc_launch(const float* x, const void* dy, long pps, bool bf32, float* slab, int N, int H, int W,
                           int Cx, int Ho, int Wo, int Cyp, int S, int pad, int st, int reflect, int Mw, int chunk,
-                          int nsplit, int kind, hipStream_t s) {
+                          int nsplit, int kind, hipStream_t s, float* dwd, int dco, int dacc) {
   const int P = N * Ho * Wo;
 #define VST_WN(BM_, WN_)                                                                                         \
   {                                                                                                              \
@@ -2573,10 +2593,10 @@ void bf_wgrad_nhwc_launch(const float* x, const void* dy, long pps, bool bf32, f
     const dim3 grid(ceil_div(Mw, T::BM) * ceil_div(Cyp, T::BN) * nsplit);                                       \
     if (bf32)                                                                                                    \
       hipLaunchKernelGGL((bf::conv_wgrad_nhwc_k<T, true>), grid, dim3(T::NT), 0, s, x, dy, pps, slab, H, W, Cx,  \
-                         Ho, Wo, Cyp, S, pad, st, reflect, Mw, P, chunk);                                        \
+                         Ho, Wo, Cyp, S, pad, st, reflect, Mw, P, chunk, dwd, dco, dacc);                        \
     else                                                                                                         \
       hipLaunchKernelGGL((bf::conv_wgrad_nhwc_k<T, false>), grid, dim3(T::NT), 0, s, x, dy, pps, slab, H, W, Cx, \
-                         Ho, Wo, Cyp, S, pad, st, reflect, Mw, P, chunk);                                        \
+                         Ho, Wo, Cyp, S, pad, st, reflect, Mw, P, chunk, dwd, dco, dacc);                        \
   }
   if (kind == 7) VST_WN(256, 64) else VST_WN(128, 32)
 #undef VST_WN

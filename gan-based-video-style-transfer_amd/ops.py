@@ -301,6 +301,9 @@ WGRAD_NHWC = True
 # ... and with dy fp32 NHWC itself (vst_conv2d_wgrad_nhwc_f32: the stride-2 convs, the ConvTranspose and
 # PatchGAN weight gradients, whose dy has no planes): no operand image at all.
 WGRAD_NHWC_F32 = True
+# ... and its im2col form for output rows shorter than 32 pixels (vst_conv2d_wgrad_nhwc_f32: the StarGAN discriminator's
+# 16x16 / 8x8 / 4x4 layers)
+WGRAD_IM2COL = True
 
 
 @functools.lru_cache(maxsize=512)
@@ -314,10 +317,19 @@ def wgrad_nhwc_ok(N, H, W, Cx, Ho, Wo, Cyp, R, stride, pad, policy=None, role="b
     return WGRAD_NHWC and _wgrad_nhwc_plan_ok(N, H, W, Cx, Ho, Wo, Cyp, R, stride, pad, _math(role))
 
 
+@functools.lru_cache(maxsize=None)
+def _wgrad_nhwc_f32_plan_ok(N, H, W, Cx, Ho, Wo, Cyp, R, stride, pad, math):
+    return bool(lib().vst_conv2d_wgrad_nhwc_f32_ok(N, H, W, Cx, Ho, Wo, Cyp, R, R, stride, pad, math))
+
+
 def wgrad_nhwc_f32_ok(N, H, W, Cx, Ho, Wo, Cyp, R, stride, pad, role="bwd"):
-    """... the fp32-dy form (vst_conv2d_wgrad_nhwc_f32): then no operand image need be made for this weight
-    gradient (the producers of x and dy write NHWC fp32 only)."""
-    return WGRAD_NHWC_F32 and _wgrad_nhwc_plan_ok(N, H, W, Cx, Ho, Wo, Cyp, R, stride, pad, _math(role))
+    """... the fp32-dy form (vst_conv2d_wgrad_nhwc_f32, including its im2col form for short output rows): then no
+    operand image need be made for this weight gradient (the producers of x and dy write NHWC fp32 only)."""
+    if not WGRAD_NHWC_F32:
+        return False
+    m = _math(role)
+    return (_wgrad_nhwc_plan_ok(N, H, W, Cx, Ho, Wo, Cyp, R, stride, pad, m) or
+            (WGRAD_IM2COL and _wgrad_nhwc_f32_plan_ok(N, H, W, Cx, Ho, Wo, Cyp, R, stride, pad, m)))
 
 
 def conv2d_wgrad(x, dy, dw, db, R, S, stride, pad, pad_mode, co, ci, so, si, accumulate=True,
@@ -350,7 +362,7 @@ def conv2d_wgrad(x, dy, dw, db, R, S, stride, pad, pad_mode, co, ci, so, si, acc
         raise RuntimeError("conv2d_wgrad: dy has NHWC planes only and this shape needs its fp32 image / plane copy")
     if (dy_apl is None and x_t is None and dy_planes is None and S == R and
             wgrad_nhwc_f32_ok(N, H, W, Cx, Ho, Wo, Cyp, R, stride, pad, role)):
-        nbytes = int(lib().vst_conv2d_wgrad_nhwc_ws_bytes(N, H, W, Cx, Ho, Wo, Cyp, R, S, stride, pad, _math(role)))
+        nbytes = int(lib().vst_conv2d_wgrad_nhwc_f32_ws_bytes(N, H, W, Cx, Ho, Wo, Cyp, R, S, stride, pad, _math(role)))
         ws = torch.empty((nbytes + 3) // 4, device=x.device)
         h = _probe_begin("wgrad", (N, H, W, Cx, Cyp, R, stride, pad, pad_mode)) if _probes else None
         _call("vst_conv2d_wgrad_nhwc_f32", _p(x), _p(dy), _p(dw), _p(ws), nbytes, N, H, W, Cx, Ho, Wo, Cyp, R, S, stride,

@@ -249,7 +249,15 @@ int vst_conv2d_wgrad_nhwc(const float* x, const void* dy_apl, float* dw, float* 
                           int W, int Cx, int Ho, int Wo, int Cyp, int R, int S, int stride, int pad, int pad_mode,
                           int Co, int Ci, long so, long si, int accumulate, int math, void* stream);
 /* ... with dy fp32 NHWC [N][Ho][Wo][Cyp] itself, split in the kernel like x (the layers whose dy has no planes:
- * the stride-2 convs and the ConvTranspose weight gradients); also the 128x128 wgrad plans. */
+ * the stride-2 convs and the ConvTranspose weight gradients); also the 128x128 wgrad plans.  Shapes with
+ * Wo % 32 != 0 over few pixels (N Ho Wo % 32 == 0, the Cx R S patches <= 64 MB: the StarGAN discriminator's small
+ * layers) run as a GEMM over an im2col copy of x's patches, with one split straight into dw (replaces the
+ * fp32-operand kernel + slab + transposing reduction).  vst_conv2d_wgrad_nhwc_f32_ok / _f32_ws_bytes (host-only):
+ * the shapes this entry takes and its workspace.  Reference: StarGAN/model.py:65-88 (the discriminator's convs). */
+int vst_conv2d_wgrad_nhwc_f32_ok(int N, int H, int W, int Cx, int Ho, int Wo, int Cyp, int R, int S, int stride,
+                                 int pad, int math);
+size_t vst_conv2d_wgrad_nhwc_f32_ws_bytes(int N, int H, int W, int Cx, int Ho, int Wo, int Cyp, int R, int S,
+                                          int stride, int pad, int math);
 int vst_conv2d_wgrad_nhwc_f32(const float* x, const float* dy, float* dw, float* ws, size_t ws_bytes, int N, int H,
                               int W, int Cx, int Ho, int Wo, int Cyp, int R, int S, int stride, int pad, int pad_mode,
                               int Co, int Ci, long so, long si, int accumulate, int math, void* stream);

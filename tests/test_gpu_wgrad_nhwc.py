@@ -125,3 +125,38 @@ def test_wgrad_nhwc_f32_bit_identical(ops, case):
     finally:
         ops.WGRAD_NHWC_F32 = prev_f
         ops.set_conv_math(prev)
+
+
+IM2COL_CASES = [
+    # name, N, H, W, Cx, Cyp, R, stride, pad, pad mode  (output rows Wo % 32 != 0: the im2col form)
+    ("sg_d4", 4, 32, 32, 256, 512, 4, 2, 1, "zero"),       # StarGAN D 256 -> 512, out 16x16 (split slabs)
+    ("sg_d5", 4, 16, 16, 512, 1024, 4, 2, 1, "zero"),      # 512 -> 1024, out 8x8 (one split, straight into dw)
+    ("sg_d6", 4, 8, 8, 1024, 2048, 4, 2, 1, "zero"),       # the widest layer, out 4x4
+    ("refl_3x3", 2, 16, 16, 64, 128, 3, 1, 1, "reflect"),  # many slabs: the two-level reduction
+]
+
+
+@pytest.mark.parametrize("case", IM2COL_CASES, ids=[c[0] for c in IM2COL_CASES])
+def test_wgrad_nhwc_f32_im2col(ops, case):
+    """vst_conv2d_wgrad_nhwc_f32's im2col form (Wo % 32 != 0, few pixels): vs torch fp64 within the x6 conv
+    tolerance, accumulating in place; and the route is taken (vst_conv2d_wgrad_nhwc_f32_ok, not the plain plan)."""
+    name, N, H, W, Cx, Cyp, R, st, pad, mode = case
+    prev = ops.set_conv_math("bf16x6")
+    try:
+        Ho, Wo = (H + 2 * pad - R) // st + 1, (W + 2 * pad - R) // st + 1
+        assert Wo % 32 and not ops.wgrad_nhwc_ok(N, H, W, Cx, Ho, Wo, Cyp, R, st, pad, "bf16x6")
+        assert ops.wgrad_nhwc_f32_ok(N, H, W, Cx, Ho, Wo, Cyp, R, st, pad), name
+        x = _g(31, (N, H, W, Cx)).to(DEV)
+        dy = _g(32, (N, Ho, Wo, Cyp)).to(DEV)
+        base = _g(33, (Cyp, Cx, R, R)).to(DEV)
+        dw = base.clone()
+        ops.conv2d_wgrad(x, dy, dw, None, R, R, st, pad, mode, Cyp, Cx, Cx * R * R, R * R)  # accumulate
+        xc = x.permute(0, 3, 1, 2).cpu().double()
+        gy = dy.permute(0, 3, 1, 2).cpu().double()
+        xp = F.pad(xc, (pad,) * 4, mode="reflect") if mode == "reflect" else F.pad(xc, (pad,) * 4)
+        ref = torch.nn.grad.conv2d_weight(xp, (Cyp, Cx, R, R), gy, stride=st)
+        got = (dw - base).cpu().double()
+        err = (got - ref).abs().max().item()
+        assert err <= CONV_TOL["bf16x6"] * ref.abs().max().item(), (name, err)
+    finally:
+        ops.set_conv_math(prev)

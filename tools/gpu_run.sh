@@ -17,6 +17,7 @@
 #   infab=ARMS           same-box inference A/B                                      (tools/gpu_infab.sh)
 #   pmc[=OPS]            counter passes over the ResnetBlock conv ops + record       (tools/profile_counters.sh)
 #   wgradab              same-box kernel A/B of the ResnetBlock weight gradient routes    (tools/wgrad_ab.sh)
+#   sgab=ARMS            same-box StarGAN C4 line A/B                                 (tools/sg_ab.sh)
 #   sgtrace | jstrace | mgtrace | rafttrace   secondary-line kernel traces
 #   stamp                the kernel-source stamp of the tree being run
 set -o pipefail
@@ -58,6 +59,7 @@ for step in "$@"; do
         timeout -k 10 120 python3 tools/pmc_resblock.py $O/pmc $O/pmc/conv 5
       rc=$? ;;
     wgradab) TAG=$TAG/wgab bash tools/wgrad_ab.sh; rc=$? ;;
+    sgab) ARMS="$arg" TAG=$TAG/sgab bash tools/sg_ab.sh; rc=$? ;;
     sgtrace) TAG=$TAG/sg bash tools/gpu_sgtrace.sh; rc=$? ;;
     jstrace) TAG=$TAG/js bash tools/gpu_jstrace.sh; rc=$? ;;
     mgtrace) TAG=$TAG/mg bash tools/gpu_mgtrace.sh; rc=$? ;;

@@ -597,12 +597,21 @@ __global__ __launch_bounds__(256) void wgrad_reduce_store_k(const float* __restr
 #pragma unroll
       for (int i = 0; i < NR; ++i) add4(acc[i], v[u][i]);
   }
-  for (; z < nsplit; ++z) {
-    float4 v[NR];
+  if (z < nsplit) {  // the last < UZ slabs: their loads issued together too (one at a time: a round trip each), then
+                    // summed in slab order as above
+    float4 v[UZ - 1][NR];
 #pragma unroll
-    for (int i = 0; i < NR; ++i) v[i] = *reinterpret_cast<const float4*>(src[i] + (ok[i] ? (long)z * zs : 0));
+    for (int u = 0; u < UZ - 1; ++u)
 #pragma unroll
-    for (int i = 0; i < NR; ++i) add4(acc[i], v[i]);
+      for (int i = 0; i < NR; ++i)
+        v[u][i] = z + u < nsplit ? *reinterpret_cast<const float4*>(src[i] + (ok[i] ? (long)(z + u) * zs : 0))
+                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int u = 0; u < UZ - 1; ++u) {
+      if (z + u >= nsplit) break;
+#pragma unroll
+      for (int i = 0; i < NR; ++i) add4(acc[i], v[u][i]);
+    }
   }
 #pragma unroll
   for (int i = 0; i < NR; ++i) {

@@ -1837,7 +1837,18 @@ __global__ __launch_bounds__(256) void fprop_splitk_reduce_inb_k(const float* __
       const long r = r0 + sub + 16 * h;
       if (r >= rows) break;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      for (int z = 0; z < ks; ++z) add_f4(v, *reinterpret_cast<const float4*>(slab + z * zst + r * Cop + n));
+      for (int z0 = 0; z0 < ks; z0 += 8) {  // batches of 8 loads in flight, summed in slab order
+        float4 q[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          q[u] = z0 + u < ks ? *reinterpret_cast<const float4*>(slab + (z0 + u) * zst + r * Cop + n)
+                             : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          if (z0 + u >= ks) break;
+          add_f4(v, q[u]);
+        }
+      }
       if (addend) add_f4(v, *reinterpret_cast<const float4*>(addend + (m_base + r) * Cop + n));
       *reinterpret_cast<float4*>(y + (m_base + r) * Cop + n) = v;
       const float4 zz = *reinterpret_cast<const float4*>(inb.z + (m_base + r) * Cop + n);
@@ -1893,7 +1904,19 @@ __global__ __launch_bounds__(256) void fprop_splitk_reduce_k(const float* __rest
       const long r = r0 + sub + 16 * h;
       if (r >= rows) break;
       float4 v = bv;
-      for (int z = 0; z < ks; ++z) add_f4(v, *reinterpret_cast<const float4*>(slab + z * zst + r * Cop + n));
+      // the slabs in batches of 8 loads in flight, summed in slab order (a load-add chain is a round trip per slab)
+      for (int z0 = 0; z0 < ks; z0 += 8) {
+        float4 q[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          q[u] = z0 + u < ks ? *reinterpret_cast<const float4*>(slab + (z0 + u) * zst + r * Cop + n)
+                             : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          if (z0 + u >= ks) break;
+          add_f4(v, q[u]);
+        }
+      }
       float o[4] = {apply_act(v.x, act, slope), apply_act(v.y, act, slope), apply_act(v.z, act, slope),
                     apply_act(v.w, act, slope)};
       if (addend) {  // added after the activation (the addend of a data gradient: the residual gradient)

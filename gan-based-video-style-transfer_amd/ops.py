@@ -449,8 +449,11 @@ def _math(role):
 
 
 def debug_set_tiles(fprop=-1, tconv=-1, wgrad=-1):
-    """Force GEMM tiles for calls from this host thread (vst_debug_set_tiles; -1 = automatic)."""
+    """Force GEMM tiles for calls from this host thread (vst_debug_set_tiles; -1 = automatic).  The cached
+    route answers depend on the planner's tiles: dropped."""
     lib().vst_debug_set_tiles(int(fprop), int(tconv), int(wgrad))
+    _wgrad_nhwc_plan_ok.cache_clear()
+    _wgrad_nhwc_f32_plan_ok.cache_clear()
 
 
 PLAN_RK, PLAN_SKINNY, PLAN_C4_DIRECT = -1, -2, -3

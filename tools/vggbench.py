@@ -17,6 +17,7 @@ if __name__ == "__main__":
     _lib.load()
     arm = sys.argv[1] if len(sys.argv) > 1 else "batched"
     faststyle.VGG_BATCHED = cycle_gan_vgg_model.VGG_BATCHED = arm == "batched"
+    torch.zeros(1, device=dev)  # the allocator's device state exists only once the context does
     torch.cuda.reset_peak_memory_stats(dev)
     j = bench.johnson_train_fps(dev, steps=10)
     j_mem = torch.cuda.max_memory_allocated(dev)

@@ -160,3 +160,27 @@ def test_wgrad_nhwc_f32_im2col(ops, case):
         assert err <= CONV_TOL["bf16x6"] * ref.abs().max().item(), (name, err)
     finally:
         ops.set_conv_math(prev)
+
+
+def test_wgrad_nhwc_f32_im2col_padded_channels(ops):
+    """The im2col form when the weight has fewer input channels than x carries (Ci < Cx: one split but not the
+    weight's own layout, so through a slab and the transposing reduction), and a shape it declines (N Ho Wo not a
+    multiple of 32)."""
+    prev = ops.set_conv_math("bf16x6")
+    try:
+        N, H, W, Cx, Ci, Cyp, R, st, pad = 4, 8, 8, 1024, 1000, 2048, 4, 2, 1
+        Ho = Wo = (H + 2 * pad - R) // st + 1
+        assert ops.wgrad_nhwc_f32_ok(N, H, W, Cx, Ho, Wo, Cyp, R, st, pad)
+        assert not ops.wgrad_nhwc_f32_ok(1, H, W, Cx, Ho, Wo, Cyp, R, st, pad)  # P = 16
+        x = _g(41, (N, H, W, Cx)).to(DEV)
+        x[..., Ci:] = 0.0
+        dy = _g(42, (N, Ho, Wo, Cyp)).to(DEV)
+        dw = torch.zeros(Cyp, Ci, R, R, device=DEV)
+        ops.conv2d_wgrad(x, dy, dw, None, R, R, st, pad, "zero", Cyp, Ci, Ci * R * R, R * R)
+        xc = x[..., :Ci].permute(0, 3, 1, 2).cpu().double()
+        gy = dy.permute(0, 3, 1, 2).cpu().double()
+        ref = torch.nn.grad.conv2d_weight(F.pad(xc, (pad,) * 4), (Cyp, Ci, R, R), gy, stride=st)
+        err = (dw.cpu().double() - ref).abs().max().item()
+        assert err <= CONV_TOL["bf16x6"] * ref.abs().max().item(), err
+    finally:
+        ops.set_conv_math(prev)

@@ -55,7 +55,7 @@ for step in "$@"; do
     infab)
       ARMS="$arg" TAG=$TAG/infab bash tools/gpu_infab.sh; rc=$? ;;
     pmc)
-      TAG=$TAG/pmc OPS="${arg:-fprop dgrad wgrad_pre wgrad c0 warp}" bash tools/profile_counters.sh &&
+      TAG=$TAG/pmc OPS="${arg:-fprop dgrad wgrad_nhwc wgrad_pre c0 warp}" bash tools/profile_counters.sh &&
         timeout -k 10 120 python3 tools/pmc_resblock.py $O/pmc $O/pmc/conv 5
       rc=$? ;;
     wgradab) TAG=$TAG/wgab bash tools/wgrad_ab.sh; rc=$? ;;

@@ -317,7 +317,7 @@ def wgrad_nhwc_ok(N, H, W, Cx, Ho, Wo, Cyp, R, stride, pad, policy=None, role="b
     return WGRAD_NHWC and _wgrad_nhwc_plan_ok(N, H, W, Cx, Ho, Wo, Cyp, R, stride, pad, _math(role))
 
 
-@functools.lru_cache(maxsize=None)
+@functools.lru_cache(maxsize=512)
 def _wgrad_nhwc_f32_plan_ok(N, H, W, Cx, Ho, Wo, Cyp, R, stride, pad, math):
     return bool(lib().vst_conv2d_wgrad_nhwc_f32_ok(N, H, W, Cx, Ho, Wo, Cyp, R, R, stride, pad, math))
 

@@ -18,7 +18,7 @@
 #   pmc[=OPS]            counter passes over the ResnetBlock conv ops + record       (tools/profile_counters.sh)
 #   wgradab              same-box kernel A/B of the ResnetBlock weight gradient routes    (tools/wgrad_ab.sh)
 #   sgab=ARMS            same-box StarGAN C4 line A/B                                 (tools/sg_ab.sh)
-#   sgtrace | jstrace | mgtrace | rafttrace   secondary-line kernel traces
+#   sgtrace | jstrace | mgtrace | rafttrace | c3trace   secondary-line kernel traces
 #   stamp                the kernel-source stamp of the tree being run
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -64,6 +64,7 @@ for step in "$@"; do
     jstrace) TAG=$TAG/js bash tools/gpu_jstrace.sh; rc=$? ;;
     mgtrace) TAG=$TAG/mg bash tools/gpu_mgtrace.sh; rc=$? ;;
     rafttrace) TAG=$TAG/raft bash tools/gpu_rafttrace.sh; rc=$? ;;
+    c3trace) TAG=$TAG/c3 bash tools/gpu_c3trace.sh; rc=$? ;;
     stamp)
       python3 -c "import sys; sys.path.insert(0, '.'); from gbvst import _lib; print(_lib.source_stamp())" | tee $O/stamp.txt
       rc=$? ;;

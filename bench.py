@@ -89,7 +89,7 @@ def DOMINANT_KEYS(B):
 
 
 PMC_FILE = os.path.join(HERE, "profiles", "r06z_conv_pmc.json")
-PROBE_EVERY = 7  # conv_roofline's sampling stride (ops.LaunchProbe.every)
+PROBE_EVERY = 13  # conv_roofline's sampling stride (ops.LaunchProbe.every)
 
 
 def _pmc_record(name, key):
@@ -855,7 +855,7 @@ def main():
         model.optimize_parameters(hookG, hookD)
         if i == 0:
             losses0 = model.get_current_losses()  # step 0: what the parity leg checks
-    # one launch in 7 of each probed op timed (36 per step each): HIP event pairs idle the stream between kernels
+    # one launch in 13 of each probed op timed (36 per step each): HIP event pairs idle the stream between kernels
     probes = {k: ops.LaunchProbe(v, every=PROBE_EVERY) for k, v in DOMINANT_KEYS(B).items()}
     ops.set_launch_probes(list(probes.values()))
     elapsed = time_steps(model, args.steps, hookG, hookD, world, device)

@@ -77,8 +77,10 @@ __device__ __forceinline__ void split(const float4& a, const float4& b, bf16x8_t
 template <int NP, int ACT, bool REFL, int RI>
 __global__ __launch_bounds__(NT, 1) void tap64_k(const float* __restrict__ x, const __bf16* __restrict__ ws, long wps,
                                                  const float* __restrict__ bias, float* __restrict__ y, int H, int W,
-                                                 int Ho, int Wo, int pad, float slope, int gpi, int groups, int nimg) {
+                                                 int Ho, int Wo, int pad, float slope, int gpi, int groups, int nimg,
+                                                 int nseg, int outw) {
   constexpr int CBW = MBW / RI;  // column blocks per wave
+  constexpr int WS = GQ / RI;    // z columns per group row: W, or a column segment of a wider row
   static_assert(CBW * RI == MBW, "RI divides the wave's M-blocks");
   __shared__ __attribute__((aligned(16))) float zl[GQ * ZS];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -106,14 +108,25 @@ __global__ __launch_bounds__(NT, 1) void tap64_k(const float* __restrict__ x, co
         b[j][p] = __builtin_bit_cast(bf16x8_t, __builtin_amdgcn_raw_buffer_load_b128(wrs, off, 0, 0));
       }
   };
-  // this lane's z columns (one per column block) and their byte offsets inside an input row
-  int colb[CBW];
+  // this lane's z columns (one per column block, local to the group's segment)
+  int colq[CBW];
 #pragma unroll
-  for (int cb = 0; cb < CBW; ++cb) colb[cb] = ((16 * (wave * CBW + cb) + (lane & 15)) * CI + 8 * kc) * (int)sizeof(float);
+  for (int cb = 0; cb < CBW; ++cb) colq[cb] = 16 * (wave * CBW + cb) + (lane & 15);
   const int rowb = W * CI * (int)sizeof(float);
 
   for (int g = blockIdx.x; g < groups; g += gridDim.x) {
-    const int n = g / gpi, ho0 = (g - n * gpi) * RI;
+    // group g = (image n, row group, column segment k): output columns [k outw, k outw + outw) from the WS z columns
+    // starting at image column zc0 (one segment per row when WS == W: zc0 = 0, outw = Wo)
+    const int k = g % nseg, gr = g / nseg;
+    const int n = gr / gpi, ho0 = (gr - n * gpi) * RI;
+    const int zc0 = nseg > 1 ? k * outw - pad : 0;
+    // byte offsets of this lane's z columns inside an input row, or -1 outside the image (their z is never read)
+    int colb[CBW];
+#pragma unroll
+    for (int cb = 0; cb < CBW; ++cb) {
+      const int ci_ = zc0 + colq[cb];
+      colb[cb] = (unsigned)ci_ < (unsigned)W ? (ci_ * CI + 8 * kc) * (int)sizeof(float) : -1;
+    }
     // byte offset of window row j (input row ho0 + j - pad) of image n, or -1 for a zero-padding row
     auto row_off = [&](int j) __attribute__((always_inline)) {
       int h = ho0 + j - pad;
@@ -129,7 +142,7 @@ __global__ __launch_bounds__(NT, 1) void tap64_k(const float* __restrict__ x, co
       const int ro = row_off(j);
 #pragma unroll
       for (int cb = 0; cb < CBW; ++cb) {
-        const int off = ro >= 0 ? ro + colb[cb] + 128 * c : (int)0x7ffffff0;
+        const int off = (ro >= 0 && colb[cb] >= 0) ? ro + colb[cb] + 128 * c : (int)0x7ffffff0;
         raw[cb][0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
         raw[cb][1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off + 16, 0, 0));
       }
@@ -198,15 +211,16 @@ __global__ __launch_bounds__(NT, 1) void tap64_k(const float* __restrict__ x, co
         for (int j = 0; j < 2; ++j)
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const int qq = rho * W + 16 * (wave * CBW + cb) + 4 * (lane >> 4) + i;
+            const int qq = rho * WS + 16 * (wave * CBW + cb) + 4 * (lane >> 4) + i;
             zl[qq * ZS + 16 * j + (lane & 15)] = acc[rho][cb][j][i];
           }
     __syncthreads();
     // column taps: output pixel (rho, p) of the group, bias then s = 0..6 in order (tapsum_h_k)
     const int rows = Ho - ho0 < RI ? Ho - ho0 : RI;
-    const int outs = rows * Wo;
+    const int p0 = nseg > 1 ? k * outw : 0, ow = nseg > 1 ? min(outw, Wo - p0) : Wo;
+    const int outs = rows * ow;
     for (int e = t; e < outs; e += NT) {
-      const int rho = e / Wo, p = e - rho * Wo;
+      const int rho = e / ow, p = p0 + (e - rho * ow);
       float4 v = bv;
 #pragma unroll
       for (int s = 0; s < R; ++s) {
@@ -214,8 +228,8 @@ __global__ __launch_bounds__(NT, 1) void tap64_k(const float* __restrict__ x, co
         if constexpr (REFL) {
           c = c < 0 ? -c : (c >= W ? 2 * (W - 1) - c : c);
         }
-        const bool in = (unsigned)c < (unsigned)W;
-        const float4 zv = in ? *reinterpret_cast<const float4*>(zl + (rho * W + c) * ZS + 4 * s)
+        const bool in = (unsigned)c < (unsigned)W;  // then c - zc0 lies in [0, WS) (the segment's halo)
+        const float4 zv = in ? *reinterpret_cast<const float4*>(zl + (rho * WS + c - zc0) * ZS + 4 * s)
                              : make_float4(0.f, 0.f, 0.f, 0.f);
         v.x += zv.x;
         v.y += zv.y;
@@ -233,9 +247,17 @@ __global__ __launch_bounds__(NT, 1) void tap64_k(const float* __restrict__ x, co
 }  // namespace tap64
 
 static constexpr bool g_tap64 = true;
+// 1024-wide rows as column segments: groups of 4 rows x 256 z columns (250 output columns + the taps' 6-column halo)
+// instead of one whole row per group — a row's K-steps each split a new input row for only one output row
+// (RI = 1), 4x the operand-split VALU per MFMA of the 4-row groups (the C3 / Sintel-size last layer and the
+// first layer's data gradient ran ~3.5x slower per pixel than at 256 wide).
+#ifndef VST_TAP64_SEG
+#define VST_TAP64_SEG 1
+#endif
 
 // Does the direct kernel take this tap conv?  64 input channels, 7 x 7, 4 (padded) outputs, x6 / x3
-// math, W in {256, 512, 1024} (a group is 1024 / W whole rows), reflect 'same' or zero padding.
+// math, W in {256, 512, 1024} (a group is 1024 / W whole rows, or 4 rows of a 1024-wide row's column segment),
+// reflect 'same' or zero padding.
 bool tap64_ok(int Cx, int R, int W, int math) {
   return g_tap64 && Cx == tap64::CI && R == tap64::R && W % 256 == 0 && tap64::GQ % W == 0 &&
          (math == VST_MATH_BF16X6 || math == VST_MATH_BF16X3);
@@ -247,12 +269,15 @@ int tap64_launch(const float* x, const void* wsplit, long wps, const float* bias
   VST_REQUIRE(Ho > 0 && Wo > 0 && (!reflect || (pad < H && pad < W)), "tap64: bad padding");
   VST_REQUIRE(W % 256 == 0 && tap64::GQ % W == 0, "tap64: W must be 256, 512 or 1024");
   VST_REQUIRE((long)N * H * W * tap64::CI * 4 < 0x7ffffff0L, "tap64: input over 2 GB (32-bit buffer offsets)");
-  const int RI = tap64::GQ / W, gpi = (Ho + RI - 1) / RI, groups = N * gpi;
+  const bool seg = VST_TAP64_SEG && W == 1024;
+  const int RI = seg ? 4 : tap64::GQ / W, gpi = (Ho + RI - 1) / RI;
+  const int outw = seg ? tap64::GQ / 4 - (tap64::R - 1) : Wo, nseg = seg ? (Wo + outw - 1) / outw : 1;
+  const int groups = N * gpi * nseg;
   const int grid = groups < VST_NUM_CUS ? groups : VST_NUM_CUS;
   const __bf16* ws = reinterpret_cast<const __bf16*>(wsplit);
 #define VST_T64K_R(NP_, ACT_, REFL_, RI_)                                                                          \
   hipLaunchKernelGGL((tap64::tap64_k<NP_, ACT_, REFL_, RI_>), dim3(grid), dim3(tap64::NT), 0, s, x, ws, wps, bias, y, \
-                     H, W, Ho, Wo, pad, slope, gpi, groups, N)
+                     H, W, Ho, Wo, pad, slope, gpi, groups, N, nseg, outw)
 #define VST_T64K(NP_, ACT_)                                  \
   switch (RI * 2 + (reflect ? 1 : 0)) {                       \
     case 2: VST_T64K_R(NP_, ACT_, false, 1); break;           \

@@ -454,11 +454,13 @@ def test_tap_conv_fwd_h_production(ops, conv_math):
 
 @pytest.mark.parametrize("N,H,W,pad,mode,act", [(2, 12, 256, 3, "reflect", "tanh"), (3, 9, 256, 6, "zero", "none"),
                                                  (1, 7, 1024, 3, "reflect", "tanh"), (2, 20, 256, 6, "zero", "none"),
-                                                 (1, 5, 512, 3, "reflect", "none"), (2, 6, 512, 6, "zero", "none")])
+                                                 (1, 5, 512, 3, "reflect", "none"), (2, 6, 512, 6, "zero", "none"),
+                                                 (2, 10, 1024, 6, "zero", "none"), (1, 13, 1024, 3, "reflect", "none")])
 def test_tap64_direct(ops, conv_math, N, H, W, pad, mode, act):
     """The direct 64 -> 4 7x7 tap kernel (conv_tap64.hip, inside vst_tapconv_h_fwd when W | 1024): the last
     layer's forward (reflect 3, tanh) and the first layer's full-correlation data-gradient form (zero pad 6,
-    (H+6) x (W+6) output), groups of 4 / 2 / 1 rows (W = 256 / 512 / 1024) with rows past an image's end,
+    (H+6) x (W+6) output), groups of 4 / 2 rows (W = 256 / 512) or of 4 rows x a 256-column segment (W = 1024,
+    five segments per row: the 6-column halo, the reflected / zero-padded row ends) with rows past an image's end,
     vs torch fp32 and vs the 1x1-conv + full tap-sum route."""
     ci, co, k = 64, 3, 7
     x = _g(111, (N, ci, H, W))

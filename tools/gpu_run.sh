@@ -18,6 +18,7 @@
 #   pmc[=OPS]            counter passes over the ResnetBlock conv ops + record       (tools/profile_counters.sh)
 #   wgradab              same-box kernel A/B of the ResnetBlock weight gradient routes    (tools/wgrad_ab.sh)
 #   sgab=ARMS            same-box StarGAN C4 line A/B                                 (tools/sg_ab.sh)
+#   fnab=FN:ARMS         same-box A/B of one bench.py line function, e.g. fnab="c3_train_fps:default X=1"  (tools/fn_ab.sh)
 #   sgtrace | jstrace | mgtrace | rafttrace | c3trace   secondary-line kernel traces
 #   stamp                the kernel-source stamp of the tree being run
 set -o pipefail
@@ -60,6 +61,7 @@ for step in "$@"; do
       rc=$? ;;
     wgradab) TAG=$TAG/wgab bash tools/wgrad_ab.sh; rc=$? ;;
     sgab) ARMS="$arg" TAG=$TAG/sgab bash tools/sg_ab.sh; rc=$? ;;
+    fnab) FN="${arg%%:*}" ARMS="${arg#*:}" TAG=$TAG/fnab_${arg%%:*} bash tools/fn_ab.sh; rc=$? ;;
     sgtrace) TAG=$TAG/sg bash tools/gpu_sgtrace.sh; rc=$? ;;
     jstrace) TAG=$TAG/js bash tools/gpu_jstrace.sh; rc=$? ;;
     mgtrace) TAG=$TAG/mg bash tools/gpu_mgtrace.sh; rc=$? ;;

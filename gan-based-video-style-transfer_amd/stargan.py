@@ -543,10 +543,24 @@ class _StarGFn(torch.autograd.Function):
 ###############################################################################
 # Solver iteration (solver.py:187-199, 234-363)
 ###############################################################################
+# Host tensors (labels, GP weights) onto the device through pinned memory, non-blocking; False: plain .to(device)
+H2D_PINNED = True
+
+
+def _h2d(t, device):
+    """A small host tensor onto the device without blocking the host: a pageable host -> device copy waits for the
+    whole stream to drain (every queued kernel) before it returns, so the host stops running ahead of the GPU and the
+    launches after it arrive one by one; from pinned memory the copy is queued like a kernel."""
+    device = torch.device(device)
+    if not H2D_PINNED or t.device.type != "cpu" or device.type != "cuda":
+        return t.to(device)
+    return t.pin_memory().to(device, non_blocking=True)
+
+
 def label2onehot(labels, dim, device):
     out = torch.zeros(labels.size(0), dim)
     out[np.arange(labels.size(0)), labels.long().cpu()] = 1
-    return out.to(device)
+    return _h2d(out, device)
 
 
 def classification_loss(logit, target, dataset="CelebA"):
@@ -616,7 +630,7 @@ class StarGANSolver:
     def train_step(self, x_real, label_org, label_trg, alpha=None):
         """One iteration of solver.py:298-363.  label_* are class indices [B]; alpha [B,1,1,1] (the
         gradient-penalty interpolation weights; torch.rand if None).  Returns the loss dict."""
-        x_real = x_real.to(self.device).float().contiguous()
+        x_real = _h2d(x_real, self.device).float().contiguous()
         c_org = label2onehot(label_org, self.c_dim, self.device)
         c_trg = label2onehot(label_trg, self.c_dim, self.device)
         # 2. discriminator (real and fake through D as one batch: D is per-sample).  x_fake is only read detached, but
@@ -630,7 +644,7 @@ class StarGANSolver:
         d_loss_fake = torch.mean(out_src[B:])
         if alpha is None:
             alpha = torch.rand(x_real.size(0), 1, 1, 1)
-        alpha = alpha.to(self.device)
+        alpha = _h2d(alpha, self.device)
         x_hat = (alpha * x_real.data + (1 - alpha) * x_fake.data).requires_grad_(True)
         out_src, _ = self.D(x_hat)
         d_loss_gp = gradient_penalty(out_src, x_hat)
